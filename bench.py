@@ -1,0 +1,163 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Inception-v3 parameter-server training, images/sec (whole node).
+
+BASELINE.json metric: "images/sec (whole node) Inception-v3 TF-PS at 1/2/4/8 MI355X".
+One process per GPU (torch.distributed.run), each process is one TF-PS *worker*
+and hosts one PS shard (colocated sharded PS, tony_amd/parallel/ps.py):
+push = RCCL reduce-scatter of bf16 grads over xGMI, apply = fused HIP SGD-momentum
+on the fp32 master shard, pull = RCCL all-gather of bf16 variables.  Compute is
+bf16 NHWC with the tony_amd HIP kernels (fused BN+ReLU, MFMA 1x1-conv GEMM,
+fused softmax-xent, fused optimizer); the whole step is replayed as a HIP graph.
+
+Data is synthetic (ImageNet-shaped 299x299x3 images, random labels) and weights
+are random-init -- no network access for datasets / checkpoints.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+       (N>1 is launched by the driver via torch.distributed.run)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=128, help="per-GPU batch (weak scaling)")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graph replay")
+    ap.add_argument("--stock", action="store_true",
+                    help="comparator: stock nn.BatchNorm2d+ReLU / MIOpen 1x1 / torch loss (not the headline)")
+    ap.add_argument("--model", default="inception_v3", choices=["inception_v3", "resnet50"])
+    ap.add_argument("--optimizer", default="sgd")
+    ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps (for rocprof)")
+    ap.add_argument("--miopen-find", action="store_true", help="MIOpen exhaustive find for the non-1x1 convs")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print(f"bench.py: --gpus {args.gpus} must be launched with torch.distributed.run", file=sys.stderr)
+            return 2
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from tony_amd.ops import cross_entropy
+    from tony_amd.parallel.ps import ParameterServer
+    from tony_amd.parallel.trainer import Trainer
+
+    torch.backends.cudnn.benchmark = args.miopen_find
+    fused = not args.stock
+    if args.model == "inception_v3":
+        from tony_amd.models.inception_v3 import inception_v3
+        model = inception_v3(fused=fused, seed=0)
+        res, aux_w = 299, 0.4
+    else:
+        from tony_amd.models.resnet import resnet50
+        model = resnet50(fused=fused, seed=0)
+        res, aux_w = 224, 0.0
+    model = model.to(dev).to(memory_format=torch.channels_last)
+    model.train()
+    ps = ParameterServer(model, optimizer=args.optimizer, lr=0.045 if args.model == "inception_v3" else 0.1,
+                         momentum=0.9, weight_decay=4e-5, mode="colocated", device=dev)
+
+    if fused:
+        xent = cross_entropy
+    else:
+        def xent(logits, y):
+            return torch.nn.functional.cross_entropy(logits.float(), y)
+
+    def loss_fn(out, y):
+        if isinstance(out, tuple):
+            logits, aux = out
+            return xent(logits, y) + aux_w * xent(aux, y)
+        return xent(out, y)
+
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    x = torch.randn((args.batch, 3, res, res), generator=g, device=dev, dtype=torch.float32)
+    x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (args.batch,), generator=g, device=dev)
+
+    trainer = Trainer(model, ps, loss_fn, use_graph=not args.no_graph)
+    t_w = time.perf_counter()
+    for i in range(args.warmup):
+        loss = trainer.step(x, y)
+        if rank == 0:
+            torch.cuda.synchronize()
+            print(f"[bench] warmup {i + 1}/{args.warmup} t={time.perf_counter() - t_w:.1f}s", file=sys.stderr,
+                  flush=True)
+    torch.cuda.synchronize()
+    if not torch.isfinite(loss).all():
+        print(f"bench.py: non-finite loss after warmup: {loss.item()}", file=sys.stderr)
+        return 3
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = trainer.step(x, y)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    for _ in range(args.profile_steps):
+        trainer.step(x, y)
+    torch.cuda.synchronize()
+
+    from tony_amd.parallel.collectives import max_over_ranks
+    elapsed = max_over_ranks(elapsed, device=dev)
+    final_loss = float(loss.float().item())
+    if rank == 0:
+        imgs = args.batch * world * args.steps
+        value = imgs / elapsed
+        rec = {
+            "metric": "images/sec (whole node) Inception-v3 TF-PS" if args.model == "inception_v3"
+            else "images/sec (whole node) ResNet-50",
+            "value": round(value, 2),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic ImageNet-shaped 299x299x3 batches, random-init weights",
+            "config": {
+                "model": args.model,
+                "global_batch": args.batch * world,
+                "per_gpu_batch": args.batch,
+                "seq_len": None,
+                "image_size": res,
+                "parallelism": f"ps-colocated-sharded dp{world} (1 PS shard + 1 worker per GPU, sync)",
+                "optimizer": "fused SGD-momentum (HIP)" if args.optimizer == "sgd" else args.optimizer,
+                "hip_graph": not args.no_graph,
+                "kernels": "stock-comparator" if args.stock else "tony_amd HIP",
+                "final_loss": round(final_loss, 4),
+            },
+        }
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,181 @@
+"""Numerics of the gfx950 HIP kernels against plain PyTorch fp32 references."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _nhwc(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def _close(a, b, rtol, atol, what):
+    a = a.float()
+    b = b.float()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{what}: {bad}/{a.numel()} outside tol, max err {err.max().item():.4g}"
+
+
+@pytest.mark.parametrize("shape", [(8, 32, 37, 37), (4, 80, 17, 17), (2, 2048, 8, 8), (3, 192, 5, 7), (16, 48, 1, 1)])
+@pytest.mark.parametrize("relu", [True, False])
+def test_bn_act_train_fwd_bwd(cuda, shape, relu):
+    from tony_amd.ops.bn import bn_act
+
+    torch.manual_seed(0)
+    n, c, h, w = shape
+    x = _nhwc(torch.randn(shape, device=cuda) * 2 + 0.5).to(torch.bfloat16)
+    x = _nhwc(x)
+    gamma = (torch.rand(c, device=cuda) + 0.5).to(torch.bfloat16)
+    beta = (torch.randn(c, device=cuda) * 0.1).to(torch.bfloat16)
+    rm = torch.zeros(c, device=cuda)
+    rv = torch.ones(c, device=cuda)
+    xr = x.float().detach().requires_grad_(True)
+    gr = gamma.float().detach().requires_grad_(True)
+    br = beta.float().detach().requires_grad_(True)
+    rm_r, rv_r = rm.clone(), rv.clone()
+    yr = torch.nn.functional.batch_norm(xr, rm_r, rv_r, gr, br, True, 0.1, 1e-3)
+    if relu:
+        yr = torch.relu(yr)
+    xk = x.detach().requires_grad_(True)
+    gk = gamma.detach().requires_grad_(True)
+    bk = beta.detach().requires_grad_(True)
+    yk = bn_act(xk, gk, bk, rm, rv, True, 0.1, 1e-3, relu)
+    assert yk.is_contiguous(memory_format=torch.channels_last)
+    _close(yk, yr, 2e-2, 2e-2, "bn fwd")
+    _close(rm, rm_r, 1e-3, 1e-4, "running_mean")
+    _close(rv, rv_r, 1e-3, 1e-3, "running_var")
+    dy = _nhwc(torch.randn(shape, device=cuda)).to(torch.bfloat16)
+    yr.backward(dy.float())
+    yk.backward(dy)
+    _close(xk.grad, xr.grad, 3e-2, 3e-2, "bn dx")
+    _close(gk.grad, gr.grad, 3e-2, 0.05 * gr.grad.abs().max().item() + 1e-2, "bn dgamma")
+    _close(bk.grad, br.grad, 3e-2, 0.05 * br.grad.abs().max().item() + 1e-2, "bn dbeta")
+
+
+def test_bn_act_strided_slice_and_eval(cuda):
+    from tony_amd.ops.bn import bn_act
+
+    big = _nhwc(torch.randn(4, 96, 9, 9, device=cuda)).to(torch.bfloat16)
+    big = _nhwc(big)
+    x = big[:, 32:64]  # channel slice of a channels_last buffer (ld = 96)
+    gamma = torch.ones(32, device=cuda)
+    beta = torch.zeros(32, device=cuda)
+    rm = torch.randn(32, device=cuda) * 0.1
+    rv = torch.rand(32, device=cuda) + 0.5
+    y = bn_act(x, gamma, beta, rm, rv, False, 0.1, 1e-3, True)
+    ref = torch.relu(torch.nn.functional.batch_norm(x.float(), rm, rv, gamma, beta, False, 0.1, 1e-3))
+    _close(y, ref, 2e-2, 2e-2, "bn eval on slice")
+
+
+@pytest.mark.parametrize("mnk", [(1000, 64, 192), (4096, 80, 64), (777, 320, 1280), (128, 1000, 2048), (33, 48, 256)])
+def test_gemm_nt(cuda, mnk):
+    from tony_amd.ops.gemm import gemm_nt
+
+    m, n, k = mnk
+    torch.manual_seed(1)
+    a = torch.randn(m, k, device=cuda).to(torch.bfloat16)
+    b = torch.randn(n, k, device=cuda).to(torch.bfloat16)
+    stats = torch.empty(2 * n, device=cuda)
+    c = gemm_nt(a, b, stats=stats)
+    ref = a.float() @ b.float().t()
+    _close(c, ref, 2e-2, 0.02 * (k ** 0.5), "gemm")
+    _close(stats[:n], ref.sum(0), 1e-2, 1e-2 * m ** 0.5 * k ** 0.5, "gemm col sum")
+    _close(stats[n:], (ref * ref).sum(0), 2e-2, 1e-1, "gemm col sumsq")
+
+
+def test_gemm_identity_asymmetric(cuda):
+    """A = I with an asymmetric B catches a transposed C/D map."""
+    from tony_amd.ops.gemm import gemm_nt
+
+    n = 96
+    a = torch.eye(128, 64, device=cuda).to(torch.bfloat16)
+    b = (torch.arange(n * 64, device=cuda).reshape(n, 64) % 17).to(torch.bfloat16)
+    c = gemm_nt(a, b)
+    ref = a.float() @ b.float().t()
+    assert torch.equal(c.float(), ref)
+
+
+@pytest.mark.parametrize("shape", [(4, 192, 35, 35, 64), (2, 64, 73, 73, 80), (8, 2048, 8, 8, 320)])
+def test_conv1x1_fwd_bwd(cuda, shape):
+    from tony_amd.ops.gemm import conv1x1
+
+    n, cin, h, w, cout = shape
+    torch.manual_seed(2)
+    x = _nhwc(torch.randn(n, cin, h, w, device=cuda)).to(torch.bfloat16)
+    x = _nhwc(x).requires_grad_(True)
+    wt = (torch.randn(cout, cin, 1, 1, device=cuda) * cin ** -0.5).to(torch.bfloat16).requires_grad_(True)
+    y = conv1x1(x, wt)
+    xr = x.detach().float().requires_grad_(True)
+    wr = wt.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, wr)
+    _close(y, yr, 2e-2, 3e-2, "conv1x1 fwd")
+    dy = _nhwc(torch.randn_like(yr)).to(torch.bfloat16)
+    y.backward(dy)
+    yr.backward(dy.float())
+    _close(x.grad, xr.grad, 2e-2, 3e-2 * (cout ** 0.5) / 4, "conv1x1 dx")
+    _close(wt.grad, wr.grad, 2e-2, 2e-2 * (n * h * w) ** 0.5, "conv1x1 dw")
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("smoothing", [0.0, 0.1])
+def test_cross_entropy(cuda, dtype, smoothing):
+    from tony_amd.ops import cross_entropy
+
+    torch.manual_seed(3)
+    logits = (torch.randn(64, 1000, device=cuda) * 3).to(dtype).requires_grad_(True)
+    y = torch.randint(0, 1000, (64,), device=cuda)
+    loss = cross_entropy(logits, y, label_smoothing=smoothing)
+    lr = logits.detach().float().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(lr, y, label_smoothing=smoothing)
+    assert abs(loss.item() - ref.item()) < 1e-3 * max(1, abs(ref.item()))
+    loss.backward()
+    ref.backward()
+    _close(logits.grad, lr.grad, 2e-2, 1e-4, "xent grad")
+
+
+@pytest.mark.parametrize("grad_dtype", [torch.bfloat16, torch.float32])
+def test_fused_sgd_matches_reference(cuda, grad_dtype):
+    from tony_amd.ops.optim import FlatSGD
+
+    n = 10_000 * 4
+    torch.manual_seed(4)
+    w0 = torch.randn(n, device=cuda)
+    opt = FlatSGD(w0.clone(), lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=False)
+    opt_ref = FlatSGD(w0.clone().cpu(), lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=False)
+    out = torch.empty(n, dtype=torch.bfloat16, device=cuda)
+    for _ in range(3):
+        g = torch.randn(n, device=cuda).to(grad_dtype)
+        opt.step(g, out_bf16=out)
+        opt_ref.step(g.cpu())
+    _close(opt.w.cpu(), opt_ref.w, 1e-5, 1e-5, "sgd w")
+    _close(out.cpu(), opt_ref.w, 1e-2, 1e-2, "sgd bf16 copy")
+
+
+def test_fused_adam_matches_torch(cuda):
+    from tony_amd.ops.optim import FlatAdam
+
+    n = 4096
+    torch.manual_seed(5)
+    w0 = torch.randn(n, device=cuda)
+    opt = FlatAdam(w0.clone(), lr=1e-2, weight_decay=1e-2, decoupled=True)
+    p = torch.nn.Parameter(w0.clone())
+    ref = torch.optim.AdamW([p], lr=1e-2, weight_decay=1e-2)
+    for _ in range(5):
+        g = torch.randn(n, device=cuda)
+        opt.step(g)
+        p.grad = g.clone()
+        ref.step()
+    _close(opt.w, p.detach(), 1e-4, 1e-5, "adamw")
+
+
+def test_grad_stats(cuda):
+    from tony_amd.ops.optim import grad_stats
+
+    g = torch.randn(4096, device=cuda).to(torch.bfloat16)
+    s = grad_stats(g)
+    assert abs(s[0].item() - (g.float() ** 2).sum().item()) < 1e-2 * s[0].item()
+    assert s[1].item() == 0
+    g[7] = float("inf")
+    assert grad_stats(g)[1].item() == 1

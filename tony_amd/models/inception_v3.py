@@ -1,0 +1,153 @@
+"""Inception-v3 (Szegedy et al. 2015), NHWC / bf16, for the TF-PS headline benchmark.
+
+The topology is the standard 299x299 Inception-v3 used by the TF-slim /
+tf_cnn_benchmarks job that TonY's paper runs as a parameter-server job
+(BASELINE.json config "Inception-v3 TF ParameterServerStrategy"): stem of five
+3x3/1x1 convs and two max-pools, 3x Inception-A (35x35), reduction-B,
+4x Inception-C with factorised 1x7/7x1 convs (17x17), the auxiliary head,
+reduction-D, 2x Inception-E with split 1x3/3x1 branches (8x8), global average
+pool, dropout and a 1000-way classifier.  BN epsilon is 1e-3 as in TF.
+
+Every conv is a ``ConvBNAct`` (conv + fused HIP BN+ReLU kernel); 1x1 convs run
+on the tony_amd MFMA GEMM.  Parameter count (with aux head): 27,161,264.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from .layers import ConvBNAct, init_weights
+
+
+class _Block(nn.Module):
+    """A set of parallel branches whose outputs are concatenated on channels."""
+
+    def __init__(self, fused):
+        super().__init__()
+        self.fused = fused
+
+    def c(self, cin, cout, k, s=1, p=0):
+        return ConvBNAct(cin, cout, k, s, p, eps=1e-3, fused=self.fused)
+
+
+class InceptionA(_Block):
+    def __init__(self, cin, pool_ch, fused=True):
+        super().__init__(fused)
+        self.b1 = self.c(cin, 64, 1)
+        self.b5 = nn.Sequential(self.c(cin, 48, 1), self.c(48, 64, 5, p=2))
+        self.b3 = nn.Sequential(self.c(cin, 64, 1), self.c(64, 96, 3, p=1), self.c(96, 96, 3, p=1))
+        self.bp = self.c(cin, pool_ch, 1)
+        self.out_channels = 64 + 64 + 96 + pool_ch
+
+    def forward(self, x):
+        p = nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=True)
+        return torch.cat([self.b1(x), self.b5(x), self.b3(x), self.bp(p)], 1)
+
+
+class InceptionB(_Block):  # 35x35 -> 17x17 reduction
+    def __init__(self, cin, fused=True):
+        super().__init__(fused)
+        self.b3 = self.c(cin, 384, 3, s=2)
+        self.bd = nn.Sequential(self.c(cin, 64, 1), self.c(64, 96, 3, p=1), self.c(96, 96, 3, s=2))
+        self.out_channels = 384 + 96 + cin
+
+    def forward(self, x):
+        return torch.cat([self.b3(x), self.bd(x), nn.functional.max_pool2d(x, 3, 2)], 1)
+
+
+class InceptionC(_Block):  # 17x17 with factorised 7x7
+    def __init__(self, cin, c7, fused=True):
+        super().__init__(fused)
+        self.b1 = self.c(cin, 192, 1)
+        self.b7 = nn.Sequential(self.c(cin, c7, 1), self.c(c7, c7, (1, 7), p=(0, 3)),
+                                self.c(c7, 192, (7, 1), p=(3, 0)))
+        self.bd = nn.Sequential(self.c(cin, c7, 1), self.c(c7, c7, (7, 1), p=(3, 0)),
+                                self.c(c7, c7, (1, 7), p=(0, 3)), self.c(c7, c7, (7, 1), p=(3, 0)),
+                                self.c(c7, 192, (1, 7), p=(0, 3)))
+        self.bp = self.c(cin, 192, 1)
+        self.out_channels = 768
+
+    def forward(self, x):
+        p = nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=True)
+        return torch.cat([self.b1(x), self.b7(x), self.bd(x), self.bp(p)], 1)
+
+
+class InceptionD(_Block):  # 17x17 -> 8x8 reduction
+    def __init__(self, cin, fused=True):
+        super().__init__(fused)
+        self.b3 = nn.Sequential(self.c(cin, 192, 1), self.c(192, 320, 3, s=2))
+        self.b7 = nn.Sequential(self.c(cin, 192, 1), self.c(192, 192, (1, 7), p=(0, 3)),
+                                self.c(192, 192, (7, 1), p=(3, 0)), self.c(192, 192, 3, s=2))
+        self.out_channels = 320 + 192 + cin
+
+    def forward(self, x):
+        return torch.cat([self.b3(x), self.b7(x), nn.functional.max_pool2d(x, 3, 2)], 1)
+
+
+class InceptionE(_Block):  # 8x8 with split 1x3 / 3x1 branches
+    def __init__(self, cin, fused=True):
+        super().__init__(fused)
+        self.b1 = self.c(cin, 320, 1)
+        self.b3 = self.c(cin, 384, 1)
+        self.b3a = self.c(384, 384, (1, 3), p=(0, 1))
+        self.b3b = self.c(384, 384, (3, 1), p=(1, 0))
+        self.bd = nn.Sequential(self.c(cin, 448, 1), self.c(448, 384, 3, p=1))
+        self.bda = self.c(384, 384, (1, 3), p=(0, 1))
+        self.bdb = self.c(384, 384, (3, 1), p=(1, 0))
+        self.bp = self.c(cin, 192, 1)
+        self.out_channels = 2048
+
+    def forward(self, x):
+        t = self.b3(x)
+        d = self.bd(x)
+        p = nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=True)
+        return torch.cat([self.b1(x), self.b3a(t), self.b3b(t), self.bda(d), self.bdb(d), self.bp(p)], 1)
+
+
+class InceptionAux(_Block):
+    def __init__(self, cin, num_classes, fused=True):
+        super().__init__(fused)
+        self.conv0 = self.c(cin, 128, 1)
+        self.conv1 = self.c(128, 768, 5)
+        self.fc = nn.Linear(768, num_classes)
+
+    def forward(self, x):
+        x = nn.functional.avg_pool2d(x, 5, 3)
+        x = self.conv1(self.conv0(x))
+        x = torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1)
+        return self.fc(x)
+
+
+class InceptionV3(nn.Module):
+    def __init__(self, num_classes=1000, aux_logits=True, dropout=0.5, fused=True):
+        super().__init__()
+        c = lambda cin, cout, k, s=1, p=0: ConvBNAct(cin, cout, k, s, p, eps=1e-3, fused=fused)  # noqa: E731
+        self.stem = nn.ModuleList([c(3, 32, 3, s=2), c(32, 32, 3), c(32, 64, 3, p=1)])
+        self.stem2 = nn.ModuleList([c(64, 80, 1), c(80, 192, 3)])
+        self.mixed_5 = nn.Sequential(InceptionA(192, 32, fused), InceptionA(256, 64, fused),
+                                     InceptionA(288, 64, fused))
+        self.mixed_6a = InceptionB(288, fused)
+        self.mixed_6 = nn.Sequential(InceptionC(768, 128, fused), InceptionC(768, 160, fused),
+                                     InceptionC(768, 160, fused), InceptionC(768, 192, fused))
+        self.aux = InceptionAux(768, num_classes, fused) if aux_logits else None
+        self.mixed_7 = nn.Sequential(InceptionD(768, fused), InceptionE(1280, fused), InceptionE(2048, fused))
+        self.dropout = nn.Dropout(dropout)
+        self.fc = nn.Linear(2048, num_classes)
+
+    def forward(self, x):
+        for m in self.stem:
+            x = m(x)
+        x = nn.functional.max_pool2d(x, 3, 2)
+        for m in self.stem2:
+            x = m(x)
+        x = nn.functional.max_pool2d(x, 3, 2)
+        x = self.mixed_6(self.mixed_6a(self.mixed_5(x)))
+        aux = self.aux(x) if (self.aux is not None and self.training) else None
+        x = self.mixed_7(x)
+        x = torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1)
+        logits = self.fc(self.dropout(x))
+        return (logits, aux) if aux is not None else logits
+
+
+def inception_v3(num_classes=1000, aux_logits=True, fused=True, seed=0) -> InceptionV3:
+    return init_weights(InceptionV3(num_classes, aux_logits, fused=fused), seed)

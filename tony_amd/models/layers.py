@@ -1,0 +1,63 @@
+"""Building blocks shared by the reference models (NHWC / channels_last, bf16).
+
+``ConvBNAct`` is the unit every CNN in tony_amd is made of: a bias-free conv
+(MIOpen implicit GEMM, or the tony_amd MFMA GEMM for 1x1/stride-1 convs) followed
+by the fused BN(+ReLU) HIP kernel.  ``fused=False`` builds the stock
+nn.BatchNorm2d + nn.ReLU pair instead; it exists only as the comparator for the
+"stock PyTorch-ROCm" baseline column and for CPU tests.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from ..ops.bn import BatchNormAct2d
+from ..ops.gemm import conv1x1
+
+
+def _pair(v):
+    return tuple(v) if isinstance(v, (tuple, list)) else (v, v)
+
+
+class ConvBNAct(nn.Module):
+    def __init__(self, cin, cout, kernel_size, stride=1, padding=0, eps=1e-3, relu=True, fused=True,
+                 momentum=0.1):
+        super().__init__()
+        k = _pair(kernel_size)
+        s = _pair(stride)
+        p = _pair(padding)
+        self.conv = nn.Conv2d(cin, cout, k, s, p, bias=False)
+        self.is_1x1 = k == (1, 1) and s == (1, 1) and p == (0, 0)
+        self.fused = fused
+        if fused:
+            self.bn = BatchNormAct2d(cout, eps=eps, momentum=momentum, relu=relu)
+        else:
+            self.bn = nn.BatchNorm2d(cout, eps=eps, momentum=momentum)
+            self.act = nn.ReLU(inplace=True) if relu else nn.Identity()
+
+    def forward(self, x):
+        if self.fused and self.is_1x1 and x.is_cuda:
+            y = conv1x1(x, self.conv.weight)
+        else:
+            y = self.conv(x)
+        if self.fused:
+            return self.bn(y)
+        return self.act(self.bn(y))
+
+
+def init_weights(model: nn.Module, seed: int = 0):
+    """Deterministic random init (truncated-normal-ish convs, zero biases)."""
+    g = torch.Generator().manual_seed(seed)
+    for m in model.modules():
+        if isinstance(m, (nn.Conv2d, nn.Linear)):
+            fan_in = m.weight[0].numel()
+            std = (2.0 / fan_in) ** 0.5 if isinstance(m, nn.Conv2d) else 0.01
+            with torch.no_grad():
+                m.weight.copy_(torch.randn(m.weight.shape, generator=g).clamp_(-2, 2) * std)
+                if m.bias is not None:
+                    m.bias.zero_()
+        elif isinstance(m, nn.BatchNorm2d):
+            with torch.no_grad():
+                m.weight.fill_(1.0)
+                m.bias.zero_()
+    return model

@@ -1,0 +1,93 @@
+"""ctypes binding of ``_tony_kernels.so`` (the gfx950 HIP kernels).
+
+torch is imported first on purpose: it loads its bundled HIP runtime, whose
+SONAME (``libamdhip64.so.7``) the kernel library then resolves to, so both share
+one runtime, one device context and the same stream handles.
+
+On a machine with a GPU the library is REQUIRED: ``lib()`` raises if it is
+missing or fails to load, so no test or benchmark silently runs an eager
+PyTorch fallback.  On a CPU-only container ops called with CPU tensors use the
+reference implementations in ``tony_amd.ops.reference``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the dlopen below)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+SO_PATH = os.path.join(_HERE, "_tony_kernels.so")
+
+_lock = threading.Lock()
+_lib = None
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_int64 = ctypes.c_int64
+c_float = ctypes.c_float
+
+_SIGNATURES = {
+    "tony_bn_fwd_train": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int,
+                          c_float, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p],
+    "tony_bn_fwd_infer": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int,
+                          c_float, c_int, c_void_p, c_void_p, c_void_p],
+    "tony_bn_bwd": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p,
+                    c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "tony_sgd_step": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p],
+    "tony_adam_step": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p],
+    "tony_grad_stats": [c_void_p, c_int, c_int64, c_void_p, c_void_p],
+    "tony_xent_fwd": [c_void_p, c_int, c_int64, c_int, c_int64, c_void_p, c_float, c_void_p, c_void_p, c_void_p],
+    "tony_xent_bwd": [c_void_p, c_int, c_int64, c_int, c_int64, c_void_p, c_float, c_void_p, c_void_p, c_void_p,
+                      c_int64, c_void_p],
+    "tony_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64,
+                       c_int, c_void_p, c_void_p],
+}
+
+
+class KernelError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the kernel library; raise loudly if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(SO_PATH):
+            raise KernelError(
+                f"{SO_PATH} is missing: run `python -m tony_amd.ops.build` (or __graft_entry__.build())")
+        h = ctypes.CDLL(SO_PATH, mode=ctypes.RTLD_LOCAL)
+        for name, argtypes in _SIGNATURES.items():
+            fn = getattr(h, name, None)
+            if fn is None:
+                continue
+            fn.argtypes = argtypes
+            fn.restype = c_int
+        _lib = h
+    return _lib
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except (KernelError, OSError):
+        return False
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def check(rc: int, name: str):
+    if rc != 0:
+        raise KernelError(f"{name} failed with code {rc}")
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()

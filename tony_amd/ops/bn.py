@@ -1,0 +1,127 @@
+"""Fused BatchNorm(+ReLU) on NHWC bf16 activations (HIP kernels in csrc/bn_act.hip).
+
+``bn_act(x, weight, bias, running_mean, running_var, training, momentum, eps, relu)``
+is a drop-in for ``relu(batch_norm(x, ...))`` on channels_last tensors.  The
+HIP path is taken for CUDA bf16 tensors; CPU tensors use the PyTorch reference
+(so the control-plane / local-mode tests run on a CPU-only container).  A CUDA
+tensor of another dtype is an error, not a silent fallback.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def _rows_view(t: torch.Tensor):
+    """Return (M, C, ld) when ``t``'s memory is M rows of C channels with row
+    stride ``ld`` (channels_last 4D, a channel slice of one, or 2D [M, C])."""
+    if t.dim() == 4:
+        n, c, h, w = t.shape
+        sn, sc, sh, sw = t.stride()
+        if sc != 1:
+            return None
+        ld = sw
+        if (h > 1 and sh != w * ld) or (n > 1 and sn != h * w * ld) or ld < c:
+            return None
+        if w == 1 and h == 1 and n > 1:
+            ld = sn
+        return n * h * w, c, ld
+    if t.dim() == 2:
+        m, c = t.shape
+        if t.stride(1) != 1:
+            return None
+        return m, c, t.stride(0) if m > 1 else c
+    return None
+
+
+def _as_rows(t: torch.Tensor):
+    rv = _rows_view(t)
+    if rv is None or rv[2] % 8 != 0 or t.data_ptr() % 16 != 0:
+        t = t.contiguous(memory_format=torch.channels_last) if t.dim() == 4 else t.contiguous()
+        rv = _rows_view(t)
+    return t, rv
+
+
+def _empty_like_rows(x: torch.Tensor) -> torch.Tensor:
+    if x.dim() == 4:
+        return torch.empty(x.shape, dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    return torch.empty(x.shape, dtype=x.dtype, device=x.device)
+
+
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, relu):
+        L = _lib.lib()
+        x, (M, C, ldx) = _as_rows(x)
+        y = _empty_like_rows(x)
+        _, _, ldy = _rows_view(y)
+        pb = int(weight is not None and weight.dtype == torch.bfloat16)
+        stream = _lib.stream_ptr(x.device)
+        if training:
+            ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+            mean = torch.empty(C, dtype=torch.float32, device=x.device)
+            invstd = torch.empty(C, dtype=torch.float32, device=x.device)
+            rc = L.tony_bn_fwd_train(x.data_ptr(), M, C, ldx, y.data_ptr(), ldy, _lib.ptr(weight), _lib.ptr(bias),
+                                     pb, float(eps), int(relu), ws.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                                     _lib.ptr(running_mean), _lib.ptr(running_var), float(momentum), stream)
+            _lib.check(rc, "tony_bn_fwd_train")
+        else:
+            mean = running_mean
+            invstd = torch.rsqrt(running_var.float() + eps)
+            rc = L.tony_bn_fwd_infer(x.data_ptr(), M, C, ldx, y.data_ptr(), ldy, _lib.ptr(weight), _lib.ptr(bias),
+                                     pb, float(eps), int(relu), running_mean.data_ptr(), running_var.data_ptr(),
+                                     stream)
+            _lib.check(rc, "tony_bn_fwd_infer")
+        ctx.save_for_backward(x, weight, bias, mean, invstd)
+        ctx.relu = relu
+        ctx.pb = pb
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = _lib.lib()
+        x, weight, bias, mean, invstd = ctx.saved_tensors
+        M, C, ldx = _rows_view(x)
+        dy, (_, _, lddy) = _as_rows(dy)
+        dx = _empty_like_rows(x)
+        _, _, lddx = _rows_view(dx)
+        ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+        dw = torch.empty_like(weight) if weight is not None else None
+        db = torch.empty_like(bias) if bias is not None else None
+        rc = L.tony_bn_bwd(x.data_ptr(), ldx, dy.data_ptr(), lddy, dx.data_ptr(), lddx, M, C, mean.data_ptr(),
+                           invstd.data_ptr(), _lib.ptr(weight), _lib.ptr(bias), ctx.pb, int(ctx.relu),
+                           ws.data_ptr(), _lib.ptr(dw), _lib.ptr(db), _lib.stream_ptr(x.device))
+        _lib.check(rc, "tony_bn_bwd")
+        return dx, dw, db, None, None, None, None, None, None
+
+
+def bn_act_reference(x, weight, bias, running_mean, running_var, training, momentum, eps, relu):
+    y = torch.nn.functional.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
+    return torch.relu(y) if relu else y
+
+
+def bn_act(x, weight, bias, running_mean, running_var, training=True, momentum=0.1, eps=1e-5, relu=True):
+    if x.is_cuda:
+        if x.dtype != torch.bfloat16:
+            raise TypeError(f"bn_act HIP kernel takes bf16 activations, got {x.dtype}")
+        return _BNActFn.apply(x, weight, bias, running_mean, running_var, training, momentum, eps, relu)
+    return bn_act_reference(x, weight, bias, running_mean, running_var, training, momentum, eps, relu)
+
+
+class BatchNormAct2d(torch.nn.BatchNorm2d):
+    """BatchNorm2d fused with an optional ReLU, NHWC bf16 on the GPU."""
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, relu=True, **kw):
+        super().__init__(num_features, eps=eps, momentum=momentum, **kw)
+        self.relu = relu
+
+    def forward(self, x):
+        training = self.training or not self.track_running_stats
+        if self.training and self.track_running_stats and self.momentum is None:
+            # only needed for cumulative averaging; skipping it saves one
+            # launch per BN layer per step on the fixed-momentum hot path
+            self.num_batches_tracked.add_(1)
+        return bn_act(x, self.weight, self.bias, self.running_mean if self.track_running_stats else None,
+                      self.running_var if self.track_running_stats else None, training, self.momentum, self.eps,
+                      self.relu)

@@ -1,0 +1,373 @@
+// NHWC BatchNorm (+ optional ReLU) for training and inference, bf16 activations.
+//
+// This is the fused "BN+ReLU" of every Inception-v3 BasicConv2d and ResNet
+// conv-bn-relu.  Layout is NHWC flattened to [M, C]
+// rows (M = N*H*W) with a row stride `ld` so a branch output can be written
+// straight into its channel slice of an Inception concat buffer (H7).
+//
+// Forward  = stats kernel (per-channel sum / sum-of-squares, fp32, LDS tree +
+//            one device atomic per channel per workgroup) + apply kernel
+//            (normalise, affine, ReLU, bf16 store).  Every workgroup of the
+//            apply kernel rebuilds scale/shift for all C channels in LDS from
+//            the sums, so no finalize launch is needed.
+// Backward = reduce kernel (sum dy', sum dy'*xhat with the ReLU mask
+//            recomputed from x, so y is never re-read) + apply kernel.
+//
+// Thread map: one 16-byte (8-channel) vector per lane; a 256-thread workgroup
+// covers RPI = 256/(C/8) rows per iteration, so a wavefront always reads a
+// contiguous 1 KiB span of the row-major image (fully coalesced for any C%8==0).
+#include "common.h"
+
+using namespace tony;
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxC = 2048;
+
+struct RowMap {
+  int CG, RPI, cg, rsub;
+  bool active;
+  __device__ RowMap(int C) {
+    CG = C >> 3;
+    RPI = kThreads / CG;
+    cg = threadIdx.x % CG;
+    rsub = threadIdx.x / CG;
+    active = rsub < RPI;
+  }
+};
+
+__device__ __forceinline__ float load_param(const void* p, int idx, int is_bf16, float dflt) {
+  if (p == nullptr) return dflt;
+  return is_bf16 ? bf2f(static_cast<const uint16_t*>(p)[idx]) : static_cast<const float*>(p)[idx];
+}
+
+__device__ __forceinline__ void store_param(void* p, int idx, int is_bf16, float v) {
+  if (p == nullptr) return;
+  if (is_bf16)
+    static_cast<uint16_t*>(p)[idx] = f2bf(v);
+  else
+    static_cast<float*>(p)[idx] = v;
+}
+
+// Reduce per-thread partials over the RPI row-lanes in LDS and add one value
+// per channel into global `out` (2*C floats: [sum | sum2]).
+__device__ __forceinline__ void block_reduce_add(float* red, const RowMap& rm, int C,
+                                                 const float* a, const float* b, float* out) {
+  if (rm.active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[rm.rsub * C + rm.cg * 8 + j] = a[j];
+      red[kMaxC + rm.rsub * C + rm.cg * 8 + j] = b[j];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    float sa = 0.f, sb = 0.f;
+    for (int k = 0; k < rm.RPI; ++k) {
+      sa += red[k * C + c];
+      sb += red[kMaxC + k * C + c];
+    }
+    atomicAdd(out + c, sa);
+    atomicAdd(out + C + c, sb);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void bn_fwd_stats_kernel(
+    const uint16_t* __restrict__ x, int64_t M, int C, int64_t ldx, int64_t rows_per_block,
+    float* __restrict__ sums) {
+  __shared__ float red[kMaxC * 2];
+  RowMap rm(C);
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  if (rm.active) {
+    const uint16_t* base = x + rm.cg * 8;
+    int64_t r = r0 + rm.rsub;
+    const int64_t step = rm.RPI;
+    for (; r + 3 * step < r1; r += 4 * step) {
+      bf16x8 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = load8(base + (r + u * step) * ldx);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float f[8];
+        v[u].to_float(f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s[j] += f[j];
+          q[j] = fmaf(f[j], f[j], q[j]);
+        }
+      }
+    }
+    for (; r < r1; r += step) {
+      float f[8];
+      load8(base + r * ldx).to_float(f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += f[j];
+        q[j] = fmaf(f[j], f[j], q[j]);
+      }
+    }
+  }
+  block_reduce_add(red, rm, C, s, q, sums);
+}
+
+// mode 0: training (stats from sums, saves mean/invstd, updates running stats)
+// mode 1: inference (stats from running_mean / running_var)
+__global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
+    const uint16_t* __restrict__ x, int64_t M, int C, int64_t ldx, int64_t rows_per_block,
+    uint16_t* __restrict__ y, int64_t ldy, const float* __restrict__ sums,
+    const void* gamma, const void* beta, int param_bf16, float eps, int relu, int mode,
+    float* __restrict__ save_mean, float* __restrict__ save_invstd,
+    float* __restrict__ running_mean, float* __restrict__ running_var, float momentum) {
+  __shared__ float scale[kMaxC];
+  __shared__ float shift[kMaxC];
+  const float inv_m = 1.f / static_cast<float>(M);
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    float mean, invstd;
+    if (mode == 0) {
+      mean = sums[c] * inv_m;
+      float var = fmaxf(sums[C + c] * inv_m - mean * mean, 0.f);
+      invstd = rsqrtf(var + eps);
+      if (blockIdx.x == 0) {
+        save_mean[c] = mean;
+        save_invstd[c] = invstd;
+        if (running_mean != nullptr) {
+          const float unbiased = M > 1 ? var * (static_cast<float>(M) / static_cast<float>(M - 1)) : var;
+          running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+          running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+        }
+      }
+    } else {
+      mean = running_mean[c];
+      invstd = rsqrtf(running_var[c] + eps);
+    }
+    const float g = load_param(gamma, c, param_bf16, 1.f);
+    const float b = load_param(beta, c, param_bf16, 0.f);
+    scale[c] = g * invstd;
+    shift[c] = b - mean * g * invstd;
+  }
+  __syncthreads();
+  RowMap rm(C);
+  if (!rm.active) return;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = scale[rm.cg * 8 + j];
+    sh[j] = shift[rm.cg * 8 + j];
+  }
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  const int64_t step = rm.RPI;
+  int64_t r = r0 + rm.rsub;
+  auto body = [&](const bf16x8& v, int64_t row) {
+    float f[8];
+    v.to_float(f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = fmaf(f[j], sc[j], sh[j]);
+      f[j] = relu ? fmaxf(t, 0.f) : t;
+    }
+    store8(y + row * ldy + rm.cg * 8, bf16x8::from_float(f));
+  };
+  for (; r + 3 * step < r1; r += 4 * step) {
+    bf16x8 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = load8(x + (r + u * step) * ldx + rm.cg * 8);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) body(v[u], r + u * step);
+  }
+  for (; r < r1; r += step) body(load8(x + r * ldx + rm.cg * 8), r);
+}
+
+// Backward reduction: dsums[c] = sum(dy'), dsums[C+c] = sum(dy' * xhat),
+// where dy' = dy masked by the ReLU (recomputed from x).
+__global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
+    const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __restrict__ dy, int64_t lddy,
+    int64_t M, int C, int64_t rows_per_block, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const void* gamma, const void* beta, int param_bf16,
+    int relu, float* __restrict__ dsums) {
+  __shared__ float red[kMaxC * 2];
+  RowMap rm(C);
+  float a[8], b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = b[j] = 0.f;
+  if (rm.active) {
+    float mu[8], is[8], sc[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = rm.cg * 8 + j;
+      mu[j] = mean[c];
+      is[j] = invstd[c];
+      const float g = load_param(gamma, c, param_bf16, 1.f);
+      sc[j] = g;
+      sh[j] = load_param(beta, c, param_bf16, 0.f);
+    }
+    const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+    const int64_t r1 = min(M, r0 + rows_per_block);
+    const int64_t step = rm.RPI;
+    auto body = [&](const bf16x8& xv, const bf16x8& gv) {
+      float xf[8], gf[8];
+      xv.to_float(xf);
+      gv.to_float(gf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xh = (xf[j] - mu[j]) * is[j];
+        float d = gf[j];
+        if (relu && fmaf(xh, sc[j], sh[j]) <= 0.f) d = 0.f;
+        a[j] += d;
+        b[j] = fmaf(d, xh, b[j]);
+      }
+    };
+    int64_t r = r0 + rm.rsub;
+    for (; r + 1 * step < r1; r += 2 * step) {
+      bf16x8 xv0 = load8(x + r * ldx + rm.cg * 8);
+      bf16x8 gv0 = load8(dy + r * lddy + rm.cg * 8);
+      bf16x8 xv1 = load8(x + (r + step) * ldx + rm.cg * 8);
+      bf16x8 gv1 = load8(dy + (r + step) * lddy + rm.cg * 8);
+      body(xv0, gv0);
+      body(xv1, gv1);
+    }
+    for (; r < r1; r += step) body(load8(x + r * ldx + rm.cg * 8), load8(dy + r * lddy + rm.cg * 8));
+  }
+  block_reduce_add(red, rm, C, a, b, dsums);
+}
+
+__global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
+    const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __restrict__ dy, int64_t lddy,
+    uint16_t* __restrict__ dx, int64_t lddx, int64_t M, int C, int64_t rows_per_block,
+    const float* __restrict__ mean, const float* __restrict__ invstd, const void* gamma,
+    const void* beta, int param_bf16, int relu, const float* __restrict__ dsums, void* dgamma,
+    void* dbeta) {
+  __shared__ float k_s[kMaxC], a_s[kMaxC], b_s[kMaxC];
+  const float inv_m = 1.f / static_cast<float>(M);
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    const float g = load_param(gamma, c, param_bf16, 1.f);
+    k_s[c] = g * invstd[c];
+    a_s[c] = dsums[c] * inv_m;
+    b_s[c] = dsums[C + c] * inv_m;
+    if (blockIdx.x == 0) {
+      store_param(dbeta, c, param_bf16, dsums[c]);
+      store_param(dgamma, c, param_bf16, dsums[C + c]);
+    }
+  }
+  __syncthreads();
+  RowMap rm(C);
+  if (!rm.active) return;
+  float mu[8], is[8], g[8], be[8], k[8], am[8], bm[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = rm.cg * 8 + j;
+    mu[j] = mean[c];
+    is[j] = invstd[c];
+    g[j] = load_param(gamma, c, param_bf16, 1.f);
+    be[j] = load_param(beta, c, param_bf16, 0.f);
+    k[j] = k_s[c];
+    am[j] = a_s[c];
+    bm[j] = b_s[c];
+  }
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  const int64_t step = rm.RPI;
+  auto body = [&](const bf16x8& xv, const bf16x8& gv, int64_t row) {
+    float xf[8], gf[8], o[8];
+    xv.to_float(xf);
+    gv.to_float(gf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float xh = (xf[j] - mu[j]) * is[j];
+      float d = gf[j];
+      if (relu && fmaf(xh, g[j], be[j]) <= 0.f) d = 0.f;
+      o[j] = k[j] * (d - am[j] - xh * bm[j]);
+    }
+    store8(dx + row * lddx + rm.cg * 8, bf16x8::from_float(o));
+  };
+  int64_t r = r0 + rm.rsub;
+  for (; r + 1 * step < r1; r += 2 * step) {
+    bf16x8 xv0 = load8(x + r * ldx + rm.cg * 8);
+    bf16x8 gv0 = load8(dy + r * lddy + rm.cg * 8);
+    bf16x8 xv1 = load8(x + (r + step) * ldx + rm.cg * 8);
+    bf16x8 gv1 = load8(dy + (r + step) * lddy + rm.cg * 8);
+    body(xv0, gv0, r);
+    body(xv1, gv1, r + step);
+  }
+  for (; r < r1; r += step) body(load8(x + r * ldx + rm.cg * 8), load8(dy + r * lddy + rm.cg * 8), r);
+}
+
+// Grid sizing: enough workgroups to cover 256 CUs several times over, but each
+// workgroup streams >= `min_iters` row groups so the per-WG LDS epilogue and
+// atomics stay amortised.
+void plan_rows(int64_t M, int C, int min_iters, int max_blocks, int64_t* rpb, int* grid) {
+  const int RPI = kThreads / (C / 8);
+  int64_t g = (M + static_cast<int64_t>(RPI) * min_iters - 1) / (static_cast<int64_t>(RPI) * min_iters);
+  if (g > max_blocks) g = max_blocks;
+  if (g < 1) g = 1;
+  int64_t r = (M + g - 1) / g;
+  r = ((r + RPI - 1) / RPI) * RPI;
+  *rpb = r;
+  *grid = static_cast<int>((M + r - 1) / r);
+}
+
+bool bad_c(int C) { return C <= 0 || C % 8 != 0 || C > kMaxC; }
+
+}  // namespace
+
+TONY_API int tony_bn_fwd_train(const void* x, int64_t M, int C, int64_t ldx, void* y, int64_t ldy,
+                               const void* gamma, const void* beta, int param_bf16, float eps,
+                               int relu, float* sums_ws, float* save_mean, float* save_invstd,
+                               float* running_mean, float* running_var, float momentum,
+                               hipStream_t stream) {
+  if (bad_c(C) || (ldx % 8) || (ldy % 8)) return -1;
+  (void)hipMemsetAsync(sums_ws, 0, sizeof(float) * 2 * C, stream);
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 16, 2048, &rpb, &grid);
+  bn_fwd_stats_kernel<<<grid, kThreads, 0, stream>>>(static_cast<const uint16_t*>(x), M, C, ldx, rpb,
+                                                    sums_ws);
+  plan_rows(M, C, 4, 4096, &rpb, &grid);
+  bn_fwd_apply_kernel<<<grid, kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), M, C, ldx, rpb, static_cast<uint16_t*>(y), ldy, sums_ws, gamma,
+      beta, param_bf16, eps, relu, 0, save_mean, save_invstd, running_mean, running_var, momentum);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+TONY_API int tony_bn_fwd_infer(const void* x, int64_t M, int C, int64_t ldx, void* y, int64_t ldy,
+                               const void* gamma, const void* beta, int param_bf16, float eps,
+                               int relu, const float* running_mean, const float* running_var,
+                               hipStream_t stream) {
+  if (bad_c(C) || (ldx % 8) || (ldy % 8)) return -1;
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 4, 4096, &rpb, &grid);
+  bn_fwd_apply_kernel<<<grid, kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), M, C, ldx, rpb, static_cast<uint16_t*>(y), ldy, nullptr, gamma,
+      beta, param_bf16, eps, relu, 1, nullptr, nullptr, const_cast<float*>(running_mean),
+      const_cast<float*>(running_var), 0.f);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+TONY_API int tony_bn_bwd(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx,
+                         int64_t lddx, int64_t M, int C, const float* mean, const float* invstd,
+                         const void* gamma, const void* beta, int param_bf16, int relu,
+                         float* dsums_ws, void* dgamma, void* dbeta, hipStream_t stream) {
+  if (bad_c(C) || (ldx % 8) || (lddy % 8) || (lddx % 8)) return -1;
+  (void)hipMemsetAsync(dsums_ws, 0, sizeof(float) * 2 * C, stream);
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 16, 2048, &rpb, &grid);
+  bn_bwd_reduce_kernel<<<grid, kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, M, C, rpb, mean,
+      invstd, gamma, beta, param_bf16, relu, dsums_ws);
+  plan_rows(M, C, 4, 4096, &rpb, &grid);
+  bn_bwd_apply_kernel<<<grid, kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy,
+      static_cast<uint16_t*>(dx), lddx, M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu,
+      dsums_ws, dgamma, dbeta);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}

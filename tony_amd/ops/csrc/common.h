@@ -1,0 +1,82 @@
+// Shared helpers for the tony_amd CDNA4 (gfx950) kernels.
+//
+// All kernels in this directory are written directly for gfx950: 64-lane
+// wavefronts, 16-byte vector memory ops, bf16 stored as raw uint16 bits and
+// converted with the hardware cvt (v_cvt_pk_bf16_f32 keeps NaN a NaN).
+// Every host entry point is `extern "C"` and takes the HIP stream explicitly so
+// the Python side (ctypes) can launch on torch's current stream and the calls
+// are capturable into HIP graphs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define TONY_API extern "C" __attribute__((visibility("default")))
+
+namespace tony {
+
+static constexpr int kWave = 64;  // CDNA wavefront width (never 32)
+
+__device__ __forceinline__ float bf2f(uint16_t v) {
+  return __uint_as_float(static_cast<uint32_t>(v) << 16);
+}
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = static_cast<__bf16>(f);  // lowers to v_cvt_pk_bf16_f32 (RNE)
+  return __builtin_bit_cast(uint16_t, b);
+}
+
+// 8 bf16 <-> one 16-byte vector register quad.
+struct bf16x8 {
+  uint4 raw;
+  __device__ __forceinline__ void to_float(float* f) const {
+    const uint32_t w[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[2 * i] = __uint_as_float(w[i] << 16);
+      f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  __device__ __forceinline__ static bf16x8 from_float(const float* f) {
+    bf16x8 r;
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      w[i] = static_cast<uint32_t>(f2bf(f[2 * i])) |
+             (static_cast<uint32_t>(f2bf(f[2 * i + 1])) << 16);
+    }
+    r.raw = make_uint4(w[0], w[1], w[2], w[3]);
+    return r;
+  }
+};
+
+__device__ __forceinline__ bf16x8 load8(const uint16_t* p) {
+  bf16x8 r;
+  r.raw = *reinterpret_cast<const uint4*>(p);
+  return r;
+}
+__device__ __forceinline__ void store8(uint16_t* p, const bf16x8& v) {
+  *reinterpret_cast<uint4*>(p) = v.raw;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+inline int ceil_div(int64_t a, int64_t b) { return static_cast<int>((a + b - 1) / b); }
+
+}  // namespace tony
+
+// Error code convention for the C ABI: 0 ok, negative = argument error,
+// positive = hipError_t from the launch.
+#define TONY_LAUNCH_CHECK()                         \
+  do {                                              \
+    hipError_t _e = hipGetLastError();              \
+    if (_e != hipSuccess) return static_cast<int>(_e); \
+  } while (0)

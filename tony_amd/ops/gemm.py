@@ -1,0 +1,86 @@
+"""MFMA bf16 GEMM (csrc/gemm.hip) and the NHWC 1x1 convolution built on it.
+
+A stride-1, unpadded 1x1 convolution on a channels_last tensor is exactly a GEMM
+over rows: Y[NHW, Cout] = X[NHW, Cin] . W[Cout, Cin]^T.  Forward and the
+backward-data GEMM run on the hand-written MFMA kernel; the weight gradient
+(a reduction over all NHW rows into a tiny Cout x Cin matrix) is a plain
+library GEMM and goes to hipBLASLt through torch.mm.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .bn import _as_rows, _rows_view
+
+
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, stats: torch.Tensor | None = None):
+    """out[M,N] = a[M,K] @ b[N,K]^T for bf16 CUDA 2-D tensors with unit inner stride."""
+    if not (a.is_cuda and b.is_cuda) or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
+        raise TypeError("gemm_nt takes bf16 CUDA tensors")
+    if a.stride(1) != 1:
+        a = a.contiguous()
+    if b.stride(1) != 1:
+        b = b.contiguous()
+    M, K = a.shape
+    N, K2 = b.shape
+    if K != K2:
+        raise ValueError(f"inner dims differ: {a.shape} x {b.shape}^T")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    rc = _lib.lib().tony_gemm_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0) if M > 1 else K,
+                                   b.stride(0) if N > 1 else K, out.stride(0) if M > 1 else N,
+                                   1 if stats is not None else 0, _lib.ptr(stats), _lib.stream_ptr(a.device))
+    _lib.check(rc, "tony_gemm_bf16")
+    return out
+
+
+def _gemm_rows(a_ptr, lda, b, M, N, K, out_ptr, ldc, device):
+    rc = _lib.lib().tony_gemm_bf16(a_ptr, b.data_ptr(), out_ptr, M, N, K, lda, b.stride(0), ldc, 0, 0,
+                                   _lib.stream_ptr(device))
+    _lib.check(rc, "tony_gemm_bf16")
+
+
+class _Conv1x1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight):
+        cout, cin = weight.shape[0], weight.shape[1]
+        x, (M, C, ldx) = _as_rows(x)
+        if C != cin:
+            raise ValueError("channel mismatch")
+        w2 = weight.reshape(cout, cin)
+        if w2.stride(1) != 1 or w2.stride(0) != cin:
+            w2 = w2.contiguous()
+        n, _, h, w = x.shape
+        y = torch.empty((n, cout, h, w), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+        _gemm_rows(x.data_ptr(), ldx, w2, M, cout, cin, y.data_ptr(), cout, x.device)
+        ctx.save_for_backward(x, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        cout, cin = weight.shape[0], weight.shape[1]
+        M, _, ldx = _rows_view(x)
+        dy, (_, _, lddy) = _as_rows(dy)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wt = weight.reshape(cout, cin).t().contiguous()  # [Cin, Cout]
+            dx = torch.empty(x.shape, dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+            _gemm_rows(dy.data_ptr(), lddy, wt, M, cin, cout, dx.data_ptr(), cin, x.device)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dy2 = dy.permute(0, 2, 3, 1).reshape(M, cout) if lddy == cout else \
+                torch.as_strided(dy, (M, cout), (lddy, 1))
+            x2 = x.permute(0, 2, 3, 1).reshape(M, cin) if ldx == cin else torch.as_strided(x, (M, cin), (ldx, 1))
+            dw = torch.mm(dy2.t(), x2).reshape(weight.shape).to(weight.dtype)
+        return dx, dw
+
+
+def conv1x1(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """Stride-1 unpadded 1x1 convolution of a channels_last bf16 tensor."""
+    if x.is_cuda:
+        if x.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16:
+            raise TypeError("conv1x1 MFMA path takes bf16 activations and weights")
+        return _Conv1x1Fn.apply(x, weight)
+    return torch.nn.functional.conv2d(x, weight)

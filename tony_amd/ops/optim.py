@@ -1,0 +1,154 @@
+"""Fused optimizers over flat parameter shards (HIP kernels in csrc/optim.hip).
+
+``FlatSGD`` / ``FlatAdam`` own an fp32 master copy of a flat parameter shard
+plus its optimizer state, consume a flat gradient (bf16 or fp32) and write the
+updated bf16 compute copy in the same pass.  The PS shard (``tony_amd.parallel.ps``)
+and the data-parallel engine use them directly; on CPU tensors the same update
+is computed with PyTorch ops (used by the CPU test-suite and local mode).
+
+Hyper-parameters are kept in a device tensor that is refreshed (a 36-byte H2D
+copy) before each step, so a captured HIP graph sees the current lr / step.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+class _FlatOptimizer:
+    n_hp = 0
+
+    def __init__(self, master: torch.Tensor, lr: float, weight_decay: float = 0.0):
+        if master.dtype != torch.float32 or master.dim() != 1:
+            raise TypeError("master shard must be a flat fp32 tensor")
+        if master.numel() % 4:
+            raise ValueError("flat shard length must be a multiple of 4 (pad the buffer)")
+        self.w = master
+        self.lr = float(lr)
+        self.weight_decay = float(weight_decay)
+        self.grad_scale = 1.0
+        self.step_count = 0
+        dev = master.device
+        self._hp_last = None
+        self._hp_dev = torch.zeros(self.n_hp, dtype=torch.float32, device=dev)
+
+    def _hp_values(self):
+        raise NotImplementedError
+
+    def _push_hp(self):
+        if self.w.is_cuda and torch.cuda.is_current_stream_capturing():
+            return  # graph capture: the Trainer refreshes hp before every replay
+        vals = [float(v) for v in self._hp_values()]
+        if vals == self._hp_last:
+            return  # unchanged (constant-lr SGD): no H2D traffic at all
+        # pageable source: the copy is staged before copy_ returns, so the host
+        # may rewrite its values for the next step without racing the DMA
+        self._hp_dev.copy_(torch.tensor(vals, dtype=torch.float32), non_blocking=True)
+        self._hp_last = vals
+
+    def state_dict(self):
+        raise NotImplementedError
+
+
+class FlatSGD(_FlatOptimizer):
+    """SGD with (Nesterov) momentum: v = mu*v + g + wd*w ; w -= lr*v (TF MomentumOptimizer semantics)."""
+
+    n_hp = 5
+
+    def __init__(self, master, lr, momentum=0.9, weight_decay=0.0, nesterov=False):
+        super().__init__(master, lr, weight_decay)
+        self.momentum = float(momentum)
+        self.nesterov = bool(nesterov)
+        self.v = torch.zeros_like(master)
+
+    def _hp_values(self):
+        return [self.lr, self.momentum, self.weight_decay, self.grad_scale, 1.0 if self.nesterov else 0.0]
+
+    def step(self, grad: torch.Tensor, out_bf16: torch.Tensor | None = None):
+        self.step_count += 1
+        if grad.numel() != self.w.numel():
+            raise ValueError("grad / shard size mismatch")
+        if self.w.is_cuda:
+            self._push_hp()
+            rc = _lib.lib().tony_sgd_step(self.w.data_ptr(), self.v.data_ptr(), grad.data_ptr(),
+                                          int(grad.dtype == torch.bfloat16), _lib.ptr(out_bf16), self.w.numel(),
+                                          self._hp_dev.data_ptr(), _lib.stream_ptr(self.w.device))
+            _lib.check(rc, "tony_sgd_step")
+            return
+        g = grad.float() * self.grad_scale + self.weight_decay * self.w
+        self.v.mul_(self.momentum).add_(g)
+        upd = g + self.momentum * self.v if self.nesterov else self.v
+        self.w.add_(upd, alpha=-self.lr)
+        if out_bf16 is not None:
+            out_bf16.copy_(self.w)
+
+    def state_dict(self):
+        return {"kind": "sgd", "step": self.step_count, "momentum_buffer": self.v, "lr": self.lr}
+
+    def load_state_dict(self, sd):
+        self.step_count = int(sd["step"])
+        self.v.copy_(sd["momentum_buffer"])
+        self.lr = float(sd.get("lr", self.lr))
+
+
+class FlatAdam(_FlatOptimizer):
+    """Adam / AdamW (``decoupled=True``) with bias correction."""
+
+    n_hp = 9
+
+    def __init__(self, master, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, decoupled=False):
+        super().__init__(master, lr, weight_decay)
+        self.b1, self.b2 = float(betas[0]), float(betas[1])
+        self.eps = float(eps)
+        self.decoupled = bool(decoupled)
+        self.m = torch.zeros_like(master)
+        self.v = torch.zeros_like(master)
+
+    def _hp_values(self):
+        t = self.step_count
+        return [self.lr, self.b1, self.b2, self.eps, self.weight_decay, self.grad_scale,
+                1.0 - self.b1 ** t, 1.0 - self.b2 ** t, 1.0 if self.decoupled else 0.0]
+
+    def step(self, grad: torch.Tensor, out_bf16: torch.Tensor | None = None):
+        self.step_count += 1
+        if self.w.is_cuda:
+            self._push_hp()
+            rc = _lib.lib().tony_adam_step(self.w.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), grad.data_ptr(),
+                                           int(grad.dtype == torch.bfloat16), _lib.ptr(out_bf16), self.w.numel(),
+                                           self._hp_dev.data_ptr(), _lib.stream_ptr(self.w.device))
+            _lib.check(rc, "tony_adam_step")
+            return
+        t = self.step_count
+        g = grad.float() * self.grad_scale
+        if self.decoupled:
+            self.w.mul_(1.0 - self.lr * self.weight_decay)
+        else:
+            g = g + self.weight_decay * self.w
+        self.m.mul_(self.b1).add_(g, alpha=1 - self.b1)
+        self.v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+        denom = (self.v.sqrt() / (1 - self.b2 ** t) ** 0.5).add_(self.eps)
+        self.w.addcdiv_(self.m, denom, value=-self.lr / (1 - self.b1 ** t))
+        if out_bf16 is not None:
+            out_bf16.copy_(self.w)
+
+    def state_dict(self):
+        return {"kind": "adam", "step": self.step_count, "exp_avg": self.m, "exp_avg_sq": self.v, "lr": self.lr}
+
+    def load_state_dict(self, sd):
+        self.step_count = int(sd["step"])
+        self.m.copy_(sd["exp_avg"])
+        self.v.copy_(sd["exp_avg_sq"])
+        self.lr = float(sd.get("lr", self.lr))
+
+
+def grad_stats(grad: torch.Tensor):
+    """Return a device tensor [sum(g^2), any_nonfinite] for a flat gradient (H12)."""
+    if grad.is_cuda:
+        out = torch.empty(2, dtype=torch.float32, device=grad.device)
+        rc = _lib.lib().tony_grad_stats(grad.data_ptr(), int(grad.dtype == torch.bfloat16), grad.numel(),
+                                        out.data_ptr(), _lib.stream_ptr(grad.device))
+        _lib.check(rc, "tony_grad_stats")
+        return out
+    g = grad.float()
+    return torch.stack([(g * g).sum(), (~torch.isfinite(g)).any().float()])

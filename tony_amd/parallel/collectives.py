@@ -1,0 +1,75 @@
+"""Collective helpers over torch.distributed (RCCL over xGMI on the GPU, gloo on CPU).
+
+On MI355X every rank is one process pinned to one GPU and the ``nccl`` backend
+IS RCCL, which runs its rings/trees over the fully-connected 8-GPU xGMI mesh.
+The helpers pick the flat, single-launch collective when the backend has it
+(``reduce_scatter_tensor`` / ``all_gather_into_tensor``) and emulate it with the
+generic ops on gloo, so the same parameter-server / data-parallel code is
+exercised by the multi-process CPU tests.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def world(group=None) -> int:
+    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+
+
+def rank(group=None) -> int:
+    return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
+
+
+def _is_gloo(group=None) -> bool:
+    return dist.get_backend(group) == "gloo"
+
+
+def reduce_scatter_flat(out: torch.Tensor, inp: torch.Tensor, group=None, async_op=False):
+    """out (= inp.numel()/world elements) <- sum over ranks of this rank's slice of inp."""
+    if world(group) == 1:
+        if out.data_ptr() != inp.data_ptr():
+            out.copy_(inp)
+        return None
+    if _is_gloo(group):
+        dist.all_reduce(inp, group=group)
+        r = rank(group)
+        n = out.numel()
+        out.copy_(inp[r * n:(r + 1) * n])
+        return None
+    return dist.reduce_scatter_tensor(out, inp, group=group, async_op=async_op)
+
+
+def all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group=None, async_op=False):
+    """out (world * inp.numel()) <- concat over ranks of inp."""
+    if world(group) == 1:
+        if out.data_ptr() != inp.data_ptr():
+            out.copy_(inp)
+        return None
+    if _is_gloo(group):
+        n = inp.numel()
+        parts = [out[i * n:(i + 1) * n] for i in range(world(group))]
+        src = inp.clone() if any(p.data_ptr() == inp.data_ptr() for p in parts) else inp
+        dist.all_gather(parts, src, group=group)
+        return None
+    return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
+
+
+def all_reduce(t: torch.Tensor, op=None, group=None, async_op=False):
+    if world(group) == 1:
+        return None
+    return dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=group, async_op=async_op)
+
+
+def broadcast(t: torch.Tensor, src: int, group=None, async_op=False):
+    if world(group) == 1:
+        return None
+    return dist.broadcast(t, src, group=group, async_op=async_op)
+
+
+def max_over_ranks(v: float, device=None) -> float:
+    if world() == 1:
+        return float(v)
+    t = torch.tensor([float(v)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

@@ -1,0 +1,89 @@
+"""One training step = forward + loss + backward + PS push/apply/pull, optionally
+captured once into a HIP graph and replayed.
+
+Graph capture removes the per-kernel host launch cost of the ~1,500 kernels an
+Inception-v3 step issues (convs, fused BN, pools, concats, the optimizer and
+the collectives): the whole step becomes one ``hipGraphLaunch``.  Inputs live in
+static device buffers that the caller refreshes (``x.copy_(batch)``) between
+replays; optimizer hyper-parameters are device-resident (ops/optim.py), so a
+replay always uses the current learning rate.
+"""
+from __future__ import annotations
+
+from typing import Callable
+
+import torch
+
+from .ps import ParameterServer
+
+
+class Trainer:
+    def __init__(self, model: torch.nn.Module, ps: ParameterServer, loss_fn: Callable, use_graph: bool = False,
+                 warmup_eager: int = 3):
+        self.model = model
+        self.ps = ps
+        self.loss_fn = loss_fn
+        self.use_graph = use_graph
+        self.warmup_eager = warmup_eager
+        self.graph = None
+        self.static_x = None
+        self.static_y = None
+        self.static_loss = None
+        self._eager_steps = 0
+
+    def _eager_step(self, x, y):
+        self.ps.zero_grad()
+        out = self.model(x)
+        loss = self.loss_fn(out, y)
+        loss.backward()
+        self.ps.step()
+        return loss.detach()
+
+    def step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        if not self.use_graph:
+            return self._eager_step(x, y)
+        if self.graph is None:
+            if self._eager_steps < self.warmup_eager:
+                # warm up on a side stream (allocator pools, MIOpen solution search)
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    loss = self._eager_step(x, y)
+                torch.cuda.current_stream().wait_stream(s)
+                self._eager_steps += 1
+                return loss
+            self._capture(x, y)
+        if x.data_ptr() != self.static_x.data_ptr():
+            self.static_x.copy_(x, non_blocking=True)
+        if y.data_ptr() != self.static_y.data_ptr():
+            self.static_y.copy_(y, non_blocking=True)
+        self._refresh_hp()
+        self.graph.replay()
+        self.ps.steps += 1
+        for opt in self.ps.optimizers.values():
+            opt.step_count += 1
+        return self.static_loss
+
+    def _refresh_hp(self):
+        for opt in self.ps.optimizers.values():
+            opt.step_count += 1
+            opt._push_hp()
+            opt.step_count -= 1
+
+    def _capture(self, x, y):
+        self.static_x = x
+        self.static_y = y
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        self._refresh_hp()
+        with torch.cuda.graph(g):
+            self.ps.zero_grad()
+            out = self.model(self.static_x)
+            loss = self.loss_fn(out, self.static_y)
+            loss.backward()
+            self.ps.step()
+            self.static_loss = loss.detach()
+        self.ps.steps -= 1  # the capture itself did not train
+        for opt in self.ps.optimizers.values():
+            opt.step_count -= 1
+        self.graph = g

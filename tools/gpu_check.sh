@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU-box session: kernel numerics tests, then short benches.
+# Stops at the first GPU fault / abort / timeout (exit codes other than 0/1).
+set -u
+mkdir -p gpurun_out
+step() {  # step <name> <timeout_s> <cmd...>
+  local name=$1 to=$2; shift 2
+  echo "== $name: $*" >&2
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" >&2
+  tail -5 "gpurun_out/$name.log" >&2
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)" >&2; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    tests) step gpu_tests 900 python -m pytest tests -m gpu -x -q ;;
+    smoke) step smoke 600 python __graft_entry__.py smoke ;;
+    bench_eager) step bench_eager 900 python bench.py --steps 10 --warmup 4 --no-graph ;;
+    bench) step bench 900 python bench.py --steps 20 --warmup 6 ;;
+    bench_stock) step bench_stock 900 python bench.py --steps 10 --warmup 4 --no-graph --stock ;;
+    *) echo "unknown step $s" >&2; exit 2 ;;
+  esac
+done
