@@ -19,13 +19,22 @@ def _rows_view(t: torch.Tensor):
     if t.dim() == 4:
         n, c, h, w = t.shape
         sn, sc, sh, sw = t.stride()
-        if sc != 1:
+        if sc != 1 and c > 1:
             return None
-        ld = sw
-        if (h > 1 and sh != w * ld) or (n > 1 and sn != h * w * ld) or ld < c:
+        # strides of size-1 dims are arbitrary: derive the row stride from the
+        # innermost non-trivial spatial / batch dim
+        if h * w == 1:
+            ld = sn if n > 1 else c
+        elif w == 1:
+            ld = sh
+            if n > 1 and sn != h * ld:
+                return None
+        else:
+            ld = sw
+            if (h > 1 and sh != w * ld) or (n > 1 and sn != h * w * ld):
+                return None
+        if ld < c:
             return None
-        if w == 1 and h == 1 and n > 1:
-            ld = sn
         return n * h * w, c, ld
     if t.dim() == 2:
         m, c = t.shape
