@@ -179,3 +179,58 @@ def test_grad_stats(cuda):
     assert s[1].item() == 0
     g[7] = float("inf")
     assert grad_stats(g)[1].item() == 1
+
+
+@pytest.mark.parametrize("mnk", [(156800, 64, 192), (8192, 320, 1280), (1000, 48, 256), (37, 8, 16), (20000, 448, 2048)])
+def test_gemm_tn_wgrad(cuda, mnk):
+    from tony_amd.ops.gemm import gemm_tn
+
+    m, n1, n2 = mnk
+    torch.manual_seed(6)
+    a = torch.randn(m, n1, device=cuda).to(torch.bfloat16)
+    b = torch.randn(m, n2, device=cuda).to(torch.bfloat16)
+    c = gemm_tn(a, b)
+    ref = a.float().t() @ b.float()
+    _close(c, ref, 1e-2, 1e-3 * m ** 0.5 + 1e-3, "gemm_tn")
+
+
+def test_gemm_tn_asymmetric_exact(cuda):
+    from tony_amd.ops.gemm import gemm_tn
+
+    m, n1, n2 = 96, 40, 24
+    a = (torch.arange(m * n1, device=cuda).reshape(m, n1) % 5).to(torch.bfloat16)
+    b = (torch.arange(m * n2, device=cuda).reshape(m, n2) % 7 - 3).to(torch.bfloat16)
+    assert torch.equal(gemm_tn(a, b), a.float().t() @ b.float())
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 35, 35), (2, 192, 17, 17), (3, 2048, 8, 8), (2, 8, 1, 1)])
+def test_avgpool3(cuda, shape):
+    from tony_amd.ops.pool import avg_pool3x3_s1
+
+    x = _nhwc(torch.randn(shape, device=cuda)).to(torch.bfloat16)
+    x = _nhwc(x).requires_grad_(True)
+    y = avg_pool3x3_s1(x)
+    xr = x.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.avg_pool2d(xr, 3, 1, 1, count_include_pad=True)
+    _close(y, yr, 1e-2, 1e-2, "avgpool fwd")
+    dy = _nhwc(torch.randn(shape, device=cuda)).to(torch.bfloat16)
+    y.backward(dy)
+    yr.backward(dy.float())
+    _close(x.grad, xr.grad, 1e-2, 1e-2, "avgpool bwd")
+
+
+@pytest.mark.parametrize("shape", [(4, 64, 147, 147), (2, 288, 35, 35), (3, 768, 17, 17), (2, 16, 4, 5)])
+def test_maxpool(cuda, shape):
+    from tony_amd.ops.pool import max_pool
+
+    torch.manual_seed(7)
+    x = _nhwc(torch.randn(shape, device=cuda)).to(torch.bfloat16)
+    x = _nhwc(x).requires_grad_(True)
+    y = max_pool(x, 3, 2)
+    xr = x.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.max_pool2d(xr, 3, 2)
+    assert torch.equal(y.float(), yr)
+    dy = _nhwc(torch.randn(yr.shape, device=cuda)).to(torch.bfloat16)
+    y.backward(dy)
+    yr.backward(dy.float())
+    _close(x.grad, xr.grad, 1e-2, 1e-2, "maxpool bwd")

@@ -16,6 +16,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from ..ops.pool import avg_pool3x3_s1, max_pool
 from .layers import ConvBNAct, init_weights
 
 
@@ -25,6 +26,12 @@ class _Block(nn.Module):
     def __init__(self, fused):
         super().__init__()
         self.fused = fused
+
+    def avgpool(self, x):
+        return avg_pool3x3_s1(x) if self.fused else nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=True)
+
+    def maxpool(self, x):
+        return max_pool(x, 3, 2) if self.fused else nn.functional.max_pool2d(x, 3, 2)
 
     def c(self, cin, cout, k, s=1, p=0):
         return ConvBNAct(cin, cout, k, s, p, eps=1e-3, fused=self.fused)
@@ -40,7 +47,7 @@ class InceptionA(_Block):
         self.out_channels = 64 + 64 + 96 + pool_ch
 
     def forward(self, x):
-        p = nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=True)
+        p = self.avgpool(x)
         return torch.cat([self.b1(x), self.b5(x), self.b3(x), self.bp(p)], 1)
 
 
@@ -52,7 +59,7 @@ class InceptionB(_Block):  # 35x35 -> 17x17 reduction
         self.out_channels = 384 + 96 + cin
 
     def forward(self, x):
-        return torch.cat([self.b3(x), self.bd(x), nn.functional.max_pool2d(x, 3, 2)], 1)
+        return torch.cat([self.b3(x), self.bd(x), self.maxpool(x)], 1)
 
 
 class InceptionC(_Block):  # 17x17 with factorised 7x7
@@ -68,7 +75,7 @@ class InceptionC(_Block):  # 17x17 with factorised 7x7
         self.out_channels = 768
 
     def forward(self, x):
-        p = nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=True)
+        p = self.avgpool(x)
         return torch.cat([self.b1(x), self.b7(x), self.bd(x), self.bp(p)], 1)
 
 
@@ -81,7 +88,7 @@ class InceptionD(_Block):  # 17x17 -> 8x8 reduction
         self.out_channels = 320 + 192 + cin
 
     def forward(self, x):
-        return torch.cat([self.b3(x), self.b7(x), nn.functional.max_pool2d(x, 3, 2)], 1)
+        return torch.cat([self.b3(x), self.b7(x), self.maxpool(x)], 1)
 
 
 class InceptionE(_Block):  # 8x8 with split 1x3 / 3x1 branches
@@ -100,7 +107,7 @@ class InceptionE(_Block):  # 8x8 with split 1x3 / 3x1 branches
     def forward(self, x):
         t = self.b3(x)
         d = self.bd(x)
-        p = nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=True)
+        p = self.avgpool(x)
         return torch.cat([self.b1(x), self.b3a(t), self.b3b(t), self.bda(d), self.bdb(d), self.bp(p)], 1)
 
 
@@ -133,14 +140,16 @@ class InceptionV3(nn.Module):
         self.mixed_7 = nn.Sequential(InceptionD(768, fused), InceptionE(1280, fused), InceptionE(2048, fused))
         self.dropout = nn.Dropout(dropout)
         self.fc = nn.Linear(2048, num_classes)
+        self.fused = fused
 
     def forward(self, x):
+        pool = max_pool if self.fused else (lambda t, k, s: nn.functional.max_pool2d(t, k, s))
         for m in self.stem:
             x = m(x)
-        x = nn.functional.max_pool2d(x, 3, 2)
+        x = pool(x, 3, 2)
         for m in self.stem2:
             x = m(x)
-        x = nn.functional.max_pool2d(x, 3, 2)
+        x = pool(x, 3, 2)
         x = self.mixed_6(self.mixed_6a(self.mixed_5(x)))
         aux = self.aux(x) if (self.aux is not None and self.training) else None
         x = self.mixed_7(x)

@@ -43,6 +43,13 @@ _SIGNATURES = {
                       c_int64, c_void_p],
     "tony_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64,
                        c_int, c_void_p, c_void_p],
+    "tony_gemm_tn_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64, c_int,
+                          c_void_p],
+    "tony_avgpool3_s1p1": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
+    "tony_maxpool_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
+                         c_void_p],
+    "tony_maxpool_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
+                         c_void_p],
 }
 
 
@@ -87,6 +94,16 @@ def stream_ptr(device=None) -> int:
 def check(rc: int, name: str):
     if rc != 0:
         raise KernelError(f"{name} failed with code {rc}")
+
+
+_NUM_CUS = {}
+
+
+def num_cus(device) -> int:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _NUM_CUS:
+        _NUM_CUS[idx] = torch.cuda.get_device_properties(idx).multi_processor_count
+    return _NUM_CUS[idx]
 
 
 def ptr(t) -> int:

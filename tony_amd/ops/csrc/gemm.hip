@@ -192,3 +192,171 @@ TONY_API int tony_gemm_bf16(const void* A, const void* B, void* C, int64_t M, in
   if (N <= 64) return launch<256, 64>(A, lda, B, ldb, C, ldc, M, N, K, st, stream);
   return launch<128, 128>(A, lda, B, ldb, C, ldc, M, N, K, st, stream);
 }
+
+// ---------------------------------------------------------------------------
+// Weight-gradient GEMM ("TN", split-K): C[N1,N2] += sum_m A[m,n1] * B[m,n2]
+// with A = dY[M, Cout] and B = X[M, Cin] (both row-major over m).  For a 1x1
+// conv this is dW = dY^T X: a huge reduction (M = N*H*W up to ~2.8M rows) into
+// a tiny output, so M is split across workgroups and partial tiles are added
+// into an fp32 workspace with device-scope atomics (one wave instruction adds
+// four 64-byte row segments).
+//
+// Both MFMA operands need 8 consecutive m per lane while memory holds rows of
+// m, so tiles are staged row-major ([m][col], 256 B rows) and read with
+// gfx950's transposing LDS read ds_read_b64_tr_b16: a 16-lane group reads a
+// 4-row x 16-column block and lane i receives column i.  The 16-byte chunk c of
+// LDS row r is stored at c ^ s(r), s(r) = 2*((r&3) | ((r>>3)&1)<<2), so the
+// eight rows a 32-lane half reads in one instruction land on 8 disjoint
+// chunk pairs = all 64 banks once (conflict free).
+// ---------------------------------------------------------------------------
+namespace {
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+constexpr int TBK = 32;    // m rows per K-step
+constexpr int TBM = 128;   // n1 (Cout) per tile
+constexpr int TBN = 128;   // n2 (Cin) per tile
+
+__device__ __forceinline__ int tr_swz(int row) { return (((row & 3) | (((row >> 3) & 1) << 2)) << 1); }
+// element offset of 16-byte chunk `ch` (0..15) of row `row` in a [TBK][128] bf16 tile
+__device__ __forceinline__ int tr_off(int row, int ch) { return row * 128 + ((ch ^ tr_swz(row)) << 3); }
+
+__device__ __forceinline__ void tn_load(uint4* regs, const uint16_t* __restrict__ G, int64_t ld, int64_t m0,
+                                        int64_t m1, int c0, int ncols) {
+  // tile = TBK rows x 128 cols = 512 chunks of 16 B; 256 threads x 2
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int v = threadIdx.x + i * kThreads;
+    const int row = v >> 4, ch = v & 15;
+    const int64_t gm = m0 + row;
+    const int gc = c0 + ch * 8;
+    if (gm < m1 && gc < ncols)
+      regs[i] = *reinterpret_cast<const uint4*>(G + gm * ld + gc);
+    else
+      regs[i] = make_uint4(0, 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void tn_store(uint16_t* lds, const uint4* regs) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int v = threadIdx.x + i * kThreads;
+    const int row = v >> 4, ch = v & 15;
+    *reinterpret_cast<uint4*>(lds + tr_off(row, ch)) = regs[i];
+  }
+}
+
+// MFMA operand fragment (8 consecutive m for one column) via two transposed reads.
+__device__ __forceinline__ bf16x8_t tr_frag(const uint16_t* lds, int kgrp, int col0, int lane) {
+  const int q = (lane & 15) >> 2, p = lane & 3;
+  const int col = col0 + 4 * p;          // this lane supplies row q, columns 4p..4p+3
+  const int ch = col >> 3, half = (col >> 2) & 1;
+  const int r0 = kgrp * 8 + q;
+  const uint16_t* a0 = lds + tr_off(r0, ch) + half * 4;
+  const uint16_t* a1 = lds + tr_off(r0 + 4, ch) + half * 4;
+  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0));
+  v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a1));
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  v8i16 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, r);
+}
+
+__global__ __launch_bounds__(kThreads) void gemm_tn_splitk_kernel(
+    const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
+    float* __restrict__ C, int64_t ldc, int64_t M, int N1, int N2, int tiles_n2, int ntiles,
+    int64_t rows_per_split) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 2 * TBK * 128];
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = wg % ntiles, split = wg / ntiles;
+  const int t1 = tile / tiles_n2, t2 = tile % tiles_n2;
+  const int n1_0 = t1 * TBM, n2_0 = t2 * TBN;
+  const int64_t m_begin = static_cast<int64_t>(split) * rows_per_split;
+  const int64_t m_end = min(M, m_begin + rows_per_split);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = static_cast<int>((m_end - m_begin + TBK - 1) / TBK);
+  uint4 ra[2], rb[2];
+  if (nk > 0) {
+    tn_load(ra, A, lda, m_begin, m_end, n1_0, N1);
+    tn_load(rb, B, ldb, m_begin, m_end, n2_0, N2);
+    tn_store(smem, ra);
+    tn_store(smem + TBK * 128, rb);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const uint16_t* As = smem + (kt & 1) * 2 * TBK * 128;
+    const uint16_t* Bs = As + TBK * 128;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      const int64_t mn = m_begin + static_cast<int64_t>(kt + 1) * TBK;
+      tn_load(ra, A, lda, mn, m_end, n1_0, N1);
+      tn_load(rb, B, ldb, mn, m_end, n2_0, N2);
+    }
+    const int kgrp = lane >> 4;
+    bf16x8_t af[4], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = tr_frag(As, kgrp, wm * 64 + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = tr_frag(Bs, kgrp, wn * 64 + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if (more) {
+      uint16_t* An = smem + ((kt + 1) & 1) * 2 * TBK * 128;
+      tn_store(An, ra);
+      tn_store(An + TBK * 128, rb);
+    }
+    __syncthreads();
+  }
+  // acc[i][j] element r: row n1 = .. + (lane>>4)*4 + r, col n2 = .. + (lane&15)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n2_0 + wn * 64 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = n1_0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        if (row < N1 && col < N2) atomicAdd(C + static_cast<int64_t>(row) * ldc + col, acc[i][j][r]);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// C (fp32, [N1, N2], zeroed here) = A^T B ; A [M, N1] (lda), B [M, N2] (ldb).
+TONY_API int tony_gemm_tn_bf16(const void* A, const void* B, float* C, int64_t M, int64_t N1, int64_t N2,
+                               int64_t lda, int64_t ldb, int64_t ldc, int num_cus, hipStream_t stream) {
+  if (M <= 0 || N1 <= 0 || N2 <= 0) return -1;
+  if ((N1 % 8) || (N2 % 8) || (lda % 8) || (ldb % 8)) return -1;
+  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -1;
+  (void)hipMemsetAsync(C, 0, sizeof(float) * N1 * ldc, stream);
+  const int tiles_n1 = ceil_div(N1, TBM), tiles_n2 = ceil_div(N2, TBN);
+  const int ntiles = tiles_n1 * tiles_n2;
+  // enough workgroups for ~2 per CU, each reducing >= 8 K-steps
+  const int target = 2 * (num_cus > 0 ? num_cus : 256);
+  int64_t splits = (target + ntiles - 1) / ntiles;
+  const int64_t max_splits = (M + 8 * TBK - 1) / (8 * TBK);
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  int64_t rows = (M + splits - 1) / splits;
+  rows = (rows + TBK - 1) / TBK * TBK;
+  splits = (M + rows - 1) / rows;
+  const int64_t grid = splits * ntiles;
+  if (grid > 0x7fffffff) return -2;
+  gemm_tn_splitk_kernel<<<static_cast<int>(grid), kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(A), lda, static_cast<const uint16_t*>(B), ldb, C, ldc, M, static_cast<int>(N1),
+      static_cast<int>(N2), tiles_n2, ntiles, rows);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,173 @@
+// NHWC pooling for Inception-v3, bf16, 8 channels (16 B) per lane.
+//
+// * avg 3x3, stride 1, pad 1, count_include_pad: y = (1/9) * box(x).  The
+//   stencil is symmetric, so the backward dx = (1/9) * box(dy) is the SAME kernel.
+// * max KxK, stride S, no padding: forward writes y and, per output element and
+//   channel, the argmax offset inside its window as one byte; backward is a
+//   gather over the <= ceil(K/S)^2 windows covering each input (no atomics).
+//
+// A lane owns one (n, h, w) site x 8 channels; neighbouring lanes own the next
+// channel groups of the same site, so every wavefront access is a contiguous
+// span of the NHWC image and the 3x3 neighbourhood re-reads hit L1/L2.
+#include "common.h"
+
+using namespace tony;
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__global__ __launch_bounds__(kThreads) void box3_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                        int N, int H, int W, int C, int64_t ldx, int64_t ldy) {
+  const int CG = C >> 3;
+  const int64_t total = static_cast<int64_t>(N) * H * W * CG;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total; t += stride) {
+    const int cg = static_cast<int>(t % CG);
+    const int64_t site = t / CG;
+    const int w = static_cast<int>(site % W);
+    const int h = static_cast<int>((site / W) % H);
+    const int64_t n = site / (static_cast<int64_t>(W) * H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int dh = -1; dh <= 1; ++dh) {
+      const int hh = h + dh;
+      if (hh < 0 || hh >= H) continue;
+#pragma unroll
+      for (int dw = -1; dw <= 1; ++dw) {
+        const int ww = w + dw;
+        if (ww < 0 || ww >= W) continue;
+        float f[8];
+        load8(x + ((n * H + hh) * W + ww) * ldx + cg * 8).to_float(f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += f[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] *= (1.f / 9.f);
+    store8(y + site * ldy + cg * 8, bf16x8::from_float(acc));
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void maxpool_fwd_kernel(const uint16_t* __restrict__ x,
+                                                               uint16_t* __restrict__ y, uint8_t* __restrict__ arg,
+                                                               int N, int H, int W, int C, int OH, int OW, int K,
+                                                               int S, int64_t ldx, int64_t ldy) {
+  const int CG = C >> 3;
+  const int64_t total = static_cast<int64_t>(N) * OH * OW * CG;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total; t += stride) {
+    const int cg = static_cast<int>(t % CG);
+    const int64_t site = t / CG;
+    const int ow = static_cast<int>(site % OW);
+    const int oh = static_cast<int>((site / OW) % OH);
+    const int64_t n = site / (static_cast<int64_t>(OW) * OH);
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      best[j] = -INFINITY;
+      bi[j] = 0;
+    }
+    for (int kh = 0; kh < K; ++kh) {
+      const int hh = oh * S + kh;
+      for (int kw = 0; kw < K; ++kw) {
+        const int ww = ow * S + kw;
+        float f[8];
+        load8(x + ((n * H + hh) * W + ww) * ldx + cg * 8).to_float(f);
+        const uint8_t idx = static_cast<uint8_t>(kh * K + kw);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (f[j] > best[j] || (f[j] != f[j])) {  // NaN propagates like torch
+            best[j] = f[j];
+            bi[j] = idx;
+          }
+        }
+      }
+    }
+    store8(y + site * ldy + cg * 8, bf16x8::from_float(best));
+    uint2 packed;
+    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (static_cast<uint32_t>(bi[3]) << 24);
+    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (static_cast<uint32_t>(bi[7]) << 24);
+    *reinterpret_cast<uint2*>(arg + site * C + cg * 8) = packed;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void maxpool_bwd_kernel(const uint16_t* __restrict__ dy,
+                                                               const uint8_t* __restrict__ arg,
+                                                               uint16_t* __restrict__ dx, int N, int H, int W, int C,
+                                                               int OH, int OW, int K, int S, int64_t lddy,
+                                                               int64_t lddx) {
+  const int CG = C >> 3;
+  const int64_t total = static_cast<int64_t>(N) * H * W * CG;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total; t += stride) {
+    const int cg = static_cast<int>(t % CG);
+    const int64_t site = t / CG;
+    const int w = static_cast<int>(site % W);
+    const int h = static_cast<int>((site / W) % H);
+    const int64_t n = site / (static_cast<int64_t>(W) * H);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // windows oh with oh*S <= h <= oh*S + K - 1
+    const int oh_lo = h >= K ? (h - K + S) / S : 0;
+    const int oh_hi = min(OH - 1, h / S);
+    const int ow_lo = w >= K ? (w - K + S) / S : 0;
+    const int ow_hi = min(OW - 1, w / S);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int local = (h - oh * S) * K + (w - ow * S);
+        const int64_t osite = (n * OH + oh) * OW + ow;
+        const uint2 packed = *reinterpret_cast<const uint2*>(arg + osite * C + cg * 8);
+        float g[8];
+        load8(dy + osite * lddy + cg * 8).to_float(g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t word = j < 4 ? packed.x : packed.y;
+          const int b = (word >> (8 * (j & 3))) & 0xff;
+          if (b == local) acc[j] += g[j];
+        }
+      }
+    }
+    store8(dx + site * lddx + cg * 8, bf16x8::from_float(acc));
+  }
+}
+
+int grid_for(int64_t work) {
+  int64_t g = (work + kThreads - 1) / kThreads;
+  if (g > 16384) g = 16384;
+  return static_cast<int>(g < 1 ? 1 : g);
+}
+
+}  // namespace
+
+// y (or dx) = box3x3(x) / 9 over NHWC rows with row strides ldx / ldy.
+TONY_API int tony_avgpool3_s1p1(const void* x, void* y, int N, int H, int W, int C, int64_t ldx, int64_t ldy,
+                                hipStream_t stream) {
+  if (C % 8 || ldx % 8 || ldy % 8) return -1;
+  box3_kernel<<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, ldx, ldy);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+TONY_API int tony_maxpool_fwd(const void* x, void* y, void* argmax, int N, int H, int W, int C, int K, int S,
+                              int64_t ldx, int64_t ldy, hipStream_t stream) {
+  if (C % 8 || ldx % 8 || ldy % 8 || K * K > 255 || H < K || W < K) return -1;
+  const int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
+  maxpool_fwd_kernel<<<grid_for(static_cast<int64_t>(N) * OH * OW * (C / 8)), kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), static_cast<uint8_t*>(argmax), N, H, W, C, OH, OW,
+      K, S, ldx, ldy);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+TONY_API int tony_maxpool_bwd(const void* dy, const void* argmax, void* dx, int N, int H, int W, int C, int K, int S,
+                              int64_t lddy, int64_t lddx, hipStream_t stream) {
+  if (C % 8 || lddy % 8 || lddx % 8 || H < K || W < K) return -1;
+  const int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
+  maxpool_bwd_kernel<<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(dy), static_cast<const uint8_t*>(argmax), static_cast<uint16_t*>(dx), N, H, W, C,
+      OH, OW, K, S, lddy, lddx);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}

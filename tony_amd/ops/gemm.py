@@ -3,8 +3,9 @@
 A stride-1, unpadded 1x1 convolution on a channels_last tensor is exactly a GEMM
 over rows: Y[NHW, Cout] = X[NHW, Cin] . W[Cout, Cin]^T.  Forward and the
 backward-data GEMM run on the hand-written MFMA kernel; the weight gradient
-(a reduction over all NHW rows into a tiny Cout x Cin matrix) is a plain
-library GEMM and goes to hipBLASLt through torch.mm.
+(a reduction over all NHW rows into a tiny Cout x Cin matrix) runs on the
+split-K MFMA kernel that reads its operands with ds_read_b64_tr_b16
+(``tony_gemm_tn_bf16``).
 """
 from __future__ import annotations
 
@@ -41,6 +42,25 @@ def _gemm_rows(a_ptr, lda, b, M, N, K, out_ptr, ldc, device):
     _lib.check(rc, "tony_gemm_bf16")
 
 
+def wgrad_tn(a_ptr, lda, b_ptr, ldb, M, n1, n2, device) -> torch.Tensor:
+    """fp32 [n1, n2] = A^T B for row-major A [M, n1], B [M, n2] (split-K MFMA kernel)."""
+    out = torch.empty((n1, n2), dtype=torch.float32, device=device)
+    rc = _lib.lib().tony_gemm_tn_bf16(a_ptr, b_ptr, out.data_ptr(), M, n1, n2, lda, ldb, n2, _lib.num_cus(device),
+                                      _lib.stream_ptr(device))
+    _lib.check(rc, "tony_gemm_tn_bf16")
+    return out
+
+
+def gemm_tn(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """fp32 a^T @ b for bf16 CUDA a [M, n1], b [M, n2] with unit inner stride."""
+    if a.stride(1) != 1:
+        a = a.contiguous()
+    if b.stride(1) != 1:
+        b = b.contiguous()
+    return wgrad_tn(a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), a.shape[0], a.shape[1], b.shape[1],
+                    a.device)
+
+
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight):
@@ -70,10 +90,8 @@ class _Conv1x1Fn(torch.autograd.Function):
             _gemm_rows(dy.data_ptr(), lddy, wt, M, cin, cout, dx.data_ptr(), cin, x.device)
         dw = None
         if ctx.needs_input_grad[1]:
-            dy2 = dy.permute(0, 2, 3, 1).reshape(M, cout) if lddy == cout else \
-                torch.as_strided(dy, (M, cout), (lddy, 1))
-            x2 = x.permute(0, 2, 3, 1).reshape(M, cin) if ldx == cin else torch.as_strided(x, (M, cin), (ldx, 1))
-            dw = torch.mm(dy2.t(), x2).reshape(weight.shape).to(weight.dtype)
+            dw = wgrad_tn(dy.data_ptr(), lddy, x.data_ptr(), ldx, M, cout, cin, x.device)
+            dw = dw.to(weight.dtype).reshape(weight.shape)
         return dx, dw
 
 

@@ -1,0 +1,74 @@
+"""NHWC pooling kernels (csrc/pool.hip): avg 3x3/s1/p1 and max KxK/sS."""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .bn import _as_rows
+
+
+def _nhwc_empty(n, c, h, w, like):
+    return torch.empty((n, c, h, w), dtype=like.dtype, device=like.device, memory_format=torch.channels_last)
+
+
+def _box3(src, n, c, h, w, ld_src):
+    out = _nhwc_empty(n, c, h, w, src)
+    rc = _lib.lib().tony_avgpool3_s1p1(src.data_ptr(), out.data_ptr(), n, h, w, c, ld_src, c,
+                                       _lib.stream_ptr(src.device))
+    _lib.check(rc, "tony_avgpool3_s1p1")
+    return out
+
+
+class _AvgPool3Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x, (_, c, ld) = _as_rows(x)
+        n, _, h, w = x.shape
+        return _box3(x, n, c, h, w, ld)
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy, (_, c, ld) = _as_rows(dy)
+        n, _, h, w = dy.shape
+        return _box3(dy, n, c, h, w, ld)  # symmetric stencil: dx = box(dy)/9
+
+
+class _MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s):
+        x, (_, c, ld) = _as_rows(x)
+        n, _, h, w = x.shape
+        oh, ow = (h - k) // s + 1, (w - k) // s + 1
+        y = _nhwc_empty(n, c, oh, ow, x)
+        arg = torch.empty((n, oh, ow, c), dtype=torch.uint8, device=x.device)
+        rc = _lib.lib().tony_maxpool_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), n, h, w, c, k, s, ld, c,
+                                         _lib.stream_ptr(x.device))
+        _lib.check(rc, "tony_maxpool_fwd")
+        ctx.save_for_backward(arg)
+        ctx.shape = (n, c, h, w, k, s)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        n, c, h, w, k, s = ctx.shape
+        dy, (_, _, lddy) = _as_rows(dy)
+        dx = _nhwc_empty(n, c, h, w, dy)
+        rc = _lib.lib().tony_maxpool_bwd(dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), n, h, w, c, k, s, lddy, c,
+                                         _lib.stream_ptr(dy.device))
+        _lib.check(rc, "tony_maxpool_bwd")
+        return dx, None, None
+
+
+def avg_pool3x3_s1(x: torch.Tensor) -> torch.Tensor:
+    """avg_pool2d(x, 3, 1, 1, count_include_pad=True) on channels_last bf16."""
+    if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0:
+        return _AvgPool3Fn.apply(x)
+    return torch.nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=True)
+
+
+def max_pool(x: torch.Tensor, k: int = 3, s: int = 2) -> torch.Tensor:
+    """max_pool2d(x, k, s) (no padding) on channels_last bf16."""
+    if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0:
+        return _MaxPoolFn.apply(x, k, s)
+    return torch.nn.functional.max_pool2d(x, k, s)
