@@ -39,7 +39,8 @@ def parse():
     ap.add_argument("--model", default="inception_v3", choices=["inception_v3", "resnet50"])
     ap.add_argument("--optimizer", default="sgd")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps (for rocprof)")
-    ap.add_argument("--miopen-find", action="store_true", help="MIOpen exhaustive find for the non-1x1 convs")
+    ap.add_argument("--no-miopen-find", action="store_true",
+                    help="MIOpen immediate mode instead of find (faster startup, slower non-1x1 convs)")
     return ap.parse_args()
 
 
@@ -61,7 +62,7 @@ def main():
     from tony_amd.parallel.ps import ParameterServer
     from tony_amd.parallel.trainer import Trainer
 
-    torch.backends.cudnn.benchmark = args.miopen_find
+    torch.backends.cudnn.benchmark = not args.no_miopen_find  # MIOpen find for the remaining MIOpen convs
     fused = not args.stock
     if args.model == "inception_v3":
         from tony_amd.models.inception_v3 import inception_v3

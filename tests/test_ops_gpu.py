@@ -9,13 +9,15 @@ def _nhwc(t):
     return t.contiguous(memory_format=torch.channels_last)
 
 
-def _close(a, b, rtol, atol, what):
+def _close(a, b, rtol, atol, what, max_bad_frac=0.0):
+    """Elementwise |a-b| <= atol + rtol|b|; ``max_bad_frac`` admits ReLU-mask flips
+    (bf16 vs fp32 pre-activations that straddle 0 take different branches)."""
     a = a.float()
-    b = b.float()
+    b = b.float().to(a.device)
     err = (a - b).abs()
     tol = atol + rtol * b.abs()
     bad = (err > tol).sum().item()
-    assert bad == 0, f"{what}: {bad}/{a.numel()} outside tol, max err {err.max().item():.4g}"
+    assert bad <= max_bad_frac * a.numel(), f"{what}: {bad}/{a.numel()} outside tol, max err {err.max().item():.4g}"
 
 
 @pytest.mark.parametrize("shape", [(8, 32, 37, 37), (4, 80, 17, 17), (2, 2048, 8, 8), (3, 192, 5, 7), (16, 48, 1, 1)])
@@ -49,7 +51,7 @@ def test_bn_act_train_fwd_bwd(cuda, shape, relu):
     dy = _nhwc(torch.randn(shape, device=cuda)).to(torch.bfloat16)
     yr.backward(dy.float())
     yk.backward(dy)
-    _close(xk.grad, xr.grad, 3e-2, 3e-2, "bn dx")
+    _close(xk.grad, xr.grad, 3e-2, 3e-2, "bn dx", max_bad_frac=1e-3)
     _close(gk.grad, gr.grad, 3e-2, 0.05 * gr.grad.abs().max().item() + 1e-2, "bn dgamma")
     _close(bk.grad, br.grad, 3e-2, 0.05 * br.grad.abs().max().item() + 1e-2, "bn dbeta")
 
@@ -210,12 +212,14 @@ def test_avgpool3(cuda, shape):
     x = _nhwc(torch.randn(shape, device=cuda)).to(torch.bfloat16)
     x = _nhwc(x).requires_grad_(True)
     y = avg_pool3x3_s1(x)
-    xr = x.detach().float().requires_grad_(True)
+    # fp32 reference on the CPU: the GPU channels_last avg_pool2d backward of this
+    # PyTorch-ROCm build returns wrong gradients (see tools/debug_pool2.py)
+    xr = x.detach().float().cpu().requires_grad_(True)
     yr = torch.nn.functional.avg_pool2d(xr, 3, 1, 1, count_include_pad=True)
     _close(y, yr, 1e-2, 1e-2, "avgpool fwd")
     dy = _nhwc(torch.randn(shape, device=cuda)).to(torch.bfloat16)
     y.backward(dy)
-    yr.backward(dy.float())
+    yr.backward(dy.float().cpu())
     _close(x.grad, xr.grad, 1e-2, 1e-2, "avgpool bwd")
 
 
@@ -234,3 +238,50 @@ def test_maxpool(cuda, shape):
     y.backward(dy)
     yr.backward(dy.float())
     _close(x.grad, xr.grad, 1e-2, 1e-2, "maxpool bwd")
+
+
+def test_avgpool3_direct_on_grad_layout(cuda):
+    """The backward reuses the forward stencil on dy; check the raw kernel on a fresh tensor."""
+    from tony_amd.ops.pool import _box3
+
+    dy = _nhwc(torch.randn(4, 64, 35, 35, device=cuda)).to(torch.bfloat16)
+    dy = _nhwc(dy)
+    out = _box3(dy, 4, 64, 35, 35, 64)
+    ref = torch.nn.functional.avg_pool2d(dy.float(), 3, 1, 1, count_include_pad=True)
+    _close(out, ref, 1e-2, 1e-2, "box3 raw")
+
+
+@pytest.mark.parametrize("cfg", [(4, 192, 35, 35, (64, 48, 64), 32), (2, 768, 17, 17, (192, 160, 160), 192),
+                                 (4, 2048, 8, 8, (320, 384, 448), 192), (2, 768, 17, 17, (192, 192), 0),
+                                 (3, 64, 9, 9, (80,), 0)])
+def test_fused_head_matches_reference(cuda, cfg):
+    from tony_amd.ops.fused import FusedHead, head_reference
+
+    n, cin, h, w, splits, npool = cfg
+    torch.manual_seed(8)
+    head = FusedHead(cin, splits, pool_cout=npool).to(cuda)
+    with torch.no_grad():
+        head.conv.weight.copy_(torch.randn_like(head.conv.weight) * cin ** -0.5)
+        head.bn.weight.copy_(torch.rand_like(head.bn.weight) + 0.5)
+        head.bn.bias.copy_(torch.randn_like(head.bn.bias) * 0.1)
+    ref_w = head.conv.weight.detach().clone().requires_grad_(True)
+    ref_g = head.bn.weight.detach().clone().requires_grad_(True)
+    ref_b = head.bn.bias.detach().clone().requires_grad_(True)
+    rm_r, rv_r = head.bn.running_mean.clone(), head.bn.running_var.clone()
+    head = head.to(torch.bfloat16)
+    head.bn.running_mean.data = head.bn.running_mean.float()
+    head.bn.running_var.data = head.bn.running_var.float()
+    x = _nhwc(torch.randn(n, cin, h, w, device=cuda)).to(torch.bfloat16)
+    x = _nhwc(x).requires_grad_(True)
+    outs = head(x)
+    xr = x.detach().float().requires_grad_(True)
+    refs = head_reference(xr, ref_w.to(torch.bfloat16).float(), ref_g.to(torch.bfloat16).float(),
+                          ref_b.to(torch.bfloat16).float(), rm_r, rv_r, splits, npool, True, 0.1, 1e-3)
+    assert len(outs) == len(refs)
+    for o, r in zip(outs, refs):
+        _close(o, r, 3e-2, 5e-2, "head fwd")
+    _close(head.bn.running_mean, rm_r, 2e-2, 2e-3, "head running_mean")
+    dys = [_nhwc(torch.randn(r.shape, device=cuda)).to(torch.bfloat16) for r in refs]
+    torch.autograd.backward(outs, dys)
+    torch.autograd.backward(refs, [d.float() for d in dys])
+    _close(x.grad, xr.grad, 5e-2, 5e-2 * xr.grad.abs().max().item(), "head dx", max_bad_frac=2e-3)

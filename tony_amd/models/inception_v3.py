@@ -8,8 +8,12 @@ tf_cnn_benchmarks job that TonY's paper runs as a parameter-server job
 reduction-D, 2x Inception-E with split 1x3/3x1 branches (8x8), global average
 pool, dropout and a 1000-way classifier.  BN epsilon is 1e-3 as in TF.
 
-Every conv is a ``ConvBNAct`` (conv + fused HIP BN+ReLU kernel); 1x1 convs run
-on the tony_amd MFMA GEMM.  Parameter count (with aux head): 27,161,264.
+Every conv is a ``ConvBNAct`` (conv + fused HIP BN+ReLU kernel).  With
+``fused=True`` the 1x1 convs that read a block's input -- including the avg-pool
+branch's 1x1, commuted in front of the pool -- are one ``FusedHead`` MFMA GEMM
+with BN statistics in its epilogue (ops/fused.py).  ``fused=False`` builds the
+textbook graph on stock PyTorch ops (the comparator).  Parameter count (with
+aux head) is 27,161,264 either way.
 """
 from __future__ import annotations
 
@@ -17,6 +21,7 @@ import torch
 from torch import nn
 
 from ..ops.pool import avg_pool3x3_s1, max_pool
+from ..ops.fused import FusedHead
 from .layers import ConvBNAct, init_weights
 
 
@@ -40,13 +45,22 @@ class _Block(nn.Module):
 class InceptionA(_Block):
     def __init__(self, cin, pool_ch, fused=True):
         super().__init__(fused)
-        self.b1 = self.c(cin, 64, 1)
-        self.b5 = nn.Sequential(self.c(cin, 48, 1), self.c(48, 64, 5, p=2))
-        self.b3 = nn.Sequential(self.c(cin, 64, 1), self.c(64, 96, 3, p=1), self.c(96, 96, 3, p=1))
-        self.bp = self.c(cin, pool_ch, 1)
+        if fused:
+            # b1 1x1/64, b5 1x1/48, b3 1x1/64 and the pool branch's 1x1 share one GEMM
+            self.head = FusedHead(cin, (64, 48, 64), pool_cout=pool_ch)
+            self.b5 = self.c(48, 64, 5, p=2)
+            self.b3 = nn.Sequential(self.c(64, 96, 3, p=1), self.c(96, 96, 3, p=1))
+        else:
+            self.b1 = self.c(cin, 64, 1)
+            self.b5 = nn.Sequential(self.c(cin, 48, 1), self.c(48, 64, 5, p=2))
+            self.b3 = nn.Sequential(self.c(cin, 64, 1), self.c(64, 96, 3, p=1), self.c(96, 96, 3, p=1))
+            self.bp = self.c(cin, pool_ch, 1)
         self.out_channels = 64 + 64 + 96 + pool_ch
 
     def forward(self, x):
+        if self.fused:
+            y1, y5, y3, yp = self.head(x)
+            return torch.cat([y1, self.b5(y5), self.b3(y3), yp], 1)
         p = self.avgpool(x)
         return torch.cat([self.b1(x), self.b5(x), self.b3(x), self.bp(p)], 1)
 
@@ -65,16 +79,25 @@ class InceptionB(_Block):  # 35x35 -> 17x17 reduction
 class InceptionC(_Block):  # 17x17 with factorised 7x7
     def __init__(self, cin, c7, fused=True):
         super().__init__(fused)
-        self.b1 = self.c(cin, 192, 1)
-        self.b7 = nn.Sequential(self.c(cin, c7, 1), self.c(c7, c7, (1, 7), p=(0, 3)),
-                                self.c(c7, 192, (7, 1), p=(3, 0)))
-        self.bd = nn.Sequential(self.c(cin, c7, 1), self.c(c7, c7, (7, 1), p=(3, 0)),
-                                self.c(c7, c7, (1, 7), p=(0, 3)), self.c(c7, c7, (7, 1), p=(3, 0)),
-                                self.c(c7, 192, (1, 7), p=(0, 3)))
-        self.bp = self.c(cin, 192, 1)
+        if fused:
+            self.head = FusedHead(cin, (192, c7, c7), pool_cout=192)
+            self.b7 = nn.Sequential(self.c(c7, c7, (1, 7), p=(0, 3)), self.c(c7, 192, (7, 1), p=(3, 0)))
+            self.bd = nn.Sequential(self.c(c7, c7, (7, 1), p=(3, 0)), self.c(c7, c7, (1, 7), p=(0, 3)),
+                                    self.c(c7, c7, (7, 1), p=(3, 0)), self.c(c7, 192, (1, 7), p=(0, 3)))
+        else:
+            self.b1 = self.c(cin, 192, 1)
+            self.b7 = nn.Sequential(self.c(cin, c7, 1), self.c(c7, c7, (1, 7), p=(0, 3)),
+                                    self.c(c7, 192, (7, 1), p=(3, 0)))
+            self.bd = nn.Sequential(self.c(cin, c7, 1), self.c(c7, c7, (7, 1), p=(3, 0)),
+                                    self.c(c7, c7, (1, 7), p=(0, 3)), self.c(c7, c7, (7, 1), p=(3, 0)),
+                                    self.c(c7, 192, (1, 7), p=(0, 3)))
+            self.bp = self.c(cin, 192, 1)
         self.out_channels = 768
 
     def forward(self, x):
+        if self.fused:
+            y1, y7, yd, yp = self.head(x)
+            return torch.cat([y1, self.b7(y7), self.bd(yd), yp], 1)
         p = self.avgpool(x)
         return torch.cat([self.b1(x), self.b7(x), self.bd(x), self.bp(p)], 1)
 
@@ -82,33 +105,52 @@ class InceptionC(_Block):  # 17x17 with factorised 7x7
 class InceptionD(_Block):  # 17x17 -> 8x8 reduction
     def __init__(self, cin, fused=True):
         super().__init__(fused)
-        self.b3 = nn.Sequential(self.c(cin, 192, 1), self.c(192, 320, 3, s=2))
-        self.b7 = nn.Sequential(self.c(cin, 192, 1), self.c(192, 192, (1, 7), p=(0, 3)),
-                                self.c(192, 192, (7, 1), p=(3, 0)), self.c(192, 192, 3, s=2))
+        if fused:
+            self.head = FusedHead(cin, (192, 192))
+            self.b3 = self.c(192, 320, 3, s=2)
+            self.b7 = nn.Sequential(self.c(192, 192, (1, 7), p=(0, 3)), self.c(192, 192, (7, 1), p=(3, 0)),
+                                    self.c(192, 192, 3, s=2))
+        else:
+            self.b3 = nn.Sequential(self.c(cin, 192, 1), self.c(192, 320, 3, s=2))
+            self.b7 = nn.Sequential(self.c(cin, 192, 1), self.c(192, 192, (1, 7), p=(0, 3)),
+                                    self.c(192, 192, (7, 1), p=(3, 0)), self.c(192, 192, 3, s=2))
         self.out_channels = 320 + 192 + cin
 
     def forward(self, x):
+        if self.fused:
+            t3, t7 = self.head(x)
+            return torch.cat([self.b3(t3), self.b7(t7), self.maxpool(x)], 1)
         return torch.cat([self.b3(x), self.b7(x), self.maxpool(x)], 1)
 
 
 class InceptionE(_Block):  # 8x8 with split 1x3 / 3x1 branches
     def __init__(self, cin, fused=True):
         super().__init__(fused)
-        self.b1 = self.c(cin, 320, 1)
-        self.b3 = self.c(cin, 384, 1)
+        if fused:
+            self.head = FusedHead(cin, (320, 384, 448), pool_cout=192)
+        else:
+            self.b1 = self.c(cin, 320, 1)
+            self.b3 = self.c(cin, 384, 1)
+            self.bd = nn.Sequential(self.c(cin, 448, 1), self.c(448, 384, 3, p=1))
+            self.bp = self.c(cin, 192, 1)
         self.b3a = self.c(384, 384, (1, 3), p=(0, 1))
         self.b3b = self.c(384, 384, (3, 1), p=(1, 0))
-        self.bd = nn.Sequential(self.c(cin, 448, 1), self.c(448, 384, 3, p=1))
+        if fused:
+            self.bd = self.c(448, 384, 3, p=1)
         self.bda = self.c(384, 384, (1, 3), p=(0, 1))
         self.bdb = self.c(384, 384, (3, 1), p=(1, 0))
-        self.bp = self.c(cin, 192, 1)
         self.out_channels = 2048
 
     def forward(self, x):
-        t = self.b3(x)
-        d = self.bd(x)
-        p = self.avgpool(x)
-        return torch.cat([self.b1(x), self.b3a(t), self.b3b(t), self.bda(d), self.bdb(d), self.bp(p)], 1)
+        if self.fused:
+            y1, t, d, yp = self.head(x)
+            d = self.bd(d)
+        else:
+            y1 = self.b1(x)
+            t = self.b3(x)
+            d = self.bd(x)
+            yp = self.bp(self.avgpool(x))
+        return torch.cat([y1, self.b3a(t), self.b3b(t), self.bda(d), self.bdb(d), yp], 1)
 
 
 class InceptionAux(_Block):

@@ -12,7 +12,7 @@ import torch
 from torch import nn
 
 from ..ops.bn import BatchNormAct2d
-from ..ops.gemm import conv1x1
+from ..ops.fused import _HeadFn
 
 
 def _pair(v):
@@ -36,10 +36,12 @@ class ConvBNAct(nn.Module):
             self.act = nn.ReLU(inplace=True) if relu else nn.Identity()
 
     def forward(self, x):
-        if self.fused and self.is_1x1 and x.is_cuda:
-            y = conv1x1(x, self.conv.weight)
-        else:
-            y = self.conv(x)
+        if self.fused and self.is_1x1 and self.bn.relu and x.is_cuda:
+            # MFMA GEMM with BN statistics in its epilogue + fused apply (ops/fused.py)
+            bn = self.bn
+            return _HeadFn.apply(x, self.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                 (self.conv.out_channels,), 0, self.training, bn.momentum, bn.eps)[0]
+        y = self.conv(x)
         if self.fused:
             return self.bn(y)
         return self.act(self.bn(y))

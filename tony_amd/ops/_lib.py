@@ -35,6 +35,14 @@ _SIGNATURES = {
                           c_float, c_int, c_void_p, c_void_p, c_void_p],
     "tony_bn_bwd": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p,
                     c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "tony_bn_stats": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p],
+    "tony_bn_apply": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+                      c_int, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p],
+    "tony_bn_bwd_reduce": [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p,
+                           c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "tony_bn_bwd_apply": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p,
+                          c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                          c_void_p],
     "tony_sgd_step": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p],
     "tony_adam_step": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p],
     "tony_grad_stats": [c_void_p, c_int, c_int64, c_void_p, c_void_p],

@@ -53,7 +53,7 @@ __device__ __forceinline__ void store_param(void* p, int idx, int is_bf16, float
 // Reduce per-thread partials over the RPI row-lanes in LDS and add one value
 // per channel into global `out` (2*C floats: [sum | sum2]).
 __device__ __forceinline__ void block_reduce_add(float* red, const RowMap& rm, int C,
-                                                 const float* a, const float* b, float* out) {
+                                                 const float* a, const float* b, float* out_a, float* out_b) {
   if (rm.active) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -68,14 +68,14 @@ __device__ __forceinline__ void block_reduce_add(float* red, const RowMap& rm, i
       sa += red[k * C + c];
       sb += red[kMaxC + k * C + c];
     }
-    atomicAdd(out + c, sa);
-    atomicAdd(out + C + c, sb);
+    atomicAdd(out_a + c, sa);
+    atomicAdd(out_b + c, sb);
   }
 }
 
 __global__ __launch_bounds__(kThreads) void bn_fwd_stats_kernel(
     const uint16_t* __restrict__ x, int64_t M, int C, int64_t ldx, int64_t rows_per_block,
-    float* __restrict__ sums) {
+    float* __restrict__ sum, float* __restrict__ sumsq) {
   __shared__ float red[kMaxC * 2];
   RowMap rm(C);
   float s[8], q[8];
@@ -112,14 +112,14 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_stats_kernel(
       }
     }
   }
-  block_reduce_add(red, rm, C, s, q, sums);
+  block_reduce_add(red, rm, C, s, q, sum, sumsq);
 }
 
 // mode 0: training (stats from sums, saves mean/invstd, updates running stats)
 // mode 1: inference (stats from running_mean / running_var)
 __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
     const uint16_t* __restrict__ x, int64_t M, int C, int64_t ldx, int64_t rows_per_block,
-    uint16_t* __restrict__ y, int64_t ldy, const float* __restrict__ sums,
+    uint16_t* __restrict__ y, int64_t ldy, const float* __restrict__ sum, const float* __restrict__ sumsq,
     const void* gamma, const void* beta, int param_bf16, float eps, int relu, int mode,
     float* __restrict__ save_mean, float* __restrict__ save_invstd,
     float* __restrict__ running_mean, float* __restrict__ running_var, float momentum) {
@@ -129,8 +129,8 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
   for (int c = threadIdx.x; c < C; c += kThreads) {
     float mean, invstd;
     if (mode == 0) {
-      mean = sums[c] * inv_m;
-      float var = fmaxf(sums[C + c] * inv_m - mean * mean, 0.f);
+      mean = sum[c] * inv_m;
+      float var = fmaxf(sumsq[c] * inv_m - mean * mean, 0.f);
       invstd = rsqrtf(var + eps);
       if (blockIdx.x == 0) {
         save_mean[c] = mean;
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __restrict__ dy, int64_t lddy,
     int64_t M, int C, int64_t rows_per_block, const float* __restrict__ mean,
     const float* __restrict__ invstd, const void* gamma, const void* beta, int param_bf16,
-    int relu, float* __restrict__ dsums) {
+    int relu, float* __restrict__ dsum, float* __restrict__ dsumx) {
   __shared__ float red[kMaxC * 2];
   RowMap rm(C);
   float a[8], b[8];
@@ -233,25 +233,25 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     }
     for (; r < r1; r += step) body(load8(x + r * ldx + rm.cg * 8), load8(dy + r * lddy + rm.cg * 8));
   }
-  block_reduce_add(red, rm, C, a, b, dsums);
+  block_reduce_add(red, rm, C, a, b, dsum, dsumx);
 }
 
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __restrict__ dy, int64_t lddy,
     uint16_t* __restrict__ dx, int64_t lddx, int64_t M, int C, int64_t rows_per_block,
     const float* __restrict__ mean, const float* __restrict__ invstd, const void* gamma,
-    const void* beta, int param_bf16, int relu, const float* __restrict__ dsums, void* dgamma,
-    void* dbeta) {
+    const void* beta, int param_bf16, int relu, const float* __restrict__ dsum,
+    const float* __restrict__ dsumx, void* dgamma, void* dbeta) {
   __shared__ float k_s[kMaxC], a_s[kMaxC], b_s[kMaxC];
   const float inv_m = 1.f / static_cast<float>(M);
   for (int c = threadIdx.x; c < C; c += kThreads) {
     const float g = load_param(gamma, c, param_bf16, 1.f);
     k_s[c] = g * invstd[c];
-    a_s[c] = dsums[c] * inv_m;
-    b_s[c] = dsums[C + c] * inv_m;
+    a_s[c] = dsum[c] * inv_m;
+    b_s[c] = dsumx[c] * inv_m;
     if (blockIdx.x == 0) {
-      store_param(dbeta, c, param_bf16, dsums[c]);
-      store_param(dgamma, c, param_bf16, dsums[C + c]);
+      store_param(dbeta, c, param_bf16, dsum[c]);
+      store_param(dgamma, c, param_bf16, dsumx[c]);
     }
   }
   __syncthreads();
@@ -315,59 +315,106 @@ bool bad_c(int C) { return C <= 0 || C % 8 != 0 || C > kMaxC; }
 
 }  // namespace
 
+// ---- composable entry points (the fused conv heads call these on channel sub-ranges) ----
+
+// sum/sumsq[C] are zeroed here and accumulated over the M rows of x.
+TONY_API int tony_bn_stats(const void* x, int64_t M, int C, int64_t ldx, float* sum, float* sumsq,
+                           hipStream_t stream) {
+  if (bad_c(C) || (ldx % 8)) return -1;
+  if (sumsq == sum + C) {
+    (void)hipMemsetAsync(sum, 0, sizeof(float) * 2 * C, stream);
+  } else {
+    (void)hipMemsetAsync(sum, 0, sizeof(float) * C, stream);
+    (void)hipMemsetAsync(sumsq, 0, sizeof(float) * C, stream);
+  }
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 16, 2048, &rpb, &grid);
+  bn_fwd_stats_kernel<<<grid, kThreads, 0, stream>>>(static_cast<const uint16_t*>(x), M, C, ldx, rpb, sum, sumsq);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// mode 0 (train): normalise with the batch stats in sum/sumsq, save mean/invstd,
+// update running stats; mode 1 (eval): use running_mean/var.
+TONY_API int tony_bn_apply(const void* x, int64_t M, int C, int64_t ldx, void* y, int64_t ldy, const float* sum,
+                           const float* sumsq, const void* gamma, const void* beta, int param_bf16, float eps,
+                           int relu, int mode, float* save_mean, float* save_invstd, float* running_mean,
+                           float* running_var, float momentum, hipStream_t stream) {
+  if (bad_c(C) || (ldx % 8) || (ldy % 8)) return -1;
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 4, 4096, &rpb, &grid);
+  bn_fwd_apply_kernel<<<grid, kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), M, C, ldx, rpb, static_cast<uint16_t*>(y), ldy, sum, sumsq, gamma, beta,
+      param_bf16, eps, relu, mode, save_mean, save_invstd, running_mean, running_var, momentum);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+TONY_API int tony_bn_bwd_reduce(const void* x, int64_t ldx, const void* dy, int64_t lddy, int64_t M, int C,
+                                const float* mean, const float* invstd, const void* gamma, const void* beta,
+                                int param_bf16, int relu, float* dsum, float* dsumx, hipStream_t stream) {
+  if (bad_c(C) || (ldx % 8) || (lddy % 8)) return -1;
+  if (dsumx == dsum + C) {
+    (void)hipMemsetAsync(dsum, 0, sizeof(float) * 2 * C, stream);
+  } else {
+    (void)hipMemsetAsync(dsum, 0, sizeof(float) * C, stream);
+    (void)hipMemsetAsync(dsumx, 0, sizeof(float) * C, stream);
+  }
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 16, 2048, &rpb, &grid);
+  bn_bwd_reduce_kernel<<<grid, kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, M, C, rpb, mean, invstd, gamma,
+      beta, param_bf16, relu, dsum, dsumx);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+TONY_API int tony_bn_bwd_apply(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx, int64_t lddx,
+                               int64_t M, int C, const float* mean, const float* invstd, const void* gamma,
+                               const void* beta, int param_bf16, int relu, const float* dsum, const float* dsumx,
+                               void* dgamma, void* dbeta, hipStream_t stream) {
+  if (bad_c(C) || (ldx % 8) || (lddy % 8) || (lddx % 8)) return -1;
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 4, 4096, &rpb, &grid);
+  bn_bwd_apply_kernel<<<grid, kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, static_cast<uint16_t*>(dx), lddx,
+      M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsum, dsumx, dgamma, dbeta);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---- one-call forms used by BatchNormAct2d ----
+
 TONY_API int tony_bn_fwd_train(const void* x, int64_t M, int C, int64_t ldx, void* y, int64_t ldy,
                                const void* gamma, const void* beta, int param_bf16, float eps,
                                int relu, float* sums_ws, float* save_mean, float* save_invstd,
                                float* running_mean, float* running_var, float momentum,
                                hipStream_t stream) {
-  if (bad_c(C) || (ldx % 8) || (ldy % 8)) return -1;
-  (void)hipMemsetAsync(sums_ws, 0, sizeof(float) * 2 * C, stream);
-  int64_t rpb;
-  int grid;
-  plan_rows(M, C, 16, 2048, &rpb, &grid);
-  bn_fwd_stats_kernel<<<grid, kThreads, 0, stream>>>(static_cast<const uint16_t*>(x), M, C, ldx, rpb,
-                                                    sums_ws);
-  plan_rows(M, C, 4, 4096, &rpb, &grid);
-  bn_fwd_apply_kernel<<<grid, kThreads, 0, stream>>>(
-      static_cast<const uint16_t*>(x), M, C, ldx, rpb, static_cast<uint16_t*>(y), ldy, sums_ws, gamma,
-      beta, param_bf16, eps, relu, 0, save_mean, save_invstd, running_mean, running_var, momentum);
-  TONY_LAUNCH_CHECK();
-  return 0;
+  int rc = tony_bn_stats(x, M, C, ldx, sums_ws, sums_ws + C, stream);
+  if (rc) return rc;
+  return tony_bn_apply(x, M, C, ldx, y, ldy, sums_ws, sums_ws + C, gamma, beta, param_bf16, eps, relu, 0, save_mean,
+                       save_invstd, running_mean, running_var, momentum, stream);
 }
 
 TONY_API int tony_bn_fwd_infer(const void* x, int64_t M, int C, int64_t ldx, void* y, int64_t ldy,
                                const void* gamma, const void* beta, int param_bf16, float eps,
                                int relu, const float* running_mean, const float* running_var,
                                hipStream_t stream) {
-  if (bad_c(C) || (ldx % 8) || (ldy % 8)) return -1;
-  int64_t rpb;
-  int grid;
-  plan_rows(M, C, 4, 4096, &rpb, &grid);
-  bn_fwd_apply_kernel<<<grid, kThreads, 0, stream>>>(
-      static_cast<const uint16_t*>(x), M, C, ldx, rpb, static_cast<uint16_t*>(y), ldy, nullptr, gamma,
-      beta, param_bf16, eps, relu, 1, nullptr, nullptr, const_cast<float*>(running_mean),
-      const_cast<float*>(running_var), 0.f);
-  TONY_LAUNCH_CHECK();
-  return 0;
+  return tony_bn_apply(x, M, C, ldx, y, ldy, nullptr, nullptr, gamma, beta, param_bf16, eps, relu, 1, nullptr,
+                       nullptr, const_cast<float*>(running_mean), const_cast<float*>(running_var), 0.f, stream);
 }
 
 TONY_API int tony_bn_bwd(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx,
                          int64_t lddx, int64_t M, int C, const float* mean, const float* invstd,
                          const void* gamma, const void* beta, int param_bf16, int relu,
                          float* dsums_ws, void* dgamma, void* dbeta, hipStream_t stream) {
-  if (bad_c(C) || (ldx % 8) || (lddy % 8) || (lddx % 8)) return -1;
-  (void)hipMemsetAsync(dsums_ws, 0, sizeof(float) * 2 * C, stream);
-  int64_t rpb;
-  int grid;
-  plan_rows(M, C, 16, 2048, &rpb, &grid);
-  bn_bwd_reduce_kernel<<<grid, kThreads, 0, stream>>>(
-      static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, M, C, rpb, mean,
-      invstd, gamma, beta, param_bf16, relu, dsums_ws);
-  plan_rows(M, C, 4, 4096, &rpb, &grid);
-  bn_bwd_apply_kernel<<<grid, kThreads, 0, stream>>>(
-      static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy,
-      static_cast<uint16_t*>(dx), lddx, M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu,
-      dsums_ws, dgamma, dbeta);
-  TONY_LAUNCH_CHECK();
-  return 0;
+  int rc = tony_bn_bwd_reduce(x, ldx, dy, lddy, M, C, mean, invstd, gamma, beta, param_bf16, relu, dsums_ws,
+                              dsums_ws + C, stream);
+  if (rc) return rc;
+  return tony_bn_bwd_apply(x, ldx, dy, lddy, dx, lddx, M, C, mean, invstd, gamma, beta, param_bf16, relu, dsums_ws,
+                           dsums_ws + C, dgamma, dbeta, stream);
 }

@@ -1,0 +1,202 @@
+"""Fused "conv head": every 1x1 conv that reads the same input, as ONE MFMA GEMM.
+
+An Inception block feeds its input x to several branches whose first layer is
+a 1x1 conv + BN + ReLU, plus an avg-pool branch (avgpool 3x3/s1/p1 -> 1x1 conv
+-> BN -> ReLU).  Per-channel BN and per-pixel 1x1 convs compose cleanly, so the
+MI355X-native schedule is:
+
+forward
+    Z = x . [W_1 | W_2 | ... | W_pool]^T          one MFMA GEMM, N = sum(C_i);
+                                                  BN sums/sum-squares of every
+                                                  column come out of its epilogue
+    y_i = relu(bn_i(Z[:, slice_i]))               apply kernels read channel slices
+    P   = avgpool3x3(Z[:, pool])                  linear ops commute: conv(avg(x)) ==
+    y_p = relu(bn_p(P))                           avg(conv(x)), and the pool now runs
+                                                  on pool_ch (32..192) channels
+                                                  instead of Cin (192..2048)
+backward
+    dZ[:, slice_i] = bn_bwd_i(dy_i)               written into one [M, sum C_i] buffer
+    dZ[:, pool]    = avgpool3x3(bn_bwd_p(dy_p))   (the box stencil is self-adjoint)
+    dx = dZ . W                                   ONE backward-data GEMM: the input
+    dW = dZ^T x                                   gradient needs no per-branch adds
+
+Compared with the textbook graph this removes the separate BN statistics pass
+of each head conv, 2-3 gradient-accumulation adds of the block input per block,
+the avg-pool over Cin channels, and turns 3-4 small GEMMs into one wide one.
+A single-split head is simply conv1x1 + BN + ReLU with epilogue statistics.
+"""
+from __future__ import annotations
+
+from typing import Sequence
+
+import torch
+from torch import nn
+
+from . import _lib
+from .bn import _as_rows, _rows_view
+from .gemm import wgrad_tn
+
+_BF16 = torch.bfloat16
+
+
+def _cl_empty(n, c, h, w, device, dtype=_BF16):
+    return torch.empty((n, c, h, w), dtype=dtype, device=device, memory_format=torch.channels_last)
+
+
+def _off(t: torch.Tensor, elems: int) -> int:
+    return t.data_ptr() + elems * t.element_size()
+
+
+class _HeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, running_mean, running_var, splits, npool, training, momentum, eps):
+        L = _lib.lib()
+        dev = x.device
+        stream = _lib.stream_ptr(dev)
+        x, (M, cin, ldx) = _as_rows(x)
+        n, _, h, w = x.shape
+        ctot = weight.shape[0]
+        w2 = weight.reshape(ctot, cin)
+        if w2.stride(0) != cin or w2.stride(1) != 1:
+            w2 = w2.contiguous()
+        pb = int(gamma.dtype == _BF16)
+        Z = _cl_empty(n, ctot, h, w, dev)
+        stats = torch.empty(2 * ctot, dtype=torch.float32, device=dev)
+        rc = L.tony_gemm_bf16(x.data_ptr(), w2.data_ptr(), Z.data_ptr(), M, ctot, cin, ldx, cin, ctot,
+                              1 if training else 0, stats.data_ptr(), stream)
+        _lib.check(rc, "tony_gemm_bf16")
+        if training:
+            mean = torch.empty(ctot, dtype=torch.float32, device=dev)
+            invstd = torch.empty(ctot, dtype=torch.float32, device=dev)
+        else:
+            mean = running_mean
+            invstd = torch.rsqrt(running_var.float() + eps)
+        mode = 0 if training else 1
+        outs = []
+        c0 = 0
+        for ci in splits:
+            y = _cl_empty(n, ci, h, w, dev)
+            rc = L.tony_bn_apply(_off(Z, c0), M, ci, ctot, y.data_ptr(), ci, _off(stats, c0), _off(stats, ctot + c0),
+                                 _off(gamma, c0), _off(beta, c0), pb, float(eps), 1, mode,
+                                 _off(mean, c0) if training else 0, _off(invstd, c0) if training else 0,
+                                 _off(running_mean, c0), _off(running_var, c0), float(momentum), stream)
+            _lib.check(rc, "tony_bn_apply")
+            outs.append(y)
+            c0 += ci
+        P = None
+        if npool:
+            P = _cl_empty(n, npool, h, w, dev)
+            rc = L.tony_avgpool3_s1p1(_off(Z, c0), P.data_ptr(), n, h, w, npool, ctot, npool, stream)
+            _lib.check(rc, "tony_avgpool3_s1p1")
+            if training:
+                rc = L.tony_bn_stats(P.data_ptr(), M, npool, npool, _off(stats, c0), _off(stats, ctot + c0), stream)
+                _lib.check(rc, "tony_bn_stats")
+            y = _cl_empty(n, npool, h, w, dev)
+            rc = L.tony_bn_apply(P.data_ptr(), M, npool, npool, y.data_ptr(), npool, _off(stats, c0),
+                                 _off(stats, ctot + c0), _off(gamma, c0), _off(beta, c0), pb, float(eps), 1, mode,
+                                 _off(mean, c0) if training else 0, _off(invstd, c0) if training else 0,
+                                 _off(running_mean, c0), _off(running_var, c0), float(momentum), stream)
+            _lib.check(rc, "tony_bn_apply")
+            outs.append(y)
+        ctx.save_for_backward(x, weight, gamma, beta, mean, invstd, Z, P)
+        ctx.splits = tuple(splits)
+        ctx.npool = npool
+        ctx.pb = pb
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *douts):
+        L = _lib.lib()
+        x, weight, gamma, beta, mean, invstd, Z, P = ctx.saved_tensors
+        dev = x.device
+        stream = _lib.stream_ptr(dev)
+        M, cin, ldx = _rows_view(x)
+        n, _, h, w = x.shape
+        ctot = weight.shape[0]
+        pb = ctx.pb
+        dZ = _cl_empty(n, ctot, h, w, dev)
+        dsum = torch.empty(2 * ctot, dtype=torch.float32, device=dev)
+        dgamma = torch.empty_like(gamma)
+        dbeta = torch.empty_like(beta)
+        c0 = 0
+        for ci, dy in zip(ctx.splits, douts):
+            dy, (_, _, lddy) = _as_rows(dy)
+            rc = L.tony_bn_bwd_reduce(_off(Z, c0), ctot, dy.data_ptr(), lddy, M, ci, _off(mean, c0), _off(invstd, c0),
+                                      _off(gamma, c0), _off(beta, c0), pb, 1, _off(dsum, c0), _off(dsum, ctot + c0),
+                                      stream)
+            _lib.check(rc, "tony_bn_bwd_reduce")
+            rc = L.tony_bn_bwd_apply(_off(Z, c0), ctot, dy.data_ptr(), lddy, _off(dZ, c0), ctot, M, ci,
+                                     _off(mean, c0), _off(invstd, c0), _off(gamma, c0), _off(beta, c0), pb, 1,
+                                     _off(dsum, c0), _off(dsum, ctot + c0), _off(dgamma, c0), _off(dbeta, c0),
+                                     stream)
+            _lib.check(rc, "tony_bn_bwd_apply")
+            c0 += ci
+        if ctx.npool:
+            npool = ctx.npool
+            dy, (_, _, lddy) = _as_rows(douts[len(ctx.splits)])
+            dP = _cl_empty(n, npool, h, w, dev)
+            rc = L.tony_bn_bwd_reduce(P.data_ptr(), npool, dy.data_ptr(), lddy, M, npool, _off(mean, c0),
+                                      _off(invstd, c0), _off(gamma, c0), _off(beta, c0), pb, 1, _off(dsum, c0),
+                                      _off(dsum, ctot + c0), stream)
+            _lib.check(rc, "tony_bn_bwd_reduce")
+            rc = L.tony_bn_bwd_apply(P.data_ptr(), npool, dy.data_ptr(), lddy, dP.data_ptr(), npool, M, npool,
+                                     _off(mean, c0), _off(invstd, c0), _off(gamma, c0), _off(beta, c0), pb, 1,
+                                     _off(dsum, c0), _off(dsum, ctot + c0), _off(dgamma, c0), _off(dbeta, c0),
+                                     stream)
+            _lib.check(rc, "tony_bn_bwd_apply")
+            rc = L.tony_avgpool3_s1p1(dP.data_ptr(), _off(dZ, c0), n, h, w, npool, npool, ctot, stream)
+            _lib.check(rc, "tony_avgpool3_s1p1")
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wt = weight.reshape(ctot, cin).t().contiguous()  # [Cin, Ctot]
+            dx = _cl_empty(n, cin, h, w, dev)
+            rc = L.tony_gemm_bf16(dZ.data_ptr(), wt.data_ptr(), dx.data_ptr(), M, cin, ctot, ctot, ctot, cin, 0, 0,
+                                  stream)
+            _lib.check(rc, "tony_gemm_bf16")
+        dw = wgrad_tn(dZ.data_ptr(), ctot, x.data_ptr(), ldx, M, ctot, cin, dev).to(weight.dtype).reshape(weight.shape)
+        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None
+
+
+def head_reference(x, weight, gamma, beta, running_mean, running_var, splits, npool, training, momentum, eps):
+    """PyTorch fp32-capable reference of the fused head (CPU path and tests)."""
+    z = torch.nn.functional.conv2d(x, weight)
+    outs = []
+    c0 = 0
+    for ci in splits:
+        sl = slice(c0, c0 + ci)
+        outs.append(torch.relu(torch.nn.functional.batch_norm(
+            z[:, sl], running_mean[sl] if running_mean is not None else None,
+            running_var[sl] if running_var is not None else None, gamma[sl], beta[sl], training, momentum, eps)))
+        c0 += ci
+    if npool:
+        sl = slice(c0, c0 + npool)
+        # contiguous NCHW on purpose: this PyTorch-ROCm build's channels_last
+        # avg_pool2d backward returns wrong gradients on the GPU
+        p = torch.nn.functional.avg_pool2d(z[:, sl].contiguous(), 3, 1, 1, count_include_pad=True)
+        outs.append(torch.relu(torch.nn.functional.batch_norm(
+            p, running_mean[sl] if running_mean is not None else None,
+            running_var[sl] if running_var is not None else None, gamma[sl], beta[sl], training, momentum, eps)))
+    return tuple(outs)
+
+
+class FusedHead(nn.Module):
+    """Parallel 1x1 conv+BN+ReLU branches (and an optional avgpool->1x1 branch) on one input."""
+
+    def __init__(self, cin: int, couts: Sequence[int], pool_cout: int = 0, eps: float = 1e-3,
+                 momentum: float = 0.1):
+        super().__init__()
+        self.splits = tuple(int(c) for c in couts)
+        self.npool = int(pool_cout)
+        total = sum(self.splits) + self.npool
+        self.conv = nn.Conv2d(cin, total, 1, bias=False)
+        self.bn = nn.BatchNorm2d(total, eps=eps, momentum=momentum)
+
+    def forward(self, x):
+        training = self.training
+        args = (x, self.conv.weight, self.bn.weight, self.bn.bias, self.bn.running_mean, self.bn.running_var,
+                self.splits, self.npool, training, self.bn.momentum, self.bn.eps)
+        if x.is_cuda:
+            if x.dtype != _BF16:
+                raise TypeError("FusedHead HIP path takes bf16 activations")
+            return _HeadFn.apply(*args)
+        return head_reference(*args)

@@ -17,16 +17,16 @@ for s in "$@"; do
   case $s in
     tests) step gpu_tests 900 python -m pytest tests -m gpu -x -q ;;
     smoke) step smoke 600 python __graft_entry__.py smoke ;;
-    bench_eager) step bench_eager 900 python bench.py --steps 10 --warmup 4 --no-graph ;;
+    bench_eager) step bench_eager 900 python bench.py --steps 10 --warmup 4 --no-graph --no-miopen-find ;;
     bench) step bench 900 python bench.py --steps 20 --warmup 6 ;;
     bench_stock) step bench_stock 900 python bench.py --steps 10 --warmup 4 --no-graph --stock ;;
     prof) export TMPDIR=/tmp; R=$(pwd)
-          step prof 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 5 --no-graph ${BENCH_ARGS:-}
+          step prof 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 5 --no-graph --no-miopen-find ${BENCH_ARGS:-}
           python3 tools/prof_summary.py gpurun_out/prof --skip 6 > gpurun_out/prof_summary.md; find gpurun_out/prof -name '*trace*' -delete ;;
     prof_stock) export TMPDIR=/tmp; R=$(pwd)
-          step prof_stock 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_stock" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 5 --no-graph --stock
+          step prof_stock 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_stock" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 5 --no-graph --no-miopen-find --stock
           python3 tools/prof_summary.py gpurun_out/prof_stock --skip 6 > gpurun_out/prof_stock_summary.md; find gpurun_out/prof_stock -name '*trace*' -delete ;;
-    bench_find) step bench_find 1100 python bench.py --steps 20 --warmup 6 --miopen-find ;;
+    bench_imm) step bench_imm 1100 python bench.py --steps 20 --warmup 6 --no-miopen-find ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
   esac
 done

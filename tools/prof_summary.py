@@ -20,8 +20,10 @@ def classify(name):
     n = name.lower()
     if "bn_fwd" in n or "bn_bwd" in n:
         return "tony HIP: fused BN+ReLU"
-    if "gemm_nt_kernel" in n:
-        return "tony HIP: MFMA GEMM (1x1 conv)"
+    if "gemm_nt_kernel" in n or "gemm_tn_splitk" in n:
+        return "tony HIP: MFMA GEMM (1x1 conv fwd/dgrad/wgrad)"
+    if "box3_kernel" in n or "maxpool_" in n:
+        return "tony HIP: pooling"
     if "sgd_kernel" in n or "adam_kernel" in n or "grad_stats" in n:
         return "tony HIP: fused optimizer"
     if "xent" in n:
