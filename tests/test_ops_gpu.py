@@ -285,3 +285,29 @@ def test_fused_head_matches_reference(cuda, cfg):
     torch.autograd.backward(outs, dys)
     torch.autograd.backward(refs, [d.float() for d in dys])
     _close(x.grad, xr.grad, 5e-2, 5e-2 * xr.grad.abs().max().item(), "head dx", max_bad_frac=2e-3)
+
+
+def test_inplace_grad_accumulation_matches_returned_grads(cuda):
+    """Fused ops adding parameter grads straight into the flat grad buffer == autograd's grads."""
+    from tony_amd.models.inception_v3 import InceptionA
+    from tony_amd.ops import _lib
+    from tony_amd.parallel.flat import FlatParams
+
+    torch.manual_seed(9)
+    blk = InceptionA(192, 32, fused=True).to(cuda).to(memory_format=torch.channels_last)
+    x = _nhwc(torch.randn(4, 192, 17, 17, device=cuda)).to(torch.bfloat16)
+    x = _nhwc(x)
+    flat = FlatParams(blk, dtype=torch.bfloat16, device=cuda)
+    for b in blk.buffers():
+        b.data = b.data.float()
+    grads = {}
+    for inplace in (False, True):
+        _lib.set_inplace_grads(inplace)
+        flat.zero_grad()
+        flat.rebind_grads()
+        out = blk(x)
+        out.float().square().mean().backward()
+        torch.cuda.synchronize()
+        grads[inplace] = flat.grad.clone()
+    _lib.set_inplace_grads(True)
+    _close(grads[True], grads[False], 2e-2, 2e-2 * grads[False].abs().max().item(), "inplace grads")

@@ -34,7 +34,7 @@ _SIGNATURES = {
     "tony_bn_fwd_infer": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int,
                           c_float, c_int, c_void_p, c_void_p, c_void_p],
     "tony_bn_bwd": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p,
-                    c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+                    c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "tony_bn_stats": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p],
     "tony_bn_apply": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                       c_int, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p],
@@ -42,7 +42,8 @@ _SIGNATURES = {
                            c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "tony_bn_bwd_apply": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p,
                           c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                          c_void_p],
+                          c_int, c_void_p],
+    "tony_add_f32": [c_void_p, c_int, c_void_p, c_int64, c_void_p],
     "tony_sgd_step": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p],
     "tony_adam_step": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p],
     "tony_grad_stats": [c_void_p, c_int, c_int64, c_void_p, c_void_p],
@@ -112,6 +113,28 @@ def num_cus(device) -> int:
     if idx not in _NUM_CUS:
         _NUM_CUS[idx] = torch.cuda.get_device_properties(idx).multi_processor_count
     return _NUM_CUS[idx]
+
+
+_INPLACE_GRADS = [True]
+
+
+def set_inplace_grads(enabled: bool) -> None:
+    """When on (default), fused ops ADD parameter gradients straight into an
+    existing ``param.grad`` (the flat gradient buffer of tony_amd.parallel) and
+    return None to autograd, which removes one AccumulateGrad add kernel and one
+    temporary per parameter per step.  Turn off for hook-driven gradient
+    bucketing that must observe every AccumulateGrad."""
+    _INPLACE_GRADS[0] = bool(enabled)
+
+
+def grad_slot(param):
+    """The tensor to accumulate ``param``'s gradient into, or None."""
+    if not _INPLACE_GRADS[0] or param is None or not isinstance(param, torch.nn.Parameter):
+        return None
+    g = param.grad
+    if g is None or g.dtype != param.dtype or g.shape != param.shape or not g.is_contiguous():
+        return None
+    return g
 
 
 def ptr(t) -> int:

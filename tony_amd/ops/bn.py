@@ -83,6 +83,7 @@ class _BNActFn(torch.autograd.Function):
                                      stream)
             _lib.check(rc, "tony_bn_fwd_infer")
         ctx.save_for_backward(x, weight, bias, mean, invstd)
+        ctx.params = (weight, bias)  # the Parameter objects (for in-place grad accumulation)
         ctx.relu = relu
         ctx.pb = pb
         return y
@@ -96,12 +97,19 @@ class _BNActFn(torch.autograd.Function):
         dx = _empty_like_rows(x)
         _, _, lddx = _rows_view(dx)
         ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
-        dw = torch.empty_like(weight) if weight is not None else None
-        db = torch.empty_like(bias) if bias is not None else None
+        gw, gb = _lib.grad_slot(ctx.params[0]), _lib.grad_slot(ctx.params[1])
+        inplace = gw is not None and gb is not None
+        if inplace:
+            dw, db = gw, gb
+        else:
+            dw = torch.empty_like(weight) if weight is not None else None
+            db = torch.empty_like(bias) if bias is not None else None
         rc = L.tony_bn_bwd(x.data_ptr(), ldx, dy.data_ptr(), lddy, dx.data_ptr(), lddx, M, C, mean.data_ptr(),
                            invstd.data_ptr(), _lib.ptr(weight), _lib.ptr(bias), ctx.pb, int(ctx.relu),
-                           ws.data_ptr(), _lib.ptr(dw), _lib.ptr(db), _lib.stream_ptr(x.device))
+                           ws.data_ptr(), _lib.ptr(dw), _lib.ptr(db), int(inplace), _lib.stream_ptr(x.device))
         _lib.check(rc, "tony_bn_bwd")
+        if inplace:
+            dw = db = None  # already added into param.grad
         return dx, dw, db, None, None, None, None, None, None
 
 

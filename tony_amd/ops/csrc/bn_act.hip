@@ -42,12 +42,16 @@ __device__ __forceinline__ float load_param(const void* p, int idx, int is_bf16,
   return is_bf16 ? bf2f(static_cast<const uint16_t*>(p)[idx]) : static_cast<const float*>(p)[idx];
 }
 
-__device__ __forceinline__ void store_param(void* p, int idx, int is_bf16, float v) {
+// accumulate=1 adds into an existing gradient (flat grad buffer, zeroed once per step)
+__device__ __forceinline__ void store_param(void* p, int idx, int is_bf16, float v, int accumulate) {
   if (p == nullptr) return;
-  if (is_bf16)
-    static_cast<uint16_t*>(p)[idx] = f2bf(v);
-  else
-    static_cast<float*>(p)[idx] = v;
+  if (is_bf16) {
+    uint16_t* q = static_cast<uint16_t*>(p) + idx;
+    *q = f2bf(accumulate ? bf2f(*q) + v : v);
+  } else {
+    float* q = static_cast<float*>(p) + idx;
+    *q = accumulate ? *q + v : v;
+  }
 }
 
 // Reduce per-thread partials over the RPI row-lanes in LDS and add one value
@@ -223,13 +227,15 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
       }
     };
     int64_t r = r0 + rm.rsub;
-    for (; r + 1 * step < r1; r += 2 * step) {
-      bf16x8 xv0 = load8(x + r * ldx + rm.cg * 8);
-      bf16x8 gv0 = load8(dy + r * lddy + rm.cg * 8);
-      bf16x8 xv1 = load8(x + (r + step) * ldx + rm.cg * 8);
-      bf16x8 gv1 = load8(dy + (r + step) * lddy + rm.cg * 8);
-      body(xv0, gv0);
-      body(xv1, gv1);
+    for (; r + 3 * step < r1; r += 4 * step) {
+      bf16x8 xv[4], gv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        xv[u] = load8(x + (r + u * step) * ldx + rm.cg * 8);
+        gv[u] = load8(dy + (r + u * step) * lddy + rm.cg * 8);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) body(xv[u], gv[u]);
     }
     for (; r < r1; r += step) body(load8(x + r * ldx + rm.cg * 8), load8(dy + r * lddy + rm.cg * 8));
   }
@@ -241,7 +247,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     uint16_t* __restrict__ dx, int64_t lddx, int64_t M, int C, int64_t rows_per_block,
     const float* __restrict__ mean, const float* __restrict__ invstd, const void* gamma,
     const void* beta, int param_bf16, int relu, const float* __restrict__ dsum,
-    const float* __restrict__ dsumx, void* dgamma, void* dbeta) {
+    const float* __restrict__ dsumx, void* dgamma, void* dbeta, int accumulate) {
   __shared__ float k_s[kMaxC], a_s[kMaxC], b_s[kMaxC];
   const float inv_m = 1.f / static_cast<float>(M);
   for (int c = threadIdx.x; c < C; c += kThreads) {
@@ -250,8 +256,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     a_s[c] = dsum[c] * inv_m;
     b_s[c] = dsumx[c] * inv_m;
     if (blockIdx.x == 0) {
-      store_param(dbeta, c, param_bf16, dsum[c]);
-      store_param(dgamma, c, param_bf16, dsumx[c]);
+      store_param(dbeta, c, param_bf16, dsum[c], accumulate);
+      store_param(dgamma, c, param_bf16, dsumx[c], accumulate);
     }
   }
   __syncthreads();
@@ -286,13 +292,15 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     store8(dx + row * lddx + rm.cg * 8, bf16x8::from_float(o));
   };
   int64_t r = r0 + rm.rsub;
-  for (; r + 1 * step < r1; r += 2 * step) {
-    bf16x8 xv0 = load8(x + r * ldx + rm.cg * 8);
-    bf16x8 gv0 = load8(dy + r * lddy + rm.cg * 8);
-    bf16x8 xv1 = load8(x + (r + step) * ldx + rm.cg * 8);
-    bf16x8 gv1 = load8(dy + (r + step) * lddy + rm.cg * 8);
-    body(xv0, gv0, r);
-    body(xv1, gv1, r + step);
+  for (; r + 3 * step < r1; r += 4 * step) {
+    bf16x8 xv[4], gv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      xv[u] = load8(x + (r + u * step) * ldx + rm.cg * 8);
+      gv[u] = load8(dy + (r + u * step) * lddy + rm.cg * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) body(xv[u], gv[u], r + u * step);
   }
   for (; r < r1; r += step) body(load8(x + r * ldx + rm.cg * 8), load8(dy + r * lddy + rm.cg * 8), r);
 }
@@ -329,7 +337,7 @@ TONY_API int tony_bn_stats(const void* x, int64_t M, int C, int64_t ldx, float* 
   }
   int64_t rpb;
   int grid;
-  plan_rows(M, C, 16, 2048, &rpb, &grid);
+  plan_rows(M, C, 8, 512, &rpb, &grid);  // few WGs: C atomics per WG contend per channel
   bn_fwd_stats_kernel<<<grid, kThreads, 0, stream>>>(static_cast<const uint16_t*>(x), M, C, ldx, rpb, sum, sumsq);
   TONY_LAUNCH_CHECK();
   return 0;
@@ -344,7 +352,7 @@ TONY_API int tony_bn_apply(const void* x, int64_t M, int C, int64_t ldx, void* y
   if (bad_c(C) || (ldx % 8) || (ldy % 8)) return -1;
   int64_t rpb;
   int grid;
-  plan_rows(M, C, 4, 4096, &rpb, &grid);
+  plan_rows(M, C, 4, 8192, &rpb, &grid);
   bn_fwd_apply_kernel<<<grid, kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), M, C, ldx, rpb, static_cast<uint16_t*>(y), ldy, sum, sumsq, gamma, beta,
       param_bf16, eps, relu, mode, save_mean, save_invstd, running_mean, running_var, momentum);
@@ -364,7 +372,7 @@ TONY_API int tony_bn_bwd_reduce(const void* x, int64_t ldx, const void* dy, int6
   }
   int64_t rpb;
   int grid;
-  plan_rows(M, C, 16, 2048, &rpb, &grid);
+  plan_rows(M, C, 8, 512, &rpb, &grid);  // few WGs: C atomics per WG contend per channel
   bn_bwd_reduce_kernel<<<grid, kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, M, C, rpb, mean, invstd, gamma,
       beta, param_bf16, relu, dsum, dsumx);
@@ -375,14 +383,14 @@ TONY_API int tony_bn_bwd_reduce(const void* x, int64_t ldx, const void* dy, int6
 TONY_API int tony_bn_bwd_apply(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx, int64_t lddx,
                                int64_t M, int C, const float* mean, const float* invstd, const void* gamma,
                                const void* beta, int param_bf16, int relu, const float* dsum, const float* dsumx,
-                               void* dgamma, void* dbeta, hipStream_t stream) {
+                               void* dgamma, void* dbeta, int accumulate, hipStream_t stream) {
   if (bad_c(C) || (ldx % 8) || (lddy % 8) || (lddx % 8)) return -1;
   int64_t rpb;
   int grid;
-  plan_rows(M, C, 4, 4096, &rpb, &grid);
+  plan_rows(M, C, 4, 8192, &rpb, &grid);
   bn_bwd_apply_kernel<<<grid, kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, static_cast<uint16_t*>(dx), lddx,
-      M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsum, dsumx, dgamma, dbeta);
+      M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsum, dsumx, dgamma, dbeta, accumulate);
   TONY_LAUNCH_CHECK();
   return 0;
 }
@@ -411,10 +419,10 @@ TONY_API int tony_bn_fwd_infer(const void* x, int64_t M, int C, int64_t ldx, voi
 TONY_API int tony_bn_bwd(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx,
                          int64_t lddx, int64_t M, int C, const float* mean, const float* invstd,
                          const void* gamma, const void* beta, int param_bf16, int relu,
-                         float* dsums_ws, void* dgamma, void* dbeta, hipStream_t stream) {
+                         float* dsums_ws, void* dgamma, void* dbeta, int accumulate, hipStream_t stream) {
   int rc = tony_bn_bwd_reduce(x, ldx, dy, lddy, M, C, mean, invstd, gamma, beta, param_bf16, relu, dsums_ws,
                               dsums_ws + C, stream);
   if (rc) return rc;
   return tony_bn_bwd_apply(x, ldx, dy, lddy, dx, lddx, M, C, mean, invstd, gamma, beta, param_bf16, relu, dsums_ws,
-                           dsums_ws + C, dgamma, dbeta, stream);
+                           dsums_ws + C, dgamma, dbeta, accumulate, stream);
 }

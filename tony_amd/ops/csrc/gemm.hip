@@ -136,22 +136,23 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(const uint16_t* __res
   }
 
   // Epilogue: C/D map of 16x16 MFMA: col = lane&15, row = (lane>>4)*4 + r.
+  // (1) optional BN column statistics straight from the fp32 accumulators;
+  // (2) the bf16 tile is staged through LDS (rows padded by 16 B so the four
+  //     row-groups of a wave hit different banks) and written back with
+  //     16-byte coalesced stores instead of 2-byte scattered ones.
+  if (stats != nullptr) {
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = n0 + wn * WN + j * 16 + (lane & 15);
-    float s = 0.f, q = 0.f;
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * WN + j * 16 + (lane & 15);
+      float s = 0.f, q = 0.f;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int rowb = m0 + wm * WM + i * 16 + (lane >> 4) * 4;
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float v = acc[i][j][r];
-        s += v;
-        q = fmaf(v, v, q);
-        if (rowb + r < M && col < N) C[static_cast<int64_t>(rowb + r) * ldc + col] = f2bf(v);
-      }
-    }
-    if (stats != nullptr) {
+        for (int r = 0; r < 4; ++r) {
+          const float v = acc[i][j][r];
+          s += v;
+          q = fmaf(v, v, q);
+        }
       // rows >= M were zero-filled, so they add nothing to the column sums
       s += __shfl_xor(s, 16, 64);
       s += __shfl_xor(s, 32, 64);
@@ -161,6 +162,33 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(const uint16_t* __res
         atomicAdd(stats + col, s);
         atomicAdd(stats + N + col, q);
       }
+    }
+  }
+  constexpr int LDC = BN + 8;
+  static_assert(BM * LDC <= 2 * (BM + BN) * BK, "C staging tile must fit in the LDS buffers");
+  uint16_t* Cs = smem;  // the K loop ended with a barrier: both buffers are free
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * WM + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * WN + j * 16 + (lane & 15);
+        Cs[row * LDC + col] = f2bf(acc[i][j][r]);
+      }
+  __syncthreads();
+  constexpr int CHUNKS = BM * BN / 8;
+  for (int v = threadIdx.x; v < CHUNKS; v += kThreads) {
+    const int row = v / (BN / 8), ch = v % (BN / 8);
+    const int grow = m0 + row, gcol = n0 + ch * 8;
+    if (grow >= M || gcol >= N) continue;
+    const uint16_t* src = Cs + row * LDC + ch * 8;
+    uint16_t* dst = C + static_cast<int64_t>(grow) * ldc + gcol;
+    if (gcol + 8 <= N && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+      *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+    } else {
+      for (int e = 0; e < 8 && gcol + e < N; ++e) dst[e] = src[e];
     }
   }
 }

@@ -188,3 +188,33 @@ TONY_API int tony_grad_stats(const void* g, int grad_bf16, int64_t n, float* out
   TONY_LAUNCH_CHECK();
   return 0;
 }
+
+// dst (bf16 or fp32) += src (fp32), n elements: folds an fp32 weight-gradient
+// workspace into the flat gradient buffer in one pass (no cast + add pair).
+namespace {
+template <bool kDstBf16>
+__global__ __launch_bounds__(kThreads) void add_f32_kernel(void* __restrict__ dst, const float* __restrict__ src,
+                                                           int64_t n) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n; i += stride) {
+    if constexpr (kDstBf16) {
+      uint16_t* d = static_cast<uint16_t*>(dst) + i;
+      *d = f2bf(bf2f(*d) + src[i]);
+    } else {
+      static_cast<float*>(dst)[i] += src[i];
+    }
+  }
+}
+}  // namespace
+
+TONY_API int tony_add_f32(void* dst, int dst_bf16, const float* src, int64_t n, hipStream_t stream) {
+  int64_t g = (n + kThreads - 1) / kThreads;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  if (dst_bf16)
+    add_f32_kernel<true><<<static_cast<int>(g), kThreads, 0, stream>>>(dst, src, n);
+  else
+    add_f32_kernel<false><<<static_cast<int>(g), kThreads, 0, stream>>>(dst, src, n);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}

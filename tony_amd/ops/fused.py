@@ -99,6 +99,7 @@ class _HeadFn(torch.autograd.Function):
             _lib.check(rc, "tony_bn_apply")
             outs.append(y)
         ctx.save_for_backward(x, weight, gamma, beta, mean, invstd, Z, P)
+        ctx.params = (weight, gamma, beta)
         ctx.splits = tuple(splits)
         ctx.npool = npool
         ctx.pb = pb
@@ -116,8 +117,11 @@ class _HeadFn(torch.autograd.Function):
         pb = ctx.pb
         dZ = _cl_empty(n, ctot, h, w, dev)
         dsum = torch.empty(2 * ctot, dtype=torch.float32, device=dev)
-        dgamma = torch.empty_like(gamma)
-        dbeta = torch.empty_like(beta)
+        gw, gg, gb = (_lib.grad_slot(p) for p in ctx.params)
+        inplace = gw is not None and gg is not None and gb is not None
+        acc = int(inplace)
+        dgamma = gg if inplace else torch.empty_like(gamma)
+        dbeta = gb if inplace else torch.empty_like(beta)
         c0 = 0
         for ci, dy in zip(ctx.splits, douts):
             dy, (_, _, lddy) = _as_rows(dy)
@@ -128,7 +132,7 @@ class _HeadFn(torch.autograd.Function):
             rc = L.tony_bn_bwd_apply(_off(Z, c0), ctot, dy.data_ptr(), lddy, _off(dZ, c0), ctot, M, ci,
                                      _off(mean, c0), _off(invstd, c0), _off(gamma, c0), _off(beta, c0), pb, 1,
                                      _off(dsum, c0), _off(dsum, ctot + c0), _off(dgamma, c0), _off(dbeta, c0),
-                                     stream)
+                                     acc, stream)
             _lib.check(rc, "tony_bn_bwd_apply")
             c0 += ci
         if ctx.npool:
@@ -142,7 +146,7 @@ class _HeadFn(torch.autograd.Function):
             rc = L.tony_bn_bwd_apply(P.data_ptr(), npool, dy.data_ptr(), lddy, dP.data_ptr(), npool, M, npool,
                                      _off(mean, c0), _off(invstd, c0), _off(gamma, c0), _off(beta, c0), pb, 1,
                                      _off(dsum, c0), _off(dsum, ctot + c0), _off(dgamma, c0), _off(dbeta, c0),
-                                     stream)
+                                     acc, stream)
             _lib.check(rc, "tony_bn_bwd_apply")
             rc = L.tony_avgpool3_s1p1(dP.data_ptr(), _off(dZ, c0), n, h, w, npool, npool, ctot, stream)
             _lib.check(rc, "tony_avgpool3_s1p1")
@@ -153,7 +157,12 @@ class _HeadFn(torch.autograd.Function):
             rc = L.tony_gemm_bf16(dZ.data_ptr(), wt.data_ptr(), dx.data_ptr(), M, cin, ctot, ctot, ctot, cin, 0, 0,
                                   stream)
             _lib.check(rc, "tony_gemm_bf16")
-        dw = wgrad_tn(dZ.data_ptr(), ctot, x.data_ptr(), ldx, M, ctot, cin, dev).to(weight.dtype).reshape(weight.shape)
+        dw32 = wgrad_tn(dZ.data_ptr(), ctot, x.data_ptr(), ldx, M, ctot, cin, dev)
+        if inplace:
+            rc = L.tony_add_f32(gw.data_ptr(), int(gw.dtype == _BF16), dw32.data_ptr(), dw32.numel(), stream)
+            _lib.check(rc, "tony_add_f32")
+            return dx, None, None, None, None, None, None, None, None, None, None
+        dw = dw32.to(weight.dtype).reshape(weight.shape)
         return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None
 
 
