@@ -1,0 +1,1 @@
+"""TonY-compatible module path (see tony_amd.cli)."""

@@ -1,0 +1,120 @@
+"""Task resource monitor (behavioural parity with T/TaskMonitor.java:25-192).
+
+Every ``tony.task.metrics-interval-ms`` it samples the RSS of the task's process
+tree (psutil) and, for the GPUs the coordinator pinned to the task (TonY
+averages over *all* GPUs of the node), busy %, VRAM-used % and memory-engine
+busy % via amd-smi, plus MI355X power / temperature; keeps running max and
+average, and pushes them to the coordinator's metrics RPC.  GPU sampling stops
+after ``MAX_REPEATED_GPU_ERROR_ALLOWED`` consecutive failures.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+from typing import Callable, Dict, List, Optional
+
+from .. import constants as C
+from .. import native
+
+LOG = logging.getLogger(__name__)
+
+
+class RunningStat:
+    def __init__(self):
+        self.max = 0.0
+        self.sum = 0.0
+        self.n = 0
+
+    def add(self, v: float) -> None:
+        self.max = max(self.max, v)
+        self.sum += v
+        self.n += 1
+
+    @property
+    def avg(self) -> float:
+        return self.sum / self.n if self.n else 0.0
+
+
+def tree_rss_bytes(pid: int) -> int:
+    try:
+        import psutil
+    except ImportError:  # pragma: no cover
+        return 0
+    try:
+        p = psutil.Process(pid)
+        procs = [p] + p.children(recursive=True)
+    except psutil.Error:
+        return 0
+    total = 0
+    for q in procs:
+        try:
+            total += q.memory_info().rss
+        except psutil.Error:
+            pass
+    return total
+
+
+class TaskMonitor:
+    def __init__(self, pid_fn: Callable[[], Optional[int]], gpu_ids: List[int], interval_ms: int,
+                 push: Callable[[Dict[str, float]], None], gpu_metrics: bool = True):
+        self.pid_fn = pid_fn
+        self.gpu_ids = gpu_ids
+        self.interval_s = max(0.05, interval_ms / 1000.0)
+        self.push = push
+        self.gpu_metrics = gpu_metrics and bool(gpu_ids)
+        self.mem = RunningStat()
+        self.util = RunningStat()
+        self.fb = RunningStat()
+        self.main = RunningStat()
+        self.power = RunningStat()
+        self.temp = RunningStat()
+        self.gpu_errors = 0
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._run, name="tony-task-monitor", daemon=True)
+
+    def start(self):
+        self._thread.start()
+
+    def stop(self):
+        self._stop.set()
+        self.refresh()
+        self._push()
+
+    def refresh(self) -> None:
+        pid = self.pid_fn()
+        if pid:
+            self.mem.add(float(tree_rss_bytes(pid)))
+        if self.gpu_metrics and self.gpu_errors < C.MAX_REPEATED_GPU_ERROR_ALLOWED:
+            samples = [native.smi_sample(g) for g in self.gpu_ids]
+            samples = [s for s in samples if s is not None]
+            if not samples:
+                self.gpu_errors += 1
+                return
+            self.gpu_errors = 0
+            n = len(samples)
+            self.util.add(sum(s.gfx_busy_pct for s in samples) / n)
+            self.fb.add(sum(100.0 * s.vram_used_mb / s.vram_total_mb for s in samples if s.vram_total_mb) / n)
+            self.main.add(sum(s.mem_busy_pct for s in samples) / n)
+            self.power.add(sum(s.power_w for s in samples))
+            self.temp.add(max(s.temp_c for s in samples))
+
+    def metrics(self) -> Dict[str, float]:
+        m = {C.MAX_MEMORY_BYTES: self.mem.max, C.AVG_MEMORY_BYTES: self.mem.avg}
+        if self.gpu_metrics:
+            m.update({C.MAX_GPU_UTILIZATION: self.util.max, C.AVG_GPU_UTILIZATION: self.util.avg,
+                      C.MAX_GPU_FB_MEMORY_USAGE: self.fb.max, C.AVG_GPU_FB_MEMORY_USAGE: self.fb.avg,
+                      C.MAX_GPU_MAIN_MEMORY_USAGE: self.main.max, C.AVG_GPU_MAIN_MEMORY_USAGE: self.main.avg,
+                      C.MAX_GPU_POWER_WATTS: self.power.max, C.AVG_GPU_POWER_WATTS: self.power.avg,
+                      C.MAX_GPU_TEMPERATURE: self.temp.max})
+        return m
+
+    def _push(self):
+        try:
+            self.push(self.metrics())
+        except Exception:  # noqa: BLE001
+            LOG.debug("metrics push failed", exc_info=True)
+
+    def _run(self):
+        while not self._stop.wait(self.interval_s):
+            self.refresh()
+            self._push()

@@ -300,11 +300,20 @@ def append_conf_resources(key: str, resource: Optional[str], conf) -> None:
 
 
 # -- process execution (Utils.java:299-328) ------------------------------------------------------------
+def _pdeathsig():  # runs in the child between fork and exec
+    import ctypes
+
+    try:
+        ctypes.CDLL("libc.so.6").prctl(1, signal.SIGKILL)  # PR_SET_PDEATHSIG
+    except OSError:
+        pass
+
+
 class ShellProcess:
     """A ``bash -c`` child in its own session/process group."""
 
     def __init__(self, command: str, env: Optional[Dict[str, str]] = None, cwd: Optional[str] = None,
-                 stdout=None, stderr=None, extra_env_unset=("MALLOC_ARENA_MAX",)):
+                 stdout=None, stderr=None, extra_env_unset=("MALLOC_ARENA_MAX",), die_with_parent: bool = False):
         penv = dict(os.environ)
         for k in extra_env_unset:
             penv.pop(k, None)
@@ -318,7 +327,7 @@ class ShellProcess:
                 LOG.warning("failed to make %s executable", exe)
         self.command = command
         self.proc = subprocess.Popen(["bash", "-c", command], env=penv, cwd=cwd, stdout=stdout, stderr=stderr,
-                                     start_new_session=True)
+                                     start_new_session=True, preexec_fn=_pdeathsig if die_with_parent else None)
         self.pid = self.proc.pid
 
     def wait(self, timeout_s: Optional[float] = None) -> int:
