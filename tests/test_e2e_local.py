@@ -1,0 +1,332 @@
+"""Local-mode end-to-end scenarios: TonY's TT/TestTonyE2E.java (27 tests), re-run on the
+single-node coordinator with CPU-only tasks and a fake 8-GPU inventory.
+
+Each test submits a real job: TonyClient -> coordinator process -> task agents ->
+user scripts (tests/fixtures/scripts), and checks the exit code / task statuses
+exactly like the reference test of the same name (line numbers in docstrings).
+"""
+import os
+import sys
+import time
+
+import pytest
+
+from tony_amd import constants as C
+from tony_amd.client.tony_client import TonyClient
+from tony_amd.cluster.session import TaskStatus
+from tony_amd.conf import Configuration
+from tony_amd.conf import keys as K
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+FIX = os.path.join(HERE, "fixtures")
+SCRIPTS = os.path.join(FIX, "scripts")
+PY = sys.executable
+
+pytestmark = pytest.mark.timeout(120)
+
+
+class Handler:
+    def __init__(self):
+        self.app_id = None
+        self.infos = set()
+
+    def on_application_id_received(self, app_id):
+        self.app_id = app_id
+
+    def on_task_infos_updated(self, infos):
+        self.infos = infos
+
+
+@pytest.fixture
+def conf(tmp_path):
+    c = Configuration()
+    c.set(K.SECURITY_ENABLED, "false")
+    c.set(K.CONTAINERS_RESOURCES, os.path.join(FIX, "common.zip"))
+    c.set(K.AMD_STAGING_DIR, str(tmp_path / "staging"))
+    c.set(K.AMD_FAKE_GPUS, "8")
+    c.set(K.AMD_VISIBLE_DEVICES_MODE, "none")
+    c.set(K.TASK_HEARTBEAT_INTERVAL_MS, "200")
+    c.set("tony.amd.stop-grace-sec", "3")
+    c.set(K.AM_WAIT_CLIENT_STOP_TIMEOUT, "5")
+    return c
+
+
+def run(conf, args, handler=None):
+    client = TonyClient(conf)
+    if handler is not None:
+        client.callback_handler = handler
+        client.add_listener(handler)
+    assert client.init(args), "client.init failed"
+    rc = client.start()
+    return rc, client
+
+
+def base(*extra):
+    return ["--src_dir", SCRIPTS, "--python_binary_path", PY, *extra]
+
+
+def test_single_node_training_should_pass(conf):
+    """TestTonyE2E.java:128"""
+    rc, _ = run(conf, base("--executes", "exit_0_check_env.py", "--shell_env", "ENV_CHECK=ENV_CHECK"))
+    assert rc == 0
+
+
+def test_single_node_training_should_fail(conf):
+    """TestTonyE2E.java:227"""
+    rc, _ = run(conf, base("--executes", "exit_1.py"))
+    assert rc == -1
+
+
+def test_ps_worker_should_fail_missed_heartbeat(conf):
+    """TestTonyE2E.java:143 -- the agent skips heartbeats (TEST_TASK_EXECUTOR_NUM_HB_MISS)."""
+    conf.set(K.TASK_MAX_MISSED_HEARTBEATS, "2")
+    rc, _ = run(conf, base("--executes", "sleep_arg.py 4", "--container_env",
+                           f"{C.TEST_TASK_EXECUTOR_NUM_HB_MISS}=5", "--conf", "tony.ps.instances=1",
+                           "--conf", "tony.worker.instances=1"))
+    assert rc != 0
+
+
+def test_ps_skewed_worker_should_pass(conf):
+    """TestTonyE2E.java:162 (skew 30 s -> 2 s here)."""
+    conf.set(K.instances_key("ps"), "1")
+    conf.set(K.instances_key("worker"), "2")
+    rc, _ = run(conf, base("--executes", "exit_0_check_env.py", "--shell_env", "ENV_CHECK=ENV_CHECK",
+                           "--container_env", f"{C.TEST_TASK_EXECUTOR_SKEW}=worker#0#2000"))
+    assert rc == 0
+
+
+def test_ps_worker_with_venv_should_pass(conf):
+    """TestTonyE2E.java:180"""
+    rc, _ = run(conf, ["--src_dir", SCRIPTS, "--executes", f"{PY} check_env_and_venv.py", "--shell_env",
+                       "ENV_CHECK=ENV_CHECK", "--python_venv", os.path.join(FIX, "test.zip"),
+                       "--conf", "tony.worker.instances=1"])
+    assert rc == 0
+
+
+def test_worker_training_pytorch_env_should_pass(conf):
+    """TestTonyE2E.java:195"""
+    rc, _ = run(conf, base("--executes", "exit_0_check_pytorchenv.py", "--shell_env", "ENV_CHECK=ENV_CHECK",
+                           "--conf", "tony.application.framework=pytorch", "--conf", "tony.ps.instances=0",
+                           "--conf", "tony.worker.instances=2"))
+    assert rc == 0
+
+
+def test_ps_worker_training_should_fail(conf):
+    """TestTonyE2E.java:212"""
+    rc, _ = run(conf, base("--executes", "exit_1.py", "--conf", "tony.ps.instances=1",
+                           "--conf", "tony.worker.instances=1"))
+    assert rc == -1
+
+
+def test_am_crash_should_fail(conf):
+    """TestTonyE2E.java:241"""
+    rc, _ = run(conf, base("--executes", "exit_0.py", "--conf", "tony.worker.instances=1",
+                           "--container_env", f"{C.TEST_AM_CRASH}=true"))
+    assert rc == -1
+
+
+def test_am_throw_exception_crash_should_fail(conf):
+    """TestTonyE2E.java:256"""
+    rc, _ = run(conf, base("--executes", "exit_0.py", "--conf", "tony.worker.instances=1",
+                           "--container_env", f"{C.TEST_AM_THROW_EXCEPTION_CRASH}=true"))
+    assert rc == -1
+
+
+def test_dag_scheduler_should_pass(conf):
+    """TestTonyE2E.java:271 -- prepare stage (dbloader, db) before training stage (ps, worker)."""
+    h = Handler()
+    rc, client = run(conf, base("--executes", "exit_0.py", "--conf", "tony.worker.instances=1",
+                                "--conf", "tony.ps.instances=1", "--conf", "tony.db.instances=1",
+                                "--conf", "tony.dbloader.instances=1",
+                                "--conf", "tony.application.prepare-stage=dbloader,db",
+                                "--conf", "tony.application.training-stage=ps,worker"), h)
+    assert rc == 0
+
+
+def test_am_stops_job_after_worker0_killed(conf):
+    """TestTonyE2E.java:298 (TEST_WORKER_TERMINATION)"""
+    rc, _ = run(conf, base("--executes", "sleep_arg.py 20", "--container_env", f"{C.TEST_WORKER_TERMINATED}=true",
+                           "--conf", "tony.worker.instances=1"))
+    assert rc == -1
+
+
+def test_rpc_client_closed_after_finish(conf):
+    """TestTonyE2E.java:310"""
+    rc, client = run(conf, base("--executes", "exit_0.py", "--conf", "tony.worker.instances=1"))
+    assert rc == 0 and client.rpc is None
+
+
+def test_non_chief_worker_fail(conf):
+    """TestTonyE2E.java:323 (worker:0 is the chief when there is no chief job)."""
+    rc, _ = run(conf, base("--executes", "exit_1.py", "--conf", "tony.ps.instances=1",
+                           "--conf", "tony.worker.instances=1"))
+    assert rc == -1
+
+
+def test_resources_flag_localization(conf):
+    """TestTonyE2E.java:339 -- ::alias, #archive, plain files and a lib directory."""
+    res = (f"{FIX}/test.zip::test20.zip,{FIX}/test2.zip#archive,,{FIX}/common.zip,{FIX}/libdir")
+    rc, _ = run(conf, ["--src_dir", SCRIPTS, "--executes", f"{PY} check_archive_file_localization.py",
+                       "--conf", "tony.worker.instances=1", "--conf", f"tony.worker.resources={res}",
+                       "--conf", "tony.ps.instances=0"])
+    assert rc == 0
+
+
+def test_tensorboard_port_set_only_on_chief(conf):
+    """TestTonyE2E.java:359"""
+    rc, _ = run(conf, ["--src_dir", SCRIPTS, "--executes", f"{PY} check_tb_port_set_in_chief_only.py",
+                       "--conf", "tony.chief.instances=1", "--conf", "tony.ps.instances=1",
+                       "--conf", "tony.worker.instances=1"])
+    assert rc == 0
+
+
+def test_standalone_should_pass(conf):
+    """TestTonyE2E.java:375"""
+    rc, _ = run(conf, base("--executes", "exit_0.py", "--conf", "tony.application.framework=standalone",
+                           "--conf", "tony.worker.instances=1"))
+    assert rc == 0
+
+
+def test_standalone_multi_instance_should_fail(conf):
+    """TestTonyE2E.java:391"""
+    rc, _ = run(conf, base("--executes", "exit_0.py", "--conf", "tony.application.framework=standalone",
+                           "--conf", "tony.worker.instances=1", "--conf", "tony.slave.instances=1"))
+    assert rc == -1
+
+
+def test_task_completion_notification_delayed_still_passes(conf):
+    """TestTonyE2E.java:412 -- the result RPC unregisters the task from the HB monitor first."""
+    rc, _ = run(conf, base("--executes", "exit_0.py", "--conf", "tony.ps.instances=0",
+                           "--conf", "tony.worker.instances=1", "--conf", f"{K.TASK_HEARTBEAT_INTERVAL_MS}=100",
+                           "--conf", f"{K.TASK_MAX_MISSED_HEARTBEATS}=5",
+                           "--container_env", f"{C.TEST_TASK_COMPLETION_NOTIFICATION_DELAYED}=true"))
+    assert rc == 0
+
+
+def test_callback_handler_and_final_statuses(conf):
+    """TestTonyE2E.java:430 -- worker SUCCEEDED, untracked ps killed -> FINISHED."""
+    h = Handler()
+    rc, _ = run(conf, ["--src_dir", SCRIPTS, "--shell_env", "ENV_CHECK=ENV_CHECK",
+                       "--python_venv", os.path.join(FIX, "test.zip"),
+                       "--conf", "tony.ps.instances=1", "--conf", "tony.worker.instances=1",
+                       "--conf", f"tony.ps.command={PY} sleep_30.py",
+                       "--conf", f"tony.worker.command={PY} check_env_and_venv.py"], h)
+    assert rc == 0
+    assert h.app_id is not None
+    st = {t.name: t.status for t in h.infos}
+    assert st == {"worker": TaskStatus.SUCCEEDED, "ps": TaskStatus.FINISHED}
+
+
+def test_ps_crash_fails_and_stops_am(conf):
+    """TestTonyE2E.java:467 -- untracked ps fails -> app fails, worker killed -> FINISHED."""
+    h = Handler()
+    rc, _ = run(conf, ["--src_dir", SCRIPTS, "--conf", "tony.ps.instances=1", "--conf", "tony.worker.instances=1",
+                       "--conf", f"tony.ps.command={PY} exit_1.py",
+                       "--conf", f"tony.worker.command={PY} sleep_30.py",
+                       "--conf", "tony.application.untracked.jobtypes=ps"], h)
+    assert rc == -1
+    st = {t.name: t.status for t in h.infos}
+    assert st == {"worker": TaskStatus.FINISHED, "ps": TaskStatus.FAILED}
+
+
+def test_sidecar_crash_still_passes(conf):
+    """TestTonyE2E.java:499"""
+    h = Handler()
+    rc, _ = run(conf, ["--src_dir", SCRIPTS, "--conf", "tony.sidecarexecutor.instances=1",
+                       "--conf", "tony.worker.instances=1",
+                       "--conf", f"tony.sidecarexecutor.command={PY} exit_1.py",
+                       "--conf", f"tony.worker.command={PY} sleep_arg.py 1",
+                       "--conf", "tony.application.sidecar.jobtypes=sidecarexecutor"], h)
+    assert rc == 0
+    st = {t.name: t.status for t in h.infos}
+    assert st["worker"] == TaskStatus.SUCCEEDED and st["sidecarexecutor"] == TaskStatus.FAILED
+
+
+def test_horovod_driver_crash_fails(conf):
+    """TestTonyE2E.java:531"""
+    rc, _ = run(conf, ["--src_dir", SCRIPTS, "--conf", "tony.worker.instances=1",
+                       "--conf", f"tony.worker.command={PY} sleep_30.py",
+                       "--conf", "tony.horovod.mode.test.fast.fail=true",
+                       "--conf", "tony.application.framework=horovod"])
+    assert rc == -1
+
+
+def test_horovod_should_pass(conf):
+    """TestTonyE2E.java:549 (test-mode driver, env checked by check_horovod_env.py)."""
+    rc, _ = run(conf, ["--src_dir", SCRIPTS, "--executes", f"{PY} check_horovod_env.py",
+                       "--conf", "tony.worker.instances=2", "--conf", "tony.horovod.mode.test=true",
+                       "--conf", "tony.application.framework=horovod"])
+    assert rc == 0
+
+
+def test_horovod_real_rendezvous_should_pass(conf):
+    """Same job with the real (non-test) driver: slot plan + HTTP rendezvous server."""
+    rc, _ = run(conf, ["--src_dir", SCRIPTS, "--executes", f"{PY} check_horovod_env.py",
+                       "--conf", "tony.worker.instances=3", "--conf", "tony.application.framework=horovod"])
+    assert rc == 0
+
+
+def test_horovod_debug_mode_should_pass(conf):
+    """TestTonyE2E.java:567"""
+    rc, _ = run(conf, ["--src_dir", SCRIPTS, "--executes", f"{PY} check_horovod_env.py",
+                       "--conf", "tony.application.framework=horovod", "--conf", "tony.horovod.mode.test=true",
+                       "--conf", "tony.horovod.driver.mode.debug=true", "--conf", "tony.worker.instances=2",
+                       "--conf", "tony.driver.instances=1", "--conf", "tony.driver.vcores=1",
+                       "--conf", "tony.application.untracked.jobtypes=driver",
+                       "--conf", f"tony.driver.command={PY} horovod_debug_driver.py -t -p 9999"])
+    assert rc == 0
+
+
+def test_sidecar_tensorboard_should_pass(conf):
+    """TestTonyE2E.java:593 -- TB_PORT only on the tensorboard sidecar, not on the chief."""
+    rc, _ = run(conf, ["--src_dir", SCRIPTS, "--executes", f"{PY} check_tb_port_set_in_chief_only.py",
+                       "--conf", "tony.chief.instances=1", "--conf", "tony.ps.instances=1",
+                       "--conf", "tony.worker.instances=2", "--sidecar_tensorboard_log_dir", "/tmp",
+                       "--conf", "tony.application.framework=tensorflow",
+                       "--container_env", f"{C.SIDECAR_TB_TEST_KEY}=true",
+                       "--container_env", "SIDECAR_TB_TEST_SLEEP_S=1"])
+    assert rc == 0
+
+
+def test_tony_final_conf(conf, tmp_path):
+    """TestTonyE2E.java:621 -- contents of tony-final.xml (multi-value keys append)."""
+    client = TonyClient(conf)
+    assert client.init(["--executes", "ls", "--shell_env", "TEST1=test", "--container_env", "TEST2=test",
+                        "--conf", "tony.worker.command=cat",
+                        "--conf", f"tony.containers.resources={FIX}/test.zip"])
+    client.app_id = "application_1_0001"
+    client.job_dir = str(tmp_path / "job")
+    os.makedirs(client.job_dir)
+    path = client.process_final_tony_conf()
+    final = Configuration.from_xml(path)
+    assert final.get(K.CONTAINERS_COMMAND) == "ls"
+    assert final.get(K.CONTAINER_LAUNCH_ENV) == "TEST2=test"
+    assert final.get(K.EXECUTION_ENV) == "TEST1=test"
+    assert final.get(K.execute_command_key("worker")) == "cat"
+    res = final.get(K.CONTAINERS_RESOURCES)
+    assert "test.zip" in res and "common.zip" in res
+
+
+def test_gpu_pinning_and_numa_env(conf):
+    """MI355X addition: each task gets its own GPU ids / NUMA node from the (fake) inventory."""
+    rc, _ = run(conf, base("--executes", "check_gpu_pinning.py", "--conf", "tony.worker.instances=4",
+                           "--conf", "tony.worker.gpus=2", "--shell_env", "EXPECT_GPUS=2",
+                           "--conf", "tony.application.framework=pytorch"))
+    assert rc == 0
+
+
+def test_gpu_request_larger_than_node_rejected(conf):
+    client = TonyClient(conf)
+    assert not client.init(base("--executes", "exit_0.py", "--conf", "tony.worker.instances=1",
+                                "--conf", "tony.worker.gpus=9"))
+
+
+def test_launch_latency_under_two_seconds(conf):
+    """Job-launch latency metric (submit -> every task RUNNING) on the local path."""
+    t0 = time.time()
+    rc, client = run(conf, base("--executes", "sleep_arg.py 1.5", "--conf", "tony.worker.instances=4",
+                                "--conf", "tony.ps.instances=1"))
+    assert rc == 0
+    lat = client.launch_latency_s()
+    assert lat is not None and lat < 2.0, lat
+    assert time.time() - t0 < 15

@@ -86,13 +86,7 @@ class TaskExecutor:
         localize_all(specs, cwd)
         staging = self.env.get(C.TONY_JOB_DIR)
         if staging:
-            for fn in (U.tony_src_zip_name(self.app_id), C.PYTHON_VENV_ZIP):
-                src = os.path.join(staging, fn)
-                if os.path.exists(src) and not os.path.exists(os.path.join(cwd, fn)):
-                    try:
-                        os.link(src, os.path.join(cwd, fn))
-                    except OSError:
-                        shutil.copy2(src, os.path.join(cwd, fn))
+            U.link_job_archives(staging, self.app_id, cwd)
         U.extract_resources(self.app_id, cwd)
 
     def pin_cpus(self) -> None:

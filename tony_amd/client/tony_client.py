@@ -359,6 +359,8 @@ class TonyClient:
         env = dict(os.environ)
         pkg_root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env["PYTHONPATH"] = pkg_root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+        # the coordinator runs with the container env too (TonY: the AM container's launch context)
+        env.update(U.parse_key_value(self.tony_conf.get_strings(K.CONTAINER_LAUNCH_ENV)))
         logs = os.path.join(self.job_dir, "logs")
         out = open(os.path.join(logs, C.AM_STDOUT_FILENAME), "ab")
         err = open(os.path.join(logs, C.AM_STDERR_FILENAME), "ab")

@@ -306,6 +306,7 @@ class Coordinator:
         from ..utils.resources import localize_all
 
         localize_all(c.get_strings(K.CONTAINERS_RESOURCES), workdir)
+        U.link_job_archives(self.job_dir, self.app_id, workdir)
         U.extract_resources(self.app_id, workdir)
         env["HOME"] = workdir
         tb = None

@@ -154,6 +154,20 @@ def client_resource_name(app_id: str, file_name: str) -> str:
     return f"{app_id}-{file_name}"
 
 
+def link_job_archives(job_dir: str, app_id: str, cwd: str) -> None:
+    """Make the job's src zip and venv.zip visible in a task working dir (hard link or copy)."""
+    import shutil
+
+    for fn in (tony_src_zip_name(app_id), C.PYTHON_VENV_ZIP):
+        src = os.path.join(job_dir, fn)
+        dst = os.path.join(cwd, fn)
+        if os.path.exists(src) and not os.path.exists(dst):
+            try:
+                os.link(src, dst)
+            except OSError:
+                shutil.copy2(src, dst)
+
+
 def extract_resources(app_id: str, cwd: str = ".") -> None:
     src_zip = os.path.join(cwd, tony_src_zip_name(app_id))
     if os.path.exists(src_zip):
