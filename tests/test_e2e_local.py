@@ -330,3 +330,29 @@ def test_launch_latency_under_two_seconds(conf):
     lat = client.launch_latency_s()
     assert lat is not None and lat < 2.0, lat
     assert time.time() - t0 < 15
+
+
+def test_notebook_submitter_proxies_notebook(conf):
+    """NotebookSubmitter.java:71-133 + ProxyServer: the notebook url is forwarded to a local port."""
+    import threading
+    import urllib.request
+
+    from tony_amd.cli.notebook_submitter import NotebookSubmitter
+
+    sub = NotebookSubmitter(TonyClient(conf))
+    out = {}
+    t = threading.Thread(target=lambda: out.setdefault("rc", sub.submit(base("--executes", "notebook_server.py"))))
+    t.start()
+    deadline = time.time() + 60
+    while sub.proxy is None and time.time() < deadline and t.is_alive():
+        time.sleep(0.1)
+    assert sub.proxy is not None, "no notebook task info / proxy"
+    body = None
+    while body is None and time.time() < deadline:
+        try:
+            body = urllib.request.urlopen(f"http://127.0.0.1:{sub.proxy.local_port}/", timeout=5).read()
+        except OSError:
+            time.sleep(0.2)
+    t.join(60)
+    assert body == b"notebook-ok"
+    assert out.get("rc") == 0

@@ -45,6 +45,7 @@ from ..conf import keys as K
 from ..events import schema as EV
 from ..events.handler import EventHandler
 from ..events.history import HistoryLayout, JobMetadata, year_month_day_dir
+from ..portal.history import write_owner
 from ..gpu.inventory import GpuAllocator, discover
 from ..rpc import protocol as P
 from ..rpc.server import RpcServer
@@ -179,6 +180,7 @@ class Coordinator:
         try:
             os.makedirs(self.history_dir, exist_ok=True)
             shutil.copy2(self.conf_path, os.path.join(self.history_dir, C.TONY_FINAL_XML))
+            write_owner(self.history_dir, self.job_dir)
         except OSError:
             LOG.exception("cannot set up history dir %s", self.history_dir)
             self.history_dir = None
