@@ -1,0 +1,174 @@
+"""Multi-process data-plane tests on CPU (gloo): DDP buckets, the Horovod API, the parameter
+server (colocated / dedicated sync / dedicated async), collectives and the MXNet-style kvstore.
+
+Each test starts one process per rank (spawn), exactly as the TonY runtimes would start one
+task per rank, and compares against a single-process fp32 reference.
+"""
+import multiprocessing as mp
+import socket
+
+import pytest
+import torch
+
+import dist_workers as W
+
+pytestmark = pytest.mark.timeout(180)
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(fn, arglists):
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(len(arglists)) as pool:
+        res = [pool.apply_async(fn, a) for a in arglists]
+        return [r.get(150) for r in res]
+
+
+def _ref_grads(world):
+    model = W._mlp(seed=0)
+    total = None
+    for r in range(world):
+        model.zero_grad()
+        x, y = W._batch(r)
+        torch.nn.functional.cross_entropy(model(x), y).backward()
+        g = [p.grad.clone() for p in model.parameters()]
+        total = g if total is None else [a + b for a, b in zip(total, g)]
+    return model, [t / world for t in total]
+
+
+@pytest.mark.parametrize("bucket_mb", [32, 0.0005])
+def test_ddp_bucketed_allreduce_matches_average(bucket_mb):
+    world, port = 2, _port()
+    outs = _run(W.ddp_rank, [(r, world, port, bucket_mb) for r in range(world)])
+    _, ref = _ref_grads(world)
+    for o in outs:
+        for g, rg in zip(o["grads"], ref):
+            torch.testing.assert_close(g, rg, rtol=1e-5, atol=1e-6)
+    if bucket_mb < 0.001:
+        assert outs[0]["n_buckets"] > 1
+    assert outs[0]["launches"] == outs[0]["n_buckets"]        # the no_sync pass launched nothing
+    assert not torch.allclose(outs[0]["local"][0], outs[1]["local"][0])   # no_sync grads are local
+    for a, b in zip(outs[0]["params"], outs[1]["params"]):
+        torch.testing.assert_close(a, b)                      # rank 0's init was broadcast
+
+
+def test_hvd_api_and_distributed_optimizer():
+    from tony_amd.horovod.rendezvous import RendezvousServer
+
+    srv = RendezvousServer("127.0.0.1")
+    port = srv.start()
+    try:
+        world = 2
+        outs = _run(W.hvd_rank, [(r, world, port) for r in range(world)])
+    finally:
+        srv.stop()
+    for r, o in enumerate(outs):
+        assert (o["rank"], o["size"]) == (r, 2)
+        assert o["avg"] == [1.5] * 3 and o["sum"] == [3.0] * 3 and o["max"] == [2.0] * 3
+        assert o["gather"] == [0.0, 0.0, 1.0]
+        assert o["bcast"] == [10.0] and o["obj"] == {"r": 0} and o["objs"] == [0, 2]
+    assert outs[0]["a2a"] == [0.0, 1.0, 100.0, 101.0] and outs[1]["a2a"] == [2.0, 3.0, 102.0, 103.0]
+    # two accumulated passes per rank, averaged over ranks
+    model, ref = _ref_grads(2)
+    for o in outs:
+        for g, rg in zip(o["grads"], ref):
+            torch.testing.assert_close(g, 2 * rg, rtol=1e-5, atol=1e-6)
+    for a, b in zip(outs[0]["params"], outs[1]["params"]):
+        torch.testing.assert_close(a, b)
+
+
+def _ps_reference(workers, steps, lr=0.1, mu=0.9):
+    """Sync PS semantics: grads averaged over the worker ranks, momentum SGD on fp32."""
+    model = W._mlp(seed=0)
+    opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=mu)
+    for _ in range(steps):
+        opt.zero_grad()
+        for r in workers:
+            x, y = W._batch(r)
+            (torch.nn.functional.cross_entropy(model(x), y) / len(workers)).backward()
+        opt.step()
+    return model
+
+
+@pytest.mark.parametrize("mode,world,workers", [("colocated", 2, [0, 1]), ("dedicated", 3, [1, 2])])
+def test_parameter_server_sync(mode, world, workers):
+    port, steps = _port(), 3
+    outs = _run(W.ps_rank, [(r, world, port, mode, True, steps) for r in range(world)])
+    ref = _ps_reference(workers, steps)
+    flat = torch.cat([p.detach().reshape(-1) for p in ref.parameters()])
+    for o in outs:
+        got = o["data"]
+        # compare parameter values at each slot (flat buffer is padded per tensor)
+        off, k = 0, 0
+        for p in ref.parameters():
+            n = p.numel()
+            torch.testing.assert_close(got[off:off + n], flat[k:k + n], rtol=1e-4, atol=1e-5)
+            off += (n + 63) // 64 * 64
+            k += n
+
+
+def test_parameter_server_async_applies_every_push():
+    world, port, steps = 3, _port(), 2
+    outs = _run(W.ps_rank, [(r, world, port, "dedicated", False, steps) for r in range(world)])
+    ps = [o for o in outs if o["is_ps"]][0]
+    init = torch.cat([p.detach().reshape(-1) for p in W._mlp(seed=0).parameters()])
+    assert not torch.allclose(ps["data"][:init.numel()], init)   # updates were applied
+    assert torch.isfinite(ps["data"]).all()
+
+
+def test_collectives_gloo():
+    world, port = 2, _port()
+    outs = _run(W.collectives_rank, [(r, world, port) for r in range(world)])
+    base = torch.arange(8, dtype=torch.float32)
+    for r, o in enumerate(outs):
+        exp = (2 * base + 1)[r * 4:(r + 1) * 4]
+        assert o["rs"] == exp.tolist()
+        assert o["ag"] == [0.0] * 4 + [1.0] * 4
+        assert o["max"] == 1.0
+
+
+@pytest.mark.parametrize("kind", ["dist_sync", "dist_async"])
+def test_kvstore_dist_scheduler_server_workers(kind):
+    port, steps = _port(), 3
+    args = [("scheduler", 0, 1, 2, port, kind, steps), ("server", 0, 1, 2, port, kind, steps),
+            ("worker", 0, 1, 2, port, kind, steps), ("worker", 1, 1, 2, port, kind, steps)]
+    outs = _run(W.kv_rank, args)
+    workers = [o for o in outs if o["role"] == "worker"]
+    assert sorted(o["rank"] for o in workers) == [0, 1] and workers[0]["n"] == 2
+    for o in workers:
+        assert o["k7"] == [1.0, 1.0]
+    if kind == "dist_sync":
+        # every round: grad = sum of pushes (1+2) * rescale 1/2 = 1.5 ; w -= 0.5*1.5
+        for o in workers:
+            for s, w in enumerate(o["seen"]):
+                torch.testing.assert_close(w, torch.full((3,), -0.75 * (s + 1)))
+    else:
+        # async: every push applied on arrival, w -= 0.5 * 0.5 * v; 3 pushes of 1 and 3 of 2 -> -2.25 after
+        # the globally last push, which the worker that made it sees on its last pull
+        final = min(float(o["seen"][-1][0]) for o in workers)
+        assert final == pytest.approx(-2.25)
+
+
+def test_kvstore_local_and_optimizer_state(tmp_path):
+    import tony_amd.kv as kv
+
+    s = kv.create("local")
+    s.init(3, torch.zeros(2))
+    s.push(3, [torch.ones(2), torch.ones(2)])       # multi-device push is summed
+    out = torch.empty(2)
+    s.pull(3, out=out)
+    assert out.tolist() == [2.0, 2.0]
+    s.set_optimizer(kv.create_optimizer("sgd", learning_rate=0.1, momentum=0.9))
+    s.push(3, torch.ones(2))
+    s.pull(3, out=out)
+    torch.testing.assert_close(out, torch.tensor([1.9, 1.9]))
+    s.save_optimizer_states(str(tmp_path / "opt.pt"))
+    s2 = kv.create("local")
+    s2.load_optimizer_states(str(tmp_path / "opt.pt"))
+    assert "mom" in s2._opt.state[3]

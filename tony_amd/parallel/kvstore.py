@@ -1,0 +1,497 @@
+"""MXNet-style key-value store (``mx.kv``) for jobs launched by TonY's mxnet runtime.
+
+TonY's mxnet runtime (T/runtime/MXNetRuntime.java:44-66) starts ``scheduler``,
+``server`` and ``worker`` tasks with ``DMLC_ROLE / DMLC_PS_ROOT_URI /
+DMLC_PS_ROOT_PORT / DMLC_NUM_SERVER / DMLC_NUM_WORKER``; the reference job
+(EX/linearregression-mxnet/src/mxnet_dist_ex.py:35,61-68) trains through
+``mx.kv.create('dist_async')``.  MXNet/ps-lite are not part of this stack, so
+this module implements the kvstore semantics itself:
+
+``local`` / ``device``
+    one process; ``push`` sums the pushed list, the updater (if set) runs on
+    the stored value, ``pull`` copies it out.
+``dist_sync``
+    servers own the keys (key id mod #servers).  A push round completes when
+    every worker has pushed a key; the server then applies the optimizer to
+    the *sum* (or stores the sum), and a worker's pull issued after its own
+    push waits for that round -- the BSP semantics of ps-lite's sync mode.
+``dist_async``
+    every push is applied on arrival; pulls return the current value.
+``dist_device_sync``
+    no servers in the data path: the workers all-reduce the pushed gradients
+    with RCCL (the xGMI path for GPU tensors) and run the same updater on
+    every worker (replicated, deterministic).
+
+Transport for the server modes: one torch.distributed (gloo) group over
+servers + workers; the scheduler task hosts its TCPStore on
+``DMLC_PS_ROOT_PORT`` and exits when every member has finished.  Requests are
+an int64 header ``[op, key, numel, dtype]`` followed by the payload.
+"""
+from __future__ import annotations
+
+import datetime
+import json
+import os
+import time
+from typing import Dict, List, Optional, Union
+
+import torch
+import torch.distributed as dist
+
+OP_INIT, OP_PUSH, OP_PULL, OP_OPT, OP_STOP = range(5)
+TAG_HDR, TAG_DATA, TAG_REPLY = 1, 2, 3
+_DTYPES = [torch.float32, torch.float16, torch.bfloat16, torch.float64, torch.int64, torch.int32, torch.uint8]
+_EXIT_KEY = "tony/kv/exited"
+
+
+def _dcode(dt: torch.dtype) -> int:
+    return _DTYPES.index(dt)
+
+
+# -- optimizers (server- or worker-side updater) -----------------------------------------------
+class Optimizer:
+    """``mx.optimizer`` subset: sgd (momentum, wd, rescale_grad, clip_gradient) and adam."""
+
+    def __init__(self, name: str = "sgd", learning_rate: float = 0.01, momentum: float = 0.0, wd: float = 0.0,
+                 rescale_grad: float = 1.0, clip_gradient: Optional[float] = None, beta1: float = 0.9,
+                 beta2: float = 0.999, epsilon: float = 1e-8):
+        self.name = name.lower()
+        if self.name not in ("sgd", "adam"):
+            raise ValueError(f"unsupported optimizer {name!r}")
+        self.cfg = dict(name=self.name, learning_rate=learning_rate, momentum=momentum, wd=wd,
+                        rescale_grad=rescale_grad, clip_gradient=clip_gradient, beta1=beta1, beta2=beta2,
+                        epsilon=epsilon)
+        self.state: Dict[int, dict] = {}
+
+    def to_json(self) -> str:
+        return json.dumps(self.cfg)
+
+    @classmethod
+    def from_json(cls, s: str) -> "Optimizer":
+        return cls(**json.loads(s))
+
+    def update(self, key: int, weight: torch.Tensor, grad: torch.Tensor) -> None:
+        c = self.cfg
+        g = grad.float() * c["rescale_grad"]
+        if c["clip_gradient"] is not None:
+            g.clamp_(-c["clip_gradient"], c["clip_gradient"])
+        w = weight if weight.dtype == torch.float32 else weight.float()
+        g.add_(w, alpha=c["wd"])
+        st = self.state.setdefault(key, {"t": 0})
+        lr = c["learning_rate"]
+        if self.name == "sgd":
+            if c["momentum"]:
+                m = st.setdefault("mom", torch.zeros_like(w))
+                m.mul_(c["momentum"]).add_(g, alpha=-lr)
+                w.add_(m)
+            else:
+                w.add_(g, alpha=-lr)
+        else:
+            st["t"] += 1
+            m = st.setdefault("m", torch.zeros_like(w))
+            v = st.setdefault("v", torch.zeros_like(w))
+            m.mul_(c["beta1"]).add_(g, alpha=1 - c["beta1"])
+            v.mul_(c["beta2"]).addcmul_(g, g, value=1 - c["beta2"])
+            t = st["t"]
+            lr_t = lr * (1 - c["beta2"] ** t) ** 0.5 / (1 - c["beta1"] ** t)
+            w.addcdiv_(m, v.sqrt().add_(c["epsilon"]), value=-lr_t)
+        if w is not weight:
+            weight.copy_(w)
+
+    def state_dict(self):
+        return {"cfg": self.cfg, "state": self.state}
+
+
+def create_optimizer(name: str = "sgd", **kw) -> Optimizer:
+    return Optimizer(name, **kw)
+
+
+def _as_list(v) -> List[torch.Tensor]:
+    return list(v) if isinstance(v, (list, tuple)) else [v]
+
+
+def _merge(vals: List[torch.Tensor]) -> torch.Tensor:
+    out = vals[0].detach().clone()
+    for v in vals[1:]:
+        out.add_(v.to(out.device))
+    return out
+
+
+class _KeyIds:
+    def __init__(self):
+        self.ids: Dict[object, int] = {}
+
+    def __call__(self, key) -> int:
+        if isinstance(key, int):
+            return key
+        if key not in self.ids:
+            self.ids[key] = len(self.ids) + (1 << 40)  # string keys live above int keys
+        return self.ids[key]
+
+
+# -- local ----------------------------------------------------------------------------------------
+class KVStore:
+    def __init__(self, kind: str = "local"):
+        self.type = kind
+        self._store: Dict[int, torch.Tensor] = {}
+        self._opt: Optional[Optimizer] = None
+        self._key = _KeyIds()
+
+    @property
+    def rank(self) -> int:
+        return 0
+
+    @property
+    def num_workers(self) -> int:
+        return 1
+
+    def _keys_vals(self, key, value):
+        if isinstance(key, (list, tuple)):
+            return list(key), list(value)
+        return [key], [value]
+
+    def init(self, key, value) -> None:
+        for k, v in zip(*self._keys_vals(key, value)):
+            self._store[self._key(k)] = _as_list(v)[0].detach().clone()
+
+    def push(self, key, value, priority: int = 0) -> None:  # noqa: ARG002
+        for k, v in zip(*self._keys_vals(key, value)):
+            kid = self._key(k)
+            g = _merge(_as_list(v))
+            self._apply(kid, g)
+
+    def _apply(self, kid: int, merged: torch.Tensor) -> None:
+        if kid not in self._store:
+            raise KeyError(f"key {kid} was not initialised")
+        if self._opt is not None:
+            self._opt.update(kid, self._store[kid], merged.to(self._store[kid].device))
+        else:
+            self._store[kid].copy_(merged)
+
+    def pull(self, key, out=None, priority: int = 0, ignore_sparse: bool = True):  # noqa: ARG002
+        keys, outs = self._keys_vals(key, out)
+        for k, o in zip(keys, outs):
+            src = self._store[self._key(k)]
+            for t in _as_list(o):
+                t.copy_(src.to(t.device))
+
+    def pushpull(self, key, value, out=None, priority: int = 0) -> None:
+        self.push(key, value, priority)
+        self.pull(key, out if out is not None else value, priority)
+
+    def set_optimizer(self, optimizer: Optimizer) -> None:
+        self._opt = optimizer
+
+    def set_gradient_compression(self, params: dict) -> None:
+        if params.get("type") not in (None, "none"):
+            raise NotImplementedError("gradient compression is not supported by this kvstore")
+
+    def barrier(self) -> None:
+        pass
+
+    def save_optimizer_states(self, fname: str, dump_optimizer: bool = False) -> None:  # noqa: ARG002
+        if self._opt is None:
+            raise RuntimeError("no optimizer set")
+        torch.save({"cfg": json.dumps(self._opt.cfg), "state": self._opt.state}, fname)
+
+    def load_optimizer_states(self, fname: str) -> None:
+        sd = torch.load(fname, weights_only=True)
+        self._opt = Optimizer.from_json(sd["cfg"])
+        self._opt.state = sd["state"]
+
+    def close(self) -> None:
+        pass
+
+
+# -- dist (servers) -------------------------------------------------------------------------------
+def _env_int(name: str, default: int) -> int:
+    try:
+        return int(os.environ.get(name, default))
+    except ValueError:
+        return default
+
+
+class _Topology:
+    def __init__(self):
+        e = os.environ
+        self.role = e.get("DMLC_ROLE", "worker")
+        self.num_servers = _env_int("DMLC_NUM_SERVER", 0)
+        self.num_workers = _env_int("DMLC_NUM_WORKER", 1)
+        self.root_uri = e.get("DMLC_PS_ROOT_URI", "127.0.0.1")
+        self.root_port = _env_int("DMLC_PS_ROOT_PORT", 0)
+        self.index = _env_int("TASK_INDEX", 0)
+
+    @property
+    def world(self) -> int:
+        return self.num_servers + self.num_workers
+
+    @property
+    def rank(self) -> int:
+        return self.index if self.role == "server" else self.num_servers + self.index
+
+    def server_of(self, kid: int) -> int:
+        return kid % self.num_servers
+
+
+def _connect(topo: _Topology, timeout_s: float = 1800.0) -> dist.TCPStore:
+    return dist.TCPStore(topo.root_uri, topo.root_port, topo.world + 1, False,
+                         timeout=datetime.timedelta(seconds=timeout_s))
+
+
+def _init_group(topo: _Topology):
+    store = _connect(topo)
+    if not dist.is_initialized():
+        dist.init_process_group("gloo", store=dist.PrefixStore("tony-kv", store), rank=topo.rank,
+                                world_size=topo.world)
+    workers = dist.new_group(list(range(topo.num_servers, topo.world)))
+    return store, workers
+
+
+def run_scheduler(poll_s: float = 0.05) -> int:
+    """The scheduler role: host the rendezvous store until every server and worker exited."""
+    topo = _Topology()
+    store = dist.TCPStore("0.0.0.0", topo.root_port, topo.world + 1, True,
+                          timeout=datetime.timedelta(seconds=1800), wait_for_workers=False)
+    while store.add(_EXIT_KEY, 0) < topo.world:
+        time.sleep(poll_s)
+    return 0
+
+
+class _Server:
+    def __init__(self, topo: _Topology, sync: bool):
+        self.topo = topo
+        self.sync = sync
+        self.values: Dict[int, torch.Tensor] = {}
+        self.accum: Dict[int, torch.Tensor] = {}
+        self.pushed: Dict[int, set] = {}
+        self.deferred: Dict[int, List[int]] = {}
+        self.opt: Optional[Optimizer] = None
+        self.early: Dict[int, list] = {}
+        self.sends = []
+        self.applied = 0
+
+    def _reply(self, kid: int, worker: int) -> None:
+        self.sends.append(dist.isend(self.values[kid].contiguous(), worker, tag=TAG_REPLY))
+
+    def _finish_round(self, kid: int) -> None:
+        merged = self.accum.pop(kid)
+        if self.opt is not None:
+            self.opt.update(kid, self.values[kid], merged)
+        else:
+            self.values[kid].copy_(merged)
+        self.applied += 1
+        self.pushed[kid] = set()
+        for w in self.deferred.pop(kid, []):
+            self._reply(kid, w)
+
+    def handle(self, worker: int, hdr: List[int], buf: Optional[torch.Tensor] = None) -> bool:
+        op, kid, numel, dcode = hdr
+        if op in (OP_INIT, OP_PUSH, OP_OPT) and buf is None:
+            buf = torch.empty(numel, dtype=_DTYPES[dcode])
+            dist.recv(buf, worker, tag=TAG_DATA)
+        if op in (OP_PUSH, OP_PULL) and kid not in self.values:
+            # raced ahead of worker 0's INIT (it is sent before the workers' barrier, but
+            # the server may poll this worker first): replay once the key exists
+            self.early.setdefault(kid, []).append((worker, hdr, buf))
+            return True
+        if op in (OP_INIT, OP_PUSH, OP_OPT):
+            if op == OP_INIT:
+                self.values[kid] = buf
+                self.pushed[kid] = set()
+                for w, h, b in self.early.pop(kid, []):
+                    self.handle(w, h, b)
+            elif op == OP_OPT:
+                self.opt = Optimizer.from_json(bytes(buf.tolist()).decode())
+            elif not self.sync:
+                self.accum[kid] = buf
+                self._finish_round(kid)
+            else:
+                acc = self.accum.get(kid)
+                self.accum[kid] = buf.to(self.values[kid].dtype) if acc is None else acc.add_(buf)
+                self.pushed[kid].add(worker)
+                if len(self.pushed[kid]) == self.topo.num_workers:
+                    self._finish_round(kid)
+        elif op == OP_PULL:
+            if self.sync and worker in self.pushed.get(kid, ()):
+                self.deferred.setdefault(kid, []).append(worker)
+            else:
+                self._reply(kid, worker)
+        elif op == OP_STOP:
+            return False
+        return True
+
+    def serve(self) -> None:
+        """Receive request headers from ANY worker (gloo recv-anysource) until all sent STOP."""
+        live = self.topo.num_workers
+        hdr = torch.empty(4, dtype=torch.int64)
+        while live:
+            w = dist.recv(hdr, tag=TAG_HDR)
+            if not self.handle(w, [int(x) for x in hdr.tolist()]):
+                live -= 1
+            if len(self.sends) > 64:
+                for s in self.sends:
+                    s.wait()
+                self.sends = []
+        for s in self.sends:
+            s.wait()
+
+
+def run_server(sync: Optional[bool] = None) -> int:
+    """The server role: own keys until every worker sent STOP."""
+    topo = _Topology()
+    store, _ = _init_group(topo)
+    if sync is None:  # every worker announces its kvstore type before its first request
+        sync = store.get("tony/kv/type").decode() != "dist_async"
+    _Server(topo, sync).serve()
+    dist.barrier()
+    store.add(_EXIT_KEY, 1)
+    return 0
+
+
+class DistKVStore(KVStore):
+    """Worker side of ``dist_sync`` / ``dist_async``."""
+
+    def __init__(self, kind: str):
+        super().__init__(kind)
+        self.topo = _Topology()
+        if self.topo.num_servers < 1:
+            raise ValueError(f"{kind} needs DMLC_NUM_SERVER >= 1 server task")
+        self.store, self.workers = _init_group(self.topo)
+        self.store.set("tony/kv/type", kind)
+        self._shapes: Dict[int, torch.Size] = {}
+        self._closed = False
+
+    @property
+    def rank(self) -> int:
+        return self.topo.index
+
+    @property
+    def num_workers(self) -> int:
+        return self.topo.num_workers
+
+    def _send(self, op: int, kid: int, payload: Optional[torch.Tensor] = None) -> int:
+        srv = self.topo.server_of(kid) if op != OP_STOP else kid
+        n, dc = (payload.numel(), _dcode(payload.dtype)) if payload is not None else (0, 0)
+        dist.send(torch.tensor([op, kid, n, dc], dtype=torch.int64), srv, tag=TAG_HDR)
+        if payload is not None:
+            dist.send(payload, srv, tag=TAG_DATA)
+        return srv
+
+    def init(self, key, value) -> None:
+        for k, v in zip(*self._keys_vals(key, value)):
+            kid = self._key(k)
+            t = _as_list(v)[0].detach()
+            self._shapes[kid] = t.shape
+            if self.rank == 0:
+                self._send(OP_INIT, kid, t.reshape(-1).cpu().contiguous())
+        self.barrier()
+
+    def push(self, key, value, priority: int = 0) -> None:  # noqa: ARG002
+        for k, v in zip(*self._keys_vals(key, value)):
+            kid = self._key(k)
+            self._send(OP_PUSH, kid, _merge(_as_list(v)).reshape(-1).cpu().contiguous())
+
+    def pull(self, key, out=None, priority: int = 0, ignore_sparse: bool = True):  # noqa: ARG002
+        keys, outs = self._keys_vals(key, out)
+        for k, o in zip(keys, outs):
+            kid = self._key(k)
+            first = _as_list(o)[0]
+            srv = self._send(OP_PULL, kid)
+            buf = torch.empty(first.numel(), dtype=first.dtype)
+            dist.recv(buf, srv, tag=TAG_REPLY)
+            for t in _as_list(o):
+                t.copy_(buf.view(t.shape).to(t.device))
+
+    def set_optimizer(self, optimizer: Optimizer) -> None:
+        """Ship the optimizer to every server (MXNet pickles it; here it is a JSON config)."""
+        if self.rank == 0:
+            payload = torch.tensor(list(optimizer.to_json().encode()), dtype=torch.uint8)
+            for s in range(self.topo.num_servers):
+                self._send_to(s, OP_OPT, payload)
+        self.barrier()
+
+    def _send_to(self, srv: int, op: int, payload: torch.Tensor) -> None:
+        dist.send(torch.tensor([op, srv, payload.numel(), _dcode(payload.dtype)], dtype=torch.int64), srv,
+                  tag=TAG_HDR)
+        dist.send(payload, srv, tag=TAG_DATA)
+
+    def barrier(self) -> None:
+        dist.barrier(group=self.workers)
+
+    def save_optimizer_states(self, fname: str, dump_optimizer: bool = False) -> None:
+        raise NotImplementedError("optimizer states live on the servers in dist modes")
+
+    def close(self) -> None:
+        """Tell every server this worker is done (MXNet does this at process exit)."""
+        if self._closed:
+            return
+        self._closed = True
+        self.barrier()
+        for s in range(self.topo.num_servers):
+            dist.send(torch.tensor([OP_STOP, s, 0, 0], dtype=torch.int64), s, tag=TAG_HDR)
+        dist.barrier()
+        self.store.add(_EXIT_KEY, 1)
+
+
+class DeviceSyncKVStore(KVStore):
+    """``dist_device_sync``: RCCL all-reduce of pushes among workers + replicated updater."""
+
+    def __init__(self, kind: str = "dist_device_sync", group=None):
+        super().__init__(kind)
+        if not dist.is_initialized():
+            from .bootstrap import init_from_env
+
+            init_from_env()
+        self.group = group
+
+    @property
+    def rank(self) -> int:
+        return dist.get_rank(self.group)
+
+    @property
+    def num_workers(self) -> int:
+        return dist.get_world_size(self.group)
+
+    def init(self, key, value) -> None:
+        for k, v in zip(*self._keys_vals(key, value)):
+            t = _as_list(v)[0].detach().clone()
+            dist.broadcast(t, 0, group=self.group)
+            self._store[self._key(k)] = t
+
+    def push(self, key, value, priority: int = 0) -> None:  # noqa: ARG002
+        for k, v in zip(*self._keys_vals(key, value)):
+            g = _merge(_as_list(v))
+            dist.all_reduce(g, group=self.group)
+            self._apply(self._key(k), g)
+
+    def barrier(self) -> None:
+        dist.barrier(group=self.group)
+
+
+def create(name: str = "local") -> KVStore:
+    name = name.lower()
+    if name in ("local", "device", "local_allreduce_cpu", "local_allreduce_device"):
+        return KVStore(name)
+    if name in ("dist_sync", "dist_async", "dist"):
+        return DistKVStore("dist_sync" if name == "dist" else name)
+    if name in ("dist_device_sync", "dist_sync_device"):
+        return DeviceSyncKVStore("dist_device_sync")
+    raise ValueError(f"unknown kvstore type {name!r}")
+
+
+def run_role() -> bool:
+    """Run the scheduler / server loop if this task is one; True when the caller should exit.
+
+    ``import mxnet`` does this implicitly for non-worker roles (mxnet_dist_ex.py:10-13).
+    """
+    role = os.environ.get("DMLC_ROLE", "worker")
+    if role == "scheduler":
+        run_scheduler()
+        return True
+    if role == "server":
+        run_server()
+        return True
+    return False
+
+
+Value = Union[torch.Tensor, List[torch.Tensor]]

@@ -142,9 +142,21 @@ class ParameterServer:
         f = self.flat
         opt = self.optimizers[0]
         opt.grad_scale = 1.0  # async: every push is applied on its own
+        if total_pushes % len(self.worker_ranks):
+            raise ValueError("total_pushes must be steps x number of workers")
+        per_worker = total_pushes // len(self.worker_ranks)
+        if coll._is_gloo(self.group):
+            # gloo cannot poll a pending irecv; it can receive from ANY source instead
+            buf = torch.empty_like(f.grad)
+            for done in range(total_pushes):
+                w = dist.recv(buf, group=self.group)  # returns the sender's global rank
+                opt.step(buf, out_bf16=f.data)
+                dist.send(f.data, dst=w, group=self.group)
+            self.steps = total_pushes
+            return
         bufs = {w: torch.empty_like(f.grad) for w in self.worker_ranks}
-        reqs = {w: dist.irecv(bufs[w], src=w, group=self.group) for w in self.worker_ranks}
-        outstanding = len(reqs)
+        got = {w: 0 for w in self.worker_ranks}
+        reqs = {w: dist.irecv(bufs[w], src=w, group=self.group) if per_worker else None for w in self.worker_ranks}
         done = 0
         while done < total_pushes:
             progressed = False
@@ -152,16 +164,13 @@ class ParameterServer:
                 if req is None or not req.is_completed():
                     continue
                 req.wait()
-                outstanding -= 1
                 opt.step(bufs[w], out_bf16=f.data)          # apply on arrival
                 dist.send(f.data, dst=w, group=self.group)  # the worker's pull
                 done += 1
+                got[w] += 1
                 progressed = True
-                if done + outstanding < total_pushes:
-                    reqs[w] = dist.irecv(bufs[w], src=w, group=self.group)
-                    outstanding += 1
-                else:
-                    reqs[w] = None
+                # each worker pushes exactly per_worker times: repost only for its own next push
+                reqs[w] = dist.irecv(bufs[w], src=w, group=self.group) if got[w] < per_worker else None
             if not progressed:
                 time.sleep(poll_s)
         self.steps = done
