@@ -1,0 +1,87 @@
+"""ResNet-50 (v1.5) for the horovod-on-tony config (BASELINE.json: "ResNet-50 ring-allreduce bf16
+on 8xMI355X"), NHWC / bf16, built from tony_amd's fused ops.
+
+Bottleneck schedule with ``fused=True`` (the default on the GPU):
+
+conv1  1x1 s1      MFMA GEMM with BN statistics in the epilogue + fused BN/ReLU apply
+conv2  3x3 s1|s2   MIOpen implicit GEMM -> fused BN+ReLU kernel
+conv3  1x1 s1      MFMA GEMM (+stats) -> ONE pass: BN apply + identity add + ReLU
+                   (ops/residual.py); its backward writes d(conv3 out) and
+                   d(identity) in the same pass
+downsample         1x1 s1|s2 conv (MIOpen) -> fused BN (no ReLU)
+
+Architecture: torchvision's resnet50 (stride on the 3x3, "v1.5"); layer
+widths 64/128/256/512 x4, blocks [3, 4, 6, 3], 7x7/s2 stem + 3x3/s2 max pool,
+global average pool, 1000-way FC.  ``fused=False`` is the stock PyTorch
+module graph (the comparator and the CPU path).
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from ..ops.bn import BatchNormAct2d
+from ..ops.residual import bn_add_relu, conv1x1_bn_add_relu
+from .layers import ConvBNAct, init_weights
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin, width, stride=1, fused=True, eps=1e-5):
+        super().__init__()
+        cout = width * self.expansion
+        self.fused = fused
+        self.conv1 = ConvBNAct(cin, width, 1, fused=fused, eps=eps)
+        self.conv2 = ConvBNAct(width, width, 3, stride=stride, padding=1, fused=fused, eps=eps)
+        self.conv3 = nn.Conv2d(width, cout, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(cout, eps=eps)
+        self.downsample = None
+        if stride != 1 or cin != cout:
+            self.downsample = nn.Sequential(
+                nn.Conv2d(cin, cout, 1, stride=stride, bias=False),
+                BatchNormAct2d(cout, eps=eps, relu=False) if fused else nn.BatchNorm2d(cout, eps=eps))
+
+    def forward(self, x):
+        identity = self.downsample(x) if self.downsample is not None else x
+        out = self.conv2(self.conv1(x))
+        bn = self.bn3
+        if self.fused and out.is_cuda:
+            return conv1x1_bn_add_relu(out, self.conv3.weight, identity, bn.weight, bn.bias, bn.running_mean,
+                                       bn.running_var, self.training, bn.momentum, bn.eps)
+        if self.fused:
+            return bn_add_relu(self.conv3(out), identity, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                               self.training, bn.momentum, bn.eps)
+        return torch.relu(bn(self.conv3(out)) + identity)
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, fused=True, eps=1e-5):
+        super().__init__()
+        self.fused = fused
+        self.stem = ConvBNAct(3, 64, 7, stride=2, padding=3, fused=fused, eps=eps)
+        blocks = []
+        cin = 64
+        for i, n in enumerate(layers):
+            width = 64 * 2 ** i
+            for j in range(n):
+                blocks.append(Bottleneck(cin, width, stride=2 if (j == 0 and i > 0) else 1, fused=fused, eps=eps))
+                cin = width * Bottleneck.expansion
+        self.blocks = nn.Sequential(*blocks)
+        self.fc = nn.Linear(cin, num_classes)
+
+    def forward(self, x):
+        x = self.stem(x)
+        x = torch.nn.functional.max_pool2d(x, 3, 2, 1)
+        x = self.blocks(x)
+        x = x.mean((2, 3))
+        return self.fc(x)
+
+
+def resnet50(num_classes: int = 1000, fused: bool = True, seed: int = 0) -> ResNet:
+    m = ResNet((3, 4, 6, 3), num_classes, fused=fused)
+    init_weights(m, seed)
+    # zero-init the last BN gamma of each block (standard large-batch ResNet recipe)
+    for b in m.blocks:
+        nn.init.zeros_(b.bn3.weight)
+    return m

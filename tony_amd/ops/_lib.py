@@ -43,6 +43,12 @@ _SIGNATURES = {
     "tony_bn_bwd_apply": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p,
                           c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_int, c_void_p],
+    "tony_bn_apply_res": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
+                          c_void_p, c_void_p, c_void_p, c_int, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                          c_void_p, c_float, c_void_p],
+    "tony_bn_bwd_res": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
+                        c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+                        c_int, c_void_p],
     "tony_add_f32": [c_void_p, c_int, c_void_p, c_int64, c_void_p],
     "tony_sgd_step": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p],
     "tony_adam_step": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p],

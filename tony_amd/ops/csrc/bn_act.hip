@@ -121,8 +121,11 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_stats_kernel(
 
 // mode 0: training (stats from sums, saves mean/invstd, updates running stats)
 // mode 1: inference (stats from running_mean / running_var)
+// RES: y = act(bn(x) + res)  (ResNet bottleneck tail: BN + identity add + ReLU in one pass)
+template <bool RES>
 __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
     const uint16_t* __restrict__ x, int64_t M, int C, int64_t ldx, int64_t rows_per_block,
+    const uint16_t* __restrict__ res, int64_t ldr,
     uint16_t* __restrict__ y, int64_t ldy, const float* __restrict__ sum, const float* __restrict__ sumsq,
     const void* gamma, const void* beta, int param_bf16, float eps, int relu, int mode,
     float* __restrict__ save_mean, float* __restrict__ save_invstd,
@@ -167,30 +170,40 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
   const int64_t r1 = min(M, r0 + rows_per_block);
   const int64_t step = rm.RPI;
   int64_t r = r0 + rm.rsub;
-  auto body = [&](const bf16x8& v, int64_t row) {
-    float f[8];
+  auto body = [&](const bf16x8& v, const bf16x8& rv, int64_t row) {
+    float f[8], q[8];
     v.to_float(f);
+    if (RES) rv.to_float(q);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float t = fmaf(f[j], sc[j], sh[j]);
+      if (RES) t += q[j];
       f[j] = relu ? fmaxf(t, 0.f) : t;
     }
     store8(y + row * ldy + rm.cg * 8, bf16x8::from_float(f));
   };
+  bf16x8 none{};
   for (; r + 3 * step < r1; r += 4 * step) {
-    bf16x8 v[4];
+    bf16x8 v[4], rv[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = load8(x + (r + u * step) * ldx + rm.cg * 8);
+    for (int u = 0; u < 4; ++u) {
+      v[u] = load8(x + (r + u * step) * ldx + rm.cg * 8);
+      if (RES) rv[u] = load8(res + (r + u * step) * ldr + rm.cg * 8);
+    }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) body(v[u], r + u * step);
+    for (int u = 0; u < 4; ++u) body(v[u], RES ? rv[u] : none, r + u * step);
   }
-  for (; r < r1; r += step) body(load8(x + r * ldx + rm.cg * 8), r);
+  for (; r < r1; r += step)
+    body(load8(x + r * ldx + rm.cg * 8), RES ? load8(res + r * ldr + rm.cg * 8) : none, r);
 }
 
 // Backward reduction: dsums[c] = sum(dy'), dsums[C+c] = sum(dy' * xhat),
-// where dy' = dy masked by the ReLU (recomputed from x).
+// where dy' = dy masked by the ReLU (recomputed from x), or -- YMASK, the
+// residual form where the ReLU followed an add -- masked by the saved output y.
+template <bool YMASK>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __restrict__ dy, int64_t lddy,
+    const uint16_t* __restrict__ ym, int64_t ldym,
     int64_t M, int C, int64_t rows_per_block, const float* __restrict__ mean,
     const float* __restrict__ invstd, const void* gamma, const void* beta, int param_bf16,
     int relu, float* __restrict__ dsum, float* __restrict__ dsumx) {
@@ -213,37 +226,50 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
     const int64_t r1 = min(M, r0 + rows_per_block);
     const int64_t step = rm.RPI;
-    auto body = [&](const bf16x8& xv, const bf16x8& gv) {
-      float xf[8], gf[8];
+    auto body = [&](const bf16x8& xv, const bf16x8& gv, const bf16x8& yv) {
+      float xf[8], gf[8], yf[8];
       xv.to_float(xf);
       gv.to_float(gf);
+      if (YMASK) yv.to_float(yf);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float xh = (xf[j] - mu[j]) * is[j];
         float d = gf[j];
-        if (relu && fmaf(xh, sc[j], sh[j]) <= 0.f) d = 0.f;
+        if (YMASK) {
+          if (yf[j] <= 0.f) d = 0.f;
+        } else if (relu && fmaf(xh, sc[j], sh[j]) <= 0.f) {
+          d = 0.f;
+        }
         a[j] += d;
         b[j] = fmaf(d, xh, b[j]);
       }
     };
+    bf16x8 none{};
     int64_t r = r0 + rm.rsub;
     for (; r + 3 * step < r1; r += 4 * step) {
-      bf16x8 xv[4], gv[4];
+      bf16x8 xv[4], gv[4], yv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         xv[u] = load8(x + (r + u * step) * ldx + rm.cg * 8);
         gv[u] = load8(dy + (r + u * step) * lddy + rm.cg * 8);
+        if (YMASK) yv[u] = load8(ym + (r + u * step) * ldym + rm.cg * 8);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) body(xv[u], gv[u]);
+      for (int u = 0; u < 4; ++u) body(xv[u], gv[u], YMASK ? yv[u] : none);
     }
-    for (; r < r1; r += step) body(load8(x + r * ldx + rm.cg * 8), load8(dy + r * lddy + rm.cg * 8));
+    for (; r < r1; r += step)
+      body(load8(x + r * ldx + rm.cg * 8), load8(dy + r * lddy + rm.cg * 8),
+           YMASK ? load8(ym + r * ldym + rm.cg * 8) : none);
   }
   block_reduce_add(red, rm, C, a, b, dsum, dsumx);
 }
 
+// YMASK: mask dy by the saved output y and also write the masked dy -- the
+// gradient of the residual branch -- to dres (when non-null).
+template <bool YMASK>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __restrict__ dy, int64_t lddy,
+    const uint16_t* __restrict__ ym, int64_t ldym, uint16_t* __restrict__ dres, int64_t lddr,
     uint16_t* __restrict__ dx, int64_t lddx, int64_t M, int C, int64_t rows_per_block,
     const float* __restrict__ mean, const float* __restrict__ invstd, const void* gamma,
     const void* beta, int param_bf16, int relu, const float* __restrict__ dsum,
@@ -278,31 +304,42 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
   const int64_t r1 = min(M, r0 + rows_per_block);
   const int64_t step = rm.RPI;
-  auto body = [&](const bf16x8& xv, const bf16x8& gv, int64_t row) {
-    float xf[8], gf[8], o[8];
+  auto body = [&](const bf16x8& xv, const bf16x8& gv, const bf16x8& yv, int64_t row) {
+    float xf[8], gf[8], yf[8], o[8];
     xv.to_float(xf);
     gv.to_float(gf);
+    if (YMASK) yv.to_float(yf);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float xh = (xf[j] - mu[j]) * is[j];
       float d = gf[j];
-      if (relu && fmaf(xh, g[j], be[j]) <= 0.f) d = 0.f;
+      if (YMASK) {
+        if (yf[j] <= 0.f) d = 0.f;
+        gf[j] = d;
+      } else if (relu && fmaf(xh, g[j], be[j]) <= 0.f) {
+        d = 0.f;
+      }
       o[j] = k[j] * (d - am[j] - xh * bm[j]);
     }
     store8(dx + row * lddx + rm.cg * 8, bf16x8::from_float(o));
+    if (YMASK && dres != nullptr) store8(dres + row * lddr + rm.cg * 8, bf16x8::from_float(gf));
   };
+  bf16x8 none{};
   int64_t r = r0 + rm.rsub;
   for (; r + 3 * step < r1; r += 4 * step) {
-    bf16x8 xv[4], gv[4];
+    bf16x8 xv[4], gv[4], yv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       xv[u] = load8(x + (r + u * step) * ldx + rm.cg * 8);
       gv[u] = load8(dy + (r + u * step) * lddy + rm.cg * 8);
+      if (YMASK) yv[u] = load8(ym + (r + u * step) * ldym + rm.cg * 8);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) body(xv[u], gv[u], r + u * step);
+    for (int u = 0; u < 4; ++u) body(xv[u], gv[u], YMASK ? yv[u] : none, r + u * step);
   }
-  for (; r < r1; r += step) body(load8(x + r * ldx + rm.cg * 8), load8(dy + r * lddy + rm.cg * 8), r);
+  for (; r < r1; r += step)
+    body(load8(x + r * ldx + rm.cg * 8), load8(dy + r * lddy + rm.cg * 8),
+         YMASK ? load8(ym + r * ldym + rm.cg * 8) : none, r);
 }
 
 // Grid sizing: enough workgroups to cover 256 CUs several times over, but each
@@ -353,9 +390,26 @@ TONY_API int tony_bn_apply(const void* x, int64_t M, int C, int64_t ldx, void* y
   int64_t rpb;
   int grid;
   plan_rows(M, C, 4, 8192, &rpb, &grid);
-  bn_fwd_apply_kernel<<<grid, kThreads, 0, stream>>>(
-      static_cast<const uint16_t*>(x), M, C, ldx, rpb, static_cast<uint16_t*>(y), ldy, sum, sumsq, gamma, beta,
-      param_bf16, eps, relu, mode, save_mean, save_invstd, running_mean, running_var, momentum);
+  bn_fwd_apply_kernel<false><<<grid, kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), M, C, ldx, rpb, nullptr, 0, static_cast<uint16_t*>(y), ldy, sum, sumsq,
+      gamma, beta, param_bf16, eps, relu, mode, save_mean, save_invstd, running_mean, running_var, momentum);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// y = act(bn(x) + res): the bottleneck tail (conv3 -> BN -> + identity -> ReLU) in one pass.
+TONY_API int tony_bn_apply_res(const void* x, int64_t M, int C, int64_t ldx, const void* res, int64_t ldr, void* y,
+                               int64_t ldy, const float* sum, const float* sumsq, const void* gamma, const void* beta,
+                               int param_bf16, float eps, int relu, int mode, float* save_mean, float* save_invstd,
+                               float* running_mean, float* running_var, float momentum, hipStream_t stream) {
+  if (bad_c(C) || (ldx % 8) || (ldy % 8) || (ldr % 8) || res == nullptr) return -1;
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 4, 8192, &rpb, &grid);
+  bn_fwd_apply_kernel<true><<<grid, kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), M, C, ldx, rpb, static_cast<const uint16_t*>(res), ldr,
+      static_cast<uint16_t*>(y), ldy, sum, sumsq, gamma, beta, param_bf16, eps, relu, mode, save_mean, save_invstd,
+      running_mean, running_var, momentum);
   TONY_LAUNCH_CHECK();
   return 0;
 }
@@ -373,9 +427,9 @@ TONY_API int tony_bn_bwd_reduce(const void* x, int64_t ldx, const void* dy, int6
   int64_t rpb;
   int grid;
   plan_rows(M, C, 8, 512, &rpb, &grid);  // few WGs: C atomics per WG contend per channel
-  bn_bwd_reduce_kernel<<<grid, kThreads, 0, stream>>>(
-      static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, M, C, rpb, mean, invstd, gamma,
-      beta, param_bf16, relu, dsum, dsumx);
+  bn_bwd_reduce_kernel<false><<<grid, kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, nullptr, 0, M, C, rpb, mean,
+      invstd, gamma, beta, param_bf16, relu, dsum, dsumx);
   TONY_LAUNCH_CHECK();
   return 0;
 }
@@ -388,9 +442,10 @@ TONY_API int tony_bn_bwd_apply(const void* x, int64_t ldx, const void* dy, int64
   int64_t rpb;
   int grid;
   plan_rows(M, C, 4, 8192, &rpb, &grid);
-  bn_bwd_apply_kernel<<<grid, kThreads, 0, stream>>>(
-      static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, static_cast<uint16_t*>(dx), lddx,
-      M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsum, dsumx, dgamma, dbeta, accumulate);
+  bn_bwd_apply_kernel<false><<<grid, kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, nullptr, 0, nullptr, 0,
+      static_cast<uint16_t*>(dx), lddx, M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsum, dsumx, dgamma,
+      dbeta, accumulate);
   TONY_LAUNCH_CHECK();
   return 0;
 }
@@ -425,4 +480,27 @@ TONY_API int tony_bn_bwd(const void* x, int64_t ldx, const void* dy, int64_t ldd
   if (rc) return rc;
   return tony_bn_bwd_apply(x, ldx, dy, lddy, dx, lddx, M, C, mean, invstd, gamma, beta, param_bf16, relu, dsums_ws,
                            dsums_ws + C, dgamma, dbeta, accumulate, stream);
+}
+
+// Backward of y = relu(bn(x) + res): dy' = dy * (y > 0); dres = dy' (if dres != null); dx = bn_bwd(dy').
+TONY_API int tony_bn_bwd_res(const void* x, int64_t ldx, const void* dy, int64_t lddy, const void* y, int64_t ldy,
+                             void* dx, int64_t lddx, void* dres, int64_t lddr, int64_t M, int C, const float* mean,
+                             const float* invstd, const void* gamma, const void* beta, int param_bf16,
+                             float* dsums_ws, void* dgamma, void* dbeta, int accumulate, hipStream_t stream) {
+  if (bad_c(C) || (ldx % 8) || (lddy % 8) || (ldy % 8) || (lddx % 8) || (lddr % 8) || y == nullptr) return -1;
+  (void)hipMemsetAsync(dsums_ws, 0, sizeof(float) * 2 * C, stream);
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 8, 512, &rpb, &grid);
+  bn_bwd_reduce_kernel<true><<<grid, kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, static_cast<const uint16_t*>(y),
+      ldy, M, C, rpb, mean, invstd, gamma, beta, param_bf16, 1, dsums_ws, dsums_ws + C);
+  TONY_LAUNCH_CHECK();
+  plan_rows(M, C, 4, 8192, &rpb, &grid);
+  bn_bwd_apply_kernel<true><<<grid, kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, static_cast<const uint16_t*>(y),
+      ldy, static_cast<uint16_t*>(dres), lddr, static_cast<uint16_t*>(dx), lddx, M, C, rpb, mean, invstd, gamma, beta,
+      param_bf16, 1, dsums_ws, dsums_ws + C, dgamma, dbeta, accumulate);
+  TONY_LAUNCH_CHECK();
+  return 0;
 }

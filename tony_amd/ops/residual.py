@@ -1,0 +1,175 @@
+"""BN + residual add + ReLU in one pass (the ResNet bottleneck tail), optionally behind a 1x1 MFMA GEMM.
+
+``y = relu(bn(z) + identity)`` is three memory passes in the textbook graph
+(BN apply, add, ReLU) plus their three backward passes.  Here:
+
+forward   stats(z) [from the GEMM epilogue when z comes from the fused 1x1 conv]
+          -> ONE apply pass reading z and identity, writing y
+backward  ONE reduce pass (dy masked by y > 0, sums for dgamma/dbeta) and ONE
+          apply pass writing both dz and d(identity) = dy * (y > 0)
+
+``conv1x1_bn_add_relu`` fuses the bottleneck's conv3 as well: Z = x . W^T with
+the BN statistics in the GEMM epilogue (csrc/gemm.hip), the backward-data GEMM
+and split-K wgrad GEMM of ops/fused.py, and parameter gradients accumulated in
+place into the flat gradient buffer when the trainer enabled it.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .bn import _as_rows, _empty_like_rows, _rows_view
+from .fused import _cl_empty
+from .gemm import wgrad_tn
+
+_BF16 = torch.bfloat16
+
+
+def _bn_stats_and_apply(L, z, ldz, M, C, res, ldr, y, ldy, gamma, beta, pb, eps, training, momentum, running_mean,
+                        running_var, stats, stream):
+    dev = z.device
+    if training:
+        mean = torch.empty(C, dtype=torch.float32, device=dev)
+        invstd = torch.empty(C, dtype=torch.float32, device=dev)
+    else:
+        mean = running_mean
+        invstd = torch.rsqrt(running_var.float() + eps)
+    rc = L.tony_bn_apply_res(z.data_ptr(), M, C, ldz, res.data_ptr(), ldr, y.data_ptr(), ldy,
+                             _lib.ptr(stats) if training else 0, _lib.ptr(stats) + 4 * C if training else 0,
+                             _lib.ptr(gamma), _lib.ptr(beta), pb, float(eps), 1, 0 if training else 1,
+                             _lib.ptr(mean) if training else 0, _lib.ptr(invstd) if training else 0,
+                             _lib.ptr(running_mean), _lib.ptr(running_var), float(momentum), stream)
+    _lib.check(rc, "tony_bn_apply_res")
+    return mean, invstd
+
+
+def _bwd_res(L, z, ldz, dy, y, M, C, mean, invstd, gamma, beta, pb, params, stream, want_dres=True):
+    dev = z.device
+    dy, (_, _, lddy) = _as_rows(dy)
+    _, _, ldy = _rows_view(y)
+    dz = _empty_like_rows(y)
+    _, _, lddz = _rows_view(dz)
+    dres = _empty_like_rows(y) if want_dres else None
+    ws = torch.empty(2 * C, dtype=torch.float32, device=dev)
+    gg, gb = _lib.grad_slot(params[0]), _lib.grad_slot(params[1])
+    inplace = gg is not None and gb is not None
+    dgamma = gg if inplace else torch.empty_like(gamma)
+    dbeta = gb if inplace else torch.empty_like(beta)
+    rc = L.tony_bn_bwd_res(z.data_ptr(), ldz, dy.data_ptr(), lddy, y.data_ptr(), ldy, dz.data_ptr(), lddz,
+                           _lib.ptr(dres), lddz, M, C, mean.data_ptr(), invstd.data_ptr(), _lib.ptr(gamma),
+                           _lib.ptr(beta), pb, ws.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), int(inplace),
+                           stream)
+    _lib.check(rc, "tony_bn_bwd_res")
+    return dz, dres, (None, None) if inplace else (dgamma, dbeta)
+
+
+class _BNAddReLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, res, gamma, beta, running_mean, running_var, training, momentum, eps):
+        L = _lib.lib()
+        stream = _lib.stream_ptr(z.device)
+        z, (M, C, ldz) = _as_rows(z)
+        res, (_, _, ldr) = _as_rows(res)
+        y = _empty_like_rows(z)
+        _, _, ldy = _rows_view(y)
+        pb = int(gamma.dtype == _BF16)
+        stats = None
+        if training:
+            stats = torch.empty(2 * C, dtype=torch.float32, device=z.device)
+            rc = L.tony_bn_stats(z.data_ptr(), M, C, ldz, stats.data_ptr(), stats.data_ptr() + 4 * C, stream)
+            _lib.check(rc, "tony_bn_stats")
+        mean, invstd = _bn_stats_and_apply(L, z, ldz, M, C, res, ldr, y, ldy, gamma, beta, pb, eps, training,
+                                           momentum, running_mean, running_var, stats, stream)
+        ctx.save_for_backward(z, y, gamma, beta, mean, invstd)
+        ctx.params = (gamma, beta)
+        ctx.pb = pb
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = _lib.lib()
+        z, y, gamma, beta, mean, invstd = ctx.saved_tensors
+        M, C, ldz = _rows_view(z)
+        dz, dres, (dg, db) = _bwd_res(L, z, ldz, dy, y, M, C, mean, invstd, gamma, beta, ctx.pb, ctx.params,
+                                      _lib.stream_ptr(z.device))
+        return dz, dres, dg, db, None, None, None, None, None
+
+
+class _Conv1x1BNAddReLUFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, res, gamma, beta, running_mean, running_var, training, momentum, eps):
+        L = _lib.lib()
+        dev = x.device
+        stream = _lib.stream_ptr(dev)
+        x, (M, cin, ldx) = _as_rows(x)
+        res, (_, _, ldr) = _as_rows(res)
+        n, _, h, w = x.shape
+        cout = weight.shape[0]
+        w2 = weight.reshape(cout, cin)
+        if w2.stride(0) != cin or w2.stride(1) != 1:
+            w2 = w2.contiguous()
+        Z = _cl_empty(n, cout, h, w, dev)
+        stats = torch.empty(2 * cout, dtype=torch.float32, device=dev)
+        rc = L.tony_gemm_bf16(x.data_ptr(), w2.data_ptr(), Z.data_ptr(), M, cout, cin, ldx, cin, cout,
+                              1 if training else 0, stats.data_ptr(), stream)
+        _lib.check(rc, "tony_gemm_bf16")
+        y = _cl_empty(n, cout, h, w, dev)
+        pb = int(gamma.dtype == _BF16)
+        mean, invstd = _bn_stats_and_apply(L, Z, cout, M, cout, res, ldr, y, cout, gamma, beta, pb, eps, training,
+                                           momentum, running_mean, running_var, stats, stream)
+        ctx.save_for_backward(x, weight, Z, y, gamma, beta, mean, invstd)
+        ctx.params = (weight, gamma, beta)
+        ctx.pb = pb
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = _lib.lib()
+        x, weight, Z, y, gamma, beta, mean, invstd = ctx.saved_tensors
+        dev = x.device
+        stream = _lib.stream_ptr(dev)
+        M, cin, ldx = _rows_view(x)
+        n, _, h, w = x.shape
+        cout = weight.shape[0]
+        dZ, dres, (dg, db) = _bwd_res(L, Z, cout, dy, y, M, cout, mean, invstd, gamma, beta, ctx.pb, ctx.params[1:],
+                                      stream)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wt = weight.reshape(cout, cin).t().contiguous()
+            dx = _cl_empty(n, cin, h, w, dev)
+            rc = L.tony_gemm_bf16(dZ.data_ptr(), wt.data_ptr(), dx.data_ptr(), M, cin, cout, cout, cout, cin, 0, 0,
+                                  stream)
+            _lib.check(rc, "tony_gemm_bf16")
+        dw32 = wgrad_tn(dZ.data_ptr(), cout, x.data_ptr(), ldx, M, cout, cin, dev)
+        gw = _lib.grad_slot(ctx.params[0])
+        if gw is not None and dg is None:
+            rc = L.tony_add_f32(gw.data_ptr(), int(gw.dtype == _BF16), dw32.data_ptr(), dw32.numel(), stream)
+            _lib.check(rc, "tony_add_f32")
+            dw = None
+        else:
+            dw = dw32.to(weight.dtype).reshape(weight.shape)
+        return dx, dw, dres, dg, db, None, None, None, None, None
+
+
+def bn_add_relu_reference(z, res, gamma, beta, running_mean, running_var, training, momentum, eps):
+    return torch.relu(torch.nn.functional.batch_norm(z, running_mean, running_var, gamma, beta, training, momentum,
+                                                     eps) + res)
+
+
+def bn_add_relu(z, res, gamma, beta, running_mean, running_var, training=True, momentum=0.1, eps=1e-5):
+    if z.is_cuda:
+        if z.dtype != _BF16:
+            raise TypeError("bn_add_relu HIP kernel takes bf16 activations")
+        return _BNAddReLUFn.apply(z, res, gamma, beta, running_mean, running_var, training, momentum, eps)
+    return bn_add_relu_reference(z, res, gamma, beta, running_mean, running_var, training, momentum, eps)
+
+
+def conv1x1_bn_add_relu(x, weight, res, gamma, beta, running_mean, running_var, training=True, momentum=0.1,
+                        eps=1e-5):
+    if x.is_cuda:
+        if x.dtype != _BF16:
+            raise TypeError("conv1x1_bn_add_relu HIP path takes bf16 activations")
+        return _Conv1x1BNAddReLUFn.apply(x, weight, res, gamma, beta, running_mean, running_var, training, momentum,
+                                         eps)
+    z = torch.nn.functional.conv2d(x, weight)
+    return bn_add_relu_reference(z, res, gamma, beta, running_mean, running_var, training, momentum, eps)
