@@ -331,7 +331,11 @@ def test_bn_add_relu_residual(cuda, shape, conv):
         x = _nhwc(torch.randn(n, cin, h, w, device=cuda)).to(torch.bfloat16)
         wt = (torch.randn(c, cin, 1, 1, device=cuda) / cin ** 0.5).to(torch.bfloat16)
         xr, wr = x.float().requires_grad_(True), wt.float().requires_grad_(True)
-        zr = torch.nn.functional.conv2d(xr, wr)
+        z32 = torch.nn.functional.conv2d(xr, wr)
+        # the kernel keeps Z in bf16 but takes the BN statistics from the fp32 GEMM accumulators
+        # (epilogue): build the reference the same way, otherwise ReLU masks of near-zero
+        # pre-activations flip and each flip smears into all Cin outputs of its pixel
+        zr = z32 + (z32.to(torch.bfloat16).float() - z32).detach()
         xk, wk = x.detach().requires_grad_(True), wt.detach().requires_grad_(True)
     else:
         z = _nhwc(torch.randn(shape, device=cuda) * 2 + 0.3).to(torch.bfloat16)
@@ -339,7 +343,14 @@ def test_bn_add_relu_residual(cuda, shape, conv):
         zk = z.detach().requires_grad_(True)
     resr = res.float().requires_grad_(True)
     gr, br = gamma.float().requires_grad_(True), beta.float().requires_grad_(True)
-    yr = torch.relu(torch.nn.functional.batch_norm(zr, rm_r, rv_r, gr, br, True, 0.1, 1e-5) + resr)
+    if conv:
+        mu = z32.mean((0, 2, 3), keepdim=True)
+        var = z32.var((0, 2, 3), unbiased=False, keepdim=True)
+        with torch.no_grad():
+            torch.nn.functional.batch_norm(z32, rm_r, rv_r, None, None, True, 0.1, 1e-5)
+        yr = torch.relu((zr - mu) * torch.rsqrt(var + 1e-5) * gr.view(1, -1, 1, 1) + br.view(1, -1, 1, 1) + resr)
+    else:
+        yr = torch.relu(torch.nn.functional.batch_norm(zr, rm_r, rv_r, gr, br, True, 0.1, 1e-5) + resr)
     resk = res.detach().requires_grad_(True)
     gk, bk = gamma.detach().requires_grad_(True), beta.detach().requires_grad_(True)
     if conv:

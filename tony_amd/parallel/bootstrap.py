@@ -17,7 +17,6 @@ from __future__ import annotations
 
 import datetime
 import os
-import socket
 import time
 from typing import Optional
 
@@ -45,7 +44,8 @@ def pick_device(local_rank: int) -> torch.device:
 
 
 def _advertised_host() -> str:
-    return os.environ.get("TONY_ADVERTISE_HOST") or socket.gethostname()
+    # same rule as the coordinator's cluster spec (utils.core.current_host): loopback on one node
+    return os.environ.get("TONY_ADVERTISE_HOST") or os.environ.get("TONY_HOST", "127.0.0.1")
 
 
 def store_via_kv(kv_addr: str, kv_port: int, rank: int, world: int, key: str = "tony/torch-store",
@@ -117,6 +117,20 @@ def init_from_env(backend: Optional[str] = None):
         store = dist.HashStore()
     dev = init_process_group(rank, world, store=store, backend=backend, local_rank=local)
     return rank, world, local, dev
+
+
+def init_from_tf_config(tc, backend: Optional[str] = None):
+    """Group over ``tc``'s rank table (see TFConfig.without_ps).  Returns (rank, world, device)."""
+    rank, world = tc.rank, tc.world
+    if rank < 0:
+        raise ValueError(f"{tc.task_type}:{tc.task_index} is not a member of the training group")
+    store = dist.HashStore()
+    if world > 1:
+        host, port = tc.master_address
+        store = dist.TCPStore(host if rank else "0.0.0.0", port, world, rank == 0, timeout=DEFAULT_TIMEOUT,
+                              wait_for_workers=False)
+    dev = init_process_group(rank, world, store=store, backend=backend, local_rank=tc.local_rank)
+    return rank, world, dev
 
 
 def wait_for(predicate, timeout_s: float, poll_s: float = 0.01) -> bool:

@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import json
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field, replace
 from typing import Dict, List, Tuple
 
 RANK_ORDER = ("chief", "master", "worker", "ps")
@@ -28,6 +28,11 @@ class TFConfig:
     cluster: Dict[str, List[str]]
     task_type: str
     task_index: int
+    roles: Tuple[str, ...] = field(default=RANK_ORDER)
+
+    def without_ps(self) -> "TFConfig":
+        """Rank table of the training tasks only (colocated PS: ``ps`` tasks just ``server.join()``)."""
+        return replace(self, roles=tuple(r for r in self.roles if r != "ps"))
 
     @classmethod
     def from_json(cls, s: str) -> "TFConfig":
@@ -51,7 +56,7 @@ class TFConfig:
     @property
     def members(self) -> List[Tuple[str, int, str]]:
         out = []
-        for job in RANK_ORDER:
+        for job in self.roles:
             for i, addr in enumerate(self.cluster.get(job, [])):
                 out.append((job, i, addr))
         return out
