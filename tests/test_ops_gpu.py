@@ -374,10 +374,12 @@ def test_bn_add_relu_residual(cuda, shape, conv):
 
 def test_resnet50_fused_matches_stock(cuda):
     """Whole-model check: fused ResNet-50 (HIP BN/GEMM/residual kernels) vs the stock module graph."""
+    from tony_amd.models.layers import cast_model
     from tony_amd.models.resnet import resnet50
 
     torch.manual_seed(0)
-    fused = resnet50(num_classes=10, fused=True).to(cuda, torch.bfloat16).to(memory_format=torch.channels_last)
+    fused = cast_model(resnet50(num_classes=10, fused=True), torch.bfloat16, cuda).to(
+        memory_format=torch.channels_last)
     stock = resnet50(num_classes=10, fused=False).to(cuda, torch.float32).to(memory_format=torch.channels_last)
     for b in list(fused.blocks) + list(stock.blocks):
         torch.nn.init.constant_(b.bn3.weight, 0.5)  # non-degenerate residual branch

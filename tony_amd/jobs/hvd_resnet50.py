@@ -21,6 +21,7 @@ import torch  # noqa: E402
 
 import tony_amd.hvd as hvd  # noqa: E402
 from tony_amd.jobs.common import Throughput, log, metric, synthetic_images  # noqa: E402
+from tony_amd.models.layers import cast_model  # noqa: E402
 from tony_amd.models.resnet import resnet50  # noqa: E402
 
 
@@ -38,7 +39,7 @@ def main(argv=None) -> int:
     dtype = torch.bfloat16 if on_gpu else torch.float32
     if on_gpu:
         torch.backends.cudnn.benchmark = True
-    model = resnet50(fused=on_gpu).to(dev, dtype).to(memory_format=torch.channels_last)
+    model = cast_model(resnet50(fused=on_gpu), dtype, dev).to(memory_format=torch.channels_last)
     opt = torch.optim.SGD(model.parameters(), lr=0.1 * hvd.size(), momentum=0.9, weight_decay=5e-5)
     opt = hvd.DistributedOptimizer(opt, named_parameters=model.named_parameters(), bucket_mb=a.bucket_mb)
     x, y = synthetic_images(a.batch_size, a.image_size, 1000, dev, dtype, seed=hvd.rank())

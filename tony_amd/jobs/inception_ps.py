@@ -58,11 +58,12 @@ def main(argv=None) -> int:
         tc = tc.without_ps()
     rank, world, dev = bootstrap.init_from_tf_config(tc)
     from tony_amd.models.inception_v3 import inception_v3
+    from tony_amd.models.layers import cast_model
 
     dtype = torch.bfloat16 if on_gpu else torch.float32
     if on_gpu:
         torch.backends.cudnn.benchmark = True
-    model = inception_v3(fused=on_gpu, seed=0).to(dev, dtype).to(memory_format=torch.channels_last)
+    model = cast_model(inception_v3(fused=on_gpu, seed=0), dtype, dev).to(memory_format=torch.channels_last)
     ps = ParameterServer(model, optimizer="sgd", lr=0.045, momentum=0.9, weight_decay=4e-5, mode=mode,
                          ps_ranks=tc.ps_ranks if mode == "dedicated" else (0,), dtype=dtype, device=dev)
     if mode == "dedicated" and ps.is_ps and not ps.is_worker:

@@ -47,6 +47,23 @@ class ConvBNAct(nn.Module):
         return self.act(self.bn(y))
 
 
+def cast_model(model: nn.Module, dtype: torch.dtype, device=None) -> nn.Module:
+    """``model.to(device, dtype)`` that keeps BatchNorm running statistics (and the batch
+    counter) in fp32: the fused BN kernels accumulate them in fp32, in place."""
+    if device is not None:
+        model.to(device)
+    for m in model.modules():
+        for name, p in m.named_parameters(recurse=False):
+            if p.is_floating_point():
+                p.data = p.data.to(dtype)
+        if isinstance(m, nn.modules.batchnorm._BatchNorm):
+            continue
+        for name, b in m.named_buffers(recurse=False):
+            if b.is_floating_point():
+                setattr(m, name, b.to(dtype))
+    return model
+
+
 def init_weights(model: nn.Module, seed: int = 0):
     """Deterministic random init (truncated-normal-ish convs, zero biases)."""
     g = torch.Generator().manual_seed(seed)

@@ -145,3 +145,14 @@ def grad_slot(param):
 
 def ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
+
+
+def check_f32_stats(*tensors) -> None:
+    """BatchNorm running statistics are fp32 device buffers that the kernels update in place.
+
+    ``model.to(torch.bfloat16)`` also casts them; passing those to a kernel that writes fp32
+    would overrun the buffer, so refuse loudly (use tony_amd.models.layers.cast_model)."""
+    for t in tensors:
+        if t is not None and t.dtype != torch.float32:
+            raise TypeError(f"BatchNorm running statistics must be float32, got {t.dtype}; "
+                            "cast models with tony_amd.models.layers.cast_model(model, dtype)")

@@ -62,6 +62,7 @@ class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, training, momentum, eps, relu):
         L = _lib.lib()
+        _lib.check_f32_stats(running_mean, running_var)
         x, (M, C, ldx) = _as_rows(x)
         y = _empty_like_rows(x)
         _, _, ldy = _rows_view(y)

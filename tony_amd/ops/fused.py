@@ -51,6 +51,7 @@ class _HeadFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, gamma, beta, running_mean, running_var, splits, npool, training, momentum, eps):
         L = _lib.lib()
+        _lib.check_f32_stats(running_mean, running_var)
         dev = x.device
         stream = _lib.stream_ptr(dev)
         x, (M, cin, ldx) = _as_rows(x)

@@ -27,6 +27,7 @@ _BF16 = torch.bfloat16
 
 def _bn_stats_and_apply(L, z, ldz, M, C, res, ldr, y, ldy, gamma, beta, pb, eps, training, momentum, running_mean,
                         running_var, stats, stream):
+    _lib.check_f32_stats(running_mean, running_var)
     dev = z.device
     if training:
         mean = torch.empty(C, dtype=torch.float32, device=dev)
