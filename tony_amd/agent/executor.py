@@ -156,7 +156,10 @@ class TaskExecutor:
     def run_user_command(self) -> int:
         env = dict(os.environ)
         env.update(self.shell_env)
-        self.user_proc = U.ShellProcess(self._command(), env=env, die_with_parent=True)
+        from ..utils.docker import wrap_if_enabled
+
+        cmd = wrap_if_enabled(self._command(), env, os.getcwd())
+        self.user_proc = U.ShellProcess(cmd, env=env, die_with_parent=True)
         try:  # the coordinator kills this group too when it stops the task
             with open(USER_PGID_FILE, "w") as f:
                 f.write(str(self.user_proc.pid))

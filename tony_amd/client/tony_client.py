@@ -204,9 +204,9 @@ class TonyClient:
         site = os.path.join(os.environ.get(C.TONY_CONF_DIR, C.DEFAULT_TONY_CONF_DIR), C.TONY_SITE_CONF)
         if os.path.exists(site):
             conf.add_resource(site, C.TONY_SITE_CONF)
-        from .. import __version__
+        from .. import version
 
-        conf.set(K.VERSION_INFO_PREFIX + "version", __version__, "VersionInfo")
+        version.inject(conf)
 
     def validate_tony_conf(self, conf: Configuration) -> bool:
         try:
