@@ -109,3 +109,36 @@ def test_checkpoint_manager_rotation_and_restore(tmp_path):
     torch.testing.assert_close(m2.weight, m.weight)
     assert CheckpointManager(str(tmp_path / "ck"), rank=1).save(50, {}, force=True) is None  # non-chief
     assert not any(f.endswith(".tmp") for f in os.listdir(tmp_path / "ck"))
+
+
+def test_tracing_ranges_and_hang_watchdog(tmp_path):
+    import subprocess
+
+    from tony_amd.utils import tracing
+
+    with tracing.trace_range("noop"):  # disabled by default: a no-op
+        pass
+    tracing.set_enabled(True)
+    with tracing.trace_range("cpu-only"):  # no GPU here: must not raise
+        pass
+    tracing.set_enabled(False)
+    # a "hung" rank: the watchdog dumps every thread's stack to stderr
+    code = ("import time; from tony_amd.utils import tracing; tracing.hang_watchdog(0.3); "
+            "time.sleep(1.0)")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=30,
+                       cwd=os.path.dirname(HERE))
+    assert "Thread" in r.stderr and "time.sleep" not in r.stdout
+
+
+def test_monitor_reports_new_uncorrectable_ecc(monkeypatch):
+    from tony_amd import constants as C
+    from tony_amd import native
+    from tony_amd.agent.monitor import TaskMonitor
+
+    counts = iter([5, 5, 7])
+    monkeypatch.setattr(native, "smi_sample", lambda g: native.GpuSample(10, 5, 100, 1000, 300.0, 60.0, 0,
+                                                                         next(counts)))
+    m = TaskMonitor(lambda: os.getpid(), [0], 1000, lambda _: None, gpu_metrics=True)
+    for _ in range(3):
+        m.refresh()
+    assert m.metrics()[C.GPU_ECC_UNCORRECTABLE] == 2.0

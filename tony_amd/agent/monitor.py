@@ -68,6 +68,8 @@ class TaskMonitor:
         self.main = RunningStat()
         self.power = RunningStat()
         self.temp = RunningStat()
+        self.ecc_base = None      # uncorrectable ECC count of the pinned GPUs when the task started
+        self.ecc_new = 0          # uncorrectable errors raised since (a GPU fault: SURVEY.md §5.3)
         self.gpu_errors = 0
         self._stop = threading.Event()
         self._thread = threading.Thread(target=self._run, name="tony-task-monitor", daemon=True)
@@ -97,6 +99,13 @@ class TaskMonitor:
             self.main.add(sum(s.mem_busy_pct for s in samples) / n)
             self.power.add(sum(s.power_w for s in samples))
             self.temp.add(max(s.temp_c for s in samples))
+            ecc = sum(s.ecc_uncorrectable for s in samples)
+            if self.ecc_base is None:
+                self.ecc_base = ecc
+            elif ecc > self.ecc_base + self.ecc_new:
+                LOG.error("GPU(s) %s raised %d new uncorrectable ECC error(s)", self.gpu_ids,
+                          ecc - self.ecc_base - self.ecc_new)
+                self.ecc_new = ecc - self.ecc_base
 
     def metrics(self) -> Dict[str, float]:
         m = {C.MAX_MEMORY_BYTES: self.mem.max, C.AVG_MEMORY_BYTES: self.mem.avg}
@@ -105,7 +114,7 @@ class TaskMonitor:
                       C.MAX_GPU_FB_MEMORY_USAGE: self.fb.max, C.AVG_GPU_FB_MEMORY_USAGE: self.fb.avg,
                       C.MAX_GPU_MAIN_MEMORY_USAGE: self.main.max, C.AVG_GPU_MAIN_MEMORY_USAGE: self.main.avg,
                       C.MAX_GPU_POWER_WATTS: self.power.max, C.AVG_GPU_POWER_WATTS: self.power.avg,
-                      C.MAX_GPU_TEMPERATURE: self.temp.max})
+                      C.MAX_GPU_TEMPERATURE: self.temp.max, C.GPU_ECC_UNCORRECTABLE: float(self.ecc_new)})
         return m
 
     def _push(self):

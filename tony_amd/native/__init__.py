@@ -33,7 +33,8 @@ class _GpuInfo(ctypes.Structure):
 class _GpuSample(ctypes.Structure):
     _fields_ = [("gfx_busy_pct", ctypes.c_uint32), ("mem_busy_pct", ctypes.c_uint32),
                 ("vram_used_mb", ctypes.c_uint32), ("vram_total_mb", ctypes.c_uint32), ("power_w", ctypes.c_double),
-                ("temp_c", ctypes.c_double)]
+                ("temp_c", ctypes.c_double), ("ecc_correctable", ctypes.c_uint64),
+                ("ecc_uncorrectable", ctypes.c_uint64)]
 
 
 def lib():
@@ -171,6 +172,8 @@ class GpuSample:
     vram_total_mb: float = 0.0
     power_w: float = 0.0
     temp_c: float = 0.0
+    ecc_correctable: int = 0
+    ecc_uncorrectable: int = 0
 
 
 def smi_devices() -> List[GpuDevice]:
@@ -195,7 +198,8 @@ def smi_sample(index: int) -> Optional[GpuSample]:
     s = _GpuSample()
     if L.tony_smi_sample(int(index), ctypes.byref(s)) != 0:
         return None
-    return GpuSample(s.gfx_busy_pct, s.mem_busy_pct, s.vram_used_mb, s.vram_total_mb, s.power_w, s.temp_c)
+    return GpuSample(s.gfx_busy_pct, s.mem_busy_pct, s.vram_used_mb, s.vram_total_mb, s.power_w, s.temp_c,
+                     int(s.ecc_correctable), int(s.ecc_uncorrectable))
 
 
 def smi_link(a: int, b: int):

@@ -122,6 +122,7 @@ struct Smi {
   decltype(&amdsmi_get_power_info) power = nullptr;
   decltype(&amdsmi_get_temp_metric) temp = nullptr;
   decltype(&amdsmi_topo_get_link_type) link_type = nullptr;
+  decltype(&amdsmi_get_gpu_total_ecc_count) ecc = nullptr;
   std::vector<amdsmi_processor_handle> gpus;
   bool ready = false;
 };
@@ -158,6 +159,7 @@ API int tony_smi_init(void) {
   sym(g_smi.h, "amdsmi_get_power_info", g_smi.power);
   sym(g_smi.h, "amdsmi_get_temp_metric", g_smi.temp);
   sym(g_smi.h, "amdsmi_topo_get_link_type", g_smi.link_type);
+  sym(g_smi.h, "amdsmi_get_gpu_total_ecc_count", g_smi.ecc);
   if (!g_smi.init || !g_smi.sockets || !g_smi.processors) return -2;
   if (g_smi.init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) return -3;
   uint32_t ns = 0;
@@ -200,6 +202,9 @@ struct tony_gpu_sample {
   uint32_t vram_total_mb;
   double power_w;
   double temp_c;
+  // RAS: accumulated ECC error counts (uncorrectable growth = a GPU fault)
+  uint64_t ecc_correctable;
+  uint64_t ecc_uncorrectable;
 };
 
 API int tony_smi_info(int idx, tony_gpu_info* out) {
@@ -249,6 +254,11 @@ API int tony_smi_sample(int idx, tony_gpu_sample* out) {
   if (g_smi.temp && g_smi.temp(p, AMDSMI_TEMPERATURE_TYPE_HOTSPOT, AMDSMI_TEMP_CURRENT, &t) == AMDSMI_STATUS_SUCCESS) {
     out->temp_c = static_cast<double>(t);
     ++ok;
+  }
+  amdsmi_error_count_t ec{};
+  if (g_smi.ecc && g_smi.ecc(p, &ec) == AMDSMI_STATUS_SUCCESS) {
+    out->ecc_correctable = ec.correctable_count;
+    out->ecc_uncorrectable = ec.uncorrectable_count;
   }
   return ok > 0 ? 0 : -2;
 }

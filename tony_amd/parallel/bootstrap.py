@@ -80,6 +80,9 @@ def init_process_group(rank: int, world: int, store: Optional[dist.Store] = None
         store = dist.TCPStore(master_addr, int(master_port), world, rank == 0, timeout=timeout,
                               wait_for_workers=False)
     dist.init_process_group(backend, store=store, rank=rank, world_size=world, timeout=timeout, **kw)
+    from ..utils.tracing import arm_from_env
+
+    arm_from_env()  # TONY_HANG_DUMP_S: dump every thread's stack when a rank stops making progress
     return dev
 
 

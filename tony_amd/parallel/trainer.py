@@ -14,6 +14,7 @@ from typing import Callable
 
 import torch
 
+from ..utils.tracing import heartbeat, trace_range
 from .ps import ParameterServer
 
 
@@ -33,10 +34,14 @@ class Trainer:
 
     def _eager_step(self, x, y):
         self.ps.zero_grad()
-        out = self.model(x)
-        loss = self.loss_fn(out, y)
-        loss.backward()
-        self.ps.step()
+        with trace_range("forward"):
+            out = self.model(x)
+            loss = self.loss_fn(out, y)
+        with trace_range("backward"):
+            loss.backward()
+        with trace_range("ps push/apply/pull"):
+            self.ps.step()
+        heartbeat()
         return loss.detach()
 
     def step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
@@ -59,6 +64,7 @@ class Trainer:
             self.static_y.copy_(y, non_blocking=True)
         self._refresh_hp()
         self.graph.replay()
+        heartbeat()
         self.ps.steps += 1
         for opt in self.ps.optimizers.values():
             opt.step_count += 1
