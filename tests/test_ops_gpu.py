@@ -373,25 +373,33 @@ def test_bn_add_relu_residual(cuda, shape, conv):
 
 
 def test_resnet50_fused_matches_stock(cuda):
-    """Whole-model check: fused ResNet-50 (HIP BN/GEMM/residual kernels) vs the stock module graph."""
+    """Whole-model check: fused ResNet-50 (HIP BN/GEMM/residual kernels, bf16) vs the stock module graph in
+    fp32.  A 16-block random-init net amplifies rounding, so the yardstick is the stock graph run in bf16:
+    the fused model must be about as close to fp32 as stock bf16 is."""
     from tony_amd.models.layers import cast_model
     from tony_amd.models.resnet import resnet50
 
     torch.manual_seed(0)
-    fused = cast_model(resnet50(num_classes=10, fused=True), torch.bfloat16, cuda).to(
-        memory_format=torch.channels_last)
-    stock = resnet50(num_classes=10, fused=False).to(cuda, torch.float32).to(memory_format=torch.channels_last)
-    for b in list(fused.blocks) + list(stock.blocks):
-        torch.nn.init.constant_(b.bn3.weight, 0.5)  # non-degenerate residual branch
-    stock.load_state_dict({k: v.float() for k, v in fused.state_dict().items()})
+
+    def build(fused, dtype):
+        m = cast_model(resnet50(num_classes=10, fused=fused), dtype, cuda).to(memory_format=torch.channels_last)
+        for b in m.blocks:
+            torch.nn.init.constant_(b.bn3.weight, 0.5)  # non-degenerate residual branch
+        return m
+
+    fused, ref, stock16 = build(True, torch.bfloat16), build(False, torch.float32), build(False, torch.bfloat16)
+    sd = fused.state_dict()
+    ref.load_state_dict({k: v.float() for k, v in sd.items()})
+    stock16.load_state_dict(sd)
     x = _nhwc(torch.randn(4, 3, 64, 64, device=cuda))
-    yk = fused(x.to(torch.bfloat16))
-    yr = stock(x)
+    yk, yr, ys = fused(x.to(torch.bfloat16)), ref(x), stock16(x.to(torch.bfloat16))
     assert torch.isfinite(yk.float()).all()
-    rel = (yk.float() - yr).norm() / yr.norm()
-    assert rel < 0.08, f"fused vs stock rel err {rel:.3f}"
-    yk.float().sum().backward()
-    yr.sum().backward()
-    gk = fused.stem.conv.weight.grad.float()
-    gr = stock.stem.conv.weight.grad
-    assert (gk - gr).norm() / gr.norm() < 0.15
+    rel_k = ((yk.float() - yr).norm() / yr.norm()).item()
+    rel_s = ((ys.float() - yr).norm() / yr.norm()).item()
+    assert rel_k < 1.5 * rel_s + 0.02, f"fused {rel_k:.3f} vs stock-bf16 {rel_s:.3f} (rel err to fp32)"
+    for m, y in ((fused, yk), (ref, yr), (stock16, ys)):
+        y.float().sum().backward()
+    gr = ref.stem.conv.weight.grad
+    gk = (fused.stem.conv.weight.grad.float() - gr).norm() / gr.norm()
+    gs = (stock16.stem.conv.weight.grad.float() - gr).norm() / gr.norm()
+    assert gk < 1.5 * gs + 0.05, f"stem dW: fused {gk:.3f} vs stock-bf16 {gs:.3f}"
