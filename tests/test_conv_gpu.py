@@ -1,0 +1,136 @@
+"""Implicit-GEMM conv kernels (csrc/conv.hip) vs PyTorch fp32 references, and the fused conv+BN layer."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+# (N, Cin, H, W, Cout, (R, S), stride, (ph, pw)) -- the Inception-v3 / ResNet-50 conv shapes, shrunk in N
+SHAPES = [
+    (4, 32, 37, 37, 64, (3, 3), 1, (1, 1)),
+    (2, 64, 35, 35, 96, (3, 3), 1, (1, 1)),
+    (2, 48, 35, 35, 64, (5, 5), 1, (2, 2)),
+    (2, 128, 17, 17, 192, (1, 7), 1, (0, 3)),
+    (2, 160, 17, 17, 160, (7, 1), 1, (3, 0)),
+    (2, 384, 8, 8, 384, (1, 3), 1, (0, 1)),
+    (2, 448, 8, 8, 384, (3, 3), 1, (1, 1)),
+    (2, 288, 35, 35, 384, (3, 3), 2, (0, 0)),
+    (2, 64, 56, 56, 64, (3, 3), 1, (1, 1)),
+    (2, 128, 28, 28, 128, (3, 3), 2, (1, 1)),
+    (3, 32, 149, 149, 32, (3, 3), 1, (0, 0)),
+    (2, 80, 73, 73, 192, (3, 3), 1, (0, 0)),
+]
+
+
+def _nhwc(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[f"{s[1]}x{s[2]}k{s[5][0]}{s[5][1]}s{s[6]}" for s in SHAPES])
+def test_conv_fwd_dgrad_wgrad(cuda, shape):
+    from tony_amd.ops.conv import conv_dgrad, conv_fwd, conv_wgrad
+
+    n, ci, h, w, co, (r, s), st, (ph, pw) = shape
+    torch.manual_seed(0)
+    x = _nhwc(torch.randn(n, ci, h, w, device=cuda)).to(torch.bfloat16)
+    wt = _nhwc(torch.randn(co, ci, r, s, device=cuda) / (ci * r * s) ** 0.5).to(torch.bfloat16)
+    xr, wr = x.float().requires_grad_(True), wt.float().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, wr, None, st, (ph, pw))
+    stats = torch.empty(2 * co, device=cuda)
+    y = conv_fwd(x, wt, st, (ph, pw), stats)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(y, yr) < 1e-2, f"fwd rel {_rel(y, yr):.4f}"
+    torch.testing.assert_close(stats[:co], yr.sum((0, 2, 3)), rtol=2e-2, atol=2e-2 * (yr.numel() / co) ** 0.5)
+    torch.testing.assert_close(stats[co:], (yr * yr).sum((0, 2, 3)), rtol=2e-2, atol=1.0)
+    dy = _nhwc(torch.randn_like(yr)).to(torch.bfloat16)
+    yr.backward(dy.float())
+    dx = conv_dgrad(dy, wt, x.shape, st, (ph, pw))
+    assert _rel(dx, xr.grad) < 1e-2, f"dgrad rel {_rel(dx, xr.grad):.4f}"
+    dw = conv_wgrad(dy, x, wt.shape, st, (ph, pw))
+    assert dw.shape == wt.shape
+    assert _rel(dw, wr.grad) < 1e-2, f"wgrad rel {_rel(dw, wr.grad):.4f}"
+
+
+def test_conv_on_channel_slice_input(cuda):
+    """The input may be a channel slice of a concat buffer (pixel stride > C)."""
+    from tony_amd.ops.conv import conv_fwd
+
+    big = _nhwc(torch.randn(2, 96, 17, 17, device=cuda)).to(torch.bfloat16)
+    x = big[:, 32:96]
+    wt = _nhwc(torch.randn(48, 64, 3, 3, device=cuda) * 0.05).to(torch.bfloat16)
+    y = conv_fwd(x, wt, 1, 1)
+    yr = torch.nn.functional.conv2d(x.float(), wt.float(), None, 1, 1)
+    assert _rel(y, yr) < 1e-2
+
+
+@pytest.mark.parametrize("relu", [True, False])
+def test_conv_bn_act_fused_matches_reference(cuda, relu):
+    from tony_amd.ops import _lib
+    from tony_amd.ops.conv import conv_bn_act
+
+    torch.manual_seed(1)
+    n, ci, h, w, co = 4, 64, 35, 35, 96
+    x = _nhwc(torch.randn(n, ci, h, w, device=cuda)).to(torch.bfloat16)
+    conv = torch.nn.Conv2d(ci, co, 3, 1, 1, bias=False).to(cuda)
+    bn = torch.nn.BatchNorm2d(co, eps=1e-3).to(cuda)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    wt = _nhwc(conv.weight.detach()).to(torch.bfloat16).requires_grad_(True)
+    g = bn.weight.detach().to(torch.bfloat16).requires_grad_(True)
+    b = bn.bias.detach().to(torch.bfloat16).requires_grad_(True)
+    rm, rv = torch.zeros(co, device=cuda), torch.ones(co, device=cuda)
+    _lib.set_inplace_grads(False)
+    try:
+        xk = x.detach().requires_grad_(True)
+        y = conv_bn_act(xk, wt, g, b, rm, rv, 1, 1, True, 0.1, 1e-3, relu)
+        xr = x.float().requires_grad_(True)
+        wr, gr, br = wt.detach().float().requires_grad_(True), g.detach().float().requires_grad_(True), \
+            b.detach().float().requires_grad_(True)
+        rm_r, rv_r = torch.zeros(co, device=cuda), torch.ones(co, device=cuda)
+        yr = torch.nn.functional.batch_norm(torch.nn.functional.conv2d(xr, wr, None, 1, 1), rm_r, rv_r, gr, br,
+                                            True, 0.1, 1e-3)
+        yr = torch.relu(yr) if relu else yr
+        assert _rel(y, yr) < 2e-2
+        torch.testing.assert_close(rm, rm_r, rtol=2e-2, atol=2e-3)
+        dy = _nhwc(torch.randn_like(yr)).to(torch.bfloat16)
+        y.backward(dy)
+        yr.backward(dy.float())
+        assert _rel(xk.grad, xr.grad) < 3e-2
+        assert _rel(wt.grad, wr.grad) < 3e-2
+        assert _rel(g.grad, gr.grad) < 3e-2 and _rel(b.grad, br.grad) < 3e-2
+    finally:
+        _lib.set_inplace_grads(True)
+
+
+def test_inception_tony_convs_match_miopen_convs(cuda):
+    """The same fused Inception-v3 with its spatial convs on tony_amd's kernels vs on MIOpen (A/B in one
+    model): forward logits and a weight gradient must agree to bf16 rounding."""
+    from tony_amd.models import layers
+    from tony_amd.models.inception_v3 import inception_v3
+    from tony_amd.models.layers import cast_model
+
+    torch.manual_seed(0)
+    model = cast_model(inception_v3(num_classes=10, fused=True, seed=0), torch.bfloat16, cuda).to(
+        memory_format=torch.channels_last)
+    model.dropout.p = 0.0  # deterministic A/B
+    x = _nhwc(torch.randn(8, 3, 299, 299, device=cuda)).to(torch.bfloat16)
+    y = torch.randint(0, 10, (8,), device=cuda)
+    outs, grads = [], []
+    old = layers.USE_TONY_CONV
+    try:
+        for use in (True, False):
+            layers.USE_TONY_CONV = use
+            model.zero_grad(set_to_none=True)
+            logits, aux = model(x)
+            (torch.nn.functional.cross_entropy(logits.float(), y)
+             + 0.4 * torch.nn.functional.cross_entropy(aux.float(), y)).backward()
+            outs.append(logits.detach().float())
+            grads.append(model.stem[2].conv.weight.grad.detach().float())  # Conv2d_2b_3x3 (32->64, p1)
+    finally:
+        layers.USE_TONY_CONV = old
+    assert _rel(outs[0], outs[1]) < 3e-2, f"logits rel {_rel(outs[0], outs[1]):.4f}"
+    assert _rel(grads[0], grads[1]) < 6e-2, f"dW rel {_rel(grads[0], grads[1]):.4f}"

@@ -11,8 +11,14 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+import os
+
+from ..ops import conv as conv_ops
 from ..ops.bn import BatchNormAct2d
 from ..ops.fused import _HeadFn
+
+# TONY_CONV=miopen keeps the spatial convs on MIOpen (A/B comparisons); default: tony_amd's kernels
+USE_TONY_CONV = os.environ.get("TONY_CONV", "tony").lower() != "miopen"
 
 
 def _pair(v):
@@ -41,6 +47,11 @@ class ConvBNAct(nn.Module):
             bn = self.bn
             return _HeadFn.apply(x, self.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                  (self.conv.out_channels,), 0, self.training, bn.momentum, bn.eps)[0]
+        if self.fused and x.is_cuda and USE_TONY_CONV and conv_ops.supported(x, self.conv.weight):
+            # implicit-GEMM conv with BN statistics in its epilogue + fused apply (ops/conv.py)
+            bn, c = self.bn, self.conv
+            return conv_ops.conv_bn_act(x, c.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, c.stride,
+                                        c.padding, self.training, bn.momentum, bn.eps, bn.relu)
         y = self.conv(x)
         if self.fused:
             return self.bn(y)

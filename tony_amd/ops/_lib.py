@@ -60,6 +60,12 @@ _SIGNATURES = {
                        c_int, c_void_p, c_void_p],
     "tony_gemm_tn_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64, c_int,
                           c_void_p],
+    "tony_conv_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                      c_int, c_int, c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_void_p],
+    "tony_conv_dgrad": [c_void_p, c_int, c_int, c_int, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                        c_void_p, c_int, c_int, c_int64, c_void_p],
+    "tony_conv_wgrad": [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int, c_int, c_int, c_int,
+                        c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
     "tony_avgpool3_s1p1": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
     "tony_maxpool_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
                          c_void_p],
@@ -138,7 +144,9 @@ def grad_slot(param):
     if not _INPLACE_GRADS[0] or param is None or not isinstance(param, torch.nn.Parameter):
         return None
     g = param.grad
-    if g is None or g.dtype != param.dtype or g.shape != param.shape or not g.is_contiguous():
+    if g is None or g.dtype != param.dtype or g.shape != param.shape:
+        return None
+    if not (g.is_contiguous() or (g.dim() == 4 and g.is_contiguous(memory_format=torch.channels_last))):
         return None
     return g
 

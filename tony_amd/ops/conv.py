@@ -1,0 +1,203 @@
+"""NHWC implicit-GEMM convolutions on MFMA (csrc/conv.hip) and the fused conv + BN(+ReLU) layer.
+
+``conv2d(x, weight, stride, padding)`` is a drop-in for ``F.conv2d`` on channels_last bf16 CUDA
+tensors with ``Cin % 8 == 0`` (every Inception-v3 / ResNet-50 conv but the 3-channel stems):
+forward, backward-data (stride 1; strided convs use MIOpen's backward-data) and split-K
+backward-weight are tony_amd kernels.
+
+``conv_bn_act(x, weight, bn...)`` fuses the BatchNorm that follows: the forward GEMM epilogue
+produces the per-channel sums of its output, so the separate statistics pass over the conv
+output disappears; the apply kernel normalises (+ReLU); the backward is the fused BN backward
+followed by the dgrad / wgrad GEMMs on dZ.  Parameter gradients are accumulated in place into the
+flat gradient buffer when ``_lib.set_inplace_grads`` is on (the trainer's default).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .bn import _as_rows, _rows_view
+
+_BF16 = torch.bfloat16
+
+
+def _pair(v):
+    return tuple(v) if isinstance(v, (tuple, list)) else (int(v), int(v))
+
+
+def supported(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, dilation=1, groups=1) -> bool:
+    return (x.is_cuda and x.dtype == _BF16 and weight.dtype == _BF16 and x.dim() == 4 and groups == 1
+            and _pair(dilation) == (1, 1) and x.shape[1] % 8 == 0 and weight.shape[0] % 8 == 0
+            and weight.shape[1] == x.shape[1])
+
+
+def out_hw(h, w, r, s, stride, padding):
+    (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
+    return (h + 2 * ph - r) // sh + 1, (w + 2 * pw - s) // sw + 1
+
+
+def _krsc(weight: torch.Tensor) -> torch.Tensor:
+    """[Co, Ci, R, S] -> memory [Co][R][S][Ci] (free for channels_last weights)."""
+    w = weight.permute(0, 2, 3, 1)
+    return w if w.is_contiguous() else w.contiguous()
+
+
+def _crsk(weight: torch.Tensor) -> torch.Tensor:
+    """[Co, Ci, R, S] -> memory [Ci][R][S][Co] (the dgrad operand)."""
+    return weight.permute(1, 2, 3, 0).contiguous()
+
+
+def _cl_empty(n, c, h, w, device):
+    return torch.empty((n, c, h, w), dtype=_BF16, device=device, memory_format=torch.channels_last)
+
+
+def conv_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: torch.Tensor | None = None):
+    x, (_, C, ldx) = _as_rows(x)
+    n, _, h, w = x.shape
+    co, _, r, s = weight.shape
+    (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
+    oh, ow = out_hw(h, w, r, s, stride, padding)
+    y = _cl_empty(n, co, oh, ow, x.device)
+    wk = _krsc(weight)
+    rc = _lib.lib().tony_conv_fwd(x.data_ptr(), n, h, w, C, ldx, wk.data_ptr(), co, r, s, sh, sw, ph, pw,
+                                  y.data_ptr(), oh, ow, co, 1 if stats is not None else 0, _lib.ptr(stats),
+                                  _lib.stream_ptr(x.device))
+    _lib.check(rc, "tony_conv_fwd")
+    return y
+
+
+def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, padding=0) -> torch.Tensor:
+    n, c, h, w = x_shape
+    co, _, r, s = weight.shape
+    if _pair(stride) != (1, 1):  # strided: MIOpen's backward-data
+        xs = torch.empty(x_shape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
+        return torch.ops.aten.convolution_backward(dy, xs, weight, None, _pair(stride), _pair(padding), (1, 1),
+                                                   False, (0, 0), 1, (True, False, False))[0]
+    dy, (_, _, lddy) = _as_rows(dy)
+    ph, pw = _pair(padding)
+    dx = _cl_empty(n, c, h, w, dy.device)
+    wt = _crsk(weight)
+    rc = _lib.lib().tony_conv_dgrad(dy.data_ptr(), n, dy.shape[2], dy.shape[3], co, lddy, wt.data_ptr(), c, r, s,
+                                    ph, pw, dx.data_ptr(), h, w, c, _lib.stream_ptr(dy.device))
+    _lib.check(rc, "tony_conv_dgrad")
+    return dx
+
+
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride=1, padding=0) -> torch.Tensor:
+    """fp32 dW with memory [Co][R][S][Ci] (returned as a [Co, Ci, R, S] channels_last view)."""
+    dy, (_, co, lddy) = _as_rows(dy)
+    x, (_, c, ldx) = _as_rows(x)
+    n, _, h, w = x.shape
+    _, _, r, s = weight_shape
+    (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
+    dw = torch.empty((co, r, s, c), dtype=torch.float32, device=x.device)
+    rc = _lib.lib().tony_conv_wgrad(dy.data_ptr(), lddy, x.data_ptr(), n, h, w, c, ldx, co, r, s, sh, sw, ph, pw,
+                                    dy.shape[2], dy.shape[3], dw.data_ptr(), _lib.num_cus(x.device),
+                                    _lib.stream_ptr(x.device))
+    _lib.check(rc, "tony_conv_wgrad")
+    return dw.permute(0, 3, 1, 2)
+
+
+def _accumulate_wgrad(weight, dw32):
+    """Add dW (a [Co, Ci, R, S] view of fp32 memory [Co][R][S][Ci]) into the parameter's flat
+    gradient slot in place and return None, or return it (bf16) for autograd to accumulate."""
+    gw = _lib.grad_slot(weight)
+    if gw is None:
+        return dw32.to(weight.dtype)
+    # same memory order as the slot: channels_last slots (FlatParams keeps conv weights that way)
+    # take dW as is; an NCHW-contiguous slot gets an NCHW-ordered copy
+    src = dw32 if gw.is_contiguous(memory_format=torch.channels_last) else dw32.contiguous()
+    rc = _lib.lib().tony_add_f32(gw.data_ptr(), int(gw.dtype == _BF16), src.data_ptr(), src.numel(),
+                                 _lib.stream_ptr(weight.device))
+    _lib.check(rc, "tony_add_f32")
+    return None
+
+
+class _ConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stride, padding):
+        y = conv_fwd(x, weight, stride, padding)
+        ctx.save_for_backward(x, weight)
+        ctx.stride, ctx.padding = stride, padding
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        dx = conv_dgrad(dy, weight, x.shape, ctx.stride, ctx.padding) if ctx.needs_input_grad[0] else None
+        dw = _accumulate_wgrad(weight, conv_wgrad(dy, x, weight.shape, ctx.stride, ctx.padding))
+        return dx, dw, None, None
+
+
+def conv2d(x, weight, stride=1, padding=0):
+    if supported(x, weight, stride, padding):
+        return _ConvFn.apply(x, weight, _pair(stride), _pair(padding))
+    return torch.nn.functional.conv2d(x, weight, None, stride, padding)
+
+
+class _ConvBNActFn(torch.autograd.Function):
+    """Z = conv(x) with BN sums from the GEMM epilogue; y = act(bn(Z)); backward through both."""
+
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, running_mean, running_var, stride, padding, training, momentum, eps,
+                relu):
+        L = _lib.lib()
+        _lib.check_f32_stats(running_mean, running_var)
+        dev = x.device
+        stream = _lib.stream_ptr(dev)
+        co = weight.shape[0]
+        stats = torch.empty(2 * co, dtype=torch.float32, device=dev) if training else None
+        Z = conv_fwd(x, weight, stride, padding, stats)
+        M, _, ldz = _rows_view(Z)
+        y = torch.empty_like(Z)
+        pb = int(gamma.dtype == _BF16)
+        if training:
+            mean = torch.empty(co, dtype=torch.float32, device=dev)
+            invstd = torch.empty(co, dtype=torch.float32, device=dev)
+        else:
+            mean = running_mean
+            invstd = torch.rsqrt(running_var.float() + eps)
+        rc = L.tony_bn_apply(Z.data_ptr(), M, co, ldz, y.data_ptr(), ldz, _lib.ptr(stats),
+                             _lib.ptr(stats) + 4 * co if training else 0, gamma.data_ptr(), beta.data_ptr(), pb,
+                             float(eps), int(relu), 0 if training else 1, _lib.ptr(mean) if training else 0,
+                             _lib.ptr(invstd) if training else 0, _lib.ptr(running_mean), _lib.ptr(running_var),
+                             float(momentum), stream)
+        _lib.check(rc, "tony_bn_apply")
+        ctx.save_for_backward(x, weight, gamma, beta, mean, invstd, Z)
+        ctx.params = (weight, gamma, beta)
+        ctx.cfg = (stride, padding, relu, pb)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = _lib.lib()
+        x, weight, gamma, beta, mean, invstd, Z = ctx.saved_tensors
+        stride, padding, relu, pb = ctx.cfg
+        dev = x.device
+        M, co, ldz = _rows_view(Z)
+        dy, (_, _, lddy) = _as_rows(dy)
+        dZ = torch.empty_like(Z)
+        ws = torch.empty(2 * co, dtype=torch.float32, device=dev)
+        gg, gb = _lib.grad_slot(ctx.params[1]), _lib.grad_slot(ctx.params[2])
+        inplace = gg is not None and gb is not None
+        dgamma = gg if inplace else torch.empty_like(gamma)
+        dbeta = gb if inplace else torch.empty_like(beta)
+        rc = L.tony_bn_bwd(Z.data_ptr(), ldz, dy.data_ptr(), lddy, dZ.data_ptr(), ldz, M, co, mean.data_ptr(),
+                           invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), pb, int(relu), ws.data_ptr(),
+                           dgamma.data_ptr(), dbeta.data_ptr(), int(inplace), _lib.stream_ptr(dev))
+        _lib.check(rc, "tony_bn_bwd")
+        dx = conv_dgrad(dZ, weight, x.shape, stride, padding) if ctx.needs_input_grad[0] else None
+        dw = _accumulate_wgrad(weight, conv_wgrad(dZ, x, weight.shape, stride, padding))
+        if inplace:
+            dgamma = dbeta = None
+        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None
+
+
+def conv_bn_act(x, weight, gamma, beta, running_mean, running_var, stride=1, padding=0, training=True,
+                momentum=0.1, eps=1e-3, relu=True):
+    if supported(x, weight, stride, padding):
+        return _ConvBNActFn.apply(x, weight, gamma, beta, running_mean, running_var, _pair(stride), _pair(padding),
+                                  training, momentum, eps, relu)
+    z = torch.nn.functional.conv2d(x, weight, None, stride, padding)
+    y = torch.nn.functional.batch_norm(z, running_mean, running_var, gamma, beta, training, momentum, eps)
+    return torch.relu(y) if relu else y

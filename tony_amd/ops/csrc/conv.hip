@@ -1,0 +1,400 @@
+// Implicit-GEMM NHWC convolutions on MFMA, bf16 in, fp32 accumulate.
+//
+// Forward   Y[m, co] = sum_k A[m, k] W[co, k],  m = (n, oy, ox), k = (r, s, ci)
+//           A[m, k]  = X[n, oy*sh - ph + r, ox*sw - pw + s, ci]   (zero outside the image)
+// Dgrad     dX[m, ci] = sum_k dY[n, iy + ph - r, ix + pw - s, co] Wt[ci, k], k = (r, s, co)
+//           (stride 1; Wt = W permuted to [Ci][R][S][Co])
+// Wgrad     dW[co, k] = sum_m dY[m, co] A[m, k]                   (split-K over m, fp32 atomics)
+//
+// The GEMM cores are those of gemm.hip (256 threads = 2x2 wave64s, 16x16x32 bf16 MFMA, BK = 64,
+// register-staged double-buffered LDS with an XOR swizzle, XCD-aware tile order, BN statistics
+// in the forward epilogue); only the operand that is an image changes: instead of a row-major
+// matrix it is gathered on the fly ("im2col in the loader").  With Cin % 8 == 0 every 16-byte
+// chunk of a K row is 8 channels of ONE filter tap, so each chunk is one aligned 16-byte load
+// from one input pixel (or zero for padding).  The tap/channel position of a thread's chunk is
+// advanced incrementally per K-step (no divisions in the loop); the per-row pixel coordinates are
+// decoded once per tile (forward/dgrad) or advanced incrementally with the row (wgrad).
+#include "mfma_common.h"
+
+using namespace tony;
+using namespace tony::mfma;
+
+namespace {
+
+struct Gather {
+  const uint16_t* src;  // source image, pixel-major: pixel p at src + p * ld
+  int64_t ld;           // elements per pixel row (>= Cs; a channel slice of a concat buffer is fine)
+  int Hs, Ws, Cs;       // source spatial dims and channels
+  int OH, OW;           // the GEMM row space: m -> (n, oy, ox) over [N][OH][OW]
+  int R, S;             // filter taps
+  int sh, sw;           // stride of the output grid in source pixels
+  int offh, offw;       // source coord = o*stride + off + sign*tap
+  int sign;             // +1 convolution, -1 transposed (dgrad)
+  int K;                // R * S * Cs
+};
+
+struct RowState {
+  int pix;   // n * Hs * Ws
+  int iy0;   // oy*sh + offh
+  int ix0;   // ox*sw + offw
+  bool ok;   // row < M
+};
+
+// position of a K chunk: channel c of tap (r, s)
+struct TapPos {
+  int c, r, s;
+  __device__ __forceinline__ void init(int k, const Gather& g) {
+    c = k % g.Cs;
+    const int tap = k / g.Cs;
+    r = tap / g.S;
+    s = tap - r * g.S;
+  }
+  __device__ __forceinline__ void advance(int dk, const Gather& g) {
+    c += dk;
+    while (c >= g.Cs) {
+      c -= g.Cs;
+      if (++s == g.S) {
+        s = 0;
+        ++r;
+      }
+    }
+  }
+};
+
+__device__ __forceinline__ uint4 gather16(const Gather& g, const RowState& rs, const TapPos& t) {
+  const int iy = rs.iy0 + g.sign * t.r, ix = rs.ix0 + g.sign * t.s;
+  if (rs.ok && t.r < g.R && static_cast<unsigned>(iy) < static_cast<unsigned>(g.Hs) &&
+      static_cast<unsigned>(ix) < static_cast<unsigned>(g.Ws))
+    return *reinterpret_cast<const uint4*>(g.src + (static_cast<int64_t>(rs.pix) + iy * g.Ws + ix) * g.ld + t.c);
+  return make_uint4(0, 0, 0, 0);
+}
+
+template <int ROWS>
+__device__ __forceinline__ void load_rows(uint4* regs, const uint16_t* __restrict__ G, int64_t ld, int row0, int nrows,
+                                          int k0, int K) {
+  constexpr int VEC = ROWS * BK / 8 / kThreads;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    const int v = threadIdx.x + i * kThreads;
+    const int row = v >> 3, ch = v & 7;
+    const int gr = row0 + row, gk = k0 + ch * 8;
+    if (gr < nrows && gk < K)
+      regs[i] = *reinterpret_cast<const uint4*>(G + static_cast<int64_t>(gr) * ld + gk);
+    else
+      regs[i] = make_uint4(0, 0, 0, 0);
+  }
+}
+
+template <int ROWS>
+__device__ __forceinline__ void store_rows(uint16_t* lds, const uint4* regs) {
+  constexpr int VEC = ROWS * BK / 8 / kThreads;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    const int v = threadIdx.x + i * kThreads;
+    const int row = v >> 3, ch = v & 7;
+    *reinterpret_cast<uint4*>(lds + lds_off(row, ch)) = regs[i];
+  }
+}
+
+// C[M, N] = gather(A)[M, K] * B[N, K]^T  (forward and stride-1 dgrad)
+template <int BM, int BN>
+__global__ __launch_bounds__(kThreads) void conv_nt_kernel(Gather g, const uint16_t* __restrict__ B,
+                                                           uint16_t* __restrict__ C, int64_t ldc, int M, int N,
+                                                           float* __restrict__ stats, int tiles_n) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int AV = BM * BK / 8 / kThreads, BV = BN * BK / 8 / kThreads;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * (BM + BN) * BK];
+
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = wg / tiles_n, tn = wg % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int K = g.K;
+
+  // rows of the A tile this thread loads: (tid >> 3) + 32 i ; its chunk column: tid & 7
+  RowState rs[AV];
+  const int ohw = g.OH * g.OW;
+#pragma unroll
+  for (int i = 0; i < AV; ++i) {
+    const int m = m0 + (threadIdx.x >> 3) + i * (kThreads / 8);
+    rs[i].ok = m < M;
+    const int mm = rs[i].ok ? m : 0;
+    const int n = mm / ohw, rem = mm - n * ohw;
+    const int oy = rem / g.OW, ox = rem - oy * g.OW;
+    rs[i].pix = n * g.Hs * g.Ws;
+    rs[i].iy0 = oy * g.sh + g.offh;
+    rs[i].ix0 = ox * g.sw + g.offw;
+  }
+  TapPos tp;
+  tp.init((threadIdx.x & 7) * 8, g);
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[AV], rb[BV];
+  const int nk = (K + BK - 1) / BK;
+#pragma unroll
+  for (int i = 0; i < AV; ++i) ra[i] = gather16(g, rs[i], tp);
+  load_rows<BN>(rb, B, K, n0, N, 0, K);
+  store_rows<BM>(smem, ra);
+  store_rows<BN>(smem + BM * BK, rb);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    uint16_t* As = smem + (kt & 1) * (BM + BN) * BK;
+    uint16_t* Bs = As + BM * BK;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      tp.advance(BK, g);
+#pragma unroll
+      for (int i = 0; i < AV; ++i) ra[i] = gather16(g, rs[i], tp);
+      load_rows<BN>(rb, B, K, n0, N, (kt + 1) * BK, K);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = kk * 4 + (lane >> 4);
+      bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(As + lds_off(wm * WM + i * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const bf16x8_t*>(Bs + lds_off(wn * WN + j * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      uint16_t* An = smem + ((kt + 1) & 1) * (BM + BN) * BK;
+      store_rows<BM>(An, ra);
+      store_rows<BN>(An + BM * BK, rb);
+    }
+    __syncthreads();
+  }
+  nt_epilogue<BM, BN, TM, TN>(acc, smem, C, ldc, M, N, m0, n0, stats);
+}
+
+template <int BM, int BN>
+int launch_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, float* stats,
+              hipStream_t stream) {
+  const int tiles_m = ceil_div(M, BM), tiles_n = ceil_div(N, BN);
+  const int64_t tiles = static_cast<int64_t>(tiles_m) * tiles_n;
+  if (tiles > 0x7fffffff) return -2;
+  conv_nt_kernel<BM, BN><<<static_cast<int>(tiles), kThreads, 0, stream>>>(
+      g, static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), ldc, static_cast<int>(M), static_cast<int>(N),
+      stats, tiles_n);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, int flags, float* stats,
+           hipStream_t stream) {
+  float* st = (flags & 1) ? stats : nullptr;
+  if (st != nullptr) (void)hipMemsetAsync(st, 0, sizeof(float) * 2 * N, stream);
+  if (N <= 64) return launch_nt<256, 64>(g, B, C, ldc, M, N, st, stream);
+  return launch_nt<128, 128>(g, B, C, ldc, M, N, st, stream);
+}
+
+// ---------------------------------------------------------------- wgrad --
+constexpr int WTBM = 128;  // Cout per tile
+constexpr int WTBN = 128;  // K = (r, s, ci) per tile
+
+// rows m of the reduction, tracked as (n, oy, ox) and advanced by TBK per K-step
+struct MRow {
+  int n, oy, ox;
+  int64_t m;
+  __device__ __forceinline__ void init(int64_t m_, const Gather& g) {
+    m = m_;
+    const int ohw = g.OH * g.OW;
+    n = static_cast<int>(m_ / ohw);
+    const int rem = static_cast<int>(m_ - static_cast<int64_t>(n) * ohw);
+    oy = rem / g.OW;
+    ox = rem - oy * g.OW;
+  }
+  __device__ __forceinline__ void advance(int dm, const Gather& g) {
+    m += dm;
+    ox += dm;
+    while (ox >= g.OW) {
+      ox -= g.OW;
+      if (++oy == g.OH) {
+        oy = 0;
+        ++n;
+      }
+    }
+  }
+};
+
+__global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __restrict__ dY, int64_t lddy,
+                                                              Gather g, float* __restrict__ C, int64_t M, int Co,
+                                                              int tiles_n2, int ntiles, int64_t rows_per_split) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 2 * TBK * 128];
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = wg % ntiles, split = wg / ntiles;
+  const int t1 = tile / tiles_n2, t2 = tile % tiles_n2;
+  const int n1_0 = t1 * WTBM, n2_0 = t2 * WTBN;
+  const int64_t m_begin = static_cast<int64_t>(split) * rows_per_split;
+  const int64_t m_end = min(M, m_begin + rows_per_split);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int K = g.K;
+
+  // this thread's two tile positions: rows (tid >> 4) and (tid >> 4) + 16, chunk column tid & 15
+  const int ch = threadIdx.x & 15;
+  const int row0 = threadIdx.x >> 4;
+  const int kcol = n2_0 + ch * 8;
+  TapPos tp;
+  tp.init(kcol < K ? kcol : 0, g);
+  const bool kok = kcol < K;
+  const int a_col = n1_0 + ch * 8;
+  const bool a_ok = a_col < Co;
+  MRow mr[2];
+  mr[0].init(m_begin + row0, g);
+  mr[1].init(m_begin + row0 + 16, g);
+
+  auto load_b = [&](uint4* regs) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const MRow& q = mr[i];
+      const int iy = q.oy * g.sh + g.offh + tp.r, ix = q.ox * g.sw + g.offw + tp.s;
+      if (kok && q.m < m_end && static_cast<unsigned>(iy) < static_cast<unsigned>(g.Hs) &&
+          static_cast<unsigned>(ix) < static_cast<unsigned>(g.Ws))
+        regs[i] = *reinterpret_cast<const uint4*>(
+            g.src + (static_cast<int64_t>(q.n) * g.Hs * g.Ws + iy * g.Ws + ix) * g.ld + tp.c);
+      else
+        regs[i] = make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto load_a = [&](uint4* regs) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t m = mr[i].m;
+      if (a_ok && m < m_end)
+        regs[i] = *reinterpret_cast<const uint4*>(dY + m * lddy + a_col);
+      else
+        regs[i] = make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store = [&](uint16_t* lds, const uint4* regs) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<uint4*>(lds + tr_off(row0 + 16 * i, ch)) = regs[i];
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = static_cast<int>((m_end - m_begin + TBK - 1) / TBK);
+  uint4 ra[2], rb[2];
+  if (nk > 0) {
+    load_a(ra);
+    load_b(rb);
+    store(smem, ra);
+    store(smem + TBK * 128, rb);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const uint16_t* As = smem + (kt & 1) * 2 * TBK * 128;
+    const uint16_t* Bs = As + TBK * 128;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      mr[0].advance(TBK, g);
+      mr[1].advance(TBK, g);
+      load_a(ra);
+      load_b(rb);
+    }
+    const int kgrp = lane >> 4;
+    bf16x8_t af[4], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = tr_frag(As, kgrp, wm * 64 + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = tr_frag(Bs, kgrp, wn * 64 + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if (more) {
+      uint16_t* An = smem + ((kt + 1) & 1) * 2 * TBK * 128;
+      store(An, ra);
+      store(An + TBK * 128, rb);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n2_0 + wn * 64 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = n1_0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        if (row < Co && col < K) atomicAdd(C + static_cast<int64_t>(row) * K + col, acc[i][j][r]);
+      }
+    }
+  }
+}
+
+bool bad_geom(int C, int64_t ld, const void* p) {
+  return C <= 0 || (C % 8) || (ld % 8) || (reinterpret_cast<uintptr_t>(p) & 15);
+}
+
+}  // namespace
+
+// Y[N*OH*OW, Co] (row stride ldy) = conv(X [N,H,W,C] pixel stride ldx, W [Co][R][S][C]).
+// flags bit0: per-channel sum / sum-of-squares of Y into stats[2*Co] (zeroed here).
+TONY_API int tony_conv_fwd(const void* x, int N, int H, int W, int C, int64_t ldx, const void* w, int Co, int R,
+                           int S, int sh, int sw, int ph, int pw, void* y, int OH, int OW, int64_t ldy, int flags,
+                           float* stats, hipStream_t stream) {
+  if (bad_geom(C, ldx, x) || (reinterpret_cast<uintptr_t>(w) & 15) || Co <= 0 || R <= 0 || S <= 0) return -1;
+  if (OH != (H + 2 * ph - R) / sh + 1 || OW != (W + 2 * pw - S) / sw + 1 || OH <= 0 || OW <= 0) return -1;
+  const int64_t M = static_cast<int64_t>(N) * OH * OW;
+  if (M > 0x7fffffff || static_cast<int64_t>(N) * H * W > 0x7fffffff) return -1;
+  Gather g{static_cast<const uint16_t*>(x), ldx, H, W, C, OH, OW, R, S, sh, sw, -ph, -pw, 1, R * S * C};
+  return run_nt(g, w, y, ldy, M, Co, flags, stats, stream);
+}
+
+// dX[N*H*W, C] (row stride lddx) of a stride-1 conv: dY [N,OH,OW,Co] (pixel stride lddy),
+// Wt = W permuted to [C][R][S][Co].
+TONY_API int tony_conv_dgrad(const void* dy, int N, int OH, int OW, int Co, int64_t lddy, const void* wt, int C,
+                             int R, int S, int ph, int pw, void* dx, int H, int W, int64_t lddx, hipStream_t stream) {
+  if (bad_geom(Co, lddy, dy) || (reinterpret_cast<uintptr_t>(wt) & 15) || C <= 0) return -1;
+  if (OH != H + 2 * ph - R + 1 || OW != W + 2 * pw - S + 1) return -1;  // stride 1 only
+  const int64_t M = static_cast<int64_t>(N) * H * W;
+  if (M > 0x7fffffff || static_cast<int64_t>(N) * OH * OW > 0x7fffffff) return -1;
+  Gather g{static_cast<const uint16_t*>(dy), lddy, OH, OW, Co, H, W, R, S, 1, 1, ph, pw, -1, R * S * Co};
+  return run_nt(g, wt, dx, lddx, M, C, 0, nullptr, stream);
+}
+
+// dW (fp32 [Co][R][S][C], zeroed here) = dY^T im2col(X); dY [N*OH*OW, Co] row stride lddy.
+TONY_API int tony_conv_wgrad(const void* dy, int64_t lddy, const void* x, int N, int H, int W, int C, int64_t ldx,
+                             int Co, int R, int S, int sh, int sw, int ph, int pw, int OH, int OW, float* dw,
+                             int num_cus, hipStream_t stream) {
+  if (bad_geom(C, ldx, x) || (Co % 8) || (lddy % 8) || (reinterpret_cast<uintptr_t>(dy) & 15)) return -1;
+  if (OH != (H + 2 * ph - R) / sh + 1 || OW != (W + 2 * pw - S) / sw + 1) return -1;
+  const int K = R * S * C;
+  const int64_t M = static_cast<int64_t>(N) * OH * OW;
+  if (M > 0x7fffffff) return -1;
+  (void)hipMemsetAsync(dw, 0, sizeof(float) * Co * K, stream);
+  Gather g{static_cast<const uint16_t*>(x), ldx, H, W, C, OH, OW, R, S, sh, sw, -ph, -pw, 1, K};
+  const int tiles_n1 = ceil_div(Co, WTBM), tiles_n2 = ceil_div(K, WTBN);
+  const int ntiles = tiles_n1 * tiles_n2;
+  const int target = 2 * (num_cus > 0 ? num_cus : 256);
+  int64_t splits = (target + ntiles - 1) / ntiles;
+  const int64_t max_splits = (M + 8 * TBK - 1) / (8 * TBK);
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  int64_t rows = (M + splits - 1) / splits;
+  rows = (rows + TBK - 1) / TBK * TBK;
+  splits = (M + rows - 1) / rows;
+  const int64_t grid = splits * ntiles;
+  if (grid > 0x7fffffff) return -2;
+  conv_wgrad_kernel<<<static_cast<int>(grid), kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(dy), lddy, g, dw, M, Co, tiles_n2, ntiles, rows);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}

@@ -17,30 +17,12 @@
 //    of `lds_off`.
 //  * Workgroup ids are remapped so that consecutive output tiles (which share
 //    an A row-panel) are dispatched onto the same XCD and hit its private L2.
-#include "common.h"
+#include "mfma_common.h"
 
 using namespace tony;
+using namespace tony::mfma;
 
 namespace {
-
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int kThreads = 256;
-constexpr int BK = 64;
-
-// Element offset of 16-byte chunk `ch` (0..7) of LDS row `row` (64 bf16 = 128 B).
-// Bank check for one ds_read_b128 lane group (rows r, chunks c fixed per half):
-// bank slot = ((r&1)*32 + (c^(r&7))*4) mod 64 -> 16 distinct slots for 16 rows.
-__device__ __forceinline__ int lds_off(int row, int ch) { return row * BK + ((ch ^ (row & 7)) << 3); }
-
-// Bijective XCD-aware remap: workgroups dispatched round-robin over 8 XCDs get
-// contiguous tile ids per XCD.
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  const int q = nwg / 8, r = nwg % 8;
-  const int xcd = bid % 8, local = bid / 8;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
-}
 
 template <int ROWS>
 __device__ __forceinline__ void load_tile(uint4* regs, const uint16_t* __restrict__ G, int64_t ld, int row0,
@@ -135,62 +117,9 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(const uint16_t* __res
     __syncthreads();
   }
 
-  // Epilogue: C/D map of 16x16 MFMA: col = lane&15, row = (lane>>4)*4 + r.
-  // (1) optional BN column statistics straight from the fp32 accumulators;
-  // (2) the bf16 tile is staged through LDS (rows padded by 16 B so the four
-  //     row-groups of a wave hit different banks) and written back with
-  //     16-byte coalesced stores instead of 2-byte scattered ones.
-  if (stats != nullptr) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = n0 + wn * WN + j * 16 + (lane & 15);
-      float s = 0.f, q = 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = acc[i][j][r];
-          s += v;
-          q = fmaf(v, v, q);
-        }
-      // rows >= M were zero-filled, so they add nothing to the column sums
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
-      if (lane < 16 && col < N) {
-        atomicAdd(stats + col, s);
-        atomicAdd(stats + N + col, q);
-      }
-    }
-  }
-  constexpr int LDC = BN + 8;
-  static_assert(BM * LDC <= 2 * (BM + BN) * BK, "C staging tile must fit in the LDS buffers");
-  uint16_t* Cs = smem;  // the K loop ended with a barrier: both buffers are free
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wm * WM + i * 16 + (lane >> 4) * 4 + r;
-        const int col = wn * WN + j * 16 + (lane & 15);
-        Cs[row * LDC + col] = f2bf(acc[i][j][r]);
-      }
-  __syncthreads();
-  constexpr int CHUNKS = BM * BN / 8;
-  for (int v = threadIdx.x; v < CHUNKS; v += kThreads) {
-    const int row = v / (BN / 8), ch = v % (BN / 8);
-    const int grow = m0 + row, gcol = n0 + ch * 8;
-    if (grow >= M || gcol >= N) continue;
-    const uint16_t* src = Cs + row * LDC + ch * 8;
-    uint16_t* dst = C + static_cast<int64_t>(grow) * ldc + gcol;
-    if (gcol + 8 <= N && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
-      *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
-    } else {
-      for (int e = 0; e < 8 && gcol + e < N; ++e) dst[e] = src[e];
-    }
-  }
+  // Epilogue (mfma_common.h): BN column statistics from the fp32 accumulators, then the bf16
+  // tile staged through LDS and written back with 16-byte coalesced stores.
+  nt_epilogue<BM, BN, TM, TN>(acc, smem, C, ldc, M, N, m0, n0, stats);
 }
 
 template <int BM, int BN>
@@ -239,16 +168,8 @@ TONY_API int tony_gemm_bf16(const void* A, const void* B, void* C, int64_t M, in
 // ---------------------------------------------------------------------------
 namespace {
 
-typedef short v4i16 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
-
-constexpr int TBK = 32;    // m rows per K-step
 constexpr int TBM = 128;   // n1 (Cout) per tile
 constexpr int TBN = 128;   // n2 (Cin) per tile
-
-__device__ __forceinline__ int tr_swz(int row) { return (((row & 3) | (((row >> 3) & 1) << 2)) << 1); }
-// element offset of 16-byte chunk `ch` (0..15) of row `row` in a [TBK][128] bf16 tile
-__device__ __forceinline__ int tr_off(int row, int ch) { return row * 128 + ((ch ^ tr_swz(row)) << 3); }
 
 __device__ __forceinline__ void tn_load(uint4* regs, const uint16_t* __restrict__ G, int64_t ld, int64_t m0,
                                         int64_t m1, int c0, int ncols) {
@@ -273,21 +194,6 @@ __device__ __forceinline__ void tn_store(uint16_t* lds, const uint4* regs) {
     const int row = v >> 4, ch = v & 15;
     *reinterpret_cast<uint4*>(lds + tr_off(row, ch)) = regs[i];
   }
-}
-
-// MFMA operand fragment (8 consecutive m for one column) via two transposed reads.
-__device__ __forceinline__ bf16x8_t tr_frag(const uint16_t* lds, int kgrp, int col0, int lane) {
-  const int q = (lane & 15) >> 2, p = lane & 3;
-  const int col = col0 + 4 * p;          // this lane supplies row q, columns 4p..4p+3
-  const int ch = col >> 3, half = (col >> 2) & 1;
-  const int r0 = kgrp * 8 + q;
-  const uint16_t* a0 = lds + tr_off(r0, ch) + half * 4;
-  const uint16_t* a1 = lds + tr_off(r0 + 4, ch) + half * 4;
-  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0));
-  v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a1));
-  typedef short v8i16 __attribute__((ext_vector_type(8)));
-  v8i16 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8_t, r);
 }
 
 __global__ __launch_bounds__(kThreads) void gemm_tn_splitk_kernel(

@@ -1,0 +1,118 @@
+// Building blocks shared by the MFMA GEMM (gemm.hip) and the implicit-GEMM
+// convolutions (conv.hip): operand typedefs, LDS swizzles, the XCD-aware tile
+// remap and the transposed-LDS fragment read.
+#pragma once
+
+#include "common.h"
+
+namespace tony {
+namespace mfma {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+constexpr int kThreads = 256;
+constexpr int BK = 64;  // K depth of one NT K-step (LDS rows of 64 bf16 = 128 B)
+
+// Element offset of 16-byte chunk `ch` (0..7) of LDS row `row` (64 bf16 = 128 B).
+// Bank check for one ds_read_b128 lane group (rows r, chunks c fixed per half):
+// bank slot = ((r&1)*32 + (c^(r&7))*4) mod 64 -> 16 distinct slots for 16 rows.
+__device__ __forceinline__ int lds_off(int row, int ch) { return row * BK + ((ch ^ (row & 7)) << 3); }
+
+// Bijective XCD-aware remap: workgroups dispatched round-robin over 8 XCDs get
+// contiguous tile ids per XCD (tiles sharing an operand panel share an L2).
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = bid % 8, local = bid / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+}
+
+// ---- "TN" operands: tiles staged row-major over the reduction dim ([m][col], 256-B rows) and read
+// with gfx950's transposing LDS read ds_read_b64_tr_b16.  Chunk c of LDS row r lives at c ^ s(r),
+// s(r) = 2*((r&3) | ((r>>3)&1)<<2): the eight rows a 32-lane half reads in one instruction land on
+// 8 disjoint chunk pairs = all 64 banks once (conflict free).
+constexpr int TBK = 32;    // reduction rows per TN K-step
+__device__ __forceinline__ int tr_swz(int row) { return (((row & 3) | (((row >> 3) & 1) << 2)) << 1); }
+__device__ __forceinline__ int tr_off(int row, int ch) { return row * 128 + ((ch ^ tr_swz(row)) << 3); }
+
+// MFMA operand fragment (8 consecutive reduction rows for one column) via two transposed reads.
+__device__ __forceinline__ bf16x8_t tr_frag(const uint16_t* lds, int kgrp, int col0, int lane) {
+  const int q = (lane & 15) >> 2, p = lane & 3;
+  const int col = col0 + 4 * p;          // this lane supplies row q, columns 4p..4p+3
+  const int ch = col >> 3, half = (col >> 2) & 1;
+  const int r0 = kgrp * 8 + q;
+  const uint16_t* a0 = lds + tr_off(r0, ch) + half * 4;
+  const uint16_t* a1 = lds + tr_off(r0 + 4, ch) + half * 4;
+  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0));
+  v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a1));
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  v8i16 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, r);
+}
+
+// NT epilogue: optional per-column BN statistics from the fp32 accumulators, then the bf16 tile
+// staged through LDS (rows padded by 16 B) and written with 16-byte coalesced stores.
+// acc layout of 16x16 MFMA: col = lane&15, row = (lane>>4)*4 + r.
+template <int BM, int BN, int TM, int TN>
+__device__ __forceinline__ void nt_epilogue(f32x4 (&acc)[TM][TN], uint16_t* smem, uint16_t* __restrict__ C,
+                                            int64_t ldc, int M, int N, int m0, int n0, float* __restrict__ stats) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  if (stats != nullptr) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * WN + j * 16 + (lane & 15);
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = acc[i][j][r];
+          s += v;
+          q = fmaf(v, v, q);
+        }
+      // rows >= M were zero-filled, so they add nothing to the column sums
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lane < 16 && col < N) {
+        atomicAdd(stats + col, s);
+        atomicAdd(stats + N + col, q);
+      }
+    }
+  }
+  constexpr int LDC = BN + 8;
+  static_assert(BM * LDC <= 2 * (BM + BN) * BK, "C staging tile must fit in the LDS buffers");
+  uint16_t* Cs = smem;  // the K loop ended with a barrier: both buffers are free
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * WM + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * WN + j * 16 + (lane & 15);
+        Cs[row * LDC + col] = f2bf(acc[i][j][r]);
+      }
+  __syncthreads();
+  constexpr int CHUNKS = BM * BN / 8;
+  for (int v = threadIdx.x; v < CHUNKS; v += kThreads) {
+    const int row = v / (BN / 8), ch = v % (BN / 8);
+    const int grow = m0 + row, gcol = n0 + ch * 8;
+    if (grow >= M || gcol >= N) continue;
+    const uint16_t* src = Cs + row * LDC + ch * 8;
+    uint16_t* dst = C + static_cast<int64_t>(grow) * ldc + gcol;
+    if (gcol + 8 <= N && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+      *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+    } else {
+      for (int e = 0; e < 8 && gcol + e < N; ++e) dst[e] = src[e];
+    }
+  }
+}
+
+}  // namespace mfma
+}  // namespace tony

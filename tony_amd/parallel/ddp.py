@@ -108,8 +108,7 @@ class BucketedAllReduce:
             return
         if not self._armed:
             self._arm()
-        s = self.flat.slots[i]
-        view = self.flat.grad[s.offset:s.offset + s.numel].view(s.shape)
+        view = self.flat.slots[i].view(self.flat.grad)
         if p.grad is not None and p.grad.data_ptr() != view.data_ptr():
             view.copy_(p.grad)  # user code replaced .grad (e.g. zero_grad(set_to_none=True))
             p.grad = view

@@ -21,6 +21,14 @@ class Slot:
     offset: int
     numel: int
     shape: torch.Size
+    channels_last: bool = False  # 4-D conv weight kept in [Co][R][S][Ci] memory order
+
+    def view(self, buf: torch.Tensor) -> torch.Tensor:
+        flat = buf[self.offset:self.offset + self.numel]
+        if self.channels_last:
+            co, ci, r, s = self.shape
+            return flat.view(co, r, s, ci).permute(0, 3, 1, 2)
+        return flat.view(self.shape)
 
 
 class FlatParams:
@@ -33,7 +41,10 @@ class FlatParams:
         self.slots = []
         off = 0
         for name, p in params:
-            self.slots.append(Slot(name, off, p.numel(), p.shape))
+            # conv weights of a channels_last model stay channels_last: the implicit-GEMM convs read
+            # them as [Co][R][S][Ci] and write dW in that order, with no per-step transposes
+            cl = p.dim() == 4 and p.is_contiguous(memory_format=torch.channels_last) and not p.is_contiguous()
+            self.slots.append(Slot(name, off, p.numel(), p.shape, cl))
             off += (p.numel() + align - 1) // align * align  # keep every view 16B aligned
         self.numel_unpadded = off
         chunk = world * align
@@ -46,10 +57,10 @@ class FlatParams:
         self.params = []
         with torch.no_grad():
             for slot, (_, p) in zip(self.slots, params):
-                view = self.data[slot.offset:slot.offset + slot.numel].view(slot.shape)
+                view = slot.view(self.data)
                 view.copy_(p.detach().to(device=device, dtype=dtype))
                 p.data = view
-                p.grad = self.grad[slot.offset:slot.offset + slot.numel].view(slot.shape)
+                p.grad = slot.view(self.grad)
                 self.params.append(p)
 
     @property
@@ -66,7 +77,7 @@ class FlatParams:
     def rebind_grads(self):
         """Re-point ``p.grad`` at the flat buffer (after user code replaced them)."""
         for slot, p in zip(self.slots, self.params):
-            p.grad = self.grad[slot.offset:slot.offset + slot.numel].view(slot.shape)
+            p.grad = slot.view(self.grad)
 
     def master_copy(self, rank: int = 0) -> torch.Tensor:
         return self.shard(self.data, rank).float().clone()
