@@ -58,11 +58,17 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--find", action="store_true")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--tony", action="store_true", help="time tony_amd's implicit-GEMM kernels instead")
+    ap.add_argument("--skip-1x1", action="store_true")
     a = ap.parse_args()
     torch.backends.cudnn.benchmark = a.find
     dev = torch.device("cuda")
     rows = []
+    from tony_amd.ops import conv as tc
+
     for (n, cin, h, w, cout, k, s, p), count in collect_shapes(a.model, a.batch).items():
+        if a.skip_1x1 and k == (1, 1):
+            continue
         x = torch.randn(n, cin, h, w, device=dev, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
         wt = torch.randn(cout, cin, *k, device=dev, dtype=torch.bfloat16).contiguous(
             memory_format=torch.channels_last)
@@ -70,18 +76,26 @@ def main():
         dy = torch.randn_like(y)
         oh, ow = y.shape[2], y.shape[3]
         flop = 2.0 * n * oh * ow * cout * cin * k[0] * k[1]
-        f = time_ms(lambda: torch.nn.functional.conv2d(x, wt, None, s, p), a.iters)
-        d = time_ms(lambda: torch.ops.aten.convolution_backward(dy, x, wt, None, s, p, (1, 1), False, (0, 0), 1,
-                                                                (True, False, False)), a.iters)
-        g = time_ms(lambda: torch.ops.aten.convolution_backward(dy, x, wt, None, s, p, (1, 1), False, (0, 0), 1,
-                                                                (False, True, False)), a.iters)
+        if a.tony:
+            if not tc.supported(x, wt):
+                continue
+            f = time_ms(lambda: tc.conv_fwd(x, wt, s, p), a.iters)
+            d = time_ms(lambda: tc.conv_dgrad(dy, wt, x.shape, s, p), a.iters)
+            g = time_ms(lambda: tc.conv_wgrad(dy, x, wt.shape, s, p), a.iters)
+        else:
+            f = time_ms(lambda: torch.nn.functional.conv2d(x, wt, None, s, p), a.iters)
+            d = time_ms(lambda: torch.ops.aten.convolution_backward(dy, x, wt, None, s, p, (1, 1), False, (0, 0),
+                                                                    1, (True, False, False)), a.iters)
+            g = time_ms(lambda: torch.ops.aten.convolution_backward(dy, x, wt, None, s, p, (1, 1), False, (0, 0),
+                                                                    1, (False, True, False)), a.iters)
         rows.append(dict(shape=f"{n}x{cin}x{h}x{w}->{cout} k{k[0]}x{k[1]} s{s[0]} p{p[0]},{p[1]}", count=count,
                          fwd_ms=f, dgrad_ms=d, wgrad_ms=g, total_ms=count * (f + d + g),
                          fwd_tf=flop / f / 1e9, dgrad_tf=flop / d / 1e9, wgrad_tf=flop / g / 1e9))
         del x, wt, y, dy
     rows.sort(key=lambda r: -r["total_ms"])
     tot = sum(r["total_ms"] for r in rows)
-    print(f"model {a.model} batch {a.batch} find={a.find}: {len(rows)} shapes, {tot:.2f} ms/step in convs")
+    print(f"model {a.model} batch {a.batch} {'tony' if a.tony else 'MIOpen'} find={a.find}: {len(rows)} shapes, "
+          f"{tot:.2f} ms/step in convs")
     print("| shape | n | fwd ms (TF/s) | dgrad ms (TF/s) | wgrad ms (TF/s) | total ms |")
     print("|---|---|---|---|---|---|")
     for r in rows:
