@@ -195,8 +195,19 @@ int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int6
            hipStream_t stream) {
   float* st = (flags & 1) ? stats : nullptr;
   if (st != nullptr) (void)hipMemsetAsync(st, 0, sizeof(float) * 2 * N, stream);
-  if (N <= 64) return launch_nt<256, 64>(g, B, C, ldc, M, N, st, stream);
-  return launch_nt<128, 128>(g, B, C, ldc, M, N, st, stream);
+  // Column tile = the output channels split evenly over ceil(N/192) tiles, rounded up to the
+  // 32-column granule of the 2x2 wave layout (16-wide MFMA per wave): no MFMA work is spent on
+  // padding columns for Cout = 32..384 (Inception's 48/80/96/160/192/320/384).
+  const int64_t ntn = (N + 191) / 192;
+  const int64_t bn = ((N + ntn - 1) / ntn + 31) / 32 * 32;
+  switch (bn) {
+    case 32: return launch_nt<256, 32>(g, B, C, ldc, M, N, st, stream);
+    case 64: return launch_nt<256, 64>(g, B, C, ldc, M, N, st, stream);
+    case 96: return launch_nt<128, 96>(g, B, C, ldc, M, N, st, stream);
+    case 128: return launch_nt<128, 128>(g, B, C, ldc, M, N, st, stream);
+    case 160: return launch_nt<128, 160>(g, B, C, ldc, M, N, st, stream);
+    default: return launch_nt<128, 192>(g, B, C, ldc, M, N, st, stream);
+  }
 }
 
 // ---------------------------------------------------------------- wgrad --
