@@ -25,10 +25,16 @@ def _pair(v):
     return tuple(v) if isinstance(v, (tuple, list)) else (int(v), int(v))
 
 
+MIN_ROWS = 2048  # below this many output pixels a tile grid cannot fill 256 CUs: leave it to MIOpen
+
+
 def supported(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, dilation=1, groups=1) -> bool:
-    return (x.is_cuda and x.dtype == _BF16 and weight.dtype == _BF16 and x.dim() == 4 and groups == 1
+    if not (x.is_cuda and x.dtype == _BF16 and weight.dtype == _BF16 and x.dim() == 4 and groups == 1
             and _pair(dilation) == (1, 1) and x.shape[1] % 8 == 0 and weight.shape[0] % 8 == 0
-            and weight.shape[1] == x.shape[1])
+            and weight.shape[1] == x.shape[1]):
+        return False
+    oh, ow = out_hw(x.shape[2], x.shape[3], weight.shape[2], weight.shape[3], stride, padding)
+    return x.shape[0] * oh * ow >= MIN_ROWS
 
 
 def out_hw(h, w, r, s, stride, padding):

@@ -239,36 +239,48 @@ struct MRow {
   }
 };
 
+// One workgroup = a (TBM x 128) tile of dW over Cout x (r, s, ci), reducing WK rows of m per stage
+// (WK/32 MFMA K-steps per barrier) over its split of the M rows.  TBM follows Cout (32 / 64 / 128)
+// so the 3-channel-free stems (Cout 32/64) waste no MFMA rows; both operand tiles are staged in
+// 256-B LDS rows and read with the transposing ds_read (tr_frag).
+constexpr int WK = 64;
+
+template <int TBM>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __restrict__ dY, int64_t lddy,
                                                               Gather g, float* __restrict__ C, int64_t M, int Co,
                                                               int tiles_n2, int ntiles, int64_t rows_per_split) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 2 * TBK * 128];
+  constexpr int TM = TBM / 32;                 // 16-row MFMA tiles per wave along Cout (2 waves)
+  constexpr int A_CH = TBM / 8;                // 16-B chunks per dY row in the tile
+  constexpr int AV = (WK * A_CH + kThreads - 1) / kThreads;
+  constexpr int BV = WK * 16 / kThreads;       // gathered X: WK rows x 16 chunks
+  constexpr int TILE = WK * 128;               // elements per staged operand
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 2 * TILE];
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int tile = wg % ntiles, split = wg / ntiles;
   const int t1 = tile / tiles_n2, t2 = tile % tiles_n2;
-  const int n1_0 = t1 * WTBM, n2_0 = t2 * WTBN;
+  const int n1_0 = t1 * TBM, n2_0 = t2 * WTBN;
   const int64_t m_begin = static_cast<int64_t>(split) * rows_per_split;
   const int64_t m_end = min(M, m_begin + rows_per_split);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int K = g.K;
 
-  // this thread's two tile positions: rows (tid >> 4) and (tid >> 4) + 16, chunk column tid & 15
-  const int ch = threadIdx.x & 15;
-  const int row0 = threadIdx.x >> 4;
-  const int kcol = n2_0 + ch * 8;
-  TapPos tp;
-  tp.init(kcol < K ? kcol : 0, g);
+  // B (gathered X): this thread's chunk column tid & 15, rows (tid >> 4) + 16 i
+  const int bch = threadIdx.x & 15;
+  const int brow = threadIdx.x >> 4;
+  const int kcol = n2_0 + bch * 8;
   const bool kok = kcol < K;
-  const int a_col = n1_0 + ch * 8;
-  const bool a_ok = a_col < Co;
-  MRow mr[2];
-  mr[0].init(m_begin + row0, g);
-  mr[1].init(m_begin + row0 + 16, g);
+  TapPos tp;
+  tp.init(kok ? kcol : 0, g);
+  MRow mr[BV];
+#pragma unroll
+  for (int i = 0; i < BV; ++i) mr[i].init(m_begin + brow + 16 * i, g);
+  // A (dY): chunk v = tid + 256 i -> row v / A_CH, chunk v % A_CH
+  int64_t arow_m = m_begin;
 
   auto load_b = [&](uint4* regs) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < BV; ++i) {
       const MRow& q = mr[i];
       const int iy = q.oy * g.sh + g.offh + tp.r, ix = q.ox * g.sw + g.offw + tp.s;
       if (kok && q.m < m_end && static_cast<unsigned>(iy) < static_cast<unsigned>(g.Hs) &&
@@ -281,73 +293,110 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __
   };
   auto load_a = [&](uint4* regs) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int64_t m = mr[i].m;
-      if (a_ok && m < m_end)
-        regs[i] = *reinterpret_cast<const uint4*>(dY + m * lddy + a_col);
+    for (int i = 0; i < AV; ++i) {
+      const int v = threadIdx.x + i * kThreads;
+      const int row = v / A_CH, ch = v % A_CH;
+      const int64_t m = arow_m + row;
+      const int col = n1_0 + ch * 8;
+      if (v < WK * A_CH && col < Co && m < m_end)
+        regs[i] = *reinterpret_cast<const uint4*>(dY + m * lddy + col);
       else
         regs[i] = make_uint4(0, 0, 0, 0);
     }
   };
-  auto store = [&](uint16_t* lds, const uint4* regs) {
+  auto store_a = [&](uint16_t* lds, const uint4* regs) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) *reinterpret_cast<uint4*>(lds + tr_off(row0 + 16 * i, ch)) = regs[i];
+    for (int i = 0; i < AV; ++i) {
+      const int v = threadIdx.x + i * kThreads;
+      if (v < WK * A_CH) *reinterpret_cast<uint4*>(lds + tr_off(v / A_CH, v % A_CH)) = regs[i];
+    }
+  };
+  auto store_b = [&](uint16_t* lds, const uint4* regs) {
+#pragma unroll
+    for (int i = 0; i < BV; ++i) *reinterpret_cast<uint4*>(lds + tr_off(brow + 16 * i, bch)) = regs[i];
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[TM][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = static_cast<int>((m_end - m_begin + TBK - 1) / TBK);
-  uint4 ra[2], rb[2];
+  const int nk = static_cast<int>((m_end - m_begin + WK - 1) / WK);
+  uint4 ra[AV], rb[BV];
   if (nk > 0) {
     load_a(ra);
     load_b(rb);
-    store(smem, ra);
-    store(smem + TBK * 128, rb);
+    store_a(smem, ra);
+    store_b(smem + TILE, rb);
   }
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    const uint16_t* As = smem + (kt & 1) * 2 * TBK * 128;
-    const uint16_t* Bs = As + TBK * 128;
+    const uint16_t* As = smem + (kt & 1) * 2 * TILE;
+    const uint16_t* Bs = As + TILE;
     const bool more = kt + 1 < nk;
     if (more) {
-      mr[0].advance(TBK, g);
-      mr[1].advance(TBK, g);
+#pragma unroll
+      for (int i = 0; i < BV; ++i) mr[i].advance(WK, g);
+      arow_m += WK;
       load_a(ra);
       load_b(rb);
     }
-    const int kgrp = lane >> 4;
-    bf16x8_t af[4], bfr[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = tr_frag(As, kgrp, wm * 64 + i * 16, lane);
+    for (int sub = 0; sub < WK / 32; ++sub) {
+      const int kgrp = (lane >> 4) + sub * 4;  // 8-row group within the WK-row stage
+      bf16x8_t af[TM], bfr[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bfr[j] = tr_frag(Bs, kgrp, wn * 64 + j * 16, lane);
+      for (int i = 0; i < TM; ++i) af[i] = tr_frag(As, kgrp, wm * (TBM / 2) + i * 16, lane);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) bfr[j] = tr_frag(Bs, kgrp, wn * 64 + j * 16, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
     if (more) {
-      uint16_t* An = smem + ((kt + 1) & 1) * 2 * TBK * 128;
-      store(An, ra);
-      store(An + TBK * 128, rb);
+      uint16_t* An = smem + ((kt + 1) & 1) * 2 * TILE;
+      store_a(An, ra);
+      store_b(An + TILE, rb);
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < TM; ++i) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int col = n2_0 + wn * 64 + j * 16 + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = n1_0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        const int row = n1_0 + wm * (TBM / 2) + i * 16 + (lane >> 4) * 4 + r;
         if (row < Co && col < K) atomicAdd(C + static_cast<int64_t>(row) * K + col, acc[i][j][r]);
       }
     }
   }
+}
+
+template <int TBM>
+int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, int64_t M, int Co, int num_cus,
+                 hipStream_t stream) {
+  const int tiles_n1 = ceil_div(Co, TBM), tiles_n2 = ceil_div(g.K, WTBN);
+  const int ntiles = tiles_n1 * tiles_n2;
+  // enough workgroups for ~2 per CU, each reducing >= 8 stages of WK rows
+  const int target = 2 * (num_cus > 0 ? num_cus : 256);
+  int64_t splits = (target + ntiles - 1) / ntiles;
+  const int64_t max_splits = (M + 8 * WK - 1) / (8 * WK);
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  int64_t rows = (M + splits - 1) / splits;
+  rows = (rows + WK - 1) / WK * WK;
+  splits = (M + rows - 1) / rows;
+  const int64_t grid = splits * ntiles;
+  if (grid > 0x7fffffff) return -2;
+  conv_wgrad_kernel<TBM><<<static_cast<int>(grid), kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(dy), lddy, g, dw, M, Co, tiles_n2, ntiles, rows);
+  TONY_LAUNCH_CHECK();
+  return 0;
 }
 
 bool bad_geom(int C, int64_t ld, const void* p) {
@@ -392,20 +441,7 @@ TONY_API int tony_conv_wgrad(const void* dy, int64_t lddy, const void* x, int N,
   if (M > 0x7fffffff) return -1;
   (void)hipMemsetAsync(dw, 0, sizeof(float) * Co * K, stream);
   Gather g{static_cast<const uint16_t*>(x), ldx, H, W, C, OH, OW, R, S, sh, sw, -ph, -pw, 1, K};
-  const int tiles_n1 = ceil_div(Co, WTBM), tiles_n2 = ceil_div(K, WTBN);
-  const int ntiles = tiles_n1 * tiles_n2;
-  const int target = 2 * (num_cus > 0 ? num_cus : 256);
-  int64_t splits = (target + ntiles - 1) / ntiles;
-  const int64_t max_splits = (M + 8 * TBK - 1) / (8 * TBK);
-  if (splits > max_splits) splits = max_splits;
-  if (splits < 1) splits = 1;
-  int64_t rows = (M + splits - 1) / splits;
-  rows = (rows + TBK - 1) / TBK * TBK;
-  splits = (M + rows - 1) / rows;
-  const int64_t grid = splits * ntiles;
-  if (grid > 0x7fffffff) return -2;
-  conv_wgrad_kernel<<<static_cast<int>(grid), kThreads, 0, stream>>>(
-      static_cast<const uint16_t*>(dy), lddy, g, dw, M, Co, tiles_n2, ntiles, rows);
-  TONY_LAUNCH_CHECK();
-  return 0;
+  if (Co <= 32) return launch_wgrad<32>(dy, lddy, g, dw, M, Co, num_cus, stream);
+  if (Co <= 64) return launch_wgrad<64>(dy, lddy, g, dw, M, Co, num_cus, stream);
+  return launch_wgrad<128>(dy, lddy, g, dw, M, Co, num_cus, stream);
 }

@@ -22,6 +22,10 @@ def classify(name):
         return "tony HIP: fused BN+ReLU"
     if "gemm_nt_kernel" in n or "gemm_tn_splitk" in n:
         return "tony HIP: MFMA GEMM (1x1 conv fwd/dgrad/wgrad)"
+    if "conv_nt_kernel" in n or "conv_wgrad_kernel" in n:
+        return "tony HIP: implicit-GEMM conv (fwd/dgrad/wgrad)"
+    if "add_f32_kernel" in n:
+        return "tony HIP: in-place grad accumulate"
     if "box3_kernel" in n or "maxpool_" in n:
         return "tony HIP: pooling"
     if "sgd_kernel" in n or "adam_kernel" in n or "grad_stats" in n:
