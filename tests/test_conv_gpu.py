@@ -39,7 +39,7 @@ def test_conv_fwd_dgrad_wgrad(cuda, shape):
     wt = _nhwc(torch.randn(co, ci, r, s, device=cuda) / (ci * r * s) ** 0.5).to(torch.bfloat16)
     xr, wr = x.float().requires_grad_(True), wt.float().requires_grad_(True)
     yr = torch.nn.functional.conv2d(xr, wr, None, st, (ph, pw))
-    stats = torch.empty(2 * co, device=cuda)
+    stats = torch.zeros(2 * co, device=cuda)  # accumulated into: zero on entry
     y = conv_fwd(x, wt, st, (ph, pw), stats)
     assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
     assert _rel(y, yr) < 1e-2, f"fwd rel {_rel(y, yr):.4f}"

@@ -11,6 +11,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
+from .arena import zeros_f32
 
 
 def _rows_view(t: torch.Tensor):
@@ -69,7 +70,7 @@ class _BNActFn(torch.autograd.Function):
         pb = int(weight is not None and weight.dtype == torch.bfloat16)
         stream = _lib.stream_ptr(x.device)
         if training:
-            ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+            ws = zeros_f32(2 * C, x.device)
             mean = torch.empty(C, dtype=torch.float32, device=x.device)
             invstd = torch.empty(C, dtype=torch.float32, device=x.device)
             rc = L.tony_bn_fwd_train(x.data_ptr(), M, C, ldx, y.data_ptr(), ldy, _lib.ptr(weight), _lib.ptr(bias),
@@ -97,7 +98,7 @@ class _BNActFn(torch.autograd.Function):
         dy, (_, _, lddy) = _as_rows(dy)
         dx = _empty_like_rows(x)
         _, _, lddx = _rows_view(dx)
-        ws = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+        ws = zeros_f32(2 * C, x.device)
         gw, gb = _lib.grad_slot(ctx.params[0]), _lib.grad_slot(ctx.params[1])
         inplace = gw is not None and gb is not None
         if inplace:

@@ -16,6 +16,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
+from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 
 _BF16 = torch.bfloat16
@@ -96,7 +97,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride=1, paddin
     n, _, h, w = x.shape
     _, _, r, s = weight_shape
     (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
-    dw = torch.empty((co, r, s, c), dtype=torch.float32, device=x.device)
+    dw = zeros_f32(co * r * s * c, x.device).view(co, r, s, c)  # split-K atomics accumulate into it
     rc = _lib.lib().tony_conv_wgrad(dy.data_ptr(), lddy, x.data_ptr(), n, h, w, c, ldx, co, r, s, sh, sw, ph, pw,
                                     dy.shape[2], dy.shape[3], dw.data_ptr(), _lib.num_cus(x.device),
                                     _lib.stream_ptr(x.device))
@@ -152,7 +153,7 @@ class _ConvBNActFn(torch.autograd.Function):
         dev = x.device
         stream = _lib.stream_ptr(dev)
         co = weight.shape[0]
-        stats = torch.empty(2 * co, dtype=torch.float32, device=dev) if training else None
+        stats = zeros_f32(2 * co, dev) if training else None
         Z = conv_fwd(x, weight, stride, padding, stats)
         M, _, ldz = _rows_view(Z)
         y = torch.empty_like(Z)
@@ -183,7 +184,7 @@ class _ConvBNActFn(torch.autograd.Function):
         M, co, ldz = _rows_view(Z)
         dy, (_, _, lddy) = _as_rows(dy)
         dZ = torch.empty_like(Z)
-        ws = torch.empty(2 * co, dtype=torch.float32, device=dev)
+        ws = zeros_f32(2 * co, dev)
         gg, gb = _lib.grad_slot(ctx.params[1]), _lib.grad_slot(ctx.params[2])
         inplace = gg is not None and gb is not None
         dgamma = gg if inplace else torch.empty_like(gamma)

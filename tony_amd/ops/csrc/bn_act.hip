@@ -362,16 +362,10 @@ bool bad_c(int C) { return C <= 0 || C % 8 != 0 || C > kMaxC; }
 
 // ---- composable entry points (the fused conv heads call these on channel sub-ranges) ----
 
-// sum/sumsq[C] are zeroed here and accumulated over the M rows of x.
+// sum/sumsq[C] (zero on entry: the caller zeroes them, ops/arena.py) accumulate over the M rows of x.
 TONY_API int tony_bn_stats(const void* x, int64_t M, int C, int64_t ldx, float* sum, float* sumsq,
                            hipStream_t stream) {
   if (bad_c(C) || (ldx % 8)) return -1;
-  if (sumsq == sum + C) {
-    (void)hipMemsetAsync(sum, 0, sizeof(float) * 2 * C, stream);
-  } else {
-    (void)hipMemsetAsync(sum, 0, sizeof(float) * C, stream);
-    (void)hipMemsetAsync(sumsq, 0, sizeof(float) * C, stream);
-  }
   int64_t rpb;
   int grid;
   plan_rows(M, C, 8, 512, &rpb, &grid);  // few WGs: C atomics per WG contend per channel
@@ -418,12 +412,6 @@ TONY_API int tony_bn_bwd_reduce(const void* x, int64_t ldx, const void* dy, int6
                                 const float* mean, const float* invstd, const void* gamma, const void* beta,
                                 int param_bf16, int relu, float* dsum, float* dsumx, hipStream_t stream) {
   if (bad_c(C) || (ldx % 8) || (lddy % 8)) return -1;
-  if (dsumx == dsum + C) {
-    (void)hipMemsetAsync(dsum, 0, sizeof(float) * 2 * C, stream);
-  } else {
-    (void)hipMemsetAsync(dsum, 0, sizeof(float) * C, stream);
-    (void)hipMemsetAsync(dsumx, 0, sizeof(float) * C, stream);
-  }
   int64_t rpb;
   int grid;
   plan_rows(M, C, 8, 512, &rpb, &grid);  // few WGs: C atomics per WG contend per channel
@@ -488,7 +476,6 @@ TONY_API int tony_bn_bwd_res(const void* x, int64_t ldx, const void* dy, int64_t
                              const float* invstd, const void* gamma, const void* beta, int param_bf16,
                              float* dsums_ws, void* dgamma, void* dbeta, int accumulate, hipStream_t stream) {
   if (bad_c(C) || (ldx % 8) || (lddy % 8) || (ldy % 8) || (lddx % 8) || (lddr % 8) || y == nullptr) return -1;
-  (void)hipMemsetAsync(dsums_ws, 0, sizeof(float) * 2 * C, stream);
   int64_t rpb;
   int grid;
   plan_rows(M, C, 8, 512, &rpb, &grid);

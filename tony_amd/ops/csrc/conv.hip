@@ -193,8 +193,7 @@ int launch_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, i
 
 int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, int flags, float* stats,
            hipStream_t stream) {
-  float* st = (flags & 1) ? stats : nullptr;
-  if (st != nullptr) (void)hipMemsetAsync(st, 0, sizeof(float) * 2 * N, stream);
+  float* st = (flags & 1) ? stats : nullptr;  // accumulated into: the caller zeroes it (ops/arena.py)
   // Column tile = the output channels split evenly over ceil(N/192) tiles, rounded up to the
   // 32-column granule of the 2x2 wave layout (16-wide MFMA per wave): no MFMA work is spent on
   // padding columns for Cout = 32..384 (Inception's 48/80/96/160/192/320/384).
@@ -406,7 +405,7 @@ bool bad_geom(int C, int64_t ld, const void* p) {
 }  // namespace
 
 // Y[N*OH*OW, Co] (row stride ldy) = conv(X [N,H,W,C] pixel stride ldx, W [Co][R][S][C]).
-// flags bit0: per-channel sum / sum-of-squares of Y into stats[2*Co] (zeroed here).
+// flags bit0: per-channel sum / sum-of-squares of Y into stats[2*Co] (zero on entry).
 TONY_API int tony_conv_fwd(const void* x, int N, int H, int W, int C, int64_t ldx, const void* w, int Co, int R,
                            int S, int sh, int sw, int ph, int pw, void* y, int OH, int OW, int64_t ldy, int flags,
                            float* stats, hipStream_t stream) {
@@ -430,7 +429,7 @@ TONY_API int tony_conv_dgrad(const void* dy, int N, int OH, int OW, int Co, int6
   return run_nt(g, wt, dx, lddx, M, C, 0, nullptr, stream);
 }
 
-// dW (fp32 [Co][R][S][C], zeroed here) = dY^T im2col(X); dY [N*OH*OW, Co] row stride lddy.
+// dW (fp32 [Co][R][S][C], zero on entry) = dY^T im2col(X); dY [N*OH*OW, Co] row stride lddy.
 TONY_API int tony_conv_wgrad(const void* dy, int64_t lddy, const void* x, int N, int H, int W, int C, int64_t ldx,
                              int Co, int R, int S, int sh, int sw, int ph, int pw, int OH, int OW, float* dw,
                              int num_cus, hipStream_t stream) {
@@ -439,7 +438,6 @@ TONY_API int tony_conv_wgrad(const void* dy, int64_t lddy, const void* x, int N,
   const int K = R * S * C;
   const int64_t M = static_cast<int64_t>(N) * OH * OW;
   if (M > 0x7fffffff) return -1;
-  (void)hipMemsetAsync(dw, 0, sizeof(float) * Co * K, stream);
   Gather g{static_cast<const uint16_t*>(x), ldx, H, W, C, OH, OW, R, S, sh, sw, -ph, -pw, 1, K};
   if (Co <= 32) return launch_wgrad<32>(dy, lddy, g, dw, M, Co, num_cus, stream);
   if (Co <= 64) return launch_wgrad<64>(dy, lddy, g, dw, M, Co, num_cus, stream);

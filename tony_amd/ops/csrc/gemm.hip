@@ -137,7 +137,7 @@ int launch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int6
 
 }  // namespace
 
-// flags bit0: compute column statistics into stats[2N] (zeroed here).
+// flags bit0: compute column statistics into stats[2N] (zero on entry).
 TONY_API int tony_gemm_bf16(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
                             int64_t ldb, int64_t ldc, int flags, float* stats, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return -1;
@@ -145,7 +145,7 @@ TONY_API int tony_gemm_bf16(const void* A, const void* B, void* C, int64_t M, in
   if (M > 0x7fffffff || N > 0x7fffffff) return -1;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -1;
   float* st = (flags & 1) ? stats : nullptr;
-  if (st != nullptr) (void)hipMemsetAsync(st, 0, sizeof(float) * 2 * N, stream);
+  // st is accumulated into with atomics: the caller hands it over zeroed (ops/arena.py)
   if (N <= 64) return launch<256, 64>(A, lda, B, ldb, C, ldc, M, N, K, st, stream);
   return launch<128, 128>(A, lda, B, ldb, C, ldc, M, N, K, st, stream);
 }
@@ -268,13 +268,13 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_splitk_kernel(
 
 }  // namespace
 
-// C (fp32, [N1, N2], zeroed here) = A^T B ; A [M, N1] (lda), B [M, N2] (ldb).
+// C (fp32, [N1, N2], zero on entry) = A^T B ; A [M, N1] (lda), B [M, N2] (ldb).
 TONY_API int tony_gemm_tn_bf16(const void* A, const void* B, float* C, int64_t M, int64_t N1, int64_t N2,
                                int64_t lda, int64_t ldb, int64_t ldc, int num_cus, hipStream_t stream) {
   if (M <= 0 || N1 <= 0 || N2 <= 0) return -1;
   if ((N1 % 8) || (N2 % 8) || (lda % 8) || (ldb % 8)) return -1;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -1;
-  (void)hipMemsetAsync(C, 0, sizeof(float) * N1 * ldc, stream);
+  // C is accumulated into with atomics: the caller hands it over zeroed (ops/arena.py)
   const int tiles_n1 = ceil_div(N1, TBM), tiles_n2 = ceil_div(N2, TBN);
   const int ntiles = tiles_n1 * tiles_n2;
   // enough workgroups for ~2 per CU, each reducing >= 8 K-steps

@@ -33,6 +33,7 @@ import torch
 from torch import nn
 
 from . import _lib
+from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 from .gemm import wgrad_tn
 
@@ -62,7 +63,7 @@ class _HeadFn(torch.autograd.Function):
             w2 = w2.contiguous()
         pb = int(gamma.dtype == _BF16)
         Z = _cl_empty(n, ctot, h, w, dev)
-        stats = torch.empty(2 * ctot, dtype=torch.float32, device=dev)
+        stats = zeros_f32(2 * ctot, dev)  # the GEMM epilogue accumulates [sum | sumsq] into it
         rc = L.tony_gemm_bf16(x.data_ptr(), w2.data_ptr(), Z.data_ptr(), M, ctot, cin, ldx, cin, ctot,
                               1 if training else 0, stats.data_ptr(), stream)
         _lib.check(rc, "tony_gemm_bf16")
@@ -89,12 +90,15 @@ class _HeadFn(torch.autograd.Function):
             P = _cl_empty(n, npool, h, w, dev)
             rc = L.tony_avgpool3_s1p1(_off(Z, c0), P.data_ptr(), n, h, w, npool, ctot, npool, stream)
             _lib.check(rc, "tony_avgpool3_s1p1")
-            if training:
-                rc = L.tony_bn_stats(P.data_ptr(), M, npool, npool, _off(stats, c0), _off(stats, ctot + c0), stream)
+            pstats = None
+            if training:  # statistics of the pooled tensor (the GEMM's columns c0.. are pre-pool)
+                pstats = zeros_f32(2 * npool, dev)
+                rc = L.tony_bn_stats(P.data_ptr(), M, npool, npool, pstats.data_ptr(), _off(pstats, npool), stream)
                 _lib.check(rc, "tony_bn_stats")
             y = _cl_empty(n, npool, h, w, dev)
-            rc = L.tony_bn_apply(P.data_ptr(), M, npool, npool, y.data_ptr(), npool, _off(stats, c0),
-                                 _off(stats, ctot + c0), _off(gamma, c0), _off(beta, c0), pb, float(eps), 1, mode,
+            rc = L.tony_bn_apply(P.data_ptr(), M, npool, npool, y.data_ptr(), npool, _lib.ptr(pstats),
+                                 _off(pstats, npool) if training else 0, _off(gamma, c0), _off(beta, c0), pb,
+                                 float(eps), 1, mode,
                                  _off(mean, c0) if training else 0, _off(invstd, c0) if training else 0,
                                  _off(running_mean, c0), _off(running_var, c0), float(momentum), stream)
             _lib.check(rc, "tony_bn_apply")
@@ -117,7 +121,7 @@ class _HeadFn(torch.autograd.Function):
         ctot = weight.shape[0]
         pb = ctx.pb
         dZ = _cl_empty(n, ctot, h, w, dev)
-        dsum = torch.empty(2 * ctot, dtype=torch.float32, device=dev)
+        dsum = zeros_f32(2 * ctot, dev)  # each split's BN-backward reduction accumulates into its slice
         gw, gg, gb = (_lib.grad_slot(p) for p in ctx.params)
         inplace = gw is not None and gg is not None and gb is not None
         acc = int(inplace)

@@ -12,6 +12,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
+from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 
 
@@ -29,6 +30,8 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, s
         raise ValueError(f"inner dims differ: {a.shape} x {b.shape}^T")
     if out is None:
         out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if stats is not None:
+        stats.zero_()  # the epilogue accumulates into it
     rc = _lib.lib().tony_gemm_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0) if M > 1 else K,
                                    b.stride(0) if N > 1 else K, out.stride(0) if M > 1 else N,
                                    1 if stats is not None else 0, _lib.ptr(stats), _lib.stream_ptr(a.device))
@@ -44,7 +47,7 @@ def _gemm_rows(a_ptr, lda, b, M, N, K, out_ptr, ldc, device):
 
 def wgrad_tn(a_ptr, lda, b_ptr, ldb, M, n1, n2, device) -> torch.Tensor:
     """fp32 [n1, n2] = A^T B for row-major A [M, n1], B [M, n2] (split-K MFMA kernel)."""
-    out = torch.empty((n1, n2), dtype=torch.float32, device=device)
+    out = zeros_f32(n1 * n2, device).view(n1, n2)  # split-K atomics accumulate into it
     rc = _lib.lib().tony_gemm_tn_bf16(a_ptr, b_ptr, out.data_ptr(), M, n1, n2, lda, ldb, n2, _lib.num_cus(device),
                                       _lib.stream_ptr(device))
     _lib.check(rc, "tony_gemm_tn_bf16")

@@ -18,6 +18,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib
+from .arena import zeros_f32
 from .bn import _as_rows, _empty_like_rows, _rows_view
 from .fused import _cl_empty
 from .gemm import wgrad_tn
@@ -51,7 +52,7 @@ def _bwd_res(L, z, ldz, dy, y, M, C, mean, invstd, gamma, beta, pb, params, stre
     dz = _empty_like_rows(y)
     _, _, lddz = _rows_view(dz)
     dres = _empty_like_rows(y) if want_dres else None
-    ws = torch.empty(2 * C, dtype=torch.float32, device=dev)
+    ws = zeros_f32(2 * C, dev)
     gg, gb = _lib.grad_slot(params[0]), _lib.grad_slot(params[1])
     inplace = gg is not None and gb is not None
     dgamma = gg if inplace else torch.empty_like(gamma)
@@ -76,7 +77,7 @@ class _BNAddReLUFn(torch.autograd.Function):
         pb = int(gamma.dtype == _BF16)
         stats = None
         if training:
-            stats = torch.empty(2 * C, dtype=torch.float32, device=z.device)
+            stats = zeros_f32(2 * C, z.device)
             rc = L.tony_bn_stats(z.data_ptr(), M, C, ldz, stats.data_ptr(), stats.data_ptr() + 4 * C, stream)
             _lib.check(rc, "tony_bn_stats")
         mean, invstd = _bn_stats_and_apply(L, z, ldz, M, C, res, ldr, y, ldy, gamma, beta, pb, eps, training,
@@ -110,7 +111,7 @@ class _Conv1x1BNAddReLUFn(torch.autograd.Function):
         if w2.stride(0) != cin or w2.stride(1) != 1:
             w2 = w2.contiguous()
         Z = _cl_empty(n, cout, h, w, dev)
-        stats = torch.empty(2 * cout, dtype=torch.float32, device=dev)
+        stats = zeros_f32(2 * cout, dev)
         rc = L.tony_gemm_bf16(x.data_ptr(), w2.data_ptr(), Z.data_ptr(), M, cout, cin, ldx, cin, cout,
                               1 if training else 0, stats.data_ptr(), stream)
         _lib.check(rc, "tony_gemm_bf16")

@@ -14,6 +14,7 @@ from typing import Callable
 
 import torch
 
+from ..ops.arena import for_device
 from ..utils.tracing import heartbeat, trace_range
 from .ps import ParameterServer
 
@@ -31,8 +32,11 @@ class Trainer:
         self.static_y = None
         self.static_loss = None
         self._eager_steps = 0
+        dev = ps.flat.device
+        # one zero-fill per step for every fused kernel's fp32 accumulators (ops/arena.py)
+        self.arena = for_device(dev) if dev.type == "cuda" else None
 
-    def _eager_step(self, x, y):
+    def _body(self, x, y):
         self.ps.zero_grad()
         with trace_range("forward"):
             out = self.model(x)
@@ -41,6 +45,14 @@ class Trainer:
             loss.backward()
         with trace_range("ps push/apply/pull"):
             self.ps.step()
+        return loss
+
+    def _eager_step(self, x, y):
+        if self.arena is not None:
+            with self.arena:
+                loss = self._body(x, y)
+        else:
+            loss = self._body(x, y)
         heartbeat()
         return loss.detach()
 
@@ -83,11 +95,11 @@ class Trainer:
         g = torch.cuda.CUDAGraph()
         self._refresh_hp()
         with torch.cuda.graph(g):
-            self.ps.zero_grad()
-            out = self.model(self.static_x)
-            loss = self.loss_fn(out, self.static_y)
-            loss.backward()
-            self.ps.step()
+            if self.arena is not None:
+                with self.arena:  # its one fill is a node of the graph; the slices keep their addresses
+                    loss = self._body(self.static_x, self.static_y)
+            else:
+                loss = self._body(self.static_x, self.static_y)
             self.static_loss = loss.detach()
         self.ps.steps -= 1  # the capture itself did not train
         for opt in self.ps.optimizers.values():
