@@ -151,6 +151,7 @@ def main():
                 "optimizer": "fused SGD-momentum (HIP)" if args.optimizer == "sgd" else args.optimizer,
                 "hip_graph": not args.no_graph,
                 "kernels": "stock-comparator" if args.stock else "tony_amd HIP",
+                "conv_impl": _conv_impl_counts(),
                 "final_loss": round(final_loss, 4),
             },
         }
@@ -158,6 +159,16 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def _conv_impl_counts():
+    """How many (pass, shape) conv problems the autotuner gave to tony_amd's kernels vs MIOpen."""
+    from tony_amd.ops.conv import choices
+
+    out = {}
+    for (pas, *_), impl in choices().items():
+        out[f"{pas}:{impl}"] = out.get(f"{pas}:{impl}", 0) + 1
+    return out
 
 
 if __name__ == "__main__":

@@ -2,16 +2,25 @@
 
 ``conv2d(x, weight, stride, padding)`` is a drop-in for ``F.conv2d`` on channels_last bf16 CUDA
 tensors with ``Cin % 8 == 0`` (every Inception-v3 / ResNet-50 conv but the 3-channel stems):
-forward, backward-data (stride 1; strided convs use MIOpen's backward-data) and split-K
-backward-weight are tony_amd kernels.
+forward, backward-data (stride 1) and split-K backward-weight are tony_amd kernels.
 
 ``conv_bn_act(x, weight, bn...)`` fuses the BatchNorm that follows: the forward GEMM epilogue
 produces the per-channel sums of its output, so the separate statistics pass over the conv
 output disappears; the apply kernel normalises (+ReLU); the backward is the fused BN backward
 followed by the dgrad / wgrad GEMMs on dZ.  Parameter gradients are accumulated in place into the
 flat gradient buffer when ``_lib.set_inplace_grads`` is on (the trainer's default).
+
+Per-shape selection.  For each (pass, shape) the first eager call times the tony kernel against
+MIOpen's solution on the real operands (the forward candidate pays for its BN statistics: MIOpen's
+output needs a separate ``tony_bn_stats`` pass) and caches the faster one -- the cudnn.benchmark
+idea applied across implementations.  Stride-2 backward-data has no tony kernel.  Decisions made
+before a HIP-graph capture are replayed by the capture; ``TONY_CONV_AUTOTUNE=0`` pins everything
+to the tony kernels.
 """
 from __future__ import annotations
+
+import os
+from typing import Callable, Dict, Tuple
 
 import torch
 
@@ -20,6 +29,8 @@ from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 
 _BF16 = torch.bfloat16
+AUTOTUNE = os.environ.get("TONY_CONV_AUTOTUNE", "1") != "0"
+_CHOICE: Dict[Tuple, str] = {}
 
 
 def _pair(v):
@@ -58,7 +69,9 @@ def _cl_empty(n, c, h, w, device):
     return torch.empty((n, c, h, w), dtype=_BF16, device=device, memory_format=torch.channels_last)
 
 
+# ---------------------------------------------------------------------------- tony kernels --
 def conv_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: torch.Tensor | None = None):
+    """Y = conv(x, w); with ``stats`` (zeroed, 2*Cout floats) the epilogue accumulates [sum | sumsq] of Y."""
     x, (_, C, ldx) = _as_rows(x)
     n, _, h, w = x.shape
     co, _, r, s = weight.shape
@@ -74,12 +87,10 @@ def conv_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: 
 
 
 def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, padding=0) -> torch.Tensor:
+    if _pair(stride) != (1, 1):
+        return _miopen_dgrad(dy, weight, x_shape, stride, padding)
     n, c, h, w = x_shape
     co, _, r, s = weight.shape
-    if _pair(stride) != (1, 1):  # strided: MIOpen's backward-data
-        xs = torch.empty(x_shape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
-        return torch.ops.aten.convolution_backward(dy, xs, weight, None, _pair(stride), _pair(padding), (1, 1),
-                                                   False, (0, 0), 1, (True, False, False))[0]
     dy, (_, _, lddy) = _as_rows(dy)
     ph, pw = _pair(padding)
     dx = _cl_empty(n, c, h, w, dy.device)
@@ -90,19 +101,113 @@ def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, paddin
     return dx
 
 
-def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride=1, padding=0) -> torch.Tensor:
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride=1, padding=0, out=None) -> torch.Tensor:
     """fp32 dW with memory [Co][R][S][Ci] (returned as a [Co, Ci, R, S] channels_last view)."""
     dy, (_, co, lddy) = _as_rows(dy)
     x, (_, c, ldx) = _as_rows(x)
     n, _, h, w = x.shape
     _, _, r, s = weight_shape
     (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
-    dw = zeros_f32(co * r * s * c, x.device).view(co, r, s, c)  # split-K atomics accumulate into it
+    # split-K atomics accumulate into it: zero on entry
+    dw = (out if out is not None else zeros_f32(co * r * s * c, x.device)).view(co, r, s, c)
     rc = _lib.lib().tony_conv_wgrad(dy.data_ptr(), lddy, x.data_ptr(), n, h, w, c, ldx, co, r, s, sh, sw, ph, pw,
                                     dy.shape[2], dy.shape[3], dw.data_ptr(), _lib.num_cus(x.device),
                                     _lib.stream_ptr(x.device))
     _lib.check(rc, "tony_conv_wgrad")
     return dw.permute(0, 3, 1, 2)
+
+
+# --------------------------------------------------------------------------------- MIOpen --
+def _miopen_fwd(x, weight, stride, padding, stats=None):
+    y = torch.nn.functional.conv2d(x, weight, None, _pair(stride), _pair(padding))
+    if not y.is_contiguous(memory_format=torch.channels_last):
+        y = y.contiguous(memory_format=torch.channels_last)
+    if stats is not None:
+        M, co, ld = _rows_view(y)
+        rc = _lib.lib().tony_bn_stats(y.data_ptr(), M, co, ld, stats.data_ptr(), stats.data_ptr() + 4 * co,
+                                      _lib.stream_ptr(y.device))
+        _lib.check(rc, "tony_bn_stats")
+    return y
+
+
+def _miopen_dgrad(dy, weight, x_shape, stride, padding):
+    xs = torch.empty(x_shape, dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
+    return torch.ops.aten.convolution_backward(dy, xs, weight, None, _pair(stride), _pair(padding), (1, 1), False,
+                                               (0, 0), 1, (True, False, False))[0]
+
+
+def _miopen_wgrad(dy, x, weight, stride, padding):
+    return torch.ops.aten.convolution_backward(dy, x, weight, None, _pair(stride), _pair(padding), (1, 1), False,
+                                               (0, 0), 1, (False, True, False))[1]
+
+
+# ------------------------------------------------------------------------------ selection --
+def _time(fn: Callable[[], object], reps: int = 3) -> float:
+    fn()
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    start.record()
+    for _ in range(reps):
+        fn()
+    end.record()
+    end.synchronize()
+    return start.elapsed_time(end) / reps
+
+
+def _choose(key: Tuple, candidates: Dict[str, Callable[[], object]], default: str = "tony") -> str:
+    c = _CHOICE.get(key)
+    if c is not None:
+        return c
+    if not AUTOTUNE or len(candidates) == 1 or torch.cuda.is_current_stream_capturing():
+        return default if default in candidates else next(iter(candidates))
+    times = {name: _time(fn) for name, fn in candidates.items()}
+    c = min(times, key=times.get)
+    _CHOICE[key] = c
+    return c
+
+
+def choices() -> Dict[Tuple, str]:
+    """The per-(pass, shape) implementation decisions made so far (for logs / profiles)."""
+    return dict(_CHOICE)
+
+
+def _fwd(x, weight, stride, padding, stats):
+    key = ("fwd", tuple(x.shape), tuple(weight.shape), stride, padding, stats is not None)
+    impl = _CHOICE.get(key)
+    if impl is None:
+        co = weight.shape[0]
+        scratch = torch.zeros(2 * co, dtype=torch.float32, device=x.device) if stats is not None else None
+        impl = _choose(key, {"tony": lambda: conv_fwd(x, weight, stride, padding, scratch),
+                             "miopen": lambda: _miopen_fwd(x, weight, stride, padding, scratch)})
+    return conv_fwd(x, weight, stride, padding, stats) if impl == "tony" else \
+        _miopen_fwd(x, weight, stride, padding, stats)
+
+
+def _dgrad(dy, weight, x_shape, stride, padding):
+    key = ("dgrad", tuple(dy.shape), tuple(weight.shape), stride, padding)
+    cands = {"miopen": lambda: _miopen_dgrad(dy, weight, x_shape, stride, padding)}
+    if _pair(stride) == (1, 1):
+        cands["tony"] = lambda: conv_dgrad(dy, weight, x_shape, stride, padding)
+    impl = _choose(key, cands)
+    return conv_dgrad(dy, weight, x_shape, stride, padding) if impl == "tony" else \
+        _miopen_dgrad(dy, weight, x_shape, stride, padding)
+
+
+def _wgrad(dy, x, weight, stride, padding):
+    """dW accumulated into the parameter's gradient slot (returns None) or returned for autograd."""
+    key = ("wgrad", tuple(dy.shape), tuple(weight.shape), stride, padding)
+    impl = _CHOICE.get(key)
+    if impl is None:
+        scratch = torch.zeros(weight.numel(), dtype=torch.float32, device=x.device)
+        impl = _choose(key, {"tony": lambda: conv_wgrad(dy, x, weight.shape, stride, padding, scratch.zero_()),
+                             "miopen": lambda: _miopen_wgrad(dy, x, weight, stride, padding)})
+    if impl == "tony":
+        return _accumulate_wgrad(weight, conv_wgrad(dy, x, weight.shape, stride, padding))
+    dw = _miopen_wgrad(dy, x, weight, stride, padding)
+    gw = _lib.grad_slot(weight)
+    if gw is None:
+        return dw
+    gw.add_(dw)
+    return None
 
 
 def _accumulate_wgrad(weight, dw32):
@@ -120,10 +225,11 @@ def _accumulate_wgrad(weight, dw32):
     return None
 
 
+# ------------------------------------------------------------------------------- autograd --
 class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, stride, padding):
-        y = conv_fwd(x, weight, stride, padding)
+        y = _fwd(x, weight, stride, padding, None)
         ctx.save_for_backward(x, weight)
         ctx.stride, ctx.padding = stride, padding
         return y
@@ -131,8 +237,9 @@ class _ConvFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
-        dx = conv_dgrad(dy, weight, x.shape, ctx.stride, ctx.padding) if ctx.needs_input_grad[0] else None
-        dw = _accumulate_wgrad(weight, conv_wgrad(dy, x, weight.shape, ctx.stride, ctx.padding))
+        dy = _as_rows(dy)[0]
+        dx = _dgrad(dy, weight, x.shape, ctx.stride, ctx.padding) if ctx.needs_input_grad[0] else None
+        dw = _wgrad(dy, x, weight, ctx.stride, ctx.padding)
         return dx, dw, None, None
 
 
@@ -154,7 +261,7 @@ class _ConvBNActFn(torch.autograd.Function):
         stream = _lib.stream_ptr(dev)
         co = weight.shape[0]
         stats = zeros_f32(2 * co, dev) if training else None
-        Z = conv_fwd(x, weight, stride, padding, stats)
+        Z = _fwd(x, weight, stride, padding, stats)
         M, _, ldz = _rows_view(Z)
         y = torch.empty_like(Z)
         pb = int(gamma.dtype == _BF16)
@@ -193,8 +300,8 @@ class _ConvBNActFn(torch.autograd.Function):
                            invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), pb, int(relu), ws.data_ptr(),
                            dgamma.data_ptr(), dbeta.data_ptr(), int(inplace), _lib.stream_ptr(dev))
         _lib.check(rc, "tony_bn_bwd")
-        dx = conv_dgrad(dZ, weight, x.shape, stride, padding) if ctx.needs_input_grad[0] else None
-        dw = _accumulate_wgrad(weight, conv_wgrad(dZ, x, weight.shape, stride, padding))
+        dx = _dgrad(dZ, weight, x.shape, stride, padding) if ctx.needs_input_grad[0] else None
+        dw = _wgrad(dZ, x, weight, stride, padding)
         if inplace:
             dgamma = dbeta = None
         return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None

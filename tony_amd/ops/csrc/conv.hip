@@ -242,7 +242,7 @@ struct MRow {
 // (WK/32 MFMA K-steps per barrier) over its split of the M rows.  TBM follows Cout (32 / 64 / 128)
 // so the 3-channel-free stems (Cout 32/64) waste no MFMA rows; both operand tiles are staged in
 // 256-B LDS rows and read with the transposing ds_read (tr_frag).
-constexpr int WK = 64;
+constexpr int WK = 32;  // 64-row stages measured slower: 2x LDS + VGPRs halve the waves hiding the gather
 
 template <int TBM>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __restrict__ dY, int64_t lddy,
