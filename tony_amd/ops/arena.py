@@ -20,9 +20,17 @@ _ALIGN = 64  # floats (256 B): every slice 16-B aligned for the kernels' vector 
 _tls = threading.local()
 
 
+def _norm(device) -> torch.device:
+    """'cuda' and 'cuda:<current>' are the same device: compare with the index filled in."""
+    d = torch.device(device)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return d
+
+
 class StepArena:
     def __init__(self, device, capacity: int = 0):
-        self.device = torch.device(device)
+        self.device = _norm(device)
         self.buf: Optional[torch.Tensor] = None
         self.capacity = 0
         self.offset = 0
@@ -86,7 +94,7 @@ def current() -> Optional[StepArena]:
 def zeros_f32(n: int, device) -> torch.Tensor:
     """A zeroed fp32 accumulator of n floats: an arena slice when a step arena is open, else torch.zeros."""
     a = current()
-    if a is not None and a.device == torch.device(device):
+    if a is not None and a.device == _norm(device):
         t = a.take(n)
         if t is not None:
             return t
@@ -97,7 +105,7 @@ _ARENAS: Dict[torch.device, StepArena] = {}
 
 
 def for_device(device) -> StepArena:
-    d = torch.device(device)
+    d = _norm(device)
     if d not in _ARENAS:
         _ARENAS[d] = StepArena(d)
     return _ARENAS[d]
