@@ -17,7 +17,10 @@ from typing import Dict, Optional
 import torch
 
 _ALIGN = 64  # floats (256 B): every slice 16-B aligned for the kernels' vector loads
-_tls = threading.local()
+# process-wide, not thread-local: autograd runs the backward of CUDA ops on its own device thread,
+# and those kernels' accumulators belong to the same step
+_CURRENT: list = [None]
+_lock = threading.Lock()
 
 
 def _norm(device) -> torch.device:
@@ -59,19 +62,20 @@ class StepArena:
         self.offset = 0
         self.need = 0
         self.active = True
-        _tls.arena = self
+        _CURRENT[0] = self
 
     def end_step(self) -> None:
         self.used_last = min(self.offset, self.capacity)
         self.active = False
-        if getattr(_tls, "arena", None) is self:
-            _tls.arena = None
+        if _CURRENT[0] is self:
+            _CURRENT[0] = None
 
     def take(self, n: int) -> Optional[torch.Tensor]:
         n_al = (n + _ALIGN - 1) // _ALIGN * _ALIGN
-        start, end = self.offset, self.offset + n_al
-        self.offset = end            # keep counting past a miss: `need` sizes the next step's arena
-        self.need = max(self.need, end)
+        with _lock:  # the forward (caller thread) and backward (autograd thread) both carve
+            start, end = self.offset, self.offset + n_al
+            self.offset = end        # keep counting past a miss: `need` sizes the next step's arena
+            self.need = max(self.need, end)
         if self.buf is None or end > self.capacity:
             self.misses += 1
             return None
@@ -87,7 +91,7 @@ class StepArena:
 
 
 def current() -> Optional[StepArena]:
-    a = getattr(_tls, "arena", None)
+    a = _CURRENT[0]
     return a if a is not None and a.active else None
 
 
