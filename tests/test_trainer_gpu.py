@@ -1,0 +1,55 @@
+"""The HIP-graph trainer: a replayed step must train exactly like the eager step, whether the
+PS push/apply/pull is captured inside the graph (1 rank) or runs eagerly after it (>1 rank)."""
+import pytest
+import torch
+from torch import nn
+
+pytestmark = pytest.mark.gpu
+
+
+class _Tiny(nn.Module):
+    def __init__(self):
+        super().__init__()
+        from tony_amd.models.layers import ConvBNAct
+        from tony_amd.ops.fused import FusedHead
+
+        self.c1 = ConvBNAct(16, 32, 3, 1, 1)
+        self.head = FusedHead(32, (32, 16), pool_cout=16)
+        self.fc = nn.Linear(64, 10)
+
+    def forward(self, x):
+        a, b, p = self.head(self.c1(x))
+        z = torch.cat([a, b, p], 1)
+        return self.fc(torch.flatten(nn.functional.adaptive_avg_pool2d(z, 1), 1))
+
+
+def _train(mode, steps=4):
+    from tony_amd.models.layers import init_weights
+    from tony_amd.ops import cross_entropy
+    from tony_amd.parallel.ps import ParameterServer
+    from tony_amd.parallel.trainer import Trainer
+
+    dev = torch.device("cuda", 0)
+    model = init_weights(_Tiny(), seed=0).to(dev).to(memory_format=torch.channels_last).train()
+    ps = ParameterServer(model, optimizer="sgd", lr=0.05, momentum=0.9, device=dev)
+    use_graph = mode != "eager"
+    tr = Trainer(model, ps, lambda o, y: cross_entropy(o, y), use_graph=use_graph, warmup_eager=1,
+                 graph_collectives=(mode == "graph_in") if use_graph else None)
+    g = torch.Generator(device=dev).manual_seed(7)
+    x = torch.randn((32, 16, 24, 24), generator=g, device=dev).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (32,), generator=g, device=dev)
+    losses = [float(tr.step(x, y).float().item()) for _ in range(steps)]
+    torch.cuda.synchronize()
+    return losses, ps.flat.data.float().clone(), ps.steps
+
+
+def test_graph_replay_matches_eager(cuda):
+    le, pe, se = _train("eager")
+    for mode in ("graph_in", "graph_out"):
+        lg, pg, sg = _train(mode)
+        assert sg == se == 4, mode
+        for a, b in zip(lg, le):
+            assert abs(a - b) <= 2e-2 * max(1.0, abs(b)), (mode, lg, le)
+        err = (pg - pe).abs().max().item()
+        assert err < 2e-2, (mode, err)

@@ -21,12 +21,17 @@ from .ps import ParameterServer
 
 class Trainer:
     def __init__(self, model: torch.nn.Module, ps: ParameterServer, loss_fn: Callable, use_graph: bool = False,
-                 warmup_eager: int = 3):
+                 warmup_eager: int = 3, graph_collectives: bool | None = None):
         self.model = model
         self.ps = ps
         self.loss_fn = loss_fn
         self.use_graph = use_graph
         self.warmup_eager = warmup_eager
+        # With >1 rank the PS push/apply/pull (RCCL reduce-scatter, one fused optimizer launch,
+        # RCCL all-gather) runs eagerly after the replayed forward+backward graph: three
+        # launches, so nothing is lost, and no communicator state is baked into the graph
+        # (RCCL's graph-capture support differs across releases).  One rank: all in the graph.
+        self.graph_collectives = (ps.world == 1) if graph_collectives is None else graph_collectives
         self.graph = None
         self.static_x = None
         self.static_y = None
@@ -36,16 +41,20 @@ class Trainer:
         # one zero-fill per step for every fused kernel's fp32 accumulators (ops/arena.py)
         self.arena = for_device(dev) if dev.type == "cuda" else None
 
-    def _body(self, x, y):
+    def _body(self, x, y, ps_step: bool = True):
         self.ps.zero_grad()
         with trace_range("forward"):
             out = self.model(x)
             loss = self.loss_fn(out, y)
         with trace_range("backward"):
             loss.backward()
+        if ps_step:
+            self._ps_step()
+        return loss
+
+    def _ps_step(self):
         with trace_range("ps push/apply/pull"):
             self.ps.step()
-        return loss
 
     def _eager_step(self, x, y):
         if self.arena is not None:
@@ -76,10 +85,13 @@ class Trainer:
             self.static_y.copy_(y, non_blocking=True)
         self._refresh_hp()
         self.graph.replay()
+        if self.graph_collectives:
+            self.ps.steps += 1
+            for opt in self.ps.optimizers.values():
+                opt.step_count += 1
+        else:
+            self._ps_step()  # eager push/apply/pull; ps.step() advances the counters itself
         heartbeat()
-        self.ps.steps += 1
-        for opt in self.ps.optimizers.values():
-            opt.step_count += 1
         return self.static_loss
 
     def _refresh_hp(self):
@@ -94,14 +106,16 @@ class Trainer:
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         self._refresh_hp()
+        inside = self.graph_collectives
         with torch.cuda.graph(g):
             if self.arena is not None:
                 with self.arena:  # its one fill is a node of the graph; the slices keep their addresses
-                    loss = self._body(self.static_x, self.static_y)
+                    loss = self._body(self.static_x, self.static_y, ps_step=inside)
             else:
-                loss = self._body(self.static_x, self.static_y)
+                loss = self._body(self.static_x, self.static_y, ps_step=inside)
             self.static_loss = loss.detach()
-        self.ps.steps -= 1  # the capture itself did not train
-        for opt in self.ps.optimizers.values():
-            opt.step_count -= 1
+        if inside:
+            self.ps.steps -= 1  # the capture itself did not train
+            for opt in self.ps.optimizers.values():
+                opt.step_count -= 1
         self.graph = g

@@ -23,6 +23,11 @@ for s in "$@"; do
     prof) export TMPDIR=/tmp; R=$(pwd)
           step prof 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 5 --no-graph --no-miopen-find ${BENCH_ARGS:-}
           python3 tools/prof_summary.py gpurun_out/prof --skip 6 > gpurun_out/prof_summary.md; find gpurun_out/prof -name '*trace*' -delete ;;
+    prof_graph) export TMPDIR=/tmp; R=$(pwd)   # the headline configuration: HIP graph + MIOpen find
+          step prof_graph 1100 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_graph" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 6 ${BENCH_ARGS:-}
+          python3 tools/prof_summary.py gpurun_out/prof_graph --skip 8 > gpurun_out/prof_graph_summary.md
+          python3 tools/prof_summary.py gpurun_out/prof_graph --skip 8 --sequence > gpurun_out/prof_graph_sequence.txt || true
+          find gpurun_out/prof_graph -name '*trace*' -delete ;;
     prof_stock) export TMPDIR=/tmp; R=$(pwd)
           step prof_stock 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_stock" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 5 --no-graph --no-miopen-find --stock
           python3 tools/prof_summary.py gpurun_out/prof_stock --skip 6 > gpurun_out/prof_stock_summary.md; find gpurun_out/prof_stock -name '*trace*' -delete ;;

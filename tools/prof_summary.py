@@ -80,6 +80,14 @@ def main():
     t0, t1 = opt_ends[skip - 1], opt_ends[-1]
     steps = len(opt_ends) - skip
     win = [(s, e, n) for s, e, n in ks if s > t0 and e <= t1]
+    if "--sequence" in sys.argv:
+        # one steady-state step in dispatch order: index, start offset, duration, gap to previous end
+        one = [(s, e, n) for s, e, n in ks if s > opt_ends[-2] and e <= t1]
+        prev = one[0][0] if one else 0
+        for i, (s, e, n) in enumerate(one):
+            print(f"{i:4d} {(s - one[0][0]) / 1e3:9.1f} {(e - s) / 1e3:8.1f} {(s - prev) / 1e3:6.1f}  {n[:110]}")
+            prev = e
+        return 0
     busy = sum(e - s for s, e, _ in win)
     wall = t1 - t0
     by_name, groups = {}, {}
