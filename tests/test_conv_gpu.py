@@ -39,8 +39,11 @@ def test_conv_fwd_dgrad_wgrad(cuda, shape):
     wt = _nhwc(torch.randn(co, ci, r, s, device=cuda) / (ci * r * s) ** 0.5).to(torch.bfloat16)
     xr, wr = x.float().requires_grad_(True), wt.float().requires_grad_(True)
     yr = torch.nn.functional.conv2d(xr, wr, None, st, (ph, pw))
-    stats = torch.zeros(2 * co, device=cuda)  # accumulated into: zero on entry
+    from tony_amd.ops import _lib
+
+    stats = torch.zeros(_lib.stat_floats(co), device=cuda)  # accumulated into: zero on entry
     y = conv_fwd(x, wt, st, (ph, pw), stats)
+    stats = _lib.fold_stats(stats, co)
     assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
     assert _rel(y, yr) < 1e-2, f"fwd rel {_rel(y, yr):.4f}"
     torch.testing.assert_close(stats[:co], yr.sum((0, 2, 3)), rtol=2e-2, atol=2e-2 * (yr.numel() / co) ** 0.5)

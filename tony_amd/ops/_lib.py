@@ -35,17 +35,20 @@ _SIGNATURES = {
                           c_float, c_int, c_void_p, c_void_p, c_void_p],
     "tony_bn_bwd": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p,
                     c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
-    "tony_bn_stats": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_void_p],
-    "tony_bn_apply": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
-                      c_int, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p],
+    # statistics buffers: shard 0 pointers + the shard stride in floats (STAT_SHARDS copies)
+    "tony_stat_shards": [],
+    "tony_bn_stats": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_int64, c_void_p],
+    "tony_bn_apply": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p,
+                      c_void_p, c_int, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
+                      c_void_p],
     "tony_bn_bwd_reduce": [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p,
-                           c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
+                           c_void_p, c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p],
     "tony_bn_bwd_apply": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p,
-                          c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                          c_int, c_void_p],
+                          c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p,
+                          c_void_p, c_int, c_void_p],
     "tony_bn_apply_res": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
-                          c_void_p, c_void_p, c_void_p, c_int, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p,
-                          c_void_p, c_float, c_void_p],
+                          c_void_p, c_int64, c_void_p, c_void_p, c_int, c_float, c_int, c_int, c_void_p, c_void_p,
+                          c_void_p, c_void_p, c_float, c_void_p],
     "tony_bn_bwd_res": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                         c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                         c_int, c_void_p],
@@ -57,13 +60,13 @@ _SIGNATURES = {
     "tony_xent_bwd": [c_void_p, c_int, c_int64, c_int, c_int64, c_void_p, c_float, c_void_p, c_void_p, c_void_p,
                       c_int64, c_void_p],
     "tony_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64,
-                       c_int, c_void_p, c_void_p],
+                       c_int, c_void_p, c_int64, c_void_p],
     "tony_gemm_tn_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64, c_int,
                           c_void_p],
     "tony_conv_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int,
-                      c_int, c_int, c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_void_p],
+                      c_int, c_int, c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_int64, c_void_p],
     "tony_conv_dgrad": [c_void_p, c_int, c_int, c_int, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int,
-                        c_void_p, c_int, c_int, c_int64, c_void_p],
+                        c_void_p, c_int, c_int, c_int64, c_int, c_void_p],
     "tony_conv_wgrad": [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int, c_int, c_int, c_int,
                         c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
     "tony_avgpool3_s1p1": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
@@ -76,6 +79,28 @@ _SIGNATURES = {
 
 class KernelError(RuntimeError):
     pass
+
+
+# BatchNorm statistics are accumulated into STAT_SHARDS copies (csrc/common.h kStatShards): a
+# statistics buffer for C channels is STAT_SHARDS x [sum C | sumsq C] floats, shard stride 2C.
+STAT_SHARDS = 8
+
+
+def stat_floats(c: int) -> int:
+    """Floats of a zeroed statistics buffer for ``c`` channels ([sum | sumsq] x STAT_SHARDS)."""
+    return STAT_SHARDS * 2 * c
+
+
+def check_stat_buffer(buf, c: int) -> None:
+    """Refuse a statistics buffer too small for the kernels' STAT_SHARDS copies (they would write past it)."""
+    if buf is not None and (buf.dtype != torch.float32 or buf.numel() < stat_floats(c) or not buf.is_contiguous()):
+        raise ValueError(f"statistics buffer for {c} channels must be {stat_floats(c)} contiguous fp32 "
+                         f"(STAT_SHARDS={STAT_SHARDS} x [sum | sumsq]); got {buf.dtype} x {buf.numel()}")
+
+
+def fold_stats(buf, c: int):
+    """[sum | sumsq] (2c floats) of a sharded statistics buffer (sums the STAT_SHARDS copies)."""
+    return buf[:stat_floats(c)].view(STAT_SHARDS, 2 * c).sum(0)
 
 
 def lib():
@@ -96,6 +121,10 @@ def lib():
                 continue
             fn.argtypes = argtypes
             fn.restype = c_int
+        n = h.tony_stat_shards()
+        if n != STAT_SHARDS:
+            raise KernelError(f"{SO_PATH} accumulates BN statistics in {n} shards, the Python side expects "
+                              f"{STAT_SHARDS}: rebuild the kernels")
         _lib = h
     return _lib
 

@@ -70,7 +70,7 @@ class _BNActFn(torch.autograd.Function):
         pb = int(weight is not None and weight.dtype == torch.bfloat16)
         stream = _lib.stream_ptr(x.device)
         if training:
-            ws = zeros_f32(2 * C, x.device)
+            ws = zeros_f32(_lib.stat_floats(C), x.device)  # STAT_SHARDS x [sum | sumsq]
             mean = torch.empty(C, dtype=torch.float32, device=x.device)
             invstd = torch.empty(C, dtype=torch.float32, device=x.device)
             rc = L.tony_bn_fwd_train(x.data_ptr(), M, C, ldx, y.data_ptr(), ldy, _lib.ptr(weight), _lib.ptr(bias),
@@ -98,7 +98,7 @@ class _BNActFn(torch.autograd.Function):
         dy, (_, _, lddy) = _as_rows(dy)
         dx = _empty_like_rows(x)
         _, _, lddx = _rows_view(dx)
-        ws = zeros_f32(2 * C, x.device)
+        ws = zeros_f32(_lib.stat_floats(C), x.device)
         gw, gb = _lib.grad_slot(ctx.params[0]), _lib.grad_slot(ctx.params[1])
         inplace = gw is not None and gb is not None
         if inplace:

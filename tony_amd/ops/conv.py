@@ -24,7 +24,7 @@ from typing import Callable, Dict, Tuple
 
 import torch
 
-from . import _lib
+from . import _lib, tune
 from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 
@@ -70,19 +70,29 @@ def _cl_empty(n, c, h, w, device):
 
 
 # ---------------------------------------------------------------------------- tony kernels --
-def conv_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: torch.Tensor | None = None):
-    """Y = conv(x, w); with ``stats`` (zeroed, 2*Cout floats) the epilogue accumulates [sum | sumsq] of Y."""
+def conv_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: torch.Tensor | None = None,
+             vflags: int | None = None):
+    """Y = conv(x, w); with ``stats`` (zeroed, ``_lib.stat_floats(Cout)`` floats) the epilogue accumulates
+    [sum | sumsq] of Y into its STAT_SHARDS copies.  ``vflags``: tile variant bits (None: autotuned)."""
     x, (_, C, ldx) = _as_rows(x)
     n, _, h, w = x.shape
     co, _, r, s = weight.shape
+    _lib.check_stat_buffer(stats, co)
     (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
     oh, ow = out_hw(h, w, r, s, stride, padding)
     y = _cl_empty(n, co, oh, ow, x.device)
     wk = _krsc(weight)
-    rc = _lib.lib().tony_conv_fwd(x.data_ptr(), n, h, w, C, ldx, wk.data_ptr(), co, r, s, sh, sw, ph, pw,
-                                  y.data_ptr(), oh, ow, co, 1 if stats is not None else 0, _lib.ptr(stats),
-                                  _lib.stream_ptr(x.device))
-    _lib.check(rc, "tony_conv_fwd")
+    L, st = _lib.lib(), _lib.stream_ptr(x.device)
+
+    def launch(vf, stats_t):
+        return L.tony_conv_fwd(x.data_ptr(), n, h, w, C, ldx, wk.data_ptr(), co, r, s, sh, sw, ph, pw, y.data_ptr(),
+                               oh, ow, co, (1 if stats_t is not None else 0) | vf, _lib.ptr(stats_t), 2 * co, st)
+
+    if vflags is None:
+        key = ("conv_fwd", tuple(x.shape), ldx, tuple(weight.shape), (sh, sw), (ph, pw), stats is not None)
+        scratch = torch.zeros(_lib.stat_floats(co), device=x.device) if stats is not None else None
+        vflags = tune.pick(key, lambda vf: launch(vf, scratch))
+    _lib.check(launch(vflags, stats), "tony_conv_fwd")
     return y
 
 
@@ -95,9 +105,14 @@ def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, paddin
     ph, pw = _pair(padding)
     dx = _cl_empty(n, c, h, w, dy.device)
     wt = _crsk(weight)
-    rc = _lib.lib().tony_conv_dgrad(dy.data_ptr(), n, dy.shape[2], dy.shape[3], co, lddy, wt.data_ptr(), c, r, s,
-                                    ph, pw, dx.data_ptr(), h, w, c, _lib.stream_ptr(dy.device))
-    _lib.check(rc, "tony_conv_dgrad")
+    L, st = _lib.lib(), _lib.stream_ptr(dy.device)
+
+    def launch(vf):
+        return L.tony_conv_dgrad(dy.data_ptr(), n, dy.shape[2], dy.shape[3], co, lddy, wt.data_ptr(), c, r, s, ph, pw,
+                                 dx.data_ptr(), h, w, c, vf, st)
+
+    vf = tune.pick(("conv_dgrad", tuple(dy.shape), lddy, tuple(weight.shape), (ph, pw)), launch)
+    _lib.check(launch(vf), "tony_conv_dgrad")
     return dx
 
 
@@ -124,7 +139,8 @@ def _miopen_fwd(x, weight, stride, padding, stats=None):
         y = y.contiguous(memory_format=torch.channels_last)
     if stats is not None:
         M, co, ld = _rows_view(y)
-        rc = _lib.lib().tony_bn_stats(y.data_ptr(), M, co, ld, stats.data_ptr(), stats.data_ptr() + 4 * co,
+        _lib.check_stat_buffer(stats, co)
+        rc = _lib.lib().tony_bn_stats(y.data_ptr(), M, co, ld, stats.data_ptr(), stats.data_ptr() + 4 * co, 2 * co,
                                       _lib.stream_ptr(y.device))
         _lib.check(rc, "tony_bn_stats")
     return y
@@ -175,7 +191,8 @@ def _fwd(x, weight, stride, padding, stats):
     impl = _CHOICE.get(key)
     if impl is None:
         co = weight.shape[0]
-        scratch = torch.zeros(2 * co, dtype=torch.float32, device=x.device) if stats is not None else None
+        scratch = torch.zeros(_lib.stat_floats(co), dtype=torch.float32, device=x.device) if stats is not None \
+            else None
         impl = _choose(key, {"tony": lambda: conv_fwd(x, weight, stride, padding, scratch),
                              "miopen": lambda: _miopen_fwd(x, weight, stride, padding, scratch)})
     return conv_fwd(x, weight, stride, padding, stats) if impl == "tony" else \
@@ -260,7 +277,7 @@ class _ConvBNActFn(torch.autograd.Function):
         dev = x.device
         stream = _lib.stream_ptr(dev)
         co = weight.shape[0]
-        stats = zeros_f32(2 * co, dev) if training else None
+        stats = zeros_f32(_lib.stat_floats(co), dev) if training else None
         Z = _fwd(x, weight, stride, padding, stats)
         M, _, ldz = _rows_view(Z)
         y = torch.empty_like(Z)
@@ -272,7 +289,8 @@ class _ConvBNActFn(torch.autograd.Function):
             mean = running_mean
             invstd = torch.rsqrt(running_var.float() + eps)
         rc = L.tony_bn_apply(Z.data_ptr(), M, co, ldz, y.data_ptr(), ldz, _lib.ptr(stats),
-                             _lib.ptr(stats) + 4 * co if training else 0, gamma.data_ptr(), beta.data_ptr(), pb,
+                             _lib.ptr(stats) + 4 * co if training else 0, 2 * co if training else 0,
+                             gamma.data_ptr(), beta.data_ptr(), pb,
                              float(eps), int(relu), 0 if training else 1, _lib.ptr(mean) if training else 0,
                              _lib.ptr(invstd) if training else 0, _lib.ptr(running_mean), _lib.ptr(running_var),
                              float(momentum), stream)
@@ -291,7 +309,7 @@ class _ConvBNActFn(torch.autograd.Function):
         M, co, ldz = _rows_view(Z)
         dy, (_, _, lddy) = _as_rows(dy)
         dZ = torch.empty_like(Z)
-        ws = zeros_f32(2 * co, dev)
+        ws = zeros_f32(_lib.stat_floats(co), dev)
         gg, gb = _lib.grad_slot(ctx.params[1]), _lib.grad_slot(ctx.params[2])
         inplace = gg is not None and gb is not None
         dgamma = gg if inplace else torch.empty_like(gamma)

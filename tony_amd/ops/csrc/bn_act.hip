@@ -79,7 +79,7 @@ __device__ __forceinline__ void block_reduce_add(float* red, const RowMap& rm, i
 
 __global__ __launch_bounds__(kThreads) void bn_fwd_stats_kernel(
     const uint16_t* __restrict__ x, int64_t M, int C, int64_t ldx, int64_t rows_per_block,
-    float* __restrict__ sum, float* __restrict__ sumsq) {
+    float* __restrict__ sum, float* __restrict__ sumsq, int64_t sstride) {
   __shared__ float red[kMaxC * 2];
   RowMap rm(C);
   float s[8], q[8];
@@ -116,7 +116,8 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_stats_kernel(
       }
     }
   }
-  block_reduce_add(red, rm, C, s, q, sum, sumsq);
+  const int64_t so = shard_off(blockIdx.x, sstride);
+  block_reduce_add(red, rm, C, s, q, sum + so, sumsq + so);
 }
 
 // mode 0: training (stats from sums, saves mean/invstd, updates running stats)
@@ -127,7 +128,7 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
     const uint16_t* __restrict__ x, int64_t M, int C, int64_t ldx, int64_t rows_per_block,
     const uint16_t* __restrict__ res, int64_t ldr,
     uint16_t* __restrict__ y, int64_t ldy, const float* __restrict__ sum, const float* __restrict__ sumsq,
-    const void* gamma, const void* beta, int param_bf16, float eps, int relu, int mode,
+    int64_t sstride, const void* gamma, const void* beta, int param_bf16, float eps, int relu, int mode,
     float* __restrict__ save_mean, float* __restrict__ save_invstd,
     float* __restrict__ running_mean, float* __restrict__ running_var, float momentum) {
   __shared__ float scale[kMaxC];
@@ -136,8 +137,8 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
   for (int c = threadIdx.x; c < C; c += kThreads) {
     float mean, invstd;
     if (mode == 0) {
-      mean = sum[c] * inv_m;
-      float var = fmaxf(sumsq[c] * inv_m - mean * mean, 0.f);
+      mean = shard_sum(sum, c, sstride) * inv_m;
+      float var = fmaxf(shard_sum(sumsq, c, sstride) * inv_m - mean * mean, 0.f);
       invstd = rsqrtf(var + eps);
       if (blockIdx.x == 0) {
         save_mean[c] = mean;
@@ -206,7 +207,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     const uint16_t* __restrict__ ym, int64_t ldym,
     int64_t M, int C, int64_t rows_per_block, const float* __restrict__ mean,
     const float* __restrict__ invstd, const void* gamma, const void* beta, int param_bf16,
-    int relu, float* __restrict__ dsum, float* __restrict__ dsumx) {
+    int relu, float* __restrict__ dsum, float* __restrict__ dsumx, int64_t sstride) {
   __shared__ float red[kMaxC * 2];
   RowMap rm(C);
   float a[8], b[8];
@@ -261,7 +262,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
       body(load8(x + r * ldx + rm.cg * 8), load8(dy + r * lddy + rm.cg * 8),
            YMASK ? load8(ym + r * ldym + rm.cg * 8) : none);
   }
-  block_reduce_add(red, rm, C, a, b, dsum, dsumx);
+  const int64_t so = shard_off(blockIdx.x, sstride);
+  block_reduce_add(red, rm, C, a, b, dsum + so, dsumx + so);
 }
 
 // YMASK: mask dy by the saved output y and also write the masked dy -- the
@@ -273,17 +275,18 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     uint16_t* __restrict__ dx, int64_t lddx, int64_t M, int C, int64_t rows_per_block,
     const float* __restrict__ mean, const float* __restrict__ invstd, const void* gamma,
     const void* beta, int param_bf16, int relu, const float* __restrict__ dsum,
-    const float* __restrict__ dsumx, void* dgamma, void* dbeta, int accumulate) {
+    const float* __restrict__ dsumx, int64_t sstride, void* dgamma, void* dbeta, int accumulate) {
   __shared__ float k_s[kMaxC], a_s[kMaxC], b_s[kMaxC];
   const float inv_m = 1.f / static_cast<float>(M);
   for (int c = threadIdx.x; c < C; c += kThreads) {
     const float g = load_param(gamma, c, param_bf16, 1.f);
+    const float ds = shard_sum(dsum, c, sstride), dsx = shard_sum(dsumx, c, sstride);
     k_s[c] = g * invstd[c];
-    a_s[c] = dsum[c] * inv_m;
-    b_s[c] = dsumx[c] * inv_m;
+    a_s[c] = ds * inv_m;
+    b_s[c] = dsx * inv_m;
     if (blockIdx.x == 0) {
-      store_param(dbeta, c, param_bf16, dsum[c], accumulate);
-      store_param(dgamma, c, param_bf16, dsumx[c], accumulate);
+      store_param(dbeta, c, param_bf16, ds, accumulate);
+      store_param(dgamma, c, param_bf16, dsx, accumulate);
     }
   }
   __syncthreads();
@@ -361,15 +364,22 @@ bool bad_c(int C) { return C <= 0 || C % 8 != 0 || C > kMaxC; }
 }  // namespace
 
 // ---- composable entry points (the fused conv heads call these on channel sub-ranges) ----
+//
+// Statistics buffers: sum/sumsq (and dsum/dsumx) point into shard 0 of a buffer holding
+// kStatShards copies `sstride` floats apart (sstride = 0: one copy).  Producers add into the
+// copy of their block index; consumers sum all copies (common.h).
+
+TONY_API int tony_stat_shards() { return kStatShards; }
 
 // sum/sumsq[C] (zero on entry: the caller zeroes them, ops/arena.py) accumulate over the M rows of x.
-TONY_API int tony_bn_stats(const void* x, int64_t M, int C, int64_t ldx, float* sum, float* sumsq,
+TONY_API int tony_bn_stats(const void* x, int64_t M, int C, int64_t ldx, float* sum, float* sumsq, int64_t sstride,
                            hipStream_t stream) {
-  if (bad_c(C) || (ldx % 8)) return -1;
+  if (bad_c(C) || (ldx % 8) || sstride < 0) return -1;
   int64_t rpb;
   int grid;
   plan_rows(M, C, 8, 512, &rpb, &grid);  // few WGs: C atomics per WG contend per channel
-  bn_fwd_stats_kernel<<<grid, kThreads, 0, stream>>>(static_cast<const uint16_t*>(x), M, C, ldx, rpb, sum, sumsq);
+  bn_fwd_stats_kernel<<<grid, kThreads, 0, stream>>>(static_cast<const uint16_t*>(x), M, C, ldx, rpb, sum, sumsq,
+                                                      sstride);
   TONY_LAUNCH_CHECK();
   return 0;
 }
@@ -377,47 +387,49 @@ TONY_API int tony_bn_stats(const void* x, int64_t M, int C, int64_t ldx, float* 
 // mode 0 (train): normalise with the batch stats in sum/sumsq, save mean/invstd,
 // update running stats; mode 1 (eval): use running_mean/var.
 TONY_API int tony_bn_apply(const void* x, int64_t M, int C, int64_t ldx, void* y, int64_t ldy, const float* sum,
-                           const float* sumsq, const void* gamma, const void* beta, int param_bf16, float eps,
-                           int relu, int mode, float* save_mean, float* save_invstd, float* running_mean,
+                           const float* sumsq, int64_t sstride, const void* gamma, const void* beta, int param_bf16,
+                           float eps, int relu, int mode, float* save_mean, float* save_invstd, float* running_mean,
                            float* running_var, float momentum, hipStream_t stream) {
-  if (bad_c(C) || (ldx % 8) || (ldy % 8)) return -1;
+  if (bad_c(C) || (ldx % 8) || (ldy % 8) || sstride < 0) return -1;
   int64_t rpb;
   int grid;
   plan_rows(M, C, 4, 8192, &rpb, &grid);
   bn_fwd_apply_kernel<false><<<grid, kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), M, C, ldx, rpb, nullptr, 0, static_cast<uint16_t*>(y), ldy, sum, sumsq,
-      gamma, beta, param_bf16, eps, relu, mode, save_mean, save_invstd, running_mean, running_var, momentum);
+      sstride, gamma, beta, param_bf16, eps, relu, mode, save_mean, save_invstd, running_mean, running_var, momentum);
   TONY_LAUNCH_CHECK();
   return 0;
 }
 
 // y = act(bn(x) + res): the bottleneck tail (conv3 -> BN -> + identity -> ReLU) in one pass.
 TONY_API int tony_bn_apply_res(const void* x, int64_t M, int C, int64_t ldx, const void* res, int64_t ldr, void* y,
-                               int64_t ldy, const float* sum, const float* sumsq, const void* gamma, const void* beta,
-                               int param_bf16, float eps, int relu, int mode, float* save_mean, float* save_invstd,
-                               float* running_mean, float* running_var, float momentum, hipStream_t stream) {
-  if (bad_c(C) || (ldx % 8) || (ldy % 8) || (ldr % 8) || res == nullptr) return -1;
+                               int64_t ldy, const float* sum, const float* sumsq, int64_t sstride, const void* gamma,
+                               const void* beta, int param_bf16, float eps, int relu, int mode, float* save_mean,
+                               float* save_invstd, float* running_mean, float* running_var, float momentum,
+                               hipStream_t stream) {
+  if (bad_c(C) || (ldx % 8) || (ldy % 8) || (ldr % 8) || res == nullptr || sstride < 0) return -1;
   int64_t rpb;
   int grid;
   plan_rows(M, C, 4, 8192, &rpb, &grid);
   bn_fwd_apply_kernel<true><<<grid, kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), M, C, ldx, rpb, static_cast<const uint16_t*>(res), ldr,
-      static_cast<uint16_t*>(y), ldy, sum, sumsq, gamma, beta, param_bf16, eps, relu, mode, save_mean, save_invstd,
-      running_mean, running_var, momentum);
+      static_cast<uint16_t*>(y), ldy, sum, sumsq, sstride, gamma, beta, param_bf16, eps, relu, mode, save_mean,
+      save_invstd, running_mean, running_var, momentum);
   TONY_LAUNCH_CHECK();
   return 0;
 }
 
 TONY_API int tony_bn_bwd_reduce(const void* x, int64_t ldx, const void* dy, int64_t lddy, int64_t M, int C,
                                 const float* mean, const float* invstd, const void* gamma, const void* beta,
-                                int param_bf16, int relu, float* dsum, float* dsumx, hipStream_t stream) {
-  if (bad_c(C) || (ldx % 8) || (lddy % 8)) return -1;
+                                int param_bf16, int relu, float* dsum, float* dsumx, int64_t sstride,
+                                hipStream_t stream) {
+  if (bad_c(C) || (ldx % 8) || (lddy % 8) || sstride < 0) return -1;
   int64_t rpb;
   int grid;
   plan_rows(M, C, 8, 512, &rpb, &grid);  // few WGs: C atomics per WG contend per channel
   bn_bwd_reduce_kernel<false><<<grid, kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, nullptr, 0, M, C, rpb, mean,
-      invstd, gamma, beta, param_bf16, relu, dsum, dsumx);
+      invstd, gamma, beta, param_bf16, relu, dsum, dsumx, sstride);
   TONY_LAUNCH_CHECK();
   return 0;
 }
@@ -425,37 +437,38 @@ TONY_API int tony_bn_bwd_reduce(const void* x, int64_t ldx, const void* dy, int6
 TONY_API int tony_bn_bwd_apply(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx, int64_t lddx,
                                int64_t M, int C, const float* mean, const float* invstd, const void* gamma,
                                const void* beta, int param_bf16, int relu, const float* dsum, const float* dsumx,
-                               void* dgamma, void* dbeta, int accumulate, hipStream_t stream) {
-  if (bad_c(C) || (ldx % 8) || (lddy % 8) || (lddx % 8)) return -1;
+                               int64_t sstride, void* dgamma, void* dbeta, int accumulate, hipStream_t stream) {
+  if (bad_c(C) || (ldx % 8) || (lddy % 8) || (lddx % 8) || sstride < 0) return -1;
   int64_t rpb;
   int grid;
   plan_rows(M, C, 4, 8192, &rpb, &grid);
   bn_bwd_apply_kernel<false><<<grid, kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, nullptr, 0, nullptr, 0,
-      static_cast<uint16_t*>(dx), lddx, M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsum, dsumx, dgamma,
-      dbeta, accumulate);
+      static_cast<uint16_t*>(dx), lddx, M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsum, dsumx, sstride,
+      dgamma, dbeta, accumulate);
   TONY_LAUNCH_CHECK();
   return 0;
 }
 
-// ---- one-call forms used by BatchNormAct2d ----
+// ---- one-call forms used by BatchNormAct2d: the workspace holds kStatShards x 2C floats, zeroed ----
 
 TONY_API int tony_bn_fwd_train(const void* x, int64_t M, int C, int64_t ldx, void* y, int64_t ldy,
                                const void* gamma, const void* beta, int param_bf16, float eps,
                                int relu, float* sums_ws, float* save_mean, float* save_invstd,
                                float* running_mean, float* running_var, float momentum,
                                hipStream_t stream) {
-  int rc = tony_bn_stats(x, M, C, ldx, sums_ws, sums_ws + C, stream);
+  const int64_t ss = 2 * static_cast<int64_t>(C);
+  int rc = tony_bn_stats(x, M, C, ldx, sums_ws, sums_ws + C, ss, stream);
   if (rc) return rc;
-  return tony_bn_apply(x, M, C, ldx, y, ldy, sums_ws, sums_ws + C, gamma, beta, param_bf16, eps, relu, 0, save_mean,
-                       save_invstd, running_mean, running_var, momentum, stream);
+  return tony_bn_apply(x, M, C, ldx, y, ldy, sums_ws, sums_ws + C, ss, gamma, beta, param_bf16, eps, relu, 0,
+                       save_mean, save_invstd, running_mean, running_var, momentum, stream);
 }
 
 TONY_API int tony_bn_fwd_infer(const void* x, int64_t M, int C, int64_t ldx, void* y, int64_t ldy,
                                const void* gamma, const void* beta, int param_bf16, float eps,
                                int relu, const float* running_mean, const float* running_var,
                                hipStream_t stream) {
-  return tony_bn_apply(x, M, C, ldx, y, ldy, nullptr, nullptr, gamma, beta, param_bf16, eps, relu, 1, nullptr,
+  return tony_bn_apply(x, M, C, ldx, y, ldy, nullptr, nullptr, 0, gamma, beta, param_bf16, eps, relu, 1, nullptr,
                        nullptr, const_cast<float*>(running_mean), const_cast<float*>(running_var), 0.f, stream);
 }
 
@@ -463,11 +476,12 @@ TONY_API int tony_bn_bwd(const void* x, int64_t ldx, const void* dy, int64_t ldd
                          int64_t lddx, int64_t M, int C, const float* mean, const float* invstd,
                          const void* gamma, const void* beta, int param_bf16, int relu,
                          float* dsums_ws, void* dgamma, void* dbeta, int accumulate, hipStream_t stream) {
+  const int64_t ss = 2 * static_cast<int64_t>(C);
   int rc = tony_bn_bwd_reduce(x, ldx, dy, lddy, M, C, mean, invstd, gamma, beta, param_bf16, relu, dsums_ws,
-                              dsums_ws + C, stream);
+                              dsums_ws + C, ss, stream);
   if (rc) return rc;
   return tony_bn_bwd_apply(x, ldx, dy, lddy, dx, lddx, M, C, mean, invstd, gamma, beta, param_bf16, relu, dsums_ws,
-                           dsums_ws + C, dgamma, dbeta, accumulate, stream);
+                           dsums_ws + C, ss, dgamma, dbeta, accumulate, stream);
 }
 
 // Backward of y = relu(bn(x) + res): dy' = dy * (y > 0); dres = dy' (if dres != null); dx = bn_bwd(dy').
@@ -476,18 +490,19 @@ TONY_API int tony_bn_bwd_res(const void* x, int64_t ldx, const void* dy, int64_t
                              const float* invstd, const void* gamma, const void* beta, int param_bf16,
                              float* dsums_ws, void* dgamma, void* dbeta, int accumulate, hipStream_t stream) {
   if (bad_c(C) || (ldx % 8) || (lddy % 8) || (ldy % 8) || (lddx % 8) || (lddr % 8) || y == nullptr) return -1;
+  const int64_t ss = 2 * static_cast<int64_t>(C);
   int64_t rpb;
   int grid;
   plan_rows(M, C, 8, 512, &rpb, &grid);
   bn_bwd_reduce_kernel<true><<<grid, kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, static_cast<const uint16_t*>(y),
-      ldy, M, C, rpb, mean, invstd, gamma, beta, param_bf16, 1, dsums_ws, dsums_ws + C);
+      ldy, M, C, rpb, mean, invstd, gamma, beta, param_bf16, 1, dsums_ws, dsums_ws + C, ss);
   TONY_LAUNCH_CHECK();
   plan_rows(M, C, 4, 8192, &rpb, &grid);
   bn_bwd_apply_kernel<true><<<grid, kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, static_cast<const uint16_t*>(y),
       ldy, static_cast<uint16_t*>(dres), lddr, static_cast<uint16_t*>(dx), lddx, M, C, rpb, mean, invstd, gamma, beta,
-      param_bf16, 1, dsums_ws, dsums_ws + C, dgamma, dbeta, accumulate);
+      param_bf16, 1, dsums_ws, dsums_ws + C, ss, dgamma, dbeta, accumulate);
   TONY_LAUNCH_CHECK();
   return 0;
 }

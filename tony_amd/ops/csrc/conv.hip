@@ -100,7 +100,8 @@ __device__ __forceinline__ void store_rows(uint16_t* lds, const uint4* regs) {
 template <int BM, int BN>
 __global__ __launch_bounds__(kThreads) void conv_nt_kernel(Gather g, const uint16_t* __restrict__ B,
                                                            uint16_t* __restrict__ C, int64_t ldc, int M, int N,
-                                                           float* __restrict__ stats, int tiles_n) {
+                                                           float* __restrict__ stats, int64_t sstride,
+                                                           int tiles_n) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int AV = BM * BK / 8 / kThreads, BV = BN * BK / 8 / kThreads;
@@ -175,37 +176,57 @@ __global__ __launch_bounds__(kThreads) void conv_nt_kernel(Gather g, const uint1
     }
     __syncthreads();
   }
-  nt_epilogue<BM, BN, TM, TN>(acc, smem, C, ldc, M, N, m0, n0, stats);
+  nt_epilogue<BM, BN, TM, TN>(acc, smem, C, ldc, M, N, m0, n0,
+                               stats != nullptr ? stats + shard_off(tm, sstride) : nullptr);
 }
 
 template <int BM, int BN>
 int launch_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, float* stats,
-              hipStream_t stream) {
+              int64_t sstride, hipStream_t stream) {
   const int tiles_m = ceil_div(M, BM), tiles_n = ceil_div(N, BN);
   const int64_t tiles = static_cast<int64_t>(tiles_m) * tiles_n;
   if (tiles > 0x7fffffff) return -2;
   conv_nt_kernel<BM, BN><<<static_cast<int>(tiles), kThreads, 0, stream>>>(
       g, static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), ldc, static_cast<int>(M), static_cast<int>(N),
-      stats, tiles_n);
+      stats, sstride, tiles_n);
   TONY_LAUNCH_CHECK();
   return 0;
 }
 
+template <int BM>
+int launch_nt_bm(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, float* st,
+                 int64_t sstride, int64_t bn, hipStream_t stream) {
+  if constexpr (BM == 256) {  // 8 x TN accumulators per wave: only narrow column tiles fit the registers
+    if (bn <= 32) return launch_nt<256, 32>(g, B, C, ldc, M, N, st, sstride, stream);
+    if (bn <= 64) return launch_nt<256, 64>(g, B, C, ldc, M, N, st, sstride, stream);
+    return -3;
+  } else {
+    switch (bn) {
+      case 32: return launch_nt<BM, 32>(g, B, C, ldc, M, N, st, sstride, stream);
+      case 64: return launch_nt<BM, 64>(g, B, C, ldc, M, N, st, sstride, stream);
+      case 96: return launch_nt<BM, 96>(g, B, C, ldc, M, N, st, sstride, stream);
+      case 128: return launch_nt<BM, 128>(g, B, C, ldc, M, N, st, sstride, stream);
+      case 160: return launch_nt<BM, 160>(g, B, C, ldc, M, N, st, sstride, stream);
+      default: return launch_nt<BM, 192>(g, B, C, ldc, M, N, st, sstride, stream);
+    }
+  }
+}
+
 int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, int flags, float* stats,
-           hipStream_t stream) {
+           int64_t sstride, hipStream_t stream) {
   float* st = (flags & 1) ? stats : nullptr;  // accumulated into: the caller zeroes it (ops/arena.py)
-  // Column tile = the output channels split evenly over ceil(N/192) tiles, rounded up to the
-  // 32-column granule of the 2x2 wave layout (16-wide MFMA per wave): no MFMA work is spent on
-  // padding columns for Cout = 32..384 (Inception's 48/80/96/160/192/320/384).
-  const int64_t ntn = (N + 191) / 192;
-  const int64_t bn = ((N + ntn - 1) / ntn + 31) / 32 * 32;
-  switch (bn) {
-    case 32: return launch_nt<256, 32>(g, B, C, ldc, M, N, st, stream);
-    case 64: return launch_nt<256, 64>(g, B, C, ldc, M, N, st, stream);
-    case 96: return launch_nt<128, 96>(g, B, C, ldc, M, N, st, stream);
-    case 128: return launch_nt<128, 128>(g, B, C, ldc, M, N, st, stream);
-    case 160: return launch_nt<128, 160>(g, B, C, ldc, M, N, st, stream);
-    default: return launch_nt<128, 192>(g, B, C, ldc, M, N, st, stream);
+  const int v = (flags >> 8) & 0xff;
+  if (v >= kNumNtVariants) return -1;
+  if (v == 0) {
+    const int64_t bn = pick_bn(N, 192);
+    return bn <= 64 ? launch_nt_bm<256>(g, B, C, ldc, M, N, st, sstride, bn, stream)
+                    : launch_nt_bm<128>(g, B, C, ldc, M, N, st, sstride, bn, stream);
+  }
+  const int64_t bn = pick_bn(N, kNtVariants[v].cap);
+  switch (kNtVariants[v].bm) {
+    case 64: return launch_nt_bm<64>(g, B, C, ldc, M, N, st, sstride, bn, stream);
+    case 128: return launch_nt_bm<128>(g, B, C, ldc, M, N, st, sstride, bn, stream);
+    default: return launch_nt_bm<256>(g, B, C, ldc, M, N, st, sstride, bn, stream);
   }
 }
 
@@ -405,28 +426,31 @@ bool bad_geom(int C, int64_t ld, const void* p) {
 }  // namespace
 
 // Y[N*OH*OW, Co] (row stride ldy) = conv(X [N,H,W,C] pixel stride ldx, W [Co][R][S][C]).
-// flags bit0: per-channel sum / sum-of-squares of Y into stats[2*Co] (zero on entry).
+// flags bit0: per-channel sum / sum-of-squares of Y into stats[2*Co] (zero on entry; kStatShards
+// copies sstride floats apart when sstride > 0); bits 8..15: tile variant (run_nt).
 TONY_API int tony_conv_fwd(const void* x, int N, int H, int W, int C, int64_t ldx, const void* w, int Co, int R,
                            int S, int sh, int sw, int ph, int pw, void* y, int OH, int OW, int64_t ldy, int flags,
-                           float* stats, hipStream_t stream) {
-  if (bad_geom(C, ldx, x) || (reinterpret_cast<uintptr_t>(w) & 15) || Co <= 0 || R <= 0 || S <= 0) return -1;
+                           float* stats, int64_t sstride, hipStream_t stream) {
+  if (bad_geom(C, ldx, x) || (reinterpret_cast<uintptr_t>(w) & 15) || Co <= 0 || R <= 0 || S <= 0 || sstride < 0)
+    return -1;
   if (OH != (H + 2 * ph - R) / sh + 1 || OW != (W + 2 * pw - S) / sw + 1 || OH <= 0 || OW <= 0) return -1;
   const int64_t M = static_cast<int64_t>(N) * OH * OW;
   if (M > 0x7fffffff || static_cast<int64_t>(N) * H * W > 0x7fffffff) return -1;
   Gather g{static_cast<const uint16_t*>(x), ldx, H, W, C, OH, OW, R, S, sh, sw, -ph, -pw, 1, R * S * C};
-  return run_nt(g, w, y, ldy, M, Co, flags, stats, stream);
+  return run_nt(g, w, y, ldy, M, Co, flags, stats, sstride, stream);
 }
 
 // dX[N*H*W, C] (row stride lddx) of a stride-1 conv: dY [N,OH,OW,Co] (pixel stride lddy),
-// Wt = W permuted to [C][R][S][Co].
+// Wt = W permuted to [C][R][S][Co].  flags bits 8..15: tile variant (run_nt).
 TONY_API int tony_conv_dgrad(const void* dy, int N, int OH, int OW, int Co, int64_t lddy, const void* wt, int C,
-                             int R, int S, int ph, int pw, void* dx, int H, int W, int64_t lddx, hipStream_t stream) {
+                             int R, int S, int ph, int pw, void* dx, int H, int W, int64_t lddx, int flags,
+                             hipStream_t stream) {
   if (bad_geom(Co, lddy, dy) || (reinterpret_cast<uintptr_t>(wt) & 15) || C <= 0) return -1;
   if (OH != H + 2 * ph - R + 1 || OW != W + 2 * pw - S + 1) return -1;  // stride 1 only
   const int64_t M = static_cast<int64_t>(N) * H * W;
   if (M > 0x7fffffff || static_cast<int64_t>(N) * OH * OW > 0x7fffffff) return -1;
   Gather g{static_cast<const uint16_t*>(dy), lddy, OH, OW, Co, H, W, R, S, 1, 1, ph, pw, -1, R * S * Co};
-  return run_nt(g, wt, dx, lddx, M, C, 0, nullptr, stream);
+  return run_nt(g, wt, dx, lddx, M, C, flags & 0xff00, nullptr, 0, stream);
 }
 
 // dW (fp32 [Co][R][S][C], zero on entry) = dY^T im2col(X); dY [N*OH*OW, Co] row stride lddy.

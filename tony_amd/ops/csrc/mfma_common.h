@@ -52,6 +52,23 @@ __device__ __forceinline__ bf16x8_t tr_frag(const uint16_t* lds, int kgrp, int c
   return __builtin_bit_cast(bf16x8_t, r);
 }
 
+// Column tile for a cap: the output channels split evenly over ceil(N/cap) tiles, rounded up to
+// the 32-column granule of the 2x2 wave layout (16-wide MFMA per wave), so no MFMA work is spent on
+// padding columns for Cout = 32..384 (Inception's 48/80/96/160/192/320/384).
+inline int64_t pick_bn(int64_t N, int64_t cap) {
+  const int64_t ntn = (N + cap - 1) / cap;
+  return ((N + ntn - 1) / ntn + 31) / 32 * 32;
+}
+
+// Tile variants (flags bits 8..15), picked per shape by the Python autotuner (ops/tune.py):
+// 0 = built-in heuristic; 1.. = (rows per tile, column-tile cap) from kNtVariants.
+struct NtVariant {
+  int bm, cap;
+};
+constexpr NtVariant kNtVariants[] = {{0, 0},    {64, 192},  {128, 192}, {256, 64}, {64, 96},
+                                     {128, 96}, {128, 128}, {64, 128},  {256, 32}};
+constexpr int kNumNtVariants = sizeof(kNtVariants) / sizeof(kNtVariants[0]);
+
 // NT epilogue: optional per-column BN statistics from the fp32 accumulators, then the bf16 tile
 // staged through LDS (rows padded by 16 B) and written with 16-byte coalesced stores.
 // acc layout of 16x16 MFMA: col = lane&15, row = (lane>>4)*4 + r.

@@ -32,7 +32,7 @@ from typing import Sequence
 import torch
 from torch import nn
 
-from . import _lib
+from . import _lib, tune
 from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 from .gemm import wgrad_tn
@@ -63,9 +63,12 @@ class _HeadFn(torch.autograd.Function):
             w2 = w2.contiguous()
         pb = int(gamma.dtype == _BF16)
         Z = _cl_empty(n, ctot, h, w, dev)
-        stats = zeros_f32(2 * ctot, dev)  # the GEMM epilogue accumulates [sum | sumsq] into it
+        # the GEMM epilogue accumulates [sum | sumsq] into it (STAT_SHARDS copies, stride 2*ctot)
+        stats = zeros_f32(_lib.stat_floats(ctot), dev)
+        ss = 2 * ctot
         rc = L.tony_gemm_bf16(x.data_ptr(), w2.data_ptr(), Z.data_ptr(), M, ctot, cin, ldx, cin, ctot,
-                              1 if training else 0, stats.data_ptr(), stream)
+                              (1 if training else 0) | tune.gemm_flags(x, w2, Z, M, ctot, cin, ldx, training),
+                              stats.data_ptr(), ss, stream)
         _lib.check(rc, "tony_gemm_bf16")
         if training:
             mean = torch.empty(ctot, dtype=torch.float32, device=dev)
@@ -79,7 +82,7 @@ class _HeadFn(torch.autograd.Function):
         for ci in splits:
             y = _cl_empty(n, ci, h, w, dev)
             rc = L.tony_bn_apply(_off(Z, c0), M, ci, ctot, y.data_ptr(), ci, _off(stats, c0), _off(stats, ctot + c0),
-                                 _off(gamma, c0), _off(beta, c0), pb, float(eps), 1, mode,
+                                 ss, _off(gamma, c0), _off(beta, c0), pb, float(eps), 1, mode,
                                  _off(mean, c0) if training else 0, _off(invstd, c0) if training else 0,
                                  _off(running_mean, c0), _off(running_var, c0), float(momentum), stream)
             _lib.check(rc, "tony_bn_apply")
@@ -92,12 +95,14 @@ class _HeadFn(torch.autograd.Function):
             _lib.check(rc, "tony_avgpool3_s1p1")
             pstats = None
             if training:  # statistics of the pooled tensor (the GEMM's columns c0.. are pre-pool)
-                pstats = zeros_f32(2 * npool, dev)
-                rc = L.tony_bn_stats(P.data_ptr(), M, npool, npool, pstats.data_ptr(), _off(pstats, npool), stream)
+                pstats = zeros_f32(_lib.stat_floats(npool), dev)
+                rc = L.tony_bn_stats(P.data_ptr(), M, npool, npool, pstats.data_ptr(), _off(pstats, npool),
+                                     2 * npool, stream)
                 _lib.check(rc, "tony_bn_stats")
             y = _cl_empty(n, npool, h, w, dev)
             rc = L.tony_bn_apply(P.data_ptr(), M, npool, npool, y.data_ptr(), npool, _lib.ptr(pstats),
-                                 _off(pstats, npool) if training else 0, _off(gamma, c0), _off(beta, c0), pb,
+                                 _off(pstats, npool) if training else 0, 2 * npool if training else 0,
+                                 _off(gamma, c0), _off(beta, c0), pb,
                                  float(eps), 1, mode,
                                  _off(mean, c0) if training else 0, _off(invstd, c0) if training else 0,
                                  _off(running_mean, c0), _off(running_var, c0), float(momentum), stream)
@@ -121,7 +126,9 @@ class _HeadFn(torch.autograd.Function):
         ctot = weight.shape[0]
         pb = ctx.pb
         dZ = _cl_empty(n, ctot, h, w, dev)
-        dsum = zeros_f32(2 * ctot, dev)  # each split's BN-backward reduction accumulates into its slice
+        # each split's BN-backward reduction accumulates into its slice (STAT_SHARDS copies, stride 2*ctot)
+        dsum = zeros_f32(_lib.stat_floats(ctot), dev)
+        ss = 2 * ctot
         gw, gg, gb = (_lib.grad_slot(p) for p in ctx.params)
         inplace = gw is not None and gg is not None and gb is not None
         acc = int(inplace)
@@ -132,11 +139,11 @@ class _HeadFn(torch.autograd.Function):
             dy, (_, _, lddy) = _as_rows(dy)
             rc = L.tony_bn_bwd_reduce(_off(Z, c0), ctot, dy.data_ptr(), lddy, M, ci, _off(mean, c0), _off(invstd, c0),
                                       _off(gamma, c0), _off(beta, c0), pb, 1, _off(dsum, c0), _off(dsum, ctot + c0),
-                                      stream)
+                                      ss, stream)
             _lib.check(rc, "tony_bn_bwd_reduce")
             rc = L.tony_bn_bwd_apply(_off(Z, c0), ctot, dy.data_ptr(), lddy, _off(dZ, c0), ctot, M, ci,
                                      _off(mean, c0), _off(invstd, c0), _off(gamma, c0), _off(beta, c0), pb, 1,
-                                     _off(dsum, c0), _off(dsum, ctot + c0), _off(dgamma, c0), _off(dbeta, c0),
+                                     _off(dsum, c0), _off(dsum, ctot + c0), ss, _off(dgamma, c0), _off(dbeta, c0),
                                      acc, stream)
             _lib.check(rc, "tony_bn_bwd_apply")
             c0 += ci
@@ -146,11 +153,11 @@ class _HeadFn(torch.autograd.Function):
             dP = _cl_empty(n, npool, h, w, dev)
             rc = L.tony_bn_bwd_reduce(P.data_ptr(), npool, dy.data_ptr(), lddy, M, npool, _off(mean, c0),
                                       _off(invstd, c0), _off(gamma, c0), _off(beta, c0), pb, 1, _off(dsum, c0),
-                                      _off(dsum, ctot + c0), stream)
+                                      _off(dsum, ctot + c0), ss, stream)
             _lib.check(rc, "tony_bn_bwd_reduce")
             rc = L.tony_bn_bwd_apply(P.data_ptr(), npool, dy.data_ptr(), lddy, dP.data_ptr(), npool, M, npool,
                                      _off(mean, c0), _off(invstd, c0), _off(gamma, c0), _off(beta, c0), pb, 1,
-                                     _off(dsum, c0), _off(dsum, ctot + c0), _off(dgamma, c0), _off(dbeta, c0),
+                                     _off(dsum, c0), _off(dsum, ctot + c0), ss, _off(dgamma, c0), _off(dbeta, c0),
                                      acc, stream)
             _lib.check(rc, "tony_bn_bwd_apply")
             rc = L.tony_avgpool3_s1p1(dP.data_ptr(), _off(dZ, c0), n, h, w, npool, npool, ctot, stream)
@@ -159,8 +166,8 @@ class _HeadFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             wt = weight.reshape(ctot, cin).t().contiguous()  # [Cin, Ctot]
             dx = _cl_empty(n, cin, h, w, dev)
-            rc = L.tony_gemm_bf16(dZ.data_ptr(), wt.data_ptr(), dx.data_ptr(), M, cin, ctot, ctot, ctot, cin, 0, 0,
-                                  stream)
+            rc = L.tony_gemm_bf16(dZ.data_ptr(), wt.data_ptr(), dx.data_ptr(), M, cin, ctot, ctot, ctot, cin,
+                                  tune.gemm_flags(dZ, wt, dx, M, cin, ctot, ctot, False), 0, 0, stream)
             _lib.check(rc, "tony_gemm_bf16")
         dw32 = wgrad_tn(dZ.data_ptr(), ctot, x.data_ptr(), ldx, M, ctot, cin, dev)
         if inplace:

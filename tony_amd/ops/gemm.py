@@ -34,13 +34,13 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, s
         stats.zero_()  # the epilogue accumulates into it
     rc = _lib.lib().tony_gemm_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0) if M > 1 else K,
                                    b.stride(0) if N > 1 else K, out.stride(0) if M > 1 else N,
-                                   1 if stats is not None else 0, _lib.ptr(stats), _lib.stream_ptr(a.device))
+                                   1 if stats is not None else 0, _lib.ptr(stats), 0, _lib.stream_ptr(a.device))
     _lib.check(rc, "tony_gemm_bf16")
     return out
 
 
 def _gemm_rows(a_ptr, lda, b, M, N, K, out_ptr, ldc, device):
-    rc = _lib.lib().tony_gemm_bf16(a_ptr, b.data_ptr(), out_ptr, M, N, K, lda, b.stride(0), ldc, 0, 0,
+    rc = _lib.lib().tony_gemm_bf16(a_ptr, b.data_ptr(), out_ptr, M, N, K, lda, b.stride(0), ldc, 0, 0, 0,
                                    _lib.stream_ptr(device))
     _lib.check(rc, "tony_gemm_bf16")
 

@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import torch
 
-from . import _lib
+from . import _lib, tune
 from .arena import zeros_f32
 from .bn import _as_rows, _empty_like_rows, _rows_view
 from .fused import _cl_empty
@@ -38,7 +38,7 @@ def _bn_stats_and_apply(L, z, ldz, M, C, res, ldr, y, ldy, gamma, beta, pb, eps,
         invstd = torch.rsqrt(running_var.float() + eps)
     rc = L.tony_bn_apply_res(z.data_ptr(), M, C, ldz, res.data_ptr(), ldr, y.data_ptr(), ldy,
                              _lib.ptr(stats) if training else 0, _lib.ptr(stats) + 4 * C if training else 0,
-                             _lib.ptr(gamma), _lib.ptr(beta), pb, float(eps), 1, 0 if training else 1,
+                             2 * C if training else 0, _lib.ptr(gamma), _lib.ptr(beta), pb, float(eps), 1, 0 if training else 1,
                              _lib.ptr(mean) if training else 0, _lib.ptr(invstd) if training else 0,
                              _lib.ptr(running_mean), _lib.ptr(running_var), float(momentum), stream)
     _lib.check(rc, "tony_bn_apply_res")
@@ -52,7 +52,7 @@ def _bwd_res(L, z, ldz, dy, y, M, C, mean, invstd, gamma, beta, pb, params, stre
     dz = _empty_like_rows(y)
     _, _, lddz = _rows_view(dz)
     dres = _empty_like_rows(y) if want_dres else None
-    ws = zeros_f32(2 * C, dev)
+    ws = zeros_f32(_lib.stat_floats(C), dev)
     gg, gb = _lib.grad_slot(params[0]), _lib.grad_slot(params[1])
     inplace = gg is not None and gb is not None
     dgamma = gg if inplace else torch.empty_like(gamma)
@@ -77,8 +77,9 @@ class _BNAddReLUFn(torch.autograd.Function):
         pb = int(gamma.dtype == _BF16)
         stats = None
         if training:
-            stats = zeros_f32(2 * C, z.device)
-            rc = L.tony_bn_stats(z.data_ptr(), M, C, ldz, stats.data_ptr(), stats.data_ptr() + 4 * C, stream)
+            stats = zeros_f32(_lib.stat_floats(C), z.device)
+            rc = L.tony_bn_stats(z.data_ptr(), M, C, ldz, stats.data_ptr(), stats.data_ptr() + 4 * C, 2 * C,
+                                 stream)
             _lib.check(rc, "tony_bn_stats")
         mean, invstd = _bn_stats_and_apply(L, z, ldz, M, C, res, ldr, y, ldy, gamma, beta, pb, eps, training,
                                            momentum, running_mean, running_var, stats, stream)
@@ -111,9 +112,10 @@ class _Conv1x1BNAddReLUFn(torch.autograd.Function):
         if w2.stride(0) != cin or w2.stride(1) != 1:
             w2 = w2.contiguous()
         Z = _cl_empty(n, cout, h, w, dev)
-        stats = zeros_f32(2 * cout, dev)
+        stats = zeros_f32(_lib.stat_floats(cout), dev)
         rc = L.tony_gemm_bf16(x.data_ptr(), w2.data_ptr(), Z.data_ptr(), M, cout, cin, ldx, cin, cout,
-                              1 if training else 0, stats.data_ptr(), stream)
+                              (1 if training else 0) | tune.gemm_flags(x, w2, Z, M, cout, cin, ldx, training),
+                              stats.data_ptr(), 2 * cout, stream)
         _lib.check(rc, "tony_gemm_bf16")
         y = _cl_empty(n, cout, h, w, dev)
         pb = int(gamma.dtype == _BF16)
@@ -139,8 +141,8 @@ class _Conv1x1BNAddReLUFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             wt = weight.reshape(cout, cin).t().contiguous()
             dx = _cl_empty(n, cin, h, w, dev)
-            rc = L.tony_gemm_bf16(dZ.data_ptr(), wt.data_ptr(), dx.data_ptr(), M, cin, cout, cout, cout, cin, 0, 0,
-                                  stream)
+            rc = L.tony_gemm_bf16(dZ.data_ptr(), wt.data_ptr(), dx.data_ptr(), M, cin, cout, cout, cout, cin,
+                                  tune.gemm_flags(dZ, wt, dx, M, cin, cout, cout, False), 0, 0, stream)
             _lib.check(rc, "tony_gemm_bf16")
         dw32 = wgrad_tn(dZ.data_ptr(), cout, x.data_ptr(), ldx, M, cout, cin, dev)
         gw = _lib.grad_slot(ctx.params[0])

@@ -1,0 +1,78 @@
+"""Per-shape tile-variant autotuning for the NT MFMA kernels (1x1-conv GEMM, implicit-GEMM conv).
+
+The NT kernels (csrc/gemm.hip, csrc/conv.hip) take a tile variant in flags bits 8..15
+(``kNtVariants`` in csrc/mfma_common.h: rows per tile x column-tile cap; 0 = built-in heuristic).
+Which one is fastest depends on the shape: Inception-v3 runs the same kernels on M = 682k rows
+(a 128-row tile gives 5,300 tiles) and on M = 8,192 rows (64 tiles of 128 rows leave 3/4 of the
+256 CUs idle), with N from 48 to 1,344 and K from 64 to 2,048.  The first eager call of each
+(kernel, shape) times every variant on the real operands and caches the fastest; a HIP-graph
+capture replays the cached decision (nothing is timed while capturing).  ``TONY_CONV_AUTOTUNE=0``
+pins the heuristic.
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, Dict, Hashable
+
+import torch
+
+AUTOTUNE = os.environ.get("TONY_CONV_AUTOTUNE", "1") != "0"
+NT_VARIANTS = tuple(range(9))  # csrc/mfma_common.h kNtVariants
+_CACHE: Dict[Hashable, int] = {}
+
+
+def time_ms(fn: Callable[[], object], reps: int = 5) -> float:
+    fn()
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    start.record()
+    for _ in range(reps):
+        fn()
+    end.record()
+    end.synchronize()
+    return start.elapsed_time(end) / reps
+
+
+def pick(key: Hashable, launch: Callable[[int], int], variants=NT_VARIANTS) -> int:
+    """Return the flags bits (variant << 8) of the fastest tile variant for ``key``.
+
+    ``launch(vflags)`` runs the kernel once with those variant bits and returns its status code
+    (non-zero: the variant does not apply to this shape and is skipped)."""
+    v = _CACHE.get(key)
+    if v is not None:
+        return v << 8
+    if not AUTOTUNE or torch.cuda.is_current_stream_capturing():
+        return 0
+    best, best_t = 0, float("inf")
+    for cand in variants:
+        if launch(cand << 8) != 0:
+            continue
+        t = time_ms(lambda: launch(cand << 8))
+        if t < best_t:
+            best, best_t = cand, t
+    _CACHE[key] = best
+    return best << 8
+
+
+def choices() -> Dict[Hashable, int]:
+    """Variant decisions so far (for logs / profiles)."""
+    return dict(_CACHE)
+
+
+def gemm_flags(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, M: int, N: int, K: int, lda: int,
+               stats: bool) -> int:
+    """Variant bits for ``tony_gemm_bf16`` C[M,N] = A[M,K] B[N,K]^T (B and C dense, ld K and N).
+
+    Timing runs write C (the caller overwrites it right after) and statistics into a scratch
+    buffer, never into the caller's accumulators."""
+    from . import _lib
+
+    key = ("gemm", M, N, K, lda, bool(stats))
+    if key in _CACHE or not AUTOTUNE or torch.cuda.is_current_stream_capturing():
+        return pick(key, lambda vf: 0)
+    L = _lib.lib()
+    dev = c.device
+    stream = _lib.stream_ptr(dev)
+    scratch = torch.zeros(_lib.stat_floats(N), dtype=torch.float32, device=dev)
+    base = 1 if stats else 0
+    return pick(key, lambda vf: L.tony_gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, lda, K, N,
+                                                 base | vf, scratch.data_ptr(), 2 * N, stream))

@@ -68,22 +68,23 @@ def main():
         y = torch.empty_like(x)
         g = torch.ones(C, device=dev)
         b = torch.zeros(C, device=dev)
-        ws = torch.zeros(2 * C, device=dev)
+        ws = torch.zeros(_lib.stat_floats(C), device=dev)
+        ss = 2 * C
         mean = torch.zeros(C, device=dev)
         inv = torch.ones(C, device=dev)
         rm = torch.zeros(C, device=dev)
         rv = torch.ones(C, device=dev)
         B = M * C * 2
-        t_s = tm(lambda: L.tony_bn_stats(x.data_ptr(), M, C, C, ws.data_ptr(), ws.data_ptr() + 4 * C, stream))
+        t_s = tm(lambda: L.tony_bn_stats(x.data_ptr(), M, C, C, ws.data_ptr(), ws.data_ptr() + 4 * C, ss, stream))
         t_a = tm(lambda: L.tony_bn_apply(x.data_ptr(), M, C, C, y.data_ptr(), C, ws.data_ptr(), ws.data_ptr() + 4 * C,
-                                         g.data_ptr(), b.data_ptr(), 0, 1e-3, 1, 0, mean.data_ptr(), inv.data_ptr(),
+                                         ss, g.data_ptr(), b.data_ptr(), 0, 1e-3, 1, 0, mean.data_ptr(), inv.data_ptr(),
                                          rm.data_ptr(), rv.data_ptr(), 0.1, stream))
         t_r = tm(lambda: L.tony_bn_bwd_reduce(x.data_ptr(), C, dy.data_ptr(), C, M, C, mean.data_ptr(),
                                               inv.data_ptr(), g.data_ptr(), b.data_ptr(), 0, 1, ws.data_ptr(),
-                                              ws.data_ptr() + 4 * C, stream))
+                                              ws.data_ptr() + 4 * C, ss, stream))
         t_p = tm(lambda: L.tony_bn_bwd_apply(x.data_ptr(), C, dy.data_ptr(), C, y.data_ptr(), C, M, C,
                                              mean.data_ptr(), inv.data_ptr(), g.data_ptr(), b.data_ptr(), 0, 1,
-                                             ws.data_ptr(), ws.data_ptr() + 4 * C, 0, 0, 0, stream))
+                                             ws.data_ptr(), ws.data_ptr() + 4 * C, ss, 0, 0, 0, stream))
         print(f"{M:>9} {C:>5} {cnt:>3} | {t_s:9.1f} {B / t_s / 1e3:6.0f} | {t_a:9.1f} {2 * B / t_a / 1e3:6.0f} | "
               f"{t_r:9.1f} {2 * B / t_r / 1e3:6.0f} | {t_p:9.1f} {3 * B / t_p / 1e3:6.0f}")
         tot["stats"] += cnt * t_s
