@@ -201,6 +201,8 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
 // Backward reduction: dsums[c] = sum(dy'), dsums[C+c] = sum(dy' * xhat),
 // where dy' = dy masked by the ReLU (recomputed from x), or -- YMASK, the
 // residual form where the ReLU followed an add -- masked by the saved output y.
+// Per-channel coefficients are built once per workgroup in LDS (xhat = x*p0 + p1,
+// pre-activation = x*p2 + p3), so no lane waits on scattered parameter loads.
 template <bool YMASK>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __restrict__ dy, int64_t lddy,
@@ -208,22 +210,30 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     int64_t M, int C, int64_t rows_per_block, const float* __restrict__ mean,
     const float* __restrict__ invstd, const void* gamma, const void* beta, int param_bf16,
     int relu, float* __restrict__ dsum, float* __restrict__ dsumx, int64_t sstride) {
-  __shared__ float red[kMaxC * 2];
+  __shared__ float red[kMaxC * 4];  // coefficient table [4][C] first, then the block reduction
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    const float mu = mean[c], is = invstd[c];
+    const float g = load_param(gamma, c, param_bf16, 1.f), be = load_param(beta, c, param_bf16, 0.f);
+    red[c] = is;
+    red[kMaxC + c] = -mu * is;
+    red[2 * kMaxC + c] = g * is;
+    red[3 * kMaxC + c] = be - g * is * mu;
+  }
+  __syncthreads();
   RowMap rm(C);
   float a[8], b[8];
+  float p0[8], p1[8], p2[8], p3[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) a[j] = b[j] = 0.f;
+  for (int j = 0; j < 8; ++j) {
+    a[j] = b[j] = 0.f;
+    const int c = (rm.active ? rm.cg * 8 : 0) + j;
+    p0[j] = red[c];
+    p1[j] = red[kMaxC + c];
+    p2[j] = red[2 * kMaxC + c];
+    p3[j] = red[3 * kMaxC + c];
+  }
+  __syncthreads();  // the table is dead: red is reused by block_reduce_add
   if (rm.active) {
-    float mu[8], is[8], sc[8], sh[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = rm.cg * 8 + j;
-      mu[j] = mean[c];
-      is[j] = invstd[c];
-      const float g = load_param(gamma, c, param_bf16, 1.f);
-      sc[j] = g;
-      sh[j] = load_param(beta, c, param_bf16, 0.f);
-    }
     const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
     const int64_t r1 = min(M, r0 + rows_per_block);
     const int64_t step = rm.RPI;
@@ -234,11 +244,11 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
       if (YMASK) yv.to_float(yf);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float xh = (xf[j] - mu[j]) * is[j];
+        const float xh = fmaf(xf[j], p0[j], p1[j]);
         float d = gf[j];
         if (YMASK) {
           if (yf[j] <= 0.f) d = 0.f;
-        } else if (relu && fmaf(xh, sc[j], sh[j]) <= 0.f) {
+        } else if (relu && fmaf(xf[j], p2[j], p3[j]) <= 0.f) {
           d = 0.f;
         }
         a[j] += d;
@@ -266,8 +276,9 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
   block_reduce_add(red, rm, C, a, b, dsum + so, dsumx + so);
 }
 
-// YMASK: mask dy by the saved output y and also write the masked dy -- the
-// gradient of the residual branch -- to dres (when non-null).
+// dx = k*(dy' - dsum/M - xhat*dsumx/M) folded per channel into dx = dy'*q0 + x*q1 + q2 (LDS table,
+// with the ReLU test x*q3 + q4 > 0).  YMASK: mask dy by the saved output y and also write the
+// masked dy -- the gradient of the residual branch -- to dres (when non-null).
 template <bool YMASK>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __restrict__ dy, int64_t lddy,
@@ -276,14 +287,19 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     const float* __restrict__ mean, const float* __restrict__ invstd, const void* gamma,
     const void* beta, int param_bf16, int relu, const float* __restrict__ dsum,
     const float* __restrict__ dsumx, int64_t sstride, void* dgamma, void* dbeta, int accumulate) {
-  __shared__ float k_s[kMaxC], a_s[kMaxC], b_s[kMaxC];
+  __shared__ float tab[5][kMaxC];
   const float inv_m = 1.f / static_cast<float>(M);
   for (int c = threadIdx.x; c < C; c += kThreads) {
-    const float g = load_param(gamma, c, param_bf16, 1.f);
+    const float g = load_param(gamma, c, param_bf16, 1.f), be = load_param(beta, c, param_bf16, 0.f);
     const float ds = shard_sum(dsum, c, sstride), dsx = shard_sum(dsumx, c, sstride);
-    k_s[c] = g * invstd[c];
-    a_s[c] = ds * inv_m;
-    b_s[c] = dsx * inv_m;
+    const float mu = mean[c], is = invstd[c];
+    const float k = g * is, am = ds * inv_m, bm = dsx * inv_m;
+    // dx = k*(d - am - (x - mu)*is*bm)
+    tab[0][c] = k;
+    tab[1][c] = -k * bm * is;
+    tab[2][c] = k * (bm * is * mu - am);
+    tab[3][c] = k;               // pre-activation = x*k + (be - k*mu)
+    tab[4][c] = be - k * mu;
     if (blockIdx.x == 0) {
       store_param(dbeta, c, param_bf16, ds, accumulate);
       store_param(dgamma, c, param_bf16, dsx, accumulate);
@@ -292,17 +308,15 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
   __syncthreads();
   RowMap rm(C);
   if (!rm.active) return;
-  float mu[8], is[8], g[8], be[8], k[8], am[8], bm[8];
+  float q0[8], q1[8], q2[8], q3[8], q4[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = rm.cg * 8 + j;
-    mu[j] = mean[c];
-    is[j] = invstd[c];
-    g[j] = load_param(gamma, c, param_bf16, 1.f);
-    be[j] = load_param(beta, c, param_bf16, 0.f);
-    k[j] = k_s[c];
-    am[j] = a_s[c];
-    bm[j] = b_s[c];
+    q0[j] = tab[0][c];
+    q1[j] = tab[1][c];
+    q2[j] = tab[2][c];
+    q3[j] = tab[3][c];
+    q4[j] = tab[4][c];
   }
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
   const int64_t r1 = min(M, r0 + rows_per_block);
@@ -314,15 +328,14 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     if (YMASK) yv.to_float(yf);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float xh = (xf[j] - mu[j]) * is[j];
       float d = gf[j];
       if (YMASK) {
         if (yf[j] <= 0.f) d = 0.f;
         gf[j] = d;
-      } else if (relu && fmaf(xh, g[j], be[j]) <= 0.f) {
+      } else if (relu && fmaf(xf[j], q3[j], q4[j]) <= 0.f) {
         d = 0.f;
       }
-      o[j] = k[j] * (d - am[j] - xh * bm[j]);
+      o[j] = fmaf(d, q0[j], fmaf(xf[j], q1[j], q2[j]));
     }
     store8(dx + row * lddx + rm.cg * 8, bf16x8::from_float(o));
     if (YMASK && dres != nullptr) store8(dres + row * lddr + rm.cg * 8, bf16x8::from_float(gf));
