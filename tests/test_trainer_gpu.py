@@ -53,3 +53,49 @@ def test_graph_replay_matches_eager(cuda):
             assert abs(a - b) <= 2e-2 * max(1.0, abs(b)), (mode, lg, le)
         err = (pg - pe).abs().max().item()
         assert err < 2e-2, (mode, err)
+
+
+def test_transpose_batch_matches_permute(cuda):
+    from tony_amd.ops.wt_cache import TransposedWeights
+
+    torch.manual_seed(0)
+    shapes = [(192, 160, 7, 1), (48, 288, 1, 1), (80, 64, 3, 3), (2048 // 8, 72, 1, 3), (32, 32, 3, 3)]
+    ws = [nn.Parameter(torch.randn(s, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+          for s in shapes]
+    c = TransposedWeights(torch.device("cuda", 0))
+    c.enabled = True
+    for w in ws:
+        assert torch.equal(c.get(w), w.permute(1, 2, 3, 0).contiguous())
+    with torch.no_grad():
+        for w in ws:
+            w.mul_(-2.0).add_(1.0)  # the "optimizer step"
+    c.refresh()
+    torch.cuda.synchronize()
+    for w in ws:
+        assert torch.equal(c.get(w), w.permute(1, 2, 3, 0).contiguous())
+
+
+def test_trainer_matches_plain_loop(cuda):
+    """Trainer (arena, cached transposed weights) vs a plain PS loop with none of its machinery."""
+    from tony_amd.models.layers import init_weights
+    from tony_amd.ops import cross_entropy
+    from tony_amd.parallel.ps import ParameterServer
+
+    le, pe, _ = _train("eager")
+    dev = torch.device("cuda", 0)
+    model = init_weights(_Tiny(), seed=0).to(dev).to(memory_format=torch.channels_last).train()
+    ps = ParameterServer(model, optimizer="sgd", lr=0.05, momentum=0.9, device=dev)
+    g = torch.Generator(device=dev).manual_seed(7)
+    x = torch.randn((32, 16, 24, 24), generator=g, device=dev).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (32,), generator=g, device=dev)
+    losses = []
+    for _ in range(4):
+        ps.zero_grad()
+        loss = cross_entropy(model(x), y)
+        loss.backward()
+        ps.step()
+        losses.append(float(loss.float().item()))
+    for a, b in zip(losses, le):
+        assert abs(a - b) <= 2e-2 * max(1.0, abs(b)), (losses, le)
+    assert (ps.flat.data.float() - pe).abs().max().item() < 2e-2

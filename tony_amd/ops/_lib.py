@@ -74,7 +74,29 @@ _SIGNATURES = {
                          c_void_p],
     "tony_maxpool_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
                          c_void_p],
+    "tony_transpose_desc_bytes": [],
+    "tony_transpose_batch": [c_void_p, c_int, c_int, c_void_p],
 }
+
+
+class _SignedLib:
+    """The loaded library, exposing ONLY the functions declared in _SIGNATURES.
+
+    ctypes passes an undeclared function's Python-int arguments as 32-bit C ints, which silently
+    truncates device pointers and streams (a GPU fault far from the call); refuse such calls."""
+
+    def __init__(self, h):
+        self._h = h
+        for name, argtypes in _SIGNATURES.items():
+            fn = getattr(h, name, None)
+            if fn is None:
+                continue
+            fn.argtypes = argtypes
+            fn.restype = c_int
+            setattr(self, name, fn)
+
+    def __getattr__(self, name):
+        raise KernelError(f"{name}: not exported by {SO_PATH} or missing from _lib._SIGNATURES")
 
 
 class KernelError(RuntimeError):
@@ -114,13 +136,7 @@ def lib():
         if not os.path.exists(SO_PATH):
             raise KernelError(
                 f"{SO_PATH} is missing: run `python -m tony_amd.ops.build` (or __graft_entry__.build())")
-        h = ctypes.CDLL(SO_PATH, mode=ctypes.RTLD_LOCAL)
-        for name, argtypes in _SIGNATURES.items():
-            fn = getattr(h, name, None)
-            if fn is None:
-                continue
-            fn.argtypes = argtypes
-            fn.restype = c_int
+        h = _SignedLib(ctypes.CDLL(SO_PATH, mode=ctypes.RTLD_LOCAL))
         n = h.tony_stat_shards()
         if n != STAT_SHARDS:
             raise KernelError(f"{SO_PATH} accumulates BN statistics in {n} shards, the Python side expects "

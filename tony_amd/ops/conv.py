@@ -24,7 +24,7 @@ from typing import Callable, Dict, Tuple
 
 import torch
 
-from . import _lib, tune
+from . import _lib, tune, wt_cache
 from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 
@@ -90,8 +90,10 @@ def conv_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: 
 
     if vflags is None:
         key = ("conv_fwd", tuple(x.shape), ldx, tuple(weight.shape), (sh, sw), (ph, pw), stats is not None)
-        scratch = torch.zeros(_lib.stat_floats(co), device=x.device) if stats is not None else None
-        vflags = tune.pick(key, lambda vf: launch(vf, scratch))
+        vflags = tune.cached(key)
+        if vflags is None:  # first call of this shape: time the variants (statistics into a scratch buffer)
+            scratch = torch.zeros(_lib.stat_floats(co), device=x.device) if stats is not None else None
+            vflags = tune.pick(key, lambda vf: launch(vf, scratch))
     _lib.check(launch(vflags, stats), "tony_conv_fwd")
     return y
 
@@ -104,7 +106,7 @@ def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, paddin
     dy, (_, _, lddy) = _as_rows(dy)
     ph, pw = _pair(padding)
     dx = _cl_empty(n, c, h, w, dy.device)
-    wt = _crsk(weight)
+    wt = wt_cache.transposed(weight)
     L, st = _lib.lib(), _lib.stream_ptr(dy.device)
 
     def launch(vf):

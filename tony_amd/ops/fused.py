@@ -32,7 +32,7 @@ from typing import Sequence
 import torch
 from torch import nn
 
-from . import _lib, tune
+from . import _lib, tune, wt_cache
 from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 from .gemm import wgrad_tn
@@ -164,7 +164,7 @@ class _HeadFn(torch.autograd.Function):
             _lib.check(rc, "tony_avgpool3_s1p1")
         dx = None
         if ctx.needs_input_grad[0]:
-            wt = weight.reshape(ctot, cin).t().contiguous()  # [Cin, Ctot]
+            wt = wt_cache.transposed(weight).reshape(cin, ctot)  # [Cin, Ctot]
             dx = _cl_empty(n, cin, h, w, dev)
             rc = L.tony_gemm_bf16(dZ.data_ptr(), wt.data_ptr(), dx.data_ptr(), M, cin, ctot, ctot, ctot, cin,
                                   tune.gemm_flags(dZ, wt, dx, M, cin, ctot, ctot, False), 0, 0, stream)

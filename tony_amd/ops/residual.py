@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import torch
 
-from . import _lib, tune
+from . import _lib, tune, wt_cache
 from .arena import zeros_f32
 from .bn import _as_rows, _empty_like_rows, _rows_view
 from .fused import _cl_empty
@@ -139,7 +139,7 @@ class _Conv1x1BNAddReLUFn(torch.autograd.Function):
                                       stream)
         dx = None
         if ctx.needs_input_grad[0]:
-            wt = weight.reshape(cout, cin).t().contiguous()
+            wt = wt_cache.transposed(weight).reshape(cin, cout)
             dx = _cl_empty(n, cin, h, w, dev)
             rc = L.tony_gemm_bf16(dZ.data_ptr(), wt.data_ptr(), dx.data_ptr(), M, cin, cout, cout, cout, cin,
                                   tune.gemm_flags(dZ, wt, dx, M, cin, cout, cout, False), 0, 0, stream)

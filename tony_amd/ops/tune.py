@@ -53,6 +53,16 @@ def pick(key: Hashable, launch: Callable[[int], int], variants=NT_VARIANTS) -> i
     return best << 8
 
 
+def cached(key: Hashable):
+    """The variant bits already chosen for ``key``, 0 when tuning is off or capturing, else None."""
+    v = _CACHE.get(key)
+    if v is not None:
+        return v << 8
+    if not AUTOTUNE or torch.cuda.is_current_stream_capturing():
+        return 0
+    return None
+
+
 def choices() -> Dict[Hashable, int]:
     """Variant decisions so far (for logs / profiles)."""
     return dict(_CACHE)

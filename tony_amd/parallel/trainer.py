@@ -14,6 +14,7 @@ from typing import Callable
 
 import torch
 
+from ..ops import wt_cache
 from ..ops.arena import for_device
 from ..utils.tracing import heartbeat, trace_range
 from .ps import ParameterServer
@@ -40,6 +41,11 @@ class Trainer:
         dev = ps.flat.device
         # one zero-fill per step for every fused kernel's fp32 accumulators (ops/arena.py)
         self.arena = for_device(dev) if dev.type == "cuda" else None
+        # transposed conv weights for the dgrads, refreshed by one batched launch per step (ops/wt_cache.py)
+        # (one cache per trainer, active only inside its steps: nothing else can read a stale copy)
+        self.wt = wt_cache.TransposedWeights(dev) if dev.type == "cuda" else None
+        if self.wt is not None:
+            self.wt.enabled = True
 
     def _body(self, x, y, ps_step: bool = True):
         self.ps.zero_grad()
@@ -55,6 +61,8 @@ class Trainer:
     def _ps_step(self):
         with trace_range("ps push/apply/pull"):
             self.ps.step()
+        if self.wt is not None:
+            self.wt.refresh()  # the dgrads of the next step read the updated weights
 
     def _eager_step(self, x, y):
         if self.arena is not None:
@@ -66,6 +74,13 @@ class Trainer:
         return loss.detach()
 
     def step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        wt_cache.activate(self.wt)
+        try:
+            return self._step(x, y)
+        finally:
+            wt_cache.activate(None)
+
+    def _step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         if not self.use_graph:
             return self._eager_step(x, y)
         if self.graph is None:
@@ -119,3 +134,5 @@ class Trainer:
             for opt in self.ps.optimizers.values():
                 opt.step_count -= 1
         self.graph = g
+        if self.wt is not None:
+            self.wt.frozen = True  # the captured refresh() holds the current work list
