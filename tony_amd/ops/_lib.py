@@ -27,6 +27,7 @@ c_void_p = ctypes.c_void_p
 c_int = ctypes.c_int
 c_int64 = ctypes.c_int64
 c_float = ctypes.c_float
+c_int_p = ctypes.POINTER(ctypes.c_int)
 
 _SIGNATURES = {
     "tony_bn_fwd_train": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int,
@@ -61,14 +62,15 @@ _SIGNATURES = {
                       c_int64, c_void_p],
     "tony_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64,
                        c_int, c_void_p, c_int64, c_void_p],
-    "tony_gemm_tn_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64, c_int,
-                          c_void_p],
+    "tony_gemm_tn_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64,
+                          c_void_p, c_int64, c_int_p, c_int, c_void_p],
+    "tony_splitk_reduce": [c_void_p, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_void_p],
     "tony_conv_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int,
                       c_int, c_int, c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_int64, c_void_p],
     "tony_conv_dgrad": [c_void_p, c_int, c_int, c_int, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int,
                         c_void_p, c_int, c_int, c_int64, c_int, c_void_p],
     "tony_conv_wgrad": [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int, c_int, c_int, c_int,
-                        c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p],
+                        c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_int_p, c_int, c_void_p],
     "tony_avgpool3_s1p1": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
     "tony_maxpool_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
                          c_void_p],

@@ -27,6 +27,7 @@ import torch
 from . import _lib, tune, wt_cache
 from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
+from .gemm import splitk_combine
 
 _BF16 = torch.bfloat16
 AUTOTUNE = os.environ.get("TONY_CONV_AUTOTUNE", "1") != "0"
@@ -118,20 +119,26 @@ def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, paddin
     return dx
 
 
-def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride=1, padding=0, out=None) -> torch.Tensor:
-    """fp32 dW with memory [Co][R][S][Ci] (returned as a [Co, Ci, R, S] channels_last view)."""
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride=1, padding=0, dst=None):
+    """fp32 dW with memory [Co][R][S][Ci] (returned as a [Co, Ci, R, S] channels_last view), or, with
+    ``dst`` (a gradient slot in [Co][R][S][Ci] memory order), dW added into dst (returns None).
+
+    The M = N*OH*OW reduction is split over ~2 workgroups per CU whose partial dW tiles are stored
+    to a slab and summed by one combine pass (gemm.splitk_combine) -- no fp32 atomics."""
     dy, (_, co, lddy) = _as_rows(dy)
     x, (_, c, ldx) = _as_rows(x)
     n, _, h, w = x.shape
     _, _, r, s = weight_shape
     (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
-    # split-K atomics accumulate into it: zero on entry
-    dw = (out if out is not None else zeros_f32(co * r * s * c, x.device)).view(co, r, s, c)
-    rc = _lib.lib().tony_conv_wgrad(dy.data_ptr(), lddy, x.data_ptr(), n, h, w, c, ldx, co, r, s, sh, sw, ph, pw,
-                                    dy.shape[2], dy.shape[3], dw.data_ptr(), _lib.num_cus(x.device),
-                                    _lib.stream_ptr(x.device))
-    _lib.check(rc, "tony_conv_wgrad")
-    return dw.permute(0, 3, 1, 2)
+    L, dev = _lib.lib(), x.device
+    tbm = 32 if co <= 32 else 64 if co <= 64 else 128  # csrc/conv.hip tony_conv_wgrad tile rows
+    ntiles = -(-co // tbm) * -(-(r * s * c) // 128)
+    out = splitk_combine(
+        lambda slab, cap, sp: L.tony_conv_wgrad(dy.data_ptr(), lddy, x.data_ptr(), n, h, w, c, ldx, co, r, s, sh, sw,
+                                                ph, pw, dy.shape[2], dy.shape[3], 0, slab, cap, sp,
+                                                _lib.num_cus(dev), _lib.stream_ptr(dev)),
+        co * r * s * c, ntiles, dev, dst)
+    return None if out is None else out.view(co, r, s, c).permute(0, 3, 1, 2)
 
 
 # --------------------------------------------------------------------------------- MIOpen --
@@ -216,10 +223,13 @@ def _wgrad(dy, x, weight, stride, padding):
     key = ("wgrad", tuple(dy.shape), tuple(weight.shape), stride, padding)
     impl = _CHOICE.get(key)
     if impl is None:
-        scratch = torch.zeros(weight.numel(), dtype=torch.float32, device=x.device)
-        impl = _choose(key, {"tony": lambda: conv_wgrad(dy, x, weight.shape, stride, padding, scratch.zero_()),
+        impl = _choose(key, {"tony": lambda: conv_wgrad(dy, x, weight.shape, stride, padding),
                              "miopen": lambda: _miopen_wgrad(dy, x, weight, stride, padding)})
     if impl == "tony":
+        gw = _lib.grad_slot(weight)
+        if gw is not None and gw.is_contiguous(memory_format=torch.channels_last):
+            conv_wgrad(dy, x, weight.shape, stride, padding, dst=gw)  # summed straight into the slot
+            return None
         return _accumulate_wgrad(weight, conv_wgrad(dy, x, weight.shape, stride, padding))
     dw = _miopen_wgrad(dy, x, weight, stride, padding)
     gw = _lib.grad_slot(weight)

@@ -268,7 +268,8 @@ constexpr int WK = 32;  // 64-row stages measured slower: 2x LDS + VGPRs halve t
 template <int TBM>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __restrict__ dY, int64_t lddy,
                                                               Gather g, float* __restrict__ C, int64_t M, int Co,
-                                                              int tiles_n2, int ntiles, int64_t rows_per_split) {
+                                                              int tiles_n2, int ntiles, int64_t rows_per_split,
+                                                              float* __restrict__ slab) {
   constexpr int TM = TBM / 32;                 // 16-row MFMA tiles per wave along Cout (2 waves)
   constexpr int A_CH = TBM / 8;                // 16-B chunks per dY row in the tile
   constexpr int AV = (WK * A_CH + kThreads - 1) / kThreads;
@@ -383,6 +384,9 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __
     }
     __syncthreads();
   }
+  // slab mode: this split's partial tile with plain stores (tony_splitk_reduce sums the splits);
+  // otherwise fp32 atomics into C
+  float* dst = slab != nullptr ? slab + static_cast<int64_t>(split) * Co * K : C;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -391,15 +395,20 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = n1_0 + wm * (TBM / 2) + i * 16 + (lane >> 4) * 4 + r;
-        if (row < Co && col < K) atomicAdd(C + static_cast<int64_t>(row) * K + col, acc[i][j][r]);
+        if (row < Co && col < K) {
+          if (slab != nullptr)
+            dst[static_cast<int64_t>(row) * K + col] = acc[i][j][r];
+          else
+            atomicAdd(dst + static_cast<int64_t>(row) * K + col, acc[i][j][r]);
+        }
       }
     }
   }
 }
 
 template <int TBM>
-int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, int64_t M, int Co, int num_cus,
-                 hipStream_t stream) {
+int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, float* slab, int64_t slab_cap,
+                 int* splits_out, int64_t M, int Co, int num_cus, hipStream_t stream) {
   const int tiles_n1 = ceil_div(Co, TBM), tiles_n2 = ceil_div(g.K, WTBN);
   const int ntiles = tiles_n1 * tiles_n2;
   // enough workgroups for ~2 per CU, each reducing >= 8 stages of WK rows
@@ -413,8 +422,10 @@ int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, int64
   splits = (M + rows - 1) / rows;
   const int64_t grid = splits * ntiles;
   if (grid > 0x7fffffff) return -2;
+  if (slab != nullptr && splits * Co * static_cast<int64_t>(g.K) > slab_cap) return -4;  // caller's bound is off
+  if (splits_out != nullptr) *splits_out = static_cast<int>(splits);
   conv_wgrad_kernel<TBM><<<static_cast<int>(grid), kThreads, 0, stream>>>(
-      static_cast<const uint16_t*>(dy), lddy, g, dw, M, Co, tiles_n2, ntiles, rows);
+      static_cast<const uint16_t*>(dy), lddy, g, dw, M, Co, tiles_n2, ntiles, rows, slab);
   TONY_LAUNCH_CHECK();
   return 0;
 }
@@ -454,16 +465,19 @@ TONY_API int tony_conv_dgrad(const void* dy, int N, int OH, int OW, int Co, int6
 }
 
 // dW (fp32 [Co][R][S][C], zero on entry) = dY^T im2col(X); dY [N*OH*OW, Co] row stride lddy.
+// With a slab (slab_cap floats >= splits * Co*R*S*C) the M splits store their partial dW there
+// instead of adding into dw with atomics; *splits_out gets the split count for tony_splitk_reduce.
 TONY_API int tony_conv_wgrad(const void* dy, int64_t lddy, const void* x, int N, int H, int W, int C, int64_t ldx,
                              int Co, int R, int S, int sh, int sw, int ph, int pw, int OH, int OW, float* dw,
-                             int num_cus, hipStream_t stream) {
+                             float* slab, int64_t slab_cap, int* splits_out, int num_cus, hipStream_t stream) {
   if (bad_geom(C, ldx, x) || (Co % 8) || (lddy % 8) || (reinterpret_cast<uintptr_t>(dy) & 15)) return -1;
   if (OH != (H + 2 * ph - R) / sh + 1 || OW != (W + 2 * pw - S) / sw + 1) return -1;
   const int K = R * S * C;
   const int64_t M = static_cast<int64_t>(N) * OH * OW;
   if (M > 0x7fffffff) return -1;
   Gather g{static_cast<const uint16_t*>(x), ldx, H, W, C, OH, OW, R, S, sh, sw, -ph, -pw, 1, K};
-  if (Co <= 32) return launch_wgrad<32>(dy, lddy, g, dw, M, Co, num_cus, stream);
-  if (Co <= 64) return launch_wgrad<64>(dy, lddy, g, dw, M, Co, num_cus, stream);
-  return launch_wgrad<128>(dy, lddy, g, dw, M, Co, num_cus, stream);
+  if (slab == nullptr && dw == nullptr) return -1;
+  if (Co <= 32) return launch_wgrad<32>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, stream);
+  if (Co <= 64) return launch_wgrad<64>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, stream);
+  return launch_wgrad<128>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, stream);
 }

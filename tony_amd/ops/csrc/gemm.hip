@@ -231,7 +231,7 @@ __device__ __forceinline__ void tn_store(uint16_t* lds, const uint4* regs) {
 __global__ __launch_bounds__(kThreads) void gemm_tn_splitk_kernel(
     const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
     float* __restrict__ C, int64_t ldc, int64_t M, int N1, int N2, int tiles_n2, int ntiles,
-    int64_t rows_per_split) {
+    int64_t rows_per_split, float* __restrict__ slab) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 2 * TBK * 128];
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int tile = wg % ntiles, split = wg / ntiles;
@@ -283,7 +283,10 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_splitk_kernel(
     }
     __syncthreads();
   }
-  // acc[i][j] element r: row n1 = .. + (lane>>4)*4 + r, col n2 = .. + (lane&15)
+  // acc[i][j] element r: row n1 = .. + (lane>>4)*4 + r, col n2 = .. + (lane&15).
+  // slab mode: this split's dense [N1][N2] partial with plain stores (tony_splitk_reduce sums them)
+  float* dst = slab != nullptr ? slab + static_cast<int64_t>(split) * N1 * N2 : C;
+  const int64_t ld = slab != nullptr ? N2 : ldc;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -292,7 +295,12 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_splitk_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = n1_0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-        if (row < N1 && col < N2) atomicAdd(C + static_cast<int64_t>(row) * ldc + col, acc[i][j][r]);
+        if (row < N1 && col < N2) {
+          if (slab != nullptr)
+            dst[static_cast<int64_t>(row) * ld + col] = acc[i][j][r];
+          else
+            atomicAdd(dst + static_cast<int64_t>(row) * ld + col, acc[i][j][r]);
+        }
       }
     }
   }
@@ -300,10 +308,13 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_splitk_kernel(
 
 }  // namespace
 
-// C (fp32, [N1, N2], zero on entry) = A^T B ; A [M, N1] (lda), B [M, N2] (ldb).
+// C (fp32, [N1, N2], zero on entry) = A^T B ; A [M, N1] (lda), B [M, N2] (ldb).  With a slab
+// (slab_cap floats >= splits * N1*N2) the M splits store dense partials there instead of atomics
+// into C; *splits_out gets the split count for tony_splitk_reduce.
 TONY_API int tony_gemm_tn_bf16(const void* A, const void* B, float* C, int64_t M, int64_t N1, int64_t N2,
-                               int64_t lda, int64_t ldb, int64_t ldc, int num_cus, hipStream_t stream) {
-  if (M <= 0 || N1 <= 0 || N2 <= 0) return -1;
+                               int64_t lda, int64_t ldb, int64_t ldc, float* slab, int64_t slab_cap,
+                               int* splits_out, int num_cus, hipStream_t stream) {
+  if (M <= 0 || N1 <= 0 || N2 <= 0 || (slab == nullptr && C == nullptr)) return -1;
   if ((N1 % 8) || (N2 % 8) || (lda % 8) || (ldb % 8)) return -1;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -1;
   // C is accumulated into with atomics: the caller hands it over zeroed (ops/arena.py)
@@ -320,9 +331,11 @@ TONY_API int tony_gemm_tn_bf16(const void* A, const void* B, float* C, int64_t M
   splits = (M + rows - 1) / rows;
   const int64_t grid = splits * ntiles;
   if (grid > 0x7fffffff) return -2;
+  if (slab != nullptr && splits * N1 * N2 > slab_cap) return -4;  // caller's bound is off
+  if (splits_out != nullptr) *splits_out = static_cast<int>(splits);
   gemm_tn_splitk_kernel<<<static_cast<int>(grid), kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(A), lda, static_cast<const uint16_t*>(B), ldb, C, ldc, M, static_cast<int>(N1),
-      static_cast<int>(N2), tiles_n2, ntiles, rows);
+      static_cast<int>(N2), tiles_n2, ntiles, rows, slab);
   TONY_LAUNCH_CHECK();
   return 0;
 }

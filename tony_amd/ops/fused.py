@@ -169,11 +169,10 @@ class _HeadFn(torch.autograd.Function):
             rc = L.tony_gemm_bf16(dZ.data_ptr(), wt.data_ptr(), dx.data_ptr(), M, cin, ctot, ctot, ctot, cin,
                                   tune.gemm_flags(dZ, wt, dx, M, cin, ctot, ctot, False), 0, 0, stream)
             _lib.check(rc, "tony_gemm_bf16")
-        dw32 = wgrad_tn(dZ.data_ptr(), ctot, x.data_ptr(), ldx, M, ctot, cin, dev)
-        if inplace:
-            rc = L.tony_add_f32(gw.data_ptr(), int(gw.dtype == _BF16), dw32.data_ptr(), dw32.numel(), stream)
-            _lib.check(rc, "tony_add_f32")
+        if inplace:  # dW summed straight into the flat gradient slot ([ctot][cin] = the slot's order)
+            wgrad_tn(dZ.data_ptr(), ctot, x.data_ptr(), ldx, M, ctot, cin, dev, dst=gw)
             return dx, None, None, None, None, None, None, None, None, None, None
+        dw32 = wgrad_tn(dZ.data_ptr(), ctot, x.data_ptr(), ldx, M, ctot, cin, dev)
         dw = dw32.to(weight.dtype).reshape(weight.shape)
         return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None
 

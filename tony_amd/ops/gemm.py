@@ -9,10 +9,11 @@ split-K MFMA kernel that reads its operands with ds_read_b64_tr_b16
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
-from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 
 
@@ -45,13 +46,36 @@ def _gemm_rows(a_ptr, lda, b, M, N, K, out_ptr, ldc, device):
     _lib.check(rc, "tony_gemm_bf16")
 
 
-def wgrad_tn(a_ptr, lda, b_ptr, ldb, M, n1, n2, device) -> torch.Tensor:
-    """fp32 [n1, n2] = A^T B for row-major A [M, n1], B [M, n2] (split-K MFMA kernel)."""
-    out = zeros_f32(n1 * n2, device).view(n1, n2)  # split-K atomics accumulate into it
-    rc = _lib.lib().tony_gemm_tn_bf16(a_ptr, b_ptr, out.data_ptr(), M, n1, n2, lda, ldb, n2, _lib.num_cus(device),
-                                      _lib.stream_ptr(device))
-    _lib.check(rc, "tony_gemm_tn_bf16")
-    return out
+def splitk_combine(launch, n: int, ntiles: int, device, dst: torch.Tensor | None = None):
+    """Run a split-K weight-gradient kernel in slab mode and sum its splits (csrc/splitk.hip).
+
+    ``launch(slab_ptr, slab_cap, splits_ref)`` launches the kernel; its M splits store dense partials
+    of the ``n``-float result into the slab.  The sum is ADDED into ``dst`` (a bf16 or fp32
+    flat-gradient slot in the kernel's element order) and None returned, or returned as a new
+    fp32 tensor of n floats.  The split count never exceeds ceil(2 * CUs / ntiles) (the kernels'
+    2-workgroups-per-CU plan), which bounds the slab."""
+    cus = _lib.num_cus(device)
+    bound = max(1, -(-2 * cus // ntiles))
+    slab = torch.empty(bound * n, dtype=torch.float32, device=device)
+    splits = ctypes.c_int(0)
+    _lib.check(launch(slab.data_ptr(), slab.numel(), ctypes.byref(splits)), "split-K wgrad")
+    out = dst if dst is not None else torch.empty(n, dtype=torch.float32, device=device)
+    rc = _lib.lib().tony_splitk_reduce(slab.data_ptr(), splits.value, n, out.data_ptr(), int(out.dtype == torch.bfloat16),
+                                       int(dst is not None), cus, _lib.stream_ptr(device))
+    _lib.check(rc, "tony_splitk_reduce")
+    return None if dst is not None else out
+
+
+def wgrad_tn(a_ptr, lda, b_ptr, ldb, M, n1, n2, device, dst: torch.Tensor | None = None):
+    """fp32 [n1, n2] = A^T B for row-major A [M, n1], B [M, n2] (split-K MFMA kernel), or, with
+    ``dst`` (a contiguous [n1, n2]-ordered gradient slot), that product added into dst (returns None)."""
+    L = _lib.lib()
+    stream = _lib.stream_ptr(device)
+    ntiles = -(-n1 // 128) * -(-n2 // 128)
+    out = splitk_combine(lambda slab, cap, sp: L.tony_gemm_tn_bf16(a_ptr, b_ptr, 0, M, n1, n2, lda, ldb, n2, slab,
+                                                                   cap, sp, _lib.num_cus(device), stream),
+                         n1 * n2, ntiles, device, dst)
+    return None if out is None else out.view(n1, n2)
 
 
 def gemm_tn(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:

@@ -144,14 +144,13 @@ class _Conv1x1BNAddReLUFn(torch.autograd.Function):
             rc = L.tony_gemm_bf16(dZ.data_ptr(), wt.data_ptr(), dx.data_ptr(), M, cin, cout, cout, cout, cin,
                                   tune.gemm_flags(dZ, wt, dx, M, cin, cout, cout, False), 0, 0, stream)
             _lib.check(rc, "tony_gemm_bf16")
-        dw32 = wgrad_tn(dZ.data_ptr(), cout, x.data_ptr(), ldx, M, cout, cin, dev)
         gw = _lib.grad_slot(ctx.params[0])
-        if gw is not None and dg is None:
-            rc = L.tony_add_f32(gw.data_ptr(), int(gw.dtype == _BF16), dw32.data_ptr(), dw32.numel(), stream)
-            _lib.check(rc, "tony_add_f32")
+        if gw is not None and dg is None:  # dW summed straight into the flat gradient slot
+            wgrad_tn(dZ.data_ptr(), cout, x.data_ptr(), ldx, M, cout, cin, dev, dst=gw)
             dw = None
         else:
-            dw = dw32.to(weight.dtype).reshape(weight.shape)
+            dw = wgrad_tn(dZ.data_ptr(), cout, x.data_ptr(), ldx, M, cout, cin, dev).to(weight.dtype)
+            dw = dw.reshape(weight.shape)
         return dx, dw, dres, dg, db, None, None, None, None, None
 
 

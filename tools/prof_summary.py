@@ -45,6 +45,8 @@ def classify(name):
         return "hipBLASLt/rocBLAS GEMM"
     if "pool" in n:
         return "PyTorch pooling"
+    if "splitk_reduce" in n:
+        return "tony HIP: split-K wgrad combine"
     if "cat" in n or "copy" in n or "elementwise" in n or "vectorized" in n or "reduce" in n or "fill" in n \
             or "subtensor" in n:
         return "PyTorch elementwise/copy/fill"
