@@ -393,6 +393,8 @@ class Coordinator:
         })
         if self.token:
             env[C.TONY_TOKEN_FILE] = os.path.join(self.job_dir, "token")
+        # data-plane collectives of the tony_amd jobs: RCCL or the xGMI peer-memory kernels
+        env["TONY_COLLECTIVE"] = c.get(K.AMD_COLLECTIVE, "rccl").lower()
         if slot is not None and slot.gpus:
             ids = ",".join(str(g) for g in slot.gpus)
             task.gpus = list(slot.gpus)

@@ -28,6 +28,9 @@ c_int = ctypes.c_int
 c_int64 = ctypes.c_int64
 c_float = ctypes.c_float
 c_int_p = ctypes.POINTER(ctypes.c_int)
+c_void_pp = ctypes.POINTER(ctypes.c_void_p)
+c_u8_p = ctypes.POINTER(ctypes.c_uint8)
+c_u64_p = ctypes.POINTER(ctypes.c_uint64)
 
 _SIGNATURES = {
     "tony_bn_fwd_train": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int,
@@ -78,6 +81,16 @@ _SIGNATURES = {
                          c_void_p],
     "tony_transpose_desc_bytes": [],
     "tony_transpose_batch": [c_void_p, c_int, c_int, c_void_p],
+    # xGMI peer-memory collectives (csrc/xgmi.hip, parallel/xgmi.py)
+    "tony_xgmi_max_ranks": [],
+    "tony_xgmi_handle_bytes": [],
+    "tony_xgmi_alloc": [c_int64, c_void_pp, c_u8_p],
+    "tony_xgmi_open": [c_u8_p, c_void_pp],
+    "tony_xgmi_close": [c_void_p],
+    "tony_xgmi_free": [c_void_p],
+    "tony_xgmi_error": [c_void_p, c_int_p],
+    "tony_xgmi_collective": [c_u64_p, c_int, c_int, c_int64, c_int, c_void_p, c_void_p, c_int64, c_int, c_int,
+                             c_float, ctypes.c_uint32, c_int, c_void_p],
 }
 
 

@@ -9,8 +9,27 @@ exercised by the multi-process CPU tests.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
+
+# TONY_COLLECTIVE=hip (conf tony.amd.collective, exported by the coordinator) routes the flat
+# GPU collectives of the default group through tony_amd's xGMI peer-memory kernels (xgmi.py)
+_XGMI = [None]
+
+
+def _xgmi(t: torch.Tensor, group):
+    """The XgmiComm to use for tensor t, or None for the torch.distributed (RCCL / gloo) path."""
+    if group is not None or not t.is_cuda or os.environ.get("TONY_COLLECTIVE", "rccl").lower() not in ("hip", "xgmi"):
+        return None
+    if t.dtype not in (torch.bfloat16, torch.float32) or (t.numel() * t.element_size()) % 16:
+        return None
+    if _XGMI[0] is None:
+        from .xgmi import XgmiComm
+
+        _XGMI[0] = XgmiComm()
+    return _XGMI[0]
 
 
 def world(group=None) -> int:
@@ -37,6 +56,10 @@ def reduce_scatter_flat(out: torch.Tensor, inp: torch.Tensor, group=None, async_
         n = out.numel()
         out.copy_(inp[r * n:(r + 1) * n])
         return None
+    x = _xgmi(inp, group)
+    if x is not None and inp.numel() * inp.element_size() <= x.slot_bytes:
+        x.reduce_scatter(out, inp)
+        return None
     return dist.reduce_scatter_tensor(out, inp, group=group, async_op=async_op)
 
 
@@ -52,17 +75,29 @@ def all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group=None, async_op=F
         src = inp.clone() if any(p.data_ptr() == inp.data_ptr() for p in parts) else inp
         dist.all_gather(parts, src, group=group)
         return None
+    x = _xgmi(inp, group)
+    if x is not None and inp.numel() * inp.element_size() <= x.slot_bytes:
+        x.all_gather(out, inp)
+        return None
     return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
 
 
 def all_reduce(t: torch.Tensor, op=None, group=None, async_op=False):
     if world(group) == 1:
         return None
+    x = _xgmi(t, group) if op in (None, dist.ReduceOp.SUM) and not _is_gloo(group) else None
+    if x is not None and t.is_contiguous():
+        x.all_reduce(t)
+        return None
     return dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=group, async_op=async_op)
 
 
 def broadcast(t: torch.Tensor, src: int, group=None, async_op=False):
     if world(group) == 1:
+        return None
+    x = _xgmi(t, group) if not _is_gloo(group) else None
+    if x is not None and t.is_contiguous():
+        x.broadcast(t, src)
         return None
     return dist.broadcast(t, src, group=group, async_op=async_op)
 

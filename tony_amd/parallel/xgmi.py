@@ -1,0 +1,162 @@
+"""Hand-written intra-node collectives over xGMI peer memory (csrc/xgmi.hip), RCCL's alternative.
+
+One process per GPU, as everywhere in tony_amd.  ``XgmiComm(group)`` allocates this rank's
+window, exchanges the IPC handles over the (already initialised) process group and maps every
+peer's window; afterwards each collective is ONE kernel launch that copies the input into the
+local window, meets the peers at a per-workgroup flag barrier and pulls the peers' data directly
+over the links (a GPU reads from all 7 xGMI links at once, where a ring uses one
+in and one out):
+
+* ``all_reduce``   one-shot below ``oneshot_max_bytes`` (latency bound: every rank reads every
+                   peer's whole buffer), two-shot above (reduce-scatter + all-gather, each rank
+                   moves 2 (n-1)/n of the bytes);
+* ``reduce_scatter`` / ``all_gather`` / ``broadcast``  the flat single-launch forms the
+                   parameter server and DDP buckets use.
+
+Messages larger than the window slot are processed in slot-sized pieces.  Sums accumulate in
+fp32 for bf16 tensors.  Selected with ``TONY_COLLECTIVE=xgmi`` (TonY conf key
+``tony.amd.collective``), otherwise the RCCL path of ``collectives.py`` runs; a barrier whose peer
+never arrives fails the call (``XgmiError``) instead of hanging the GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _lib
+
+KIND = {"allreduce_oneshot": 0, "allreduce_twoshot": 1, "reduce_scatter": 2, "all_gather": 3, "broadcast": 4}
+
+
+class XgmiError(RuntimeError):
+    pass
+
+
+class XgmiComm:
+    def __init__(self, group=None, slot_bytes: int = 64 << 20, oneshot_max_bytes: int = 512 << 10,
+                 blocks: int = 64, device=None):
+        if not dist.is_initialized():
+            raise XgmiError("XgmiComm needs an initialised torch.distributed process group")
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        L = _lib.lib()
+        if self.world > L.tony_xgmi_max_ranks():
+            raise XgmiError(f"{self.world} ranks > {L.tony_xgmi_max_ranks()} supported on one node")
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self.slot_bytes = (int(slot_bytes) + 65535) // 65536 * 65536
+        self.oneshot_max_bytes = int(oneshot_max_bytes)
+        self.blocks = int(blocks)
+        self.epoch = 0
+        hsize = L.tony_xgmi_handle_bytes()
+        window = ctypes.c_void_p()
+        handle = (ctypes.c_uint8 * hsize)()
+        with torch.cuda.device(self.device):
+            _lib.check(L.tony_xgmi_alloc(self.slot_bytes, ctypes.byref(window), handle), "tony_xgmi_alloc")
+        self.window = window.value
+        handles: List[Optional[bytes]] = [None] * self.world
+        dist.all_gather_object(handles, bytes(handle), group=group)
+        self.peers = []
+        ptrs = []
+        for r, h in enumerate(handles):
+            if r == self.rank:
+                ptrs.append(self.window)
+                continue
+            p = ctypes.c_void_p()
+            buf = (ctypes.c_uint8 * hsize).from_buffer_copy(h)
+            with torch.cuda.device(self.device):
+                _lib.check(L.tony_xgmi_open(buf, ctypes.byref(p)), f"tony_xgmi_open(rank {r})")
+            self.peers.append(p.value)
+            ptrs.append(p.value)
+        self._windows = (ctypes.c_uint64 * self.world)(*ptrs)
+        dist.barrier(group=group)
+
+    # -- plumbing -------------------------------------------------------------------------------
+    def _launch(self, kind: int, inp: torch.Tensor, out: torch.Tensor, nbytes: int, root: int = 0,
+                scale: float = 1.0, in_off: int = 0, out_off: int = 0):
+        self.epoch += 1
+        rc = _lib.lib().tony_xgmi_collective(self._windows, self.rank, self.world, self.slot_bytes, kind,
+                                             inp.data_ptr() + in_off, out.data_ptr() + out_off, nbytes,
+                                             int(inp.dtype == torch.bfloat16), root, float(scale),
+                                             self.epoch & 0xFFFFFFFF, self.blocks, _lib.stream_ptr(self.device))
+        _lib.check(rc, "tony_xgmi_collective")
+
+    @staticmethod
+    def _check(t: torch.Tensor):
+        if not (t.is_cuda and t.is_contiguous() and t.dtype in (torch.bfloat16, torch.float32)):
+            raise XgmiError("xgmi collectives take contiguous bf16 / fp32 CUDA tensors")
+        if (t.numel() * t.element_size()) % 16 or t.data_ptr() % 16:
+            raise XgmiError("xgmi collectives need 16-byte aligned sizes and addresses")
+
+    def check_error(self) -> None:
+        """Raise if a barrier of this rank timed out (synchronises the device)."""
+        err = ctypes.c_int(0)
+        _lib.check(_lib.lib().tony_xgmi_error(ctypes.c_void_p(self.window), ctypes.byref(err)), "tony_xgmi_error")
+        if err.value:
+            raise XgmiError(f"rank {self.rank}: a peer never reached an xgmi barrier")
+
+    # -- collectives ----------------------------------------------------------------------------
+    def all_reduce(self, t: torch.Tensor, average: bool = False) -> torch.Tensor:
+        """In-place sum (or average) of ``t`` over all ranks."""
+        self._check(t)
+        scale = 1.0 / self.world if average else 1.0
+        nbytes = t.numel() * t.element_size()
+        if nbytes <= min(self.oneshot_max_bytes, self.slot_bytes):
+            self._launch(KIND["allreduce_oneshot"], t, t, nbytes, scale=scale)
+            return t
+        piece = self.slot_bytes // (16 * self.world) * (16 * self.world)
+        off = 0
+        while off < nbytes:
+            n = min(piece, nbytes - off)
+            if n % (16 * self.world):  # tail not divisible into equal shards: one-shot it
+                self._launch(KIND["allreduce_oneshot"], t, t, n, scale=scale, in_off=off, out_off=off)
+            else:
+                self._launch(KIND["allreduce_twoshot"], t, t, n, scale=scale, in_off=off, out_off=off)
+            off += n
+        return t
+
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, average: bool = False) -> torch.Tensor:
+        """out (inp.numel() / world elements) = this rank's shard of the sum over ranks of inp."""
+        self._check(inp)
+        self._check(out)
+        nbytes = inp.numel() * inp.element_size()
+        if out.numel() * self.world != inp.numel() or nbytes > self.slot_bytes:
+            raise XgmiError("reduce_scatter: out must be inp/world and inp must fit the window slot")
+        self._launch(KIND["reduce_scatter"], inp, out, nbytes, scale=1.0 / self.world if average else 1.0)
+        return out
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        """out (world x inp.numel()) = concatenation over ranks of inp."""
+        self._check(inp)
+        self._check(out)
+        nbytes = inp.numel() * inp.element_size()
+        if out.numel() != inp.numel() * self.world or nbytes > self.slot_bytes:
+            raise XgmiError("all_gather: out must be world x inp and inp must fit the window slot")
+        self._launch(KIND["all_gather"], inp, out, nbytes)
+        return out
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        self._check(t)
+        nbytes = t.numel() * t.element_size()
+        off = 0
+        while off < nbytes:
+            n = min(self.slot_bytes, nbytes - off)
+            self._launch(KIND["broadcast"], t, t, n, root=src, in_off=off, out_off=off)
+            off += n
+        return t
+
+    def close(self) -> None:
+        """Unmap the peers and free the window (collective: every rank calls it)."""
+        if self.window is None:
+            return
+        torch.cuda.synchronize(self.device)
+        dist.barrier(group=self.group)  # no peer may still be reading this rank's window
+        L = _lib.lib()
+        for p in self.peers:
+            L.tony_xgmi_close(ctypes.c_void_p(p))
+        L.tony_xgmi_free(ctypes.c_void_p(self.window))
+        self.window = None
+        self.peers = []
