@@ -99,3 +99,37 @@ def test_trainer_matches_plain_loop(cuda):
     for a, b in zip(losses, le):
         assert abs(a - b) <= 2e-2 * max(1.0, abs(b)), (losses, le)
     assert (ps.flat.data.float() - pe).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("block", ["A", "B", "C", "D", "E"])
+def test_zero_copy_concat_matches_copy_path(cuda, block, monkeypatch):
+    """Inception blocks writing branch outputs straight into the concat buffer == the copy path."""
+    from tony_amd.models import inception_v3 as iv3
+    from tony_amd.models.layers import init_weights
+    from tony_amd.ops import concat
+
+    mk = {"A": (lambda: iv3.InceptionA(192, 32), 35), "B": (lambda: iv3.InceptionB(288), 35),
+          "C": (lambda: iv3.InceptionC(768, 128), 17), "D": (lambda: iv3.InceptionD(768), 17),
+          "E": (lambda: iv3.InceptionE(1280), 8)}[block]
+    cin = {"A": 192, "B": 288, "C": 768, "D": 768, "E": 1280}[block]
+    torch.manual_seed(0)
+    x0 = torch.randn(16, cin, mk[1], mk[1], device=cuda).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+
+    def run(zero_copy):
+        m = init_weights(mk[0](), seed=1).to(cuda).to(memory_format=torch.channels_last).train()
+        for p in m.parameters():
+            p.data = p.data.to(torch.bfloat16)
+        if not zero_copy:
+            monkeypatch.setattr(concat, "take", lambda *a, **k: None)
+        x = x0.clone().requires_grad_(True)
+        y = m(x)
+        g = torch.randn(y.shape, device=cuda, generator=torch.Generator(device=cuda).manual_seed(3))
+        (y.float() * g).sum().backward()
+        monkeypatch.undo()
+        return y.detach().float(), x.grad.float()
+
+    y1, g1 = run(True)
+    y2, g2 = run(False)
+    assert (y1 - y2).abs().max().item() < 5e-2
+    assert ((g1 - g2).norm() / g2.norm()).item() < 2e-2

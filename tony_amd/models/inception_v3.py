@@ -20,9 +20,26 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from ..ops.concat import Slot, assemble, concat_buffer
 from ..ops.pool import avg_pool3x3_s1, max_pool
 from ..ops.fused import FusedHead
 from .layers import ConvBNAct, init_weights
+
+
+def _seq(seq, x, slot):
+    """Run an nn.Sequential of ConvBNAct whose last layer writes into ``slot``."""
+    mods = list(seq) if isinstance(seq, nn.Sequential) else [seq]
+    for m in mods[:-1]:
+        x = m(x)
+    return mods[-1](x, slot=slot)
+
+
+def _slots(buf, widths):
+    out, c0 = [], 0
+    for w in widths:
+        out.append(Slot(buf, c0))
+        c0 += w
+    return out
 
 
 class _Block(nn.Module):
@@ -58,9 +75,12 @@ class InceptionA(_Block):
         self.out_channels = 64 + 64 + 96 + pool_ch
 
     def forward(self, x):
-        if self.fused:
-            y1, y5, y3, yp = self.head(x)
-            return torch.cat([y1, self.b5(y5), self.b3(y3), yp], 1)
+        if self.fused:  # every branch writes its slice of one output buffer (ops/concat.py)
+            n, _, h, w = x.shape
+            buf = concat_buffer(n, self.out_channels, h, w, x)
+            s1, s5, s3, sp = _slots(buf, (64, 64, 96, self.out_channels - 224))
+            y1, y5, y3, yp = self.head(x, slots=(s1, None, None, sp))
+            return assemble(buf, [y1, self.b5(y5, slot=s5), _seq(self.b3, y3, s3), yp])
         p = self.avgpool(x)
         return torch.cat([self.b1(x), self.b5(x), self.b3(x), self.bp(p)], 1)
 
@@ -73,6 +93,11 @@ class InceptionB(_Block):  # 35x35 -> 17x17 reduction
         self.out_channels = 384 + 96 + cin
 
     def forward(self, x):
+        if self.fused:
+            n, c, h, w = x.shape
+            buf = concat_buffer(n, self.out_channels, (h - 3) // 2 + 1, (w - 3) // 2 + 1, x)
+            s3, sd, sp = _slots(buf, (384, 96, c))
+            return assemble(buf, [self.b3(x, slot=s3), _seq(self.bd, x, sd), max_pool(x, 3, 2, slot=sp)])
         return torch.cat([self.b3(x), self.bd(x), self.maxpool(x)], 1)
 
 
@@ -96,8 +121,11 @@ class InceptionC(_Block):  # 17x17 with factorised 7x7
 
     def forward(self, x):
         if self.fused:
-            y1, y7, yd, yp = self.head(x)
-            return torch.cat([y1, self.b7(y7), self.bd(yd), yp], 1)
+            n, _, h, w = x.shape
+            buf = concat_buffer(n, 768, h, w, x)
+            s1, s7, sd, sp = _slots(buf, (192, 192, 192, 192))
+            y1, y7, yd, yp = self.head(x, slots=(s1, None, None, sp))
+            return assemble(buf, [y1, _seq(self.b7, y7, s7), _seq(self.bd, yd, sd), yp])
         p = self.avgpool(x)
         return torch.cat([self.b1(x), self.b7(x), self.bd(x), self.bp(p)], 1)
 
@@ -118,8 +146,11 @@ class InceptionD(_Block):  # 17x17 -> 8x8 reduction
 
     def forward(self, x):
         if self.fused:
+            n, c, h, w = x.shape
+            buf = concat_buffer(n, self.out_channels, (h - 3) // 2 + 1, (w - 3) // 2 + 1, x)
+            s3, s7, sp = _slots(buf, (320, 192, c))
             t3, t7 = self.head(x)
-            return torch.cat([self.b3(t3), self.b7(t7), self.maxpool(x)], 1)
+            return assemble(buf, [self.b3(t3, slot=s3), _seq(self.b7, t7, s7), max_pool(x, 3, 2, slot=sp)])
         return torch.cat([self.b3(x), self.b7(x), self.maxpool(x)], 1)
 
 
@@ -143,8 +174,13 @@ class InceptionE(_Block):  # 8x8 with split 1x3 / 3x1 branches
 
     def forward(self, x):
         if self.fused:
-            y1, t, d, yp = self.head(x)
+            n, _, h, w = x.shape
+            buf = concat_buffer(n, 2048, h, w, x)
+            s1, sa, sb, sda, sdb, sp = _slots(buf, (320, 384, 384, 384, 384, 192))
+            y1, t, d, yp = self.head(x, slots=(s1, None, None, sp))
             d = self.bd(d)
+            return assemble(buf, [y1, self.b3a(t, slot=sa), self.b3b(t, slot=sb), self.bda(d, slot=sda),
+                                  self.bdb(d, slot=sdb), yp])
         else:
             y1 = self.b1(x)
             t = self.b3(x)

@@ -41,18 +41,21 @@ class ConvBNAct(nn.Module):
             self.bn = nn.BatchNorm2d(cout, eps=eps, momentum=momentum)
             self.act = nn.ReLU(inplace=True) if relu else nn.Identity()
 
-    def forward(self, x):
+    def forward(self, x, slot=None):
+        """``slot`` (ops/concat.Slot): write the output into a block's concat buffer when the fused
+        kernels run (ignored on the stock / CPU path, where the block copies it in)."""
         if self.fused and self.is_1x1 and self.bn.relu and x.is_cuda:
             # MFMA GEMM with BN statistics in its epilogue + fused apply (ops/fused.py)
             bn = self.bn
             return _HeadFn.apply(x, self.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                                 (self.conv.out_channels,), 0, self.training, bn.momentum, bn.eps)[0]
+                                 (self.conv.out_channels,), 0, self.training, bn.momentum, bn.eps,
+                                 (slot,) if slot is not None else None)[0]
         if self.fused and x.is_cuda and USE_TONY_CONV and conv_ops.supported(x, self.conv.weight, self.conv.stride,
                                                                               self.conv.padding):
             # implicit-GEMM conv with BN statistics in its epilogue + fused apply (ops/conv.py)
             bn, c = self.bn, self.conv
             return conv_ops.conv_bn_act(x, c.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, c.stride,
-                                        c.padding, self.training, bn.momentum, bn.eps, bn.relu)
+                                        c.padding, self.training, bn.momentum, bn.eps, bn.relu, slot)
         y = self.conv(x)
         if self.fused:
             return self.bn(y)

@@ -24,7 +24,7 @@ from typing import Callable, Dict, Tuple
 
 import torch
 
-from . import _lib, tune, wt_cache
+from . import _lib, concat, tune, wt_cache
 from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 from .gemm import splitk_combine
@@ -283,7 +283,7 @@ class _ConvBNActFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, gamma, beta, running_mean, running_var, stride, padding, training, momentum, eps,
-                relu):
+                relu, slot=None):
         L = _lib.lib()
         _lib.check_f32_stats(running_mean, running_var)
         dev = x.device
@@ -292,7 +292,10 @@ class _ConvBNActFn(torch.autograd.Function):
         stats = zeros_f32(_lib.stat_floats(co), dev) if training else None
         Z = _fwd(x, weight, stride, padding, stats)
         M, _, ldz = _rows_view(Z)
-        y = torch.empty_like(Z)
+        y = concat.take(slot, *Z.shape, Z)  # write straight into the block's concat buffer (ops/concat.py)
+        if y is None:
+            y = torch.empty_like(Z)
+        _, _, ldy = _rows_view(y)
         pb = int(gamma.dtype == _BF16)
         if training:
             mean = torch.empty(co, dtype=torch.float32, device=dev)
@@ -300,7 +303,7 @@ class _ConvBNActFn(torch.autograd.Function):
         else:
             mean = running_mean
             invstd = torch.rsqrt(running_var.float() + eps)
-        rc = L.tony_bn_apply(Z.data_ptr(), M, co, ldz, y.data_ptr(), ldz, _lib.ptr(stats),
+        rc = L.tony_bn_apply(Z.data_ptr(), M, co, ldz, y.data_ptr(), ldy, _lib.ptr(stats),
                              _lib.ptr(stats) + 4 * co if training else 0, 2 * co if training else 0,
                              gamma.data_ptr(), beta.data_ptr(), pb,
                              float(eps), int(relu), 0 if training else 1, _lib.ptr(mean) if training else 0,
@@ -334,14 +337,15 @@ class _ConvBNActFn(torch.autograd.Function):
         dw = _wgrad(dZ, x, weight, stride, padding)
         if inplace:
             dgamma = dbeta = None
-        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None
+        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None
 
 
 def conv_bn_act(x, weight, gamma, beta, running_mean, running_var, stride=1, padding=0, training=True,
-                momentum=0.1, eps=1e-3, relu=True):
+                momentum=0.1, eps=1e-3, relu=True, slot=None):
+    """relu(bn(conv(x))); with a ``concat.Slot`` the result is written into that channel slice."""
     if supported(x, weight, stride, padding):
         return _ConvBNActFn.apply(x, weight, gamma, beta, running_mean, running_var, _pair(stride), _pair(padding),
-                                  training, momentum, eps, relu)
+                                  training, momentum, eps, relu, slot)
     z = torch.nn.functional.conv2d(x, weight, None, stride, padding)
     y = torch.nn.functional.batch_norm(z, running_mean, running_var, gamma, beta, training, momentum, eps)
     return torch.relu(y) if relu else y

@@ -32,7 +32,7 @@ from typing import Sequence
 import torch
 from torch import nn
 
-from . import _lib, tune, wt_cache
+from . import _lib, concat, tune, wt_cache
 from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 from .gemm import wgrad_tn
@@ -50,7 +50,8 @@ def _off(t: torch.Tensor, elems: int) -> int:
 
 class _HeadFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, gamma, beta, running_mean, running_var, splits, npool, training, momentum, eps):
+    def forward(ctx, x, weight, gamma, beta, running_mean, running_var, splits, npool, training, momentum, eps,
+                slots=None):
         L = _lib.lib()
         _lib.check_f32_stats(running_mean, running_var)
         dev = x.device
@@ -79,9 +80,14 @@ class _HeadFn(torch.autograd.Function):
         mode = 0 if training else 1
         outs = []
         c0 = 0
-        for ci in splits:
-            y = _cl_empty(n, ci, h, w, dev)
-            rc = L.tony_bn_apply(_off(Z, c0), M, ci, ctot, y.data_ptr(), ci, _off(stats, c0), _off(stats, ctot + c0),
+        slots = slots or ()
+        for k, ci in enumerate(splits):
+            # a final branch output goes straight into the block's concat buffer (ops/concat.py)
+            y = concat.take(slots[k] if k < len(slots) else None, n, ci, h, w, x)
+            if y is None:
+                y = _cl_empty(n, ci, h, w, dev)
+            ldy = _rows_view(y)[2]
+            rc = L.tony_bn_apply(_off(Z, c0), M, ci, ctot, y.data_ptr(), ldy, _off(stats, c0), _off(stats, ctot + c0),
                                  ss, _off(gamma, c0), _off(beta, c0), pb, float(eps), 1, mode,
                                  _off(mean, c0) if training else 0, _off(invstd, c0) if training else 0,
                                  _off(running_mean, c0), _off(running_var, c0), float(momentum), stream)
@@ -99,8 +105,11 @@ class _HeadFn(torch.autograd.Function):
                 rc = L.tony_bn_stats(P.data_ptr(), M, npool, npool, pstats.data_ptr(), _off(pstats, npool),
                                      2 * npool, stream)
                 _lib.check(rc, "tony_bn_stats")
-            y = _cl_empty(n, npool, h, w, dev)
-            rc = L.tony_bn_apply(P.data_ptr(), M, npool, npool, y.data_ptr(), npool, _lib.ptr(pstats),
+            k = len(splits)
+            y = concat.take(slots[k] if k < len(slots) else None, n, npool, h, w, x)
+            if y is None:
+                y = _cl_empty(n, npool, h, w, dev)
+            rc = L.tony_bn_apply(P.data_ptr(), M, npool, npool, y.data_ptr(), _rows_view(y)[2], _lib.ptr(pstats),
                                  _off(pstats, npool) if training else 0, 2 * npool if training else 0,
                                  _off(gamma, c0), _off(beta, c0), pb,
                                  float(eps), 1, mode,
@@ -171,10 +180,10 @@ class _HeadFn(torch.autograd.Function):
             _lib.check(rc, "tony_gemm_bf16")
         if inplace:  # dW summed straight into the flat gradient slot ([ctot][cin] = the slot's order)
             wgrad_tn(dZ.data_ptr(), ctot, x.data_ptr(), ldx, M, ctot, cin, dev, dst=gw)
-            return dx, None, None, None, None, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None, None, None, None, None
         dw32 = wgrad_tn(dZ.data_ptr(), ctot, x.data_ptr(), ldx, M, ctot, cin, dev)
         dw = dw32.to(weight.dtype).reshape(weight.shape)
-        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None
+        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None
 
 
 def head_reference(x, weight, gamma, beta, running_mean, running_var, splits, npool, training, momentum, eps):
@@ -211,12 +220,14 @@ class FusedHead(nn.Module):
         self.conv = nn.Conv2d(cin, total, 1, bias=False)
         self.bn = nn.BatchNorm2d(total, eps=eps, momentum=momentum)
 
-    def forward(self, x):
+    def forward(self, x, slots=None):
+        """One output per split (+ the pool branch); ``slots`` (per output, None or a concat.Slot)
+        lets final branch outputs land directly in the block's concat buffer."""
         training = self.training
         args = (x, self.conv.weight, self.bn.weight, self.bn.bias, self.bn.running_mean, self.bn.running_var,
                 self.splits, self.npool, training, self.bn.momentum, self.bn.eps)
         if x.is_cuda:
             if x.dtype != _BF16:
                 raise TypeError("FusedHead HIP path takes bf16 activations")
-            return _HeadFn.apply(*args)
+            return _HeadFn.apply(*args, tuple(slots) if slots else None)
         return head_reference(*args)

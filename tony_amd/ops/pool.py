@@ -3,8 +3,8 @@ from __future__ import annotations
 
 import torch
 
-from . import _lib
-from .bn import _as_rows
+from . import _lib, concat
+from .bn import _as_rows, _rows_view
 
 
 def _nhwc_empty(n, c, h, w, like):
@@ -35,14 +35,16 @@ class _AvgPool3Fn(torch.autograd.Function):
 
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k, s):
+    def forward(ctx, x, k, s, slot=None):
         x, (_, c, ld) = _as_rows(x)
         n, _, h, w = x.shape
         oh, ow = (h - k) // s + 1, (w - k) // s + 1
-        y = _nhwc_empty(n, c, oh, ow, x)
+        y = concat.take(slot, n, c, oh, ow, x)  # straight into the block's concat buffer
+        if y is None:
+            y = _nhwc_empty(n, c, oh, ow, x)
         arg = torch.empty((n, oh, ow, c), dtype=torch.uint8, device=x.device)
-        rc = _lib.lib().tony_maxpool_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), n, h, w, c, k, s, ld, c,
-                                         _lib.stream_ptr(x.device))
+        rc = _lib.lib().tony_maxpool_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), n, h, w, c, k, s, ld,
+                                         _rows_view(y)[2], _lib.stream_ptr(x.device))
         _lib.check(rc, "tony_maxpool_fwd")
         ctx.save_for_backward(arg)
         ctx.shape = (n, c, h, w, k, s)
@@ -57,7 +59,7 @@ class _MaxPoolFn(torch.autograd.Function):
         rc = _lib.lib().tony_maxpool_bwd(dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), n, h, w, c, k, s, lddy, c,
                                          _lib.stream_ptr(dy.device))
         _lib.check(rc, "tony_maxpool_bwd")
-        return dx, None, None
+        return dx, None, None, None
 
 
 def avg_pool3x3_s1(x: torch.Tensor) -> torch.Tensor:
@@ -67,8 +69,8 @@ def avg_pool3x3_s1(x: torch.Tensor) -> torch.Tensor:
     return torch.nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=True)
 
 
-def max_pool(x: torch.Tensor, k: int = 3, s: int = 2) -> torch.Tensor:
-    """max_pool2d(x, k, s) (no padding) on channels_last bf16."""
+def max_pool(x: torch.Tensor, k: int = 3, s: int = 2, slot=None) -> torch.Tensor:
+    """max_pool2d(x, k, s) (no padding) on channels_last bf16 (into a concat.Slot when given)."""
     if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0:
-        return _MaxPoolFn.apply(x, k, s)
+        return _MaxPoolFn.apply(x, k, s, slot)
     return torch.nn.functional.max_pool2d(x, k, s)
