@@ -27,7 +27,7 @@ import torch
 from . import _lib, concat, tune, wt_cache
 from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
-from .gemm import splitk_combine
+from .gemm import WGRAD_OCC, splitk_combine, wgrad_cus
 
 _BF16 = torch.bfloat16
 AUTOTUNE = os.environ.get("TONY_CONV_AUTOTUNE", "1") != "0"
@@ -133,11 +133,17 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride=1, paddin
     L, dev = _lib.lib(), x.device
     tbm = 32 if co <= 32 else 64 if co <= 64 else 128  # csrc/conv.hip tony_conv_wgrad tile rows
     ntiles = -(-co // tbm) * -(-(r * s * c) // 128)
-    out = splitk_combine(
-        lambda slab, cap, sp: L.tony_conv_wgrad(dy.data_ptr(), lddy, x.data_ptr(), n, h, w, c, ldx, co, r, s, sh, sw,
-                                                ph, pw, dy.shape[2], dy.shape[3], 0, slab, cap, sp,
-                                                _lib.num_cus(dev), _lib.stream_ptr(dev)),
-        co * r * s * c, ntiles, dev, dst)
+
+    def run(occ, dst_=None):
+        return splitk_combine(
+            lambda slab, cap, sp: L.tony_conv_wgrad(dy.data_ptr(), lddy, x.data_ptr(), n, h, w, c, ldx, co, r, s, sh,
+                                                    sw, ph, pw, dy.shape[2], dy.shape[3], 0, slab, cap, sp,
+                                                    wgrad_cus(dev, occ), _lib.stream_ptr(dev)),
+            co * r * s * c, ntiles, dev, dst_, occ)
+
+    occ = tune.pick_choice(("wgrad_occ", tuple(dy.shape), lddy, tuple(x.shape), ldx, tuple(weight_shape), sh, sw,
+                            ph, pw), WGRAD_OCC, run)
+    out = run(occ, dst)
     return None if out is None else out.view(co, r, s, c).permute(0, 3, 1, 2)
 
 
@@ -167,15 +173,8 @@ def _miopen_wgrad(dy, x, weight, stride, padding):
 
 
 # ------------------------------------------------------------------------------ selection --
-def _time(fn: Callable[[], object], reps: int = 3) -> float:
-    fn()
-    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    start.record()
-    for _ in range(reps):
-        fn()
-    end.record()
-    end.synchronize()
-    return start.elapsed_time(end) / reps
+def _time(fn: Callable[[], object], reps: int = 5) -> float:
+    return tune.time_ms(fn, reps)
 
 
 def _choose(key: Tuple, candidates: Dict[str, Callable[[], object]], default: str = "tony") -> str:

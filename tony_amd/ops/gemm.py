@@ -13,7 +13,7 @@ import ctypes
 
 import torch
 
-from . import _lib
+from . import _lib, tune
 from .bn import _as_rows, _rows_view
 
 
@@ -46,7 +46,18 @@ def _gemm_rows(a_ptr, lda, b, M, N, K, out_ptr, ldc, device):
     _lib.check(rc, "tony_gemm_bf16")
 
 
-def splitk_combine(launch, n: int, ntiles: int, device, dst: torch.Tensor | None = None):
+# The split-K wgrad kernels size their grid as 2 workgroups per "CU" they are told about; telling
+# them occ x the real CU count keeps more splits in flight per CU (bigger slab, more latency hiding,
+# more combine traffic).  The best occ depends on the shape (tools/conv_bench.py --tony: 4 beats 1
+# on the 147x147 stem, changes nothing at 17x17), so it is autotuned per shape (ops/tune.py).
+WGRAD_OCC = (1, 2, 4, 8)
+
+
+def wgrad_cus(device, occ: int = 1) -> int:
+    return _lib.num_cus(device) * occ
+
+
+def splitk_combine(launch, n: int, ntiles: int, device, dst: torch.Tensor | None = None, occ: int = 1):
     """Run a split-K weight-gradient kernel in slab mode and sum its splits (csrc/splitk.hip).
 
     ``launch(slab_ptr, slab_cap, splits_ref)`` launches the kernel; its M splits store dense partials
@@ -54,7 +65,7 @@ def splitk_combine(launch, n: int, ntiles: int, device, dst: torch.Tensor | None
     flat-gradient slot in the kernel's element order) and None returned, or returned as a new
     fp32 tensor of n floats.  The split count never exceeds ceil(2 * CUs / ntiles) (the kernels'
     2-workgroups-per-CU plan), which bounds the slab."""
-    cus = _lib.num_cus(device)
+    cus = wgrad_cus(device, occ)
     bound = max(1, -(-2 * cus // ntiles))
     slab = torch.empty(bound * n, dtype=torch.float32, device=device)
     splits = ctypes.c_int(0)
@@ -72,9 +83,15 @@ def wgrad_tn(a_ptr, lda, b_ptr, ldb, M, n1, n2, device, dst: torch.Tensor | None
     L = _lib.lib()
     stream = _lib.stream_ptr(device)
     ntiles = -(-n1 // 128) * -(-n2 // 128)
-    out = splitk_combine(lambda slab, cap, sp: L.tony_gemm_tn_bf16(a_ptr, b_ptr, 0, M, n1, n2, lda, ldb, n2, slab,
-                                                                   cap, sp, _lib.num_cus(device), stream),
-                         n1 * n2, ntiles, device, dst)
+
+    def run(occ, dst_=None):
+        return splitk_combine(lambda slab, cap, sp: L.tony_gemm_tn_bf16(a_ptr, b_ptr, 0, M, n1, n2, lda, ldb, n2,
+                                                                        slab, cap, sp, wgrad_cus(device, occ),
+                                                                        stream),
+                              n1 * n2, ntiles, device, dst_, occ)
+
+    occ = tune.pick_choice(("wgrad_tn", M, n1, n2, lda, ldb), WGRAD_OCC, run)
+    out = run(occ, dst)
     return None if out is None else out.view(n1, n2)
 
 

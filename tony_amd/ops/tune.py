@@ -22,8 +22,14 @@ _CACHE: Dict[Hashable, int] = {}
 
 
 def time_ms(fn: Callable[[], object], reps: int = 5) -> float:
+    """GPU time of ``fn`` (ms).  A spin kernel keeps the GPU busy while the host enqueues the reps, so
+    the events bracket back-to-back kernels: the host cost of a Python/ctypes launch (tens of us, as
+    long as a small kernel) would otherwise be measured instead of the kernel and make the choice
+    between candidates random for small shapes."""
     fn()
+    torch.cuda.synchronize()
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda._sleep(4_000_000)  # ~2 ms of spinning: longer than enqueueing the reps
     start.record()
     for _ in range(reps):
         fn()
@@ -51,6 +57,20 @@ def pick(key: Hashable, launch: Callable[[int], int], variants=NT_VARIANTS) -> i
             best, best_t = cand, t
     _CACHE[key] = best
     return best << 8
+
+
+def pick_choice(key: Hashable, choices, run: Callable[[object], object]):
+    """The fastest of ``choices`` for ``key``: ``run(choice)`` executes the op once with it (timed
+    on the first eager call, cached; the first choice while capturing or with tuning off)."""
+    c = _CACHE.get(key)
+    if c is not None:
+        return c
+    if not AUTOTUNE or torch.cuda.is_current_stream_capturing():
+        return choices[0]
+    times = {ch: time_ms(lambda: run(ch)) for ch in choices}
+    best = min(times, key=times.get)
+    _CACHE[key] = best
+    return best
 
 
 def cached(key: Hashable):
