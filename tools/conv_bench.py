@@ -40,15 +40,11 @@ def collect_shapes(model_name, batch):
 
 
 def time_ms(fn, iters):
-    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    fn()
-    torch.cuda.synchronize()
-    start.record()
-    for _ in range(iters):
-        fn()
-    end.record()
-    torch.cuda.synchronize()
-    return start.elapsed_time(end) / iters
+    """GPU time per call: a spin kernel keeps the GPU busy while the host enqueues the calls, so
+    Python / ctypes launch overhead is not measured (tony_amd.ops.tune.time_ms)."""
+    from tony_amd.ops.tune import time_ms as gpu_time_ms
+
+    return gpu_time_ms(fn, iters)
 
 
 def main():
