@@ -140,7 +140,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic ImageNet-shaped 299x299x3 batches, random-init weights",
+            "data": f"synthetic ImageNet-shaped {res}x{res}x3 batches, random-init weights",
             "config": {
                 "model": args.model,
                 "global_batch": args.batch * world,
