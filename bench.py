@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--model", default="inception_v3", choices=["inception_v3", "resnet50"])
     ap.add_argument("--optimizer", default="sgd")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps (for rocprof)")
+    ap.add_argument("--no-wgrad-stream", action="store_true",
+                    help="serial backward (no weight gradients on a second stream)")
     ap.add_argument("--no-miopen-find", action="store_true",
                     help="MIOpen immediate mode instead of find (faster startup, slower non-1x1 convs)")
     return ap.parse_args()
@@ -94,7 +96,7 @@ def main():
     x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 1000, (args.batch,), generator=g, device=dev)
 
-    trainer = Trainer(model, ps, loss_fn, use_graph=not args.no_graph)
+    trainer = Trainer(model, ps, loss_fn, use_graph=not args.no_graph, overlap_wgrad=not args.no_wgrad_stream)
     t_w = time.perf_counter()
     for i in range(args.warmup):
         loss = trainer.step(x, y)
@@ -150,6 +152,7 @@ def main():
                 "parallelism": f"ps-colocated-sharded dp{world} (1 PS shard + 1 worker per GPU, sync)",
                 "optimizer": "fused SGD-momentum (HIP)" if args.optimizer == "sgd" else args.optimizer,
                 "hip_graph": not args.no_graph,
+                "wgrad_stream": not args.no_wgrad_stream,
                 "kernels": "stock-comparator" if args.stock else "tony_amd HIP",
                 "conv_impl": _conv_impl_counts(),
                 "final_loss": round(final_loss, 4),

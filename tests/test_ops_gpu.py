@@ -240,6 +240,25 @@ def test_maxpool(cuda, shape):
     _close(x.grad, xr.grad, 1e-2, 1e-2, "maxpool bwd")
 
 
+@pytest.mark.parametrize("cfg", [((4, 768, 17, 17), 5, 3), ((3, 2048, 8, 8), 8, 1), ((2, 16, 9, 7), 3, 2),
+                                 ((2, 64, 1, 1), 1, 1)])
+def test_avgpool_kxk(cuda, cfg):
+    """Aux-head 5x5/s3 and global average pooling vs the fp32 CPU reference."""
+    from tony_amd.ops.pool import avg_pool
+
+    shape, k, s = cfg
+    torch.manual_seed(9)
+    x = _nhwc(_nhwc(torch.randn(shape, device=cuda)).to(torch.bfloat16)).requires_grad_(True)
+    y = avg_pool(x, k, s)
+    xr = x.detach().float().cpu().requires_grad_(True)
+    yr = torch.nn.functional.avg_pool2d(xr, k, s)
+    _close(y, yr, 1e-2, 1e-2, "avgpool kxk fwd")
+    dy = _nhwc(torch.randn(yr.shape, device=cuda)).to(torch.bfloat16)
+    y.backward(dy)
+    yr.backward(dy.float().cpu())
+    _close(x.grad, xr.grad, 1e-2, 1e-2, "avgpool kxk bwd")
+
+
 def test_avgpool3_direct_on_grad_layout(cuda):
     """The backward reuses the forward stencil on dy; check the raw kernel on a fresh tensor."""
     from tony_amd.ops.pool import _box3

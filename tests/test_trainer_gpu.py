@@ -23,25 +23,55 @@ class _Tiny(nn.Module):
         return self.fc(torch.flatten(nn.functional.adaptive_avg_pool2d(z, 1), 1))
 
 
-def _train(mode, steps=4):
+class _Block(nn.Module):
+    """An Inception-A block (fused head, 5x5 / double-3x3 branches, zero-copy concat) + classifier."""
+
+    def __init__(self):
+        super().__init__()
+        from tony_amd.models.inception_v3 import InceptionA
+
+        self.block = InceptionA(64, 32)
+        self.fc = nn.Linear(256, 10)
+
+    def forward(self, x):
+        from tony_amd.ops.pool import global_avg_pool
+
+        return self.fc(global_avg_pool(self.block(x)))
+
+
+def _train(mode, steps=4, overlap=True, net=_Tiny, shape=(32, 16, 24, 24)):
     from tony_amd.models.layers import init_weights
     from tony_amd.ops import cross_entropy
     from tony_amd.parallel.ps import ParameterServer
     from tony_amd.parallel.trainer import Trainer
 
     dev = torch.device("cuda", 0)
-    model = init_weights(_Tiny(), seed=0).to(dev).to(memory_format=torch.channels_last).train()
+    model = init_weights(net(), seed=0).to(dev).to(memory_format=torch.channels_last).train()
     ps = ParameterServer(model, optimizer="sgd", lr=0.05, momentum=0.9, device=dev)
     use_graph = mode != "eager"
     tr = Trainer(model, ps, lambda o, y: cross_entropy(o, y), use_graph=use_graph, warmup_eager=1,
-                 graph_collectives=(mode == "graph_in") if use_graph else None)
+                 graph_collectives=(mode == "graph_in") if use_graph else None, overlap_wgrad=overlap)
     g = torch.Generator(device=dev).manual_seed(7)
-    x = torch.randn((32, 16, 24, 24), generator=g, device=dev).to(torch.bfloat16)
+    x = torch.randn(shape, generator=g, device=dev).to(torch.bfloat16)
     x = x.contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 10, (32,), generator=g, device=dev)
+    y = torch.randint(0, 10, (shape[0],), generator=g, device=dev)
     losses = [float(tr.step(x, y).float().item()) for _ in range(steps)]
     torch.cuda.synchronize()
+    if overlap and mode == "eager" and steps > 1:
+        assert tr.side_ops > 0, "no weight gradient ran on the side stream"
     return losses, ps.flat.data.float().clone(), ps.steps
+
+
+@pytest.mark.parametrize("mode", ["eager", "graph_in"])
+def test_wgrad_stream_overlap_matches_serial(cuda, mode):
+    """Weight gradients on the side stream (ops/streams.py) train exactly like the serial backward."""
+    kw = dict(net=_Block, shape=(8, 64, 35, 35), steps=5)
+    ls, ps_, _ = _train(mode, overlap=False, **kw)
+    lo, po, _ = _train(mode, overlap=True, **kw)
+    for a, b in zip(lo, ls):
+        assert abs(a - b) <= 1e-2 * max(1.0, abs(b)), (lo, ls)
+    err = (po - ps_).abs().max().item()
+    assert err < 1e-2, err
 
 
 def test_graph_replay_matches_eager(cuda):
@@ -131,5 +161,6 @@ def test_zero_copy_concat_matches_copy_path(cuda, block, monkeypatch):
 
     y1, g1 = run(True)
     y2, g2 = run(False)
-    assert (y1 - y2).abs().max().item() < 5e-2
+    # the two paths may pick different autotuned kernels: allow one bf16 ulp of the output scale
+    assert ((y1 - y2).abs() <= 5e-2 + 2 ** -7 * y2.abs()).all().item(), (y1 - y2).abs().max().item()
     assert ((g1 - g2).norm() / g2.norm()).item() < 2e-2

@@ -21,7 +21,7 @@ import torch
 from torch import nn
 
 from ..ops.concat import Slot, assemble, concat_buffer
-from ..ops.pool import avg_pool3x3_s1, max_pool
+from ..ops.pool import avg_pool, avg_pool3x3_s1, global_avg_pool, max_pool
 from ..ops.fused import FusedHead
 from .layers import ConvBNAct, init_weights
 
@@ -197,9 +197,9 @@ class InceptionAux(_Block):
         self.fc = nn.Linear(768, num_classes)
 
     def forward(self, x):
-        x = nn.functional.avg_pool2d(x, 5, 3)
+        x = avg_pool(x, 5, 3) if self.fused else nn.functional.avg_pool2d(x, 5, 3)
         x = self.conv1(self.conv0(x))
-        x = torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1)
+        x = global_avg_pool(x) if self.fused else torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)
 
 
@@ -231,7 +231,7 @@ class InceptionV3(nn.Module):
         x = self.mixed_6(self.mixed_6a(self.mixed_5(x)))
         aux = self.aux(x) if (self.aux is not None and self.training) else None
         x = self.mixed_7(x)
-        x = torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1)
+        x = global_avg_pool(x) if self.fused else torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1)
         logits = self.fc(self.dropout(x))
         return (logits, aux) if aux is not None else logits
 

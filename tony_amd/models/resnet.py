@@ -21,6 +21,7 @@ import torch
 from torch import nn
 
 from ..ops.bn import BatchNormAct2d
+from ..ops.pool import global_avg_pool
 from ..ops.residual import bn_add_relu, conv1x1_bn_add_relu
 from .layers import ConvBNAct, init_weights
 
@@ -74,7 +75,7 @@ class ResNet(nn.Module):
         x = self.stem(x)
         x = torch.nn.functional.max_pool2d(x, 3, 2, 1)
         x = self.blocks(x)
-        x = x.mean((2, 3))
+        x = global_avg_pool(x) if self.fused else x.mean((2, 3))
         return self.fc(x)
 
 

@@ -79,6 +79,8 @@ _SIGNATURES = {
                          c_void_p],
     "tony_maxpool_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
                          c_void_p],
+    "tony_avgpool_fwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
+    "tony_avgpool_bwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
     "tony_transpose_desc_bytes": [],
     "tony_transpose_batch": [c_void_p, c_int, c_int, c_void_p],
     # xGMI peer-memory collectives (csrc/xgmi.hip, parallel/xgmi.py)

@@ -24,7 +24,7 @@ from typing import Callable, Dict, Tuple
 
 import torch
 
-from . import _lib, concat, tune, wt_cache
+from . import _lib, concat, streams, tune, wt_cache
 from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 from .gemm import WGRAD_OCC, splitk_combine, wgrad_cus
@@ -224,18 +224,19 @@ def _wgrad(dy, x, weight, stride, padding):
     if impl is None:
         impl = _choose(key, {"tony": lambda: conv_wgrad(dy, x, weight.shape, stride, padding),
                              "miopen": lambda: _miopen_wgrad(dy, x, weight, stride, padding)})
-    if impl == "tony":
-        gw = _lib.grad_slot(weight)
-        if gw is not None and gw.is_contiguous(memory_format=torch.channels_last):
-            conv_wgrad(dy, x, weight.shape, stride, padding, dst=gw)  # summed straight into the slot
-            return None
-        return _accumulate_wgrad(weight, conv_wgrad(dy, x, weight.shape, stride, padding))
-    dw = _miopen_wgrad(dy, x, weight, stride, padding)
     gw = _lib.grad_slot(weight)
+    if impl == "tony":
+        if gw is not None and gw.is_contiguous(memory_format=torch.channels_last):
+            # summed straight into the slot (on the weight-gradient stream when one is active)
+            return streams.run(lambda: conv_wgrad(dy, x, weight.shape, stride, padding, dst=gw), dy, x)
+        return _accumulate_wgrad(weight, conv_wgrad(dy, x, weight.shape, stride, padding))
     if gw is None:
-        return dw
-    gw.add_(dw)
-    return None
+        return _miopen_wgrad(dy, x, weight, stride, padding)
+
+    def into_slot():
+        gw.add_(_miopen_wgrad(dy, x, weight, stride, padding))
+
+    return streams.run(into_slot, dy, x)
 
 
 def _accumulate_wgrad(weight, dw32):
@@ -266,8 +267,8 @@ class _ConvFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
         dy = _as_rows(dy)[0]
+        dw = _wgrad(dy, x, weight, ctx.stride, ctx.padding)  # first: overlaps the dgrad on the side stream
         dx = _dgrad(dy, weight, x.shape, ctx.stride, ctx.padding) if ctx.needs_input_grad[0] else None
-        dw = _wgrad(dy, x, weight, ctx.stride, ctx.padding)
         return dx, dw, None, None
 
 
@@ -332,8 +333,8 @@ class _ConvBNActFn(torch.autograd.Function):
                            invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), pb, int(relu), ws.data_ptr(),
                            dgamma.data_ptr(), dbeta.data_ptr(), int(inplace), _lib.stream_ptr(dev))
         _lib.check(rc, "tony_bn_bwd")
+        dw = _wgrad(dZ, x, weight, stride, padding)  # first: overlaps the dgrad on the side stream
         dx = _dgrad(dZ, weight, x.shape, stride, padding) if ctx.needs_input_grad[0] else None
-        dw = _wgrad(dZ, x, weight, stride, padding)
         if inplace:
             dgamma = dbeta = None
         return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None

@@ -2,6 +2,8 @@
 //
 // * avg 3x3, stride 1, pad 1, count_include_pad: y = (1/9) * box(x).  The
 //   stencil is symmetric, so the backward dx = (1/9) * box(dy) is the SAME kernel.
+// * avg KxK, stride S, no padding (aux head, global pool): direct window sum; backward gathers
+//   over the covering windows like the max-pool backward.
 // * max KxK, stride S, no padding: forward writes y and, per output element and
 //   channel, the argmax offset inside its window as one byte; backward is a
 //   gather over the <= ceil(K/S)^2 windows covering each input (no atomics).
@@ -19,15 +21,18 @@ constexpr int kThreads = 256;
 
 __global__ __launch_bounds__(kThreads) void box3_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                         int N, int H, int W, int C, int64_t ldx, int64_t ldy) {
-  const int CG = C >> 3;
-  const int64_t total = static_cast<int64_t>(N) * H * W * CG;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
-  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total; t += stride) {
-    const int cg = static_cast<int>(t % CG);
-    const int64_t site = t / CG;
+  // 32-bit index math (the host checks the element count fits): 64-bit div/mod are long
+  // instruction sequences and made these memory-bound kernels ALU-bound
+  const uint32_t CG = C >> 3;
+  const uint32_t total = static_cast<uint32_t>(N) * H * W * CG;
+  const uint32_t stride = gridDim.x * kThreads;
+  for (uint32_t t = blockIdx.x * kThreads + threadIdx.x; t < total; t += stride) {
+    const uint32_t cg = t % CG;
+    const uint32_t site = t / CG;
     const int w = static_cast<int>(site % W);
-    const int h = static_cast<int>((site / W) % H);
-    const int64_t n = site / (static_cast<int64_t>(W) * H);
+    const uint32_t nh = site / W;
+    const int h = static_cast<int>(nh % H);
+    const int64_t n = nh / H;
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int dh = -1; dh <= 1; ++dh) {
@@ -45,7 +50,7 @@ __global__ __launch_bounds__(kThreads) void box3_kernel(const uint16_t* __restri
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] *= (1.f / 9.f);
-    store8(y + site * ldy + cg * 8, bf16x8::from_float(acc));
+    store8(y + static_cast<int64_t>(site) * ldy + cg * 8, bf16x8::from_float(acc));
   }
 }
 
@@ -53,15 +58,16 @@ __global__ __launch_bounds__(kThreads) void maxpool_fwd_kernel(const uint16_t* _
                                                                uint16_t* __restrict__ y, uint8_t* __restrict__ arg,
                                                                int N, int H, int W, int C, int OH, int OW, int K,
                                                                int S, int64_t ldx, int64_t ldy) {
-  const int CG = C >> 3;
-  const int64_t total = static_cast<int64_t>(N) * OH * OW * CG;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
-  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total; t += stride) {
-    const int cg = static_cast<int>(t % CG);
-    const int64_t site = t / CG;
+  const uint32_t CG = C >> 3;
+  const uint32_t total = static_cast<uint32_t>(N) * OH * OW * CG;
+  const uint32_t stride = gridDim.x * kThreads;
+  for (uint32_t t = blockIdx.x * kThreads + threadIdx.x; t < total; t += stride) {
+    const uint32_t cg = t % CG;
+    const uint32_t site = t / CG;
     const int ow = static_cast<int>(site % OW);
-    const int oh = static_cast<int>((site / OW) % OH);
-    const int64_t n = site / (static_cast<int64_t>(OW) * OH);
+    const uint32_t nh = site / OW;
+    const int oh = static_cast<int>(nh % OH);
+    const int64_t n = nh / OH;
     float best[8];
     uint8_t bi[8];
 #pragma unroll
@@ -85,11 +91,11 @@ __global__ __launch_bounds__(kThreads) void maxpool_fwd_kernel(const uint16_t* _
         }
       }
     }
-    store8(y + site * ldy + cg * 8, bf16x8::from_float(best));
+    store8(y + static_cast<int64_t>(site) * ldy + cg * 8, bf16x8::from_float(best));
     uint2 packed;
     packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (static_cast<uint32_t>(bi[3]) << 24);
     packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (static_cast<uint32_t>(bi[7]) << 24);
-    *reinterpret_cast<uint2*>(arg + site * C + cg * 8) = packed;
+    *reinterpret_cast<uint2*>(arg + static_cast<int64_t>(site) * C + cg * 8) = packed;
   }
 }
 
@@ -98,15 +104,16 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd_kernel(const uint16_t* _
                                                                uint16_t* __restrict__ dx, int N, int H, int W, int C,
                                                                int OH, int OW, int K, int S, int64_t lddy,
                                                                int64_t lddx) {
-  const int CG = C >> 3;
-  const int64_t total = static_cast<int64_t>(N) * H * W * CG;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
-  for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total; t += stride) {
-    const int cg = static_cast<int>(t % CG);
-    const int64_t site = t / CG;
+  const uint32_t CG = C >> 3;
+  const uint32_t total = static_cast<uint32_t>(N) * H * W * CG;
+  const uint32_t stride = gridDim.x * kThreads;
+  for (uint32_t t = blockIdx.x * kThreads + threadIdx.x; t < total; t += stride) {
+    const uint32_t cg = t % CG;
+    const uint32_t site = t / CG;
     const int w = static_cast<int>(site % W);
-    const int h = static_cast<int>((site / W) % H);
-    const int64_t n = site / (static_cast<int64_t>(W) * H);
+    const uint32_t nh = site / W;
+    const int h = static_cast<int>(nh % H);
+    const int64_t n = nh / H;
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     // windows oh with oh*S <= h <= oh*S + K - 1
     const int oh_lo = h >= K ? (h - K + S) / S : 0;
@@ -128,7 +135,73 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd_kernel(const uint16_t* _
         }
       }
     }
-    store8(dx + site * lddx + cg * 8, bf16x8::from_float(acc));
+    store8(dx + static_cast<int64_t>(site) * lddx + cg * 8, bf16x8::from_float(acc));
+  }
+}
+
+// avg KxK, stride S, no padding (Inception aux head 5x5/s3; K = H = W is the global average pool).
+__global__ __launch_bounds__(kThreads) void avgpool_fwd_kernel(const uint16_t* __restrict__ x,
+                                                               uint16_t* __restrict__ y, int N, int H, int W, int C,
+                                                               int OH, int OW, int K, int S, int64_t ldx,
+                                                               int64_t ldy) {
+  const uint32_t CG = C >> 3;
+  const uint32_t total = static_cast<uint32_t>(N) * OH * OW * CG;
+  const uint32_t stride = gridDim.x * kThreads;
+  const float inv = 1.f / static_cast<float>(K * K);
+  for (uint32_t t = blockIdx.x * kThreads + threadIdx.x; t < total; t += stride) {
+    const uint32_t cg = t % CG;
+    const uint32_t site = t / CG;
+    const int ow = static_cast<int>(site % OW);
+    const uint32_t nh = site / OW;
+    const int oh = static_cast<int>(nh % OH);
+    const int64_t n = nh / OH;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int r = 0; r < K; ++r) {
+      const int64_t row = (n * H + oh * S + r) * W + ow * S;
+      for (int s = 0; s < K; ++s) {
+        float v[8];
+        load8(x + (row + s) * ldx + cg * 8).to_float(v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += v[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] *= inv;
+    store8(y + static_cast<int64_t>(site) * ldy + cg * 8, bf16x8::from_float(acc));
+  }
+}
+
+// dx[h, w] = (1/K^2) * sum of dy over the <= ceil(K/S)^2 windows covering (h, w): a gather, no atomics
+__global__ __launch_bounds__(kThreads) void avgpool_bwd_kernel(const uint16_t* __restrict__ dy,
+                                                               uint16_t* __restrict__ dx, int N, int H, int W, int C,
+                                                               int OH, int OW, int K, int S, int64_t lddy,
+                                                               int64_t lddx) {
+  const uint32_t CG = C >> 3;
+  const uint32_t total = static_cast<uint32_t>(N) * H * W * CG;
+  const uint32_t stride = gridDim.x * kThreads;
+  const float inv = 1.f / static_cast<float>(K * K);
+  for (uint32_t t = blockIdx.x * kThreads + threadIdx.x; t < total; t += stride) {
+    const uint32_t cg = t % CG;
+    const uint32_t site = t / CG;
+    const int w = static_cast<int>(site % W);
+    const uint32_t nh = site / W;
+    const int h = static_cast<int>(nh % H);
+    const int64_t n = nh / H;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int oh_lo = h >= K ? (h - K + S) / S : 0;
+    const int oh_hi = min(OH - 1, h / S);
+    const int ow_lo = w >= K ? (w - K + S) / S : 0;
+    const int ow_hi = min(OW - 1, w / S);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh)
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        float g[8];
+        load8(dy + ((n * OH + oh) * OW + ow) * lddy + cg * 8).to_float(g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += g[j];
+      }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] *= inv;
+    store8(dx + static_cast<int64_t>(site) * lddx + cg * 8, bf16x8::from_float(acc));
   }
 }
 
@@ -143,7 +216,7 @@ int grid_for(int64_t work) {
 // y (or dx) = box3x3(x) / 9 over NHWC rows with row strides ldx / ldy.
 TONY_API int tony_avgpool3_s1p1(const void* x, void* y, int N, int H, int W, int C, int64_t ldx, int64_t ldy,
                                 hipStream_t stream) {
-  if (C % 8 || ldx % 8 || ldy % 8) return -1;
+  if (C % 8 || ldx % 8 || ldy % 8 || static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
   box3_kernel<<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, ldx, ldy);
   TONY_LAUNCH_CHECK();
@@ -153,6 +226,7 @@ TONY_API int tony_avgpool3_s1p1(const void* x, void* y, int N, int H, int W, int
 TONY_API int tony_maxpool_fwd(const void* x, void* y, void* argmax, int N, int H, int W, int C, int K, int S,
                               int64_t ldx, int64_t ldy, hipStream_t stream) {
   if (C % 8 || ldx % 8 || ldy % 8 || K * K > 255 || H < K || W < K) return -1;
+  if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
   const int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
   maxpool_fwd_kernel<<<grid_for(static_cast<int64_t>(N) * OH * OW * (C / 8)), kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), static_cast<uint8_t*>(argmax), N, H, W, C, OH, OW,
@@ -164,10 +238,33 @@ TONY_API int tony_maxpool_fwd(const void* x, void* y, void* argmax, int N, int H
 TONY_API int tony_maxpool_bwd(const void* dy, const void* argmax, void* dx, int N, int H, int W, int C, int K, int S,
                               int64_t lddy, int64_t lddx, hipStream_t stream) {
   if (C % 8 || lddy % 8 || lddx % 8 || H < K || W < K) return -1;
+  if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
   const int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
   maxpool_bwd_kernel<<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(dy), static_cast<const uint8_t*>(argmax), static_cast<uint16_t*>(dx), N, H, W, C,
       OH, OW, K, S, lddy, lddx);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+TONY_API int tony_avgpool_fwd(const void* x, void* y, int N, int H, int W, int C, int K, int S, int64_t ldx,
+                              int64_t ldy, hipStream_t stream) {
+  if (C % 8 || ldx % 8 || ldy % 8 || K < 1 || S < 1 || H < K || W < K) return -1;
+  if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
+  const int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
+  avgpool_fwd_kernel<<<grid_for(static_cast<int64_t>(N) * OH * OW * (C / 8)), kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, OH, OW, K, S, ldx, ldy);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+TONY_API int tony_avgpool_bwd(const void* dy, void* dx, int N, int H, int W, int C, int K, int S, int64_t lddy,
+                              int64_t lddx, hipStream_t stream) {
+  if (C % 8 || lddy % 8 || lddx % 8 || K < 1 || S < 1 || H < K || W < K) return -1;
+  if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
+  const int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
+  avgpool_bwd_kernel<<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(dy), static_cast<uint16_t*>(dx), N, H, W, C, OH, OW, K, S, lddy, lddx);
   TONY_LAUNCH_CHECK();
   return 0;
 }

@@ -32,7 +32,7 @@ from typing import Sequence
 import torch
 from torch import nn
 
-from . import _lib, concat, tune, wt_cache
+from . import _lib, concat, streams, tune, wt_cache
 from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 from .gemm import wgrad_tn
@@ -171,6 +171,9 @@ class _HeadFn(torch.autograd.Function):
             _lib.check(rc, "tony_bn_bwd_apply")
             rc = L.tony_avgpool3_s1p1(dP.data_ptr(), _off(dZ, c0), n, h, w, npool, npool, ctot, stream)
             _lib.check(rc, "tony_avgpool3_s1p1")
+        if inplace:  # dW summed straight into the flat gradient slot ([ctot][cin] = the slot's order),
+            # issued first so that it overlaps the dgrad GEMM on the weight-gradient stream
+            streams.run(lambda: wgrad_tn(dZ.data_ptr(), ctot, x.data_ptr(), ldx, M, ctot, cin, dev, dst=gw), dZ, x)
         dx = None
         if ctx.needs_input_grad[0]:
             wt = wt_cache.transposed(weight).reshape(cin, ctot)  # [Cin, Ctot]
@@ -178,8 +181,7 @@ class _HeadFn(torch.autograd.Function):
             rc = L.tony_gemm_bf16(dZ.data_ptr(), wt.data_ptr(), dx.data_ptr(), M, cin, ctot, ctot, ctot, cin,
                                   tune.gemm_flags(dZ, wt, dx, M, cin, ctot, ctot, False), 0, 0, stream)
             _lib.check(rc, "tony_gemm_bf16")
-        if inplace:  # dW summed straight into the flat gradient slot ([ctot][cin] = the slot's order)
-            wgrad_tn(dZ.data_ptr(), ctot, x.data_ptr(), ldx, M, ctot, cin, dev, dst=gw)
+        if inplace:
             return dx, None, None, None, None, None, None, None, None, None, None, None
         dw32 = wgrad_tn(dZ.data_ptr(), ctot, x.data_ptr(), ldx, M, ctot, cin, dev)
         dw = dw32.to(weight.dtype).reshape(weight.shape)

@@ -62,6 +62,44 @@ class _MaxPoolFn(torch.autograd.Function):
         return dx, None, None, None
 
 
+class _AvgPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s):
+        x, (_, c, ld) = _as_rows(x)
+        n, _, h, w = x.shape
+        oh, ow = (h - k) // s + 1, (w - k) // s + 1
+        y = _nhwc_empty(n, c, oh, ow, x)
+        rc = _lib.lib().tony_avgpool_fwd(x.data_ptr(), y.data_ptr(), n, h, w, c, k, s, ld, c,
+                                         _lib.stream_ptr(x.device))
+        _lib.check(rc, "tony_avgpool_fwd")
+        ctx.shape = (n, c, h, w, k, s)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, c, h, w, k, s = ctx.shape
+        dy, (_, _, lddy) = _as_rows(dy)
+        dx = _nhwc_empty(n, c, h, w, dy)
+        rc = _lib.lib().tony_avgpool_bwd(dy.data_ptr(), dx.data_ptr(), n, h, w, c, k, s, lddy, c,
+                                         _lib.stream_ptr(dy.device))
+        _lib.check(rc, "tony_avgpool_bwd")
+        return dx, None, None
+
+
+def avg_pool(x: torch.Tensor, k: int, s: int) -> torch.Tensor:
+    """avg_pool2d(x, k, s) (no padding) on channels_last bf16; k = H = W is the global average pool."""
+    if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0:
+        return _AvgPoolFn.apply(x, k, s)
+    return torch.nn.functional.avg_pool2d(x, k, s)
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    """adaptive_avg_pool2d(x, 1) flattened to [N, C]."""
+    if x.shape[2] == x.shape[3]:
+        return torch.flatten(avg_pool(x, x.shape[2], 1), 1)
+    return torch.flatten(torch.nn.functional.adaptive_avg_pool2d(x, 1), 1)
+
+
 def avg_pool3x3_s1(x: torch.Tensor) -> torch.Tensor:
     """avg_pool2d(x, 3, 1, 1, count_include_pad=True) on channels_last bf16."""
     if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0:

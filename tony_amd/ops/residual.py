@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import torch
 
-from . import _lib, tune, wt_cache
+from . import _lib, streams, tune, wt_cache
 from .arena import zeros_f32
 from .bn import _as_rows, _empty_like_rows, _rows_view
 from .fused import _cl_empty
@@ -137,6 +137,10 @@ class _Conv1x1BNAddReLUFn(torch.autograd.Function):
         cout = weight.shape[0]
         dZ, dres, (dg, db) = _bwd_res(L, Z, cout, dy, y, M, cout, mean, invstd, gamma, beta, ctx.pb, ctx.params[1:],
                                       stream)
+        gw = _lib.grad_slot(ctx.params[0])
+        dw = None
+        if gw is not None and dg is None:  # dW summed straight into the flat gradient slot (side stream)
+            streams.run(lambda: wgrad_tn(dZ.data_ptr(), cout, x.data_ptr(), ldx, M, cout, cin, dev, dst=gw), dZ, x)
         dx = None
         if ctx.needs_input_grad[0]:
             wt = wt_cache.transposed(weight).reshape(cin, cout)
@@ -144,11 +148,7 @@ class _Conv1x1BNAddReLUFn(torch.autograd.Function):
             rc = L.tony_gemm_bf16(dZ.data_ptr(), wt.data_ptr(), dx.data_ptr(), M, cin, cout, cout, cout, cin,
                                   tune.gemm_flags(dZ, wt, dx, M, cin, cout, cout, False), 0, 0, stream)
             _lib.check(rc, "tony_gemm_bf16")
-        gw = _lib.grad_slot(ctx.params[0])
-        if gw is not None and dg is None:  # dW summed straight into the flat gradient slot
-            wgrad_tn(dZ.data_ptr(), cout, x.data_ptr(), ldx, M, cout, cin, dev, dst=gw)
-            dw = None
-        else:
+        if gw is None or dg is not None:
             dw = wgrad_tn(dZ.data_ptr(), cout, x.data_ptr(), ldx, M, cout, cin, dev).to(weight.dtype)
             dw = dw.reshape(weight.shape)
         return dx, dw, dres, dg, db, None, None, None, None, None

@@ -14,7 +14,7 @@ from typing import Callable
 
 import torch
 
-from ..ops import wt_cache
+from ..ops import streams, wt_cache
 from ..ops.arena import for_device
 from ..utils.tracing import heartbeat, trace_range
 from .ps import ParameterServer
@@ -22,7 +22,7 @@ from .ps import ParameterServer
 
 class Trainer:
     def __init__(self, model: torch.nn.Module, ps: ParameterServer, loss_fn: Callable, use_graph: bool = False,
-                 warmup_eager: int = 3, graph_collectives: bool | None = None):
+                 warmup_eager: int = 3, graph_collectives: bool | None = None, overlap_wgrad: bool = True):
         self.model = model
         self.ps = ps
         self.loss_fn = loss_fn
@@ -33,6 +33,9 @@ class Trainer:
         # launches, so nothing is lost, and no communicator state is baked into the graph
         # (RCCL's graph-capture support differs across releases).  One rank: all in the graph.
         self.graph_collectives = (ps.world == 1) if graph_collectives is None else graph_collectives
+        self.overlap_wgrad = overlap_wgrad
+        self._tuned = False
+        self.side_ops = 0
         self.graph = None
         self.static_x = None
         self.static_y = None
@@ -52,8 +55,16 @@ class Trainer:
         with trace_range("forward"):
             out = self.model(x)
             loss = self.loss_fn(out, y)
+        # weight gradients on a second stream, overlapped with the data-gradient chain (ops/streams.py);
+        # not in the first step, whose autotuning times kernels on the current stream
+        overlap = self.overlap_wgrad and self._tuned and streams.begin(self.ps.flat.device)
         with trace_range("backward"):
-            loss.backward()
+            try:
+                loss.backward()
+            finally:
+                if overlap:
+                    self.side_ops = streams.end()  # joined before the PS reads the gradients
+        self._tuned = True
         if ps_step:
             self._ps_step()
         return loss

@@ -15,7 +15,7 @@ step() {  # step <name> <timeout_s> <cmd...>
 }
 for s in "$@"; do
   case $s in
-    tests) step gpu_tests 900 python -m pytest tests -m gpu -x -q ;;
+    tests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     smoke) step smoke 600 python __graft_entry__.py smoke ;;
     bench_eager) step bench_eager 900 python bench.py --steps 10 --warmup 4 --no-graph --no-miopen-find ;;
     bench) step bench 900 python bench.py --steps 20 --warmup 6 ;;
@@ -25,12 +25,13 @@ for s in "$@"; do
           python3 tools/prof_summary.py gpurun_out/prof --skip 6 > gpurun_out/prof_summary.md; find gpurun_out/prof -name '*trace*' -delete ;;
     prof_graph) export TMPDIR=/tmp; R=$(pwd)   # the headline configuration: HIP graph + MIOpen find
           step prof_graph 1100 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_graph" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 6 ${BENCH_ARGS:-}
-          python3 tools/prof_summary.py gpurun_out/prof_graph --skip 8 > gpurun_out/prof_graph_summary.md
+          python3 tools/prof_summary.py gpurun_out/prof_graph --skip 8 --top 100 > gpurun_out/prof_graph_summary.md
           python3 tools/prof_summary.py gpurun_out/prof_graph --skip 8 --sequence > gpurun_out/prof_graph_sequence.txt || true
           find gpurun_out/prof_graph -name '*trace*' -delete ;;
     prof_stock) export TMPDIR=/tmp; R=$(pwd)
           step prof_stock 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_stock" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 5 --no-graph --no-miopen-find --stock
           python3 tools/prof_summary.py gpurun_out/prof_stock --skip 6 > gpurun_out/prof_stock_summary.md; find gpurun_out/prof_stock -name '*trace*' -delete ;;
+    bench_serial) step bench_serial 900 python bench.py --steps 20 --warmup 6 --no-wgrad-stream ;;
     bench_imm) step bench_imm 1100 python bench.py --steps 20 --warmup 6 --no-miopen-find ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
   esac
