@@ -24,3 +24,18 @@ def test_arena_grows_then_serves_zeroed_slices():
     t = zeros_f32(7, "cpu")  # outside a step: plain zeros
     assert t.abs().sum() == 0 and t.data_ptr() != a.buf.data_ptr()
     del t1, t2
+
+
+def test_side_stream_inactive_runs_inline():
+    """ops/streams.py: without a CUDA device (or before begin()) gradient work runs right here."""
+    from tony_amd.ops import streams
+
+    assert streams.begin("cpu") is False and not streams.active()
+    acc = torch.zeros(4)
+
+    def work():
+        acc.add_(1.0)
+
+    assert streams.run(work, acc) is None
+    assert acc.tolist() == [1.0] * 4
+    assert streams.end() == 0

@@ -170,7 +170,14 @@ def available() -> bool:
         return False
 
 
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(device=None) -> int:
+    """The current HIP stream of ``device`` as an integer (the raw binding: every kernel launch asks)."""
+    if _RAW_STREAM is not None:
+        idx = getattr(device, "index", None)
+        return _RAW_STREAM(torch.cuda.current_device() if idx is None else idx)
     return torch.cuda.current_stream(device).cuda_stream
 
 

@@ -177,13 +177,15 @@ def _time(fn: Callable[[], object], reps: int = 5) -> float:
     return tune.time_ms(fn, reps)
 
 
-def _choose(key: Tuple, candidates: Dict[str, Callable[[], object]], default: str = "tony") -> str:
+def _choose(key: Tuple, candidates: Dict[str, Callable[[], object]], default: str = "tony",
+            weight: Dict[str, float] | None = None) -> str:
+    """Fastest candidate for ``key`` (cached); ``weight`` scales a candidate's measured time."""
     c = _CHOICE.get(key)
     if c is not None:
         return c
     if not AUTOTUNE or len(candidates) == 1 or torch.cuda.is_current_stream_capturing():
         return default if default in candidates else next(iter(candidates))
-    times = {name: _time(fn) for name, fn in candidates.items()}
+    times = {name: _time(fn) * (weight or {}).get(name, 1.0) for name, fn in candidates.items()}
     c = min(times, key=times.get)
     _CHOICE[key] = c
     return c
@@ -217,13 +219,22 @@ def _dgrad(dy, weight, x_shape, stride, padding):
         _miopen_dgrad(dy, weight, x_shape, stride, padding)
 
 
+MIOPEN_WGRAD_WEIGHT = float(os.environ.get("TONY_MIOPEN_WGRAD_WEIGHT", "1.6"))
+# TONY_WGRAD_IMPL=tony|miopen pins the weight-gradient implementation (autotuned per shape otherwise)
+WGRAD_IMPL = os.environ.get("TONY_WGRAD_IMPL", "")
+
+
 def _wgrad(dy, x, weight, stride, padding):
     """dW accumulated into the parameter's gradient slot (returns None) or returned for autograd."""
     key = ("wgrad", tuple(dy.shape), tuple(weight.shape), stride, padding)
-    impl = _CHOICE.get(key)
+    impl = _CHOICE.get(key) or WGRAD_IMPL or None
     if impl is None:
+        # With the weight gradients on the side stream (ops/streams.py) their GPU time hides behind the
+        # data-gradient chain, while MIOpen's costs 3 more launches (output fill, fp32->bf16 cast, add
+        # into the slot) and ~40 us of host time each: MIOpen must win by a margin to be picked.
         impl = _choose(key, {"tony": lambda: conv_wgrad(dy, x, weight.shape, stride, padding),
-                             "miopen": lambda: _miopen_wgrad(dy, x, weight, stride, padding)})
+                             "miopen": lambda: _miopen_wgrad(dy, x, weight, stride, padding)},
+                       weight={"miopen": MIOPEN_WGRAD_WEIGHT if streams.ENABLED else 1.0})
     gw = _lib.grad_slot(weight)
     if impl == "tony":
         if gw is not None and gw.is_contiguous(memory_format=torch.channels_last):
