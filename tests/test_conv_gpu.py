@@ -147,3 +147,51 @@ def test_inception_tony_convs_match_miopen_convs(cuda):
     assert len(rels) > 40
     worst = max(rels)
     assert worst[0] < 2e-2, f"layer {worst[1]} differs by {worst[0]:.4f}"
+
+
+@pytest.mark.parametrize("cfg", [(4, 64, 35, 35, 96, (3, 3), 1, (1, 1)), (2, 160, 17, 17, 192, (7, 1), 1, (3, 0)),
+                                 (2, 288, 35, 35, 384, (3, 3), 2, (0, 0)), (3, 256, 9, 9, 80, (1, 1), 1, (0, 0)),
+                                 (1, 384, 8, 8, 384, (1, 3), 1, (0, 1))])
+@pytest.mark.parametrize("relu", [True, False])
+def test_conv_bn_act_infer_folded_epilogue(cuda, cfg, relu):
+    """Inference conv + BN(running stats) + ReLU in one kernel (H5) vs fp32 conv2d + batch_norm."""
+    from tony_amd.ops import concat
+    from tony_amd.ops.conv import conv_bn_act_infer
+
+    n, ci, h, w, co, k, st, pad = cfg
+    torch.manual_seed(11)
+    x = torch.randn(n, ci, h, w, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wt = (torch.randn(co, ci, *k, device=cuda) * (ci * k[0] * k[1]) ** -0.5).to(torch.bfloat16)
+    wt = wt.contiguous(memory_format=torch.channels_last)
+    g, b = torch.rand(co, device=cuda) + 0.5, torch.randn(co, device=cuda) * 0.1
+    rm, rv = torch.randn(co, device=cuda) * 0.1, torch.rand(co, device=cuda) + 0.5
+    with torch.no_grad():
+        ref = torch.nn.functional.conv2d(x.float(), wt.float(), None, st, pad)
+        ref = torch.nn.functional.batch_norm(ref, rm, rv, g, b, False, 0.0, 1e-3)
+        ref = torch.relu(ref) if relu else ref
+        y = conv_bn_act_infer(x, wt, g, b, rm, rv, st, pad, 1e-3, relu)
+        assert y.is_contiguous(memory_format=torch.channels_last)
+        torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+        # straight into a channel slice of a wider concat buffer
+        buf = concat.concat_buffer(n, co + 32, ref.shape[2], ref.shape[3], x)
+        ys = conv_bn_act_infer(x, wt, g, b, rm, rv, st, pad, 1e-3, relu, slot=concat.Slot(buf, 32))
+        assert ys.data_ptr() == buf[:, 32:].data_ptr()
+        torch.testing.assert_close(buf[:, 32:].float(), ref, rtol=2e-2, atol=2e-2)
+
+
+def test_inception_eval_folded_matches_unfolded(cuda):
+    """Inception-v3 eval under no_grad (folded-BN epilogues) == eval with autograd on (separate BN apply)."""
+    from tony_amd.models.inception_v3 import inception_v3
+
+    m = inception_v3(seed=3).to(cuda).to(memory_format=torch.channels_last)
+    for p in m.parameters():
+        p.data = p.data.to(torch.bfloat16)
+    m.train()
+    x = torch.randn(8, 3, 299, 299, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    m(x)  # one training forward: non-trivial running statistics
+    m.eval()
+    with torch.no_grad():
+        y_fold = m(x).float()
+    y_ref = m(x).float().detach()
+    err = ((y_fold - y_ref).norm() / y_ref.norm()).item()
+    assert err < 3e-2, err

@@ -44,6 +44,13 @@ class ConvBNAct(nn.Module):
     def forward(self, x, slot=None):
         """``slot`` (ops/concat.Slot): write the output into a block's concat buffer when the fused
         kernels run (ignored on the stock / CPU path, where the block copies it in)."""
+        if (self.fused and x.is_cuda and not self.training and not torch.is_grad_enabled()
+                and conv_ops.supported(x, self.conv.weight, self.conv.stride, self.conv.padding, min_rows=1)
+                and (self.is_1x1 or USE_TONY_CONV)):
+            # inference: BN folded into the conv's MFMA epilogue, one kernel per layer (ops/conv.py)
+            bn, c = self.bn, self.conv
+            return conv_ops.conv_bn_act_infer(x, c.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                              c.stride, c.padding, bn.eps, bn.relu, slot)
         if self.fused and self.is_1x1 and self.bn.relu and x.is_cuda:
             # MFMA GEMM with BN statistics in its epilogue + fused apply (ops/fused.py)
             bn = self.bn

@@ -41,13 +41,15 @@ def _pair(v):
 MIN_ROWS = 2048  # below this many output pixels a tile grid cannot fill 256 CUs: leave it to MIOpen
 
 
-def supported(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, dilation=1, groups=1) -> bool:
+def supported(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, dilation=1, groups=1,
+              min_rows: int = 0) -> bool:
+    """Whether the tony kernels take this conv (``min_rows``: fewest output pixels, default MIN_ROWS)."""
     if not (x.is_cuda and x.dtype == _BF16 and weight.dtype == _BF16 and x.dim() == 4 and groups == 1
             and _pair(dilation) == (1, 1) and x.shape[1] % 8 == 0 and weight.shape[0] % 8 == 0
             and weight.shape[1] == x.shape[1]):
         return False
     oh, ow = out_hw(x.shape[2], x.shape[3], weight.shape[2], weight.shape[3], stride, padding)
-    return x.shape[0] * oh * ow >= MIN_ROWS
+    return x.shape[0] * oh * ow >= (min_rows or MIN_ROWS)
 
 
 def out_hw(h, w, r, s, stride, padding):
@@ -360,3 +362,54 @@ def conv_bn_act(x, weight, gamma, beta, running_mean, running_var, stride=1, pad
     z = torch.nn.functional.conv2d(x, weight, None, stride, padding)
     y = torch.nn.functional.batch_norm(z, running_mean, running_var, gamma, beta, training, momentum, eps)
     return torch.relu(y) if relu else y
+
+
+# ------------------------------------------------------------------------------ inference --
+_AFF: Dict[int, Tuple] = {}
+
+
+def folded_bn(gamma, beta, running_mean, running_var, eps) -> torch.Tensor:
+    """[scale | shift] fp32 of an inference BatchNorm (y = z * scale + shift), cached until any of
+    the four tensors changes (their version counters)."""
+    key = id(gamma)
+    ver = (gamma._version, beta._version, running_mean._version, running_var._version, float(eps),
+           gamma.data_ptr(), running_var.data_ptr())
+    hit = _AFF.get(key)
+    if hit is not None and hit[0] == ver:
+        return hit[1]
+    scale = gamma.float() * torch.rsqrt(running_var.float() + eps)
+    aff = torch.cat([scale, beta.float() - running_mean.float() * scale]).contiguous()
+    _AFF[key] = (ver, aff)
+    return aff
+
+
+def conv_bn_act_infer(x, weight, gamma, beta, running_mean, running_var, stride=1, padding=0, eps=1e-3,
+                      relu=True, slot=None):
+    """Inference conv + BatchNorm(running statistics) + ReLU in ONE kernel: the
+    BN folds into a per-channel scale / shift applied to the fp32 accumulators in the MFMA epilogue
+    (implicit-GEMM conv, or the NT GEMM for 1x1 / stride-1 convs), so the activation is written once
+    and never re-read.  No autograd (call under ``torch.no_grad()``); with a ``concat.Slot`` the
+    output goes straight into the block's concat buffer."""
+    x, (M, C, ldx) = _as_rows(x)
+    n, _, h, w = x.shape
+    co, _, r, s = weight.shape
+    (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
+    oh, ow = out_hw(h, w, r, s, stride, padding)
+    aff = folded_bn(gamma, beta, running_mean, running_var, eps)
+    y = concat.take(slot, n, co, oh, ow, x)
+    if y is None:
+        y = _cl_empty(n, co, oh, ow, x.device)
+    _, _, ldy = _rows_view(y)
+    L, st = _lib.lib(), _lib.stream_ptr(x.device)
+    epi = 2 | (4 if relu else 0)
+    wk = _krsc(weight)
+    if (r, s, sh, sw, ph, pw) == (1, 1, 1, 1, 0, 0):
+        rc = L.tony_gemm_bf16(x.data_ptr(), wk.data_ptr(), y.data_ptr(), M, co, C, ldx, C, ldy, epi,
+                              aff.data_ptr(), 0, st)
+        _lib.check(rc, "tony_gemm_bf16 (folded BN)")
+        return y
+    rc = L.tony_conv_fwd(x.data_ptr(), n, h, w, C, ldx, wk.data_ptr(), co, r, s, sh, sw, ph, pw, y.data_ptr(), oh,
+                         ow, ldy, epi, aff.data_ptr(), 0, st)
+    _lib.check(rc, "tony_conv_fwd (folded BN)")
+    return y
+

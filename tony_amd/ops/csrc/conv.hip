@@ -101,7 +101,7 @@ template <int BM, int BN>
 __global__ __launch_bounds__(kThreads) void conv_nt_kernel(Gather g, const uint16_t* __restrict__ B,
                                                            uint16_t* __restrict__ C, int64_t ldc, int M, int N,
                                                            float* __restrict__ stats, int64_t sstride,
-                                                           int tiles_n) {
+                                                           int epi, int tiles_n) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int AV = BM * BK / 8 / kThreads, BV = BN * BK / 8 / kThreads;
@@ -176,57 +176,65 @@ __global__ __launch_bounds__(kThreads) void conv_nt_kernel(Gather g, const uint1
     }
     __syncthreads();
   }
+  // epi bit0: BN statistics into stats (sharded); bit1: stats holds [scale | shift] for the folded
+  // inference BN (H5), bit2: ReLU after it
   nt_epilogue<BM, BN, TM, TN>(acc, smem, C, ldc, M, N, m0, n0,
-                               stats != nullptr ? stats + shard_off(tm, sstride) : nullptr);
+                               (epi & 1) ? stats + shard_off(tm, sstride) : nullptr,
+                               (epi & 2) ? stats : nullptr, (epi & 4) != 0);
 }
 
 template <int BM, int BN>
 int launch_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, float* stats,
-              int64_t sstride, hipStream_t stream) {
+              int64_t sstride, int epi, hipStream_t stream) {
   const int tiles_m = ceil_div(M, BM), tiles_n = ceil_div(N, BN);
   const int64_t tiles = static_cast<int64_t>(tiles_m) * tiles_n;
   if (tiles > 0x7fffffff) return -2;
   conv_nt_kernel<BM, BN><<<static_cast<int>(tiles), kThreads, 0, stream>>>(
       g, static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), ldc, static_cast<int>(M), static_cast<int>(N),
-      stats, sstride, tiles_n);
+      stats, sstride, epi, tiles_n);
   TONY_LAUNCH_CHECK();
   return 0;
 }
 
 template <int BM>
 int launch_nt_bm(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, float* st,
-                 int64_t sstride, int64_t bn, hipStream_t stream) {
+                 int64_t sstride, int epi, int64_t bn, hipStream_t stream) {
   if constexpr (BM == 256) {  // 8 x TN accumulators per wave: only narrow column tiles fit the registers
-    if (bn <= 32) return launch_nt<256, 32>(g, B, C, ldc, M, N, st, sstride, stream);
-    if (bn <= 64) return launch_nt<256, 64>(g, B, C, ldc, M, N, st, sstride, stream);
+    if (bn <= 32) return launch_nt<256, 32>(g, B, C, ldc, M, N, st, sstride, epi, stream);
+    if (bn <= 64) return launch_nt<256, 64>(g, B, C, ldc, M, N, st, sstride, epi, stream);
     return -3;
   } else {
     switch (bn) {
-      case 32: return launch_nt<BM, 32>(g, B, C, ldc, M, N, st, sstride, stream);
-      case 64: return launch_nt<BM, 64>(g, B, C, ldc, M, N, st, sstride, stream);
-      case 96: return launch_nt<BM, 96>(g, B, C, ldc, M, N, st, sstride, stream);
-      case 128: return launch_nt<BM, 128>(g, B, C, ldc, M, N, st, sstride, stream);
-      case 160: return launch_nt<BM, 160>(g, B, C, ldc, M, N, st, sstride, stream);
-      default: return launch_nt<BM, 192>(g, B, C, ldc, M, N, st, sstride, stream);
+      case 32: return launch_nt<BM, 32>(g, B, C, ldc, M, N, st, sstride, epi, stream);
+      case 64: return launch_nt<BM, 64>(g, B, C, ldc, M, N, st, sstride, epi, stream);
+      case 96: return launch_nt<BM, 96>(g, B, C, ldc, M, N, st, sstride, epi, stream);
+      case 128: return launch_nt<BM, 128>(g, B, C, ldc, M, N, st, sstride, epi, stream);
+      case 160: return launch_nt<BM, 160>(g, B, C, ldc, M, N, st, sstride, epi, stream);
+      default: return launch_nt<BM, 192>(g, B, C, ldc, M, N, st, sstride, epi, stream);
     }
   }
 }
 
 int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, int flags, float* stats,
            int64_t sstride, hipStream_t stream) {
-  float* st = (flags & 1) ? stats : nullptr;  // accumulated into: the caller zeroes it (ops/arena.py)
+  // flags bit0: statistics accumulated into stats (the caller zeroes it, ops/arena.py);
+  // bit1: stats = [scale | shift] of the folded inference BN, bit2: ReLU after it (H5)
+  const int epi = flags & 7;
+  if ((epi & 1) && (epi & 2)) return -1;
+  if ((epi & 3) && stats == nullptr) return -1;
+  float* st = stats;
   const int v = (flags >> 8) & 0xff;
   if (v >= kNumNtVariants) return -1;
   if (v == 0) {
     const int64_t bn = pick_bn(N, 192);
-    return bn <= 64 ? launch_nt_bm<256>(g, B, C, ldc, M, N, st, sstride, bn, stream)
-                    : launch_nt_bm<128>(g, B, C, ldc, M, N, st, sstride, bn, stream);
+    return bn <= 64 ? launch_nt_bm<256>(g, B, C, ldc, M, N, st, sstride, epi, bn, stream)
+                    : launch_nt_bm<128>(g, B, C, ldc, M, N, st, sstride, epi, bn, stream);
   }
   const int64_t bn = pick_bn(N, kNtVariants[v].cap);
   switch (kNtVariants[v].bm) {
-    case 64: return launch_nt_bm<64>(g, B, C, ldc, M, N, st, sstride, bn, stream);
-    case 128: return launch_nt_bm<128>(g, B, C, ldc, M, N, st, sstride, bn, stream);
-    default: return launch_nt_bm<256>(g, B, C, ldc, M, N, st, sstride, bn, stream);
+    case 64: return launch_nt_bm<64>(g, B, C, ldc, M, N, st, sstride, epi, bn, stream);
+    case 128: return launch_nt_bm<128>(g, B, C, ldc, M, N, st, sstride, epi, bn, stream);
+    default: return launch_nt_bm<256>(g, B, C, ldc, M, N, st, sstride, epi, bn, stream);
   }
 }
 

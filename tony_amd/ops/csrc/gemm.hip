@@ -56,7 +56,7 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(const uint16_t* __res
                                                            const uint16_t* __restrict__ B, int64_t ldb,
                                                            uint16_t* __restrict__ C, int64_t ldc, int M, int N,
                                                            int K, float* __restrict__ stats, int64_t sstride,
-                                                           int tiles_n) {
+                                                           int epi, int tiles_n) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int AV = BM * BK / 8 / kThreads, BV = BN * BK / 8 / kThreads;
@@ -120,38 +120,41 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(const uint16_t* __res
 
   // Epilogue (mfma_common.h): BN column statistics from the fp32 accumulators, then the bf16
   // tile staged through LDS and written back with 16-byte coalesced stores.
+  // epi bit0: BN statistics into stats (sharded); bit1: stats holds [scale | shift] for the folded
+  // inference BN (H5), bit2: ReLU after it
   nt_epilogue<BM, BN, TM, TN>(acc, smem, C, ldc, M, N, m0, n0,
-                               stats != nullptr ? stats + shard_off(tm, sstride) : nullptr);
+                               (epi & 1) ? stats + shard_off(tm, sstride) : nullptr,
+                               (epi & 2) ? stats : nullptr, (epi & 4) != 0);
 }
 
 template <int BM, int BN>
 int launch(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
-           int64_t K, float* stats, int64_t sstride, hipStream_t stream) {
+           int64_t K, float* stats, int64_t sstride, int epi, hipStream_t stream) {
   const int tiles_m = ceil_div(M, BM), tiles_n = ceil_div(N, BN);
   const int64_t tiles = static_cast<int64_t>(tiles_m) * tiles_n;
   if (tiles > 0x7fffffff) return -2;
   gemm_nt_kernel<BM, BN><<<static_cast<int>(tiles), kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(A), lda, static_cast<const uint16_t*>(B), ldb, static_cast<uint16_t*>(C), ldc,
-      static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), stats, sstride, tiles_n);
+      static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), stats, sstride, epi, tiles_n);
   TONY_LAUNCH_CHECK();
   return 0;
 }
 
 template <int BM>
 int launch_bm(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N,
-              int64_t K, float* st, int64_t sstride, int64_t bn, hipStream_t stream) {
+              int64_t K, float* st, int64_t sstride, int epi, int64_t bn, hipStream_t stream) {
   if constexpr (BM == 256) {  // 8 x TN accumulators per wave: only narrow column tiles fit the registers
-    if (bn <= 32) return launch<256, 32>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, stream);
-    if (bn <= 64) return launch<256, 64>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, stream);
+    if (bn <= 32) return launch<256, 32>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, epi, stream);
+    if (bn <= 64) return launch<256, 64>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, epi, stream);
     return -3;
   } else {
     switch (bn) {
-      case 32: return launch<BM, 32>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, stream);
-      case 64: return launch<BM, 64>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, stream);
-      case 96: return launch<BM, 96>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, stream);
-      case 128: return launch<BM, 128>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, stream);
-      case 160: return launch<BM, 160>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, stream);
-      default: return launch<BM, 192>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, stream);
+      case 32: return launch<BM, 32>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, epi, stream);
+      case 64: return launch<BM, 64>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, epi, stream);
+      case 96: return launch<BM, 96>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, epi, stream);
+      case 128: return launch<BM, 128>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, epi, stream);
+      case 160: return launch<BM, 160>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, epi, stream);
+      default: return launch<BM, 192>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, epi, stream);
     }
   }
 }
@@ -159,26 +162,31 @@ int launch_bm(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, i
 }  // namespace
 
 // flags bit0: compute column statistics into stats[2N] (zero on entry; kStatShards copies sstride
-// floats apart when sstride > 0, common.h); bits 8..15: tile variant (kNtVariants, mfma_common.h).
+// floats apart when sstride > 0, common.h); bit1: C = bf16(acc * stats[col] + stats[N + col]) (folded
+// inference BN), bit2: ReLU after it; bits 8..15: tile variant (kNtVariants, mfma_common.h).
 TONY_API int tony_gemm_bf16(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
                             int64_t ldb, int64_t ldc, int flags, float* stats, int64_t sstride, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || sstride < 0) return -1;
   if ((K % 8) || (lda % 8) || (ldb % 8)) return -1;
   if (M > 0x7fffffff || N > 0x7fffffff) return -1;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -1;
-  float* st = (flags & 1) ? stats : nullptr;
-  // st is accumulated into with atomics: the caller hands it over zeroed (ops/arena.py)
+  // bit0: st is accumulated into with atomics (the caller hands it over zeroed, ops/arena.py);
+  // bit1: st = [scale | shift] of the folded inference BN, bit2: ReLU after it (H5)
+  const int epi = flags & 7;
+  if ((epi & 1) && (epi & 2)) return -1;
+  if ((epi & 3) && stats == nullptr) return -1;
+  float* st = stats;
   const int v = (flags >> 8) & 0xff;
   if (v >= kNumNtVariants) return -1;
   if (v == 0) {
-    if (N <= 64) return launch<256, 64>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, stream);
-    return launch<128, 128>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, stream);
+    if (N <= 64) return launch<256, 64>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, epi, stream);
+    return launch<128, 128>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, epi, stream);
   }
   const int64_t bn = pick_bn(N, kNtVariants[v].cap);
   switch (kNtVariants[v].bm) {
-    case 64: return launch_bm<64>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, bn, stream);
-    case 128: return launch_bm<128>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, bn, stream);
-    default: return launch_bm<256>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, bn, stream);
+    case 64: return launch_bm<64>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, epi, bn, stream);
+    case 128: return launch_bm<128>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, epi, bn, stream);
+    default: return launch_bm<256>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, epi, bn, stream);
   }
 }
 

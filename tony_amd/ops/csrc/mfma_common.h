@@ -72,9 +72,12 @@ constexpr int kNumNtVariants = sizeof(kNtVariants) / sizeof(kNtVariants[0]);
 // NT epilogue: optional per-column BN statistics from the fp32 accumulators, then the bf16 tile
 // staged through LDS (rows padded by 16 B) and written with 16-byte coalesced stores.
 // acc layout of 16x16 MFMA: col = lane&15, row = (lane>>4)*4 + r.
+// With ``aff`` ([scale N | shift N] fp32, the folded inference BatchNorm) the stored value is
+// act(acc * scale[col] + shift[col]) (act = ReLU when ``relu``): conv + BN + ReLU in one pass (H5).
 template <int BM, int BN, int TM, int TN>
 __device__ __forceinline__ void nt_epilogue(f32x4 (&acc)[TM][TN], uint16_t* smem, uint16_t* __restrict__ C,
-                                            int64_t ldc, int M, int N, int m0, int n0, float* __restrict__ stats) {
+                                            int64_t ldc, int M, int N, int m0, int n0, float* __restrict__ stats,
+                                            const float* __restrict__ aff = nullptr, bool relu = false) {
   constexpr int WM = BM / 2, WN = BN / 2;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -105,16 +108,33 @@ __device__ __forceinline__ void nt_epilogue(f32x4 (&acc)[TM][TN], uint16_t* smem
   constexpr int LDC = BN + 8;
   static_assert(BM * LDC <= 2 * (BM + BN) * BK, "C staging tile must fit in the LDS buffers");
   uint16_t* Cs = smem;  // the K loop ended with a barrier: both buffers are free
+  if (aff != nullptr) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * WN + j * 16 + (lane & 15);
+      const int gcol = min(n0 + col, N - 1);
+      const float sc = aff[gcol], sh = aff[N + gcol];
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wm * WM + i * 16 + (lane >> 4) * 4 + r;
-        const int col = wn * WN + j * 16 + (lane & 15);
-        Cs[row * LDC + col] = f2bf(acc[i][j][r]);
-      }
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * WM + i * 16 + (lane >> 4) * 4 + r;
+          const float v = fmaf(acc[i][j][r], sc, sh);
+          Cs[row * LDC + col] = f2bf(relu ? fmaxf(v, 0.f) : v);
+        }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * WM + i * 16 + (lane >> 4) * 4 + r;
+          const int col = wn * WN + j * 16 + (lane & 15);
+          Cs[row * LDC + col] = f2bf(acc[i][j][r]);
+        }
+  }
   __syncthreads();
   constexpr int CHUNKS = BM * BN / 8;
   for (int v = threadIdx.x; v < CHUNKS; v += kThreads) {
