@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps (for rocprof)")
     ap.add_argument("--no-wgrad-stream", action="store_true",
                     help="serial backward (no weight gradients on a second stream)")
+    ap.add_argument("--no-branch-streams", action="store_true",
+                    help="Inception branches on one stream (branch streams are opt-in: TONY_BRANCH_STREAMS=1)")
     ap.add_argument("--no-miopen-find", action="store_true",
                     help="MIOpen immediate mode instead of find (faster startup, slower non-1x1 convs)")
     return ap.parse_args()
@@ -102,7 +104,8 @@ def main():
     from tony_amd.parallel.collectives import max_over_ranks
 
     mode = "eager" if args.no_graph else args.mode
-    trainer = Trainer(model, ps, loss_fn, use_graph=mode != "eager", overlap_wgrad=not args.no_wgrad_stream)
+    trainer = Trainer(model, ps, loss_fn, use_graph=mode != "eager", overlap_wgrad=not args.no_wgrad_stream,
+                      branch_streams=not args.no_branch_streams)
     t_w = time.perf_counter()
     setup = {}
     if mode == "auto":
@@ -191,7 +194,10 @@ def main():
                 "step_mode": mode,
                 "mode_setup_ms": setup or None,
                 "wgrad_stream": not args.no_wgrad_stream,
+                "branch_streams": _branch_streams_on(args),
                 "host_ms_per_step": round(1000.0 * host / args.steps, 3),
+                "host_fwd_bwd_ms_last_eager_step": [round(1000.0 * trainer.host_fwd_s, 3),
+                                                    round(1000.0 * trainer.host_bwd_s, 3)],
                 "kernels": "stock-comparator" if args.stock else "tony_amd HIP",
                 "conv_impl": _conv_impl_counts(),
                 "final_loss": round(final_loss, 4),
@@ -201,6 +207,12 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def _branch_streams_on(args) -> bool:
+    from tony_amd.ops import streams
+
+    return streams.BRANCHES_ENABLED and not args.no_branch_streams and not args.no_wgrad_stream
 
 
 def _conv_impl_counts():

@@ -24,14 +24,16 @@ class _Tiny(nn.Module):
 
 
 class _Block(nn.Module):
-    """An Inception-A block (fused head, 5x5 / double-3x3 branches, zero-copy concat) + classifier."""
+    """One Inception block (fused head, parallel branches, zero-copy concat) + classifier."""
 
-    def __init__(self):
+    def __init__(self, kind="A"):
         super().__init__()
-        from tony_amd.models.inception_v3 import InceptionA
+        from tony_amd.models import inception_v3 as iv3
 
-        self.block = InceptionA(64, 32)
-        self.fc = nn.Linear(256, 10)
+        self.block = {"A": lambda: iv3.InceptionA(64, 32), "B": lambda: iv3.InceptionB(64),
+                      "C": lambda: iv3.InceptionC(64, 32), "D": lambda: iv3.InceptionD(64),
+                      "E": lambda: iv3.InceptionE(64)}[kind]()
+        self.fc = nn.Linear(self.block.out_channels, 10)
 
     def forward(self, x):
         from tony_amd.ops.pool import global_avg_pool
@@ -62,10 +64,13 @@ def _train(mode, steps=4, overlap=True, net=_Tiny, shape=(32, 16, 24, 24)):
     return losses, ps.flat.data.float().clone(), ps.steps
 
 
-@pytest.mark.parametrize("mode", ["eager", "graph_in"])
-def test_wgrad_stream_overlap_matches_serial(cuda, mode):
-    """Weight gradients on the side stream (ops/streams.py) train exactly like the serial backward."""
-    kw = dict(net=_Block, shape=(8, 64, 35, 35), steps=5)
+@pytest.mark.parametrize("mode,kind", [("eager", "A"), ("graph_in", "A"), ("eager", "B"), ("eager", "C"),
+                                       ("eager", "D"), ("eager", "E")])
+def test_wgrad_stream_overlap_matches_serial(cuda, mode, kind):
+    """Weight gradients on the side stream and block branches on branch streams (ops/streams.py)
+    train exactly like the serial single-stream step."""
+    hw = {"A": 35, "B": 35, "C": 17, "D": 17, "E": 8}[kind]
+    kw = dict(net=lambda: _Block(kind), shape=(max(8, 2048 // (hw * hw)), 64, hw, hw), steps=5)
     ls, ps_, _ = _train(mode, overlap=False, **kw)
     lo, po, _ = _train(mode, overlap=True, **kw)
     for a, b in zip(lo, ls):
@@ -163,4 +168,6 @@ def test_zero_copy_concat_matches_copy_path(cuda, block, monkeypatch):
     y2, g2 = run(False)
     # the two paths may pick different autotuned kernels: allow one bf16 ulp of the output scale
     assert ((y1 - y2).abs() <= 5e-2 + 2 ** -7 * y2.abs()).all().item(), (y1 - y2).abs().max().item()
-    assert ((g1 - g2).norm() / g2.norm()).item() < 2e-2
+    # input gradients pass 2-5 bf16 conv+BN backward layers whose BN statistics are summed with
+    # float atomics (order-dependent): a few % relative difference is rounding, not a wrong slice
+    assert ((g1 - g2).norm() / g2.norm()).item() < 4e-2

@@ -22,6 +22,7 @@ from torch import nn
 
 from ..ops.concat import Slot, assemble, concat_buffer
 from ..ops.pool import avg_pool, avg_pool3x3_s1, global_avg_pool, max_pool
+from ..ops import streams
 from ..ops.fused import FusedHead
 from .layers import ConvBNAct, init_weights
 
@@ -80,7 +81,10 @@ class InceptionA(_Block):
             buf = concat_buffer(n, self.out_channels, h, w, x)
             s1, s5, s3, sp = _slots(buf, (64, 64, 96, self.out_channels - 224))
             y1, y5, y3, yp = self.head(x, slots=(s1, None, None, sp))
-            return assemble(buf, [y1, self.b5(y5, slot=s5), _seq(self.b3, y3, s3), yp])
+            # the double-3x3 chain on this stream, the 5x5 beside it (ops/streams.py)
+            o3, o5 = streams.parallel(lambda: _seq(self.b3, y3, s3), lambda: self.b5(y5, slot=s5))
+            streams.keep(y5, y3)
+            return assemble(buf, [y1, o5, o3, yp])
         p = self.avgpool(x)
         return torch.cat([self.b1(x), self.b5(x), self.b3(x), self.bp(p)], 1)
 
@@ -97,7 +101,10 @@ class InceptionB(_Block):  # 35x35 -> 17x17 reduction
             n, c, h, w = x.shape
             buf = concat_buffer(n, self.out_channels, (h - 3) // 2 + 1, (w - 3) // 2 + 1, x)
             s3, sd, sp = _slots(buf, (384, 96, c))
-            return assemble(buf, [self.b3(x, slot=s3), _seq(self.bd, x, sd), max_pool(x, 3, 2, slot=sp)])
+            od, o3, op = streams.parallel(lambda: _seq(self.bd, x, sd), lambda: self.b3(x, slot=s3),
+                                          lambda: max_pool(x, 3, 2, slot=sp))
+            streams.keep(x)
+            return assemble(buf, [o3, od, op])
         return torch.cat([self.b3(x), self.bd(x), self.maxpool(x)], 1)
 
 
@@ -125,7 +132,9 @@ class InceptionC(_Block):  # 17x17 with factorised 7x7
             buf = concat_buffer(n, 768, h, w, x)
             s1, s7, sd, sp = _slots(buf, (192, 192, 192, 192))
             y1, y7, yd, yp = self.head(x, slots=(s1, None, None, sp))
-            return assemble(buf, [y1, _seq(self.b7, y7, s7), _seq(self.bd, yd, sd), yp])
+            od, o7 = streams.parallel(lambda: _seq(self.bd, yd, sd), lambda: _seq(self.b7, y7, s7))
+            streams.keep(y7, yd)
+            return assemble(buf, [y1, o7, od, yp])
         p = self.avgpool(x)
         return torch.cat([self.b1(x), self.b7(x), self.bd(x), self.bp(p)], 1)
 
@@ -150,7 +159,10 @@ class InceptionD(_Block):  # 17x17 -> 8x8 reduction
             buf = concat_buffer(n, self.out_channels, (h - 3) // 2 + 1, (w - 3) // 2 + 1, x)
             s3, s7, sp = _slots(buf, (320, 192, c))
             t3, t7 = self.head(x)
-            return assemble(buf, [self.b3(t3, slot=s3), _seq(self.b7, t7, s7), max_pool(x, 3, 2, slot=sp)])
+            o7, o3, op = streams.parallel(lambda: _seq(self.b7, t7, s7), lambda: self.b3(t3, slot=s3),
+                                          lambda: max_pool(x, 3, 2, slot=sp))
+            streams.keep(x, t3, t7)
+            return assemble(buf, [o3, o7, op])
         return torch.cat([self.b3(x), self.b7(x), self.maxpool(x)], 1)
 
 
@@ -178,9 +190,14 @@ class InceptionE(_Block):  # 8x8 with split 1x3 / 3x1 branches
             buf = concat_buffer(n, 2048, h, w, x)
             s1, sa, sb, sda, sdb, sp = _slots(buf, (320, 384, 384, 384, 384, 192))
             y1, t, d, yp = self.head(x, slots=(s1, None, None, sp))
-            d = self.bd(d)
-            return assemble(buf, [y1, self.b3a(t, slot=sa), self.b3b(t, slot=sb), self.bda(d, slot=sda),
-                                  self.bdb(d, slot=sdb), yp])
+
+            def dbl():
+                dd = self.bd(d)
+                return self.bda(dd, slot=sda), self.bdb(dd, slot=sdb)
+
+            (oda, odb), oa, ob = streams.parallel(dbl, lambda: self.b3a(t, slot=sa), lambda: self.b3b(t, slot=sb))
+            streams.keep(t, d)
+            return assemble(buf, [y1, oa, ob, oda, odb, yp])
         else:
             y1 = self.b1(x)
             t = self.b3(x)

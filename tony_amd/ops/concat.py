@@ -66,6 +66,9 @@ class _AssembleFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dbuf):
+        from . import streams
+
+        streams.keep(dbuf)  # its slices feed branch-stream backward nodes
         grads, c0 = [], 0
         for c in ctx.widths:
             grads.append(dbuf[:, c0:c0 + c])

@@ -282,6 +282,7 @@ class _ConvFn(torch.autograd.Function):
         dy = _as_rows(dy)[0]
         dw = _wgrad(dy, x, weight, ctx.stride, ctx.padding)  # first: overlaps the dgrad on the side stream
         dx = _dgrad(dy, weight, x.shape, ctx.stride, ctx.padding) if ctx.needs_input_grad[0] else None
+        streams.keep(dx)  # may be consumed on another (branch) stream
         return dx, dw, None, None
 
 
@@ -348,6 +349,7 @@ class _ConvBNActFn(torch.autograd.Function):
         _lib.check(rc, "tony_bn_bwd")
         dw = _wgrad(dZ, x, weight, stride, padding)  # first: overlaps the dgrad on the side stream
         dx = _dgrad(dZ, weight, x.shape, stride, padding) if ctx.needs_input_grad[0] else None
+        streams.keep(dx)  # may be consumed on another (branch) stream
         if inplace:
             dgamma = dbeta = None
         return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None

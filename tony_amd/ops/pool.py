@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import torch
 
-from . import _lib, concat
+from . import _lib, concat, streams
 from .bn import _as_rows, _rows_view
 
 
@@ -59,6 +59,7 @@ class _MaxPoolFn(torch.autograd.Function):
         rc = _lib.lib().tony_maxpool_bwd(dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), n, h, w, c, k, s, lddy, c,
                                          _lib.stream_ptr(dy.device))
         _lib.check(rc, "tony_maxpool_bwd")
+        streams.keep(dx)  # may be consumed on another (branch) stream
         return dx, None, None, None
 
 

@@ -49,43 +49,122 @@ def _side(device: torch.device) -> torch.cuda.Stream:
     return s
 
 
-def begin(device) -> bool:
-    """Route in-place weight gradients to the side stream until ``end()``; False when disabled."""
+# ---- parallel model branches (Inception blocks) -------------------------------------------------
+# With branches on, ``parallel(*thunks)`` runs the first thunk on the current stream and each other
+# one on its own branch stream (forked from the current stream, joined back after), so the 2-3
+# independent conv chains of an Inception block execute concurrently; autograd then replays each
+# branch's backward on the stream its forward ran on.  Tensors that cross streams are kept
+# referenced until ``end()`` (``keep``), which joins every stream used into the current one.
+BRANCHES_ENABLED = os.environ.get("TONY_BRANCH_STREAMS", "0") == "1"  # measured: no gain (GPU already full), +1.5 ms host
+_branch_pool: Dict[int, List[torch.cuda.Stream]] = {}
+_branches_on = [False]
+_used: Dict[int, torch.cuda.Stream] = {}
+
+
+def _branch_streams(device: torch.device, n: int) -> List[torch.cuda.Stream]:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    pool = _branch_pool.setdefault(idx, [])
+    while len(pool) < n:
+        pool.append(torch.cuda.Stream(device=torch.device("cuda", idx)))
+    return pool[:n]
+
+
+def begin(device, branches: bool = False) -> bool:
+    """Route in-place weight gradients to the side stream (and, with ``branches``, model branches to
+    branch streams) until ``end()``; False when disabled."""
     device = torch.device(device)
     if not ENABLED or device.type != "cuda":
         return False
     _active[0] = _side(device)
     _issued[0] = 0
+    _branches_on[0] = branches and BRANCHES_ENABLED
     return True
+
+
+def branches_active() -> bool:
+    return _branches_on[0]
+
+
+def keep(*tensors) -> None:
+    """Hold tensors (read or written on another stream than the one that allocated them) until end()."""
+    if _branches_on[0] or _active[0] is not None:
+        with _lock:
+            _keep.extend(t for t in tensors if isinstance(t, torch.Tensor))
+
+
+def parallel(*thunks):
+    """Results of the independent ``thunks``; concurrently on branch streams when branches are on."""
+    if not _branches_on[0] or len(thunks) < 2:
+        return [f() for f in thunks]
+    main = torch.cuda.current_stream()
+    side = _branch_streams(main.device, len(thunks) - 1)
+    outs = [None] * len(thunks)
+    for i, (f, s) in enumerate(zip(thunks[1:], side), 1):
+        s.wait_stream(main)
+        with torch.cuda.stream(s):
+            outs[i] = f()
+        _used[id(s)] = s
+    outs[0] = thunks[0]()
+    for s in side:
+        main.wait_stream(s)
+    keep(*[o for o in outs if isinstance(o, torch.Tensor)])
+    return outs
 
 
 def active() -> bool:
     return _active[0] is not None
 
 
+# Work is handed to the side stream in batches of BATCH ops: one fork (event record + stream wait,
+# ~10 us of host time) and one stream switch per batch instead of per op.  A batch forks from the
+# current stream's position at flush time -- later than each op needs, never earlier.
+BATCH = int(os.environ.get("TONY_WGRAD_BATCH", "1"))  # measured: 1 (16.34 ms) beats 4 (16.77 ms)
+_pending: List[Callable[[], object]] = []
+
+
+def _flush(side: torch.cuda.Stream) -> None:
+    with _lock:
+        work = list(_pending)
+        _pending.clear()
+    if not work:
+        return
+    side.wait_stream(torch.cuda.current_stream(side.device))
+    with torch.cuda.stream(side):
+        for fn in work:
+            out = fn()
+            assert out is None, "only in-place gradient work may run on the side stream"
+
+
 def run(fn: Callable[[], object], *keep: torch.Tensor):
     """Run ``fn`` (which must write its result in place and return None) on the side stream when one
-    is active, else right here.  ``keep``: tensors ``fn`` reads that the caller may drop."""
+    is active -- possibly deferred to the next batch flush or ``end()`` -- else right here.  ``keep``:
+    tensors ``fn`` reads that the caller may drop."""
     side = _active[0]
     if side is None:
         return fn()
-    side.wait_stream(torch.cuda.current_stream(side.device))
-    with torch.cuda.stream(side):
-        out = fn()
-    assert out is None, "only in-place gradient work may run on the side stream"
     with _lock:
+        _pending.append(fn)
         _keep.extend(keep)
         _issued[0] += 1
+        full = len(_pending) >= BATCH
+    if full:
+        _flush(side)
     return None
 
 
 def end() -> int:
-    """Join the side stream into the current stream and release the kept operands; returns how many
-    ops ran on the side stream this step."""
+    """Issue the deferred work, join the side stream into the current stream and release the kept
+    operands; returns how many ops ran on the side stream this step."""
     side = _active[0]
     _active[0] = None
+    _branches_on[0] = False
     if side is not None:
-        torch.cuda.current_stream(side.device).wait_stream(side)
+        _flush(side)
+        cur = torch.cuda.current_stream(side.device)
+        cur.wait_stream(side)
+        for s in _used.values():  # backward kernels of branch nodes ran on these
+            cur.wait_stream(s)
+        _used.clear()
     with _lock:
         _keep.clear()
         n, _issued[0] = _issued[0], 0

@@ -10,6 +10,7 @@ replay always uses the current learning rate.
 """
 from __future__ import annotations
 
+import time
 from typing import Callable
 
 import torch
@@ -22,7 +23,8 @@ from .ps import ParameterServer
 
 class Trainer:
     def __init__(self, model: torch.nn.Module, ps: ParameterServer, loss_fn: Callable, use_graph: bool = False,
-                 warmup_eager: int = 3, graph_collectives: bool | None = None, overlap_wgrad: bool = True):
+                 warmup_eager: int = 3, graph_collectives: bool | None = None, overlap_wgrad: bool = True,
+                 branch_streams: bool = True):
         self.model = model
         self.ps = ps
         self.loss_fn = loss_fn
@@ -34,8 +36,10 @@ class Trainer:
         # (RCCL's graph-capture support differs across releases).  One rank: all in the graph.
         self.graph_collectives = (ps.world == 1) if graph_collectives is None else graph_collectives
         self.overlap_wgrad = overlap_wgrad
+        self.branch_streams = branch_streams
         self._tuned = False
         self.side_ops = 0
+        self.host_fwd_s = self.host_bwd_s = 0.0
         self.graph = None
         self.static_x = None
         self.static_y = None
@@ -51,19 +55,26 @@ class Trainer:
             self.wt.enabled = True
 
     def _body(self, x, y, ps_step: bool = True):
+        t0 = time.perf_counter()
         self.ps.zero_grad()
-        with trace_range("forward"):
-            out = self.model(x)
-            loss = self.loss_fn(out, y)
-        # weight gradients on a second stream, overlapped with the data-gradient chain (ops/streams.py);
-        # not in the first step, whose autotuning times kernels on the current stream
-        overlap = self.overlap_wgrad and self._tuned and streams.begin(self.ps.flat.device)
-        with trace_range("backward"):
-            try:
+        # weight gradients on a second stream, overlapped with the data-gradient chain, and the model's
+        # independent branches on branch streams (ops/streams.py); not in the first step, whose
+        # autotuning times kernels on the current stream
+        overlap = self.overlap_wgrad and self._tuned and streams.begin(self.ps.flat.device,
+                                                                        branches=self.branch_streams)
+        t1 = t0
+        try:
+            with trace_range("forward"):
+                out = self.model(x)
+                loss = self.loss_fn(out, y)
+            t1 = time.perf_counter()
+            with trace_range("backward"):
                 loss.backward()
-            finally:
-                if overlap:
-                    self.side_ops = streams.end()  # joined before the PS reads the gradients
+        finally:
+            if overlap:
+                self.side_ops = streams.end()  # every stream joined before the PS reads the gradients
+        # host seconds spent issuing the forward / the backward (eager steps; the GPU runs behind)
+        self.host_fwd_s, self.host_bwd_s = t1 - t0, time.perf_counter() - t1
         self._tuned = True
         if ps_step:
             self._ps_step()
