@@ -142,3 +142,19 @@ def test_monitor_reports_new_uncorrectable_ecc(monkeypatch):
     for _ in range(3):
         m.refresh()
     assert m.metrics()[C.GPU_ECC_UNCORRECTABLE] == 2.0
+
+
+def test_node_example_tony_sh_writes_loadable_conf(tmp_path):
+    """examples/mi355x-node/tony.sh (counterpart of tony-in-gcp/scripts/tony.sh) -> tony.xml that the
+    configuration loader layers over tony-default.xml."""
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "tony.xml"
+    env = dict(os.environ, TONY_WORKERS="4", TONY_WORKER_GPUS="1", TONY_PS="1", TONY_FRAMEWORK="pytorch")
+    subprocess.run(["bash", os.path.join(root, "examples", "mi355x-node", "tony.sh"), str(out)], check=True, env=env,
+                   capture_output=True)
+    c = Configuration().add_resource(str(out))
+    assert c.get("tony.worker.instances") == "4" and c.get("tony.worker.gpus") == "1"
+    assert c.get("tony.ps.instances") == "1" and c.get(K.FRAMEWORK_NAME if hasattr(K, "FRAMEWORK_NAME")
+                                                       else "tony.application.framework") == "pytorch"
