@@ -14,6 +14,9 @@
 // from one input pixel (or zero for padding).  The tap/channel position of a thread's chunk is
 // advanced incrementally per K-step (no divisions in the loop); the per-row pixel coordinates are
 // decoded once per tile (forward/dgrad) or advanced incrementally with the row (wgrad).
+#include <cstdlib>
+#include <type_traits>
+
 #include "mfma_common.h"
 
 using namespace tony;
@@ -414,6 +417,131 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __
   }
 }
 
+// ---- wgrad with LDS-DMA staging (Cout tiles of 128): the same tile and split-K plan as
+// conv_wgrad_kernel<128>, but each operand stage is written straight into LDS by
+// global_load_lds_dwordx4 (no VGPR staging) into a ring of 3 stages, so two stages are always in
+// flight behind the MFMAs instead of one.  The LDS image is lane-linear (a wave instruction fills
+// 4 rows of 256 B); the tr_off swizzle is applied on the SOURCE side: lane l of a row fetches
+// logical chunk (l & 15) ^ tr_swz(row), which is where tr_frag looks for it.  Out-of-range rows /
+// columns / taps fetch 16 zero bytes.  The DMAs are issued from inline asm, so hipcc neither
+// counts them nor makes the ds_reads of the current slot wait for the DMAs into the other slots
+// (it cannot tell LDS-DMA targets apart and would emit vmcnt(0) there); completion is one counted
+// `s_waitcnt vmcnt(4)` + a raw s_barrier per stage (a __syncthreads() would drain the ring).
+constexpr int kWgStages = 3;
+
+__global__ __launch_bounds__(kThreads) void conv_wgrad_glds_kernel(const uint16_t* __restrict__ dY, int64_t lddy,
+                                                                   Gather g, int64_t M, int Co, int tiles_n2,
+                                                                   int ntiles, int64_t rows_per_split,
+                                                                   float* __restrict__ slab) {
+  constexpr int TBM = 128;
+  constexpr int TM = TBM / 32;
+  constexpr int TILE = WK * 128;           // elements per staged operand (32 rows x 256 B)
+  constexpr int STAGE = 2 * TILE;          // A then B
+  __shared__ __attribute__((aligned(16))) uint16_t smem[kWgStages * STAGE];
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = wg % ntiles, split = wg / ntiles;
+  const int t1 = tile / tiles_n2, t2 = tile % tiles_n2;
+  const int n1_0 = t1 * TBM, n2_0 = t2 * WTBN;
+  const int64_t m_begin = static_cast<int64_t>(split) * rows_per_split;
+  const int64_t m_end = min(M, m_begin + rows_per_split);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int K = g.K;
+
+  // this thread fetches rows r0 and r0 + 16 of every stage, logical chunk ch of each
+  const int r0 = threadIdx.x >> 4;
+  const int ch = (threadIdx.x & 15) ^ tr_swz(r0);  // tr_swz(r0 + 16) == tr_swz(r0)
+  const int acol = n1_0 + ch * 8;
+  const bool acol_ok = acol < Co;
+  const int kcol = n2_0 + ch * 8;
+  const bool kok = kcol < K;
+  TapPos tp;
+  tp.init(kok ? kcol : 0, g);
+  MRow mr[2];
+  mr[0].init(m_begin + r0, g);
+  mr[1].init(m_begin + r0 + 16, g);
+  int64_t am = m_begin + r0;  // A row of the next stage to issue (second row: + 16)
+  // wave-uniform LDS byte addresses: instruction i of this wave fills rows 4 * (wave + 4 i) .. + 3
+  const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(smem) + (4 * wave) * 256);
+  constexpr uint32_t kRow16 = 16 * 256, kStageB = STAGE * 2, kTileB = TILE * 2;
+
+  auto issue = [&](int slot) {
+    const uint32_t As = base + slot * kStageB, Bs = As + kTileB;
+    const void* z = &kZeroChunk;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t m = am + 16 * i;
+      const bool ok = acol_ok & (m < m_end);
+      glds16(ok ? static_cast<const void*>(dY + m * lddy + acol) : z, As + i * kRow16);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const MRow& q = mr[i];
+      const int iy = q.oy * g.sh + g.offh + tp.r, ix = q.ox * g.sw + g.offw + tp.s;
+      const bool ok = kok & (q.m < m_end) & (static_cast<unsigned>(iy) < static_cast<unsigned>(g.Hs)) &
+                      (static_cast<unsigned>(ix) < static_cast<unsigned>(g.Ws));
+      const uint16_t* src = g.src + (static_cast<int64_t>(q.n) * g.Hs * g.Ws + iy * g.Ws + ix) * g.ld + tp.c;
+      glds16(ok ? static_cast<const void*>(src) : z, Bs + i * kRow16);
+    }
+    am += WK;
+    mr[0].advance(WK, g);
+    mr[1].advance(WK, g);
+  };
+
+  f32x4 acc[TM][4];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = static_cast<int>((m_end - m_begin + WK - 1) / WK);
+  issue(0);
+  issue(1);
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt has landed in this wave (4 DMAs per stage; stage kt+1's 4 may still fly) and, after
+    // the barrier, in every wave; every wave is also done reading stage kt-1, whose slot is refilled
+    // with stage kt+2 (past the end: zero / unread fills, which keeps the count uniform)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue((kt + 2) % kWgStages);
+    const uint16_t* As = smem + (kt % kWgStages) * STAGE;
+    const uint16_t* Bs = As + TILE;
+    const int kgrp = lane >> 4;
+    bf16x8_t af[TM], bfr[4];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = tr_frag(As, kgrp, wm * (TBM / 2) + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = tr_frag(Bs, kgrp, wn * 64 + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup retires
+  float* dst = slab + static_cast<int64_t>(split) * Co * K;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n2_0 + wn * 64 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = n1_0 + wm * (TBM / 2) + i * 16 + (lane >> 4) * 4 + r;
+        if (row < Co && col < K) dst[static_cast<int64_t>(row) * K + col] = acc[i][j][r];
+      }
+    }
+  }
+}
+
+bool wgrad_glds_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("TONY_WGRAD_GLDS");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
 template <int TBM>
 int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, float* slab, int64_t slab_cap,
                  int* splits_out, int64_t M, int Co, int num_cus, hipStream_t stream) {
@@ -432,8 +560,12 @@ int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, float
   if (grid > 0x7fffffff) return -2;
   if (slab != nullptr && splits * Co * static_cast<int64_t>(g.K) > slab_cap) return -4;  // caller's bound is off
   if (splits_out != nullptr) *splits_out = static_cast<int>(splits);
-  conv_wgrad_kernel<TBM><<<static_cast<int>(grid), kThreads, 0, stream>>>(
-      static_cast<const uint16_t*>(dy), lddy, g, dw, M, Co, tiles_n2, ntiles, rows, slab);
+  if (TBM == 128 && slab != nullptr && wgrad_glds_enabled())
+    conv_wgrad_glds_kernel<<<static_cast<int>(grid), kThreads, 0, stream>>>(
+        static_cast<const uint16_t*>(dy), lddy, g, M, Co, tiles_n2, ntiles, rows, slab);
+  else
+    conv_wgrad_kernel<TBM><<<static_cast<int>(grid), kThreads, 0, stream>>>(
+        static_cast<const uint16_t*>(dy), lddy, g, dw, M, Co, tiles_n2, ntiles, rows, slab);
   TONY_LAUNCH_CHECK();
   return 0;
 }

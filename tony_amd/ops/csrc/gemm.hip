@@ -17,6 +17,8 @@
 //    of `lds_off`.
 //  * Workgroup ids are remapped so that consecutive output tiles (which share
 //    an A row-panel) are dispatched onto the same XCD and hit its private L2.
+#include <cstdlib>
+
 #include "mfma_common.h"
 
 using namespace tony;
@@ -236,6 +238,99 @@ __device__ __forceinline__ void tn_store(uint16_t* lds, const uint4* regs) {
   }
 }
 
+// The same split-K TN GEMM with both operand stages written straight into a 3-slot LDS ring by
+// LDS-DMA (mfma_common.h glds16): two stages in flight behind the MFMAs instead of one, no VGPR
+// staging.  Lane-linear LDS image; the tr_off swizzle moves to the source side (lane l of a row
+// fetches logical chunk (l & 15) ^ tr_swz(row)).  Slab mode only.
+constexpr int kTnStages = 3;
+
+__global__ __launch_bounds__(kThreads) void gemm_tn_glds_kernel(
+    const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb, int64_t M, int N1,
+    int N2, int tiles_n2, int ntiles, int64_t rows_per_split, float* __restrict__ slab) {
+  constexpr int TILE = TBK * 128, STAGE = 2 * TILE;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[kTnStages * STAGE];
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = wg % ntiles, split = wg / ntiles;
+  const int t1 = tile / tiles_n2, t2 = tile % tiles_n2;
+  const int n1_0 = t1 * TBM, n2_0 = t2 * TBN;
+  const int64_t m_begin = static_cast<int64_t>(split) * rows_per_split;
+  const int64_t m_end = min(M, m_begin + rows_per_split);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int r0 = threadIdx.x >> 4;
+  const int ch = (threadIdx.x & 15) ^ tr_swz(r0);  // tr_swz(r0 + 16) == tr_swz(r0)
+  const bool aok = n1_0 + ch * 8 < N1, bok = n2_0 + ch * 8 < N2;
+  const uint16_t* ap = A + n1_0 + ch * 8;
+  const uint16_t* bp = B + n2_0 + ch * 8;
+  int64_t am = m_begin + r0;
+  const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(smem) + (4 * wave) * 256);
+  constexpr uint32_t kRow16 = 16 * 256, kStageB = STAGE * 2, kTileB = TILE * 2;
+  auto issue = [&](int slot) {
+    const uint32_t As = base + slot * kStageB, Bs = As + kTileB;
+    const void* z = &kZeroChunk;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t m = am + 16 * i;
+      const bool mok = m < m_end;
+      glds16(aok & mok ? static_cast<const void*>(ap + m * lda) : z, As + i * kRow16);
+      glds16(bok & mok ? static_cast<const void*>(bp + m * ldb) : z, Bs + i * kRow16);
+    }
+    am += TBK;
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = static_cast<int>((m_end - m_begin + TBK - 1) / TBK);
+  issue(0);
+  issue(1);
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt landed here (4 DMAs per stage, stage kt+1's may still fly) and, after the barrier,
+    // everywhere; stage kt-1's slot is free for stage kt+2 (zero fills past the end)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue((kt + 2) % kTnStages);
+    const uint16_t* As = smem + (kt % kTnStages) * STAGE;
+    const uint16_t* Bs = As + TILE;
+    const int kgrp = lane >> 4;
+    bf16x8_t af[4], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = tr_frag(As, kgrp, wm * 64 + i * 16, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = tr_frag(Bs, kgrp, wn * 64 + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float* dst = slab + static_cast<int64_t>(split) * N1 * N2;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n2_0 + wn * 64 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = n1_0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        if (row < N1 && col < N2) dst[static_cast<int64_t>(row) * N2 + col] = acc[i][j][r];
+      }
+    }
+  }
+}
+
+bool tn_glds_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("TONY_WGRAD_GLDS");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
 __global__ __launch_bounds__(kThreads) void gemm_tn_splitk_kernel(
     const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
     float* __restrict__ C, int64_t ldc, int64_t M, int N1, int N2, int tiles_n2, int ntiles,
@@ -341,9 +436,14 @@ TONY_API int tony_gemm_tn_bf16(const void* A, const void* B, float* C, int64_t M
   if (grid > 0x7fffffff) return -2;
   if (slab != nullptr && splits * N1 * N2 > slab_cap) return -4;  // caller's bound is off
   if (splits_out != nullptr) *splits_out = static_cast<int>(splits);
-  gemm_tn_splitk_kernel<<<static_cast<int>(grid), kThreads, 0, stream>>>(
-      static_cast<const uint16_t*>(A), lda, static_cast<const uint16_t*>(B), ldb, C, ldc, M, static_cast<int>(N1),
-      static_cast<int>(N2), tiles_n2, ntiles, rows, slab);
+  if (slab != nullptr && tn_glds_enabled())
+    gemm_tn_glds_kernel<<<static_cast<int>(grid), kThreads, 0, stream>>>(
+        static_cast<const uint16_t*>(A), lda, static_cast<const uint16_t*>(B), ldb, M, static_cast<int>(N1),
+        static_cast<int>(N2), tiles_n2, ntiles, rows, slab);
+  else
+    gemm_tn_splitk_kernel<<<static_cast<int>(grid), kThreads, 0, stream>>>(
+        static_cast<const uint16_t*>(A), lda, static_cast<const uint16_t*>(B), ldb, C, ldc, M, static_cast<int>(N1),
+        static_cast<int>(N2), tiles_n2, ntiles, rows, slab);
   TONY_LAUNCH_CHECK();
   return 0;
 }

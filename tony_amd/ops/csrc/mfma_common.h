@@ -52,6 +52,30 @@ __device__ __forceinline__ bf16x8_t tr_frag(const uint16_t* lds, int kgrp, int c
   return __builtin_bit_cast(bf16x8_t, r);
 }
 
+// ---- LDS-DMA staging (global_load_lds_dwordx4): a wave instruction writes 64 x 16 B lane-linearly
+// from the wave-uniform LDS byte address in M0.  Issued from inline asm so that hipcc neither counts
+// it nor makes every ds_read wait vmcnt(0) for it (it cannot tell LDS-DMA targets apart); the
+// kernel waits with its own counted s_waitcnt vmcnt(N) + s_barrier.  Out-of-range lanes fetch the
+// 16 zero bytes of kZeroChunk.
+__device__ const uint4 kZeroChunk = {0u, 0u, 0u, 0u};
+
+__device__ __forceinline__ void glds16(const void* src, uint32_t lds_wave_base) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_wave_base)
+      : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)p));
+}
+
 // Column tile for a cap: the output channels split evenly over ceil(N/cap) tiles, rounded up to
 // the 32-column granule of the 2x2 wave layout (16-wide MFMA per wave), so no MFMA work is spent on
 // padding columns for Cout = 32..384 (Inception's 48/80/96/160/192/320/384).
