@@ -213,6 +213,11 @@ def _fwd(x, weight, stride, padding, stats):
 
 def _dgrad(dy, weight, x_shape, stride, padding):
     key = ("dgrad", tuple(dy.shape), tuple(weight.shape), stride, padding)
+    impl = _CHOICE.get(key)  # steady state: no candidate closures to build
+    if impl == "tony":
+        return conv_dgrad(dy, weight, x_shape, stride, padding)
+    if impl == "miopen":
+        return _miopen_dgrad(dy, weight, x_shape, stride, padding)
     cands = {"miopen": lambda: _miopen_dgrad(dy, weight, x_shape, stride, padding)}
     if _pair(stride) == (1, 1):
         cands["tony"] = lambda: conv_dgrad(dy, weight, x_shape, stride, padding)

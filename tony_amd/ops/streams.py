@@ -122,17 +122,42 @@ BATCH = int(os.environ.get("TONY_WGRAD_BATCH", "1"))  # measured: 1 (16.34 ms) b
 _pending: List[Callable[[], object]] = []
 
 
+# A fork costs host time on every weight gradient (~66 per Inception step), so it avoids the
+# convenience wrappers: Stream.wait_stream() creates a new HIP event per call and the stream()
+# context manager re-resolves the device; here a ring of pre-created events is re-recorded (a
+# recorded event may be recorded again once the wait on it is enqueued) and the current stream is
+# switched with the raw setter.
+_EVENTS: Dict[int, List] = {}
+_ev_next = [0]
+_EV_RING = 256
+
+
+def _fork_event(device_index: int):
+    ring = _EVENTS.get(device_index)
+    if ring is None:
+        ring = _EVENTS[device_index] = [torch.cuda.Event() for _ in range(_EV_RING)]
+    ev = ring[_ev_next[0] % _EV_RING]
+    _ev_next[0] += 1
+    return ev
+
+
 def _flush(side: torch.cuda.Stream) -> None:
     with _lock:
         work = list(_pending)
         _pending.clear()
     if not work:
         return
-    side.wait_stream(torch.cuda.current_stream(side.device))
-    with torch.cuda.stream(side):
+    cur = torch.cuda.current_stream(side.device)
+    ev = _fork_event(side.device_index)
+    ev.record(cur)
+    side.wait_event(ev)
+    torch.cuda.set_stream(side)
+    try:
         for fn in work:
             out = fn()
             assert out is None, "only in-place gradient work may run on the side stream"
+    finally:
+        torch.cuda.set_stream(cur)
 
 
 def run(fn: Callable[[], object], *keep: torch.Tensor):
