@@ -195,3 +195,30 @@ def test_inception_eval_folded_matches_unfolded(cuda):
     y_ref = m(x).float().detach()
     err = ((y_fold - y_ref).norm() / y_ref.norm()).item()
     assert err < 3e-2, err
+
+
+@pytest.mark.parametrize("shape", [(2, 32, 37, 35, 32, 0), (2, 32, 19, 21, 64, 1), (2, 64, 17, 33, 64, 1),
+                                   (1, 64, 9, 9, 32, 0), (3, 32, 24, 16, 64, 1)])
+def test_halo_tile_conv3x3(cuda, shape):
+    """The halo-tile 3x3 kernel (tile variant 9, csrc/conv.hip conv_halo_kernel) for fwd (+BN statistics)
+    and dgrad vs fp32 references, including partial edge blocks and both paddings."""
+    from tony_amd.ops import _lib
+    from tony_amd.ops.conv import conv_dgrad, conv_fwd
+
+    n, ci, h, w, co, p = shape
+    torch.manual_seed(5)
+    x = _nhwc(torch.randn(n, ci, h, w, device=cuda)).to(torch.bfloat16)
+    wt = _nhwc(torch.randn(co, ci, 3, 3, device=cuda) / (ci * 9) ** 0.5).to(torch.bfloat16)
+    xr, wr = x.float().requires_grad_(True), wt.float()
+    yr = torch.nn.functional.conv2d(xr, wr, None, 1, p)
+    stats = torch.zeros(_lib.stat_floats(co), device=cuda)
+    y = conv_fwd(x, wt, 1, p, stats, vflags=9 << 8)
+    assert _rel(y, yr) < 1e-2, f"halo fwd rel {_rel(y, yr):.4f}"
+    st = _lib.fold_stats(stats, co)
+    torch.testing.assert_close(st[:co], yr.sum((0, 2, 3)), rtol=2e-2, atol=2e-2 * (yr.numel() / co) ** 0.5)
+    torch.testing.assert_close(st[co:], (yr * yr).sum((0, 2, 3)), rtol=2e-2, atol=1.0)
+    dy = _nhwc(torch.randn_like(yr)).to(torch.bfloat16)
+    yr.backward(dy.float())
+    if co in (32, 64):  # dgrad runs the kernel with Cin' = co
+        dx = conv_dgrad(dy, wt, x.shape, 1, p, vflags=9 << 8)
+        assert _rel(dx, xr.grad) < 1e-2, f"halo dgrad rel {_rel(dx, xr.grad):.4f}"

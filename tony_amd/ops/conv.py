@@ -101,7 +101,8 @@ def conv_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: 
     return y
 
 
-def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, padding=0) -> torch.Tensor:
+def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, padding=0,
+               vflags: int | None = None) -> torch.Tensor:
     if _pair(stride) != (1, 1):
         return _miopen_dgrad(dy, weight, x_shape, stride, padding)
     n, c, h, w = x_shape
@@ -116,7 +117,8 @@ def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, paddin
         return L.tony_conv_dgrad(dy.data_ptr(), n, dy.shape[2], dy.shape[3], co, lddy, wt.data_ptr(), c, r, s, ph, pw,
                                  dx.data_ptr(), h, w, c, vf, st)
 
-    vf = tune.pick(("conv_dgrad", tuple(dy.shape), lddy, tuple(weight.shape), (ph, pw)), launch)
+    vf = vflags if vflags is not None else tune.pick(("conv_dgrad", tuple(dy.shape), lddy, tuple(weight.shape),
+                                                         (ph, pw)), launch)
     _lib.check(launch(vf), "tony_conv_dgrad")
     return dx
 

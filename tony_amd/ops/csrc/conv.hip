@@ -34,6 +34,7 @@ struct Gather {
   int offh, offw;       // source coord = o*stride + off + sign*tap
   int sign;             // +1 convolution, -1 transposed (dgrad)
   int K;                // R * S * Cs
+  int halo_images;      // batch count N (the halo-tile path walks images x tile rows x tile columns)
 };
 
 struct RowState {
@@ -218,6 +219,190 @@ int launch_nt_bm(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M
   }
 }
 
+// ---- 3x3 stride-1 convs with few channels (Cin 32 / 64): halo tiles instead of im2col -----------
+// The im2col loader of conv_nt_kernel fetches every input pixel 9 times (once per tap) through
+// L2; for Cin = 32/64 (Inception's 147x147 stem layers, ResNet's 56x56 layers, and their dgrads)
+// that gather, not the MFMAs, bounds the kernel.  Here a workgroup computes a 2-D block of
+// HT x WT = 8 x 16 output pixels (128 GEMM rows) x BN output channels: it loads the (HT+2) x (WT+2)
+// input patch once into LDS (zeros outside the image), the BN x 9*Cin weight panel once, and reads
+// the MFMA A fragments straight out of the patch at the 9 tap offsets.  LDS pixel rows and weight
+// rows are padded by 16 B so the 16 lanes of a fragment read hit 16 distinct 4-bank groups.
+// Same GEMM view as conv_nt_kernel (m = (n, oy, ox), k = (r, s, c)); the dgrad is the same kernel
+// on dY with flipped taps (g.sign = -1) and the transposed weights.
+constexpr int kHaloH = 8, kHaloW = 16;  // 16 x 16 measured no faster (one-shot load phase dominates)
+constexpr int kHaloVariant = 9;  // tile-variant id the autotuner uses for this path (ops/tune.py)
+
+template <int CS, int BN>
+__global__ __launch_bounds__(kThreads) void conv_halo_kernel(Gather g, const uint16_t* __restrict__ B,
+                                                            uint16_t* __restrict__ C, int64_t ldc, int N,
+                                                            float* __restrict__ stats, int64_t sstride, int epi,
+                                                            int tiles_x, int tiles_y) {
+  constexpr int R = 3, S = 3;
+  constexpr int HH = kHaloH + R - 1, HW = kHaloW + S - 1;
+  constexpr int PSTR = CS + 8;                 // LDS elements per halo pixel (16-B pad)
+  constexpr int KK = R * S * CS;               // GEMM K
+  constexpr int KP = KK + 8;                   // LDS elements per weight row (16-B pad)
+  constexpr int HALO = HH * HW * PSTR;
+  constexpr int WTS = BN * KP;
+  constexpr int BM = kHaloH * kHaloW;          // 128 rows
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  constexpr int LDC = BN + 8;
+  static_assert(BM * LDC <= HALO + WTS, "the C staging tile reuses the patch + weight panel");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[HALO + WTS];
+  uint16_t* halo = smem;
+  uint16_t* wts = smem + HALO;
+
+  // block -> (n, tile y, tile x, column tile); consecutive blocks share an image row band
+  int b = blockIdx.x;
+  const int ntn = N / BN;
+  const int tn = b % ntn;
+  b /= ntn;
+  const int tx = b % tiles_x;
+  b /= tiles_x;
+  const int ty = b % tiles_y;
+  const int n = b / tiles_y;
+  const int oy0 = ty * kHaloH, ox0 = tx * kHaloW, n0 = tn * BN;
+  const int hy0 = oy0 + g.offh - (g.sign < 0 ? R - 1 : 0);
+  const int hx0 = ox0 + g.offw - (g.sign < 0 ? S - 1 : 0);
+  const int64_t pix0 = static_cast<int64_t>(n) * g.Hs * g.Ws;
+
+  // stage the input patch and the weight panel (all loads in flight together, one barrier)
+  constexpr int HCH = HH * HW * (CS / 8);
+  for (int v = threadIdx.x; v < HCH; v += kThreads) {
+    const int c8 = v % (CS / 8), px = v / (CS / 8);
+    const int hy = px / HW, hx = px - hy * HW;
+    const int iy = hy0 + hy, ix = hx0 + hx;
+    uint4 val = make_uint4(0, 0, 0, 0);
+    if (static_cast<unsigned>(iy) < static_cast<unsigned>(g.Hs) && static_cast<unsigned>(ix) < static_cast<unsigned>(g.Ws))
+      val = *reinterpret_cast<const uint4*>(g.src + (pix0 + iy * g.Ws + ix) * g.ld + c8 * 8);
+    *reinterpret_cast<uint4*>(halo + px * PSTR + c8 * 8) = val;
+  }
+  constexpr int WCH = BN * (KK / 8);
+  for (int v = threadIdx.x; v < WCH; v += kThreads) {
+    const int k8 = v % (KK / 8), row = v / (KK / 8);
+    *reinterpret_cast<uint4*>(wts + row * KP + k8 * 8) =
+        *reinterpret_cast<const uint4*>(B + static_cast<int64_t>(n0 + row) * KK + k8 * 8);
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int kq = lane >> 4;  // which 8-element quarter of a 32-deep K slice this lane holds
+  int abase[TM];             // halo pixel of this lane's A row, tap (0, 0)
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int rl = wm * WM + i * 16 + (lane & 15);
+    abase[i] = ((rl / kHaloW) * HW + (rl % kHaloW)) * PSTR + kq * 8;
+  }
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+#pragma unroll
+    for (int s2 = 0; s2 < S; ++s2) {
+      const int rr = g.sign > 0 ? r : R - 1 - r, ss = g.sign > 0 ? s2 : S - 1 - s2;
+      const int aoff = (rr * HW + ss) * PSTR;
+#pragma unroll
+      for (int cb = 0; cb < CS / 32; ++cb) {
+        const int k0 = (r * S + s2) * CS + cb * 32 + kq * 8;
+        bf16x8_t af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(halo + abase[i] + aoff + cb * 32);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bfr[j] = *reinterpret_cast<const bf16x8_t*>(wts + (wn * WN + j * 16 + (lane & 15)) * KP + k0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+
+  // epilogue: rows outside the output image (partial edge blocks) hold real sums of halo data, so
+  // they are masked out of the statistics and the stores
+  bool rv[TM][4];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rl = wm * WM + i * 16 + (lane >> 4) * 4 + q;
+      rv[i][q] = (oy0 + rl / kHaloW < g.OH) & (ox0 + rl % kHaloW < g.OW);
+    }
+  if ((epi & 1) && stats != nullptr) {
+    float* st = stats + shard_off(blockIdx.x, sstride);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * WN + j * 16 + (lane & 15);
+      float sm = 0.f, sq = 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float v = rv[i][q] ? acc[i][j][q] : 0.f;
+          sm += v;
+          sq = fmaf(v, v, sq);
+        }
+      sm += __shfl_xor(sm, 16, 64);
+      sm += __shfl_xor(sm, 32, 64);
+      sq += __shfl_xor(sq, 16, 64);
+      sq += __shfl_xor(sq, 32, 64);
+      if (lane < 16) {
+        atomicAdd(st + col, sm);
+        atomicAdd(st + N + col, sq);
+      }
+    }
+  }
+  __syncthreads();  // everyone is done with patch and weights: they become the C staging tile
+  uint16_t* Cs = smem;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = wm * WM + i * 16 + (lane >> 4) * 4 + q;
+        const int col = wn * WN + j * 16 + (lane & 15);
+        Cs[row * LDC + col] = f2bf(acc[i][j][q]);
+      }
+  __syncthreads();
+  for (int v = threadIdx.x; v < BM * (BN / 8); v += kThreads) {
+    const int row = v / (BN / 8), ch = v % (BN / 8);
+    const int oy = oy0 + row / kHaloW, ox = ox0 + row % kHaloW;
+    if (oy >= g.OH || ox >= g.OW) continue;
+    uint16_t* dst = C + ((static_cast<int64_t>(n) * g.OH + oy) * g.OW + ox) * ldc + n0 + ch * 8;
+    *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(Cs + row * LDC + ch * 8);
+  }
+}
+
+// The halo kernel for this shape, or -3 when it does not apply (caller falls back to a tile variant).
+int run_halo(const Gather& g, const void* B, void* C, int64_t ldc, int64_t N, int epi, float* st, int64_t sstride,
+             hipStream_t stream) {
+  if (g.R != 3 || g.S != 3 || g.sh != 1 || g.sw != 1 || (epi & 6) || (ldc % 8) ||
+      (reinterpret_cast<uintptr_t>(C) & 15) || (reinterpret_cast<uintptr_t>(B) & 15))
+    return -3;
+  const int tiles_x = ceil_div(g.OW, kHaloW), tiles_y = ceil_div(g.OH, kHaloH);
+  const auto launch = [&](auto cs, auto bn, int64_t images) -> int {
+    constexpr int CS = decltype(cs)::value, BN = decltype(bn)::value;
+    const int64_t grid = images * tiles_y * tiles_x * (N / BN);
+    if (grid > 0x7fffffff) return -2;
+    conv_halo_kernel<CS, BN><<<static_cast<int>(grid), kThreads, 0, stream>>>(
+        g, static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), ldc, static_cast<int>(N), st, sstride, epi,
+        tiles_x, tiles_y);
+    TONY_LAUNCH_CHECK();
+    return 0;
+  };
+  const int64_t images = g.halo_images;
+  if (images <= 0) return -3;
+  if (g.Cs == 32 && N % 64 == 0) return launch(std::integral_constant<int, 32>{}, std::integral_constant<int, 64>{}, images);
+  if (g.Cs == 32 && N % 32 == 0) return launch(std::integral_constant<int, 32>{}, std::integral_constant<int, 32>{}, images);
+  if (g.Cs == 64 && N % 32 == 0) return launch(std::integral_constant<int, 64>{}, std::integral_constant<int, 32>{}, images);
+  return -3;
+}
+
 int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, int flags, float* stats,
            int64_t sstride, hipStream_t stream) {
   // flags bit0: statistics accumulated into stats (the caller zeroes it, ops/arena.py);
@@ -227,6 +412,7 @@ int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int6
   if ((epi & 3) && stats == nullptr) return -1;
   float* st = stats;
   const int v = (flags >> 8) & 0xff;
+  if (v == kHaloVariant) return run_halo(g, B, C, ldc, N, epi, st, sstride, stream);
   if (v >= kNumNtVariants) return -1;
   if (v == 0) {
     const int64_t bn = pick_bn(N, 192);
@@ -589,7 +775,7 @@ TONY_API int tony_conv_fwd(const void* x, int N, int H, int W, int C, int64_t ld
   if (OH != (H + 2 * ph - R) / sh + 1 || OW != (W + 2 * pw - S) / sw + 1 || OH <= 0 || OW <= 0) return -1;
   const int64_t M = static_cast<int64_t>(N) * OH * OW;
   if (M > 0x7fffffff || static_cast<int64_t>(N) * H * W > 0x7fffffff) return -1;
-  Gather g{static_cast<const uint16_t*>(x), ldx, H, W, C, OH, OW, R, S, sh, sw, -ph, -pw, 1, R * S * C};
+  Gather g{static_cast<const uint16_t*>(x), ldx, H, W, C, OH, OW, R, S, sh, sw, -ph, -pw, 1, R * S * C, N};
   return run_nt(g, w, y, ldy, M, Co, flags, stats, sstride, stream);
 }
 
@@ -602,7 +788,7 @@ TONY_API int tony_conv_dgrad(const void* dy, int N, int OH, int OW, int Co, int6
   if (OH != H + 2 * ph - R + 1 || OW != W + 2 * pw - S + 1) return -1;  // stride 1 only
   const int64_t M = static_cast<int64_t>(N) * H * W;
   if (M > 0x7fffffff || static_cast<int64_t>(N) * OH * OW > 0x7fffffff) return -1;
-  Gather g{static_cast<const uint16_t*>(dy), lddy, OH, OW, Co, H, W, R, S, 1, 1, ph, pw, -1, R * S * Co};
+  Gather g{static_cast<const uint16_t*>(dy), lddy, OH, OW, Co, H, W, R, S, 1, 1, ph, pw, -1, R * S * Co, N};
   return run_nt(g, wt, dx, lddx, M, C, flags & 0xff00, nullptr, 0, stream);
 }
 
@@ -617,7 +803,7 @@ TONY_API int tony_conv_wgrad(const void* dy, int64_t lddy, const void* x, int N,
   const int K = R * S * C;
   const int64_t M = static_cast<int64_t>(N) * OH * OW;
   if (M > 0x7fffffff) return -1;
-  Gather g{static_cast<const uint16_t*>(x), ldx, H, W, C, OH, OW, R, S, sh, sw, -ph, -pw, 1, K};
+  Gather g{static_cast<const uint16_t*>(x), ldx, H, W, C, OH, OW, R, S, sh, sw, -ph, -pw, 1, K, 0};
   if (slab == nullptr && dw == nullptr) return -1;
   if (Co <= 32) return launch_wgrad<32>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, stream);
   if (Co <= 64) return launch_wgrad<64>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, stream);

@@ -17,7 +17,7 @@ from typing import Callable, Dict, Hashable
 import torch
 
 AUTOTUNE = os.environ.get("TONY_CONV_AUTOTUNE", "1") != "0"
-NT_VARIANTS = tuple(range(9))  # csrc/mfma_common.h kNtVariants
+NT_VARIANTS = tuple(range(10))  # csrc/mfma_common.h kNtVariants (0-8) + 9: conv.hip halo-tile 3x3 path
 _CACHE: Dict[Hashable, int] = {}
 
 
