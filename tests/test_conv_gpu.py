@@ -222,3 +222,38 @@ def test_halo_tile_conv3x3(cuda, shape):
     if co in (32, 64):  # dgrad runs the kernel with Cin' = co
         dx = conv_dgrad(dy, wt, x.shape, 1, p, vflags=9 << 8)
         assert _rel(dx, xr.grad) < 1e-2, f"halo dgrad rel {_rel(dx, xr.grad):.4f}"
+
+
+@pytest.mark.parametrize("shape", [(2, 32, 37, 37, 64, 1), (2, 80, 35, 35, 192, 0)])  # M >= MIN_ROWS: both paths on tony kernels
+def test_conv_bn_act_pool_fused_matches_unfused(cuda, shape):
+    """conv -> BN -> ReLU -> maxpool 3x3/2 as one BN+ReLU+pool kernel == conv_bn_act then max_pool
+    (outputs, running statistics, input / weight / gamma / beta gradients)."""
+    from tony_amd.ops.conv import conv_bn_act, conv_bn_act_pool
+    from tony_amd.ops.pool import max_pool
+
+    n, ci, h, w, co, p = shape
+    torch.manual_seed(6)
+    x0 = _nhwc(torch.randn(n, ci, h, w, device=cuda)).to(torch.bfloat16)
+    w0 = _nhwc(torch.randn(co, ci, 3, 3, device=cuda) / (ci * 9) ** 0.5).to(torch.bfloat16)
+    g0 = (torch.rand(co, device=cuda) + 0.5)
+    b0 = torch.randn(co, device=cuda) * 0.1
+
+    def run(fused):
+        x = x0.clone().requires_grad_(True)
+        wt = torch.nn.Parameter(w0.clone())
+        g, b = torch.nn.Parameter(g0.clone()), torch.nn.Parameter(b0.clone())
+        rm, rv = torch.zeros(co, device=cuda), torch.ones(co, device=cuda)
+        if fused:
+            y = conv_bn_act_pool(x, wt, g, b, rm, rv, 1, p, 0.1, 1e-3, 3, 2)
+        else:
+            y = max_pool(conv_bn_act(x, wt, g, b, rm, rv, 1, p, True, 0.1, 1e-3, True), 3, 2)
+        gy = torch.randn(y.shape, device=cuda, generator=torch.Generator(device=cuda).manual_seed(2))
+        (y.float() * gy).sum().backward()
+        return y.detach().float(), rm, rv, x.grad.float(), wt.grad.float(), g.grad.float(), b.grad.float()
+
+    fu, ref = run(True), run(False)
+    assert torch.equal(fu[0], ref[0]), "pooled outputs differ"
+    torch.testing.assert_close(fu[1], ref[1], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(fu[2], ref[2], rtol=1e-5, atol=1e-6)
+    for a, b, what in zip(fu[3:], ref[3:], ("dx", "dw", "dgamma", "dbeta")):
+        assert _rel(a, b) < 2e-2, f"{what} rel {_rel(a, b):.4f}"

@@ -24,7 +24,7 @@ from ..ops.concat import Slot, assemble, concat_buffer
 from ..ops.pool import avg_pool, avg_pool3x3_s1, global_avg_pool, max_pool
 from ..ops import streams
 from ..ops.fused import FusedHead
-from .layers import ConvBNAct, init_weights
+from .layers import ConvBNAct, conv_bn_act_maxpool, init_weights
 
 
 def _seq(seq, x, slot):
@@ -238,13 +238,14 @@ class InceptionV3(nn.Module):
         self.fused = fused
 
     def forward(self, x):
-        pool = max_pool if self.fused else (lambda t, k, s: nn.functional.max_pool2d(t, k, s))
-        for m in self.stem:
+        # stem: the last conv of each group feeds a 3x3/2 max pool; fused training runs BN + ReLU + pool
+        # as one kernel there (models/layers.py conv_bn_act_maxpool)
+        for m in self.stem[:-1]:
             x = m(x)
-        x = pool(x, 3, 2)
-        for m in self.stem2:
+        x = conv_bn_act_maxpool(self.stem[-1], x, 3, 2)
+        for m in self.stem2[:-1]:
             x = m(x)
-        x = pool(x, 3, 2)
+        x = conv_bn_act_maxpool(self.stem2[-1], x, 3, 2)
         x = self.mixed_6(self.mixed_6a(self.mixed_5(x)))
         aux = self.aux(x) if (self.aux is not None and self.training) else None
         x = self.mixed_7(x)

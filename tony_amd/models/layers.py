@@ -69,6 +69,20 @@ class ConvBNAct(nn.Module):
         return self.act(self.bn(y))
 
 
+def conv_bn_act_maxpool(layer: "ConvBNAct", x, k: int = 3, s: int = 2):
+    """max_pool(layer(x), k, s); in fused training on the tony conv path one kernel does BN + ReLU +
+    pool, so the full-resolution activation is never materialised (ops/conv.py conv_bn_act_pool)."""
+    from ..ops.pool import max_pool
+
+    c, bn = layer.conv, layer.bn
+    if (layer.fused and layer.training and x.is_cuda and bn.relu and not layer.is_1x1 and USE_TONY_CONV
+            and torch.is_grad_enabled() and conv_ops.supported(x, c.weight, c.stride, c.padding)):
+        return conv_ops.conv_bn_act_pool(x, c.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, c.stride,
+                                         c.padding, bn.momentum, bn.eps, k, s)
+    y = layer(x)
+    return max_pool(y, k, s) if layer.fused else nn.functional.max_pool2d(y, k, s)
+
+
 def cast_model(model: nn.Module, dtype: torch.dtype, device=None) -> nn.Module:
     """``model.to(device, dtype)`` that keeps BatchNorm running statistics (and the batch
     counter) in fp32: the fused BN kernels accumulate them in fp32, in place."""

@@ -338,28 +338,89 @@ class _ConvBNActFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        L = _lib.lib()
         x, weight, gamma, beta, mean, invstd, Z = ctx.saved_tensors
-        stride, padding, relu, pb = ctx.cfg
-        dev = x.device
-        M, co, ldz = _rows_view(Z)
-        dy, (_, _, lddy) = _as_rows(dy)
-        dZ = torch.empty_like(Z)
-        ws = zeros_f32(_lib.stat_floats(co), dev)
-        gg, gb = _lib.grad_slot(ctx.params[1]), _lib.grad_slot(ctx.params[2])
-        inplace = gg is not None and gb is not None
-        dgamma = gg if inplace else torch.empty_like(gamma)
-        dbeta = gb if inplace else torch.empty_like(beta)
-        rc = L.tony_bn_bwd(Z.data_ptr(), ldz, dy.data_ptr(), lddy, dZ.data_ptr(), ldz, M, co, mean.data_ptr(),
-                           invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), pb, int(relu), ws.data_ptr(),
-                           dgamma.data_ptr(), dbeta.data_ptr(), int(inplace), _lib.stream_ptr(dev))
-        _lib.check(rc, "tony_bn_bwd")
-        dw = _wgrad(dZ, x, weight, stride, padding)  # first: overlaps the dgrad on the side stream
-        dx = _dgrad(dZ, weight, x.shape, stride, padding) if ctx.needs_input_grad[0] else None
-        streams.keep(dx)  # may be consumed on another (branch) stream
-        if inplace:
-            dgamma = dbeta = None
+        dx, dw, dgamma, dbeta = _conv_bn_backward(ctx, x, weight, gamma, beta, mean, invstd, Z, dy)
         return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None
+
+
+def _conv_bn_backward(ctx, x, weight, gamma, beta, mean, invstd, Z, dy):
+    """BN(+ReLU) backward from Z (the ReLU mask is recomputed from it), then the conv's wgrad (side
+    stream when active) and dgrad; parameter gradients go straight into their flat slots."""
+    L = _lib.lib()
+    stride, padding, relu, pb = ctx.cfg
+    dev = x.device
+    M, co, ldz = _rows_view(Z)
+    dy, (_, _, lddy) = _as_rows(dy)
+    dZ = torch.empty_like(Z)
+    ws = zeros_f32(_lib.stat_floats(co), dev)
+    gg, gb = _lib.grad_slot(ctx.params[1]), _lib.grad_slot(ctx.params[2])
+    inplace = gg is not None and gb is not None
+    dgamma = gg if inplace else torch.empty_like(gamma)
+    dbeta = gb if inplace else torch.empty_like(beta)
+    rc = L.tony_bn_bwd(Z.data_ptr(), ldz, dy.data_ptr(), lddy, dZ.data_ptr(), ldz, M, co, mean.data_ptr(),
+                       invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), pb, int(relu), ws.data_ptr(),
+                       dgamma.data_ptr(), dbeta.data_ptr(), int(inplace), _lib.stream_ptr(dev))
+    _lib.check(rc, "tony_bn_bwd")
+    dw = _wgrad(dZ, x, weight, stride, padding)  # first: overlaps the dgrad on the side stream
+    dx = _dgrad(dZ, weight, x.shape, stride, padding) if ctx.needs_input_grad[0] else None
+    streams.keep(dx)  # may be consumed on another (branch) stream
+    if inplace:
+        dgamma = dbeta = None
+    return dx, dw, dgamma, dbeta
+
+
+class _ConvBNActPoolFn(torch.autograd.Function):
+    """maxpool_KxK/S(relu(bn(conv(x)))) in training: the conv epilogue produces the BN sums and one
+    kernel normalises + ReLUs + pools (csrc/bn_act.hip bn_relu_maxpool_kernel), so the
+    full-resolution activation is never written or re-read.  Backward: max-pool backward through
+    the saved argmax, then the BN + conv backward of _ConvBNActFn."""
+
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, running_mean, running_var, stride, padding, momentum, eps, k, s):
+        L = _lib.lib()
+        _lib.check_f32_stats(running_mean, running_var)
+        dev = x.device
+        co = weight.shape[0]
+        stats = zeros_f32(_lib.stat_floats(co), dev)
+        Z = _fwd(x, weight, stride, padding, stats)
+        _, _, ldz = _rows_view(Z)
+        n, _, h, w = Z.shape
+        oh, ow = (h - k) // s + 1, (w - k) // s + 1
+        y = _cl_empty(n, co, oh, ow, dev)
+        arg = torch.empty((n, oh, ow, co), dtype=torch.uint8, device=dev)
+        mean = torch.empty(co, dtype=torch.float32, device=dev)
+        invstd = torch.empty(co, dtype=torch.float32, device=dev)
+        pb = int(gamma.dtype == _BF16)
+        rc = L.tony_bn_relu_maxpool(Z.data_ptr(), ldz, stats.data_ptr(), stats.data_ptr() + 4 * co, 2 * co,
+                                    gamma.data_ptr(), beta.data_ptr(), pb, float(eps), mean.data_ptr(),
+                                    invstd.data_ptr(), _lib.ptr(running_mean), _lib.ptr(running_var), float(momentum),
+                                    y.data_ptr(), co, arg.data_ptr(), n, h, w, co, k, s, _lib.stream_ptr(dev))
+        _lib.check(rc, "tony_bn_relu_maxpool")
+        ctx.save_for_backward(x, weight, gamma, beta, mean, invstd, Z, arg)
+        ctx.params = (weight, gamma, beta)
+        ctx.cfg = (stride, padding, True, pb)
+        ctx.pool = (k, s)
+        return y
+
+    @staticmethod
+    def backward(ctx, dyp):
+        x, weight, gamma, beta, mean, invstd, Z, arg = ctx.saved_tensors
+        k, s = ctx.pool
+        n, co, h, w = Z.shape
+        dyp, (_, _, lddy) = _as_rows(dyp)
+        dy = _cl_empty(n, co, h, w, Z.device)
+        rc = _lib.lib().tony_maxpool_bwd(dyp.data_ptr(), arg.data_ptr(), dy.data_ptr(), n, h, w, co, k, s, lddy, co,
+                                         _lib.stream_ptr(Z.device))
+        _lib.check(rc, "tony_maxpool_bwd")
+        dx, dw, dgamma, dbeta = _conv_bn_backward(ctx, x, weight, gamma, beta, mean, invstd, Z, dy)
+        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None
+
+
+def conv_bn_act_pool(x, weight, gamma, beta, running_mean, running_var, stride=1, padding=0, momentum=0.1,
+                     eps=1e-3, k=3, s=2):
+    """max_pool2d(relu(batch_norm(conv2d(x))), k, s) in training mode, fused (see _ConvBNActPoolFn)."""
+    return _ConvBNActPoolFn.apply(x, weight, gamma, beta, running_mean, running_var, _pair(stride), _pair(padding),
+                                  momentum, eps, k, s)
 
 
 def conv_bn_act(x, weight, gamma, beta, running_mean, running_var, stride=1, padding=0, training=True,

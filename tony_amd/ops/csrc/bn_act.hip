@@ -374,6 +374,86 @@ void plan_rows(int64_t M, int C, int min_iters, int max_blocks, int64_t* rpb, in
 
 bool bad_c(int C) { return C <= 0 || C % 8 != 0 || C > kMaxC; }
 
+// Training BN + ReLU fused with the KxK / stride-S max pool that follows it (Inception's stem:
+// conv -> BN -> ReLU -> maxpool 3x3/2 at 147x147 and 71x71).  The full-resolution activation is
+// never written: each lane normalises the 9 window inputs of its 8 channels on the fly (scale /
+// shift rebuilt per workgroup from the conv epilogue's statistics, as in bn_fwd_apply_kernel),
+// rounds them to bf16 (so max and argmax match the unfused pair exactly) and writes the pooled
+// value and the window argmax byte.  The backward needs only Z (the BN backward recomputes the ReLU
+// mask from it) and the argmax.
+__global__ __launch_bounds__(kThreads) void bn_relu_maxpool_kernel(
+    const uint16_t* __restrict__ z, int64_t ldz, const float* __restrict__ sum, const float* __restrict__ sumsq,
+    int64_t sstride, const void* gamma, const void* beta, int param_bf16, float eps,
+    float* __restrict__ save_mean, float* __restrict__ save_invstd, float* __restrict__ running_mean,
+    float* __restrict__ running_var, float momentum, uint16_t* __restrict__ y, int64_t ldy,
+    uint8_t* __restrict__ arg, int N, int H, int W, int C, int OH, int OW, int K, int S) {
+  __shared__ float scale[kMaxC];
+  __shared__ float shift[kMaxC];
+  const int64_t M = static_cast<int64_t>(N) * H * W;
+  const float inv_m = 1.f / static_cast<float>(M);
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    const float mean = shard_sum(sum, c, sstride) * inv_m;
+    const float var = fmaxf(shard_sum(sumsq, c, sstride) * inv_m - mean * mean, 0.f);
+    const float invstd = rsqrtf(var + eps);
+    if (blockIdx.x == 0) {
+      save_mean[c] = mean;
+      save_invstd[c] = invstd;
+      if (running_mean != nullptr) {
+        const float unbiased = M > 1 ? var * (static_cast<float>(M) / static_cast<float>(M - 1)) : var;
+        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+      }
+    }
+    const float g = load_param(gamma, c, param_bf16, 1.f);
+    const float b = load_param(beta, c, param_bf16, 0.f);
+    scale[c] = g * invstd;
+    shift[c] = b - mean * g * invstd;
+  }
+  __syncthreads();
+  const uint32_t CG = C >> 3;
+  const uint32_t total = static_cast<uint32_t>(N) * OH * OW * CG;
+  const uint32_t stride = gridDim.x * kThreads;
+  for (uint32_t t = blockIdx.x * kThreads + threadIdx.x; t < total; t += stride) {
+    const uint32_t cg = t % CG;
+    const uint32_t site = t / CG;
+    const int ow = static_cast<int>(site % OW);
+    const uint32_t nh = site / OW;
+    const int oh = static_cast<int>(nh % OH);
+    const int64_t n = nh / OH;
+    float sc[8], sh[8], best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = scale[cg * 8 + j];
+      sh[j] = shift[cg * 8 + j];
+      best[j] = -__builtin_huge_valf();
+      bi[j] = 0;
+    }
+    for (int kh = 0; kh < K; ++kh) {
+      const int hh = oh * S + kh;
+      for (int kw = 0; kw < K; ++kw) {
+        const int ww = ow * S + kw;
+        float f[8];
+        load8(z + ((n * H + hh) * W + ww) * ldz + cg * 8).to_float(f);
+        const uint8_t idx = static_cast<uint8_t>(kh * K + kw);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = bf2f(f2bf(fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f)));  // the bf16 activation
+          if (v > best[j] || (v != v)) {
+            best[j] = v;
+            bi[j] = idx;
+          }
+        }
+      }
+    }
+    store8(y + static_cast<int64_t>(site) * ldy + cg * 8, bf16x8::from_float(best));
+    uint2 packed;
+    packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (static_cast<uint32_t>(bi[3]) << 24);
+    packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (static_cast<uint32_t>(bi[7]) << 24);
+    *reinterpret_cast<uint2*>(arg + static_cast<int64_t>(site) * C + cg * 8) = packed;
+  }
+}
+
 }  // namespace
 
 // ---- composable entry points (the fused conv heads call these on channel sub-ranges) ----
@@ -516,6 +596,28 @@ TONY_API int tony_bn_bwd_res(const void* x, int64_t ldx, const void* dy, int64_t
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, static_cast<const uint16_t*>(y),
       ldy, static_cast<uint16_t*>(dres), lddr, static_cast<uint16_t*>(dx), lddx, M, C, rpb, mean, invstd, gamma, beta,
       param_bf16, 1, dsums_ws, dsums_ws + C, ss, dgamma, dbeta, accumulate);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// Training BN(+ReLU) of z [N,H,W,C] (pixel stride ldz) from the sharded conv-epilogue statistics,
+// fused with a KxK / stride-S max pool: writes the pooled y [N,OH,OW,C] (pixel stride ldy) and the
+// argmax bytes [N,OH,OW,C]; saves mean / invstd and updates the running statistics.
+TONY_API int tony_bn_relu_maxpool(const void* z, int64_t ldz, const float* sum, const float* sumsq, int64_t sstride,
+                                  const void* gamma, const void* beta, int param_bf16, float eps, float* save_mean,
+                                  float* save_invstd, float* running_mean, float* running_var, float momentum,
+                                  void* y, int64_t ldy, void* argmax, int N, int H, int W, int C, int K, int S,
+                                  hipStream_t stream) {
+  if (bad_c(C) || (ldz % 8) || (ldy % 8) || sstride < 0 || K * K > 255 || H < K || W < K || S < 1) return -1;
+  if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
+  const int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
+  int64_t work = static_cast<int64_t>(N) * OH * OW * (C / 8);
+  int64_t grid = (work + kThreads - 1) / kThreads;
+  if (grid > 16384) grid = 16384;
+  bn_relu_maxpool_kernel<<<static_cast<int>(grid < 1 ? 1 : grid), kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(z), ldz, sum, sumsq, sstride, gamma, beta, param_bf16, eps, save_mean, save_invstd,
+      running_mean, running_var, momentum, static_cast<uint16_t*>(y), ldy, static_cast<uint8_t*>(argmax), N, H, W, C,
+      OH, OW, K, S);
   TONY_LAUNCH_CHECK();
   return 0;
 }
