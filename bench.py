@@ -46,6 +46,9 @@ def parse():
                     help="serial backward (no weight gradients on a second stream)")
     ap.add_argument("--no-branch-streams", action="store_true",
                     help="Inception branches on one stream (branch streams are opt-in: TONY_BRANCH_STREAMS=1)")
+    ap.add_argument("--tune-cache", default=None,
+                    help="JSON of kernel-choice decisions: loaded when it exists (no autotuning for those "
+                         "shapes), written after setup otherwise (reproducible profiles, faster startup)")
     ap.add_argument("--no-miopen-find", action="store_true",
                     help="MIOpen immediate mode instead of find (faster startup, slower non-1x1 convs)")
     return ap.parse_args()
@@ -103,6 +106,11 @@ def main():
 
     from tony_amd.parallel.collectives import max_over_ranks
 
+    from tony_amd.ops import tune
+
+    tune_loaded = 0
+    if args.tune_cache and os.path.exists(args.tune_cache):
+        tune_loaded = tune.load(args.tune_cache)
     mode = "eager" if args.no_graph else args.mode
     trainer = Trainer(model, ps, loss_fn, use_graph=mode != "eager", overlap_wgrad=not args.no_wgrad_stream,
                       branch_streams=not args.no_branch_streams)
@@ -146,6 +154,9 @@ def main():
         print(f"bench.py: non-finite loss after warmup: {loss.item()}", file=sys.stderr)
         return 3
 
+    if args.tune_cache and not tune_loaded and rank == 0:  # every shape has been tuned by now
+        n_saved = tune.save(args.tune_cache)
+        print(f"[bench] saved {n_saved} kernel-choice decisions to {args.tune_cache}", file=sys.stderr, flush=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -193,6 +204,7 @@ def main():
                 "hip_graph": mode == "graph",
                 "step_mode": mode,
                 "mode_setup_ms": setup or None,
+                "tune_cache_loaded": tune_loaded,
                 "wgrad_stream": not args.no_wgrad_stream,
                 "branch_streams": _branch_streams_on(args),
                 "host_ms_per_step": round(1000.0 * host / args.steps, 3),

@@ -106,3 +106,36 @@ def gemm_flags(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, M: int, N: int
     base = 1 if stats else 0
     return pick(key, lambda vf: L.tony_gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, lda, K, N,
                                                  base | vf, scratch.data_ptr(), 2 * N, stream))
+
+
+# ---- persistent decisions (the MIOpen find-db idea for tony_amd's own choices) -------------------
+def save(path: str) -> int:
+    """Write every decision made so far -- tile variants / split plans (this module) and the
+    tony-vs-MIOpen choice per conv pass and shape (ops/conv.py) -- to a JSON file; returns the count.
+    Keys are the repr of the in-process tuple keys (ints, strings, tuples, bools only)."""
+    import json
+
+    from . import conv
+
+    rec = {"tune": {repr(k): v for k, v in _CACHE.items()}, "conv": {repr(k): v for k, v in conv._CHOICE.items()}}
+    with open(path, "w") as f:
+        json.dump(rec, f, indent=0, sort_keys=True)
+    return len(rec["tune"]) + len(rec["conv"])
+
+
+def load(path: str) -> int:
+    """Seed the decision caches from ``save()``'s file (same hardware: the choices are only about
+    speed, every variant computes the same result).  Returns how many decisions were loaded."""
+    import ast
+    import json
+
+    from . import conv
+
+    with open(path) as f:
+        rec = json.load(f)
+    for k, v in rec.get("tune", {}).items():
+        _CACHE[ast.literal_eval(k)] = v
+    for k, v in rec.get("conv", {}).items():
+        conv._CHOICE[ast.literal_eval(k)] = v
+    return len(rec.get("tune", {})) + len(rec.get("conv", {}))
+

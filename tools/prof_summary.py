@@ -20,13 +20,15 @@ def classify(name):
     n = name.lower()
     if "bn_fwd" in n or "bn_bwd" in n:
         return "tony HIP: fused BN+ReLU"
-    if "gemm_nt_kernel" in n or "gemm_tn_splitk" in n:
+    if "bn_relu_maxpool" in n:
+        return "tony HIP: fused BN+ReLU+maxpool (stem)"
+    if "gemm_nt_kernel" in n or "gemm_tn_splitk" in n or "gemm_tn_glds" in n:
         return "tony HIP: MFMA GEMM (1x1 conv fwd/dgrad/wgrad)"
-    if "conv_nt_kernel" in n or "conv_wgrad_kernel" in n:
+    if "conv_nt_kernel" in n or "conv_wgrad_kernel" in n or "conv_wgrad_glds" in n or "conv_halo" in n:
         return "tony HIP: implicit-GEMM conv (fwd/dgrad/wgrad)"
     if "add_f32_kernel" in n:
         return "tony HIP: in-place grad accumulate"
-    if "box3_kernel" in n or "maxpool_" in n:
+    if "box3_kernel" in n or "maxpool_" in n or "avgpool_" in n:
         return "tony HIP: pooling"
     if "sgd_kernel" in n or "adam_kernel" in n or "grad_stats" in n:
         return "tony HIP: fused optimizer"
