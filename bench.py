@@ -63,10 +63,14 @@ def main():
         if world == 1 and args.gpus > 1:
             print(f"bench.py: --gpus {args.gpus} must be launched with torch.distributed.run", file=sys.stderr)
             return 2
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # test hooks for rehearsing the multi-rank path on a one-GPU box: several ranks on one device
+    # over gloo (TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0); the driver's runs use RCCL, one GPU per rank
+    backend = os.environ.get("TONY_BENCH_BACKEND", "nccl")
+    dev_index = int(os.environ.get("TONY_BENCH_DEVICE", local_rank))
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     from tony_amd.ops import cross_entropy
     from tony_amd.parallel.ps import ParameterServer
