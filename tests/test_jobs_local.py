@@ -148,3 +148,14 @@ def test_cluster_discovery(conf):
     rc, client, _ = run_job(conf, "cluster_discovery.py", ["tony.head.instances=1", "tony.worker.instances=1",
                                                            "tony.ps.instances=0"])
     assert rc == 0, _diag(client)
+
+
+def test_resnet50_ddp_minimum_slice(conf):
+    """SURVEY.md §7.3's minimum slice: PyTorch runtime env -> init_process_group -> ResNet-50 under
+    tony_amd's bucketed DDP (tiny images on the CPU here; bf16 fused kernels on a GPU node)."""
+    rc, client, _ = run_job(conf, "resnet50_ddp.py", ["tony.application.framework=pytorch", "tony.worker.instances=2",
+                                                      "tony.ps.instances=0"],
+                            "--batch-size 2 --image-size 32 --steps 1 --warmup 1")
+    assert rc == 0, _diag(client)
+    ms = _metrics(client)
+    assert len(ms) == 1 and ms[0]["world"] == 2 and ms[0]["images_per_sec"] > 0
