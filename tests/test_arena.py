@@ -39,3 +39,30 @@ def test_side_stream_inactive_runs_inline():
     assert streams.run(work, acc) is None
     assert acc.tolist() == [1.0] * 4
     assert streams.end() == 0
+
+
+def test_tune_cache_roundtrip(tmp_path):
+    """ops/tune.py save/load: tile variants, split plans and tony-vs-MIOpen choices survive a JSON round
+    trip with their tuple keys intact (bench.py --tune-cache)."""
+    from tony_amd.ops import conv, tune
+
+    saved_t, saved_c = dict(tune._CACHE), dict(conv._CHOICE)
+    try:
+        tune._CACHE.clear()
+        conv._CHOICE.clear()
+        tune._CACHE[("conv_fwd", (128, 64, 35, 35), 64, (96, 64, 3, 3), (1, 1), (1, 1), True)] = 4
+        tune._CACHE[("wgrad_occ", (128, 96, 35, 35), 96, (128, 64, 35, 35), 64, (96, 64, 3, 3), 1, 1, 1, 1)] = 2
+        conv._CHOICE[("wgrad", (128, 96, 35, 35), (96, 64, 3, 3), (1, 1), (1, 1))] = "tony"
+        path = str(tmp_path / "tune.json")
+        assert tune.save(path) == 3
+        want_t, want_c = dict(tune._CACHE), dict(conv._CHOICE)
+        tune._CACHE.clear()
+        conv._CHOICE.clear()
+        assert tune.load(path) == 3
+        assert tune._CACHE == want_t and conv._CHOICE == want_c
+        assert tune.cached(("conv_fwd", (128, 64, 35, 35), 64, (96, 64, 3, 3), (1, 1), (1, 1), True)) == 4 << 8
+    finally:
+        tune._CACHE.clear()
+        tune._CACHE.update(saved_t)
+        conv._CHOICE.clear()
+        conv._CHOICE.update(saved_c)
