@@ -361,8 +361,16 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
 // Grid sizing: enough workgroups to cover 256 CUs several times over, but each
 // workgroup streams >= `min_iters` row groups so the per-WG LDS epilogue and
 // atomics stay amortised.
-void plan_rows(int64_t M, int C, int min_iters, int max_blocks, int64_t* rpb, int* grid) {
+void plan_rows(int64_t M, int C, int min_iters, int max_blocks, int64_t* rpb, int* grid, bool fill = false) {
   const int RPI = kThreads / (C / 8);
+  // fill: small images (Inception's 17x17 / 8x8 layers: M = 37k / 8k rows) would get fewer
+  // workgroups than the cap at the default depth; trade per-workgroup iterations for workgroups.
+  // Measured (tools/bn_bench.py): pays for the backward reduction (-121 us/step), costs the apply
+  // kernels (+180 us/step), so only the reduction asks for it.
+  const int64_t want = max_blocks < 1024 ? max_blocks : 1024;
+  while (fill && min_iters > 1 &&
+         (M + static_cast<int64_t>(RPI) * min_iters - 1) / (static_cast<int64_t>(RPI) * min_iters) < want)
+    min_iters >>= 1;
   int64_t g = (M + static_cast<int64_t>(RPI) * min_iters - 1) / (static_cast<int64_t>(RPI) * min_iters);
   if (g > max_blocks) g = max_blocks;
   if (g < 1) g = 1;
@@ -519,7 +527,7 @@ TONY_API int tony_bn_bwd_reduce(const void* x, int64_t ldx, const void* dy, int6
   if (bad_c(C) || (ldx % 8) || (lddy % 8) || sstride < 0) return -1;
   int64_t rpb;
   int grid;
-  plan_rows(M, C, 8, 512, &rpb, &grid);  // few WGs: C atomics per WG contend per channel
+  plan_rows(M, C, 8, 512, &rpb, &grid, true);  // few WGs: C atomics per WG contend per channel
   bn_bwd_reduce_kernel<false><<<grid, kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, nullptr, 0, M, C, rpb, mean,
       invstd, gamma, beta, param_bf16, relu, dsum, dsumx, sstride);
