@@ -226,7 +226,9 @@ int launch_nt_bm(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M
 // HT x WT = 8 x 16 output pixels (128 GEMM rows) x BN output channels: it loads the (HT+2) x (WT+2)
 // input patch once into LDS (zeros outside the image), the BN x 9*Cin weight panel once, and reads
 // the MFMA A fragments straight out of the patch at the 9 tap offsets.  LDS pixel rows and weight
-// rows are padded by 16 B so the 16 lanes of a fragment read hit 16 distinct 4-bank groups.
+// rows are padded by 32 B: with ds_read_b128's lane groups ({0-3,12-15,20-27}, ...) that is the
+// smallest pad for which every group's 16 addresses hit distinct 4-bank sets (a 16-B pad measured
+// SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE = 38 %).
 // Same GEMM view as conv_nt_kernel (m = (n, oy, ox), k = (r, s, c)); the dgrad is the same kernel
 // on dY with flipped taps (g.sign = -1) and the transposed weights.
 constexpr int kHaloH = 8, kHaloW = 16;  // 16 x 16 measured no faster (one-shot load phase dominates)
@@ -239,9 +241,9 @@ __global__ __launch_bounds__(kThreads) void conv_halo_kernel(Gather g, const uin
                                                             int tiles_x, int tiles_y) {
   constexpr int R = 3, S = 3;
   constexpr int HH = kHaloH + R - 1, HW = kHaloW + S - 1;
-  constexpr int PSTR = CS + 8;                 // LDS elements per halo pixel (16-B pad)
+  constexpr int PSTR = CS + 16;                // LDS elements per halo pixel (32-B pad)
   constexpr int KK = R * S * CS;               // GEMM K
-  constexpr int KP = KK + 8;                   // LDS elements per weight row (16-B pad)
+  constexpr int KP = KK + 16;                  // LDS elements per weight row (32-B pad)
   constexpr int HALO = HH * HW * PSTR;
   constexpr int WTS = BN * KP;
   constexpr int BM = kHaloH * kHaloW;          // 128 rows
