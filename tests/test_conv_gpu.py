@@ -257,3 +257,65 @@ def test_conv_bn_act_pool_fused_matches_unfused(cuda, shape):
     torch.testing.assert_close(fu[2], ref[2], rtol=1e-5, atol=1e-6)
     for a, b, what in zip(fu[3:], ref[3:], ("dx", "dw", "dgamma", "dbeta")):
         assert _rel(a, b) < 2e-2, f"{what} rel {_rel(a, b):.4f}"
+
+
+# (N, H, W, (R, S), stride, (ph, pw)): Inception-v3's 3x3/2 stem (shrunk in N and H/W, with a
+# partial last workgroup) and a 7x7/2 p3 stem on the same kernel
+STEM_SHAPES = [(2, 299, 299, (3, 3), 2, (0, 0)), (3, 37, 41, (3, 3), 2, (0, 0)), (2, 45, 33, (7, 7), 2, (3, 3)),
+               (1, 20, 20, (3, 3), 1, (1, 1))]
+
+
+@pytest.mark.parametrize("shape", STEM_SHAPES, ids=[f"{s[1]}x{s[2]}k{s[3][0]}s{s[4]}" for s in STEM_SHAPES])
+def test_stem_fwd_direct_kernel(cuda, shape):
+    """csrc/stem.hip (3-channel direct conv + BN statistics epilogue) vs the fp32 conv2d."""
+    from tony_amd.ops import _lib
+    from tony_amd.ops.conv import stem_fwd, stem_supported
+
+    n, h, w, k, s, p = shape
+    torch.manual_seed(3)
+    x = _nhwc(torch.randn(n, 3, h, w, device=cuda)).to(torch.bfloat16)
+    wt = _nhwc(0.2 * torch.randn(32, 3, *k, device=cuda)).to(torch.bfloat16)
+    assert stem_supported(x, wt, s, p)
+    stats = torch.zeros(_lib.stat_floats(32), device=cuda)
+    y = stem_fwd(x, wt, s, p, stats)
+    ref = torch.nn.functional.conv2d(x.float(), wt.float(), None, s, p)
+    assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(y, ref) < 1e-2
+    st = _lib.fold_stats(stats, 32)
+    torch.testing.assert_close(st[:32], ref.sum((0, 2, 3)), rtol=1e-3, atol=ref.numel() / 32 * 1e-4)
+    torch.testing.assert_close(st[32:], (ref * ref).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+
+
+def test_stem_conv_bn_act_layer_fwd_bwd(cuda):
+    """The fused ConvBNAct layer on a 3-channel input (direct forward, MIOpen wgrad) vs fp32."""
+    from tony_amd.ops import _lib
+    from tony_amd.ops import conv as C
+
+    torch.manual_seed(4)
+    n, h, w, co = 4, 75, 75, 32
+    x = _nhwc(torch.randn(n, 3, h, w, device=cuda)).to(torch.bfloat16)
+    wt = _nhwc(0.2 * torch.randn(co, 3, 3, 3, device=cuda)).to(torch.bfloat16).requires_grad_(True)
+    g = torch.empty(co, device=cuda).uniform_(0.5, 1.5).to(torch.bfloat16).requires_grad_(True)
+    b = torch.empty(co, device=cuda).uniform_(-0.2, 0.2).to(torch.bfloat16).requires_grad_(True)
+    rm, rv = torch.zeros(co, device=cuda), torch.ones(co, device=cuda)
+    _lib.set_inplace_grads(False)
+    saved = C.AUTOTUNE, C.STEM
+    C.AUTOTUNE, C.STEM = False, True  # route the stem to the fused layer and pin the direct kernel
+    try:
+        y = C.conv_bn_act(x, wt, g, b, rm, rv, 2, 0, True, 0.1, 1e-3, True)
+        key = [k for k in C._CHOICE if k[0] == "fwd" and k[2] == (co, 3, 3, 3)]
+        assert not key or C._CHOICE[key[0]] == "tony"
+        wr, gr, br = (t.detach().float().requires_grad_(True) for t in (wt, g, b))
+        rm_r, rv_r = torch.zeros(co, device=cuda), torch.ones(co, device=cuda)
+        yr = torch.relu(torch.nn.functional.batch_norm(torch.nn.functional.conv2d(x.float(), wr, None, 2, 0), rm_r,
+                                                       rv_r, gr, br, True, 0.1, 1e-3))
+        assert _rel(y, yr) < 2e-2
+        torch.testing.assert_close(rm, rm_r, rtol=2e-2, atol=2e-3)
+        dy = _nhwc(torch.randn_like(yr)).to(torch.bfloat16)
+        y.backward(dy)
+        yr.backward(dy.float())
+        assert _rel(wt.grad, wr.grad) < 3e-2
+        assert _rel(g.grad, gr.grad) < 3e-2 and _rel(b.grad, br.grad) < 3e-2
+    finally:
+        C.AUTOTUNE, C.STEM = saved
+        _lib.set_inplace_grads(True)

@@ -57,8 +57,10 @@ class ConvBNAct(nn.Module):
             return _HeadFn.apply(x, self.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                  (self.conv.out_channels,), 0, self.training, bn.momentum, bn.eps,
                                  (slot,) if slot is not None else None)[0]
-        if self.fused and x.is_cuda and USE_TONY_CONV and conv_ops.supported(x, self.conv.weight, self.conv.stride,
-                                                                              self.conv.padding):
+        if self.fused and x.is_cuda and USE_TONY_CONV and (
+                conv_ops.supported(x, self.conv.weight, self.conv.stride, self.conv.padding)
+                or (conv_ops.STEM and conv_ops.stem_supported(x, self.conv.weight, self.conv.stride,
+                                                              self.conv.padding))):
             # implicit-GEMM conv with BN statistics in its epilogue + fused apply (ops/conv.py)
             bn, c = self.bn, self.conv
             return conv_ops.conv_bn_act(x, c.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, c.stride,

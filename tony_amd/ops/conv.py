@@ -38,6 +38,11 @@ def _pair(v):
     return tuple(v) if isinstance(v, (tuple, list)) else (int(v), int(v))
 
 
+# TONY_STEM=1 routes 3-channel stems through the fused conv+BN layer with the direct kernel
+# (csrc/stem.hip) as a per-shape autotune candidate against MIOpen.  Off by default: on MI355X it
+# measured 174 us vs MIOpen's 156 us (fwd + BN statistics, Inception stem at batch 128,
+# profiles/r1_stem_direct_kernel.log), so the stem stays on MIOpen + a separate statistics pass.
+STEM = os.environ.get("TONY_STEM", "0") == "1"
 MIN_ROWS = 2048  # below this many output pixels a tile grid cannot fill 256 CUs: leave it to MIOpen
 
 
@@ -50,6 +55,15 @@ def supported(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, dilati
         return False
     oh, ow = out_hw(x.shape[2], x.shape[3], weight.shape[2], weight.shape[3], stride, padding)
     return x.shape[0] * oh * ow >= (min_rows or MIN_ROWS)
+
+
+def stem_supported(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, dilation=1, groups=1) -> bool:
+    """Whether the direct 3-channel stem kernel (csrc/stem.hip) takes this forward conv: dense NHWC
+    bf16 RGB input, 32 output channels, R*S <= 49."""
+    return (x.is_cuda and x.dtype == _BF16 and weight.dtype == _BF16 and x.dim() == 4 and groups == 1
+            and _pair(dilation) == (1, 1) and x.shape[1] == 3 and tuple(weight.shape[:2]) == (32, 3)
+            and weight.shape[2] * weight.shape[3] <= 49 and x.is_contiguous(memory_format=torch.channels_last)
+            and x.numel() < 2 ** 31)
 
 
 def out_hw(h, w, r, s, stride, padding):
@@ -77,6 +91,8 @@ def conv_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: 
              vflags: int | None = None):
     """Y = conv(x, w); with ``stats`` (zeroed, ``_lib.stat_floats(Cout)`` floats) the epilogue accumulates
     [sum | sumsq] of Y into its STAT_SHARDS copies.  ``vflags``: tile variant bits (None: autotuned)."""
+    if x.shape[1] == 3:
+        return stem_fwd(x, weight, stride, padding, stats)
     x, (_, C, ldx) = _as_rows(x)
     n, _, h, w = x.shape
     co, _, r, s = weight.shape
@@ -101,9 +117,28 @@ def conv_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: 
     return y
 
 
+def stem_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: torch.Tensor | None = None):
+    """Forward of a 3-channel stem conv on the vector ALUs (csrc/stem.hip), optional BN statistics
+    epilogue in the ``conv_fwd`` layout.  Its backward-weight stays on MIOpen (``_wgrad``)."""
+    if not stem_supported(x, weight, stride, padding):
+        raise ValueError(f"stem_fwd: unsupported conv x={tuple(x.shape)} w={tuple(weight.shape)}")
+    n, c, h, w = x.shape
+    co, _, r, s = weight.shape
+    _lib.check_stat_buffer(stats, co)
+    (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
+    oh, ow = out_hw(h, w, r, s, stride, padding)
+    y = _cl_empty(n, co, oh, ow, x.device)
+    wk = weight.permute(2, 3, 1, 0).float().contiguous()  # fp32 [R][S][3][Co]: wave-uniform scalar loads
+    rc = _lib.lib().tony_stem_fwd(x.data_ptr(), n, h, w, c, wk.data_ptr(), co, r, s, sh, sw, ph, pw, y.data_ptr(),
+                                  oh, ow, co, 1 if stats is not None else 0, _lib.ptr(stats),
+                                  2 * co if stats is not None else 0, _lib.stream_ptr(x.device))
+    _lib.check(rc, "tony_stem_fwd")
+    return y
+
+
 def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, padding=0,
                vflags: int | None = None) -> torch.Tensor:
-    if _pair(stride) != (1, 1):
+    if _pair(stride) != (1, 1) or x_shape[1] % 8:
         return _miopen_dgrad(dy, weight, x_shape, stride, padding)
     n, c, h, w = x_shape
     co, _, r, s = weight.shape
@@ -221,7 +256,7 @@ def _dgrad(dy, weight, x_shape, stride, padding):
     if impl == "miopen":
         return _miopen_dgrad(dy, weight, x_shape, stride, padding)
     cands = {"miopen": lambda: _miopen_dgrad(dy, weight, x_shape, stride, padding)}
-    if _pair(stride) == (1, 1):
+    if _pair(stride) == (1, 1) and x_shape[1] % 8 == 0:
         cands["tony"] = lambda: conv_dgrad(dy, weight, x_shape, stride, padding)
     impl = _choose(key, cands)
     return conv_dgrad(dy, weight, x_shape, stride, padding) if impl == "tony" else \
@@ -237,6 +272,8 @@ def _wgrad(dy, x, weight, stride, padding):
     """dW accumulated into the parameter's gradient slot (returns None) or returned for autograd."""
     key = ("wgrad", tuple(dy.shape), tuple(weight.shape), stride, padding)
     impl = _CHOICE.get(key) or WGRAD_IMPL or None
+    if x.shape[1] % 8:
+        impl = "miopen"  # 3-channel stem: no tony weight-gradient kernel
     if impl is None:
         # With the weight gradients on the side stream (ops/streams.py) their GPU time hides behind the
         # data-gradient chain, while MIOpen's costs 3 more launches (output fill, fp32->bf16 cast, add
@@ -426,7 +463,7 @@ def conv_bn_act_pool(x, weight, gamma, beta, running_mean, running_var, stride=1
 def conv_bn_act(x, weight, gamma, beta, running_mean, running_var, stride=1, padding=0, training=True,
                 momentum=0.1, eps=1e-3, relu=True, slot=None):
     """relu(bn(conv(x))); with a ``concat.Slot`` the result is written into that channel slice."""
-    if supported(x, weight, stride, padding):
+    if supported(x, weight, stride, padding) or (STEM and stem_supported(x, weight, stride, padding)):
         return _ConvBNActFn.apply(x, weight, gamma, beta, running_mean, running_var, _pair(stride), _pair(padding),
                                   training, momentum, eps, relu, slot)
     z = torch.nn.functional.conv2d(x, weight, None, stride, padding)

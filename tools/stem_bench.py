@@ -1,6 +1,7 @@
 """Time the Inception-v3 3-channel stem conv (128x3x299x299 -> 32, 3x3/2) two ways, NHWC bf16:
 
   miopen : F.conv2d forward + MIOpen backward-weight (what the 3-channel stem runs on today);
+  direct : csrc/stem.hip, the 27-tap direct kernel with the statistics epilogue (the shipped path);
   pad8   : input zero-padded to 8 channels (one copy) + tony implicit-GEMM forward (with the BN
            statistics epilogue) + tony split-K backward-weight on the padded operands.
 
@@ -59,6 +60,8 @@ def main():
         "pad 3->8": gpu_ms(pad, args.iters),
         "tony fwd+stats (pad8)": gpu_ms(lambda: C.conv_fwd(x8, w8, 2, 0, stats), args.iters),
         "tony wgrad (pad8)": gpu_ms(lambda: C.conv_wgrad(dy, x8, w8.shape, 2, 0), args.iters),
+        "direct fwd (stem.hip)": gpu_ms(lambda: C.stem_fwd(x, w, 2, 0), args.iters),
+        "direct fwd+stats (stem.hip)": gpu_ms(lambda: C.stem_fwd(x, w, 2, 0, stats), args.iters),
     }
     # numerics of the padded path vs the fp32 reference
     ref = torch.nn.functional.conv2d(x.float(), w.float(), None, 2, 0)
@@ -69,6 +72,8 @@ def main():
         print(f"{k:>24}: {v * 1000:8.1f} us")
     print(f"miopen total {1000 * (res['miopen fwd+stats'] + res['miopen wgrad']):.1f} us; pad8 total "
           f"{1000 * (res['pad 3->8'] + res['tony fwd+stats (pad8)'] + res['tony wgrad (pad8)']):.1f} us")
+    got_d = C.stem_fwd(x, w, 2, 0).float()
+    print("direct fwd rel err", ((got_d - ref).norm() / ref.norm()).item())
     print("fwd max rel err", ((got - ref).abs().max() / ref.abs().max()).item(),
           "wgrad max rel err", ((dwg - dwr).abs().max() / dwr.abs().max()).item())
 
