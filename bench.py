@@ -217,6 +217,8 @@ def main():
                                                     round(1000.0 * trainer.host_bwd_s, 3)],
                 "kernels": "stock-comparator" if args.stock else "tony_amd HIP",
                 "conv_impl": _conv_impl_counts(),
+                "grad_buckets": len(ps.buckets),
+                "buckets_overlapped_with_backward": ps.overlapped_buckets,
                 "final_loss": round(final_loss, 4),
             },
         }

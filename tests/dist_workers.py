@@ -75,24 +75,31 @@ def hvd_rank(rank, world, rdv_port):
     return out
 
 
-def ps_rank(rank, world, port, mode, sync, steps):
+def ps_rank(rank, world, port, mode, sync, steps, bucket_mb=32, ps_ranks=(0,), overlap=False, wire=None):
     from tony_amd.parallel.ps import ParameterServer
 
     _init(rank, world, port)
     model = _mlp(seed=rank)
     ps = ParameterServer(model, optimizer="sgd", lr=0.1, momentum=0.9, mode=mode, sync=sync, dtype=torch.float32,
-                         ps_ranks=(0,))
+                         ps_ranks=ps_ranks, bucket_mb=bucket_mb, wire_dtype=wire)
+    ps.engine.log = []
+    overlapped = []
     if mode == "dedicated" and not sync and ps.is_ps:
         ps.serve_async(total_pushes=steps * (world - 1))
     else:
         for _ in range(steps):
             if ps.is_worker:
                 ps.zero_grad()
+                if overlap:
+                    ps.begin_step(overlap=True)  # buckets launch from the AccumulateGrad hooks
                 x, y = _batch(rank)
                 torch.nn.functional.cross_entropy(model(x), y).backward()
+                overlapped.append(ps.overlapped_buckets)
             ps.step()
     dist.barrier()
-    out = {"data": ps.flat.data.clone(), "is_ps": ps.is_ps}
+    out = {"data": ps.flat.data.clone(), "is_ps": ps.is_ps, "n_buckets": len(ps.buckets), "log": ps.engine.log,
+           "overlapped": overlapped, "slots": [(s.offset, s.numel) for s in ps.flat.slots],
+           "sd": ps.state_dict()}
     dist.destroy_process_group()
     return out
 

@@ -1,0 +1,83 @@
+"""Rank body for tests/test_overlap_gpu.py: 2 processes share the box's one GPU over gloo and train
+a fused Inception block through the bucketed, backward-overlapped PS and DDP data planes."""
+import os
+import traceback
+
+import torch
+import torch.distributed as dist
+
+
+def _model(kind, dev):
+    from torch import nn
+
+    from tony_amd.models import inception_v3 as iv3
+    from tony_amd.models.layers import init_weights
+    from tony_amd.ops.pool import global_avg_pool
+
+    class Net(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.block = {"A": lambda: iv3.InceptionA(64, 32), "C": lambda: iv3.InceptionC(64, 32)}[kind]()
+            self.fc = nn.Linear(self.block.out_channels, 10)
+
+        def forward(self, x):
+            return self.fc(global_avg_pool(self.block(x)))
+
+    return init_weights(Net(), seed=0).to(dev).to(memory_format=torch.channels_last).train()
+
+
+def _data(rank, kind, dev):
+    hw = {"A": 35, "C": 17}[kind]
+    g = torch.Generator(device=dev).manual_seed(11 + rank)
+    x = torch.randn((8, 64, hw, hw), generator=g, device=dev).to(torch.bfloat16)
+    return x.contiguous(memory_format=torch.channels_last), torch.randint(0, 10, (8,), generator=g, device=dev)
+
+
+def ps_run(rank, kind, overlap, bucket_mb, steps=3):
+    from tony_amd.ops import cross_entropy
+    from tony_amd.parallel.ps import ParameterServer
+    from tony_amd.parallel.trainer import Trainer
+
+    dev = torch.device("cuda", 0)
+    model = _model(kind, dev)
+    ps = ParameterServer(model, optimizer="sgd", lr=0.05, momentum=0.9, device=dev, bucket_mb=bucket_mb)
+    tr = Trainer(model, ps, lambda o, y: cross_entropy(o, y), overlap_comm=overlap)
+    x, y = _data(rank, kind, dev)
+    for s in range(steps):
+        if s == steps - 1:
+            ps.engine.log = []
+        tr.step(x, y)
+    torch.cuda.synchronize()
+    return {"params": ps.flat.data.float().cpu(), "log": ps.engine.log, "n_buckets": len(ps.buckets),
+            "overlapped": ps.overlapped_buckets}
+
+
+def ddp_run(rank, kind, bucket_mb):
+    from tony_amd.ops import cross_entropy
+    from tony_amd.parallel.ddp import DistributedDataParallel
+
+    dev = torch.device("cuda", 0)
+    model = _model(kind, dev)
+    for p in model.parameters():
+        p.data = p.data.to(torch.bfloat16)
+    ddp = DistributedDataParallel(model, bucket_mb=bucket_mb, device=dev)
+    x, y = _data(rank, kind, dev)
+    ddp.zero_grad()
+    cross_entropy(ddp(x), y).backward()
+    torch.cuda.synchronize()
+    return {"grad": ddp.flat.grad.float().cpu(), "n_buckets": len(ddp.reducer.buckets),
+            "overlapped": ddp.reducer.overlapped_buckets, "launches": ddp.reducer.launches}
+
+
+def run(rank, world, port, q, kind, bucket_mb):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        out = {"ps_overlap": ps_run(rank, kind, True, bucket_mb), "ps_serial": ps_run(rank, kind, False, bucket_mb),
+               "ddp": ddp_run(rank, kind, bucket_mb)}
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, out))
+    except Exception:  # noqa: BLE001 - reported to the parent
+        q.put((rank, {"error": traceback.format_exc()}))

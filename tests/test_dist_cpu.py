@@ -96,21 +96,60 @@ def _ps_reference(workers, steps, lr=0.1, mu=0.9):
     return model
 
 
-@pytest.mark.parametrize("mode,world,workers", [("colocated", 2, [0, 1]), ("dedicated", 3, [1, 2])])
-def test_parameter_server_sync(mode, world, workers):
+@pytest.mark.parametrize("mode,world,workers,bucket_mb,ps_ranks,overlap", [
+    ("colocated", 2, [0, 1], 32, (0,), False),
+    ("colocated", 3, [0, 1, 2], 0.0003, (0,), True),       # several buckets, 3-way split, launched in backward
+    ("dedicated", 3, [1, 2], 32, (0,), False),
+    ("dedicated", 4, [2, 3], 0.0003, (0, 1), True),        # 2 ps tasks own alternate buckets
+])
+def test_parameter_server_sync(mode, world, workers, bucket_mb, ps_ranks, overlap):
     port, steps = _port(), 3
-    outs = _run(W.ps_rank, [(r, world, port, mode, True, steps) for r in range(world)])
+    outs = _run(W.ps_rank, [(r, world, port, mode, True, steps, bucket_mb, ps_ranks, overlap)
+                            for r in range(world)])
     ref = _ps_reference(workers, steps)
-    flat = torch.cat([p.detach().reshape(-1) for p in ref.parameters()])
     for o in outs:
         got = o["data"]
         # compare parameter values at each slot (flat buffer is padded per tensor)
-        off, k = 0, 0
-        for p in ref.parameters():
-            n = p.numel()
-            torch.testing.assert_close(got[off:off + n], flat[k:k + n], rtol=1e-4, atol=1e-5)
-            off += (n + 63) // 64 * 64
-            k += n
+        for (off, n), p in zip(o["slots"], ref.parameters()):
+            torch.testing.assert_close(got[off:off + n], p.detach().reshape(-1), rtol=1e-4, atol=1e-5)
+    if bucket_mb < 0.001:
+        assert outs[0]["n_buckets"] > 1
+    if overlap:
+        for o, r in zip(outs, range(world)):
+            if r in workers:
+                # every bucket but the last (the first layer's) went out while backward was still running
+                assert all(k >= o["n_buckets"] - 1 for k in o["overlapped"]), o["overlapped"]
+                launches = [e for e in o["log"] if e.startswith("launch:")]
+                assert launches[:o["n_buckets"]] == [f"launch:{i}" for i in range(o["n_buckets"])]
+                first_launch = o["log"].index("launch:0")
+                assert any(e.startswith("ready:") for e in o["log"][first_launch:o["log"].index("launch:1")]) \
+                    if o["n_buckets"] > 1 else True
+
+
+def test_bucket_engine_order_and_double_report():
+    from tony_amd.parallel.buckets import GradBucketEngine, make_buckets
+    from tony_amd.parallel.flat import FlatParams
+
+    model = torch.nn.Sequential(torch.nn.Linear(8, 8), torch.nn.Linear(8, 8), torch.nn.Linear(8, 8))
+    flat = FlatParams(model, dtype=torch.float32)
+    buckets = make_buckets(flat, bucket_mb=64 * 4 / 2 ** 20 * 1.5)   # ~1.5 padded params per bucket
+    assert [b.index for b in buckets] == list(range(len(buckets))) and len(buckets) >= 3
+    assert buckets[0].hi == flat.numel and buckets[-1].lo == 0
+    covered = sorted(i for b in buckets for i in b.params)
+    assert covered == list(range(len(flat.slots)))
+    seen = []
+    eng = GradBucketEngine(flat, buckets, lambda b: seen.append(b.index))
+    eng.begin(overlap=True)
+    params = flat.params
+    # report the FIRST layer's parameters first: nothing may launch before bucket 0 is complete
+    eng.ready(params[:2])
+    assert seen == []
+    eng.ready(params[2:])
+    assert seen == list(range(len(buckets)))
+    with pytest.raises(RuntimeError, match="written again"):
+        eng.ready(params[-1:])
+    eng.end()
+    assert eng.launches == len(buckets)
 
 
 def test_parameter_server_async_applies_every_push():

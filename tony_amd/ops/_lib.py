@@ -14,6 +14,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import weakref
 
 import torch  # noqa: F401  (must precede the dlopen below)
 
@@ -223,6 +224,36 @@ def grad_slot(param):
     if not (g.is_contiguous() or (g.dim() == 4 and g.is_contiguous(memory_format=torch.channels_last))):
         return None
     return g
+
+
+_GRAD_LISTENERS: "weakref.WeakSet" = weakref.WeakSet()
+
+
+def add_grad_listener(listener) -> None:
+    """Register an object whose ``ready(params)`` is told when fused ops finish writing gradients
+    in place (the gradient-bucket engines of tony_amd.parallel.buckets); held weakly."""
+    _GRAD_LISTENERS.add(listener)
+
+
+def remove_grad_listener(listener) -> None:
+    _GRAD_LISTENERS.discard(listener)
+
+
+def grads_ready(*params) -> None:
+    """Called by a fused op's backward, after its last kernel is enqueued, for every parameter whose
+    gradient it accumulated in place (those never reach AccumulateGrad or its hooks)."""
+    if _GRAD_LISTENERS:
+        ps = [p for p in params if p is not None]
+        for lst in list(_GRAD_LISTENERS):
+            lst.ready(ps)
+
+
+def report_inplace(params, returned) -> None:
+    """``grads_ready`` for the trainable ``params`` whose gradient a backward node returned as None,
+    i.e. accumulated in place into the flat gradient buffer."""
+    if _GRAD_LISTENERS:
+        grads_ready(*[p for p, g in zip(params, returned)
+                      if g is None and isinstance(p, torch.nn.Parameter) and p.requires_grad])
 
 
 def ptr(t) -> int:

@@ -112,6 +112,7 @@ class _BNActFn(torch.autograd.Function):
         _lib.check(rc, "tony_bn_bwd")
         if inplace:
             dw = db = None  # already added into param.grad
+        _lib.report_inplace(ctx.params, (dw, db))
         return dx, dw, db, None, None, None, None, None, None
 
 

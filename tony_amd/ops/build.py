@@ -116,6 +116,11 @@ def build_native(verbose: bool = False, force: bool = False) -> str:
             f"-I{ROCM}/include", "-ldl", "-lpthread",
         ]
         _run(cmd, verbose)
+    # stand-alone helper executables (no Python between fork and exec in the task agent)
+    for src in sorted(glob.glob(os.path.join(ndir, "launcher", "*.cpp"))):
+        exe = os.path.join(ndir, os.path.splitext(os.path.basename(src))[0])
+        if force or _newer(exe, [src]):
+            _run(["g++", "-O2", "-std=c++17", "-Wall", "-o", exe, src], verbose)
     return NATIVE_SO
 
 

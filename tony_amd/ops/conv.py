@@ -317,6 +317,7 @@ class _ConvFn(torch.autograd.Function):
     def forward(ctx, x, weight, stride, padding):
         y = _fwd(x, weight, stride, padding, None)
         ctx.save_for_backward(x, weight)
+        ctx.params = (weight,)
         ctx.stride, ctx.padding = stride, padding
         return y
 
@@ -327,6 +328,7 @@ class _ConvFn(torch.autograd.Function):
         dw = _wgrad(dy, x, weight, ctx.stride, ctx.padding)  # first: overlaps the dgrad on the side stream
         dx = _dgrad(dy, weight, x.shape, ctx.stride, ctx.padding) if ctx.needs_input_grad[0] else None
         streams.keep(dx)  # may be consumed on another (branch) stream
+        _lib.report_inplace(ctx.params, (dw,))
         return dx, dw, None, None
 
 
@@ -403,6 +405,7 @@ def _conv_bn_backward(ctx, x, weight, gamma, beta, mean, invstd, Z, dy):
     streams.keep(dx)  # may be consumed on another (branch) stream
     if inplace:
         dgamma = dbeta = None
+    _lib.report_inplace(ctx.params, (dw, dgamma, dbeta))  # after the dgrad: the bucket may now be applied
     return dx, dw, dgamma, dbeta
 
 

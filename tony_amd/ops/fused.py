@@ -182,6 +182,7 @@ class _HeadFn(torch.autograd.Function):
                                   tune.gemm_flags(dZ, wt, dx, M, cin, ctot, ctot, False), 0, 0, stream)
             _lib.check(rc, "tony_gemm_bf16")
         if inplace:
+            _lib.report_inplace(ctx.params, (None, None, None))
             return dx, None, None, None, None, None, None, None, None, None, None, None
         dw32 = wgrad_tn(dZ.data_ptr(), ctot, x.data_ptr(), ldx, M, ctot, cin, dev)
         dw = dw32.to(weight.dtype).reshape(weight.shape)

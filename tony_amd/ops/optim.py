@@ -47,6 +47,22 @@ class _FlatOptimizer:
         self._hp_dev.copy_(torch.tensor(vals, dtype=torch.float32), non_blocking=True)
         self._hp_last = vals
 
+    def begin_step(self):
+        """Advance the step counter and push this step's hyper-parameters (before any apply_range)."""
+        self.step_count += 1
+        if self.w.is_cuda:
+            self._push_hp()
+
+    def apply_range(self, grad: torch.Tensor, lo: int = 0, out_bf16: torch.Tensor | None = None):
+        raise NotImplementedError
+
+    def step(self, grad: torch.Tensor, out_bf16: torch.Tensor | None = None):
+        """One whole-shard update: ``begin_step`` + ``apply_range`` over every element."""
+        if grad.numel() != self.w.numel():
+            raise ValueError("grad / shard size mismatch")
+        self.begin_step()
+        self.apply_range(grad, 0, out_bf16)
+
     def state_dict(self):
         raise NotImplementedError
 
@@ -65,23 +81,25 @@ class FlatSGD(_FlatOptimizer):
     def _hp_values(self):
         return [self.lr, self.momentum, self.weight_decay, self.grad_scale, 1.0 if self.nesterov else 0.0]
 
-    def step(self, grad: torch.Tensor, out_bf16: torch.Tensor | None = None):
-        self.step_count += 1
-        if grad.numel() != self.w.numel():
-            raise ValueError("grad / shard size mismatch")
+    def apply_range(self, grad: torch.Tensor, lo: int = 0, out_bf16: torch.Tensor | None = None):
+        """Update master elements [lo, lo + grad.numel()) (one bucket of a sharded PS) with ``grad``;
+        hyper-parameters are those pushed by the last ``begin_step``."""
+        n = grad.numel()
+        if lo < 0 or lo + n > self.w.numel() or lo % 4 or n % 4:
+            raise ValueError(f"range [{lo}, {lo + n}) outside the {self.w.numel()}-element shard or not 4-aligned")
         if self.w.is_cuda:
-            self._push_hp()
-            rc = _lib.lib().tony_sgd_step(self.w.data_ptr(), self.v.data_ptr(), grad.data_ptr(),
-                                          int(grad.dtype == torch.bfloat16), _lib.ptr(out_bf16), self.w.numel(),
+            rc = _lib.lib().tony_sgd_step(self.w.data_ptr() + 4 * lo, self.v.data_ptr() + 4 * lo, grad.data_ptr(),
+                                          int(grad.dtype == torch.bfloat16), _lib.ptr(out_bf16), n,
                                           self._hp_dev.data_ptr(), _lib.stream_ptr(self.w.device))
             _lib.check(rc, "tony_sgd_step")
             return
-        g = grad.float() * self.grad_scale + self.weight_decay * self.w
-        self.v.mul_(self.momentum).add_(g)
-        upd = g + self.momentum * self.v if self.nesterov else self.v
-        self.w.add_(upd, alpha=-self.lr)
+        w, v = self.w[lo:lo + n], self.v[lo:lo + n]
+        g = grad.float() * self.grad_scale + self.weight_decay * w
+        v.mul_(self.momentum).add_(g)
+        upd = g + self.momentum * v if self.nesterov else v
+        w.add_(upd, alpha=-self.lr)
         if out_bf16 is not None:
-            out_bf16.copy_(self.w)
+            out_bf16.copy_(w)
 
     def state_dict(self):
         return {"kind": "sgd", "step": self.step_count, "momentum_buffer": self.v, "lr": self.lr}
@@ -110,27 +128,30 @@ class FlatAdam(_FlatOptimizer):
         return [self.lr, self.b1, self.b2, self.eps, self.weight_decay, self.grad_scale,
                 1.0 - self.b1 ** t, 1.0 - self.b2 ** t, 1.0 if self.decoupled else 0.0]
 
-    def step(self, grad: torch.Tensor, out_bf16: torch.Tensor | None = None):
-        self.step_count += 1
+    def apply_range(self, grad: torch.Tensor, lo: int = 0, out_bf16: torch.Tensor | None = None):
+        n = grad.numel()
+        if lo < 0 or lo + n > self.w.numel() or lo % 4 or n % 4:
+            raise ValueError(f"range [{lo}, {lo + n}) outside the {self.w.numel()}-element shard or not 4-aligned")
         if self.w.is_cuda:
-            self._push_hp()
-            rc = _lib.lib().tony_adam_step(self.w.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), grad.data_ptr(),
-                                           int(grad.dtype == torch.bfloat16), _lib.ptr(out_bf16), self.w.numel(),
+            rc = _lib.lib().tony_adam_step(self.w.data_ptr() + 4 * lo, self.m.data_ptr() + 4 * lo,
+                                           self.v.data_ptr() + 4 * lo, grad.data_ptr(),
+                                           int(grad.dtype == torch.bfloat16), _lib.ptr(out_bf16), n,
                                            self._hp_dev.data_ptr(), _lib.stream_ptr(self.w.device))
             _lib.check(rc, "tony_adam_step")
             return
         t = self.step_count
+        w, m, v = self.w[lo:lo + n], self.m[lo:lo + n], self.v[lo:lo + n]
         g = grad.float() * self.grad_scale
         if self.decoupled:
-            self.w.mul_(1.0 - self.lr * self.weight_decay)
+            w.mul_(1.0 - self.lr * self.weight_decay)
         else:
-            g = g + self.weight_decay * self.w
-        self.m.mul_(self.b1).add_(g, alpha=1 - self.b1)
-        self.v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
-        denom = (self.v.sqrt() / (1 - self.b2 ** t) ** 0.5).add_(self.eps)
-        self.w.addcdiv_(self.m, denom, value=-self.lr / (1 - self.b1 ** t))
+            g = g + self.weight_decay * w
+        m.mul_(self.b1).add_(g, alpha=1 - self.b1)
+        v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+        denom = (v.sqrt() / (1 - self.b2 ** t) ** 0.5).add_(self.eps)
+        w.addcdiv_(m, denom, value=-self.lr / (1 - self.b1 ** t))
         if out_bf16 is not None:
-            out_bf16.copy_(self.w)
+            out_bf16.copy_(w)
 
     def state_dict(self):
         return {"kind": "adam", "step": self.step_count, "exp_avg": self.m, "exp_avg_sq": self.v, "lr": self.lr}

@@ -95,6 +95,7 @@ class _BNAddReLUFn(torch.autograd.Function):
         M, C, ldz = _rows_view(z)
         dz, dres, (dg, db) = _bwd_res(L, z, ldz, dy, y, M, C, mean, invstd, gamma, beta, ctx.pb, ctx.params,
                                       _lib.stream_ptr(z.device))
+        _lib.report_inplace(ctx.params, (dg, db))
         return dz, dres, dg, db, None, None, None, None, None
 
 
@@ -151,6 +152,7 @@ class _Conv1x1BNAddReLUFn(torch.autograd.Function):
         if gw is None or dg is not None:
             dw = wgrad_tn(dZ.data_ptr(), cout, x.data_ptr(), ldx, M, cout, cin, dev).to(weight.dtype)
             dw = dw.reshape(weight.shape)
+        _lib.report_inplace(ctx.params, (dw, dg, db))
         return dx, dw, dres, dg, db, None, None, None, None, None
 
 

@@ -177,6 +177,21 @@ def run(fn: Callable[[], object], *keep: torch.Tensor):
     return None
 
 
+def fence_into(stream: torch.cuda.Stream) -> None:
+    """Make ``stream`` wait for everything issued so far on the weight-gradient side stream and the
+    branch streams (deferred work is issued first), without making the compute streams wait."""
+    side = _active[0]
+    if side is None:
+        return
+    _flush(side)
+    for s in [side, *_used.values()]:
+        if s is stream:
+            continue
+        ev = _fork_event(s.device_index)
+        ev.record(s)
+        stream.wait_event(ev)
+
+
 def end() -> int:
     """Issue the deferred work, join the side stream into the current stream and release the kept
     operands; returns how many ops ran on the side stream this step."""

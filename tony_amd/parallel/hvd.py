@@ -340,6 +340,15 @@ class _DistributedOptimizer:
         self.optimizer = optimizer
         self.backward_passes_per_step = int(backward_passes_per_step)
         params = [p for g in optimizer.param_groups for p in g["params"] if p.requires_grad]
+        if named_parameters is not None:  # Horovod's check: names must cover every optimized parameter
+            named = list(named_parameters)
+            names = [n for n, _ in named]
+            if len(set(names)) != len(names):
+                raise ValueError("named_parameters has duplicate names")
+            known = {id(p) for _, p in named}
+            missing = [i for i, p in enumerate(params) if id(p) not in known]
+            if missing:
+                raise ValueError(f"named_parameters does not cover {len(missing)} optimizer parameter(s)")
         by_dtype: Dict[torch.dtype, List[torch.nn.Parameter]] = {}
         for p in params:
             by_dtype.setdefault(p.dtype, []).append(p)
@@ -351,7 +360,8 @@ class _DistributedOptimizer:
             flat = FlatParams(m, dtype=dt, world=1)
             if _state["size"] > 1:
                 dist.broadcast(flat.data, 0)
-            red = BucketedAllReduce(flat, bucket_mb, average=(op is Average), compression=compression.dtype)
+            red = BucketedAllReduce(flat, bucket_mb, average=(op is Average), compression=compression.dtype,
+                                    predivide=gradient_predivide_factor if op is Average else 1.0)
             red.passes_per_reduce = self.backward_passes_per_step
             red.register_hooks()
             self.groups.append((flat, red))

@@ -4,36 +4,47 @@ TonY runs TF PS jobs as ``ps`` + ``worker`` tasks wired together by ``TF_CONFIG`
 (reference: ``T/runtime/TFRuntime.java:45-59``, ``EX/mnist-tensorflow/mnist_distributed.py:206-241``):
 the ``ps`` tasks hold the variables and apply the optimizer; workers pull the
 variables, compute gradients and push them back.  TF itself is not part of this
-stack, so this module implements those semantics directly on HBM and xGMI:
+stack, so this module implements those semantics directly on HBM and xGMI.
+
+Every gradient exchange is BUCKETED and OVERLAPPED with backward (parallel/buckets.py): the flat
+gradient buffer is cut into ~8 MB buckets in reverse layer order; as soon as the last gradient of
+a bucket is written (reported by the fused HIP ops or AccumulateGrad) the bucket's push, apply and
+pull are enqueued on a communication stream while backward keeps running on the compute streams.
+Only the last bucket (the stem's gradients) is exposed after backward.
 
 ``mode="colocated"`` (default, the benchmark topology)
-    One PS shard per GPU process.  Variables are partitioned over the shards
-    (contiguous ranges of the flat buffer: TF's ``replica_device_setter``
-    round-robin with a byte-balanced split).  A step is:
-    push  = ``reduce_scatter`` of the flat bf16 gradient (each shard receives
-            the sum of its range from every worker, over all 7 xGMI links);
-    apply = ONE fused HIP optimizer launch over the shard's fp32 master copy,
-            which also emits the bf16 copy;
-    pull  = ``all_gather`` of the bf16 shards into every worker's flat params.
+    One PS shard per GPU process.  Each bucket is split evenly over the shards (rank r owns the
+    r-th piece of every bucket: TF's ``replica_device_setter`` spreads variables over ps tasks, here
+    balanced to the byte).  Per bucket:
+    push  = ``reduce_scatter`` of the bucket (each shard receives the sum of its piece from every
+            worker over all 7 xGMI links);
+    apply = one fused HIP optimizer launch over the piece of the shard's fp32 master copy, writing
+            the new bf16 variables straight into this rank's piece of the flat parameter buffer;
+    pull  = in-place ``all_gather`` of the bucket's pieces into every worker's flat parameters.
 ``mode="dedicated"``
-    The paper topology (1 ps + N workers).  PS ranks own the variables and run
-    no model; workers push with ``reduce`` to the owning PS and pull with
-    ``broadcast``.  ``sync=False`` gives TF's default *asynchronous* PS: each
-    worker's push is applied on arrival (point-to-point send/recv, PS polls
-    the outstanding receives) and the worker pulls the post-apply variables.
+    The paper topology (1 ps + N workers).  PS ranks own the variables and run no model; bucket b
+    belongs to ps task ``b % n_ps`` (round-robin placement, ``replica_device_setter``).  Per
+    bucket: push = ``reduce`` of the bucket to its owner, apply on the owner, pull = ``broadcast``
+    from the owner.  ``sync=False`` gives TF's default *asynchronous* PS: each worker's push is
+    applied on arrival (point-to-point send/recv, the PS polls the outstanding receives) and the
+    worker pulls the post-apply variables.
 
-Gradients are averaged over workers (TF SyncReplicasOptimizer semantics) by the
-optimizer's ``grad_scale``.
+Gradients are averaged over workers (TF SyncReplicasOptimizer semantics) by the optimizer's
+``grad_scale``.  ``wire_dtype=torch.float32`` pushes and sums fp32 gradients (the reference TF job
+is fp32 end to end) even when the gradient buffer the kernels accumulate into is bf16.
 """
 from __future__ import annotations
 
+import math
 import time
+from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
 
 from ..ops.optim import FlatAdam, FlatSGD
 from . import collectives as coll
+from .buckets import DEFAULT_BUCKET_MB, Bucket, GradBucketEngine, make_buckets
 from .flat import FlatParams
 
 
@@ -48,12 +59,19 @@ def make_optimizer(kind: str, master: torch.Tensor, lr: float, momentum: float =
     raise ValueError(f"unknown optimizer {kind!r}")
 
 
+def _wait(work) -> None:
+    """Make the current stream wait for an async collective (no host block on RCCL)."""
+    if work is not None:
+        work.wait()
+
+
 class ParameterServer:
-    """Owns the variables of a model (sharded or dedicated) and runs push/apply/pull."""
+    """Owns the variables of a model (sharded or dedicated) and runs bucketed push/apply/pull."""
 
     def __init__(self, model: torch.nn.Module, optimizer: str = "sgd", lr: float = 0.1, momentum: float = 0.9,
                  weight_decay: float = 0.0, mode: str = "colocated", sync: bool = True, ps_ranks=(0,),
-                 group=None, dtype=torch.bfloat16, device=None, **opt_kw):
+                 group=None, dtype=torch.bfloat16, device=None, wire_dtype: Optional[torch.dtype] = None,
+                 bucket_mb: float = DEFAULT_BUCKET_MB, **opt_kw):
         self.mode = mode
         self.sync = sync
         self.group = group
@@ -73,19 +91,54 @@ class ParameterServer:
             raise ValueError(f"unknown PS mode {mode!r}")
         self.is_ps = self.rank in self.ps_ranks
         self.is_worker = self.rank in self.worker_ranks
-        n_shards = len(self.ps_ranks)
-        self.flat = FlatParams(model, dtype=dtype, device=device, world=n_shards)
-        # every rank starts from PS shard 0's init: broadcast rank 0's variables
+        n_split = self.world if mode == "colocated" else 1
+        # every bucket must split into n_split pieces of whole 16-byte vectors (8 bf16)
+        align = 64 * (8 * n_split) // math.gcd(64, 8 * n_split)
+        self.flat = FlatParams(model, dtype=dtype, device=device, world=n_split, align=align)
+        self.wire_dtype = wire_dtype or self.flat.grad.dtype
+        # every rank starts from rank 0's variables
         coll.broadcast(self.flat.data, src=0, group=group)
-        self.optimizers = {}
-        for i, r in enumerate(self.ps_ranks):
-            if r == self.rank:
-                master = self.flat.shard(self.flat.data, i).float().clone()
-                opt = make_optimizer(optimizer, master, lr, momentum, weight_decay, **opt_kw)
-                opt.grad_scale = 1.0 / len(self.worker_ranks)
-                self.optimizers[i] = opt
+        self.buckets: List[Bucket] = make_buckets(self.flat, bucket_mb, multiple=8 * n_split)
         self.steps = 0
         self.push_bytes = 0
+        self.optimizers: Dict[int, object] = {}
+        # per bucket: (offset into this rank's master shard, length) -- None where this rank owns nothing
+        self._master_range: List[Optional[tuple]] = [None] * len(self.buckets)
+        f = self.flat
+        if mode == "colocated":
+            pieces, m = [], 0
+            for b in self.buckets:
+                p = b.numel // n_split
+                self._master_range[b.index] = (m, p)
+                pieces.append(f.data[b.lo + self.rank * p:b.lo + (self.rank + 1) * p])
+                m += p
+            master = torch.cat(pieces).float()
+            opt = make_optimizer(optimizer, master, lr, momentum, weight_decay, **opt_kw)
+            opt.grad_scale = 1.0 / len(self.worker_ranks)
+            self.optimizers[self.rank] = opt
+            self._gshard = torch.zeros(m, dtype=self.wire_dtype, device=f.device) if self.world > 1 else None
+        elif sync:
+            m, pieces = 0, []
+            for b in self.buckets:
+                if self._owner(b) == self.rank:
+                    self._master_range[b.index] = (m, b.numel)
+                    pieces.append(f.data[b.lo:b.hi])
+                    m += b.numel
+            if pieces:
+                master = torch.cat(pieces).float()
+                opt = make_optimizer(optimizer, master, lr, momentum, weight_decay, **opt_kw)
+                opt.grad_scale = 1.0 / len(self.worker_ranks)
+                self.optimizers[self.rank] = opt
+        else:  # asynchronous: the single ps task owns the whole buffer
+            if self.is_ps:
+                opt = make_optimizer(optimizer, f.data.float().clone(), lr, momentum, weight_decay, **opt_kw)
+                self.optimizers[self.rank] = opt
+        self._wire = None
+        if self.world > 1 and self.wire_dtype != f.grad.dtype:
+            self._wire = torch.zeros(f.numel, dtype=self.wire_dtype, device=f.device)
+        self.engine = GradBucketEngine(f, self.buckets, self._launch)
+        if mode == "colocated" or sync:
+            self.engine.attach()
 
     # -- helpers ---------------------------------------------------------------
     def zero_grad(self):
@@ -95,39 +148,83 @@ class ParameterServer:
     def params(self):
         return self.flat.params
 
-    def _shard_index(self) -> int:
-        return self.ps_ranks.index(self.rank)
+    def _owner(self, b: Bucket) -> int:
+        return self.ps_ranks[b.index % len(self.ps_ranks)]
+
+    @property
+    def comm_stream(self):
+        return self.engine.comm
 
     # -- the PS step -----------------------------------------------------------
+    def begin_step(self, overlap: bool = True):
+        """Arm the bucket engine before the forward: with ``overlap`` each bucket's push/apply/pull is
+        enqueued as soon as backward completes its gradients."""
+        if self.mode == "dedicated" and not self.sync:
+            return
+        for opt in self.optimizers.values():
+            opt.begin_step()
+        if self.mode == "dedicated" and not self.is_worker:
+            self.flat.grad.zero_()  # a PS-only rank contributes nothing to the pushed sums
+            overlap = False         # and runs no backward: all buckets go in order from step()
+        self.engine.begin(overlap)
+
     def step(self):
-        """push (gradients) -> apply (fused optimizer on the PS) -> pull (variables)."""
-        if self.mode == "colocated":
-            self._step_colocated()
-        elif self.sync:
-            self._step_dedicated_sync()
-        else:
+        """Finish push (gradients) -> apply (fused optimizer on the PS) -> pull (variables)."""
+        if self.mode == "dedicated" and not self.sync:
             self._step_dedicated_async_worker()
+            self.steps += 1
+            return
+        if not self.engine.armed:
+            self.begin_step(overlap=False)
+        self.engine.end()
         self.steps += 1
 
-    def _step_colocated(self):
-        f = self.flat
-        i = self._shard_index()
-        g_shard = f.shard(f.grad, i)
-        coll.reduce_scatter_flat(g_shard, f.grad, group=self.group)       # push
-        self.optimizers[i].step(g_shard, out_bf16=f.shard(f.data, i))       # apply (HIP)
-        coll.all_gather_flat(f.data, f.shard(f.data, i), group=self.group)  # pull
-        self.push_bytes += f.grad.numel() * f.grad.element_size()
+    @property
+    def overlapped_buckets(self) -> int:
+        """Buckets of the last step whose communication was issued while backward was running."""
+        return self.engine.launched_during_backward
 
-    def _step_dedicated_sync(self):
+    def _wire_grad(self, b: Bucket) -> torch.Tensor:
+        g = self.flat.grad[b.lo:b.hi]
+        if self._wire is not None:
+            w = self._wire[b.lo:b.hi]
+            w.copy_(g)
+            return w
+        return g
+
+    def _launch(self, b: Bucket):
+        """Enqueue bucket b's push / apply / pull (the communication stream is current)."""
         f = self.flat
-        for i, ps in enumerate(self.ps_ranks):
-            g = f.shard(f.grad, i)
-            if self.is_ps and not self.is_worker:
-                g.zero_()  # PS contributes nothing to the gradient sum
-            dist.reduce(g, dst=ps, group=self.group)                          # push
-            if self.rank == ps:
-                self.optimizers[i].step(g, out_bf16=f.shard(f.data, i))       # apply
-            dist.broadcast(f.shard(f.data, i), src=ps, group=self.group)      # pull
+        opt = self.optimizers.get(self.rank)
+        if self.mode == "colocated":
+            m, p = self._master_range[b.index]
+            own = f.data[b.lo + self.rank * p:b.lo + (self.rank + 1) * p]
+            if self.world == 1:
+                self._apply(opt, f.grad[b.lo:b.hi], m, own)
+                return
+            g = self._wire_grad(b)
+            gs = self._gshard[m:m + p]
+            _wait(coll.reduce_scatter_flat(gs, g, group=self.group, async_op=True))     # push
+            self._apply(opt, gs, m, own)                                                  # apply (HIP)
+            _wait(coll.all_gather_flat(f.data[b.lo:b.hi], own, group=self.group, async_op=True))  # pull
+            self.push_bytes += g.numel() * g.element_size()
+            return
+        owner = self._owner(b)
+        g = self._wire_grad(b)
+        _wait(dist.reduce(g, dst=owner, group=self.group, async_op=True))                # push
+        if self.rank == owner:
+            m, _ = self._master_range[b.index]
+            self._apply(opt, g, m, f.data[b.lo:b.hi])                                     # apply
+        _wait(dist.broadcast(f.data[b.lo:b.hi], src=owner, group=self.group, async_op=True))  # pull
+        if self.is_worker:
+            self.push_bytes += g.numel() * g.element_size()
+
+    def _apply(self, opt, grad: torch.Tensor, m: int, out: torch.Tensor):
+        if out.dtype == torch.bfloat16 or not out.is_cuda:
+            opt.apply_range(grad, m, out_bf16=out)
+        else:  # fp32 variables (reference-precision runs): the master range IS the new value
+            opt.apply_range(grad, m, out_bf16=None)
+            out.copy_(opt.w[m:m + out.numel()])
 
     def _step_dedicated_async_worker(self):
         f = self.flat
@@ -140,7 +237,7 @@ class ParameterServer:
         if not self.is_ps or self.sync or self.mode != "dedicated":
             raise RuntimeError("serve_async runs on the ps rank of an async dedicated PS")
         f = self.flat
-        opt = self.optimizers[0]
+        opt = self.optimizers[self.rank]
         opt.grad_scale = 1.0  # async: every push is applied on its own
         if total_pushes % len(self.worker_ranks):
             raise ValueError("total_pushes must be steps x number of workers")
@@ -150,7 +247,8 @@ class ParameterServer:
             buf = torch.empty_like(f.grad)
             for done in range(total_pushes):
                 w = dist.recv(buf, group=self.group)  # returns the sender's global rank
-                opt.step(buf, out_bf16=f.data)
+                opt.begin_step()
+                self._apply(opt, buf, 0, f.data)
                 dist.send(f.data, dst=w, group=self.group)
             self.steps = total_pushes
             return
@@ -164,7 +262,8 @@ class ParameterServer:
                 if req is None or not req.is_completed():
                     continue
                 req.wait()
-                opt.step(bufs[w], out_bf16=f.data)          # apply on arrival
+                opt.begin_step()
+                self._apply(opt, bufs[w], 0, f.data)        # apply on arrival
                 dist.send(f.data, dst=w, group=self.group)  # the worker's pull
                 done += 1
                 got[w] += 1
@@ -176,16 +275,26 @@ class ParameterServer:
         self.steps = done
 
     # -- checkpoint ------------------------------------------------------------
+    def layout(self) -> dict:
+        """What a shard checkpoint is only valid for (restoring under another layout is refused)."""
+        return {"mode": self.mode, "world": self.world, "ps_ranks": list(self.ps_ranks), "numel": self.flat.numel,
+                "buckets": [(b.lo, b.hi) for b in self.buckets]}
+
     def state_dict(self):
-        sd = {"steps": self.steps, "flat": self.flat.data.detach().clone(), "shards": {}}
-        for i, opt in self.optimizers.items():
-            sd["shards"][i] = {"master": opt.w.detach().clone(), "opt": opt.state_dict()}
+        """This rank's part of the PS state: the bf16/fp32 variables plus the fp32 master and
+        optimizer state of the shard it owns (every rank saves its own file, utils/checkpoint.py)."""
+        sd = {"steps": self.steps, "flat": self.flat.data.detach().clone(), "layout": self.layout(),
+              "rank": self.rank, "shards": {}}
+        for r, opt in self.optimizers.items():
+            sd["shards"][r] = {"master": opt.w.detach().clone(), "opt": opt.state_dict()}
         return sd
 
     def load_state_dict(self, sd):
+        if sd.get("layout") is not None and sd["layout"] != self.layout():
+            raise ValueError(f"PS checkpoint layout {sd['layout']} does not match this job's {self.layout()}")
         self.steps = int(sd["steps"])
         self.flat.data.copy_(sd["flat"])
-        for i, opt in self.optimizers.items():
-            s = sd["shards"][i]
+        for r, opt in self.optimizers.items():
+            s = sd["shards"][r]
             opt.w.copy_(s["master"])
             opt.load_state_dict(s["opt"])

@@ -24,7 +24,7 @@ from .ps import ParameterServer
 class Trainer:
     def __init__(self, model: torch.nn.Module, ps: ParameterServer, loss_fn: Callable, use_graph: bool = False,
                  warmup_eager: int = 3, graph_collectives: bool | None = None, overlap_wgrad: bool = True,
-                 branch_streams: bool = True):
+                 branch_streams: bool = True, overlap_comm: bool = True):
         self.model = model
         self.ps = ps
         self.loss_fn = loss_fn
@@ -36,6 +36,7 @@ class Trainer:
         # (RCCL's graph-capture support differs across releases).  One rank: all in the graph.
         self.graph_collectives = (ps.world == 1) if graph_collectives is None else graph_collectives
         self.overlap_wgrad = overlap_wgrad
+        self.overlap_comm = overlap_comm
         self.branch_streams = branch_streams
         self._tuned = False
         self.side_ops = 0
@@ -57,6 +58,11 @@ class Trainer:
     def _body(self, x, y, ps_step: bool = True):
         t0 = time.perf_counter()
         self.ps.zero_grad()
+        if ps_step:
+            # arm the gradient buckets: each bucket's push/apply/pull is enqueued on the communication
+            # stream as soon as backward has written its gradients (parallel/buckets.py); not in the
+            # first (autotuning) step, whose kernel timings must not race the communication stream
+            self.ps.begin_step(overlap=self.overlap_comm and self._tuned)
         # weight gradients on a second stream, overlapped with the data-gradient chain, and the model's
         # independent branches on branch streams (ops/streams.py); not in the first step, whose
         # autotuning times kernels on the current stream

@@ -323,6 +323,9 @@ def _pdeathsig():  # runs in the child between fork and exec
         pass
 
 
+_PDEATH_HELPER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "native", "tony_pdeath")
+
+
 class ShellProcess:
     """A ``bash -c`` child in its own session/process group."""
 
@@ -340,8 +343,15 @@ class ShellProcess:
             except OSError:
                 LOG.warning("failed to make %s executable", exe)
         self.command = command
-        self.proc = subprocess.Popen(["bash", "-c", command], env=penv, cwd=cwd, stdout=stdout, stderr=stderr,
-                                     start_new_session=True, preexec_fn=_pdeathsig if die_with_parent else None)
+        argv, preexec = ["bash", "-c", command], None
+        if die_with_parent:
+            if os.access(_PDEATH_HELPER, os.X_OK):
+                # native helper: no Python (and no gRPC at-fork handlers) between fork and exec
+                argv = [_PDEATH_HELPER, str(os.getpid())] + argv
+            else:
+                preexec = _pdeathsig
+        self.proc = subprocess.Popen(argv, env=penv, cwd=cwd, stdout=stdout, stderr=stderr,
+                                     start_new_session=True, preexec_fn=preexec)
         self.pid = self.proc.pid
 
     def wait(self, timeout_s: Optional[float] = None) -> int:
