@@ -2,17 +2,30 @@
 """Headline benchmark: Inception-v3 parameter-server training, images/sec (whole node).
 
 BASELINE.json metric: "images/sec (whole node) Inception-v3 TF-PS at 1/2/4/8 MI355X".
-One process per GPU (torch.distributed.run), each process is one TF-PS *worker*
-and hosts one PS shard (colocated sharded PS, tony_amd/parallel/ps.py):
-push = RCCL reduce-scatter of bf16 grads over xGMI, apply = fused HIP SGD-momentum
-on the fp32 master shard, pull = RCCL all-gather of bf16 variables.  Compute is
-bf16 NHWC with the tony_amd HIP kernels (fused BN+ReLU, MFMA 1x1-conv GEMM,
-fused softmax-xent, fused optimizer); the whole step is replayed as a HIP graph.
+One process per GPU (torch.distributed.run, RCCL over xGMI).  Two PS topologies:
 
-Data is synthetic (ImageNet-shaped 299x299x3 images, random labels) and weights
-are random-init -- no network access for datasets / checkpoints.
+``--ps-mode colocated`` (default)
+    every process is one TF-PS *worker* and hosts one PS shard (tony_amd/parallel/ps.py).  The
+    flat gradient is cut into ~8 MB buckets; as backward completes a bucket, its push (RCCL
+    reduce-scatter), apply (fused HIP SGD-momentum on the fp32 master shard) and pull (RCCL
+    all-gather) are enqueued on a communication stream while backward continues
+    (parallel/buckets.py).
+``--ps-mode dedicated``
+    the paper topology: rank 0 is the ps task (owns the fp32 variables, runs no model), ranks
+    1..N-1 are workers; per bucket push = reduce to the ps, apply on the ps, pull = broadcast.
+    Images/sec counts the N-1 workers' images only.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+Compute is bf16 NHWC with the tony_amd HIP kernels (fused BN+ReLU, MFMA implicit-GEMM convs, fused
+heads, fused softmax-xent, fused optimizer); the step is issued eagerly (weight gradients on a side
+stream) or replayed as a HIP graph, whichever measured faster in setup (``--mode auto``).
+``--dtype fp32`` runs the reference-precision row (TF's Inception-v3 PS job is fp32): stock
+PyTorch-ROCm layers (MIOpen / hipBLASLt) in fp32 with fp32 variables and fp32 pushed gradients.
+``--grad-dtype fp32`` keeps bf16 compute but pushes and sums fp32 gradients.
+
+Data is synthetic (ImageNet-shaped 299x299x3 images, random labels) and weights are random-init --
+no network access for datasets / checkpoints.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--ps-mode M] [--dtype D]
        (N>1 is launched by the driver via torch.distributed.run)
 """
 from __future__ import annotations
@@ -37,8 +50,17 @@ def parse():
                     help="graph: replay the step as one HIP graph; eager: launch kernels from Python (weight "
                          "gradients overlap the data-gradient chain on a second stream); auto: time both in setup")
     ap.add_argument("--no-graph", action="store_true", help="same as --mode eager")
+    ap.add_argument("--ps-mode", default="colocated", choices=["colocated", "dedicated"],
+                    help="colocated: one PS shard per GPU; dedicated: rank 0 = the ps task, the rest are workers")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="compute dtype; fp32 = the reference-precision row (stock layers, fp32 variables)")
+    ap.add_argument("--grad-dtype", default=None, choices=["bf16", "fp32"],
+                    help="dtype of the pushed / summed gradients (default: the compute dtype)")
+    ap.add_argument("--bucket-mb", type=float, default=None, help="gradient bucket size (default 8 MB)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="push/apply/pull every bucket after backward instead of during it")
     ap.add_argument("--stock", action="store_true",
-                    help="comparator: stock nn.BatchNorm2d+ReLU / MIOpen 1x1 / torch loss (not the headline)")
+                    help="comparator: stock nn.BatchNorm2d+ReLU / MIOpen convs / torch loss (not the headline)")
     ap.add_argument("--model", default="inception_v3", choices=["inception_v3", "resnet50"])
     ap.add_argument("--optimizer", default="sgd")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps (for rocprof)")
@@ -54,30 +76,89 @@ def parse():
     return ap.parse_args()
 
 
+def fail(msg: str, code: int = 4) -> int:
+    print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+    return code
+
+
+class _PSOnly:
+    """The dedicated ps rank's step: no model, just the bucketed reduce -> apply -> broadcast, issued
+    in the same collective order as the workers' (so the bench loop is identical on every rank)."""
+
+    def __init__(self, ps, dev):
+        self.ps = ps
+        self.use_graph = False
+        self.warmup_eager = 1
+        self.host_fwd_s = self.host_bwd_s = 0.0
+        self.phase_events = None
+        self._zero = torch.zeros((), device=dev)
+
+    def step(self, x, y):  # noqa: ARG002 - the ps runs no model
+        self.ps.begin_step(overlap=False)
+        self.ps.step()
+        return self._zero
+
+    def enable_phase_timing(self):
+        pass
+
+    def phase_ms(self):
+        return (0.0, 0.0, 0.0)
+
+
+def diagnose(world: int, rank: int, dev, backend: str, shared_ok: bool) -> dict:
+    """N>1 self-checks for the driver's scaling run: one distinct GPU per rank over RCCL.  Returns
+    what was found (printed by rank 0); raises SystemExit on a fallback the run must not hide."""
+    info = {"backend": backend, "world_size": dist.get_world_size()}
+    try:
+        info["rccl_version"] = ".".join(str(v) for v in torch.cuda.nccl.version())
+    except Exception:  # noqa: BLE001 - informational
+        info["rccl_version"] = None
+    p = torch.cuda.get_device_properties(dev)
+    me = {"rank": rank, "device": dev.index, "bdf": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+          "uuid": str(getattr(p, "uuid", ""))}
+    allp = [None] * world
+    dist.all_gather_object(allp, me)
+    info["devices"] = [a["bdf"] for a in allp]
+    if len({a["bdf"] for a in allp}) != world and not shared_ok:
+        raise SystemExit(fail(f"ranks share a GPU ({info['devices']}): each rank must own one device"))
+    if backend != "nccl" and not shared_ok:
+        raise SystemExit(fail(f"process group backend is {backend!r}, not RCCL"))
+    return info
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print(f"bench.py: --gpus {args.gpus} must be launched with torch.distributed.run", file=sys.stderr)
-            return 2
+        return fail(f"--gpus {args.gpus} but WORLD_SIZE={world}: N>1 must be launched with torch.distributed.run "
+                    f"--nproc-per-node N", 2)
+    if args.ps_mode == "dedicated" and world < 2:
+        return fail("--ps-mode dedicated needs >= 2 ranks (1 ps + workers)", 2)
     # test hooks for rehearsing the multi-rank path on a one-GPU box: several ranks on one device
     # over gloo (TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0); the driver's runs use RCCL, one GPU per rank
     backend = os.environ.get("TONY_BENCH_BACKEND", "nccl")
+    rehearsal = "TONY_BENCH_BACKEND" in os.environ or "TONY_BENCH_DEVICE" in os.environ
     dev_index = int(os.environ.get("TONY_BENCH_DEVICE", local_rank))
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
+    diag = {}
     if world > 1:
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
+        diag = diagnose(world, rank, dev, dist.get_backend(), rehearsal)
 
-    from tony_amd.ops import cross_entropy
+    from tony_amd.ops import cross_entropy, tune
+    from tony_amd.parallel import collectives as coll
+    from tony_amd.parallel.collectives import max_over_ranks
     from tony_amd.parallel.ps import ParameterServer
     from tony_amd.parallel.trainer import Trainer
 
-    torch.backends.cudnn.benchmark = not args.no_miopen_find  # MIOpen find for the remaining MIOpen convs
-    fused = not args.stock
+    torch.backends.cudnn.benchmark = not args.no_miopen_find  # MIOpen find for the MIOpen convs
+    fp32 = args.dtype == "fp32"
+    dtype = torch.float32 if fp32 else torch.bfloat16
+    grad_dtype = {"bf16": torch.bfloat16, "fp32": torch.float32, None: dtype}[args.grad_dtype]
+    fused = not (args.stock or fp32)  # the tony kernels are bf16; fp32 = stock MIOpen / hipBLASLt layers
     if args.model == "inception_v3":
         from tony_amd.models.inception_v3 import inception_v3
         model = inception_v3(fused=fused, seed=0)
@@ -88,8 +169,11 @@ def main():
         res, aux_w = 224, 0.0
     model = model.to(dev).to(memory_format=torch.channels_last)
     model.train()
+    ps_kw = {} if args.bucket_mb is None else {"bucket_mb": args.bucket_mb}
     ps = ParameterServer(model, optimizer=args.optimizer, lr=0.045 if args.model == "inception_v3" else 0.1,
-                         momentum=0.9, weight_decay=4e-5, mode="colocated", device=dev)
+                         momentum=0.9, weight_decay=4e-5, mode=args.ps_mode, ps_ranks=(0,), dtype=dtype, device=dev,
+                         wire_dtype=grad_dtype, **ps_kw)
+    n_workers = len(ps.worker_ranks)
 
     if fused:
         xent = cross_entropy
@@ -105,26 +189,25 @@ def main():
 
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     x = torch.randn((args.batch, 3, res, res), generator=g, device=dev, dtype=torch.float32)
-    x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x = x.to(dtype).contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 1000, (args.batch,), generator=g, device=dev)
-
-    from tony_amd.parallel.collectives import max_over_ranks
-
-    from tony_amd.ops import tune
 
     tune_loaded = 0
     if args.tune_cache and os.path.exists(args.tune_cache):
         tune_loaded = tune.load(args.tune_cache)
     mode = "eager" if args.no_graph else args.mode
-    trainer = Trainer(model, ps, loss_fn, use_graph=mode != "eager", overlap_wgrad=not args.no_wgrad_stream,
-                      branch_streams=not args.no_branch_streams)
+    if ps.is_worker:
+        trainer = Trainer(model, ps, loss_fn, use_graph=mode != "eager", overlap_wgrad=not args.no_wgrad_stream,
+                          branch_streams=not args.no_branch_streams, overlap_comm=not args.no_overlap)
+    else:
+        trainer = _PSOnly(ps, dev)
     t_w = time.perf_counter()
     setup = {}
     if mode == "auto":
         # Setup (untimed, before the W warmup steps): the first step autotunes every conv / GEMM shape,
-        # then 3 eager steps and 3 graph replays are timed and the faster way of issuing the step is
+        # then eager steps and graph replays are timed and the faster way of issuing the step is
         # kept -- eager launches overlap the weight gradients with the data-gradient chain on a second
-        # stream, which the HIP-graph runtime's own multi-queue scheduling of the same DAG does not.
+        # stream and the bucketed PS communication with backward, which a replayed graph does not.
         def timed(n):
             if world > 1:
                 dist.barrier()
@@ -141,13 +224,15 @@ def main():
         timed(2)  # the warm-up steps ran on a side stream: let the allocator fill this stream's pool
         # best of two windows per mode: one host hiccup must not decide the mode for the whole run
         setup["eager_ms"] = round(1000 * min(timed(4), timed(4)), 3)
-        trainer.use_graph = True
+        if ps.is_worker:
+            trainer.use_graph = True
         trainer.step(x, y)  # capture
         setup["graph_ms"] = round(1000 * min(timed(4), timed(4)), 3)
         mode = "graph" if setup["graph_ms"] <= setup["eager_ms"] else "eager"
-        trainer.use_graph = mode == "graph"
+        trainer.use_graph = mode == "graph" and ps.is_worker
         if rank == 0:
             print(f"[bench] setup {time.perf_counter() - t_w:.1f}s: {setup} -> {mode}", file=sys.stderr, flush=True)
+    loss = None
     for i in range(args.warmup):
         loss = trainer.step(x, y)
         if rank == 0:
@@ -155,9 +240,12 @@ def main():
             print(f"[bench] warmup {i + 1}/{args.warmup} t={time.perf_counter() - t_w:.1f}s", file=sys.stderr,
                   flush=True)
     torch.cuda.synchronize()
-    if not torch.isfinite(loss).all():
-        print(f"bench.py: non-finite loss after warmup: {loss.item()}", file=sys.stderr)
-        return 3
+    # every rank decides together: a rank that stopped alone would leave the others in a collective
+    bad = torch.tensor([0.0 if loss is None or torch.isfinite(loss).all() else 1.0], device=dev)
+    if world > 1:
+        dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+    if bad.item():
+        return fail(f"non-finite loss after warmup on some rank (rank {rank}: {loss.float().item()})", 3)
 
     if args.tune_cache and not tune_loaded and rank == 0:  # every shape has been tuned by now
         n_saved = tune.save(args.tune_cache)
@@ -175,15 +263,29 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # untimed: one eager step with GPU events at the phase boundaries (fwd / bwd / exposed PS tail)
+    phases = None
+    was_graph = trainer.use_graph
+    trainer.use_graph = False
+    trainer.enable_phase_timing()
+    trainer.step(x, y)
+    phases = [max_over_ranks(v, device=dev) for v in trainer.phase_ms()]
+    trainer.phase_events = None
+    trainer.use_graph = was_graph
     for _ in range(args.profile_steps):
         trainer.step(x, y)
     torch.cuda.synchronize()
 
     elapsed = max_over_ranks(elapsed, device=dev)
     final_loss = float(loss.float().item())
+    fallbacks = coll.fallback_count()
     if rank == 0:
-        imgs = args.batch * world * args.steps
+        imgs = args.batch * n_workers * args.steps
         value = imgs / elapsed
+        if args.ps_mode == "colocated":
+            par = f"ps-colocated-sharded dp{world} (1 PS shard + 1 worker per GPU, sync)"
+        else:
+            par = f"ps-dedicated 1 ps + {n_workers} workers (sync)"
         rec = {
             "metric": "images/sec (whole node) Inception-v3 TF-PS" if args.model == "inception_v3"
             else "images/sec (whole node) ResNet-50",
@@ -196,15 +298,19 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": args.dtype,
             "data": f"synthetic ImageNet-shaped {res}x{res}x3 batches, random-init weights",
             "config": {
                 "model": args.model,
-                "global_batch": args.batch * world,
+                "global_batch": args.batch * n_workers,
                 "per_gpu_batch": args.batch,
                 "seq_len": None,
                 "image_size": res,
-                "parallelism": f"ps-colocated-sharded dp{world} (1 PS shard + 1 worker per GPU, sync)",
+                "parallelism": par,
+                "ps_mode": args.ps_mode,
+                "workers": n_workers,
+                "grad_dtype": "fp32" if grad_dtype == torch.float32 else "bf16",
+                "variables": f"fp32 master on the PS, {args.dtype} compute copy",
                 "optimizer": "fused SGD-momentum (HIP)" if args.optimizer == "sgd" else args.optimizer,
                 "hip_graph": mode == "graph",
                 "step_mode": mode,
@@ -212,20 +318,27 @@ def main():
                 "tune_cache_loaded": tune_loaded,
                 "wgrad_stream": not args.no_wgrad_stream,
                 "branch_streams": _branch_streams_on(args),
+                "grad_buckets": len(ps.buckets),
+                "buckets_overlapped_with_backward": ps.overlapped_buckets,
+                "phase_ms_eager_step_max_over_ranks":
+                    dict(zip(("forward", "backward", "exposed_ps_push_apply_pull"), [round(v, 3) for v in phases])),
                 "host_ms_per_step": round(1000.0 * host / args.steps, 3),
                 "host_fwd_bwd_ms_last_eager_step": [round(1000.0 * trainer.host_fwd_s, 3),
                                                     round(1000.0 * trainer.host_bwd_s, 3)],
-                "kernels": "stock-comparator" if args.stock else "tony_amd HIP",
+                "kernels": "tony_amd HIP" if fused else "stock PyTorch-ROCm (MIOpen / hipBLASLt)",
                 "conv_impl": _conv_impl_counts(),
-                "grad_buckets": len(ps.buckets),
-                "buckets_overlapped_with_backward": ps.overlapped_buckets,
+                "collective_fallbacks": fallbacks,
+                "dist": diag or None,
                 "final_loss": round(final_loss, 4),
             },
         }
         print(json.dumps(rec), flush=True)
+    rc = 0
+    if os.environ.get("TONY_COLLECTIVE", "rccl").lower() in ("hip", "xgmi") and fallbacks:
+        rc = fail(f"TONY_COLLECTIVE=xgmi requested but {fallbacks} collectives fell back to RCCL")
     if world > 1:
         dist.destroy_process_group()
-    return 0
+    return rc
 
 
 def _branch_streams_on(args) -> bool:
@@ -235,7 +348,7 @@ def _branch_streams_on(args) -> bool:
 
 
 def _conv_impl_counts():
-    """How many (pass, shape) conv problems the autotuner gave to tony_amd's kernels vs MIOpen."""
+    """How many (pass, shape) conv problems went to tony_amd's kernels vs MIOpen."""
     from tony_amd.ops.conv import choices
 
     out = {}

@@ -70,14 +70,25 @@ def ddp_run(rank, kind, bucket_mb):
 
 
 def run(rank, world, port, q, kind, bucket_mb):
+    import faulthandler
+
+    os.makedirs("gpurun_out", exist_ok=True)
+    trace = open(os.path.join("gpurun_out", f"overlap_rank{rank}.txt"), "w")
+    faulthandler.enable(file=trace, all_threads=True)
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        out = {"ps_overlap": ps_run(rank, kind, True, bucket_mb), "ps_serial": ps_run(rank, kind, False, bucket_mb),
-               "ddp": ddp_run(rank, kind, bucket_mb)}
+        out = {}
+        for name, fn in (("ps_overlap", lambda: ps_run(rank, kind, True, bucket_mb)),
+                         ("ps_serial", lambda: ps_run(rank, kind, False, bucket_mb)),
+                         ("ddp", lambda: ddp_run(rank, kind, bucket_mb))):
+            print(f"rank {rank}: {name}", file=trace, flush=True)
+            out[name] = fn()
         dist.barrier()
         dist.destroy_process_group()
-        q.put((rank, out))
+        # by value: a tensor would travel as a shared-memory handle that dies with this process
+        q.put((rank, {k: {kk: vv.numpy() if isinstance(vv, torch.Tensor) else vv for kk, vv in v.items()}
+                      for k, v in out.items()}))
     except Exception:  # noqa: BLE001 - reported to the parent
         q.put((rank, {"error": traceback.format_exc()}))

@@ -211,3 +211,44 @@ def test_kvstore_local_and_optimizer_state(tmp_path):
     s2 = kv.create("local")
     s2.load_optimizer_states(str(tmp_path / "opt.pt"))
     assert "mom" in s2._opt.state[3]
+
+
+def test_bucket_engine_inplace_report_then_accumulate_hook():
+    """A fused op accumulates in place, reports, returns None -- and AccumulateGrad's hook still fires
+    right after: the repeat is ignored, buckets launch in order during backward."""
+    from tony_amd.ops import _lib
+    from tony_amd.parallel.buckets import GradBucketEngine, make_buckets
+    from tony_amd.parallel.flat import FlatParams
+
+    class InPlaceMul(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, w):
+            ctx.params = (w,)
+            ctx.save_for_backward(x)
+            return x * w
+
+        @staticmethod
+        def backward(ctx, g):
+            (x,) = ctx.saved_tensors
+            w = ctx.params[0]
+            w.grad.add_((g * x).sum(0))
+            _lib.report_inplace(ctx.params, (None,))
+            return g * w, None
+
+    m = torch.nn.Module()
+    m.w1 = torch.nn.Parameter(torch.ones(64))
+    m.w2 = torch.nn.Parameter(torch.ones(64))
+    flat = FlatParams(m, dtype=torch.float32)
+    seen = []
+    eng = GradBucketEngine(flat, make_buckets(flat, 64 * 4 / 2 ** 20), lambda b: seen.append(b.index))
+    eng.attach()
+    eng.log = []
+    eng.begin(overlap=True)
+    x = torch.ones(2, 64, requires_grad=True)
+    InPlaceMul.apply(InPlaceMul.apply(x, m.w1), m.w2).sum().backward()
+    eng.end()
+    assert seen == [0, 1]
+    assert eng.log == ["ready:w2", "launch:0", "ready:w1", "launch:1"]
+    assert eng.launched_during_backward == 2
+    torch.testing.assert_close(m.w1.grad, torch.full((64,), 2.0))
+    eng.detach()

@@ -7,6 +7,7 @@ import os
 import sys
 
 import pytest
+import torch
 
 from tony_amd.client.tony_client import TonyClient
 from tony_amd.conf import Configuration
@@ -159,3 +160,36 @@ def test_resnet50_ddp_minimum_slice(conf):
     assert rc == 0, _diag(client)
     ms = _metrics(client)
     assert len(ms) == 1 and ms[0]["world"] == 2 and ms[0]["images_per_sec"] > 0
+
+
+def _final_shards(d):
+    out = {}
+    for n in sorted(os.listdir(d)):
+        if n.startswith("ckpt-4-shard"):
+            out[n] = torch.load(os.path.join(d, n), weights_only=True)
+    return out
+
+
+def test_inception_ps_sharded_checkpoint_resume_after_gang_retry(conf, tmp_path):
+    """A worker dies mid-training (session 0); the coordinator's retry relaunches the gang, which
+    restores every rank's PS shard from the newest complete step and finishes with variables, fp32
+    masters and momentum BIT-identical to an uninterrupted run (3 workers = 3 shards over gloo)."""
+    confs = ["tony.ps.instances=1", "tony.worker.instances=3"]
+    args = "--ps-mode colocated --batch-size 2 --image-size 299 --steps 4 --warmup 0 --save-steps 2"
+    ref_dir, dir_ = tmp_path / "ref", tmp_path / "retry"
+    rc, client, _ = run_job(conf, "inception_ps.py", confs, f"{args} --checkpoint-dir {ref_dir}")
+    assert rc == 0, _diag(client)
+    rc, client, _ = run_job(conf, "inception_ps.py", confs + ["tony.am.retry-count=1"],
+                            f"{args} --checkpoint-dir {dir_} --fail-at-step 3")
+    assert rc == 0, _diag(client)
+    ms = _metrics(client)
+    assert ms and ms[-1]["start_step"] == 2 and ms[-1]["steps"] == 4   # resumed at the step-2 checkpoint
+    ref, got = _final_shards(ref_dir), _final_shards(dir_)
+    assert sorted(ref) == sorted(got) and len(ref) == 3
+    for name in ref:
+        a, b = ref[name]["ps"], got[name]["ps"]
+        assert torch.equal(a["flat"], b["flat"]), name
+        assert a["shards"].keys() == b["shards"].keys() and len(a["shards"]) == 1
+        for r in a["shards"]:
+            assert torch.equal(a["shards"][r]["master"], b["shards"][r]["master"])
+            assert torch.equal(a["shards"][r]["opt"]["momentum_buffer"], b["shards"][r]["opt"]["momentum_buffer"])

@@ -61,6 +61,10 @@ def test_two_ranks_overlap_ps_and_ddp(cuda, kind):
                 p.kill()
     for r in range(world):
         assert "error" not in out[r], out[r]["error"]
+        for v in out[r].values():
+            for k in ("params", "grad"):
+                if k in v:
+                    v[k] = torch.from_numpy(v[k])
     o0, o1 = out[0]["ps_overlap"], out[1]["ps_overlap"]
     assert o0["n_buckets"] > 2
     assert o0["overlapped"] >= o0["n_buckets"] - 1

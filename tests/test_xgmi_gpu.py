@@ -19,13 +19,16 @@ def _port():
     return p
 
 
-def test_xgmi_collectives_two_ranks():
+@pytest.mark.parametrize("world", [2, 3])
+def test_xgmi_collectives(world, monkeypatch):
     import xgmi_worker as W
 
+    # barriers give up after ~1 s of polling (the default is minutes): the skipped-call case below
+    monkeypatch.setenv("TONY_XGMI_SPIN_LIMIT", str(1 << 20))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    world, port = 2, _port()
-    procs = [ctx.Process(target=W.run, args=(r, world, port, q)) for r in range(world)]
+    port = _port()
+    procs = [ctx.Process(target=W.run, args=(r, world, port, q, world == 2)) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -39,3 +42,5 @@ def test_xgmi_collectives_two_ranks():
         assert "error" not in out[r], out[r]
         bad = [k for k, v in out[r].items() if not v]
         assert not bad, (r, bad)
+    if world == 2:
+        assert out[0]["skip_raises"] is True

@@ -5,12 +5,12 @@ import torch
 import torch.distributed as dist
 
 
-def run(rank, world, port, q):
+def run(rank, world, port, q, skip=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     try:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.cuda.set_device(0)  # every rank on the one GPU of the test box: IPC + the protocol
-        from tony_amd.parallel.xgmi import XgmiComm
+        from tony_amd.parallel.xgmi import XgmiComm, XgmiError
 
         comm = XgmiComm(slot_bytes=1 << 20, oneshot_max_bytes=64 << 10, blocks=8)
         dev = torch.device("cuda", 0)
@@ -36,8 +36,37 @@ def run(rank, world, port, q):
             b = torch.full((8192,), float(rank + 10), device=dev, dtype=dtype)
             comm.broadcast(b, src=1)
             res[f"bc_{dtype}"] = bool((b.float() == 11.0).all().item())
+            # larger than the 1 MB slot: reduce-scatter / all-gather go in slot-sized pieces
+            m = (3 << 20) // 4 // world // 8 * 8 + 8 * 13            # odd piece count, not a slot multiple
+            x = (torch.arange(world * m, device=dev, dtype=torch.float32).remainder(5) + rank).to(dtype)
+            out = torch.empty(m, device=dev, dtype=dtype)
+            comm.reduce_scatter(out, x)
+            full = sum((torch.arange(world * m, device=dev, dtype=torch.float32).remainder(5) + r) for r in range(world))
+            res[f"rs_big_{dtype}"] = bool(torch.allclose(out.float(), full[rank * m:(rank + 1) * m], rtol=1e-2))
+            shard = (torch.arange(m, device=dev, dtype=torch.float32).remainder(3) + 10 * rank).to(dtype)
+            g = torch.empty(world * m, device=dev, dtype=dtype)
+            comm.all_gather(g, shard)
+            exp = torch.cat([torch.arange(m, device=dev, dtype=torch.float32).remainder(3) + 10 * r
+                             for r in range(world)])
+            res[f"ag_big_{dtype}"] = bool(torch.equal(g.float(), exp))
+        # many back-to-back calls: the slot parity / epoch protocol never desynchronises
+        t = torch.ones(4096, device=dev)
+        for _ in range(300):
+            comm.all_reduce(t, average=True)
+        res["back_to_back"] = bool((t == 1.0).all().item())
         torch.cuda.synchronize()
         comm.check_error()
+        # a peer that skips a collective: the waiting rank's barrier gives up and the NEXT check raises
+        if skip:
+            if rank == 0:
+                comm.all_reduce(torch.ones(1024, device=dev))
+                try:
+                    comm.check_error()
+                    res["skip_raises"] = False
+                except XgmiError:
+                    res["skip_raises"] = True
+                comm.check_error()  # cleared after being reported once
+            dist.barrier()
         comm.close()
         dist.destroy_process_group()
         q.put((rank, res))

@@ -12,7 +12,14 @@ variables and apply the optimizer, workers push gradients and pull variables eve
 ``--ps-mode dedicated``
     The ps task(s) join the group and own the variables (give them GPUs: tony.ps.gpus=1).
 
-The step (forward, loss, backward, push/apply/pull) is captured once into a HIP graph.
+The step (forward, loss, backward, push/apply/pull) runs eagerly with the bucketed push/apply/pull
+overlapped with backward, or replayed as a HIP graph (``--graph``).
+
+Checkpoint / resume: with ``--save-steps K`` every rank writes its own PS shard
+(fp32 master + momentum of the variables it owns, the variables, its BN running statistics) every K
+steps (utils/checkpoint.py, sharded); a relaunched gang (``tony.am.retry-count`` > 0, SESSION_ID > 0)
+resumes from the newest step complete on every rank.  ``--fail-at-step S`` is a test hook: in the
+first session, worker 1 exits at step S (the TEST_WORKER_TERMINATION idea, mid-training).
 
   tony --src_dir tony_amd/jobs --executes inception_ps.py --conf tony.ps.instances=1 \
        --conf tony.worker.instances=4 --conf tony.worker.gpus=1
@@ -29,11 +36,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from tony_amd.jobs.common import Throughput, log, metric, synthetic_images  # noqa: E402
+from tony_amd.jobs.common import Throughput, log, metric, synthetic_images, working_dir  # noqa: E402
 from tony_amd.parallel import bootstrap  # noqa: E402
 from tony_amd.parallel.ps import ParameterServer  # noqa: E402
 from tony_amd.parallel.tf_config import TFConfig  # noqa: E402
 from tony_amd.parallel.trainer import Trainer  # noqa: E402
+from tony_amd.utils.checkpoint import CheckpointManager, resume_step  # noqa: E402
 
 
 def main(argv=None) -> int:
@@ -43,7 +51,11 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--image-size", type=int, default=299)
-    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="(default) issue the step eagerly")
+    ap.add_argument("--graph", action="store_true", help="replay the step as a HIP graph")
+    ap.add_argument("--checkpoint-dir", default=None, help="default: <job dir>/inception_ps")
+    ap.add_argument("--save-steps", type=int, default=0, help="checkpoint every K steps (0: never)")
+    ap.add_argument("--fail-at-step", type=int, default=-1, help="test hook (session 0, worker 1)")
     a = ap.parse_args(argv)
     tc = TFConfig.from_env()
     on_gpu = torch.cuda.is_available()
@@ -57,6 +69,7 @@ def main(argv=None) -> int:
                 time.sleep(3600)
         tc = tc.without_ps()
     rank, world, dev = bootstrap.init_from_tf_config(tc)
+    torch.manual_seed(1000 + rank)  # dropout masks: reproducible per rank (and restored on resume)
     from tony_amd.models.inception_v3 import inception_v3
     from tony_amd.models.layers import cast_model
 
@@ -66,11 +79,6 @@ def main(argv=None) -> int:
     model = cast_model(inception_v3(fused=on_gpu, seed=0), dtype, dev).to(memory_format=torch.channels_last)
     ps = ParameterServer(model, optimizer="sgd", lr=0.045, momentum=0.9, weight_decay=4e-5, mode=mode,
                          ps_ranks=tc.ps_ranks if mode == "dedicated" else (0,), dtype=dtype, device=dev)
-    if mode == "dedicated" and ps.is_ps and not ps.is_worker:
-        for _ in range(a.warmup + a.steps):
-            ps.step()
-        dist.barrier()
-        return 0
 
     def loss_fn(out, y):
         logits, aux = out if isinstance(out, tuple) else (out, None)
@@ -79,21 +87,67 @@ def main(argv=None) -> int:
             loss = loss + 0.4 * torch.nn.functional.cross_entropy(aux.float(), y)
         return loss
 
-    trainer = Trainer(model, ps, loss_fn, use_graph=on_gpu and not a.no_graph)
+    total = a.warmup + a.steps
+    ckpt = CheckpointManager(a.checkpoint_dir or working_dir("inception_ps"), save_steps=a.save_steps,
+                             sharded=True)
+    start = 0
+    state = ckpt.restore(device=dev if on_gpu else None)
+    if state is not None:
+        ps.load_state_dict(state["ps"])
+        with torch.no_grad():
+            for k, b in model.named_buffers():
+                b.copy_(state["buffers"][k])
+        torch.set_rng_state(state["rng_cpu"])  # dropout masks continue exactly where they were
+        if on_gpu and "rng_cuda" in state:
+            torch.cuda.set_rng_state(state["rng_cuda"], dev)
+        start = resume_step(state)
+        log(f"session {os.environ.get('SESSION_ID', '0')}: resumed from step {start}")
+
+    def save(step, force=False):
+        st = {"ps": ps.state_dict(), "buffers": dict(model.named_buffers()), "rng_cpu": torch.get_rng_state()}
+        if on_gpu:
+            st["rng_cuda"] = torch.cuda.get_rng_state(dev)
+        ckpt.save(step, st, force=force)
+
+    if mode == "dedicated" and ps.is_ps and not ps.is_worker:
+        for s in range(start, total):  # the ps task: reduce -> apply -> broadcast, bucket by bucket
+            ps.step()
+            if ckpt.should_save(s + 1):
+                save(s + 1)
+        if a.save_steps:
+            save(total, force=True)
+            ckpt.wait()
+        dist.barrier()
+        return 0
+
+    trainer = Trainer(model, ps, loss_fn, use_graph=on_gpu and a.graph)
     x, y = synthetic_images(a.batch_size, a.image_size, 1000, dev, dtype, seed=rank)
     tp = Throughput(dev)
-    for s in range(a.warmup + a.steps):
-        if s == a.warmup:
+    timed = 0
+    loss = torch.zeros(())
+    for s in range(start, total):
+        if s == a.fail_at_step and os.environ.get("SESSION_ID", "0") == "0" and tc.task_type == "worker" \
+                and tc.task_index == 1:
+            log(f"test hook: worker 1 fails at step {s}")
+            os._exit(17)
+        if s == max(start, a.warmup):
             dist.barrier()
             tp.start()
         loss = trainer.step(x, y)
-        if s >= a.warmup:
+        if s >= max(start, a.warmup):
             tp.add(a.batch_size)
-    rate = torch.tensor([tp.rate()], dtype=torch.float64, device=dev if on_gpu else "cpu")
+            timed += 1
+        if ckpt.should_save(s + 1):
+            save(s + 1)
+    if a.save_steps:
+        save(total, force=True)
+        ckpt.wait()
+    rate = torch.tensor([tp.rate() if timed else 0.0], dtype=torch.float64, device=dev if on_gpu else "cpu")
     dist.all_reduce(rate)
     workers = len(ps.worker_ranks)
     if tc.is_chief or rank == 0:
-        metric(model="inception_v3", images_per_sec=float(rate), workers=workers, ps_mode=mode, loss=float(loss))
+        metric(model="inception_v3", images_per_sec=float(rate), workers=workers, ps_mode=mode, loss=float(loss),
+               start_step=start, steps=total)
     log(f"{float(rate):.1f} images/sec total over {workers} workers ({mode} PS)")
     dist.barrier()
     return 0

@@ -97,6 +97,7 @@ _SIGNATURES = {
     "tony_xgmi_close": [c_void_p],
     "tony_xgmi_free": [c_void_p],
     "tony_xgmi_error": [c_void_p, c_int_p],
+    "tony_xgmi_error_async": [c_void_p, c_void_p, c_void_p],
     "tony_xgmi_collective": [c_u64_p, c_int, c_int, c_int64, c_int, c_void_p, c_void_p, c_int64, c_int, c_int,
                              c_float, ctypes.c_uint32, c_int, c_void_p],
 }

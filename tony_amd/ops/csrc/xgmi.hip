@@ -21,6 +21,8 @@
 // error in the window's error word and exit instead of hanging the GPU; the host raises on it.
 #include <cstring>
 
+#include <cstdlib>
+
 #include "common.h"
 
 using namespace tony;
@@ -38,6 +40,7 @@ struct Comm {
   uint8_t* win[kMaxRanks];  // window base of every rank as mapped in THIS process
   int rank, nranks;
   int64_t slot_bytes;
+  long spin_limit;  // polls before a barrier gives up (kSpinLimit; TONY_XGMI_SPIN_LIMIT overrides)
 };
 
 __device__ __forceinline__ uint32_t* flags(uint8_t* w, int phase) {
@@ -62,7 +65,7 @@ __device__ bool peer_barrier(const Comm& c, int phase, uint32_t epoch) {
     uint32_t* mine = flags(c.win[c.rank], phase) + t * kMaxBlocks + blockIdx.x;
     long spins = 0;
     while (__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-      if (++spins > kSpinLimit) {
+      if (++spins > c.spin_limit) {
         ok = 0;
         int* err = reinterpret_cast<int*>(c.win[c.rank] + kErrOff);
         __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -215,9 +218,20 @@ TONY_API int tony_xgmi_close(void* ptr) { return static_cast<int>(hipIpcCloseMem
 TONY_API int tony_xgmi_free(void* window) { return static_cast<int>(hipFree(window)); }
 TONY_API int tony_xgmi_handle_bytes() { return static_cast<int>(sizeof(hipIpcMemHandle_t)); }
 
-// Non-zero when a barrier of this rank timed out (a peer never arrived).
+// Non-zero when a barrier of this rank timed out (a peer never arrived).  Synchronous; the error
+// word is cleared after it has been read, so one failure is reported once.
 TONY_API int tony_xgmi_error(void* window, int* err) {
-  return static_cast<int>(hipMemcpy(err, static_cast<uint8_t*>(window) + kErrOff, sizeof(int), hipMemcpyDeviceToHost));
+  int* word = reinterpret_cast<int*>(static_cast<uint8_t*>(window) + kErrOff);
+  hipError_t e = hipMemcpy(err, word, sizeof(int), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && *err != 0) e = hipMemset(word, 0, sizeof(int));
+  return static_cast<int>(e);
+}
+
+// Stream-ordered copy of the error word into host memory (pinned): the host checks it before its
+// next collective, so a timed-out barrier fails the run one call later without a device sync.
+TONY_API int tony_xgmi_error_async(void* window, int* host_err, hipStream_t stream) {
+  return static_cast<int>(hipMemcpyAsync(host_err, static_cast<uint8_t*>(window) + kErrOff, sizeof(int),
+                                         hipMemcpyDeviceToHost, stream));
 }
 
 // windows: host array of nranks window pointers as mapped in this process (own window at [rank]).
@@ -239,6 +253,11 @@ TONY_API int tony_xgmi_collective(const uint64_t* windows, int rank, int nranks,
   c.rank = rank;
   c.nranks = nranks;
   c.slot_bytes = slot_bytes;
+  c.spin_limit = kSpinLimit;
+  if (const char* lim = std::getenv("TONY_XGMI_SPIN_LIMIT")) {
+    const long v = std::strtol(lim, nullptr, 10);
+    if (v > 0) c.spin_limit = v;
+  }
   if (blocks < 1) blocks = 1;
   if (blocks > kMaxBlocks) blocks = kMaxBlocks;
   if (dtype_bf16)

@@ -14,7 +14,9 @@ gradients are complete when every parameter in it has been written.  Two produce
   into the flat buffer and return None to autograd, call ``_lib.grads_ready(*params)`` at the end
   of their backward node (after the node's data-gradient kernels are enqueued, so nothing of that
   node still reads the old parameters when the bucket's apply rewrites them);
-* every other parameter goes through AccumulateGrad, whose post-accumulate hook reports it.
+* every other parameter goes through AccumulateGrad, whose post-accumulate hook reports it (the
+  hook also fires, with nothing accumulated, right after a fused node returned None for a
+  parameter: such a repeat report is ignored).
 
 Ordering.  Buckets launch strictly in index order (a ready bucket waits for its predecessors), so
 every rank issues its collectives in the same sequence -- the RCCL/NCCL requirement -- whatever
@@ -108,7 +110,10 @@ class GradBucketEngine:
         self.comm: Optional[torch.cuda.Stream] = None
         if self.device.type == "cuda":
             self.comm = torch.cuda.Stream(device=self.device)
-        self._hooks = []
+        self._hooks: Dict[int, object] = {}
+        self._inplace = [False] * len(flat.slots)  # reported by a fused op: its AccumulateGrad hook is dropped
+        esz = flat.grad.element_size()
+        self._slot_ptr = [flat.grad.data_ptr() + s.offset * esz for s in flat.slots]
         self.armed = False
         self.overlap = False
         self._next = 0
@@ -126,13 +131,13 @@ class GradBucketEngine:
             return
         _lib.add_grad_listener(self)
         for i, p in enumerate(self.flat.params):
-            self._hooks.append(p.register_post_accumulate_grad_hook(lambda p, i=i: self._on_accumulate(i, p)))
+            self._hooks[i] = p.register_post_accumulate_grad_hook(lambda p, i=i: self._on_accumulate(i, p))
 
     def detach(self) -> None:
         _lib.remove_grad_listener(self)
-        for h in self._hooks:
+        for h in self._hooks.values():
             h.remove()
-        self._hooks = []
+        self._hooks = {}
 
     # -- per step -------------------------------------------------------------------------------
     def begin(self, overlap: bool = True) -> None:
@@ -158,18 +163,24 @@ class GradBucketEngine:
         for p in params:
             i = self._index.get(id(p))
             if i is not None:
+                self._inplace[i] = True
                 self._mark(i)
         self._drain()
 
     def _on_accumulate(self, i: int, p: torch.Tensor) -> None:
-        view = self.flat.slots[i].view(self.flat.grad)
-        if p.grad is not None and p.grad.data_ptr() != view.data_ptr():
-            view.copy_(p.grad)  # user code replaced .grad (e.g. zero_grad(set_to_none=True))
+        g = p.grad
+        if g is not None and g.data_ptr() != self._slot_ptr[i]:
+            view = self.flat.slots[i].view(self.flat.grad)
+            view.copy_(g)  # user code replaced .grad (e.g. zero_grad(set_to_none=True))
             p.grad = view
         if not self.armed:
             if self.auto_arm is None:
                 return
             self.auto_arm()
+        if self._seen[i]:
+            # AccumulateGrad runs (and fires this hook) even when a fused op returned None for the
+            # parameter after accumulating in place and reporting it: nothing new was written
+            return
         self._mark(i)
         self._drain()
 
@@ -214,8 +225,17 @@ class GradBucketEngine:
         finally:
             torch.cuda.set_stream(cur)
 
+    def _drop_inplace_hooks(self) -> None:
+        """Parameters the fused ops report themselves need no AccumulateGrad hook: each Python hook
+        call costs ~10 us of host time on the backward's critical issue path (x ~300 parameters)."""
+        for i, done in enumerate(self._inplace):
+            h = self._hooks.pop(i, None) if done else None
+            if h is not None:
+                h.remove()
+
     def end(self) -> None:
         """Launch the remaining buckets in order and make the current stream wait for all of them."""
+        self._drop_inplace_hooks()
         for b in self.buckets:
             if not b.launched:
                 self._launch(b)

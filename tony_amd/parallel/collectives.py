@@ -19,11 +19,20 @@ import torch.distributed as dist
 _XGMI = [None]
 
 
+_FALLBACKS = [0]
+
+
+def fallback_count() -> int:
+    """Collectives that TONY_COLLECTIVE=xgmi asked for but that ran on RCCL (dtype / size / group)."""
+    return _FALLBACKS[0]
+
+
 def _xgmi(t: torch.Tensor, group):
     """The XgmiComm to use for tensor t, or None for the torch.distributed (RCCL / gloo) path."""
-    if group is not None or not t.is_cuda or os.environ.get("TONY_COLLECTIVE", "rccl").lower() not in ("hip", "xgmi"):
+    if os.environ.get("TONY_COLLECTIVE", "rccl").lower() not in ("hip", "xgmi") or not t.is_cuda:
         return None
-    if t.dtype not in (torch.bfloat16, torch.float32) or (t.numel() * t.element_size()) % 16:
+    if group is not None or t.dtype not in (torch.bfloat16, torch.float32) or (t.numel() * t.element_size()) % 16:
+        _FALLBACKS[0] += 1
         return None
     if _XGMI[0] is None:
         from .xgmi import XgmiComm
@@ -57,7 +66,7 @@ def reduce_scatter_flat(out: torch.Tensor, inp: torch.Tensor, group=None, async_
         out.copy_(inp[r * n:(r + 1) * n])
         return None
     x = _xgmi(inp, group)
-    if x is not None and inp.numel() * inp.element_size() <= x.slot_bytes:
+    if x is not None:
         x.reduce_scatter(out, inp)
         return None
     return dist.reduce_scatter_tensor(out, inp, group=group, async_op=async_op)
@@ -76,7 +85,7 @@ def all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group=None, async_op=F
         dist.all_gather(parts, src, group=group)
         return None
     x = _xgmi(inp, group)
-    if x is not None and inp.numel() * inp.element_size() <= x.slot_bytes:
+    if x is not None:
         x.all_gather(out, inp)
         return None
     return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)

@@ -37,6 +37,7 @@ class Trainer:
         self.graph_collectives = (ps.world == 1) if graph_collectives is None else graph_collectives
         self.overlap_wgrad = overlap_wgrad
         self.overlap_comm = overlap_comm
+        self.phase_events = None
         self.branch_streams = branch_streams
         self._tuned = False
         self.side_ops = 0
@@ -55,8 +56,24 @@ class Trainer:
         if self.wt is not None:
             self.wt.enabled = True
 
+    def _mark(self, i: int) -> None:
+        ev = self.phase_events
+        if ev is not None and not torch.cuda.is_current_stream_capturing():
+            ev[i].record()
+
+    def enable_phase_timing(self) -> None:
+        """Record GPU events at step start / after forward / after backward / after the PS step."""
+        self.phase_events = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+
+    def phase_ms(self):
+        """(forward, backward, exposed PS push/apply/pull) GPU ms of the last eager step."""
+        ev = self.phase_events
+        ev[3].synchronize()
+        return tuple(ev[i].elapsed_time(ev[i + 1]) for i in range(3))
+
     def _body(self, x, y, ps_step: bool = True):
         t0 = time.perf_counter()
+        self._mark(0)
         self.ps.zero_grad()
         if ps_step:
             # arm the gradient buckets: each bucket's push/apply/pull is enqueued on the communication
@@ -74,16 +91,19 @@ class Trainer:
                 out = self.model(x)
                 loss = self.loss_fn(out, y)
             t1 = time.perf_counter()
+            self._mark(1)
             with trace_range("backward"):
                 loss.backward()
         finally:
             if overlap:
                 self.side_ops = streams.end()  # every stream joined before the PS reads the gradients
+        self._mark(2)
         # host seconds spent issuing the forward / the backward (eager steps; the GPU runs behind)
         self.host_fwd_s, self.host_bwd_s = t1 - t0, time.perf_counter() - t1
         self._tuned = True
         if ps_step:
             self._ps_step()
+            self._mark(3)
         return loss
 
     def _ps_step(self):

@@ -13,7 +13,8 @@ in and one out):
 * ``reduce_scatter`` / ``all_gather`` / ``broadcast``  the flat single-launch forms the
                    parameter server and DDP buckets use.
 
-Messages larger than the window slot are processed in slot-sized pieces.  Sums accumulate in
+Messages larger than the window slot are processed in slot-sized pieces (all-reduce, broadcast,
+reduce-scatter and all-gather alike).  Sums accumulate in
 fp32 for bf16 tensors.  Selected with ``TONY_COLLECTIVE=xgmi`` (TonY conf key
 ``tony.amd.collective``), otherwise the RCCL path of ``collectives.py`` runs; a barrier whose peer
 never arrives fails the call (``XgmiError``) instead of hanging the GPU.
@@ -72,17 +73,25 @@ class XgmiComm:
             self.peers.append(p.value)
             ptrs.append(p.value)
         self._windows = (ctypes.c_uint64 * self.world)(*ptrs)
+        # the error word, copied (stream-ordered) into pinned host memory after every collective and
+        # checked before the next one: a barrier that timed out fails the run one call later
+        self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         dist.barrier(group=group)
 
     # -- plumbing -------------------------------------------------------------------------------
     def _launch(self, kind: int, inp: torch.Tensor, out: torch.Tensor, nbytes: int, root: int = 0,
                 scale: float = 1.0, in_off: int = 0, out_off: int = 0):
+        if int(self._err_host[0]):  # an earlier collective's barrier timed out
+            self.check_error()
         self.epoch += 1
-        rc = _lib.lib().tony_xgmi_collective(self._windows, self.rank, self.world, self.slot_bytes, kind,
-                                             inp.data_ptr() + in_off, out.data_ptr() + out_off, nbytes,
-                                             int(inp.dtype == torch.bfloat16), root, float(scale),
-                                             self.epoch & 0xFFFFFFFF, self.blocks, _lib.stream_ptr(self.device))
+        L, stream = _lib.lib(), _lib.stream_ptr(self.device)
+        rc = L.tony_xgmi_collective(self._windows, self.rank, self.world, self.slot_bytes, kind,
+                                    inp.data_ptr() + in_off, out.data_ptr() + out_off, nbytes,
+                                    int(inp.dtype == torch.bfloat16), root, float(scale),
+                                    self.epoch & 0xFFFFFFFF, self.blocks, stream)
         _lib.check(rc, "tony_xgmi_collective")
+        _lib.check(L.tony_xgmi_error_async(ctypes.c_void_p(self.window), self._err_host.data_ptr(), stream),
+                   "tony_xgmi_error_async")
 
     @staticmethod
     def _check(t: torch.Tensor):
@@ -92,11 +101,14 @@ class XgmiComm:
             raise XgmiError("xgmi collectives need 16-byte aligned sizes and addresses")
 
     def check_error(self) -> None:
-        """Raise if a barrier of this rank timed out (synchronises the device)."""
+        """Raise if a barrier of this rank timed out (synchronises the device; clears the word)."""
+        torch.cuda.synchronize(self.device)
         err = ctypes.c_int(0)
         _lib.check(_lib.lib().tony_xgmi_error(ctypes.c_void_p(self.window), ctypes.byref(err)), "tony_xgmi_error")
+        self._err_host.zero_()
         if err.value:
-            raise XgmiError(f"rank {self.rank}: a peer never reached an xgmi barrier")
+            raise XgmiError(f"rank {self.rank}: a peer never reached an xgmi barrier: the results of the "
+                            f"collectives since the last check are invalid")
 
     # -- collectives ----------------------------------------------------------------------------
     def all_reduce(self, t: torch.Tensor, average: bool = False) -> torch.Tensor:
@@ -122,10 +134,23 @@ class XgmiComm:
         """out (inp.numel() / world elements) = this rank's shard of the sum over ranks of inp."""
         self._check(inp)
         self._check(out)
-        nbytes = inp.numel() * inp.element_size()
-        if out.numel() * self.world != inp.numel() or nbytes > self.slot_bytes:
-            raise XgmiError("reduce_scatter: out must be inp/world and inp must fit the window slot")
-        self._launch(KIND["reduce_scatter"], inp, out, nbytes, scale=1.0 / self.world if average else 1.0)
+        if out.numel() * self.world != inp.numel():
+            raise XgmiError("reduce_scatter: out must be inp/world")
+        esz = inp.element_size()
+        shard = out.numel() * esz
+        # a slot holds one piece of every rank's shard: process the shards in slot-sized column pieces
+        piece = max(16, self.slot_bytes // self.world // 16 * 16)
+        off = 0
+        while off < shard:
+            n = min(piece, shard - off)
+            if n == shard:
+                self._launch(KIND["reduce_scatter"], inp, out, n * self.world,
+                             scale=1.0 / self.world if average else 1.0)
+            else:  # rank r's rows [off, off+n) of every shard: gather them contiguously first
+                cols = inp.view(self.world, -1)[:, off // esz:(off + n) // esz].contiguous()
+                self._launch(KIND["reduce_scatter"], cols, out, n * self.world,
+                             scale=1.0 / self.world if average else 1.0, out_off=off)
+            off += n
         return out
 
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
@@ -133,9 +158,21 @@ class XgmiComm:
         self._check(inp)
         self._check(out)
         nbytes = inp.numel() * inp.element_size()
-        if out.numel() != inp.numel() * self.world or nbytes > self.slot_bytes:
-            raise XgmiError("all_gather: out must be world x inp and inp must fit the window slot")
-        self._launch(KIND["all_gather"], inp, out, nbytes)
+        if out.numel() != inp.numel() * self.world:
+            raise XgmiError("all_gather: out must be world x inp")
+        if nbytes <= self.slot_bytes:  # each rank stages its shard in its own slot
+            self._launch(KIND["all_gather"], inp, out, nbytes)
+            return out
+        esz = inp.element_size()
+        piece = self.slot_bytes // 16 * 16
+        tmp = torch.empty(self.world * min(piece, nbytes) // esz, dtype=inp.dtype, device=inp.device)
+        off = 0
+        while off < nbytes:
+            n = min(piece, nbytes - off)
+            part = tmp[:self.world * n // esz]
+            self._launch(KIND["all_gather"], inp, part, n, in_off=off)
+            out.view(self.world, -1)[:, off // esz:(off + n) // esz].copy_(part.view(self.world, -1))
+            off += n
         return out
 
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
@@ -152,7 +189,7 @@ class XgmiComm:
         """Unmap the peers and free the window (collective: every rank calls it)."""
         if self.window is None:
             return
-        torch.cuda.synchronize(self.device)
+        self.check_error()
         dist.barrier(group=self.group)  # no peer may still be reading this rank's window
         L = _lib.lib()
         for p in self.peers:
