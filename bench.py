@@ -126,8 +126,23 @@ def diagnose(world: int, rank: int, dev, backend: str, shared_ok: bool) -> dict:
     return info
 
 
+def _heartbeat(t0: float, every_s: float = 45.0) -> None:
+    """Progress line while setup runs silently for minutes (MIOpen find, first-step autotuning):
+    the GPU-box runner treats a command that stops writing for 3 minutes as hung."""
+    import threading
+
+    def beat():
+        while True:
+            time.sleep(every_s)
+            print(f"[bench] alive t={time.perf_counter() - t0:.0f}s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, name="bench-heartbeat", daemon=True).start()
+
+
 def main():
     args = parse()
+    if int(os.environ.get("RANK", "0")) == 0:
+        _heartbeat(time.perf_counter())
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

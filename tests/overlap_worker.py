@@ -40,7 +40,8 @@ def ps_run(rank, kind, overlap, bucket_mb, steps=3):
 
     dev = torch.device("cuda", 0)
     model = _model(kind, dev)
-    ps = ParameterServer(model, optimizer="sgd", lr=0.05, momentum=0.9, device=dev, bucket_mb=bucket_mb)
+    ps = ParameterServer(model, optimizer="sgd", lr=0.05, momentum=0.9, device=dev, bucket_mb=bucket_mb,
+                         bucketed_single=True)
     tr = Trainer(model, ps, lambda o, y: cross_entropy(o, y), overlap_comm=overlap)
     x, y = _data(rank, kind, dev)
     for s in range(steps):

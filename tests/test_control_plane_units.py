@@ -540,3 +540,74 @@ def test_rpc_token_auth_and_roundtrip():
         assert e.value.code() == grpc.StatusCode.UNAUTHENTICATED
     finally:
         srv.stop(0)
+
+
+# -- GPU ordinal mapping and CPU slicing (amd-smi index != HIP ordinal) -------------------
+def test_hip_ordinals_follow_kfd_order_by_bdf():
+    from tony_amd.gpu.inventory import hip_ordinals
+    from tony_amd.native import GpuDevice
+
+    # amd-smi lists the GPUs in one order, KFD (= HIP) in another: map by BDF
+    smi = [GpuDevice(i, bdf=b, numa_node=i // 4) for i, b in
+           enumerate(["0000:05:00.0", "0000:15:00.0", "0000:65:00.0", "0000:75:00.0",
+                      "0000:85:00.0", "0000:95:00.0", "0000:e5:00.0", "0000:f5:00.0"])]
+    kfd = ["0000:15:00.0", "0000:05:00.0", "0000:75:00.0", "0000:65:00.0",
+           "0000:95:00.0", "0000:85:00.0", "0000:f5:00.0", "0000:e5:00.0"]
+    m = hip_ordinals(smi, kfd)
+    assert m == {0: 1, 1: 0, 2: 3, 3: 2, 4: 5, 5: 4, 6: 7, 7: 6}
+    # amd-smi may print the BDF without the domain / function
+    assert hip_ordinals([GpuDevice(0, bdf="15:00.0")], kfd) == {0: 0}
+    with pytest.raises(RuntimeError, match="not among the HIP-visible"):
+        hip_ordinals([GpuDevice(0, bdf="0000:aa:00.0")], kfd)
+    with pytest.raises(RuntimeError, match="no PCI BDF"):
+        hip_ordinals([GpuDevice(0)], kfd)
+    fake = [GpuDevice(i, bdf=f"fake:{i:02x}", fake=True) for i in range(3)]
+    assert hip_ordinals(fake, kfd) == {0: 0, 1: 1, 2: 2}
+
+
+def test_kfd_bdfs_read_in_node_order(tmp_path):
+    from tony_amd.gpu.inventory import kfd_gpu_bdfs
+
+    for node, (simd, loc) in {"0": (0, 0), "2": (304, 0x7500), "10": (304, 0x0500), "1": (304, 0x1508)}.items():
+        d = tmp_path / node
+        d.mkdir()
+        (d / "properties").write_text(f"simd_count {simd}\nlocation_id {loc}\ndomain 0\nnuma_node 0\n")
+    # node ids sort numerically (1, 2, 10); the CPU node (simd 0) is skipped
+    assert kfd_gpu_bdfs(str(tmp_path)) == ["0000:15:01.0", "0000:75:00.0", "0000:05:00.0"]
+
+
+def test_verify_visible_device_detects_mispinning(monkeypatch):
+    from types import SimpleNamespace
+
+    import torch
+
+    from tony_amd.gpu.inventory import verify_visible_device
+
+    props = SimpleNamespace(pci_domain_id=0, pci_bus_id=0x75, pci_device_id=0)
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda i: props)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "3")
+    monkeypatch.setenv("TONY_GPU_BDFS", "0000:75:00.0")
+    assert verify_visible_device(0) == "0000:75:00.0"
+    monkeypatch.setenv("TONY_GPU_BDFS", "0000:65:00.0")
+    with pytest.raises(RuntimeError, match="does not select the allocated GPU"):
+        verify_visible_device(0)
+
+
+def test_allocator_slices_numa_cpus_by_vcores():
+    from tony_amd.gpu.inventory import GpuAllocator
+    from tony_amd.native import GpuDevice
+
+    devs = [GpuDevice(i, bdf=f"fake:{i}", numa_node=i // 4, fake=True) for i in range(8)]
+    cpus = {0: list(range(0, 16)), 1: list(range(16, 32))}
+    a = GpuAllocator(devs, cpus_of_node=lambda n: cpus[n])
+    s1 = a.allocate("w0", 1, vcores=4)
+    s2 = a.allocate("w1", 1, vcores=4)
+    assert s1.numa_node == s2.numa_node == 0
+    assert len(s1.cpus) == 4 and len(s2.cpus) == 4 and not set(s1.cpus) & set(s2.cpus)
+    whole = a.allocate("w2", 1, vcores=0)
+    assert whole.cpus == cpus[0]
+    a.release("w0")
+    s3 = a.allocate("w3", 1, vcores=4)
+    assert s3.cpus == s1.cpus                        # released CPUs are handed out again
+    big = a.allocate("w4", 1, vcores=12)             # only 4 unowned left on node 0: oversubscribe
+    assert len(big.cpus) == 12

@@ -18,6 +18,12 @@ SHAPES = [
     (2, 128, 28, 28, 128, (3, 3), 2, (1, 1)),
     (3, 32, 149, 149, 32, (3, 3), 1, (0, 0)),
     (2, 80, 73, 73, 192, (3, 3), 1, (0, 0)),
+    # strided backward-data: one tony launch per residue class of dX (no MIOpen)
+    (2, 96, 35, 35, 96, (3, 3), 2, (0, 0)),        # Mixed_6a double-3x3 tail
+    (2, 192, 17, 17, 320, (3, 3), 2, (0, 0)),      # Mixed_7a
+    (2, 256, 56, 56, 512, (1, 1), 2, (0, 0)),      # ResNet downsample: odd classes get no taps (zeros)
+    (2, 64, 57, 57, 64, (3, 3), 2, (1, 1)),        # odd size + padding
+    (2, 32, 20, 20, 48, (5, 5), 3, (2, 2)),        # stride 3: nine classes
 ]
 
 
@@ -303,7 +309,7 @@ def test_stem_conv_bn_act_layer_fwd_bwd(cuda):
     C.AUTOTUNE, C.STEM = False, True  # route the stem to the fused layer and pin the direct kernel
     try:
         y = C.conv_bn_act(x, wt, g, b, rm, rv, 2, 0, True, 0.1, 1e-3, True)
-        key = [k for k in C._CHOICE if k[0] == "fwd" and k[2] == (co, 3, 3, 3)]
+        key = [k for k in C._CHOICE if k[0] == "fwd" and k[1] == tuple(x.shape) and k[2] == (co, 3, 3, 3)]
         assert not key or C._CHOICE[key[0]] == "tony"
         wr, gr, br = (t.detach().float().requires_grad_(True) for t in (wt, g, b))
         rm_r, rv_r = torch.zeros(co, device=cuda), torch.ones(co, device=cuda)

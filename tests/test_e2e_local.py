@@ -356,3 +356,30 @@ def test_notebook_submitter_proxies_notebook(conf):
     t.join(60)
     assert body == b"notebook-ok"
     assert out.get("rc") == 0
+
+
+def test_task_over_memory_limit_is_stopped(conf):
+    """YARN's NodeManager kills a container whose process tree exceeds its physical-memory request
+    (tony.<job>.memory); here the task agent samples the tree's RSS and stops the task, which FAILS
+    with the memory-limit diagnostic."""
+    conf.set(K.TASK_METRICS_UPDATE_INTERVAL_MS, "200")
+    conf.set(K.resource_key("worker", "memory"), "200m")
+    rc, client = run(conf, base("--executes", "alloc_memory.py", "--task_params", "600 60",
+                                "--conf", "tony.worker.instances=1", "--conf", "tony.ps.instances=0"))
+    assert rc == -1
+    tasks = {t.name: t for t in client.get_task_infos()} if hasattr(client, "get_task_infos") else {}
+    diag = open(os.path.join(client.job_dir, "logs", "amstderr.log")).read()
+    assert "memory limit" in diag, diag[-2000:]
+    assert tasks == {} or tasks["worker"].status == TaskStatus.FAILED
+
+
+def test_max_total_memory_rejected(conf):
+    """TonyClient.enforceResourceLimits (TonyClient.java:824-857): 3 x 2g > tony.task.max-total-memory."""
+    conf.set("tony.task.max-total-memory", "4096")
+    client = TonyClient(conf)
+    ok = client.init(base("--executes", "exit_0.py", "--conf", "tony.worker.instances=3",
+                          "--conf", "tony.worker.memory=2g", "--conf", "tony.ps.instances=0"))
+    assert not ok
+    conf.set("tony.task.max-total-memory", "6144")
+    assert TonyClient(conf).init(base("--executes", "exit_0.py", "--conf", "tony.worker.instances=3",
+                                      "--conf", "tony.worker.memory=2g", "--conf", "tony.ps.instances=0"))

@@ -184,15 +184,29 @@ class TaskExecutor:
         if port is not None:
             port.release()
 
+    def _on_fault(self, message: str) -> None:
+        """A GPU fault (new uncorrectable ECC errors) or a memory-limit breach: stop the user process
+        (its exit is then reported with the fault's exit status and diagnostic)."""
+        if "GPU fault" in message and not self.conf.get_bool(K.AMD_GPU_FAULT_STOPS_TASK, True):
+            return
+        LOG.error("[%s] stopping the task: %s", self.task_id, message)
+        if self.user_proc is not None:
+            self.user_proc.kill(signal.SIGKILL)
+
     # -- main ------------------------------------------------------------------------------------
     def run(self) -> int:
         self.localize(".")
         self.pin_cpus()
         self.setup_ports()
+        mem_limit = 0
+        if self.conf.get_bool(K.AMD_MEMORY_ENFORCED, True):
+            mem_limit = U.parse_memory_string(self.conf.get(K.resource_key(self.job_name, C.MEMORY),
+                                                            K.DEFAULT_MEMORY)) * 2 ** 20
         self.monitor = TaskMonitor(lambda: self.user_proc.pid if self.user_proc else os.getpid(), self.gpu_ids,
                                    self.conf.get_int(K.TASK_METRICS_UPDATE_INTERVAL_MS, 5000),
                                    lambda m: self.client.update_metrics(self.job_name, self.task_index, m),
-                                   self.conf.get_bool(K.TASK_GPU_METRICS_ENABLED, True))
+                                   self.conf.get_bool(K.TASK_GPU_METRICS_ENABLED, True),
+                                   on_fault=self._on_fault, memory_limit_bytes=mem_limit)
         self.monitor.start()
         self.cluster_spec = self.register_and_get_cluster_spec()
         LOG.info("[%s] got cluster spec: %s", self.task_id, self.cluster_spec)
@@ -202,6 +216,8 @@ class TaskExecutor:
             self.release_port(self.tb_port)
         try:
             exit_code = self.adapter.run()
+            if self.monitor.fault is not None and exit_code != 0:
+                exit_code = self.monitor.fault_code  # stopped by the agent: report why, not the signal
             self._skew_and_hang_if_testing()
             U.poll_till_non_null(lambda: self.client.register_execution_result(
                 exit_code, self.job_name, str(self.task_index), self.session_id), 1, 60)

@@ -56,7 +56,8 @@ def tree_rss_bytes(pid: int) -> int:
 
 class TaskMonitor:
     def __init__(self, pid_fn: Callable[[], Optional[int]], gpu_ids: List[int], interval_ms: int,
-                 push: Callable[[Dict[str, float]], None], gpu_metrics: bool = True):
+                 push: Callable[[Dict[str, float]], None], gpu_metrics: bool = True,
+                 on_fault: Optional[Callable[[str], None]] = None, memory_limit_bytes: int = 0):
         self.pid_fn = pid_fn
         self.gpu_ids = gpu_ids
         self.interval_s = max(0.05, interval_ms / 1000.0)
@@ -71,6 +72,9 @@ class TaskMonitor:
         self.ecc_base = None      # uncorrectable ECC count of the pinned GPUs when the task started
         self.ecc_new = 0          # uncorrectable errors raised since (a GPU fault: SURVEY.md §5.3)
         self.gpu_errors = 0
+        self.on_fault = on_fault              # called once with a diagnostic on a GPU fault / over-limit memory
+        self.memory_limit = int(memory_limit_bytes)
+        self.fault: Optional[str] = None
         self._stop = threading.Event()
         self._thread = threading.Thread(target=self._run, name="tony-task-monitor", daemon=True)
 
@@ -85,7 +89,11 @@ class TaskMonitor:
     def refresh(self) -> None:
         pid = self.pid_fn()
         if pid:
-            self.mem.add(float(tree_rss_bytes(pid)))
+            rss = float(tree_rss_bytes(pid))
+            self.mem.add(rss)
+            if self.memory_limit and rss > self.memory_limit:
+                self._raise_fault(f"memory limit: process tree RSS {rss / 2 ** 20:.0f} MiB > "
+                                  f"{self.memory_limit / 2 ** 20:.0f} MiB", C.EXIT_MEMORY_LIMIT)
         if self.gpu_metrics and self.gpu_errors < C.MAX_REPEATED_GPU_ERROR_ALLOWED:
             samples = [native.smi_sample(g) for g in self.gpu_ids]
             samples = [s for s in samples if s is not None]
@@ -106,6 +114,21 @@ class TaskMonitor:
                 LOG.error("GPU(s) %s raised %d new uncorrectable ECC error(s)", self.gpu_ids,
                           ecc - self.ecc_base - self.ecc_new)
                 self.ecc_new = ecc - self.ecc_base
+                self._raise_fault(f"GPU fault: {self.ecc_new} uncorrectable ECC error(s) on GPU(s) {self.gpu_ids}",
+                                  C.EXIT_GPU_FAULT)
+
+    def _raise_fault(self, message: str, code: int) -> None:
+        """First fault wins: record it and let the agent stop the task."""
+        if self.fault is not None:
+            return
+        self.fault = message
+        self.fault_code = code
+        LOG.error("%s", message)
+        if self.on_fault is not None:
+            try:
+                self.on_fault(message)
+            except Exception:  # noqa: BLE001
+                LOG.exception("fault handler failed")
 
     def metrics(self) -> Dict[str, float]:
         m = {C.MAX_MEMORY_BYTES: self.mem.max, C.AVG_MEMORY_BYTES: self.mem.avg}

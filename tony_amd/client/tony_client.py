@@ -230,9 +230,13 @@ class TonyClient:
             if not m or m.group(1) == "instances":
                 continue
             res = m.group(1)
-            limit = conf.get_int(key, -1)
-            want = sum(conf.get_int(K.resource_key(j, res), 0) * r.num_instances for j, r in requests.items()) \
-                if res != C.MEMORY else 0
+            # TonyClient.enforceResourceLimits (TonyClient.java:824-857): memory in MB ("2g" = 2048)
+            limit = U.parse_memory_string(conf.get(key)) if res == C.MEMORY else conf.get_int(key, -1)
+            want = 0
+            for j, r in requests.items():
+                v = conf.get(K.resource_key(j, res))
+                if v is not None:
+                    want += (U.parse_memory_string(v) if res == C.MEMORY else int(v)) * r.num_instances
             if 0 <= limit < want:
                 LOG.error("Job requests %d %s, %s is %d", want, res, key, limit)
                 return False

@@ -46,7 +46,7 @@ from ..events import schema as EV
 from ..events.handler import EventHandler
 from ..events.history import HistoryLayout, JobMetadata, year_month_day_dir
 from ..portal.history import write_owner
-from ..gpu.inventory import GpuAllocator, discover
+from ..gpu.inventory import GpuAllocator, discover, hip_ordinals
 from ..rpc import protocol as P
 from ..rpc.server import RpcServer
 from ..runtime.base import get_runtime
@@ -165,6 +165,8 @@ class Coordinator:
         fake = c.get_int(K.AMD_FAKE_GPUS, -1)
         devices = discover(fake)
         self.allocator = GpuAllocator(devices)
+        # amd-smi index -> HIP ordinal by PCI BDF (raises on a GPU HIP does not show: no silent mis-pinning)
+        self.hip_ordinal = hip_ordinals(devices)
         LOG.info("GPU inventory: %d device(s)%s", len(devices), " (fake)" if devices and devices[0].fake else "")
         self.hb = HeartbeatMonitor(self.hb_interval_ms, self.max_missed_hb, self._on_task_deemed_dead)
         self.hb.start()
@@ -359,7 +361,8 @@ class Coordinator:
                 task = self.session.init_task(req.job_name)
                 if task is None:
                     continue
-                slot = self.allocator.allocate(f"{task.id}@{task.session_id}", req.gpus) if req.gpus > 0 else None
+                slot = self.allocator.allocate(f"{task.id}@{task.session_id}", req.gpus, req.vcores) \
+                    if req.gpus > 0 else None
                 self._launch(task, req, slot)
             self.pending_requests = still
 
@@ -404,10 +407,13 @@ class Coordinator:
             if slot.cpus and c.get_bool(K.AMD_NUMA_BIND, True):
                 env["TONY_CPUS"] = ",".join(str(x) for x in slot.cpus)
             mode = c.get(K.AMD_VISIBLE_DEVICES_MODE, "hip").lower()
+            ordinals = ",".join(str(self.hip_ordinal.get(g, g)) for g in slot.gpus)
+            devs = {d.index: d for d in self.allocator.devices}
+            env["TONY_GPU_BDFS"] = ",".join(devs[g].bdf for g in slot.gpus if g in devs)
             if mode == "hip":
-                env[C.HIP_VISIBLE_DEVICES] = ids
+                env[C.HIP_VISIBLE_DEVICES] = ordinals
             elif mode == "rocr":
-                env[C.ROCR_VISIBLE_DEVICES] = ids
+                env[C.ROCR_VISIBLE_DEVICES] = ordinals
             task.info.gpus = ids
         if c.get_bool(K.DOCKER_ENABLED, False):
             image = c.get(K.docker_image_key(task.job_name)) or c.get(K.DOCKER_CONTAINERS_IMAGE, "")
@@ -458,7 +464,7 @@ class Coordinator:
         if self.session is None or task.session_id != self.session.session_id:
             return  # completion of a past session
         LOG.info("task %s finished with exit status %d", task.id, exit_code)
-        diag = None if exit_code == 0 else f"exit status {exit_code}"
+        diag = None if exit_code == 0 else C.EXIT_DIAGNOSTICS.get(exit_code, f"exit status {exit_code}")
         self.session.on_task_completed(task.job_name, task.task_index, exit_code, diag)
         if self.scheduler is not None:
             self.scheduler.register_dependency_completed(task.job_name)

@@ -119,6 +119,8 @@ AMD_CLIENT_POLL_MS = AMD + "client-poll-ms"                # client app-status p
 AMD_STAGING_DIR = AMD + "staging-dir"                      # job dirs (YARN app dir equivalent)
 AMD_PROFILE = AMD + "profile"                              # wrap tasks in rocprofv3 --kernel-trace --stats
 AMD_PROFILE_JOBTYPES = AMD + "profile.jobtypes"
+AMD_MEMORY_ENFORCED = AMD + "memory-enforced"              # stop tasks whose RSS exceeds tony.<job>.memory
+AMD_GPU_FAULT_STOPS_TASK = AMD + "gpu-fault-stops-task"    # new uncorrectable ECC errors stop the task
 
 # multi-value keys are appended (not overridden) by --conf (TonyConfigurationKeys.java:307-308)
 MULTI_VALUE_CONF = (CONTAINER_LAUNCH_ENV, EXECUTION_ENV, CONTAINERS_RESOURCES)

@@ -123,6 +123,11 @@ AVG_GPU_POWER_WATTS = "AVG_GPU_POWER_WATTS"
 MAX_GPU_TEMPERATURE = "MAX_GPU_TEMPERATURE"
 GPU_ECC_UNCORRECTABLE = "GPU_ECC_UNCORRECTABLE"  # new uncorrectable ECC errors on the task's GPUs
 MAX_REPEATED_GPU_ERROR_ALLOWED = 10
+# exit statuses the agent reports for failures the user process did not cause (coordinator diagnostics)
+EXIT_GPU_FAULT = 75          # new uncorrectable ECC errors on a pinned GPU: the task was stopped
+EXIT_MEMORY_LIMIT = 76       # the task's process tree exceeded tony.<job>.memory
+EXIT_DIAGNOSTICS = {EXIT_GPU_FAULT: "GPU fault: uncorrectable ECC errors on the task's GPU(s); task stopped",
+                    EXIT_MEMORY_LIMIT: "task exceeded its memory limit (tony.<job>.memory); task stopped"}
 
 # -- fault injection hooks (test-only env vars read by production code) -----------------
 TEST_AM_CRASH = "TEST_AM_CRASH"

@@ -11,7 +11,12 @@ single MI355X node the coordinator owns that decision:
   preferring GPUs that share a NUMA node (the 8 GPUs of an MI355X node hang off
   2 sockets; all pairs are xGMI-connected, so NUMA locality of the host side is
   the placement criterion that matters);
-* CPU pinning -- the task's CPUs are the cores of its first GPU's NUMA node.
+* CPU pinning -- a task gets ``tony.<job>.vcores`` CPUs of its first GPU's NUMA node, sliced so that
+  tasks on the same node get disjoint CPUs while there are enough (YARN's vcores as a cpuset);
+* device ordinals -- amd-smi enumerates GPUs in its own order, HIP in KFD-topology order;
+  ``hip_ordinals`` maps one to the other by PCI BDF so ``HIP_VISIBLE_DEVICES`` names the GPU the
+  allocator picked (and the NUMA binding matches it); the task re-checks the BDF it sees
+  (``verify_visible_device``, TONY_GPU_BDFS).
 """
 from __future__ import annotations
 
@@ -53,16 +58,92 @@ def num_numa_nodes() -> int:
     return max(1, len(glob.glob("/sys/devices/system/node/node[0-9]*")))
 
 
-def _kfd_devices() -> List[GpuDevice]:
+KFD_TOPOLOGY = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def _kfd_node_id(path: str) -> int:
+    try:
+        return int(os.path.basename(os.path.dirname(path)))
+    except ValueError:
+        return 1 << 30
+
+
+def kfd_gpu_bdfs(root: str = KFD_TOPOLOGY) -> List[str]:
+    """PCI BDFs ("dddd:bb:dd.f") of the GPU agents in KFD topology-node order -- the order in which
+    ROCr/HIP number devices (HIP ordinal i = i-th GPU node)."""
     out = []
-    for props in sorted(glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties")):
+    for props in sorted(glob.glob(os.path.join(root, "*", "properties")), key=_kfd_node_id):
         try:
             kv = dict(line.split() for line in open(props) if len(line.split()) == 2)
         except (OSError, ValueError):
             continue
         if int(kv.get("simd_count", "0")) <= 0:
             continue
-        out.append(GpuDevice(len(out), numa_node=int(kv.get("numa_node", "-1"))))
+        loc, dom = int(kv.get("location_id", "0")), int(kv.get("domain", "0"))
+        out.append(f"{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 0x7}")
+    return out
+
+
+def _norm_bdf(bdf: str) -> str:
+    """Canonical lower-case dddd:bb:dd.f (amd-smi may print without the domain or the function)."""
+    b = bdf.strip().lower()
+    if b.count(":") == 1:
+        b = "0000:" + b
+    if "." not in b:
+        b += ".0"
+    return b
+
+
+def hip_ordinals(devices: List[GpuDevice], kfd_bdfs: Optional[List[str]] = None) -> Dict[int, int]:
+    """amd-smi index -> HIP ordinal, matched by BDF.  Identity for fake inventories; raises when a
+    real GPU's BDF is not among the HIP-visible devices (wrong pinning must not pass silently)."""
+    if not devices or all(d.fake for d in devices):
+        return {d.index: d.index for d in devices}
+    kfd = [_norm_bdf(b) for b in (kfd_bdfs if kfd_bdfs is not None else kfd_gpu_bdfs())]
+    if not kfd:
+        LOG.warning("KFD topology unreadable: assuming amd-smi order == HIP order")
+        return {d.index: d.index for d in devices}
+    pos = {b: i for i, b in enumerate(kfd)}
+    out = {}
+    for d in devices:
+        if not d.bdf:
+            raise RuntimeError(f"GPU {d.index} has no PCI BDF: cannot map it to a HIP ordinal")
+        b = _norm_bdf(d.bdf)
+        if b not in pos:
+            raise RuntimeError(f"GPU {d.index} ({b}) is not among the HIP-visible devices {kfd}")
+        out[d.index] = pos[b]
+    return out
+
+
+def verify_visible_device(device_index: int = 0) -> Optional[str]:
+    """In a task: the BDF torch/HIP sees for ``device_index`` vs the one the coordinator pinned
+    (TONY_GPU_BDFS, same order as HIP_VISIBLE_DEVICES).  Returns the BDF; raises on a mismatch."""
+    want = [b for b in os.environ.get("TONY_GPU_BDFS", "").split(",") if b]
+    if not want or os.environ.get("HIP_VISIBLE_DEVICES") is None:
+        return None
+    import torch
+
+    p = torch.cuda.get_device_properties(device_index)
+    got = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+    exp = _norm_bdf(want[device_index])
+    if exp.rsplit(".", 1)[0] != got.rsplit(".", 1)[0]:
+        raise RuntimeError(f"HIP device {device_index} is {got} but the coordinator pinned {exp}: "
+                           "HIP_VISIBLE_DEVICES does not select the allocated GPU")
+    return got
+
+
+def _kfd_devices() -> List[GpuDevice]:
+    out = []
+    for props in sorted(glob.glob(os.path.join(KFD_TOPOLOGY, "*", "properties")), key=_kfd_node_id):
+        try:
+            kv = dict(line.split() for line in open(props) if len(line.split()) == 2)
+        except (OSError, ValueError):
+            continue
+        if int(kv.get("simd_count", "0")) <= 0:
+            continue
+        loc, dom = int(kv.get("location_id", "0")), int(kv.get("domain", "0"))
+        bdf = f"{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 0x7}"
+        out.append(GpuDevice(len(out), bdf=bdf, numa_node=int(kv.get("numa_node", "-1"))))
     return out
 
 
@@ -90,10 +171,12 @@ class Slot:
 
 
 class GpuAllocator:
-    def __init__(self, devices: List[GpuDevice]):
+    def __init__(self, devices: List[GpuDevice], cpus_of_node=None):
         self.devices = devices
         self._free = [d.index for d in devices]
         self._owner: Dict[int, str] = {}
+        self._cpu_owner: Dict[int, str] = {}
+        self._cpus_of_node = cpus_of_node or numa_cpus
         self._lock = threading.Lock()
 
     @property
@@ -104,8 +187,9 @@ class GpuAllocator:
         with self._lock:
             return len(self._free)
 
-    def allocate(self, owner: str, n: int) -> Optional[Slot]:
-        """Reserve ``n`` GPUs for ``owner`` (NUMA-local first); None if not enough are free."""
+    def allocate(self, owner: str, n: int, vcores: int = 0) -> Optional[Slot]:
+        """Reserve ``n`` GPUs for ``owner`` (NUMA-local first) and ``vcores`` CPUs of their NUMA node
+        (0: the whole node); None if not enough GPUs are free."""
         if n <= 0:
             return Slot([], -1, [])
         with self._lock:
@@ -128,7 +212,23 @@ class GpuAllocator:
                 self._free.remove(g)
                 self._owner[g] = owner
         node = self.devices[chosen[0]].numa_node
-        return Slot(chosen, node, numa_cpus(node) if node >= 0 else [])
+        return Slot(chosen, node, self._take_cpus(owner, node, vcores) if node >= 0 else [])
+
+    def _take_cpus(self, owner: str, node: int, vcores: int) -> List[int]:
+        """``vcores`` CPUs of ``node`` for ``owner``: unowned ones first, then (oversubscribed) the
+        least recently handed out; the whole node when vcores <= 0."""
+        cpus = self._cpus_of_node(node)
+        if vcores <= 0 or vcores >= len(cpus):
+            return list(cpus)
+        with self._lock:
+            free = [c for c in cpus if c not in self._cpu_owner]
+            take = free[:vcores]
+            if len(take) < vcores:
+                shared = [c for c in cpus if c not in take]
+                take += shared[:vcores - len(take)]
+            for c in take:
+                self._cpu_owner.setdefault(c, owner)
+        return sorted(take)
 
     def release(self, owner: str) -> None:
         with self._lock:
@@ -137,6 +237,9 @@ class GpuAllocator:
                     del self._owner[g]
                     self._free.append(g)
             self._free.sort()
+            for c, o in list(self._cpu_owner.items()):
+                if o == owner:
+                    del self._cpu_owner[c]
 
     def owners(self) -> Dict[int, str]:
         with self._lock:

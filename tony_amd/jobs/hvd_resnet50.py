@@ -1,10 +1,10 @@
 """ResNet-50 bf16 data-parallel training through the Horovod API (BASELINE.json config
 "horovod-on-tony ResNet-50 ring-allreduce bf16 on 8xMI355X").
 
-Per rank: the fused-kernel ResNet-50 (NHWC bf16, tony_amd BN/GEMM/residual HIP kernels, MIOpen
-for the spatial convs), synthetic ImageNet batches generated on the device, SGD-momentum through
-``hvd.DistributedOptimizer`` whose bucketed all-reduce (RCCL over xGMI) overlaps the backward
-pass.  Reports images/sec over all ranks.
+Per rank: the fused-kernel ResNet-50 (NHWC bf16, tony_amd conv/BN/GEMM/residual HIP kernels; MIOpen
+only for the 3-channel 7x7 stem), synthetic ImageNet batches generated on the device, SGD-momentum
+through ``hvd.DistributedOptimizer``: its bucketed all-reduce (RCCL over xGMI) overlaps the backward
+pass and the update is one fused HIP SGD launch per flat buffer.  Reports images/sec over all ranks.
 
   tony --src_dir tony_amd/jobs --executes hvd_resnet50.py --conf tony.application.framework=horovod \
        --conf tony.worker.instances=8 --conf tony.worker.gpus=1

@@ -65,6 +65,8 @@ class ConvBNAct(nn.Module):
             bn, c = self.bn, self.conv
             return conv_ops.conv_bn_act(x, c.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, c.stride,
                                         c.padding, self.training, bn.momentum, bn.eps, bn.relu, slot)
+        if self.fused and x.is_cuda:
+            conv_ops._record_unsupported("fwd", x.shape, self.conv.weight.shape, self.conv.stride, self.conv.padding)
         y = self.conv(x)
         if self.fused:
             return self.bn(y)

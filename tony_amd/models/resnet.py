@@ -4,11 +4,11 @@ on 8xMI355X"), NHWC / bf16, built from tony_amd's fused ops.
 Bottleneck schedule with ``fused=True`` (the default on the GPU):
 
 conv1  1x1 s1      MFMA GEMM with BN statistics in the epilogue + fused BN/ReLU apply
-conv2  3x3 s1|s2   MIOpen implicit GEMM -> fused BN+ReLU kernel
+conv2  3x3 s1|s2   tony_amd MFMA implicit GEMM (BN statistics epilogue) -> fused BN+ReLU apply
 conv3  1x1 s1      MFMA GEMM (+stats) -> ONE pass: BN apply + identity add + ReLU
                    (ops/residual.py); its backward writes d(conv3 out) and
                    d(identity) in the same pass
-downsample         1x1 s1|s2 conv (MIOpen) -> fused BN (no ReLU)
+downsample         1x1 s1|s2 conv (tony_amd implicit GEMM; strided dgrad per residue class) -> fused BN
 
 Architecture: torchvision's resnet50 (stride on the 3x3, "v1.5"); layer
 widths 64/128/256/512 x4, blocks [3, 4, 6, 3], 7x7/s2 stem + 3x3/s2 max pool,

@@ -78,6 +78,8 @@ _SIGNATURES = {
                       c_int, c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_int64, c_void_p],
     "tony_conv_dgrad": [c_void_p, c_int, c_int, c_int, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int,
                         c_void_p, c_int, c_int, c_int64, c_int, c_void_p],
+    "tony_conv_dgrad_strided": [c_void_p, c_int, c_int, c_int, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_int,
+                                c_int, c_int, c_int, c_void_p, c_int, c_int, c_int64, c_int, c_void_p],
     "tony_conv_wgrad": [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int, c_int, c_int, c_int,
                         c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_int_p, c_int, c_void_p],
     "tony_avgpool3_s1p1": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],

@@ -10,12 +10,11 @@ output disappears; the apply kernel normalises (+ReLU); the backward is the fuse
 followed by the dgrad / wgrad GEMMs on dZ.  Parameter gradients are accumulated in place into the
 flat gradient buffer when ``_lib.set_inplace_grads`` is on (the trainer's default).
 
-Per-shape selection.  For each (pass, shape) the first eager call times the tony kernel against
-MIOpen's solution on the real operands (the forward candidate pays for its BN statistics: MIOpen's
-output needs a separate ``tony_bn_stats`` pass) and caches the faster one -- the cudnn.benchmark
-idea applied across implementations.  Stride-2 backward-data has no tony kernel.  Decisions made
-before a HIP-graph capture are replayed by the capture; ``TONY_CONV_AUTOTUNE=0`` pins everything
-to the tony kernels.
+Per-shape selection.  Every (pass, shape) a tony kernel covers runs on it -- including strided
+backward-data (one MFMA launch per residue class of dX).  ``TONY_MIOPEN_CANDIDATES=1`` turns MIOpen
+into a per-shape autotune candidate (the first eager call times both on the real operands and
+caches the faster: A/B studies, test oracle).  Decisions made before a HIP-graph capture are
+replayed by the capture; ``choices()`` records every pass, MIOpen ones included.
 """
 from __future__ import annotations
 
@@ -136,25 +135,44 @@ def stem_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: 
     return y
 
 
+def dgrad_supported(x_shape, weight: torch.Tensor, stride=1, padding=0) -> bool:
+    """Whether a tony kernel computes this conv's input gradient (every stride <= 4, Cin % 8 == 0)."""
+    (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
+    r, s = weight.shape[2], weight.shape[3]
+    return x_shape[1] % 8 == 0 and 1 <= sh <= 4 and 1 <= sw <= 4 and 0 <= ph < r and 0 <= pw < s
+
+
 def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, padding=0,
                vflags: int | None = None) -> torch.Tensor:
-    if _pair(stride) != (1, 1) or x_shape[1] % 8:
-        return _miopen_dgrad(dy, weight, x_shape, stride, padding)
+    """dX of conv(x, w): stride 1 is one implicit-GEMM transposed conv; a strided conv is one
+    launch per residue class of dX (csrc/conv.hip tony_conv_dgrad_strided, no MIOpen)."""
+    if not dgrad_supported(x_shape, weight, stride, padding):
+        raise ValueError(f"conv_dgrad: unsupported x={tuple(x_shape)} w={tuple(weight.shape)} stride={stride} "
+                         f"padding={padding}")
     n, c, h, w = x_shape
     co, _, r, s = weight.shape
     dy, (_, _, lddy) = _as_rows(dy)
-    ph, pw = _pair(padding)
+    (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
     dx = _cl_empty(n, c, h, w, dy.device)
     wt = wt_cache.transposed(weight)
     L, st = _lib.lib(), _lib.stream_ptr(dy.device)
 
-    def launch(vf):
-        return L.tony_conv_dgrad(dy.data_ptr(), n, dy.shape[2], dy.shape[3], co, lddy, wt.data_ptr(), c, r, s, ph, pw,
-                                 dx.data_ptr(), h, w, c, vf, st)
+    if (sh, sw) == (1, 1):
+        def launch(vf):
+            return L.tony_conv_dgrad(dy.data_ptr(), n, dy.shape[2], dy.shape[3], co, lddy, wt.data_ptr(), c, r, s, ph,
+                                     pw, dx.data_ptr(), h, w, c, vf, st)
+        name = "tony_conv_dgrad"
+    else:
+        def launch(vf):
+            if (vf >> 8) & 0xff == 9:  # the halo tile variant is stride-1 only
+                return -3
+            return L.tony_conv_dgrad_strided(dy.data_ptr(), n, dy.shape[2], dy.shape[3], co, lddy, wt.data_ptr(), c,
+                                             r, s, sh, sw, ph, pw, dx.data_ptr(), h, w, c, vf, st)
+        name = "tony_conv_dgrad_strided"
 
     vf = vflags if vflags is not None else tune.pick(("conv_dgrad", tuple(dy.shape), lddy, tuple(weight.shape),
-                                                         (ph, pw)), launch)
-    _lib.check(launch(vf), "tony_conv_dgrad")
+                                                         (sh, sw), (ph, pw)), launch)
+    _lib.check(launch(vf), name)
     return dx
 
 
@@ -216,18 +234,32 @@ def _time(fn: Callable[[], object], reps: int = 5) -> float:
     return tune.time_ms(fn, reps)
 
 
+# MIOpen is a per-shape autotune candidate only when TONY_MIOPEN_CANDIDATES=1 (A/B studies and as a
+# test oracle); by default every conv pass tony_amd has a kernel for runs on it, and MIOpen serves
+# only what has none (recorded as such in choices(), so bench's conv_impl shows every MIOpen use).
+MIOPEN_CANDIDATES = os.environ.get("TONY_MIOPEN_CANDIDATES", "0") == "1"
+
+
 def _choose(key: Tuple, candidates: Dict[str, Callable[[], object]], default: str = "tony",
             weight: Dict[str, float] | None = None) -> str:
     """Fastest candidate for ``key`` (cached); ``weight`` scales a candidate's measured time."""
     c = _CHOICE.get(key)
     if c is not None:
         return c
+    if not MIOPEN_CANDIDATES and len(candidates) > 1:
+        candidates = {k: v for k, v in candidates.items() if k != "miopen"}
     if not AUTOTUNE or len(candidates) == 1 or torch.cuda.is_current_stream_capturing():
-        return default if default in candidates else next(iter(candidates))
-    times = {name: _time(fn) * (weight or {}).get(name, 1.0) for name, fn in candidates.items()}
-    c = min(times, key=times.get)
+        c = default if default in candidates else next(iter(candidates))
+    else:
+        times = {name: _time(fn) * (weight or {}).get(name, 1.0) for name, fn in candidates.items()}
+        c = min(times, key=times.get)
     _CHOICE[key] = c
     return c
+
+
+def _record_unsupported(pas: str, x_shape, w_shape, stride, padding) -> None:
+    """Count a conv pass no tony kernel takes (MIOpen) in choices()."""
+    _CHOICE.setdefault((pas, tuple(x_shape), tuple(w_shape), _pair(stride), _pair(padding)), "miopen")
 
 
 def choices() -> Dict[Tuple, str]:
@@ -256,7 +288,7 @@ def _dgrad(dy, weight, x_shape, stride, padding):
     if impl == "miopen":
         return _miopen_dgrad(dy, weight, x_shape, stride, padding)
     cands = {"miopen": lambda: _miopen_dgrad(dy, weight, x_shape, stride, padding)}
-    if _pair(stride) == (1, 1) and x_shape[1] % 8 == 0:
+    if dgrad_supported(x_shape, weight, stride, padding):
         cands["tony"] = lambda: conv_dgrad(dy, weight, x_shape, stride, padding)
     impl = _choose(key, cands)
     return conv_dgrad(dy, weight, x_shape, stride, padding) if impl == "tony" else \
@@ -274,6 +306,7 @@ def _wgrad(dy, x, weight, stride, padding):
     impl = _CHOICE.get(key) or WGRAD_IMPL or None
     if x.shape[1] % 8:
         impl = "miopen"  # 3-channel stem: no tony weight-gradient kernel
+        _CHOICE.setdefault(key, impl)
     if impl is None:
         # With the weight gradients on the side stream (ops/streams.py) their GPU time hides behind the
         # data-gradient chain, while MIOpen's costs 3 more launches (output fill, fp32->bf16 cast, add
@@ -335,6 +368,8 @@ class _ConvFn(torch.autograd.Function):
 def conv2d(x, weight, stride=1, padding=0):
     if supported(x, weight, stride, padding):
         return _ConvFn.apply(x, weight, _pair(stride), _pair(padding))
+    if x.is_cuda:
+        _record_unsupported("fwd", x.shape, weight.shape, stride, padding)
     return torch.nn.functional.conv2d(x, weight, None, stride, padding)
 
 
@@ -469,6 +504,8 @@ def conv_bn_act(x, weight, gamma, beta, running_mean, running_var, stride=1, pad
     if supported(x, weight, stride, padding) or (STEM and stem_supported(x, weight, stride, padding)):
         return _ConvBNActFn.apply(x, weight, gamma, beta, running_mean, running_var, _pair(stride), _pair(padding),
                                   training, momentum, eps, relu, slot)
+    if x.is_cuda:
+        _record_unsupported("fwd", x.shape, weight.shape, stride, padding)
     z = torch.nn.functional.conv2d(x, weight, None, stride, padding)
     y = torch.nn.functional.batch_norm(z, running_mean, running_var, gamma, beta, training, momentum, eps)
     return torch.relu(y) if relu else y

@@ -100,12 +100,44 @@ __device__ __forceinline__ void store_rows(uint16_t* lds, const uint4* regs) {
   }
 }
 
-// C[M, N] = gather(A)[M, K] * B[N, K]^T  (forward and stride-1 dgrad)
-template <int BM, int BN>
+// One residue class of a strided backward-data conv (tony_conv_dgrad_strided): the dX pixels
+// (iy, ix) with iy % sh == py, ix % sw == px only receive the filter taps r = r0 + sh*a,
+// s = s0 + sw*b, so they form a stride-1 transposed conv over the class's sub-grid with that
+// reduced filter.  The A operand is the usual flipped-tap gather of dY (Gather over the taps (a, b));
+// B rows are read straight out of the full transposed filter Wt [Ci][R][S][Co] at the class's taps
+// (no per-class weight copies), and the epilogue scatters GEMM rows back to the class's pixels.
+struct Phase {
+  int R, S;      // taps of the full filter: Wt row layout [R][S][Co]
+  int r0, s0;    // the class's first tap
+  int tsy, tsx;  // tap step (= conv stride)
+  RowMap rows;   // GEMM row -> dX pixel
+};
+
+// B rows [row0, row0 + ROWS) x this thread's K chunk, where the K position is the thread's A tap
+// (the A and B chunk columns of conv_nt_kernel coincide: both are threadIdx.x & 7)
+template <int ROWS>
+__device__ __forceinline__ void load_rows_phase(uint4* regs, const uint16_t* __restrict__ B, const Phase& ph,
+                                                const Gather& g, const TapPos& t, int row0, int nrows) {
+  constexpr int VEC = ROWS * BK / 8 / kThreads;
+  const int64_t ldb = static_cast<int64_t>(ph.R) * ph.S * g.Cs;
+  const int64_t koff = (static_cast<int64_t>(ph.r0 + ph.tsy * t.r) * ph.S + ph.s0 + ph.tsx * t.s) * g.Cs + t.c;
+  const bool kok = t.r < g.R;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    const int gr = row0 + ((threadIdx.x + i * kThreads) >> 3);
+    if (kok && gr < nrows)
+      regs[i] = *reinterpret_cast<const uint4*>(B + static_cast<int64_t>(gr) * ldb + koff);
+    else
+      regs[i] = make_uint4(0, 0, 0, 0);
+  }
+}
+
+// C[M, N] = gather(A)[M, K] * B[N, K]^T  (forward and stride-1 dgrad; PH: one class of a strided dgrad)
+template <int BM, int BN, bool PH = false>
 __global__ __launch_bounds__(kThreads) void conv_nt_kernel(Gather g, const uint16_t* __restrict__ B,
                                                            uint16_t* __restrict__ C, int64_t ldc, int M, int N,
                                                            float* __restrict__ stats, int64_t sstride,
-                                                           int epi, int tiles_n) {
+                                                           int epi, int tiles_n, Phase ph) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int AV = BM * BK / 8 / kThreads, BV = BN * BK / 8 / kThreads;
@@ -145,7 +177,10 @@ __global__ __launch_bounds__(kThreads) void conv_nt_kernel(Gather g, const uint1
   const int nk = (K + BK - 1) / BK;
 #pragma unroll
   for (int i = 0; i < AV; ++i) ra[i] = gather16(g, rs[i], tp);
-  load_rows<BN>(rb, B, K, n0, N, 0, K);
+  if constexpr (PH)
+    load_rows_phase<BN>(rb, B, ph, g, tp, n0, N);
+  else
+    load_rows<BN>(rb, B, K, n0, N, 0, K);
   store_rows<BM>(smem, ra);
   store_rows<BN>(smem + BM * BK, rb);
   __syncthreads();
@@ -158,7 +193,10 @@ __global__ __launch_bounds__(kThreads) void conv_nt_kernel(Gather g, const uint1
       tp.advance(BK, g);
 #pragma unroll
       for (int i = 0; i < AV; ++i) ra[i] = gather16(g, rs[i], tp);
-      load_rows<BN>(rb, B, K, n0, N, (kt + 1) * BK, K);
+      if constexpr (PH)
+        load_rows_phase<BN>(rb, B, ph, g, tp, n0, N);
+      else
+        load_rows<BN>(rb, B, K, n0, N, (kt + 1) * BK, K);
     }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -184,37 +222,37 @@ __global__ __launch_bounds__(kThreads) void conv_nt_kernel(Gather g, const uint1
   // inference BN (H5), bit2: ReLU after it
   nt_epilogue<BM, BN, TM, TN>(acc, smem, C, ldc, M, N, m0, n0,
                                (epi & 1) ? stats + shard_off(tm, sstride) : nullptr,
-                               (epi & 2) ? stats : nullptr, (epi & 4) != 0);
+                               (epi & 2) ? stats : nullptr, (epi & 4) != 0, PH ? ph.rows : RowMap{});
 }
 
-template <int BM, int BN>
+template <int BM, int BN, bool PH>
 int launch_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, float* stats,
-              int64_t sstride, int epi, hipStream_t stream) {
+              int64_t sstride, int epi, const Phase& ph, hipStream_t stream) {
   const int tiles_m = ceil_div(M, BM), tiles_n = ceil_div(N, BN);
   const int64_t tiles = static_cast<int64_t>(tiles_m) * tiles_n;
   if (tiles > 0x7fffffff) return -2;
-  conv_nt_kernel<BM, BN><<<static_cast<int>(tiles), kThreads, 0, stream>>>(
+  conv_nt_kernel<BM, BN, PH><<<static_cast<int>(tiles), kThreads, 0, stream>>>(
       g, static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), ldc, static_cast<int>(M), static_cast<int>(N),
-      stats, sstride, epi, tiles_n);
+      stats, sstride, epi, tiles_n, ph);
   TONY_LAUNCH_CHECK();
   return 0;
 }
 
-template <int BM>
+template <int BM, bool PH = false>
 int launch_nt_bm(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, float* st,
-                 int64_t sstride, int epi, int64_t bn, hipStream_t stream) {
+                 int64_t sstride, int epi, int64_t bn, hipStream_t stream, const Phase& ph = Phase{}) {
   if constexpr (BM == 256) {  // 8 x TN accumulators per wave: only narrow column tiles fit the registers
-    if (bn <= 32) return launch_nt<256, 32>(g, B, C, ldc, M, N, st, sstride, epi, stream);
-    if (bn <= 64) return launch_nt<256, 64>(g, B, C, ldc, M, N, st, sstride, epi, stream);
+    if (bn <= 32) return launch_nt<256, 32, PH>(g, B, C, ldc, M, N, st, sstride, epi, ph, stream);
+    if (bn <= 64) return launch_nt<256, 64, PH>(g, B, C, ldc, M, N, st, sstride, epi, ph, stream);
     return -3;
   } else {
     switch (bn) {
-      case 32: return launch_nt<BM, 32>(g, B, C, ldc, M, N, st, sstride, epi, stream);
-      case 64: return launch_nt<BM, 64>(g, B, C, ldc, M, N, st, sstride, epi, stream);
-      case 96: return launch_nt<BM, 96>(g, B, C, ldc, M, N, st, sstride, epi, stream);
-      case 128: return launch_nt<BM, 128>(g, B, C, ldc, M, N, st, sstride, epi, stream);
-      case 160: return launch_nt<BM, 160>(g, B, C, ldc, M, N, st, sstride, epi, stream);
-      default: return launch_nt<BM, 192>(g, B, C, ldc, M, N, st, sstride, epi, stream);
+      case 32: return launch_nt<BM, 32, PH>(g, B, C, ldc, M, N, st, sstride, epi, ph, stream);
+      case 64: return launch_nt<BM, 64, PH>(g, B, C, ldc, M, N, st, sstride, epi, ph, stream);
+      case 96: return launch_nt<BM, 96, PH>(g, B, C, ldc, M, N, st, sstride, epi, ph, stream);
+      case 128: return launch_nt<BM, 128, PH>(g, B, C, ldc, M, N, st, sstride, epi, ph, stream);
+      case 160: return launch_nt<BM, 160, PH>(g, B, C, ldc, M, N, st, sstride, epi, ph, stream);
+      default: return launch_nt<BM, 192, PH>(g, B, C, ldc, M, N, st, sstride, epi, ph, stream);
     }
   }
 }
@@ -426,6 +464,23 @@ int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int6
     case 64: return launch_nt_bm<64>(g, B, C, ldc, M, N, st, sstride, epi, bn, stream);
     case 128: return launch_nt_bm<128>(g, B, C, ldc, M, N, st, sstride, epi, bn, stream);
     default: return launch_nt_bm<256>(g, B, C, ldc, M, N, st, sstride, epi, bn, stream);
+  }
+}
+
+// One residue class of a strided dgrad with tile variant v (flags bits 8..15 of tony_conv_dgrad_strided).
+int run_nt_phase(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, int v, const Phase& ph,
+                 hipStream_t stream) {
+  if (v == kHaloVariant || v >= kNumNtVariants) return -1;
+  if (v == 0) {
+    const int64_t bn = pick_bn(N, 192);
+    return bn <= 64 ? launch_nt_bm<256, true>(g, B, C, ldc, M, N, nullptr, 0, 0, bn, stream, ph)
+                    : launch_nt_bm<128, true>(g, B, C, ldc, M, N, nullptr, 0, 0, bn, stream, ph);
+  }
+  const int64_t bn = pick_bn(N, kNtVariants[v].cap);
+  switch (kNtVariants[v].bm) {
+    case 64: return launch_nt_bm<64, true>(g, B, C, ldc, M, N, nullptr, 0, 0, bn, stream, ph);
+    case 128: return launch_nt_bm<128, true>(g, B, C, ldc, M, N, nullptr, 0, 0, bn, stream, ph);
+    default: return launch_nt_bm<256, true>(g, B, C, ldc, M, N, nullptr, 0, 0, bn, stream, ph);
   }
 }
 
@@ -792,6 +847,48 @@ TONY_API int tony_conv_dgrad(const void* dy, int N, int OH, int OW, int Co, int6
   if (M > 0x7fffffff || static_cast<int64_t>(N) * OH * OW > 0x7fffffff) return -1;
   Gather g{static_cast<const uint16_t*>(dy), lddy, OH, OW, Co, H, W, R, S, 1, 1, ph, pw, -1, R * S * Co, N};
   return run_nt(g, wt, dx, lddx, M, C, flags & 0xff00, nullptr, 0, stream);
+}
+
+// dX[N*H*W, C] (row stride lddx) of a STRIDED conv (stride sh x sw, padding ph, pw): one MFMA
+// implicit-GEMM launch per residue class (iy % sh, ix % sw) of dX, each a stride-1 transposed conv
+// over the class's sub-grid with the class's taps of Wt = W permuted to [C][R][S][Co] (Phase).
+// Every dX pixel is written exactly once (classes with no taps write zeros).  flags bits 8..15:
+// tile variant (run_nt_phase).
+TONY_API int tony_conv_dgrad_strided(const void* dy, int N, int OH, int OW, int Co, int64_t lddy, const void* wt,
+                                     int C, int R, int S, int sh, int sw, int ph, int pw, void* dx, int H, int W,
+                                     int64_t lddx, int flags, hipStream_t stream) {
+  if (bad_geom(Co, lddy, dy) || (reinterpret_cast<uintptr_t>(wt) & 15) || C <= 0 || C % 8 || (lddx % 8) ||
+      (reinterpret_cast<uintptr_t>(dx) & 15))
+    return -1;
+  if (sh < 1 || sw < 1 || sh > 4 || sw > 4 || ph < 0 || pw < 0 || ph >= R || pw >= S) return -1;
+  if (OH != (H + 2 * ph - R) / sh + 1 || OW != (W + 2 * pw - S) / sw + 1 || OH <= 0 || OW <= 0) return -1;
+  if (static_cast<int64_t>(N) * H * W > 0x7fffffff || static_cast<int64_t>(N) * OH * OW > 0x7fffffff) return -1;
+  const int v = (flags >> 8) & 0xff;
+  for (int py = 0; py < sh; ++py) {
+    for (int px = 0; px < sw; ++px) {
+      const int QH = H > py ? (H - py + sh - 1) / sh : 0, QW = W > px ? (W - px + sw - 1) / sw : 0;
+      const int64_t M = static_cast<int64_t>(N) * QH * QW;
+      if (M == 0) continue;
+      // taps r = r0 + sh*a reach the pixels iy = sh*qy + py:  oy = (iy + ph - r) / sh = qy + cy - a
+      const int r0 = (py + ph) % sh, s0 = (px + pw) % sw;
+      int Ra = r0 < R ? (R - r0 + sh - 1) / sh : 0, Sb = s0 < S ? (S - s0 + sw - 1) / sw : 0;
+      const int cy = (py + ph - r0) / sh, cx = (px + pw - s0) / sw;
+      if (Ra == 0 || Sb == 0) Ra = 0, Sb = 1;  // no taps: the GEMM has K = 0 and writes zeros
+      Gather g{static_cast<const uint16_t*>(dy), lddy, OH, OW, Co, QH, QW, Ra, Sb, 1, 1, cy, cx, -1, Ra * Sb * Co, N};
+      Phase phz{R, S, r0, s0, sh, sw, RowMap{}};
+      phz.rows.qw = QW;
+      phz.rows.qhw = QH * QW;
+      phz.rows.W = W;
+      phz.rows.HW = H * W;
+      phz.rows.sy = sh;
+      phz.rows.sx = sw;
+      phz.rows.y0 = py;
+      phz.rows.x0 = px;
+      const int rc = run_nt_phase(g, wt, dx, lddx, M, C, v, phz, stream);
+      if (rc != 0) return rc;
+    }
+  }
+  return 0;
 }
 
 // dW (fp32 [Co][R][S][C], zero on entry) = dY^T im2col(X); dY [N*OH*OW, Co] row stride lddy.

@@ -93,6 +93,21 @@ constexpr NtVariant kNtVariants[] = {{0, 0},    {64, 192},  {128, 192}, {256, 64
                                      {128, 96}, {128, 128}, {64, 128},  {256, 32}};
 constexpr int kNumNtVariants = sizeof(kNtVariants) / sizeof(kNtVariants[0]);
 
+// Output-row remap of the NT epilogue: GEMM row m -> output pixel.  Identity when qw == 0; else
+// m = (n, qy, qx) over an [N][QH][QW] sub-grid of an [N][H][W] image and the pixel is
+// n*HW + (qy*sy + y0)*W + qx*sx + x0 (one phase of a stride-2 backward-data conv).
+struct RowMap {
+  int qw = 0, qhw = 0;  // sub-grid width and height*width
+  int W = 0, HW = 0;    // image width and height*width
+  int sy = 1, sx = 1, y0 = 0, x0 = 0;
+  __device__ __forceinline__ int64_t pixel(int m) const {
+    if (qw == 0) return m;
+    const int n = m / qhw, rem = m - n * qhw;
+    const int qy = rem / qw, qx = rem - qy * qw;
+    return static_cast<int64_t>(n) * HW + (qy * sy + y0) * W + qx * sx + x0;
+  }
+};
+
 // NT epilogue: optional per-column BN statistics from the fp32 accumulators, then the bf16 tile
 // staged through LDS (rows padded by 16 B) and written with 16-byte coalesced stores.
 // acc layout of 16x16 MFMA: col = lane&15, row = (lane>>4)*4 + r.
@@ -101,7 +116,8 @@ constexpr int kNumNtVariants = sizeof(kNtVariants) / sizeof(kNtVariants[0]);
 template <int BM, int BN, int TM, int TN>
 __device__ __forceinline__ void nt_epilogue(f32x4 (&acc)[TM][TN], uint16_t* smem, uint16_t* __restrict__ C,
                                             int64_t ldc, int M, int N, int m0, int n0, float* __restrict__ stats,
-                                            const float* __restrict__ aff = nullptr, bool relu = false) {
+                                            const float* __restrict__ aff = nullptr, bool relu = false,
+                                            const RowMap rm = RowMap{}) {
   constexpr int WM = BM / 2, WN = BN / 2;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -166,7 +182,7 @@ __device__ __forceinline__ void nt_epilogue(f32x4 (&acc)[TM][TN], uint16_t* smem
     const int grow = m0 + row, gcol = n0 + ch * 8;
     if (grow >= M || gcol >= N) continue;
     const uint16_t* src = Cs + row * LDC + ch * 8;
-    uint16_t* dst = C + static_cast<int64_t>(grow) * ldc + gcol;
+    uint16_t* dst = C + rm.pixel(grow) * ldc + gcol;
     if (gcol + 8 <= N && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
       *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
     } else {

@@ -40,6 +40,9 @@ def pick_device(local_rank: int) -> torch.device:
     n = torch.cuda.device_count()
     dev = torch.device("cuda", local_rank % n)
     torch.cuda.set_device(dev)
+    from ..gpu.inventory import verify_visible_device
+
+    verify_visible_device(dev.index)  # the coordinator's pinned BDF == the device HIP shows (raises if not)
     return dev
 
 

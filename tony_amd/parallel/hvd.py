@@ -333,7 +333,7 @@ class _DistributedOptimizer:
 
     def __init__(self, optimizer, named_parameters=None, compression=Compression.none,
                  backward_passes_per_step: int = 1, op=Average, bucket_mb: float = DEFAULT_BUCKET_MB,
-                 gradient_predivide_factor: float = 1.0):
+                 gradient_predivide_factor: float = 1.0, fused: Optional[bool] = None):
         _need_init()
         if op not in (Average, Sum):
             raise ValueError("DistributedOptimizer supports op=Average or op=Sum")
@@ -365,6 +365,24 @@ class _DistributedOptimizer:
             red.passes_per_reduce = self.backward_passes_per_step
             red.register_hooks()
             self.groups.append((flat, red))
+        # fused apply: a single-group torch SGD on GPU tensors becomes ONE fused HIP SGD-momentum launch
+        # per flat buffer (fp32 master + momentum, writes the bf16 compute copy; ops/optim.py)
+        self._fused = []
+        can_fuse = (isinstance(optimizer, torch.optim.SGD) and len(optimizer.param_groups) == 1
+                    and all(f.device.type == "cuda" for f, _ in self.groups)
+                    and not optimizer.param_groups[0].get("dampening", 0)
+                    and not optimizer.param_groups[0].get("maximize", False))
+        if fused is None:
+            fused = can_fuse
+        elif fused and not can_fuse:
+            raise ValueError("fused=True needs a single-group, dampening-free torch.optim.SGD on GPU tensors")
+        if fused:
+            from ..ops.optim import FlatSGD
+
+            g = optimizer.param_groups[0]
+            for flat, _ in self.groups:
+                self._fused.append((flat, FlatSGD(flat.data.float().clone(), g["lr"], momentum=g["momentum"],
+                                                  weight_decay=g["weight_decay"], nesterov=g["nesterov"])))
 
     # torch.optim.Optimizer surface
     @property
@@ -391,7 +409,18 @@ class _DistributedOptimizer:
 
     def step(self, closure=None):
         """Call after ``backward_passes_per_step`` backward passes (their sum is averaged)."""
-        return self.optimizer.step(closure)
+        if not self._fused:
+            return self.optimizer.step(closure)
+        loss = closure() if closure is not None else None
+        g = self.optimizer.param_groups[0]  # lr schedules edit the wrapped optimizer's group
+        for flat, opt in self._fused:
+            opt.lr, opt.momentum, opt.weight_decay = g["lr"], g["momentum"], g["weight_decay"]
+            if flat.data.dtype == torch.bfloat16:
+                opt.step(flat.grad, out_bf16=flat.data)
+            else:
+                opt.step(flat.grad)
+                flat.data.copy_(opt.w)
+        return loss
 
     def __getattr__(self, name):
         return getattr(self.optimizer, name)
@@ -399,6 +428,8 @@ class _DistributedOptimizer:
 
 def DistributedOptimizer(optimizer, named_parameters=None, compression=Compression.none,  # noqa: N802
                          backward_passes_per_step: int = 1, op=Average, **kw):
+    """Horovod's DistributedOptimizer: bucketed gradient averaging overlapped with backward; a plain
+    torch SGD on GPU tensors is applied by the fused HIP kernel (``fused=False`` keeps torch's)."""
     return _DistributedOptimizer(optimizer, named_parameters, compression, backward_passes_per_step, op, **kw)
 
 

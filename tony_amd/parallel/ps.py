@@ -71,7 +71,7 @@ class ParameterServer:
     def __init__(self, model: torch.nn.Module, optimizer: str = "sgd", lr: float = 0.1, momentum: float = 0.9,
                  weight_decay: float = 0.0, mode: str = "colocated", sync: bool = True, ps_ranks=(0,),
                  group=None, dtype=torch.bfloat16, device=None, wire_dtype: Optional[torch.dtype] = None,
-                 bucket_mb: float = DEFAULT_BUCKET_MB, **opt_kw):
+                 bucket_mb: float = DEFAULT_BUCKET_MB, bucketed_single: bool = False, **opt_kw):
         self.mode = mode
         self.sync = sync
         self.group = group
@@ -90,6 +90,7 @@ class ParameterServer:
         else:
             raise ValueError(f"unknown PS mode {mode!r}")
         self.is_ps = self.rank in self.ps_ranks
+        self._begun = False
         self.is_worker = self.rank in self.worker_ranks
         n_split = self.world if mode == "colocated" else 1
         # every bucket must split into n_split pieces of whole 16-byte vectors (8 bf16)
@@ -106,8 +107,10 @@ class ParameterServer:
         self._master_range: List[Optional[tuple]] = [None] * len(self.buckets)
         f = self.flat
         if mode == "colocated":
+            # master pieces in flat order (ascending lo): with one rank the master shard IS the flat
+            # buffer's layout and the whole update is one fused launch
             pieces, m = [], 0
-            for b in self.buckets:
+            for b in sorted(self.buckets, key=lambda b: b.lo):
                 p = b.numel // n_split
                 self._master_range[b.index] = (m, p)
                 pieces.append(f.data[b.lo + self.rank * p:b.lo + (self.rank + 1) * p])
@@ -137,7 +140,11 @@ class ParameterServer:
         if self.world > 1 and self.wire_dtype != f.grad.dtype:
             self._wire = torch.zeros(f.numel, dtype=self.wire_dtype, device=f.device)
         self.engine = GradBucketEngine(f, self.buckets, self._launch)
-        if mode == "colocated" or sync:
+        # one rank: nothing to communicate, so nothing to overlap -- the step is ONE fused apply over
+        # the whole shard after backward, with no per-parameter readiness bookkeeping on the host
+        # (``bucketed_single`` keeps the bucket engine: tests of the overlap machinery on one GPU)
+        self.single = mode == "colocated" and self.world == 1 and not bucketed_single
+        if (mode == "colocated" or sync) and not self.single:
             self.engine.attach()
 
     # -- helpers ---------------------------------------------------------------
@@ -163,6 +170,9 @@ class ParameterServer:
             return
         for opt in self.optimizers.values():
             opt.begin_step()
+        if self.single:
+            self._begun = True
+            return
         if self.mode == "dedicated" and not self.is_worker:
             self.flat.grad.zero_()  # a PS-only rank contributes nothing to the pushed sums
             overlap = False         # and runs no backward: all buckets go in order from step()
@@ -172,6 +182,14 @@ class ParameterServer:
         """Finish push (gradients) -> apply (fused optimizer on the PS) -> pull (variables)."""
         if self.mode == "dedicated" and not self.sync:
             self._step_dedicated_async_worker()
+            self.steps += 1
+            return
+        if self.single:
+            if not self._begun:
+                self.begin_step()
+            self._begun = False
+            opt = self.optimizers[self.rank]
+            self._apply(opt, self.flat.grad, 0, self.flat.data)
             self.steps += 1
             return
         if not self.engine.armed:

@@ -6,7 +6,8 @@ standard variables so ``init_process_group("nccl")`` -- RCCL over xGMI on
 MI355X -- works without arguments: MASTER_ADDR / MASTER_PORT (worker:0's
 reserved port, released by its agent just before the user process starts so
 rank 0 can host the c10d TCPStore there), WORLD_SIZE, LOCAL_RANK,
-LOCAL_WORLD_SIZE.  GPU pinning variables come from the agent (agent/pinning.py).
+LOCAL_WORLD_SIZE.  GPU pinning variables (HIP_VISIBLE_DEVICES, TONY_CPUS) come from the coordinator's
+slot assignment (cluster/coordinator.py, gpu/inventory.py).
 """
 from __future__ import annotations
 

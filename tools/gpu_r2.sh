@@ -18,6 +18,12 @@ for s in "$@"; do
     tests) step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
     bench) step bench 900 python bench.py --steps 20 --warmup 6 --tune-cache gpurun_out/tune.json ;;
     bench2) step bench2_gloo 900 env TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 6 --warmup 3 --mode eager ;;
+    conv) step conv 400 python -u -m pytest tests/test_conv_gpu.py -x -v --timeout 200 --timeout-method thread ;;
+    xgmi) step xgmi 300 python -u -m pytest tests/test_xgmi_gpu.py -x -v --timeout 200 --timeout-method thread ;;
+    bench_fp32) step bench_fp32 900 python bench.py --steps 10 --warmup 4 --dtype fp32 --mode eager ;;
+    bench_gradfp32) step bench_gradfp32 900 python bench.py --steps 20 --warmup 6 --grad-dtype fp32 --tune-cache gpurun_out/tune.json ;;
+    bench_nooverlap) step bench_nooverlap 900 python bench.py --steps 20 --warmup 6 --no-overlap --mode eager --tune-cache gpurun_out/tune.json ;;
+    bench2_ded) step bench2_ded 900 env TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 3 --warmup 2 --mode eager --ps-mode dedicated ;;
     prof) export TMPDIR=/tmp; R=$(pwd)
           step prof 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 5 --mode eager ${BENCH_ARGS:-}
           python3 tools/prof_summary.py gpurun_out/prof --skip 6 > gpurun_out/prof_summary.md; find gpurun_out/prof -name '*trace*' -delete ;;
