@@ -611,3 +611,44 @@ def test_allocator_slices_numa_cpus_by_vcores():
     assert s3.cpus == s1.cpus                        # released CPUs are handed out again
     big = a.allocate("w4", 1, vcores=12)             # only 4 unowned left on node 0: oversubscribe
     assert len(big.cpus) == 12
+
+
+def test_task_monitor_gpu_fault_and_xgmi_rates(monkeypatch):
+    """New uncorrectable ECC errors on a pinned GPU call the agent's fault handler once (it stops the
+    task); xGMI GB/s come from amd-smi's accumulated per-link KB counters."""
+    from tony_amd import constants as C
+    from tony_amd import native
+    from tony_amd.agent import monitor as M
+
+    state = {"ecc": 0, "rd": 0, "t": 100.0}
+
+    def sample(_gpu):
+        return native.GpuSample(50, 10, 1000, 2000, 500.0, 60.0, 0, state["ecc"], state["rd"], state["rd"] // 2, 64)
+
+    monkeypatch.setattr(native, "smi_sample", sample)
+    monkeypatch.setattr(M.time, "monotonic", lambda: state["t"])
+    faults = []
+    mon = M.TaskMonitor(lambda: None, [0], 1000, lambda m: None, True, on_fault=faults.append)
+    mon.refresh()
+    state["rd"], state["t"] = 2_000_000, 101.0   # 2 GB read over 1 s
+    mon.refresh()
+    assert faults == [] and mon.fault is None
+    state["ecc"], state["t"] = 3, 102.0
+    mon.refresh()
+    mon.refresh()
+    assert len(faults) == 1 and "uncorrectable ECC" in faults[0] and mon.fault_code == C.EXIT_GPU_FAULT
+    m = mon.metrics()
+    assert m[C.GPU_ECC_UNCORRECTABLE] == 3.0
+    assert m[C.MAX_XGMI_READ_GBPS] == pytest.approx(2.0) and m[C.MAX_XGMI_WRITE_GBPS] == pytest.approx(1.0)
+
+
+def test_task_monitor_memory_limit(monkeypatch):
+    from tony_amd import constants as C
+    from tony_amd.agent import monitor as M
+
+    monkeypatch.setattr(M, "tree_rss_bytes", lambda pid: 300 << 20)
+    faults = []
+    mon = M.TaskMonitor(lambda: 1234, [], 1000, lambda m: None, False, on_fault=faults.append,
+                        memory_limit_bytes=256 << 20)
+    mon.refresh()
+    assert len(faults) == 1 and "memory limit" in faults[0] and mon.fault_code == C.EXIT_MEMORY_LIMIT

@@ -422,3 +422,67 @@ def test_resnet50_fused_matches_stock(cuda):
     gk = (fused.stem.conv.weight.grad.float() - gr).norm() / gr.norm()
     gs = (stock16.stem.conv.weight.grad.float() - gr).norm() / gr.norm()
     assert gk < 1.5 * gs + 0.05, f"stem dW: fused {gk:.3f} vs stock-bf16 {gs:.3f}"
+
+
+@pytest.mark.parametrize("M,C,relu", [(128 * 147 * 147, 64, True), (128 * 17 * 17, 192, True), (128 * 8 * 8, 2048, False),
+                                      (37, 8, True), (4096, 1280, True)])
+def test_bn_bwd_onepass_matches_two_kernels_and_fp32(cuda, M, C, relu):
+    """One-launch BN backward (grid barrier between reduce and apply) == the reduce + apply pair, and both
+    match an fp32 autograd reference."""
+    from tony_amd.ops import _lib
+
+    torch.manual_seed(M % 1000 + C)
+    x = torch.randn(M, C, device=cuda).mul_(1.5).add_(0.3).to(torch.bfloat16)
+    dy = torch.randn(M, C, device=cuda).to(torch.bfloat16)
+    g = torch.empty(C, device=cuda).uniform_(0.5, 1.5).to(torch.bfloat16)
+    b = torch.empty(C, device=cuda).uniform_(-0.3, 0.3).to(torch.bfloat16)
+    xf = x.float()
+    mean = xf.mean(0)
+    invstd = torch.rsqrt(xf.var(0, unbiased=False) + 1e-3)
+    outs = {}
+    saved = _lib.BN_ONEPASS
+    for onepass in (True, False):
+        _lib.BN_ONEPASS = onepass  # the one-launch kernel is opt-in: exercise both forms
+        ws = torch.zeros(_lib.bn_bwd_ws_floats(C) if onepass else _lib.stat_floats(C), device=cuda)
+        dx = torch.empty_like(x)
+        dg = torch.zeros(C, device=cuda, dtype=torch.bfloat16)
+        db = torch.zeros(C, device=cuda, dtype=torch.bfloat16)
+        _lib.bn_bwd(x, C, dy, C, dx, C, M, C, mean, invstd, g, b, 1, relu, ws, dg, db, True, cuda)
+        outs[onepass] = (dx.float(), dg.float(), db.float())
+    _lib.BN_ONEPASS = saved
+    torch.cuda.synchronize()
+    for a, bb in zip(outs[True], outs[False]):
+        torch.testing.assert_close(a, bb, rtol=2e-2, atol=2e-2)
+    xr = xf.clone().requires_grad_(True)
+    gr, br = g.float().requires_grad_(True), b.float().requires_grad_(True)
+    y = torch.nn.functional.batch_norm(xr, None, None, gr, br, True, 0.1, 1e-3)
+    if relu:
+        y = torch.relu(y)
+    y.backward(dy.float())
+    dx1, dg1, db1 = outs[True]
+    assert ((dx1 - xr.grad).norm() / xr.grad.norm()).item() < 2e-2
+    torch.testing.assert_close(dg1, gr.grad, rtol=3e-2, atol=3e-2 * gr.grad.abs().max().item() + 1e-2)
+    torch.testing.assert_close(db1, br.grad, rtol=3e-2, atol=3e-2 * br.grad.abs().max().item() + 1e-2)
+
+
+def test_splitk_fold_matches_combine_pass(cuda, monkeypatch):
+    """The opt-in in-kernel split-K fold (last workgroup of a tile sums the partials) == the combine pass,
+    for a bf16 accumulate-into-slot destination and a fresh fp32 result."""
+    from tony_amd.ops import gemm
+    from tony_amd.ops.conv import conv_wgrad
+
+    torch.manual_seed(3)
+    x = torch.randn(8, 64, 35, 35, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(8, 96, 35, 35, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    a = torch.randn(4096, 192, device=cuda).to(torch.bfloat16)
+    b = torch.randn(4096, 256, device=cuda).to(torch.bfloat16)
+    res = {}
+    for fold in (False, True):
+        monkeypatch.setattr(gemm, "SPLITK_FOLD", fold)
+        dw = conv_wgrad(dy, x, (96, 64, 3, 3), 1, 1)
+        slot = torch.ones(96 * 3 * 3 * 64, device=cuda, dtype=torch.bfloat16)
+        conv_wgrad(dy, x, (96, 64, 3, 3), 1, 1, dst=slot)
+        res[fold] = (dw.float(), slot.float(), gemm.gemm_tn(a, b))
+    torch.cuda.synchronize()
+    for u, v in zip(res[True], res[False]):
+        torch.testing.assert_close(u, v, rtol=1e-2, atol=1e-2)

@@ -4,13 +4,15 @@ Every ``tony.task.metrics-interval-ms`` it samples the RSS of the task's process
 tree (psutil) and, for the GPUs the coordinator pinned to the task (TonY
 averages over *all* GPUs of the node), busy %, VRAM-used % and memory-engine
 busy % via amd-smi, plus MI355X power / temperature; keeps running max and
-average, and pushes them to the coordinator's metrics RPC.  GPU sampling stops
+average, and pushes them to the coordinator's metrics RPC.  Also the xGMI traffic of the pinned GPUs
+(GB/s read / written over all links, from amd-smi's accumulated per-link counters).  GPU sampling stops
 after ``MAX_REPEATED_GPU_ERROR_ALLOWED`` consecutive failures.
 """
 from __future__ import annotations
 
 import logging
 import threading
+import time
 from typing import Callable, Dict, List, Optional
 
 from .. import constants as C
@@ -69,6 +71,9 @@ class TaskMonitor:
         self.main = RunningStat()
         self.power = RunningStat()
         self.temp = RunningStat()
+        self.xgmi_rd = RunningStat()   # GB/s read over the xGMI links of the pinned GPUs (interval deltas)
+        self.xgmi_wr = RunningStat()
+        self._xgmi_last = None         # (time, read KB, write KB) of the previous sample
         self.ecc_base = None      # uncorrectable ECC count of the pinned GPUs when the task started
         self.ecc_new = 0          # uncorrectable errors raised since (a GPU fault: SURVEY.md §5.3)
         self.gpu_errors = 0
@@ -107,6 +112,13 @@ class TaskMonitor:
             self.main.add(sum(s.mem_busy_pct for s in samples) / n)
             self.power.add(sum(s.power_w for s in samples))
             self.temp.add(max(s.temp_c for s in samples))
+            rd, wr = sum(s.xgmi_read_kb for s in samples), sum(s.xgmi_write_kb for s in samples)
+            now = time.monotonic()
+            if self._xgmi_last is not None and now > self._xgmi_last[0] and rd >= self._xgmi_last[1]:
+                dt = now - self._xgmi_last[0]
+                self.xgmi_rd.add((rd - self._xgmi_last[1]) / dt / 1e6)   # KB/s -> GB/s
+                self.xgmi_wr.add((wr - self._xgmi_last[2]) / dt / 1e6)
+            self._xgmi_last = (now, rd, wr)
             ecc = sum(s.ecc_uncorrectable for s in samples)
             if self.ecc_base is None:
                 self.ecc_base = ecc
@@ -137,7 +149,9 @@ class TaskMonitor:
                       C.MAX_GPU_FB_MEMORY_USAGE: self.fb.max, C.AVG_GPU_FB_MEMORY_USAGE: self.fb.avg,
                       C.MAX_GPU_MAIN_MEMORY_USAGE: self.main.max, C.AVG_GPU_MAIN_MEMORY_USAGE: self.main.avg,
                       C.MAX_GPU_POWER_WATTS: self.power.max, C.AVG_GPU_POWER_WATTS: self.power.avg,
-                      C.MAX_GPU_TEMPERATURE: self.temp.max, C.GPU_ECC_UNCORRECTABLE: float(self.ecc_new)})
+                      C.MAX_GPU_TEMPERATURE: self.temp.max, C.GPU_ECC_UNCORRECTABLE: float(self.ecc_new),
+                      C.MAX_XGMI_READ_GBPS: self.xgmi_rd.max, C.AVG_XGMI_READ_GBPS: self.xgmi_rd.avg,
+                      C.MAX_XGMI_WRITE_GBPS: self.xgmi_wr.max, C.AVG_XGMI_WRITE_GBPS: self.xgmi_wr.avg})
         return m
 
     def _push(self):

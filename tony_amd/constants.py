@@ -122,6 +122,10 @@ MAX_GPU_POWER_WATTS = "MAX_GPU_POWER_WATTS"
 AVG_GPU_POWER_WATTS = "AVG_GPU_POWER_WATTS"
 MAX_GPU_TEMPERATURE = "MAX_GPU_TEMPERATURE"
 GPU_ECC_UNCORRECTABLE = "GPU_ECC_UNCORRECTABLE"  # new uncorrectable ECC errors on the task's GPUs
+MAX_XGMI_READ_GBPS = "MAX_XGMI_READ_GBPS"
+AVG_XGMI_READ_GBPS = "AVG_XGMI_READ_GBPS"
+MAX_XGMI_WRITE_GBPS = "MAX_XGMI_WRITE_GBPS"
+AVG_XGMI_WRITE_GBPS = "AVG_XGMI_WRITE_GBPS"
 MAX_REPEATED_GPU_ERROR_ALLOWED = 10
 # exit statuses the agent reports for failures the user process did not cause (coordinator diagnostics)
 EXIT_GPU_FAULT = 75          # new uncorrectable ECC errors on a pinned GPU: the task was stopped

@@ -34,7 +34,9 @@ class _GpuSample(ctypes.Structure):
     _fields_ = [("gfx_busy_pct", ctypes.c_uint32), ("mem_busy_pct", ctypes.c_uint32),
                 ("vram_used_mb", ctypes.c_uint32), ("vram_total_mb", ctypes.c_uint32), ("power_w", ctypes.c_double),
                 ("temp_c", ctypes.c_double), ("ecc_correctable", ctypes.c_uint64),
-                ("ecc_uncorrectable", ctypes.c_uint64)]
+                ("ecc_uncorrectable", ctypes.c_uint64), ("xgmi_read_kb", ctypes.c_uint64),
+                ("xgmi_write_kb", ctypes.c_uint64), ("xgmi_link_speed_gbps", ctypes.c_uint32),
+                ("xgmi_link_width", ctypes.c_uint32)]
 
 
 def lib():
@@ -174,6 +176,9 @@ class GpuSample:
     temp_c: float = 0.0
     ecc_correctable: int = 0
     ecc_uncorrectable: int = 0
+    xgmi_read_kb: int = 0      # accumulated over all links since boot
+    xgmi_write_kb: int = 0
+    xgmi_link_speed_gbps: int = 0
 
 
 def smi_devices() -> List[GpuDevice]:
@@ -199,7 +204,8 @@ def smi_sample(index: int) -> Optional[GpuSample]:
     if L.tony_smi_sample(int(index), ctypes.byref(s)) != 0:
         return None
     return GpuSample(s.gfx_busy_pct, s.mem_busy_pct, s.vram_used_mb, s.vram_total_mb, s.power_w, s.temp_c,
-                     int(s.ecc_correctable), int(s.ecc_uncorrectable))
+                     int(s.ecc_correctable), int(s.ecc_uncorrectable), int(s.xgmi_read_kb), int(s.xgmi_write_kb),
+                     int(s.xgmi_link_speed_gbps))
 
 
 def smi_link(a: int, b: int):

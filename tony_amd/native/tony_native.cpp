@@ -123,6 +123,7 @@ struct Smi {
   decltype(&amdsmi_get_temp_metric) temp = nullptr;
   decltype(&amdsmi_topo_get_link_type) link_type = nullptr;
   decltype(&amdsmi_get_gpu_total_ecc_count) ecc = nullptr;
+  decltype(&amdsmi_get_gpu_metrics_info) metrics = nullptr;
   std::vector<amdsmi_processor_handle> gpus;
   bool ready = false;
 };
@@ -160,6 +161,7 @@ API int tony_smi_init(void) {
   sym(g_smi.h, "amdsmi_get_temp_metric", g_smi.temp);
   sym(g_smi.h, "amdsmi_topo_get_link_type", g_smi.link_type);
   sym(g_smi.h, "amdsmi_get_gpu_total_ecc_count", g_smi.ecc);
+  sym(g_smi.h, "amdsmi_get_gpu_metrics_info", g_smi.metrics);
   if (!g_smi.init || !g_smi.sockets || !g_smi.processors) return -2;
   if (g_smi.init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) return -3;
   uint32_t ns = 0;
@@ -205,6 +207,11 @@ struct tony_gpu_sample {
   // RAS: accumulated ECC error counts (uncorrectable growth = a GPU fault)
   uint64_t ecc_correctable;
   uint64_t ecc_uncorrectable;
+  // xGMI traffic: accumulated KB over all links (read / written by this GPU) and the link bitrate
+  uint64_t xgmi_read_kb;
+  uint64_t xgmi_write_kb;
+  uint32_t xgmi_link_speed_gbps;
+  uint32_t xgmi_link_width;
 };
 
 API int tony_smi_info(int idx, tony_gpu_info* out) {
@@ -259,6 +266,20 @@ API int tony_smi_sample(int idx, tony_gpu_sample* out) {
   if (g_smi.ecc && g_smi.ecc(p, &ec) == AMDSMI_STATUS_SUCCESS) {
     out->ecc_correctable = ec.correctable_count;
     out->ecc_uncorrectable = ec.uncorrectable_count;
+  }
+  if (g_smi.metrics) {
+    // the metrics table is large: keep it off the (monitor thread's) stack
+    static thread_local amdsmi_gpu_metrics_t m;
+    memset(&m, 0, sizeof(m));
+    if (g_smi.metrics(p, &m) == AMDSMI_STATUS_SUCCESS) {
+      for (int l = 0; l < AMDSMI_MAX_NUM_XGMI_LINKS; ++l) {
+        // unsupported entries read as all-ones
+        if (m.xgmi_read_data_acc[l] != UINT64_MAX) out->xgmi_read_kb += m.xgmi_read_data_acc[l];
+        if (m.xgmi_write_data_acc[l] != UINT64_MAX) out->xgmi_write_kb += m.xgmi_write_data_acc[l];
+      }
+      if (m.xgmi_link_speed != UINT16_MAX) out->xgmi_link_speed_gbps = m.xgmi_link_speed;
+      if (m.xgmi_link_width != UINT16_MAX) out->xgmi_link_width = m.xgmi_link_width;
+    }
   }
   return ok > 0 ? 0 : -2;
 }

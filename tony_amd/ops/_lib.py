@@ -60,6 +60,9 @@ _SIGNATURES = {
     "tony_bn_bwd_res": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                         c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                         c_int, c_void_p],
+    "tony_bn_bwd_onepass": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p,
+                            c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                            c_void_p, c_int, c_void_p],
     "tony_add_f32": [c_void_p, c_int, c_void_p, c_int64, c_void_p],
     "tony_sgd_step": [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p],
     "tony_adam_step": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p],
@@ -70,7 +73,7 @@ _SIGNATURES = {
     "tony_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64,
                        c_int, c_void_p, c_int64, c_void_p],
     "tony_gemm_tn_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64,
-                          c_void_p, c_int64, c_int_p, c_int, c_void_p],
+                          c_void_p, c_int64, c_int_p, c_int, c_void_p, c_void_p, c_int, c_void_p],
     "tony_splitk_reduce": [c_void_p, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_void_p],
     "tony_conv_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int,
                       c_int, c_int, c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_int64, c_void_p],
@@ -81,7 +84,8 @@ _SIGNATURES = {
     "tony_conv_dgrad_strided": [c_void_p, c_int, c_int, c_int, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_int,
                                 c_int, c_int, c_int, c_void_p, c_int, c_int, c_int64, c_int, c_void_p],
     "tony_conv_wgrad": [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int, c_int, c_int, c_int,
-                        c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_int_p, c_int, c_void_p],
+                        c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_int_p, c_int, c_void_p,
+                        c_void_p, c_int, c_void_p],
     "tony_avgpool3_s1p1": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
     "tony_maxpool_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
                          c_void_p],
@@ -144,6 +148,36 @@ def check_stat_buffer(buf, c: int) -> None:
     if buf is not None and (buf.dtype != torch.float32 or buf.numel() < stat_floats(c) or not buf.is_contiguous()):
         raise ValueError(f"statistics buffer for {c} channels must be {stat_floats(c)} contiguous fp32 "
                          f"(STAT_SHARDS={STAT_SHARDS} x [sum | sumsq]); got {buf.dtype} x {buf.numel()}")
+
+
+# TONY_BN_ONEPASS=1: BatchNorm backward in ONE launch (reduce -> grid barrier -> apply,
+# csrc/bn_act.hip; the arrival counter is the word after the statistics floats of the zeroed
+# workspace).  Off by default: its grid must stay co-resident (<= 2 workgroups per CU), which starves
+# the memory pipeline -- measured 109 us per layer vs 43 us for the reduce + apply pair
+# (profiles/r2_rejected_splitk_fold_bn_onepass_prof.md).
+BN_ONEPASS = os.environ.get("TONY_BN_ONEPASS", "0") == "1"
+
+
+def bn_bwd_ws_floats(c: int) -> int:
+    """Floats of a zeroed BN-backward workspace: the sharded [dsum | dsumx] + the barrier counter."""
+    return stat_floats(c) + 4
+
+
+def bn_bwd(x, ldx: int, dy, lddy: int, dx, lddx: int, M: int, C: int, mean, invstd, gamma, beta, pb: int,
+           relu: bool, ws, dgamma, dbeta, accumulate: bool, device) -> None:
+    """dx (and dgamma/dbeta, added into when ``accumulate``) of y = relu?(bn(x)) from dy."""
+    L = lib()
+    if BN_ONEPASS and ws.numel() >= stat_floats(C) + 1:
+        rc = L.tony_bn_bwd_onepass(x.data_ptr(), ldx, dy.data_ptr(), lddy, dx.data_ptr(), lddx, M, C,
+                                   mean.data_ptr(), invstd.data_ptr(), ptr(gamma), ptr(beta), pb, int(relu),
+                                   ws.data_ptr(), ptr(dgamma), ptr(dbeta), int(accumulate),
+                                   ws.data_ptr() + 4 * stat_floats(C), num_cus(device), stream_ptr(device))
+        check(rc, "tony_bn_bwd_onepass")
+        return
+    rc = L.tony_bn_bwd(x.data_ptr(), ldx, dy.data_ptr(), lddy, dx.data_ptr(), lddx, M, C, mean.data_ptr(),
+                       invstd.data_ptr(), ptr(gamma), ptr(beta), pb, int(relu), ws.data_ptr(), ptr(dgamma), ptr(dbeta),
+                       int(accumulate), stream_ptr(device))
+    check(rc, "tony_bn_bwd")
 
 
 def fold_stats(buf, c: int):

@@ -98,7 +98,7 @@ class _BNActFn(torch.autograd.Function):
         dy, (_, _, lddy) = _as_rows(dy)
         dx = _empty_like_rows(x)
         _, _, lddx = _rows_view(dx)
-        ws = zeros_f32(_lib.stat_floats(C), x.device)
+        ws = zeros_f32(_lib.bn_bwd_ws_floats(C), x.device)
         gw, gb = _lib.grad_slot(ctx.params[0]), _lib.grad_slot(ctx.params[1])
         inplace = gw is not None and gb is not None
         if inplace:
@@ -106,10 +106,8 @@ class _BNActFn(torch.autograd.Function):
         else:
             dw = torch.empty_like(weight) if weight is not None else None
             db = torch.empty_like(bias) if bias is not None else None
-        rc = L.tony_bn_bwd(x.data_ptr(), ldx, dy.data_ptr(), lddy, dx.data_ptr(), lddx, M, C, mean.data_ptr(),
-                           invstd.data_ptr(), _lib.ptr(weight), _lib.ptr(bias), ctx.pb, int(ctx.relu),
-                           ws.data_ptr(), _lib.ptr(dw), _lib.ptr(db), int(inplace), _lib.stream_ptr(x.device))
-        _lib.check(rc, "tony_bn_bwd")
+        _lib.bn_bwd(x, ldx, dy, lddy, dx, lddx, M, C, mean, invstd, weight, bias, ctx.pb, ctx.relu, ws, dw, db,
+                    inplace, x.device)
         if inplace:
             dw = db = None  # already added into param.grad
         _lib.report_inplace(ctx.params, (dw, db))

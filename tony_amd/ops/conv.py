@@ -181,7 +181,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride=1, paddin
     ``dst`` (a gradient slot in [Co][R][S][Ci] memory order), dW added into dst (returns None).
 
     The M = N*OH*OW reduction is split over ~2 workgroups per CU whose partial dW tiles are stored
-    to a slab and summed by one combine pass (gemm.splitk_combine) -- no fp32 atomics."""
+    to a slab; the last split of each tile sums them (gemm.splitk_combine) -- no fp32 atomics."""
     dy, (_, co, lddy) = _as_rows(dy)
     x, (_, c, ldx) = _as_rows(x)
     n, _, h, w = x.shape
@@ -193,9 +193,9 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride=1, paddin
 
     def run(occ, dst_=None):
         return splitk_combine(
-            lambda slab, cap, sp: L.tony_conv_wgrad(dy.data_ptr(), lddy, x.data_ptr(), n, h, w, c, ldx, co, r, s, sh,
-                                                    sw, ph, pw, dy.shape[2], dy.shape[3], 0, slab, cap, sp,
-                                                    wgrad_cus(dev, occ), _lib.stream_ptr(dev)),
+            lambda slab, cap, sp, fc, fd, ff: L.tony_conv_wgrad(
+                dy.data_ptr(), lddy, x.data_ptr(), n, h, w, c, ldx, co, r, s, sh, sw, ph, pw, dy.shape[2],
+                dy.shape[3], 0, slab, cap, sp, wgrad_cus(dev, occ), fc, fd, ff, _lib.stream_ptr(dev)),
             co * r * s * c, ntiles, dev, dst_, occ)
 
     occ = tune.pick_choice(("wgrad_occ", tuple(dy.shape), lddy, tuple(x.shape), ldx, tuple(weight_shape), sh, sw,
@@ -426,15 +426,13 @@ def _conv_bn_backward(ctx, x, weight, gamma, beta, mean, invstd, Z, dy):
     M, co, ldz = _rows_view(Z)
     dy, (_, _, lddy) = _as_rows(dy)
     dZ = torch.empty_like(Z)
-    ws = zeros_f32(_lib.stat_floats(co), dev)
+    ws = zeros_f32(_lib.bn_bwd_ws_floats(co), dev)
     gg, gb = _lib.grad_slot(ctx.params[1]), _lib.grad_slot(ctx.params[2])
     inplace = gg is not None and gb is not None
     dgamma = gg if inplace else torch.empty_like(gamma)
     dbeta = gb if inplace else torch.empty_like(beta)
-    rc = L.tony_bn_bwd(Z.data_ptr(), ldz, dy.data_ptr(), lddy, dZ.data_ptr(), ldz, M, co, mean.data_ptr(),
-                       invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), pb, int(relu), ws.data_ptr(),
-                       dgamma.data_ptr(), dbeta.data_ptr(), int(inplace), _lib.stream_ptr(dev))
-    _lib.check(rc, "tony_bn_bwd")
+    _lib.bn_bwd(Z, ldz, dy, lddy, dZ, ldz, M, co, mean, invstd, gamma, beta, pb, relu, ws, dgamma, dbeta, inplace,
+                dev)
     dw = _wgrad(dZ, x, weight, stride, padding)  # first: overlaps the dgrad on the side stream
     dx = _dgrad(dZ, weight, x.shape, stride, padding) if ctx.needs_input_grad[0] else None
     streams.keep(dx)  # may be consumed on another (branch) stream

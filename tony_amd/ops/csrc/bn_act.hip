@@ -358,6 +358,148 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
          YMASK ? load8(ym + r * ldym + rm.cg * 8) : none, r);
 }
 
+// ---- one-launch BN(+ReLU) backward: reduce -> grid barrier -> apply ------------------------------
+// The two-kernel backward (reduce, then apply) reads x and dy twice from HBM and pays two launches
+// per layer (x 96 layers per Inception step).  Here a workgroup reduces its rows, all workgroups
+// meet at a grid barrier (an atomic arrival counter in the zeroed statistics workspace), and each
+// then applies to the SAME rows it just reduced -- the second read mostly hits the L2 / MALL.
+// The grid is at most 2 workgroups per CU with <= 40 KB of LDS each, so every workgroup of the
+// launch is resident on an otherwise idle GPU (4 fit per CU): no workgroup can wait on one that
+// never gets a CU.  Arrival is a release atomic by one lane after __syncthreads; the wait polls
+// with an acquire load at agent scope (vector memory, never the scalar cache).
+__device__ __forceinline__ void grid_barrier(unsigned* counter) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    while (__hip_atomic_load(counter, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x)
+      __builtin_amdgcn_s_sleep(1);
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ float shard_sum_acquire(const float* p, int c, int64_t sstride) {
+  float s = 0.f;
+  const int n = sstride == 0 ? 1 : kStatShards;
+  for (int k = 0; k < n; ++k)
+    s += __hip_atomic_load(p + k * sstride + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return s;
+}
+
+__global__ __launch_bounds__(kThreads) void bn_bwd_onepass_kernel(
+    const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __restrict__ dy, int64_t lddy,
+    uint16_t* __restrict__ dx, int64_t lddx, int64_t M, int C, int64_t rows_per_block,
+    const float* __restrict__ mean, const float* __restrict__ invstd, const void* gamma, const void* beta,
+    int param_bf16, int relu, float* __restrict__ dsum, float* __restrict__ dsumx, int64_t sstride,
+    void* dgamma, void* dbeta, int accumulate, unsigned* counter) {
+  __shared__ float lds[5 * kMaxC];  // phase 1: coefficient table [4][C] then the block reduction; phase 2: [5][C]
+  RowMap rm(C);
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  const int64_t step = rm.RPI;
+  // ---- phase 1: dsum[c] = sum dy', dsumx[c] = sum dy' * xhat over this workgroup's rows
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    const float mu = mean[c], is = invstd[c];
+    const float g = load_param(gamma, c, param_bf16, 1.f), be = load_param(beta, c, param_bf16, 0.f);
+    lds[c] = is;
+    lds[kMaxC + c] = -mu * is;
+    lds[2 * kMaxC + c] = g * is;
+    lds[3 * kMaxC + c] = be - g * is * mu;
+  }
+  __syncthreads();
+  float a[8], b[8], p0[8], p1[8], p2[8], p3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] = b[j] = 0.f;
+    const int c = (rm.active ? rm.cg * 8 : 0) + j;
+    p0[j] = lds[c];
+    p1[j] = lds[kMaxC + c];
+    p2[j] = lds[2 * kMaxC + c];
+    p3[j] = lds[3 * kMaxC + c];
+  }
+  __syncthreads();
+  if (rm.active) {
+    auto red_body = [&](const bf16x8& xv, const bf16x8& gv) {
+      float xf[8], gf[8];
+      xv.to_float(xf);
+      gv.to_float(gf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xh = fmaf(xf[j], p0[j], p1[j]);
+        const float d = (relu && fmaf(xf[j], p2[j], p3[j]) <= 0.f) ? 0.f : gf[j];
+        a[j] += d;
+        b[j] = fmaf(d, xh, b[j]);
+      }
+    };
+    int64_t r = r0 + rm.rsub;
+    for (; r + 3 * step < r1; r += 4 * step) {
+      bf16x8 xv[4], gv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        xv[u] = load8(x + (r + u * step) * ldx + rm.cg * 8);
+        gv[u] = load8(dy + (r + u * step) * lddy + rm.cg * 8);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) red_body(xv[u], gv[u]);
+    }
+    for (; r < r1; r += step) red_body(load8(x + r * ldx + rm.cg * 8), load8(dy + r * lddy + rm.cg * 8));
+  }
+  const int64_t so = shard_off(blockIdx.x, sstride);
+  block_reduce_add(lds, rm, C, a, b, dsum + so, dsumx + so);
+  grid_barrier(counter);
+  // ---- phase 2: dx = dy'*q0 + x*q1 + q2 with the completed sums
+  const float inv_m = 1.f / static_cast<float>(M);
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    const float g = load_param(gamma, c, param_bf16, 1.f), be = load_param(beta, c, param_bf16, 0.f);
+    const float ds = shard_sum_acquire(dsum, c, sstride), dsx = shard_sum_acquire(dsumx, c, sstride);
+    const float mu = mean[c], is = invstd[c];
+    const float k = g * is, am = ds * inv_m, bm = dsx * inv_m;
+    lds[c] = k;
+    lds[kMaxC + c] = -k * bm * is;
+    lds[2 * kMaxC + c] = k * (bm * is * mu - am);
+    lds[3 * kMaxC + c] = k;
+    lds[4 * kMaxC + c] = be - k * mu;
+    if (blockIdx.x == 0) {
+      store_param(dbeta, c, param_bf16, ds, accumulate);
+      store_param(dgamma, c, param_bf16, dsx, accumulate);
+    }
+  }
+  __syncthreads();
+  if (!rm.active) return;
+  float q0[8], q1[8], q2[8], q3[8], q4[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = rm.cg * 8 + j;
+    q0[j] = lds[c];
+    q1[j] = lds[kMaxC + c];
+    q2[j] = lds[2 * kMaxC + c];
+    q3[j] = lds[3 * kMaxC + c];
+    q4[j] = lds[4 * kMaxC + c];
+  }
+  auto app_body = [&](const bf16x8& xv, const bf16x8& gv, int64_t row) {
+    float xf[8], gf[8], o[8];
+    xv.to_float(xf);
+    gv.to_float(gf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = (relu && fmaf(xf[j], q3[j], q4[j]) <= 0.f) ? 0.f : gf[j];
+      o[j] = fmaf(d, q0[j], fmaf(xf[j], q1[j], q2[j]));
+    }
+    store8(dx + row * lddx + rm.cg * 8, bf16x8::from_float(o));
+  };
+  int64_t r = r0 + rm.rsub;
+  for (; r + 3 * step < r1; r += 4 * step) {
+    bf16x8 xv[4], gv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      xv[u] = load8(x + (r + u * step) * ldx + rm.cg * 8);
+      gv[u] = load8(dy + (r + u * step) * lddy + rm.cg * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) app_body(xv[u], gv[u], r + u * step);
+  }
+  for (; r < r1; r += step) app_body(load8(x + r * ldx + rm.cg * 8), load8(dy + r * lddy + rm.cg * 8), r);
+}
+
 // Grid sizing: enough workgroups to cover 256 CUs several times over, but each
 // workgroup streams >= `min_iters` row groups so the per-WG LDS epilogue and
 // atomics stay amortised.
@@ -571,6 +713,25 @@ TONY_API int tony_bn_fwd_infer(const void* x, int64_t M, int C, int64_t ldx, voi
                                hipStream_t stream) {
   return tony_bn_apply(x, M, C, ldx, y, ldy, nullptr, nullptr, 0, gamma, beta, param_bf16, eps, relu, 1, nullptr,
                        nullptr, const_cast<float*>(running_mean), const_cast<float*>(running_var), 0.f, stream);
+}
+
+// One-launch backward (bn_bwd_onepass_kernel) when ``counter`` (a zeroed uint32, e.g. the word after
+// the statistics workspace) is given and ``num_cus`` > 0; the reduce + apply pair otherwise.
+TONY_API int tony_bn_bwd_onepass(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx, int64_t lddx,
+                                 int64_t M, int C, const float* mean, const float* invstd, const void* gamma,
+                                 const void* beta, int param_bf16, int relu, float* dsums_ws, void* dgamma,
+                                 void* dbeta, int accumulate, unsigned* counter, int num_cus, hipStream_t stream) {
+  if (bad_c(C) || (ldx % 8) || (lddy % 8) || (lddx % 8) || counter == nullptr || num_cus <= 0 || M <= 0) return -1;
+  const int64_t ss = 2 * static_cast<int64_t>(C);
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 4, 2 * num_cus, &rpb, &grid);  // <= 2 workgroups per CU: all co-resident
+  bn_bwd_onepass_kernel<<<grid, kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, static_cast<uint16_t*>(dx), lddx,
+      M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsums_ws, dsums_ws + C, ss, dgamma, dbeta, accumulate,
+      counter);
+  TONY_LAUNCH_CHECK();
+  return 0;
 }
 
 TONY_API int tony_bn_bwd(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx,

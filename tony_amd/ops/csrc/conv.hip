@@ -523,7 +523,7 @@ template <int TBM>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __restrict__ dY, int64_t lddy,
                                                               Gather g, float* __restrict__ C, int64_t M, int Co,
                                                               int tiles_n2, int ntiles, int64_t rows_per_split,
-                                                              float* __restrict__ slab) {
+                                                              float* __restrict__ slab, SplitFold fold) {
   constexpr int TM = TBM / 32;                 // 16-row MFMA tiles per wave along Cout (2 waves)
   constexpr int A_CH = TBM / 8;                // 16-B chunks per dY row in the tile
   constexpr int AV = (WK * A_CH + kThreads - 1) / kThreads;
@@ -658,6 +658,9 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __
       }
     }
   }
+  if (slab != nullptr && fold.counters != nullptr)
+    splitk_fold_tile<TBM, WTBN>(slab, static_cast<int64_t>(Co) * K, gridDim.x / ntiles, K, n1_0, Co, n2_0, K, tile,
+                                fold);
 }
 
 // ---- wgrad with LDS-DMA staging: the same tiles and split-K plan as conv_wgrad_kernel<TBM>, but each operand stage is written straight into LDS by
@@ -675,7 +678,7 @@ template <int TBM>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_glds_kernel(const uint16_t* __restrict__ dY, int64_t lddy,
                                                                    Gather g, int64_t M, int Co, int tiles_n2,
                                                                    int ntiles, int64_t rows_per_split,
-                                                                   float* __restrict__ slab) {
+                                                                   float* __restrict__ slab, SplitFold fold) {
   constexpr int TM = TBM / 32;
   constexpr int TILE = WK * 128;           // elements per staged operand (32 rows x 256 B)
   constexpr int STAGE = 2 * TILE;          // A then B
@@ -775,6 +778,9 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_glds_kernel(const uint16_
       }
     }
   }
+  if (fold.counters != nullptr)
+    splitk_fold_tile<TBM, WTBN>(slab, static_cast<int64_t>(Co) * K, gridDim.x / ntiles, K, n1_0, Co, n2_0, K, tile,
+                                fold);
 }
 
 bool wgrad_glds_enabled() {
@@ -787,7 +793,7 @@ bool wgrad_glds_enabled() {
 
 template <int TBM>
 int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, float* slab, int64_t slab_cap,
-                 int* splits_out, int64_t M, int Co, int num_cus, hipStream_t stream) {
+                 int* splits_out, int64_t M, int Co, int num_cus, const SplitFold& fold, hipStream_t stream) {
   const int tiles_n1 = ceil_div(Co, TBM), tiles_n2 = ceil_div(g.K, WTBN);
   const int ntiles = tiles_n1 * tiles_n2;
   // enough workgroups for ~2 per CU, each reducing >= 8 stages of WK rows
@@ -807,10 +813,10 @@ int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, float
   // are half / quarter zero chunks, run 4-8 % slower than the register-staged kernel)
   if (TBM == 128 && slab != nullptr && wgrad_glds_enabled())
     conv_wgrad_glds_kernel<TBM><<<static_cast<int>(grid), kThreads, 0, stream>>>(
-        static_cast<const uint16_t*>(dy), lddy, g, M, Co, tiles_n2, ntiles, rows, slab);
+        static_cast<const uint16_t*>(dy), lddy, g, M, Co, tiles_n2, ntiles, rows, slab, fold);
   else
     conv_wgrad_kernel<TBM><<<static_cast<int>(grid), kThreads, 0, stream>>>(
-        static_cast<const uint16_t*>(dy), lddy, g, dw, M, Co, tiles_n2, ntiles, rows, slab);
+        static_cast<const uint16_t*>(dy), lddy, g, dw, M, Co, tiles_n2, ntiles, rows, slab, fold);
   TONY_LAUNCH_CHECK();
   return 0;
 }
@@ -893,10 +899,13 @@ TONY_API int tony_conv_dgrad_strided(const void* dy, int N, int OH, int OW, int 
 
 // dW (fp32 [Co][R][S][C], zero on entry) = dY^T im2col(X); dY [N*OH*OW, Co] row stride lddy.
 // With a slab (slab_cap floats >= splits * Co*R*S*C) the M splits store their partial dW there
-// instead of adding into dw with atomics; *splits_out gets the split count for tony_splitk_reduce.
+// instead of adding into dw with atomics; *splits_out gets the split count.  With fold_counters
+// (ceil(Co/TBM) * ceil(K/128) zeroed uint32) the last split of each tile also sums the slab into
+// fold_dst (fold_flags bit0 bf16, bit1 accumulate): no tony_splitk_reduce launch.
 TONY_API int tony_conv_wgrad(const void* dy, int64_t lddy, const void* x, int N, int H, int W, int C, int64_t ldx,
                              int Co, int R, int S, int sh, int sw, int ph, int pw, int OH, int OW, float* dw,
-                             float* slab, int64_t slab_cap, int* splits_out, int num_cus, hipStream_t stream) {
+                             float* slab, int64_t slab_cap, int* splits_out, int num_cus, unsigned* fold_counters,
+                             void* fold_dst, int fold_flags, hipStream_t stream) {
   if (bad_geom(C, ldx, x) || (Co % 8) || (lddy % 8) || (reinterpret_cast<uintptr_t>(dy) & 15)) return -1;
   if (OH != (H + 2 * ph - R) / sh + 1 || OW != (W + 2 * pw - S) / sw + 1) return -1;
   const int K = R * S * C;
@@ -904,7 +913,11 @@ TONY_API int tony_conv_wgrad(const void* dy, int64_t lddy, const void* x, int N,
   if (M > 0x7fffffff) return -1;
   Gather g{static_cast<const uint16_t*>(x), ldx, H, W, C, OH, OW, R, S, sh, sw, -ph, -pw, 1, K, 0};
   if (slab == nullptr && dw == nullptr) return -1;
-  if (Co <= 32) return launch_wgrad<32>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, stream);
-  if (Co <= 64) return launch_wgrad<64>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, stream);
-  return launch_wgrad<128>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, stream);
+  if (fold_counters != nullptr && (slab == nullptr || fold_dst == nullptr || (K % 4) ||
+                                   (reinterpret_cast<uintptr_t>(fold_dst) & 7)))
+    return -1;
+  const SplitFold fold{fold_counters, fold_dst, fold_flags};
+  if (Co <= 32) return launch_wgrad<32>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream);
+  if (Co <= 64) return launch_wgrad<64>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream);
+  return launch_wgrad<128>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream);
 }

@@ -246,7 +246,7 @@ constexpr int kTnStages = 3;
 
 __global__ __launch_bounds__(kThreads) void gemm_tn_glds_kernel(
     const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb, int64_t M, int N1,
-    int N2, int tiles_n2, int ntiles, int64_t rows_per_split, float* __restrict__ slab) {
+    int N2, int tiles_n2, int ntiles, int64_t rows_per_split, float* __restrict__ slab, SplitFold fold) {
   constexpr int TILE = TBK * 128, STAGE = 2 * TILE;
   __shared__ __attribute__((aligned(16))) uint16_t smem[kTnStages * STAGE];
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
@@ -321,6 +321,9 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_glds_kernel(
       }
     }
   }
+  if (fold.counters != nullptr)
+    splitk_fold_tile<TBM, TBN>(slab, static_cast<int64_t>(N1) * N2, gridDim.x / ntiles, N2, n1_0, N1, n2_0, N2, tile,
+                               fold);
 }
 
 bool tn_glds_enabled() {
@@ -334,7 +337,7 @@ bool tn_glds_enabled() {
 __global__ __launch_bounds__(kThreads) void gemm_tn_splitk_kernel(
     const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
     float* __restrict__ C, int64_t ldc, int64_t M, int N1, int N2, int tiles_n2, int ntiles,
-    int64_t rows_per_split, float* __restrict__ slab) {
+    int64_t rows_per_split, float* __restrict__ slab, SplitFold fold) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 2 * TBK * 128];
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int tile = wg % ntiles, split = wg / ntiles;
@@ -407,6 +410,9 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_splitk_kernel(
       }
     }
   }
+  if (slab != nullptr && fold.counters != nullptr)
+    splitk_fold_tile<TBM, TBN>(slab, static_cast<int64_t>(N1) * N2, gridDim.x / ntiles, N2, n1_0, N1, n2_0, N2, tile,
+                               fold);
 }
 
 }  // namespace
@@ -416,8 +422,12 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_splitk_kernel(
 // into C; *splits_out gets the split count for tony_splitk_reduce.
 TONY_API int tony_gemm_tn_bf16(const void* A, const void* B, float* C, int64_t M, int64_t N1, int64_t N2,
                                int64_t lda, int64_t ldb, int64_t ldc, float* slab, int64_t slab_cap,
-                               int* splits_out, int num_cus, hipStream_t stream) {
+                               int* splits_out, int num_cus, unsigned* fold_counters, void* fold_dst, int fold_flags,
+                               hipStream_t stream) {
   if (M <= 0 || N1 <= 0 || N2 <= 0 || (slab == nullptr && C == nullptr)) return -1;
+  if (fold_counters != nullptr && (slab == nullptr || fold_dst == nullptr || (reinterpret_cast<uintptr_t>(fold_dst) & 7)))
+    return -1;
+  const SplitFold fold{fold_counters, fold_dst, fold_flags};
   if ((N1 % 8) || (N2 % 8) || (lda % 8) || (ldb % 8)) return -1;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -1;
   // C is accumulated into with atomics: the caller hands it over zeroed (ops/arena.py)
@@ -439,11 +449,11 @@ TONY_API int tony_gemm_tn_bf16(const void* A, const void* B, float* C, int64_t M
   if (slab != nullptr && tn_glds_enabled())
     gemm_tn_glds_kernel<<<static_cast<int>(grid), kThreads, 0, stream>>>(
         static_cast<const uint16_t*>(A), lda, static_cast<const uint16_t*>(B), ldb, M, static_cast<int>(N1),
-        static_cast<int>(N2), tiles_n2, ntiles, rows, slab);
+        static_cast<int>(N2), tiles_n2, ntiles, rows, slab, fold);
   else
     gemm_tn_splitk_kernel<<<static_cast<int>(grid), kThreads, 0, stream>>>(
         static_cast<const uint16_t*>(A), lda, static_cast<const uint16_t*>(B), ldb, C, ldc, M, static_cast<int>(N1),
-        static_cast<int>(N2), tiles_n2, ntiles, rows, slab);
+        static_cast<int>(N2), tiles_n2, ntiles, rows, slab, fold);
   TONY_LAUNCH_CHECK();
   return 0;
 }

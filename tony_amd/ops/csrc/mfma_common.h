@@ -76,7 +76,67 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const void*)p));
 }
 
-// Column tile for a cap: the output channels split evenly over ceil(N/cap) tiles, rounded up to
+// ---- split-K fold: the LAST workgroup of a tile sums every split's partial (no combine launch) ----
+// A slab-mode split-K kernel stores its partial tile to slab[split * n + ...]; each workgroup then
+// announces its arrival on a per-tile counter (release), and the workgroup that arrives last
+// (acquire) sums the `splits` partials of its tile in split order -- deterministic whichever
+// workgroup that is -- and writes the result into dst: fp32 or bf16, stored or added.
+struct SplitFold {
+  unsigned* counters;  // one per tile, zero on entry; nullptr: the caller runs tony_splitk_reduce
+  void* dst;
+  int flags;           // bit0: dst is bf16; bit1: add into dst
+};
+
+template <int TR, int TC>
+__device__ __forceinline__ void splitk_fold_tile(const float* __restrict__ slab, int64_t n, int splits, int64_t ld,
+                                                 int r0, int rlim, int c0, int clim, int tile, const SplitFold& f) {
+  __shared__ int s_last;
+  __threadfence();  // this thread's partial stores are visible device-wide before the arrival below
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(f.counters + tile, 1u) == static_cast<unsigned>(splits - 1);
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  constexpr int C4 = TC / 4;
+  const bool bf16 = f.flags & 1, acc = f.flags & 2;
+  for (int v = threadIdx.x; v < TR * C4; v += kThreads) {
+    const int row = r0 + v / C4, col = c0 + (v % C4) * 4;
+    if (row >= rlim || col >= clim) continue;
+    const int64_t off = static_cast<int64_t>(row) * ld + col;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < splits; ++k) {
+      const float4 a = *reinterpret_cast<const float4*>(slab + k * n + off);
+      s.x += a.x;
+      s.y += a.y;
+      s.z += a.z;
+      s.w += a.w;
+    }
+    if (bf16) {
+      uint2* p = reinterpret_cast<uint2*>(static_cast<uint16_t*>(f.dst) + off);
+      if (acc) {
+        const uint2 o = *p;
+        s.x += __uint_as_float(o.x << 16);
+        s.y += __uint_as_float(o.x & 0xffff0000u);
+        s.z += __uint_as_float(o.y << 16);
+        s.w += __uint_as_float(o.y & 0xffff0000u);
+      }
+      *p = make_uint2(static_cast<uint32_t>(f2bf(s.x)) | (static_cast<uint32_t>(f2bf(s.y)) << 16),
+                      static_cast<uint32_t>(f2bf(s.z)) | (static_cast<uint32_t>(f2bf(s.w)) << 16));
+    } else {
+      float4* p = reinterpret_cast<float4*>(static_cast<float*>(f.dst) + off);
+      if (acc) {
+        const float4 o = *p;
+        s.x += o.x;
+        s.y += o.y;
+        s.z += o.z;
+        s.w += o.w;
+      }
+      *p = s;
+    }
+  }
+}
+
+// Column tile for a cap:// Column tile for a cap: the output channels split evenly over ceil(N/cap) tiles, rounded up to
 // the 32-column granule of the 2x2 wave layout (16-wide MFMA per wave), so no MFMA work is spent on
 // padding columns for Cout = 32..384 (Inception's 48/80/96/160/192/320/384).
 inline int64_t pick_bn(int64_t N, int64_t cap) {

@@ -10,10 +10,12 @@ split-K MFMA kernel that reads its operands with ds_read_b64_tr_b16
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
 from . import _lib, tune
+from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 
 
@@ -57,11 +59,20 @@ def wgrad_cus(device, occ: int = 1) -> int:
     return _lib.num_cus(device) * occ
 
 
-def splitk_combine(launch, n: int, ntiles: int, device, dst: torch.Tensor | None = None, occ: int = 1):
-    """Run a split-K weight-gradient kernel in slab mode and sum its splits (csrc/splitk.hip).
+# TONY_SPLITK_FOLD=1: the last workgroup of each dW tile sums the split partials inside the wgrad
+# kernel (mfma_common.h splitk_fold_tile) instead of a separate combine launch.  Off by default:
+# measured on MI355X it serialises each tile's ~100-split reduction on ONE workgroup -- the Inception
+# wgrads went from 74 to 404 us (profiles/r2_rejected_splitk_fold_bn_onepass_prof.md).
+SPLITK_FOLD = os.environ.get("TONY_SPLITK_FOLD", "0") == "1"
 
-    ``launch(slab_ptr, slab_cap, splits_ref)`` launches the kernel; its M splits store dense partials
-    of the ``n``-float result into the slab.  The sum is ADDED into ``dst`` (a bf16 or fp32
+
+def splitk_combine(launch, n: int, ntiles: int, device, dst: torch.Tensor | None = None, occ: int = 1):
+    """Run a split-K weight-gradient kernel in slab mode and sum its splits.
+
+    ``launch(slab_ptr, slab_cap, splits_ref, fold_counters, fold_dst, fold_flags)`` launches the
+    kernel; its M splits store dense partials of the ``n``-float result into the slab and, with
+    fold counters, the last split of every tile sums them into ``fold_dst`` in the same launch
+    (else csrc/splitk.hip's combine kernel does).  The sum is ADDED into ``dst`` (a bf16 or fp32
     flat-gradient slot in the kernel's element order) and None returned, or returned as a new
     fp32 tensor of n floats.  The split count never exceeds ceil(2 * CUs / ntiles) (the kernels'
     2-workgroups-per-CU plan), which bounds the slab."""
@@ -69,8 +80,14 @@ def splitk_combine(launch, n: int, ntiles: int, device, dst: torch.Tensor | None
     bound = max(1, -(-2 * cus // ntiles))
     slab = torch.empty(bound * n, dtype=torch.float32, device=device)
     splits = ctypes.c_int(0)
-    _lib.check(launch(slab.data_ptr(), slab.numel(), ctypes.byref(splits)), "split-K wgrad")
     out = dst if dst is not None else torch.empty(n, dtype=torch.float32, device=device)
+    flags = int(out.dtype == torch.bfloat16) | (2 if dst is not None else 0)
+    if SPLITK_FOLD:
+        counters = zeros_f32(ntiles, device)  # zero bits = zero uint32 arrival counters
+        _lib.check(launch(slab.data_ptr(), slab.numel(), ctypes.byref(splits), counters.data_ptr(), out.data_ptr(),
+                          flags), "split-K wgrad (fold)")
+        return None if dst is not None else out
+    _lib.check(launch(slab.data_ptr(), slab.numel(), ctypes.byref(splits), 0, 0, 0), "split-K wgrad")
     rc = _lib.lib().tony_splitk_reduce(slab.data_ptr(), splits.value, n, out.data_ptr(), int(out.dtype == torch.bfloat16),
                                        int(dst is not None), cus, _lib.stream_ptr(device))
     _lib.check(rc, "tony_splitk_reduce")
@@ -85,9 +102,8 @@ def wgrad_tn(a_ptr, lda, b_ptr, ldb, M, n1, n2, device, dst: torch.Tensor | None
     ntiles = -(-n1 // 128) * -(-n2 // 128)
 
     def run(occ, dst_=None):
-        return splitk_combine(lambda slab, cap, sp: L.tony_gemm_tn_bf16(a_ptr, b_ptr, 0, M, n1, n2, lda, ldb, n2,
-                                                                        slab, cap, sp, wgrad_cus(device, occ),
-                                                                        stream),
+        return splitk_combine(lambda slab, cap, sp, fc, fd, ff: L.tony_gemm_tn_bf16(
+            a_ptr, b_ptr, 0, M, n1, n2, lda, ldb, n2, slab, cap, sp, wgrad_cus(device, occ), fc, fd, ff, stream),
                               n1 * n2, ntiles, device, dst_, occ)
 
     occ = tune.pick_choice(("wgrad_tn", M, n1, n2, lda, ldb), WGRAD_OCC, run)
