@@ -265,35 +265,47 @@ def test_conv_bn_act_pool_fused_matches_unfused(cuda, shape):
         assert _rel(a, b) < 2e-2, f"{what} rel {_rel(a, b):.4f}"
 
 
-# (N, H, W, (R, S), stride, (ph, pw)): Inception-v3's 3x3/2 stem (shrunk in N and H/W, with a
-# partial last workgroup) and a 7x7/2 p3 stem on the same kernel
-STEM_SHAPES = [(2, 299, 299, (3, 3), 2, (0, 0)), (3, 37, 41, (3, 3), 2, (0, 0)), (2, 45, 33, (7, 7), 2, (3, 3)),
-               (1, 20, 20, (3, 3), 1, (1, 1))]
+# (N, H, W, (R, S), stride, (ph, pw), Cout): Inception-v3's 3x3/2 stem (shrunk in N and H/W, with a
+# partial last workgroup and workgroups straddling two images), ResNet's 7x7/2 p3 stem (5 K steps,
+# 3 wgrad column groups), and a padded stride-1 case
+STEM_SHAPES = [(2, 299, 299, (3, 3), 2, (0, 0), 32), (3, 37, 41, (3, 3), 2, (0, 0), 32),
+               (2, 45, 33, (7, 7), 2, (3, 3), 64), (1, 20, 20, (3, 3), 1, (1, 1), 32),
+               (3, 56, 56, (7, 7), 2, (3, 3), 64)]
 
 
-@pytest.mark.parametrize("shape", STEM_SHAPES, ids=[f"{s[1]}x{s[2]}k{s[3][0]}s{s[4]}" for s in STEM_SHAPES])
-def test_stem_fwd_direct_kernel(cuda, shape):
-    """csrc/stem.hip (3-channel direct conv + BN statistics epilogue) vs the fp32 conv2d."""
+@pytest.mark.parametrize("shape", STEM_SHAPES, ids=[f"{s[1]}x{s[2]}k{s[3][0]}s{s[4]}c{s[6]}" for s in STEM_SHAPES])
+def test_stem_fwd_wgrad_mfma(cuda, shape):
+    """csrc/stem.hip: MFMA stem forward (+ BN statistics epilogue) and split-K weight gradient vs fp32."""
     from tony_amd.ops import _lib
-    from tony_amd.ops.conv import stem_fwd, stem_supported
+    from tony_amd.ops.conv import stem_fwd, stem_supported, stem_wgrad
 
-    n, h, w, k, s, p = shape
+    n, h, w, k, s, p, co = shape
     torch.manual_seed(3)
     x = _nhwc(torch.randn(n, 3, h, w, device=cuda)).to(torch.bfloat16)
-    wt = _nhwc(0.2 * torch.randn(32, 3, *k, device=cuda)).to(torch.bfloat16)
+    wt = _nhwc(0.2 * torch.randn(co, 3, *k, device=cuda)).to(torch.bfloat16)
     assert stem_supported(x, wt, s, p)
-    stats = torch.zeros(_lib.stat_floats(32), device=cuda)
+    stats = torch.zeros(_lib.stat_floats(co), device=cuda)
     y = stem_fwd(x, wt, s, p, stats)
-    ref = torch.nn.functional.conv2d(x.float(), wt.float(), None, s, p)
+    xr = x.float().requires_grad_(False)
+    wr = wt.float().requires_grad_(True)
+    ref = torch.nn.functional.conv2d(xr, wr, None, s, p)
     assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
     assert _rel(y, ref) < 1e-2
-    st = _lib.fold_stats(stats, 32)
-    torch.testing.assert_close(st[:32], ref.sum((0, 2, 3)), rtol=1e-3, atol=ref.numel() / 32 * 1e-4)
-    torch.testing.assert_close(st[32:], (ref * ref).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    st = _lib.fold_stats(stats, co)
+    torch.testing.assert_close(st[:co], ref.sum((0, 2, 3)), rtol=1e-3, atol=ref.numel() / co * 1e-4)
+    torch.testing.assert_close(st[co:], (ref * ref).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    dy = _nhwc(torch.randn_like(ref)).to(torch.bfloat16)
+    ref.backward(dy.float())
+    dw = stem_wgrad(dy, x, wt.shape, s, p)
+    assert dw.shape == wt.shape and _rel(dw, wr.grad) < 1e-2
+    # accumulate into a bf16 channels_last gradient slot
+    slot = _nhwc(torch.ones_like(wt))
+    assert stem_wgrad(dy, x, wt.shape, s, p, dst=slot) is None
+    assert _rel(slot.float() - 1.0, wr.grad) < 2e-2
 
 
 def test_stem_conv_bn_act_layer_fwd_bwd(cuda):
-    """The fused ConvBNAct layer on a 3-channel input (direct forward, MIOpen wgrad) vs fp32."""
+    """The fused ConvBNAct layer on a 3-channel input (MFMA stem forward + wgrad, no MIOpen) vs fp32."""
     from tony_amd.ops import _lib
     from tony_amd.ops import conv as C
 
@@ -306,11 +318,12 @@ def test_stem_conv_bn_act_layer_fwd_bwd(cuda):
     rm, rv = torch.zeros(co, device=cuda), torch.ones(co, device=cuda)
     _lib.set_inplace_grads(False)
     saved = C.AUTOTUNE, C.STEM
-    C.AUTOTUNE, C.STEM = False, True  # route the stem to the fused layer and pin the direct kernel
+    C.AUTOTUNE, C.STEM = False, True  # route the stem to the fused layer and its MFMA kernels
     try:
         y = C.conv_bn_act(x, wt, g, b, rm, rv, 2, 0, True, 0.1, 1e-3, True)
         key = [k for k in C._CHOICE if k[0] == "fwd" and k[1] == tuple(x.shape) and k[2] == (co, 3, 3, 3)]
         assert not key or C._CHOICE[key[0]] == "tony"
+        assert "miopen" not in {v for k, v in C._CHOICE.items() if k[1] == tuple(x.shape)}
         wr, gr, br = (t.detach().float().requires_grad_(True) for t in (wt, g, b))
         rm_r, rv_r = torch.zeros(co, device=cuda), torch.ones(co, device=cuda)
         yr = torch.relu(torch.nn.functional.batch_norm(torch.nn.functional.conv2d(x.float(), wr, None, 2, 0), rm_r,

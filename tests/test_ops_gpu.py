@@ -486,3 +486,82 @@ def test_splitk_fold_matches_combine_pass(cuda, monkeypatch):
     torch.cuda.synchronize()
     for u, v in zip(res[True], res[False]):
         torch.testing.assert_close(u, v, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("bias", [True, False])
+@pytest.mark.parametrize("dims", [(128, 2048, 1000), (37, 768, 1000), (5, 64, 16)])
+def test_linear_mfma_fwd_bwd(cuda, dims, bias):
+    """ops/linear.py (MFMA NT GEMM with the bias in the epilogue, TN wgrad) vs fp32 F.linear."""
+    from tony_amd.ops import _lib
+    from tony_amd.ops.linear import Linear, supported
+
+    m, k, n = dims
+    torch.manual_seed(5)
+    lin = Linear(k, n, bias=bias).to(cuda, torch.bfloat16)
+    x = torch.randn(m, k, device=cuda).to(torch.bfloat16).requires_grad_(True)
+    assert supported(x, lin.weight)
+    wr = lin.weight.detach().float().requires_grad_(True)
+    br = lin.bias.detach().float().requires_grad_(True) if bias else None
+    xr = x.detach().float().requires_grad_(True)
+    _lib.set_inplace_grads(False)
+    try:
+        y = lin(x)
+        yr = torch.nn.functional.linear(xr, wr, br)
+        _close(y, yr, 2e-2, 2e-2, "y")
+        dy = torch.randn_like(yr).to(torch.bfloat16)
+        y.backward(dy)
+        yr.backward(dy.float())
+    finally:
+        _lib.set_inplace_grads(True)
+    _close(x.grad, xr.grad, 2e-2, 3e-2, "dx")
+    _close(lin.weight.grad, wr.grad, 2e-2, 3e-2, "dW")
+    if bias:
+        _close(lin.bias.grad, br.grad, 2e-2, 5e-2, "db")
+
+
+def test_linear_grad_into_flat_slot(cuda):
+    """With a bf16 gradient slot on the parameters, dW / db are summed into it in place."""
+    from tony_amd.ops.linear import Linear
+
+    torch.manual_seed(6)
+    lin = Linear(256, 64).to(cuda, torch.bfloat16)
+    lin.weight.grad = torch.ones_like(lin.weight)
+    lin.bias.grad = torch.ones_like(lin.bias)
+    x = torch.randn(32, 256, device=cuda).to(torch.bfloat16)
+    dy = torch.randn(32, 64, device=cuda).to(torch.bfloat16)
+    lin(x).backward(dy)
+    _close(lin.weight.grad.float() - 1, dy.float().t() @ x.float(), 2e-2, 5e-2, "dW slot")
+    _close(lin.bias.grad.float() - 1, dy.float().sum(0), 2e-2, 5e-2, "db slot")
+
+
+def test_whole_input_conv_bn_is_gemm(cuda):
+    """Inception aux head's 5x5 conv on a 5x5 map (+ BN + ReLU): the whole-input filter runs as a
+    plain GEMM (ops/conv.py _gemm_*, no MIOpen) and matches fp32 PyTorch fwd + bwd."""
+    from tony_amd.ops import _lib
+    from tony_amd.ops import conv as C
+
+    torch.manual_seed(7)
+    n, cin, co = 16, 128, 96
+    x = _nhwc(torch.randn(n, cin, 5, 5, device=cuda)).to(torch.bfloat16).requires_grad_(True)
+    wt = _nhwc(0.05 * torch.randn(co, cin, 5, 5, device=cuda)).to(torch.bfloat16).requires_grad_(True)
+    g = torch.empty(co, device=cuda).uniform_(0.5, 1.5).to(torch.bfloat16).requires_grad_(True)
+    b = torch.empty(co, device=cuda).uniform_(-0.2, 0.2).to(torch.bfloat16).requires_grad_(True)
+    rm, rv = torch.zeros(co, device=cuda), torch.ones(co, device=cuda)
+    assert C.fullcover(x.shape, wt.shape, 1, 0) and C.supported(x, wt, 1, 0)
+    _lib.set_inplace_grads(False)
+    try:
+        y = C.conv_bn_act(x, wt, g, b, rm, rv, 1, 0, True, 0.1, 1e-3, True)
+        xr, wr, gr, br = (t.detach().float().requires_grad_(True) for t in (x, wt, g, b))
+        yr = torch.relu(torch.nn.functional.batch_norm(torch.nn.functional.conv2d(xr, wr), torch.zeros(co, device=cuda),
+                                                       torch.ones(co, device=cuda), gr, br, True, 0.1, 1e-3))
+        _close(y, yr, 3e-2, 3e-2, "y", max_bad_frac=0.01)
+        dy = _nhwc(torch.randn_like(yr)).to(torch.bfloat16)
+        y.backward(dy)
+        yr.backward(dy.float())
+    finally:
+        _lib.set_inplace_grads(True)
+    rel = lambda a, r: ((a.float() - r).norm() / r.norm()).item()  # noqa: E731
+    assert rel(x.grad, xr.grad) < 3e-2 and rel(wt.grad, wr.grad) < 3e-2
+    assert rel(g.grad, gr.grad) < 3e-2 and rel(b.grad, br.grad) < 3e-2
+    impls = {k[0]: v for k, v in C.choices().items() if k[1] in (tuple(x.shape), (n, co, 1, 1))}
+    assert set(impls.values()) == {"gemm"}, impls

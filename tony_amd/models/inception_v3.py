@@ -24,6 +24,7 @@ from ..ops.concat import Slot, assemble, concat_buffer
 from ..ops.pool import avg_pool, avg_pool3x3_s1, global_avg_pool, max_pool
 from ..ops import streams
 from ..ops.fused import FusedHead
+from ..ops.linear import Linear
 from .layers import ConvBNAct, conv_bn_act_maxpool, init_weights
 
 
@@ -211,7 +212,7 @@ class InceptionAux(_Block):
         super().__init__(fused)
         self.conv0 = self.c(cin, 128, 1)
         self.conv1 = self.c(128, 768, 5)
-        self.fc = nn.Linear(768, num_classes)
+        self.fc = (Linear if fused else nn.Linear)(768, num_classes)
 
     def forward(self, x):
         x = avg_pool(x, 5, 3) if self.fused else nn.functional.avg_pool2d(x, 5, 3)
@@ -234,7 +235,7 @@ class InceptionV3(nn.Module):
         self.aux = InceptionAux(768, num_classes, fused) if aux_logits else None
         self.mixed_7 = nn.Sequential(InceptionD(768, fused), InceptionE(1280, fused), InceptionE(2048, fused))
         self.dropout = nn.Dropout(dropout)
-        self.fc = nn.Linear(2048, num_classes)
+        self.fc = (Linear if fused else nn.Linear)(2048, num_classes)
         self.fused = fused
 
     def forward(self, x):

@@ -12,7 +12,8 @@ downsample         1x1 s1|s2 conv (tony_amd implicit GEMM; strided dgrad per res
 
 Architecture: torchvision's resnet50 (stride on the 3x3, "v1.5"); layer
 widths 64/128/256/512 x4, blocks [3, 4, 6, 3], 7x7/s2 stem + 3x3/s2 max pool,
-global average pool, 1000-way FC.  ``fused=False`` is the stock PyTorch
+global average pool, 1000-way FC (MFMA GEMMs, ops/linear.py).  The 7x7/s2 stem runs on the
+MFMA stem kernels (csrc/stem.hip).  ``fused=False`` is the stock PyTorch
 module graph (the comparator and the CPU path).
 """
 from __future__ import annotations
@@ -21,6 +22,7 @@ import torch
 from torch import nn
 
 from ..ops.bn import BatchNormAct2d
+from ..ops.linear import Linear
 from ..ops.pool import global_avg_pool
 from ..ops.residual import bn_add_relu, conv1x1_bn_add_relu
 from .layers import ConvBNAct, init_weights
@@ -69,7 +71,7 @@ class ResNet(nn.Module):
                 blocks.append(Bottleneck(cin, width, stride=2 if (j == 0 and i > 0) else 1, fused=fused, eps=eps))
                 cin = width * Bottleneck.expansion
         self.blocks = nn.Sequential(*blocks)
-        self.fc = nn.Linear(cin, num_classes)
+        self.fc = (Linear if fused else nn.Linear)(cin, num_classes)
 
     def forward(self, x):
         x = self.stem(x)

@@ -1,8 +1,9 @@
 """NHWC implicit-GEMM convolutions on MFMA (csrc/conv.hip) and the fused conv + BN(+ReLU) layer.
 
 ``conv2d(x, weight, stride, padding)`` is a drop-in for ``F.conv2d`` on channels_last bf16 CUDA
-tensors with ``Cin % 8 == 0`` (every Inception-v3 / ResNet-50 conv but the 3-channel stems):
-forward, backward-data (stride 1) and split-K backward-weight are tony_amd kernels.
+tensors with ``Cin % 8 == 0``: forward, backward-data (every stride) and split-K backward-weight
+are tony_amd kernels.  Image stems (``Cin < 8``, e.g. the 3-channel Inception-v3 / ResNet-50 first
+layers) run forward and backward-weight on the MFMA stem kernels of csrc/stem.hip.
 
 ``conv_bn_act(x, weight, bn...)`` fuses the BatchNorm that follows: the forward GEMM epilogue
 produces the per-channel sums of its output, so the separate statistics pass over the conv
@@ -18,6 +19,7 @@ replayed by the capture; ``choices()`` records every pass, MIOpen ones included.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from typing import Callable, Dict, Tuple
 
@@ -26,7 +28,7 @@ import torch
 from . import _lib, concat, streams, tune, wt_cache
 from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
-from .gemm import WGRAD_OCC, splitk_combine, wgrad_cus
+from .gemm import WGRAD_OCC, splitk_combine, wgrad_cus, wgrad_tn
 
 _BF16 = torch.bfloat16
 AUTOTUNE = os.environ.get("TONY_CONV_AUTOTUNE", "1") != "0"
@@ -37,11 +39,9 @@ def _pair(v):
     return tuple(v) if isinstance(v, (tuple, list)) else (int(v), int(v))
 
 
-# TONY_STEM=1 routes 3-channel stems through the fused conv+BN layer with the direct kernel
-# (csrc/stem.hip) as a per-shape autotune candidate against MIOpen.  Off by default: on MI355X it
-# measured 174 us vs MIOpen's 156 us (fwd + BN statistics, Inception stem at batch 128,
-# profiles/r1_stem_direct_kernel.log), so the stem stays on MIOpen + a separate statistics pass.
-STEM = os.environ.get("TONY_STEM", "0") == "1"
+# Image stems (3-channel input) run on the MFMA stem kernels of csrc/stem.hip: forward with the BN
+# statistics epilogue and the split-K weight gradient.  TONY_STEM=0 sends them back to MIOpen (A/B).
+STEM = os.environ.get("TONY_STEM", "1") != "0"
 MIN_ROWS = 2048  # below this many output pixels a tile grid cannot fill 256 CUs: leave it to MIOpen
 
 
@@ -52,17 +52,28 @@ def supported(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, dilati
             and _pair(dilation) == (1, 1) and x.shape[1] % 8 == 0 and weight.shape[0] % 8 == 0
             and weight.shape[1] == x.shape[1]):
         return False
+    if fullcover(x.shape, weight.shape, stride, padding):
+        return True
     oh, ow = out_hw(x.shape[2], x.shape[3], weight.shape[2], weight.shape[3], stride, padding)
     return x.shape[0] * oh * ow >= (min_rows or MIN_ROWS)
 
 
+def fullcover(x_shape, w_shape, stride=1, padding=0) -> bool:
+    """A conv whose filter covers its whole unpadded input -- one output pixel per image, e.g. the
+    Inception-v3 aux head's 5x5 conv on a 5x5 map: a plain GEMM over images (``_gemm_*``)."""
+    return (_pair(padding) == (0, 0) and tuple(w_shape[2:]) == tuple(x_shape[2:]) and x_shape[1] % 8 == 0
+            and w_shape[0] % 8 == 0 and w_shape[1] == x_shape[1])
+
+
 def stem_supported(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, dilation=1, groups=1) -> bool:
-    """Whether the direct 3-channel stem kernel (csrc/stem.hip) takes this forward conv: dense NHWC
-    bf16 RGB input, 32 output channels, R*S <= 49."""
+    """Whether the MFMA stem kernels (csrc/stem.hip) take this conv: dense NHWC bf16 input with fewer
+    than 8 channels (an image), 32 or 64 output channels, padding smaller than the filter."""
+    (ph, pw) = _pair(padding)
     return (x.is_cuda and x.dtype == _BF16 and weight.dtype == _BF16 and x.dim() == 4 and groups == 1
-            and _pair(dilation) == (1, 1) and x.shape[1] == 3 and tuple(weight.shape[:2]) == (32, 3)
-            and weight.shape[2] * weight.shape[3] <= 49 and x.is_contiguous(memory_format=torch.channels_last)
-            and x.numel() < 2 ** 31)
+            and _pair(dilation) == (1, 1) and 0 < x.shape[1] < 8 and weight.shape[0] in (32, 64)
+            and weight.shape[1] == x.shape[1] and ph < weight.shape[2] and pw < weight.shape[3]
+            and x.is_contiguous(memory_format=torch.channels_last) and x.numel() < 2 ** 31
+            and x.data_ptr() % 16 == 0)
 
 
 def out_hw(h, w, r, s, stride, padding):
@@ -90,7 +101,7 @@ def conv_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: 
              vflags: int | None = None):
     """Y = conv(x, w); with ``stats`` (zeroed, ``_lib.stat_floats(Cout)`` floats) the epilogue accumulates
     [sum | sumsq] of Y into its STAT_SHARDS copies.  ``vflags``: tile variant bits (None: autotuned)."""
-    if x.shape[1] == 3:
+    if x.shape[1] < 8:  # image stem (csrc/stem.hip)
         return stem_fwd(x, weight, stride, padding, stats)
     x, (_, C, ldx) = _as_rows(x)
     n, _, h, w = x.shape
@@ -117,8 +128,8 @@ def conv_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: 
 
 
 def stem_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: torch.Tensor | None = None):
-    """Forward of a 3-channel stem conv on the vector ALUs (csrc/stem.hip), optional BN statistics
-    epilogue in the ``conv_fwd`` layout.  Its backward-weight stays on MIOpen (``_wgrad``)."""
+    """Forward of an image-stem conv on MFMA (csrc/stem.hip: K = R*S*C padded to 32-deep steps, the
+    input rows staged in LDS), optional BN statistics epilogue in the ``conv_fwd`` layout."""
     if not stem_supported(x, weight, stride, padding):
         raise ValueError(f"stem_fwd: unsupported conv x={tuple(x.shape)} w={tuple(weight.shape)}")
     n, c, h, w = x.shape
@@ -127,12 +138,37 @@ def stem_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: 
     (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
     oh, ow = out_hw(h, w, r, s, stride, padding)
     y = _cl_empty(n, co, oh, ow, x.device)
-    wk = weight.permute(2, 3, 1, 0).float().contiguous()  # fp32 [R][S][3][Co]: wave-uniform scalar loads
+    wk = _krsc(weight)
     rc = _lib.lib().tony_stem_fwd(x.data_ptr(), n, h, w, c, wk.data_ptr(), co, r, s, sh, sw, ph, pw, y.data_ptr(),
                                   oh, ow, co, 1 if stats is not None else 0, _lib.ptr(stats),
-                                  2 * co if stats is not None else 0, _lib.stream_ptr(x.device))
+                                  2 * co if stats is not None else 0, _lib.num_cus(x.device),
+                                  _lib.stream_ptr(x.device))
     _lib.check(rc, "tony_stem_fwd")
     return y
+
+
+def stem_wgrad(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride=1, padding=0, dst=None):
+    """dW of an image-stem conv (csrc/stem.hip split-K MFMA kernel + csrc/splitk.hip combine): fp32
+    memory [Co][R][S][C] returned as a [Co, C, R, S] view, or added into ``dst`` (a gradient slot in
+    that memory order; returns None)."""
+    dy, (_, co, lddy) = _as_rows(dy)
+    n, c, h, w = x.shape
+    _, _, r, s = weight_shape
+    (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
+    L, dev = _lib.lib(), x.device
+    cus = _lib.num_cus(dev)
+    nel = co * r * s * c
+    slab = torch.empty(2 * cus * nel, dtype=torch.float32, device=dev)
+    splits = ctypes.c_int(0)
+    st = _lib.stream_ptr(dev)
+    rc = L.tony_stem_wgrad(dy.data_ptr(), lddy, x.data_ptr(), n, h, w, c, co, r, s, sh, sw, ph, pw, dy.shape[2],
+                           dy.shape[3], slab.data_ptr(), slab.numel(), ctypes.byref(splits), cus, st)
+    _lib.check(rc, "tony_stem_wgrad")
+    out = dst if dst is not None else torch.empty(nel, dtype=torch.float32, device=dev)
+    rc = L.tony_splitk_reduce(slab.data_ptr(), splits.value, nel, out.data_ptr(), int(out.dtype == _BF16),
+                              int(dst is not None), cus, st)
+    _lib.check(rc, "tony_splitk_reduce")
+    return None if dst is not None else out.view(co, r, s, c).permute(0, 3, 1, 2)
 
 
 def dgrad_supported(x_shape, weight: torch.Tensor, stride=1, padding=0) -> bool:
@@ -204,6 +240,55 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride=1, paddin
     return None if out is None else out.view(co, r, s, c).permute(0, 3, 1, 2)
 
 
+# ------------------------------------------------------- whole-input filters: plain GEMMs --
+def _dense_rows(x: torch.Tensor) -> torch.Tensor:
+    """x with every image one contiguous [H*W*C] row (dense channels_last)."""
+    x = _as_rows(x)[0]
+    return x if _rows_view(x)[2] == x.shape[1] else x.contiguous(memory_format=torch.channels_last)
+
+
+def _gemm_fwd(x, weight, stats=None):
+    """Y[n, co] = X[n, (r, s, c)] . W[co, (r, s, c)]^T on the MFMA NT GEMM (+ BN statistics epilogue)."""
+    x = _dense_rows(x)
+    n = x.shape[0]
+    co = weight.shape[0]
+    k = x[0].numel()
+    _lib.check_stat_buffer(stats, co)
+    wk = _krsc(weight).reshape(co, k)
+    y = _cl_empty(n, co, 1, 1, x.device)
+    rc = _lib.lib().tony_gemm_bf16(x.data_ptr(), wk.data_ptr(), y.data_ptr(), n, co, k, k, k, co,
+                                   1 if stats is not None else 0, _lib.ptr(stats), 2 * co if stats is not None else 0,
+                                   _lib.stream_ptr(x.device))
+    _lib.check(rc, "tony_gemm_bf16 (whole-input conv)")
+    return y
+
+
+def _gemm_dgrad(dy, weight, x_shape):
+    """dX[n, (r, s, c)] = dY[n, co] . W[co, (r, s, c)] (NT GEMM on the transposed weight)."""
+    dy, (_, co, lddy) = _as_rows(dy)
+    n, c, h, w = x_shape
+    k = c * h * w
+    wt = _krsc(weight).reshape(co, k).t().contiguous()  # [(r, s, c)][co]
+    dx = _cl_empty(n, c, h, w, dy.device)
+    rc = _lib.lib().tony_gemm_bf16(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), n, k, co, lddy, co, k, 0, 0, 0,
+                                   _lib.stream_ptr(dy.device))
+    _lib.check(rc, "tony_gemm_bf16 (whole-input conv dgrad)")
+    return dx
+
+
+def _gemm_wgrad(dy, x, weight_shape, dst=None):
+    """dW[co, (r, s, c)] = dY^T X (split-K TN GEMM), added into ``dst`` or returned [Co, C, R, S]."""
+    dy, (_, co, lddy) = _as_rows(dy)
+    x = _dense_rows(x)
+    n = x.shape[0]
+    k = x[0].numel()
+    out = wgrad_tn(dy.data_ptr(), lddy, x.data_ptr(), k, n, co, k, x.device, dst=dst)
+    if out is None:
+        return None
+    _, c, r, s = weight_shape
+    return out.view(co, r, s, c).permute(0, 3, 1, 2)
+
+
 # --------------------------------------------------------------------------------- MIOpen --
 def _miopen_fwd(x, weight, stride, padding, stats=None):
     y = torch.nn.functional.conv2d(x, weight, None, _pair(stride), _pair(padding))
@@ -269,6 +354,9 @@ def choices() -> Dict[Tuple, str]:
 
 def _fwd(x, weight, stride, padding, stats):
     key = ("fwd", tuple(x.shape), tuple(weight.shape), stride, padding, stats is not None)
+    if fullcover(x.shape, weight.shape, stride, padding):
+        _CHOICE.setdefault(key, "gemm")
+        return _gemm_fwd(x, weight, stats)
     impl = _CHOICE.get(key)
     if impl is None:
         co = weight.shape[0]
@@ -282,6 +370,9 @@ def _fwd(x, weight, stride, padding, stats):
 
 def _dgrad(dy, weight, x_shape, stride, padding):
     key = ("dgrad", tuple(dy.shape), tuple(weight.shape), stride, padding)
+    if fullcover(x_shape, weight.shape, stride, padding):
+        _CHOICE.setdefault(key, "gemm")
+        return _gemm_dgrad(dy, weight, x_shape)
     impl = _CHOICE.get(key)  # steady state: no candidate closures to build
     if impl == "tony":
         return conv_dgrad(dy, weight, x_shape, stride, padding)
@@ -304,8 +395,11 @@ def _wgrad(dy, x, weight, stride, padding):
     """dW accumulated into the parameter's gradient slot (returns None) or returned for autograd."""
     key = ("wgrad", tuple(dy.shape), tuple(weight.shape), stride, padding)
     impl = _CHOICE.get(key) or WGRAD_IMPL or None
-    if x.shape[1] % 8:
-        impl = "miopen"  # 3-channel stem: no tony weight-gradient kernel
+    if fullcover(x.shape, weight.shape, stride, padding):
+        impl = "gemm"
+        _CHOICE.setdefault(key, impl)
+    elif x.shape[1] % 8:  # image stem: the MFMA stem kernel, or MIOpen if it does not take the shape
+        impl = "stem" if STEM and stem_supported(x, weight, stride, padding) else "miopen"
         _CHOICE.setdefault(key, impl)
     if impl is None:
         # With the weight gradients on the side stream (ops/streams.py) their GPU time hides behind the
@@ -315,6 +409,14 @@ def _wgrad(dy, x, weight, stride, padding):
                              "miopen": lambda: _miopen_wgrad(dy, x, weight, stride, padding)},
                        weight={"miopen": MIOPEN_WGRAD_WEIGHT if streams.ENABLED else 1.0})
     gw = _lib.grad_slot(weight)
+    if impl == "gemm":
+        if gw is not None and gw.is_contiguous(memory_format=torch.channels_last):
+            return streams.run(lambda: _gemm_wgrad(dy, x, weight.shape, dst=gw), dy, x)
+        return _accumulate_wgrad(weight, _gemm_wgrad(dy, x, weight.shape))
+    if impl == "stem":
+        if gw is not None and gw.is_contiguous(memory_format=torch.channels_last):
+            return streams.run(lambda: stem_wgrad(dy, x, weight.shape, stride, padding, dst=gw), dy, x)
+        return _accumulate_wgrad(weight, stem_wgrad(dy, x, weight.shape, stride, padding))
     if impl == "tony":
         if gw is not None and gw.is_contiguous(memory_format=torch.channels_last):
             # summed straight into the slot (on the weight-gradient stream when one is active)

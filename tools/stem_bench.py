@@ -1,11 +1,13 @@
-"""Time the Inception-v3 3-channel stem conv (128x3x299x299 -> 32, 3x3/2) two ways, NHWC bf16:
+"""Time the image-stem conv (Inception-v3: 128x3x299x299 -> 32, 3x3/2; --resnet: 7x7/2 p3 -> 64 at
+224x224), NHWC bf16, MIOpen vs the MFMA stem kernels of csrc/stem.hip:
 
-  miopen : F.conv2d forward + MIOpen backward-weight (what the 3-channel stem runs on today);
-  direct : csrc/stem.hip, the 27-tap direct kernel with the statistics epilogue (the shipped path);
-  pad8   : input zero-padded to 8 channels (one copy) + tony implicit-GEMM forward (with the BN
-           statistics epilogue) + tony split-K backward-weight on the padded operands.
+  miopen : F.conv2d forward (+ a tony statistics pass) and MIOpen backward-weight (the TONY_STEM=0 path)
+  mfma   : tony_stem_fwd (statistics epilogue) and tony_stem_wgrad + split-K combine (the default path)
 
-usage: python tools/stem_bench.py [--batch 128] [--iters 20]
+Prints per-pass microseconds, the HBM bytes each pass must move and the implied TB/s, plus the
+numerics of the MFMA kernels against fp32.
+
+usage: python tools/stem_bench.py [--batch 128] [--iters 20] [--resnet]
 """
 import argparse
 import os
@@ -33,6 +35,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--resnet", action="store_true")
     args = ap.parse_args()
     from tony_amd.ops import _lib
     from tony_amd.ops import conv as C
@@ -40,42 +43,32 @@ def main():
     torch.backends.cudnn.benchmark = True
     dev = torch.device("cuda", 0)
     cl = torch.channels_last
-    x = torch.randn(args.batch, 3, 299, 299, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
-    w = (0.1 * torch.randn(32, 3, 3, 3, device=dev)).to(torch.bfloat16).contiguous(memory_format=cl)
-    y = torch.nn.functional.conv2d(x, w, None, 2, 0)
+    hw, co, k, s, p = (224, 64, 7, 2, 3) if args.resnet else (299, 32, 3, 2, 0)
+    x = torch.randn(args.batch, 3, hw, hw, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
+    w = (0.1 * torch.randn(co, 3, k, k, device=dev)).to(torch.bfloat16).contiguous(memory_format=cl)
+    y = torch.nn.functional.conv2d(x, w, None, s, p)
     dy = torch.randn_like(y).contiguous(memory_format=cl)
-
-    x8 = torch.zeros(args.batch, 8, 299, 299, device=dev, dtype=torch.bfloat16).contiguous(memory_format=cl)
-    w8 = torch.zeros(32, 8, 3, 3, device=dev, dtype=torch.bfloat16).contiguous(memory_format=cl)
-    w8[:, :3] = w
-    stats = torch.zeros(_lib.stat_floats(32), device=dev)
-
-    def pad():
-        x8[:, :3].copy_(x)
+    stats = torch.zeros(_lib.stat_floats(co), device=dev)
+    slot = torch.zeros_like(w)
 
     res = {
-        "miopen fwd": gpu_ms(lambda: C._miopen_fwd(x, w, 2, 0), args.iters),
-        "miopen fwd+stats": gpu_ms(lambda: C._miopen_fwd(x, w, 2, 0, stats), args.iters),
-        "miopen wgrad": gpu_ms(lambda: C._miopen_wgrad(dy, x, w, 2, 0), args.iters),
-        "pad 3->8": gpu_ms(pad, args.iters),
-        "tony fwd+stats (pad8)": gpu_ms(lambda: C.conv_fwd(x8, w8, 2, 0, stats), args.iters),
-        "tony wgrad (pad8)": gpu_ms(lambda: C.conv_wgrad(dy, x8, w8.shape, 2, 0), args.iters),
-        "direct fwd (stem.hip)": gpu_ms(lambda: C.stem_fwd(x, w, 2, 0), args.iters),
-        "direct fwd+stats (stem.hip)": gpu_ms(lambda: C.stem_fwd(x, w, 2, 0, stats), args.iters),
+        "miopen fwd+stats": gpu_ms(lambda: C._miopen_fwd(x, w, s, p, stats), args.iters),
+        "miopen wgrad": gpu_ms(lambda: C._miopen_wgrad(dy, x, w, s, p), args.iters),
+        "mfma fwd": gpu_ms(lambda: C.stem_fwd(x, w, s, p), args.iters),
+        "mfma fwd+stats": gpu_ms(lambda: C.stem_fwd(x, w, s, p, stats), args.iters),
+        "mfma wgrad (into slot)": gpu_ms(lambda: C.stem_wgrad(dy, x, w.shape, s, p, dst=slot), args.iters),
     }
-    # numerics of the padded path vs the fp32 reference
-    ref = torch.nn.functional.conv2d(x.float(), w.float(), None, 2, 0)
-    got = C.conv_fwd(x8, w8, 2, 0).float()
-    dwr = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), 2, 0)
-    dwg = C.conv_wgrad(dy, x8, w8.shape, 2, 0)[:, :3].float()
-    for k, v in res.items():
-        print(f"{k:>24}: {v * 1000:8.1f} us")
-    print(f"miopen total {1000 * (res['miopen fwd+stats'] + res['miopen wgrad']):.1f} us; pad8 total "
-          f"{1000 * (res['pad 3->8'] + res['tony fwd+stats (pad8)'] + res['tony wgrad (pad8)']):.1f} us")
-    got_d = C.stem_fwd(x, w, 2, 0).float()
-    print("direct fwd rel err", ((got_d - ref).norm() / ref.norm()).item())
-    print("fwd max rel err", ((got - ref).abs().max() / ref.abs().max()).item(),
-          "wgrad max rel err", ((dwg - dwr).abs().max() / dwr.abs().max()).item())
+    xb, yb = x.numel() * 2, y.numel() * 2
+    moved = {"miopen fwd+stats": xb + 2 * yb, "miopen wgrad": xb + yb, "mfma fwd": xb + yb,
+             "mfma fwd+stats": xb + yb, "mfma wgrad (into slot)": xb + yb}
+    for name, ms in res.items():
+        print(f"{name:>24}: {ms * 1000:8.1f} us  ({moved[name] / ms / 1e9:5.2f} TB/s of {moved[name] / 1e6:.0f} MB)")
+    ref = torch.nn.functional.conv2d(x.float(), w.float(), None, s, p)
+    got = C.stem_fwd(x, w, s, p).float()
+    dwr = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), s, p)
+    dwg = C.stem_wgrad(dy, x, w.shape, s, p).float()
+    print("fwd rel err", ((got - ref).norm() / ref.norm()).item(),
+          "wgrad rel err", ((dwg - dwr).norm() / dwr.norm()).item())
 
 
 if __name__ == "__main__":
