@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--tune-cache", default=None,
                     help="JSON of kernel-choice decisions: loaded when it exists (no autotuning for those "
                          "shapes), written after setup otherwise (reproducible profiles, faster startup)")
+    ap.add_argument("--collective", default=None, choices=["rccl", "hip"],
+                    help="gradient push / pull collectives: RCCL (default) or tony_amd's xGMI peer-memory "
+                         "kernels (csrc/xgmi.hip); sets TONY_COLLECTIVE")
     ap.add_argument("--no-miopen-find", action="store_true",
                     help="MIOpen immediate mode instead of find (faster startup, slower non-1x1 convs)")
     return ap.parse_args()
@@ -141,6 +144,8 @@ def _heartbeat(t0: float, every_s: float = 45.0) -> None:
 
 def main():
     args = parse()
+    if args.collective:
+        os.environ["TONY_COLLECTIVE"] = args.collective
     if int(os.environ.get("RANK", "0")) == 0:
         _heartbeat(time.perf_counter())
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -292,7 +297,8 @@ def main():
     torch.cuda.synchronize()
 
     elapsed = max_over_ranks(elapsed, device=dev)
-    final_loss = float(loss.float().item())
+    # the dedicated ps rank runs no model: report a worker's loss
+    final_loss = max_over_ranks(float(loss.float().item()) if ps.is_worker else float("-inf"), device=dev)
     fallbacks = coll.fallback_count()
     if rank == 0:
         imgs = args.batch * n_workers * args.steps
@@ -342,6 +348,8 @@ def main():
                                                     round(1000.0 * trainer.host_bwd_s, 3)],
                 "kernels": "tony_amd HIP" if fused else "stock PyTorch-ROCm (MIOpen / hipBLASLt)",
                 "conv_impl": _conv_impl_counts(),
+                "collective": "hip-xgmi" if os.environ.get("TONY_COLLECTIVE", "rccl").lower() in ("hip", "xgmi")
+                else ("rccl" if dist.is_initialized() and dist.get_backend() == "nccl" else None),
                 "collective_fallbacks": fallbacks,
                 "dist": diag or None,
                 "final_loss": round(final_loss, 4),

@@ -1,7 +1,11 @@
-"""xGMI peer-memory collectives (csrc/xgmi.hip): 2 ranks as 2 processes sharing the test box's GPU.
+"""xGMI peer-memory collectives (csrc/xgmi.hip): 2-4 ranks as processes sharing the test box's GPU.
 
-The single-GPU box cannot exercise real xGMI links; this checks the IPC window exchange, the
-per-workgroup flag barriers, the slot parity protocol and the reductions against exact values.
+The single-GPU box cannot exercise real xGMI links; this checks the IPC window exchange, the push
+reduce-scatter into peer windows, the per-workgroup flag barriers, the slot parity protocol (1,000
+back-to-back calls, alternating parities with changing data), odd sizes and slot-sized pieces
+against exact values, and that a rank whose peer skips a call gets XgmiError instead of a result.
+A peer killed outright is not staged here: the survivor's push would store into the dead process's
+freed window (a GPU fault on a shared box); the skipped call exercises the same bounded barrier.
 """
 import multiprocessing as mp
 import socket
@@ -19,7 +23,7 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_xgmi_collectives(world, monkeypatch):
     import xgmi_worker as W
 

@@ -16,7 +16,8 @@ def run(rank, world, port, q, skip=False):
         dev = torch.device("cuda", 0)
         res = {}
         for dtype in (torch.float32, torch.bfloat16):
-            for n in (1024, 40960, 3 * (1 << 20) // 4 + 4096):  # one-shot, two-shot, multi-piece
+            # one-shot, two-shot, odd size (two-shot pieces + a one-shot tail), multi-piece
+            for n in (1024, 40960, 100040, 3 * (1 << 20) // 4 + 4096):
                 t = torch.full((n,), float(rank + 1), device=dev, dtype=dtype)
                 t += torch.arange(n, device=dev, dtype=torch.float32).remainder(7).to(dtype)
                 comm.all_reduce(t)
@@ -51,9 +52,17 @@ def run(rank, world, port, q, skip=False):
             res[f"ag_big_{dtype}"] = bool(torch.equal(g.float(), exp))
         # many back-to-back calls: the slot parity / epoch protocol never desynchronises
         t = torch.ones(4096, device=dev)
-        for _ in range(300):
+        for _ in range(1000):
             comm.all_reduce(t, average=True)
         res["back_to_back"] = bool((t == 1.0).all().item())
+        # slot wrap: two-shot calls alternating between the two slot parities with changing data
+        u = torch.empty(world * 8192, device=dev)
+        ok = True
+        for k in range(20):
+            u.fill_(float(k + rank))
+            comm.all_reduce(u)
+            ok &= bool((u == float(world * k + sum(range(world)))).all().item())
+        res["slot_wrap"] = ok
         torch.cuda.synchronize()
         comm.check_error()
         # a peer that skips a collective: the waiting rank's barrier gives up and the NEXT check raises

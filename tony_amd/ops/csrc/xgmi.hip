@@ -2,20 +2,27 @@
 // alternative to RCCL for one-process-per-GPU jobs: one-shot and two-shot all-reduce,
 // reduce-scatter, all-gather and broadcast, bf16 or fp32, fp32 accumulation.
 //
-// Every rank owns one "window" (hipExtMallocWithFlags, uncached so peer stores and polls are
-// coherent without cache maintenance) that all peers map with hipIpcOpenMemHandle:
+// Every rank owns one "window" that all peers map with hipIpcOpenMemHandle:
 //
-//   [flags: 2 phases x kMaxRanks x kMaxBlocks u32 | slot 0 | slot 1 | result 0 | result 1]
+//   [flags: 2 phases x kMaxRanks x kMaxBlocks u32, error word | slot 0 | slot 1 | result 0 | result 1]
 //
-// A call copies its input into this rank's slot (parity = epoch & 1, so back-to-back calls never
-// overwrite a slot a slow peer may still read: a rank can only start call k+2 after every peer
-// passed call k+1's first barrier, i.e. finished call k), then every workgroup b meets workgroup b
-// of every peer at a flag barrier and reads the peers' slots directly over xGMI -- each GPU pulls
-// from all 7 links at once instead of one ring neighbour.
+// Windows are fine-grained device memory (cached; hipDeviceMallocUncached with
+// TONY_XGMI_MEM=uncached); every hand-off is a system-scope release (writer) / acquire (reader)
+// around a per-workgroup flag barrier.
 //
-//   one-shot  (small messages): read chunk b of every peer's slot, sum, write out.
-//   two-shot  (large): reduce-scatter -- rank r reduces shard r (chunk b) from all peers into its
-//             result region -- barrier -- all-gather of the reduced shards from every peer.
+// Reductions PUSH: workgroup b of rank r writes chunk b of its input shard s straight into rank
+// s's slot at row r (remote stores over the s<->r link; no copy of the input into the local
+// window), meets workgroup b of every peer at a flag barrier, then reduces chunk b of its own shard
+// from its own input and the peers' rows of its (local) slot.  Slot parity = epoch & 1, so
+// back-to-back calls never overwrite a row a slow peer may still read: a rank can only start call
+// k+2 after every peer passed call k+1's barrier, i.e. finished reading call k.
+//
+//   one-shot  (small): every rank pushes its whole buffer to every peer; each reduces all of it.
+//   two-shot  (large): push reduce-scatter -> reduced shard into the local result region ->
+//             barrier -> all-gather PULLED from every peer's result region (each GPU reads from all
+//             7 links at once instead of one ring neighbour).
+//   all-gather / broadcast: the own shard (1/n of the output) / the root's buffer is staged in
+//             the local slot and every peer pulls it.
 //
 // Barriers spin with a bound: a peer that never arrives (crashed rank) makes the kernel record an
 // error in the window's error word and exit instead of hanging the GPU; the host raises on it.
@@ -30,9 +37,10 @@ using namespace tony;
 namespace {
 
 constexpr int kMaxRanks = 8;
-constexpr int kMaxBlocks = 64;  // workgroups per collective launch
+constexpr int kMaxBlocks = 256;  // workgroups per collective launch
 constexpr int64_t kFlagBytes = 2LL * kMaxRanks * kMaxBlocks * 4;
-constexpr int64_t kHeader = 65536;  // flags + error word, keeps the slots 64 KiB aligned
+constexpr int64_t kHeader = 65536;  // flags (16 KiB) + error word, keeps the slots 64 KiB aligned
+static_assert(kFlagBytes + 64 <= kHeader, "flags + error word fit the header");
 constexpr int64_t kErrOff = kFlagBytes;
 constexpr long kSpinLimit = 1L << 26;  // ~seconds of polling before a barrier gives up
 
@@ -118,18 +126,18 @@ __device__ __forceinline__ void copy16(uint8_t* dst, const uint8_t* src, int64_t
     reinterpret_cast<uint4*>(dst)[v] = reinterpret_cast<const uint4*>(src)[v];
 }
 
-// dst vectors [v0,v1) = scale * sum over ranks of src_r (each src at byte offset off of slot/result)
+// dst vectors [v0,v1) = scale * (own[v] + sum over peers p of row p of this rank's slot at off)
 template <bool BF16>
-__device__ void reduce_peers(const Comm& c, int which, uint32_t epoch, int64_t off, uint8_t* dst, int64_t v0,
-                             int64_t v1, float scale) {
+__device__ void reduce_rows(const Comm& c, uint32_t epoch, const uint8_t* own, int64_t row_bytes, int64_t off,
+                            uint8_t* dst, int64_t v0, int64_t v1, float scale) {
   using E = Elem<BF16>;
+  const uint8_t* base = slot(c, c.rank, 0, epoch) + off;
   for (int64_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
     float acc[E::kVec], f[E::kVec];
-#pragma unroll
-    for (int j = 0; j < E::kVec; ++j) acc[j] = 0.f;
-    for (int r = 0; r < c.nranks; ++r) {
-      const int p = (c.rank + r) % c.nranks;  // stagger the peers so the 7 links are loaded evenly
-      E::load(slot(c, p, which, epoch) + off + v * 16, f);
+    E::load(own + v * 16, acc);
+    for (int p = 0; p < c.nranks; ++p) {
+      if (p == c.rank) continue;
+      E::load(base + p * row_bytes + v * 16, f);
 #pragma unroll
       for (int j = 0; j < E::kVec; ++j) acc[j] += f[j];
     }
@@ -147,29 +155,36 @@ __global__ __launch_bounds__(512) void xgmi_kernel(Comm c, int kind, const uint8
   const int64_t nvec = bytes / 16;
   int64_t v0, v1;
   uint8_t* my_slot = slot(c, c.rank, 0, epoch);
-  if (kind == 0) {  // one-shot
+  if (kind == 0) {  // one-shot: push the whole buffer to row `rank` of every peer's slot
     chunk(nvec, &v0, &v1);
-    copy16(my_slot, in, v0, v1);
+    for (int i = 1; i < c.nranks; ++i) {
+      const int p = (c.rank + i) % c.nranks;  // stagger the peers so the 7 links are loaded evenly
+      copy16(slot(c, p, 0, epoch) + static_cast<int64_t>(c.rank) * bytes, in, v0, v1);
+    }
     if (!peer_barrier(c, 0, epoch)) return;
-    reduce_peers<BF16>(c, 0, epoch, 0, out, v0, v1, scale);
+    reduce_rows<BF16>(c, epoch, in, bytes, 0, out, v0, v1, scale);
     return;
   }
-  if (kind == 1 || kind == 2) {  // reduce-scatter (+ all-gather for two-shot); bytes = full input
+  if (kind == 1 || kind == 2) {  // push reduce-scatter (+ pulled all-gather for two-shot); bytes = full input
     const int64_t svec = nvec / c.nranks;  // vectors per shard
+    const int64_t sbytes = svec * 16;
     chunk(svec, &v0, &v1);
-    for (int s = 0; s < c.nranks; ++s) copy16(my_slot + s * svec * 16, in + s * svec * 16, v0, v1);
+    for (int i = 1; i < c.nranks; ++i) {  // shard p of the input -> row `rank` of rank p's slot
+      const int p = (c.rank + i) % c.nranks;
+      copy16(slot(c, p, 0, epoch) + static_cast<int64_t>(c.rank) * sbytes, in + p * sbytes, v0, v1);
+    }
     if (!peer_barrier(c, 0, epoch)) return;
-    const int64_t off = static_cast<int64_t>(c.rank) * svec * 16;
+    const int64_t off = static_cast<int64_t>(c.rank) * sbytes;
     if (kind == 2) {
-      reduce_peers<BF16>(c, 0, epoch, off, out, v0, v1, scale);
+      reduce_rows<BF16>(c, epoch, in + off, sbytes, 0, out, v0, v1, scale);
       return;
     }
     uint8_t* my_res = slot(c, c.rank, 1, epoch);
-    reduce_peers<BF16>(c, 0, epoch, off, my_res + off, v0, v1, scale);
+    reduce_rows<BF16>(c, epoch, in + off, sbytes, 0, my_res + off, v0, v1, scale);
     if (!peer_barrier(c, 1, epoch)) return;
     for (int r = 0; r < c.nranks; ++r) {
       const int p = (c.rank + r) % c.nranks;
-      const int64_t o = static_cast<int64_t>(p) * svec * 16;
+      const int64_t o = static_cast<int64_t>(p) * sbytes;
       copy16(out + o, slot(c, p, 1, epoch) + o, v0, v1);
     }
     return;
@@ -200,7 +215,9 @@ TONY_API int tony_xgmi_max_ranks() { return kMaxRanks; }
 TONY_API int tony_xgmi_alloc(int64_t slot_bytes, void** window, void* handle) {
   if (slot_bytes <= 0 || (slot_bytes % 65536) || window == nullptr || handle == nullptr) return -1;
   const size_t total = static_cast<size_t>(kHeader + 4 * slot_bytes);
-  hipError_t e = hipExtMallocWithFlags(window, total, hipDeviceMallocUncached);
+  const char* mem = std::getenv("TONY_XGMI_MEM");
+  const bool uncached = mem != nullptr && std::strcmp(mem, "uncached") == 0;
+  hipError_t e = hipExtMallocWithFlags(window, total, uncached ? hipDeviceMallocUncached : hipDeviceMallocFinegrained);
   if (e != hipSuccess) return static_cast<int>(e);
   e = hipMemset(*window, 0, total);
   if (e != hipSuccess) return static_cast<int>(e);
@@ -236,12 +253,14 @@ TONY_API int tony_xgmi_error_async(void* window, int* host_err, hipStream_t stre
 
 // windows: host array of nranks window pointers as mapped in this process (own window at [rank]).
 // kind as xgmi_kernel; bytes: input bytes (multiple of 16; for reduce-scatter / two-shot a multiple
-// of 16 * nranks); scale multiplies the reduced sums (1/nranks for an average).
+// of 16 * nranks; one-shot: nranks * bytes must fit a slot); scale multiplies the reduced sums
+// (1/nranks for an average).  blocks: workgroups (<= 256), the SAME on every rank for a call.
 TONY_API int tony_xgmi_collective(const uint64_t* windows, int rank, int nranks, int64_t slot_bytes, int kind,
                                   const void* in, void* out, int64_t bytes, int dtype_bf16, int root, float scale,
                                   uint32_t epoch, int blocks, hipStream_t stream) {
   if (nranks < 1 || nranks > kMaxRanks || rank < 0 || rank >= nranks || kind < 0 || kind > 4) return -1;
   if (bytes <= 0 || (bytes % 16) || bytes > slot_bytes) return -1;
+  if (kind == 0 && bytes * nranks > slot_bytes) return -1;  // one-shot: a row per rank
   if ((kind == 1 || kind == 2) && (bytes % (16LL * nranks))) return -1;
   if (((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) || epoch == 0) return -1;
   if (root < 0 || root >= nranks) return -1;

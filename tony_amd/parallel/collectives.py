@@ -14,8 +14,10 @@ import os
 import torch
 import torch.distributed as dist
 
-# TONY_COLLECTIVE=hip (conf tony.amd.collective, exported by the coordinator) routes the flat
-# GPU collectives of the default group through tony_amd's xGMI peer-memory kernels (xgmi.py)
+# TONY_COLLECTIVE=hip (conf tony.amd.collective, exported by the coordinator; bench.py
+# --collective hip) routes the flat GPU collectives of the default group through tony_amd's xGMI
+# peer-memory kernels (xgmi.py), whatever the process group's backend (a gloo group only carries
+# the IPC-handle exchange: the one-GPU multi-process rehearsal of that path)
 _XGMI = [None]
 
 
@@ -59,15 +61,15 @@ def reduce_scatter_flat(out: torch.Tensor, inp: torch.Tensor, group=None, async_
         if out.data_ptr() != inp.data_ptr():
             out.copy_(inp)
         return None
+    x = _xgmi(inp, group)  # before the gloo emulation: a gloo group can carry the xGMI handshake
+    if x is not None:
+        x.reduce_scatter(out, inp)
+        return None
     if _is_gloo(group):
         dist.all_reduce(inp, group=group)
         r = rank(group)
         n = out.numel()
         out.copy_(inp[r * n:(r + 1) * n])
-        return None
-    x = _xgmi(inp, group)
-    if x is not None:
-        x.reduce_scatter(out, inp)
         return None
     return dist.reduce_scatter_tensor(out, inp, group=group, async_op=async_op)
 
@@ -78,15 +80,15 @@ def all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group=None, async_op=F
         if out.data_ptr() != inp.data_ptr():
             out.copy_(inp)
         return None
+    x = _xgmi(inp, group)
+    if x is not None:
+        x.all_gather(out, inp)
+        return None
     if _is_gloo(group):
         n = inp.numel()
         parts = [out[i * n:(i + 1) * n] for i in range(world(group))]
         src = inp.clone() if any(p.data_ptr() == inp.data_ptr() for p in parts) else inp
         dist.all_gather(parts, src, group=group)
-        return None
-    x = _xgmi(inp, group)
-    if x is not None:
-        x.all_gather(out, inp)
         return None
     return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
 
@@ -94,7 +96,7 @@ def all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group=None, async_op=F
 def all_reduce(t: torch.Tensor, op=None, group=None, async_op=False):
     if world(group) == 1:
         return None
-    x = _xgmi(t, group) if op in (None, dist.ReduceOp.SUM) and not _is_gloo(group) else None
+    x = _xgmi(t, group) if op in (None, dist.ReduceOp.SUM) else None
     if x is not None and t.is_contiguous():
         x.all_reduce(t)
         return None
@@ -104,7 +106,7 @@ def all_reduce(t: torch.Tensor, op=None, group=None, async_op=False):
 def broadcast(t: torch.Tensor, src: int, group=None, async_op=False):
     if world(group) == 1:
         return None
-    x = _xgmi(t, group) if not _is_gloo(group) else None
+    x = _xgmi(t, group)
     if x is not None and t.is_contiguous():
         x.broadcast(t, src)
         return None

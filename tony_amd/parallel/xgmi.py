@@ -1,15 +1,15 @@
 """Hand-written intra-node collectives over xGMI peer memory (csrc/xgmi.hip), RCCL's alternative.
 
 One process per GPU, as everywhere in tony_amd.  ``XgmiComm(group)`` allocates this rank's
-window, exchanges the IPC handles over the (already initialised) process group and maps every
-peer's window; afterwards each collective is ONE kernel launch that copies the input into the
-local window, meets the peers at a per-workgroup flag barrier and pulls the peers' data directly
-over the links (a GPU reads from all 7 xGMI links at once, where a ring uses one
-in and one out):
+window (fine-grained device memory), exchanges the IPC handles over the (already initialised)
+process group and maps every peer's window; afterwards each collective is ONE kernel launch whose
+workgroups push their input shards straight into the owning peers' windows (no copy of the input
+into the local window), meet the peers at a per-workgroup flag barrier and reduce / pull over the
+links (a GPU drives all 7 xGMI links at once, where a ring uses one in and one out):
 
-* ``all_reduce``   one-shot below ``oneshot_max_bytes`` (latency bound: every rank reads every
-                   peer's whole buffer), two-shot above (reduce-scatter + all-gather, each rank
-                   moves 2 (n-1)/n of the bytes);
+* ``all_reduce``   one-shot below ``oneshot_max_bytes`` (latency bound: every rank pushes its
+                   whole buffer to every peer), two-shot above (push reduce-scatter + pulled
+                   all-gather, each rank moves 2 (n-1)/n of the bytes);
 * ``reduce_scatter`` / ``all_gather`` / ``broadcast``  the flat single-launch forms the
                    parameter server and DDP buckets use.
 
@@ -38,7 +38,7 @@ class XgmiError(RuntimeError):
 
 class XgmiComm:
     def __init__(self, group=None, slot_bytes: int = 64 << 20, oneshot_max_bytes: int = 512 << 10,
-                 blocks: int = 64, device=None):
+                 blocks: Optional[int] = None, device=None):
         if not dist.is_initialized():
             raise XgmiError("XgmiComm needs an initialised torch.distributed process group")
         self.group = group
@@ -50,7 +50,7 @@ class XgmiComm:
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.slot_bytes = (int(slot_bytes) + 65535) // 65536 * 65536
         self.oneshot_max_bytes = int(oneshot_max_bytes)
-        self.blocks = int(blocks)
+        self.blocks = None if blocks is None else max(1, min(256, int(blocks)))
         self.epoch = 0
         hsize = L.tony_xgmi_handle_bytes()
         window = ctypes.c_void_p()
@@ -79,6 +79,14 @@ class XgmiComm:
         dist.barrier(group=group)
 
     # -- plumbing -------------------------------------------------------------------------------
+    def grid(self, nbytes: int) -> int:
+        """Workgroups of a launch moving ``nbytes``: one per ~256 KiB, 8..256 (every CU of the GPU
+        for large buckets, so each keeps xGMI requests in flight on all 7 links).  A pure function of
+        the size: all ranks must agree on the chunking of a call."""
+        if self.blocks is not None:
+            return self.blocks
+        return max(8, min(256, nbytes >> 18))
+
     def _launch(self, kind: int, inp: torch.Tensor, out: torch.Tensor, nbytes: int, root: int = 0,
                 scale: float = 1.0, in_off: int = 0, out_off: int = 0):
         if int(self._err_host[0]):  # an earlier collective's barrier timed out
@@ -88,7 +96,7 @@ class XgmiComm:
         rc = L.tony_xgmi_collective(self._windows, self.rank, self.world, self.slot_bytes, kind,
                                     inp.data_ptr() + in_off, out.data_ptr() + out_off, nbytes,
                                     int(inp.dtype == torch.bfloat16), root, float(scale),
-                                    self.epoch & 0xFFFFFFFF, self.blocks, stream)
+                                    self.epoch & 0xFFFFFFFF, self.grid(nbytes), stream)
         _lib.check(rc, "tony_xgmi_collective")
         _lib.check(L.tony_xgmi_error_async(ctypes.c_void_p(self.window), self._err_host.data_ptr(), stream),
                    "tony_xgmi_error_async")
@@ -116,17 +124,20 @@ class XgmiComm:
         self._check(t)
         scale = 1.0 / self.world if average else 1.0
         nbytes = t.numel() * t.element_size()
-        if nbytes <= min(self.oneshot_max_bytes, self.slot_bytes):
+        if nbytes <= min(self.oneshot_max_bytes, self.slot_bytes // self.world):  # a slot row per rank
             self._launch(KIND["allreduce_oneshot"], t, t, nbytes, scale=scale)
             return t
-        piece = self.slot_bytes // (16 * self.world) * (16 * self.world)
+        unit = 16 * self.world
+        piece = self.slot_bytes // unit * unit
         off = 0
         while off < nbytes:
             n = min(piece, nbytes - off)
-            if n % (16 * self.world):  # tail not divisible into equal shards: one-shot it
-                self._launch(KIND["allreduce_oneshot"], t, t, n, scale=scale, in_off=off, out_off=off)
-            else:
-                self._launch(KIND["allreduce_twoshot"], t, t, n, scale=scale, in_off=off, out_off=off)
+            main = n // unit * unit
+            if main:
+                self._launch(KIND["allreduce_twoshot"], t, t, main, scale=scale, in_off=off, out_off=off)
+            if n > main:  # < 16 * world bytes that do not split into equal shards: one-shot them
+                self._launch(KIND["allreduce_oneshot"], t, t, n - main, scale=scale, in_off=off + main,
+                             out_off=off + main)
             off += n
         return t
 

@@ -22,6 +22,8 @@ for s in "$@"; do
     newtests) step newtests 600 python -u -m pytest tests/test_ops_gpu.py tests/test_hvd_gpu.py tests/test_convergence_gpu.py tests/test_model_fp32_gpu.py -x -v -s --timeout 300 --timeout-method thread ;;
     stem) step stem 400 python -u -m pytest tests/test_conv_gpu.py tests/test_ops_gpu.py -x -v -k "stem or linear or whole_input" --timeout 200 --timeout-method thread ;;
     xgmi) step xgmi 300 python -u -m pytest tests/test_xgmi_gpu.py -x -v --timeout 200 --timeout-method thread ;;
+    bench2_hip) step bench2_hip 900 env TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 2 --steps 6 --warmup 3 --mode eager --collective hip ;;
+    coll2) step coll2 300 env TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29514 tools/coll_bench.py --max-mb 64 --json gpurun_out/coll2.json ;;
     bench_fp32) step bench_fp32 900 python bench.py --steps 10 --warmup 4 --dtype fp32 --mode eager ;;
     bench_gradfp32) step bench_gradfp32 900 python bench.py --steps 20 --warmup 6 --grad-dtype fp32 --tune-cache gpurun_out/tune.json ;;
     bench_nooverlap) step bench_nooverlap 900 python bench.py --steps 20 --warmup 6 --no-overlap --mode eager --tune-cache gpurun_out/tune.json ;;
