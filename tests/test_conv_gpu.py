@@ -338,3 +338,33 @@ def test_stem_conv_bn_act_layer_fwd_bwd(cuda):
     finally:
         C.AUTOTUNE, C.STEM = saved
         _lib.set_inplace_grads(True)
+
+
+# (N, Cin, H, W, Cout, padding): the shapes of the persistent direct 3x3 kernel (tile variant 10),
+# with partial edge tiles in both directions and several tiles per workgroup
+DIRECT_SHAPES = [(3, 32, 37, 45, 32, (0, 0)), (4, 32, 37, 37, 64, (1, 1)), (2, 64, 29, 35, 32, (1, 1)),
+                 (2, 64, 24, 20, 64, (1, 1)), (64, 32, 19, 21, 32, (1, 1))]
+
+
+@pytest.mark.parametrize("shape", DIRECT_SHAPES, ids=[f"{s[1]}->{s[4]}_{s[2]}x{s[3]}p{s[5][0]}" for s in DIRECT_SHAPES])
+def test_conv_direct_variant(cuda, shape):
+    """csrc/conv.hip conv_direct_kernel (variant 10): forward + BN statistics and backward-data vs fp32."""
+    from tony_amd.ops import _lib
+    from tony_amd.ops.conv import conv_dgrad, conv_fwd
+
+    n, c, h, w, co, p = shape
+    torch.manual_seed(11)
+    x = _nhwc(torch.randn(n, c, h, w, device=cuda)).to(torch.bfloat16)
+    wt = _nhwc(0.1 * torch.randn(co, c, 3, 3, device=cuda)).to(torch.bfloat16)
+    stats = torch.zeros(_lib.stat_floats(co), device=cuda)
+    y = conv_fwd(x, wt, 1, p, stats, vflags=10 << 8)
+    xr = x.float().requires_grad_(True)
+    ref = torch.nn.functional.conv2d(xr, wt.float(), None, 1, p)
+    assert _rel(y, ref) < 1e-2
+    st = _lib.fold_stats(stats, co)
+    torch.testing.assert_close(st[:co], ref.detach().sum((0, 2, 3)), rtol=2e-3, atol=ref.numel() / co * 2e-4)
+    torch.testing.assert_close(st[co:], (ref.detach() ** 2).sum((0, 2, 3)), rtol=2e-3, atol=1e-1)
+    dy = _nhwc(torch.randn_like(ref)).to(torch.bfloat16)
+    ref.backward(dy.float())
+    dx = conv_dgrad(dy, wt, x.shape, 1, p, vflags=10 << 8)
+    assert _rel(dx, xr.grad) < 1e-2

@@ -14,6 +14,7 @@
 // from one input pixel (or zero for padding).  The tap/channel position of a thread's chunk is
 // advanced incrementally per K-step (no divisions in the loop); the per-row pixel coordinates are
 // decoded once per tile (forward/dgrad) or advanced incrementally with the row (wgrad).
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -443,6 +444,224 @@ int run_halo(const Gather& g, const void* B, void* C, int64_t ldc, int64_t N, in
   return -3;
 }
 
+// ---- 3x3 stride-1 convs with 32 / 64 channels on both sides: persistent direct kernel ---------
+// Inception's 149x149 / 147x147 stem layers (and their dgrads, ResNet's 56x56 3x3s) move ~0.2-0.5
+// GB each for 50-100 GFLOP: they must run at HBM speed.  The halo kernel above re-stages the weight
+// panel for every 8x16 tile and serialises load -> barrier -> MFMA -> epilogue inside each
+// workgroup, so it is latency bound (~300 TF/s).  Here a persistent workgroup
+//   * stages the [CO][9*CS] weight panel in LDS ONCE,
+//   * walks 8 x TW output tiles (b, b + grid, ...), the NEXT tile's (8+2) x (TW+2) input halo in
+//     flight in registers while the current one computes (one LDS write + two barriers per tile),
+//   * computes D[co][px] = W . X^T (weights = MFMA A operand, halo pixels = B operand), so each lane
+//     ends with 4 consecutive channels of one pixel and stores them straight to global memory (8 B):
+//     no LDS staging of the output and no barrier in the epilogue,
+//   * keeps the BN statistics in registers over all its tiles (one sharded atomic per channel).
+constexpr int kDirectVariant = 10;  // tile-variant id the autotuner uses for this path (ops/tune.py)
+constexpr int kDirH = 8;
+
+template <int CS, int CO, int TW>
+struct DirectCfg {
+  static constexpr int R = 3, S = 3, TH = kDirH;
+  static constexpr int HH = TH + R - 1, HW = TW + S - 1;
+  static constexpr int PSTR = CS + 16;  // halo pixel pitch: 32-B pad, conflict-free ds_read_b128 groups
+  static constexpr int K = R * S * CS;
+  static constexpr int KP = K + 16;     // weight row pitch
+  static constexpr int HALO = HH * HW * PSTR;
+  static constexpr int WTS = CO * KP;
+  static constexpr int WPX = TH * TW / 4;  // pixels per wave
+  static constexpr int PB = WPX / 16, CB = CO / 16;
+  static constexpr int HCH = HH * HW * (CS / 8);  // 16-byte chunks of a halo
+  static constexpr int PFN = (HCH + kThreads - 1) / kThreads;
+  static constexpr size_t kLds = static_cast<size_t>(HALO + WTS) * sizeof(uint16_t);
+};
+
+template <int CS, int CO, int TW>
+__global__ __launch_bounds__(kThreads) void conv_direct_kernel(Gather g, const uint16_t* __restrict__ B,
+                                                              uint16_t* __restrict__ C, int64_t ldc,
+                                                              float* __restrict__ stats, int64_t sstride,
+                                                              int tiles_x, int tiles_y, int ntiles) {
+  using D = DirectCfg<CS, CO, TW>;
+  extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
+  uint16_t* halo = dsm;
+  uint16_t* wts = dsm + D::HALO;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kq = lane >> 4;
+
+  // weight panel [CO][K] -> LDS rows of KP (once per workgroup)
+  for (int v = threadIdx.x; v < CO * (D::K / 8); v += kThreads) {
+    const int row = v / (D::K / 8), k8 = v - row * (D::K / 8);
+    *reinterpret_cast<uint4*>(wts + row * D::KP + k8 * 8) =
+        *reinterpret_cast<const uint4*>(B + static_cast<int64_t>(row) * D::K + k8 * 8);
+  }
+
+  uint4 pf[D::PFN];
+  auto tile_origin = [&](int t, int& n, int& oy0, int& ox0) {
+    const int tx = t % tiles_x, rest = t / tiles_x;
+    const int ty = rest % tiles_y;
+    n = rest / tiles_y;
+    oy0 = ty * D::TH;
+    ox0 = tx * TW;
+  };
+  auto prefetch = [&](int t) {  // the halo of tile t into registers (zeros outside the image)
+    int n, oy0, ox0;
+    tile_origin(t, n, oy0, ox0);
+    const int hy0 = oy0 + g.offh - (g.sign < 0 ? D::R - 1 : 0);
+    const int hx0 = ox0 + g.offw - (g.sign < 0 ? D::S - 1 : 0);
+    const int64_t pix0 = static_cast<int64_t>(n) * g.Hs * g.Ws;
+#pragma unroll
+    for (int i = 0; i < D::PFN; ++i) {
+      const int v = i * kThreads + threadIdx.x;
+      const int hp = v / (CS / 8), c8 = v - hp * (CS / 8);
+      const int hy = hp / D::HW, hx = hp - hy * D::HW;
+      const int iy = hy0 + hy, ix = hx0 + hx;
+      pf[i] = make_uint4(0u, 0u, 0u, 0u);
+      if (v < D::HCH && static_cast<unsigned>(iy) < static_cast<unsigned>(g.Hs) &&
+          static_cast<unsigned>(ix) < static_cast<unsigned>(g.Ws))
+        pf[i] = *reinterpret_cast<const uint4*>(g.src + (pix0 + iy * g.Ws + ix) * g.ld + c8 * 8);
+    }
+  };
+
+  float ssum[D::CB][4], ssq[D::CB][4];
+#pragma unroll
+  for (int c = 0; c < D::CB; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ssum[c][r] = ssq[c][r] = 0.f;
+
+  if (blockIdx.x < ntiles) prefetch(blockIdx.x);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    __syncthreads();  // every wave is done reading the previous halo
+#pragma unroll
+    for (int i = 0; i < D::PFN; ++i) {
+      const int v = i * kThreads + threadIdx.x;
+      if (v < D::HCH) {
+        const int hp = v / (CS / 8), c8 = v - hp * (CS / 8);
+        *reinterpret_cast<uint4*>(halo + hp * D::PSTR + c8 * 8) = pf[i];
+      }
+    }
+    __syncthreads();
+    if (t + static_cast<int>(gridDim.x) < ntiles) prefetch(t + gridDim.x);  // in flight during the MFMAs
+
+    int pbase[D::PB];  // halo element offset of this lane's pixel in each 16-pixel block, tap (0, 0)
+#pragma unroll
+    for (int b = 0; b < D::PB; ++b) {
+      const int p = wave * D::WPX + b * 16 + (lane & 15);
+      pbase[b] = ((p / TW) * D::HW + (p % TW)) * D::PSTR + kq * 8;
+    }
+    f32x4 acc[D::PB][D::CB];
+#pragma unroll
+    for (int b = 0; b < D::PB; ++b)
+#pragma unroll
+      for (int c = 0; c < D::CB; ++c) acc[b][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < D::R; ++r)
+#pragma unroll
+      for (int s2 = 0; s2 < D::S; ++s2) {
+        const int rr = g.sign > 0 ? r : D::R - 1 - r, ss = g.sign > 0 ? s2 : D::S - 1 - s2;
+        const int hoff = (rr * D::HW + ss) * D::PSTR;
+#pragma unroll
+        for (int cb = 0; cb < CS / 32; ++cb) {
+          const int k0 = (r * D::S + s2) * CS + cb * 32 + kq * 8;
+          bf16x8_t wf[D::CB], xf[D::PB];
+#pragma unroll
+          for (int c = 0; c < D::CB; ++c)
+            wf[c] = *reinterpret_cast<const bf16x8_t*>(wts + (c * 16 + (lane & 15)) * D::KP + k0);
+#pragma unroll
+          for (int b = 0; b < D::PB; ++b) xf[b] = *reinterpret_cast<const bf16x8_t*>(halo + pbase[b] + hoff + cb * 32);
+#pragma unroll
+          for (int b = 0; b < D::PB; ++b)
+#pragma unroll
+            for (int c = 0; c < D::CB; ++c)
+              acc[b][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[c], xf[b], acc[b][c], 0, 0, 0);
+        }
+      }
+
+    // epilogue: lane holds channels c*16 + 4kq .. +3 of pixel b*16 + (lane & 15): one 8-byte store
+    int n, oy0, ox0;
+    tile_origin(t, n, oy0, ox0);
+#pragma unroll
+    for (int b = 0; b < D::PB; ++b) {
+      const int p = wave * D::WPX + b * 16 + (lane & 15);
+      const int oy = oy0 + p / TW, ox = ox0 + p % TW;
+      if (oy >= g.OH || ox >= g.OW) continue;
+      uint16_t* dst = C + ((static_cast<int64_t>(n) * g.OH + oy) * g.OW + ox) * ldc + kq * 4;
+#pragma unroll
+      for (int c = 0; c < D::CB; ++c) {
+        const f32x4 a = acc[b][c];
+        *reinterpret_cast<uint2*>(dst + c * 16) =
+            make_uint2(static_cast<uint32_t>(f2bf(a[0])) | (static_cast<uint32_t>(f2bf(a[1])) << 16),
+                       static_cast<uint32_t>(f2bf(a[2])) | (static_cast<uint32_t>(f2bf(a[3])) << 16));
+        if (stats != nullptr) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            ssum[c][r] += a[r];
+            ssq[c][r] = fmaf(a[r], a[r], ssq[c][r]);
+          }
+        }
+      }
+    }
+  }
+  if (stats == nullptr) return;
+  float* st = stats + shard_off(blockIdx.x, sstride);
+#pragma unroll
+  for (int c = 0; c < D::CB; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float a = ssum[c][r], q = ssq[c][r];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {  // sum over the 16 pixels of the lane's quarter
+        a += __shfl_xor(a, o, 64);
+        q += __shfl_xor(q, o, 64);
+      }
+      if ((lane & 15) == 0) {
+        atomicAdd(st + c * 16 + kq * 4 + r, a);
+        atomicAdd(st + CO + c * 16 + kq * 4 + r, q);
+      }
+    }
+}
+
+// The direct kernel for this shape, or -3 when it does not apply.
+int run_direct(const Gather& g, const void* B, void* C, int64_t ldc, int64_t N, int epi, float* st, int64_t sstride,
+               hipStream_t stream) {
+  if (g.R != 3 || g.S != 3 || g.sh != 1 || g.sw != 1 || (epi & 6) || (ldc % 4) || g.halo_images <= 0 ||
+      (reinterpret_cast<uintptr_t>(C) & 7) || (reinterpret_cast<uintptr_t>(B) & 15))
+    return -3;
+  const auto launch = [&](auto cs, auto co, auto tw) -> int {
+    constexpr int CS = decltype(cs)::value, CO = decltype(co)::value, TW = decltype(tw)::value;
+    using D = DirectCfg<CS, CO, TW>;
+    const void* fn = reinterpret_cast<const void*>(&conv_direct_kernel<CS, CO, TW>);
+    static int per_cu = 0;  // per template instance: resident workgroups per CU (occupancy query)
+    if (per_cu == 0) {
+      if (D::kLds > 65536 &&
+          hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(D::kLds)) != hipSuccess)
+        return -3;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kThreads, D::kLds) != hipSuccess || per_cu <= 0)
+        per_cu = -1;
+    }
+    if (per_cu < 0) return -3;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess)
+      return -3;
+    const int tiles_x = ceil_div(g.OW, TW), tiles_y = ceil_div(g.OH, kDirH);
+    const int64_t ntiles = static_cast<int64_t>(g.halo_images) * tiles_x * tiles_y;
+    if (ntiles > 0x7fffffff) return -2;
+    const int grid = static_cast<int>(std::min<int64_t>(ntiles, static_cast<int64_t>(per_cu) * cus));
+    conv_direct_kernel<CS, CO, TW><<<grid, kThreads, D::kLds, stream>>>(
+        g, static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), ldc, st, sstride, tiles_x, tiles_y,
+        static_cast<int>(ntiles));
+    TONY_LAUNCH_CHECK();
+    return 0;
+  };
+  using I = std::integral_constant<int, 32>;
+  using I64 = std::integral_constant<int, 64>;
+  using I16 = std::integral_constant<int, 16>;
+  if (g.Cs == 32 && N == 32) return launch(I{}, I{}, I{});
+  if (g.Cs == 32 && N == 64) return launch(I{}, I64{}, I16{});  // 8 x 32 tiles: 258 VGPRs, 1 wave/SIMD
+  if (g.Cs == 64 && N == 32) return launch(I64{}, I{}, I16{});
+  if (g.Cs == 64 && N == 64) return launch(I64{}, I64{}, I16{});
+  return -3;
+}
+
 int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, int flags, float* stats,
            int64_t sstride, hipStream_t stream) {
   // flags bit0: statistics accumulated into stats (the caller zeroes it, ops/arena.py);
@@ -453,6 +672,7 @@ int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int6
   float* st = stats;
   const int v = (flags >> 8) & 0xff;
   if (v == kHaloVariant) return run_halo(g, B, C, ldc, N, epi, st, sstride, stream);
+  if (v == kDirectVariant) return run_direct(g, B, C, ldc, N, epi, st, sstride, stream);
   if (v >= kNumNtVariants) return -1;
   if (v == 0) {
     const int64_t bn = pick_bn(N, 192);
@@ -470,7 +690,7 @@ int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int6
 // One residue class of a strided dgrad with tile variant v (flags bits 8..15 of tony_conv_dgrad_strided).
 int run_nt_phase(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, int v, const Phase& ph,
                  hipStream_t stream) {
-  if (v == kHaloVariant || v >= kNumNtVariants) return -1;
+  if (v == kHaloVariant || v == kDirectVariant || v >= kNumNtVariants) return -1;
   if (v == 0) {
     const int64_t bn = pick_bn(N, 192);
     return bn <= 64 ? launch_nt_bm<256, true>(g, B, C, ldc, M, N, nullptr, 0, 0, bn, stream, ph)

@@ -17,7 +17,8 @@ from typing import Callable, Dict, Hashable
 import torch
 
 AUTOTUNE = os.environ.get("TONY_CONV_AUTOTUNE", "1") != "0"
-NT_VARIANTS = tuple(range(10))  # csrc/mfma_common.h kNtVariants (0-8) + 9: conv.hip halo-tile 3x3 path
+NT_VARIANTS = tuple(range(11))  # csrc/mfma_common.h kNtVariants (0-8) + 9: conv.hip halo-tile 3x3 path,
+# 10: conv.hip persistent direct 3x3 kernel (32/64 channels)
 _CACHE: Dict[Hashable, int] = {}
 
 

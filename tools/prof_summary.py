@@ -24,8 +24,11 @@ def classify(name):
         return "tony HIP: fused BN+ReLU+maxpool (stem)"
     if "gemm_nt_kernel" in n or "gemm_tn_splitk" in n or "gemm_tn_glds" in n:
         return "tony HIP: MFMA GEMM (1x1 conv fwd/dgrad/wgrad)"
-    if "conv_nt_kernel" in n or "conv_wgrad_kernel" in n or "conv_wgrad_glds" in n or "conv_halo" in n:
+    if "conv_nt_kernel" in n or "conv_wgrad_kernel" in n or "conv_wgrad_glds" in n or "conv_halo" in n \
+            or "conv_direct_kernel" in n:
         return "tony HIP: implicit-GEMM conv (fwd/dgrad/wgrad)"
+    if "stem_fwd_kernel" in n or "stem_wgrad_kernel" in n:
+        return "tony HIP: MFMA image-stem conv (fwd/wgrad)"
     if "add_f32_kernel" in n:
         return "tony HIP: in-place grad accumulate"
     if "box3_kernel" in n or "maxpool_" in n or "avgpool_" in n:

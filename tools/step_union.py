@@ -16,6 +16,8 @@ def main():
     ap.add_argument("trace_dir")
     ap.add_argument("--marker", default="xent_fwd")
     ap.add_argument("--markers-per-step", type=int, default=2)
+    ap.add_argument("--per-queue", action="store_true", help="busy time per queue + the busiest queue's gaps")
+    ap.add_argument("--gaps", type=int, default=12)
     a = ap.parse_args()
     path = glob.glob(os.path.join(a.trace_dir, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
@@ -33,6 +35,29 @@ def main():
         u += ce - cs
         print(f"{hi - lo:5d} kernels  wall {wall / 1e6:7.2f} ms  kernel-sum {busy / 1e6:7.2f} ms  "
               f"union {u / 1e6:7.2f} ms")
+        if a.per_queue:
+            per_queue(rows[lo:hi], a.gaps)
+
+
+def per_queue(rows, ngaps):
+    """Busy time per hardware queue / stream of one step and the longest idle gaps of the busiest
+    one (the critical chain: a gap there is time the chain waited on the host or another stream)."""
+    key = "Stream_Id" if "Stream_Id" in rows[0] else "Queue_Id"
+    qs = {}
+    for r in rows:
+        qs.setdefault(r.get(key, "?"), []).append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    main_q = max(qs, key=lambda q: sum(e - s for s, e, _ in qs[q]))
+    for q, iv in sorted(qs.items(), key=lambda kv: -len(kv[1])):
+        busy = sum(e - s for s, e, _ in iv)
+        span = iv[-1][1] - iv[0][0]
+        print(f"    {key} {q}: {len(iv)} kernels, busy {busy / 1e6:.2f} ms over {span / 1e6:.2f} ms"
+              + ("  <- busiest" if q == main_q else ""))
+    iv = sorted(qs[main_q])
+    gaps = sorted(((b[0] - a[1], a[2][:60], b[2][:60]) for a, b in zip(iv, iv[1:])), reverse=True)
+    tot = sum(g for g, _, _ in gaps if g > 0)
+    print(f"    busiest queue: {tot / 1e6:.2f} ms of gaps between its kernels; longest:")
+    for g, a_, b_ in gaps[:ngaps]:
+        print(f"      {g / 1e3:8.1f} us  after {a_}  before {b_}")
 
 
 if __name__ == "__main__":
