@@ -82,9 +82,9 @@ _SIGNATURES = {
     "tony_stem_wgrad": [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                         c_int, c_int, c_int, c_int, c_void_p, c_int64, c_int_p, c_int, c_void_p],
     "tony_conv_dgrad": [c_void_p, c_int, c_int, c_int, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int,
-                        c_void_p, c_int, c_int, c_int64, c_int, c_void_p],
+                        c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_void_p],
     "tony_conv_dgrad_strided": [c_void_p, c_int, c_int, c_int, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_int,
-                                c_int, c_int, c_int, c_void_p, c_int, c_int, c_int64, c_int, c_void_p],
+                                c_int, c_int, c_int, c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_void_p],
     "tony_conv_wgrad": [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int, c_int, c_int, c_int,
                         c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_int_p, c_int, c_void_p,
                         c_void_p, c_int, c_void_p],
@@ -109,6 +109,15 @@ _SIGNATURES = {
     "tony_xgmi_collective": [c_u64_p, c_int, c_int, c_int64, c_int, c_void_p, c_void_p, c_int64, c_int, c_int,
                              c_float, ctypes.c_uint32, c_int, c_void_p],
 }
+
+
+class BnRed(ctypes.Structure):
+    """csrc/conv.hip ``BnRed``: the BatchNorm-backward reduction a backward-data kernel fuses into its
+    epilogue (z = layer L's BN input, the dgrad's output is dY of layer L); ``done`` is set when the
+    launched kernel reduced (a tile variant without the fused epilogue leaves it 0)."""
+    _fields_ = [("z", c_void_p), ("ldz", c_int64), ("mean", c_void_p), ("invstd", c_void_p), ("gamma", c_void_p),
+                ("beta", c_void_p), ("pb", c_int), ("relu", c_int), ("dsum", c_void_p), ("sstride", c_int64),
+                ("done", c_int)]
 
 
 class _SignedLib:
@@ -166,9 +175,18 @@ def bn_bwd_ws_floats(c: int) -> int:
 
 
 def bn_bwd(x, ldx: int, dy, lddy: int, dx, lddx: int, M: int, C: int, mean, invstd, gamma, beta, pb: int,
-           relu: bool, ws, dgamma, dbeta, accumulate: bool, device) -> None:
-    """dx (and dgamma/dbeta, added into when ``accumulate``) of y = relu?(bn(x)) from dy."""
+           relu: bool, ws, dgamma, dbeta, accumulate: bool, device, sums=None) -> None:
+    """dx (and dgamma/dbeta, added into when ``accumulate``) of y = relu?(bn(x)) from dy.  ``sums``:
+    the sharded [dsum | dsumx] already reduced by the kernel that produced dy (a dgrad epilogue,
+    csrc/conv.hip BnRed): only the apply pass runs."""
     L = lib()
+    if sums is not None:
+        rc = L.tony_bn_bwd_apply(x.data_ptr(), ldx, dy.data_ptr(), lddy, dx.data_ptr(), lddx, M, C, mean.data_ptr(),
+                                 invstd.data_ptr(), ptr(gamma), ptr(beta), pb, int(relu), sums.data_ptr(),
+                                 sums.data_ptr() + 4 * C, 2 * C, ptr(dgamma), ptr(dbeta), int(accumulate),
+                                 stream_ptr(device))
+        check(rc, "tony_bn_bwd_apply")
+        return
     if BN_ONEPASS and ws.numel() >= stat_floats(C) + 1:
         rc = L.tony_bn_bwd_onepass(x.data_ptr(), ldx, dy.data_ptr(), lddy, dx.data_ptr(), lddx, M, C,
                                    mean.data_ptr(), invstd.data_ptr(), ptr(gamma), ptr(beta), pb, int(relu),

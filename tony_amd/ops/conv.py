@@ -179,9 +179,11 @@ def dgrad_supported(x_shape, weight: torch.Tensor, stride=1, padding=0) -> bool:
 
 
 def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, padding=0,
-               vflags: int | None = None) -> torch.Tensor:
+               vflags: int | None = None, bnr: "_lib.BnRed | None" = None) -> torch.Tensor:
     """dX of conv(x, w): stride 1 is one implicit-GEMM transposed conv; a strided conv is one
-    launch per residue class of dX (csrc/conv.hip tony_conv_dgrad_strided, no MIOpen)."""
+    launch per residue class of dX (csrc/conv.hip tony_conv_dgrad_strided, no MIOpen).  With ``bnr``
+    the epilogue also accumulates the BN-backward reduction of the layer whose output x is
+    (``bnr.done`` tells whether the chosen kernel did)."""
     if not dgrad_supported(x_shape, weight, stride, padding):
         raise ValueError(f"conv_dgrad: unsupported x={tuple(x_shape)} w={tuple(weight.shape)} stride={stride} "
                          f"padding={padding}")
@@ -194,22 +196,70 @@ def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, paddin
     L, st = _lib.lib(), _lib.stream_ptr(dy.device)
 
     if (sh, sw) == (1, 1):
-        def launch(vf):
+        def launch(vf, br=None):
             return L.tony_conv_dgrad(dy.data_ptr(), n, dy.shape[2], dy.shape[3], co, lddy, wt.data_ptr(), c, r, s, ph,
-                                     pw, dx.data_ptr(), h, w, c, vf, st)
+                                     pw, dx.data_ptr(), h, w, c, vf, None if br is None else ctypes.byref(br), st)
         name = "tony_conv_dgrad"
     else:
-        def launch(vf):
-            if (vf >> 8) & 0xff == 9:  # the halo tile variant is stride-1 only
+        def launch(vf, br=None):
+            if (vf >> 8) & 0xff in (9, 10):  # the halo / direct tile variants are stride-1 only
                 return -3
             return L.tony_conv_dgrad_strided(dy.data_ptr(), n, dy.shape[2], dy.shape[3], co, lddy, wt.data_ptr(), c,
-                                             r, s, sh, sw, ph, pw, dx.data_ptr(), h, w, c, vf, st)
+                                             r, s, sh, sw, ph, pw, dx.data_ptr(), h, w, c, vf,
+                                             None if br is None else ctypes.byref(br), st)
         name = "tony_conv_dgrad_strided"
 
+    # variants are timed without the fused reduction (it must run exactly once)
     vf = vflags if vflags is not None else tune.pick(("conv_dgrad", tuple(dy.shape), lddy, tuple(weight.shape),
                                                          (sh, sw), (ph, pw)), launch)
-    _lib.check(launch(vf), name)
+    _lib.check(launch(vf, bnr), name)
     return dx
+
+
+class BnCtx:
+    """What a consumer's backward-data kernel needs to fuse layer L's BN-backward reduction
+    (csrc/conv.hip BnRed): L's BN input Z and its batch statistics / affine.  Attached by
+    ``_ConvBNActFn.forward`` to its output (``_tony_bnr``) and picked up by the conv that consumes it."""
+    __slots__ = ("Z", "ldz", "mean", "invstd", "gamma", "beta", "pb", "relu", "C", "__weakref__")
+
+    def __init__(self, Z, ldz, mean, invstd, gamma, beta, pb, relu):
+        self.Z, self.ldz, self.mean, self.invstd = Z, ldz, mean, invstd
+        self.gamma, self.beta, self.pb, self.relu, self.C = gamma, beta, pb, int(relu), Z.shape[1]
+
+
+# Opt-in (TONY_BN_FUSED_REDUCE=1).  Measured on MI355X it is a net loss: 24 of the 96 Inception-v3
+# reductions fuse (branch heads are _HeadFn layers, whose BN output no conv ctx reaches), the dgrad
+# epilogues grow by the Z reads + fold (+0.55 ms), and the apply pass no longer finds Z / dY warm in
+# the caches behind the reduce (+0.5 ms): 15.88 vs 15.60 ms/step, alternating A/B in one box session
+# (profiles/r2s3_rejected_bn_reduce_in_dgrad_ab.log).
+FUSED_REDUCE = os.environ.get("TONY_BN_FUSED_REDUCE", "0") == "1"
+FUSED_REDUCE_HITS = [0]  # BN backward passes that used a dgrad-fused reduction (tests, bench record)
+
+
+def _dgrad_fused_bn(ctx, dy, weight, x_shape, stride, padding):
+    """dX of the layer's conv; when its input is the output of a BN layer (``ctx.bnc_in``) the dgrad
+    also reduces that layer's BN-backward sums and tags dX with them (``_tony_bnsums``): if autograd
+    hands dX unchanged to that layer's backward, it skips its reduce kernel (``_bn_presums``)."""
+    bnc = getattr(ctx, "bnc_in", None)
+    if bnc is None or not FUSED_REDUCE or tuple(bnc.Z.shape) != tuple(x_shape):
+        return _dgrad(dy, weight, x_shape, stride, padding)
+    sums = zeros_f32(_lib.stat_floats(bnc.C), dy.device)
+    br = _lib.BnRed(bnc.Z.data_ptr(), bnc.ldz, bnc.mean.data_ptr(), bnc.invstd.data_ptr(), _lib.ptr(bnc.gamma),
+                    _lib.ptr(bnc.beta), bnc.pb, bnc.relu, sums.data_ptr(), 2 * bnc.C, 0)
+    dx = _dgrad(dy, weight, x_shape, stride, padding, br)
+    if br.done:
+        dx._tony_bnsums = (bnc, sums, dx._version)
+    return dx
+
+
+def _bn_presums(ctx, dy):
+    """The [dsum | dsumx] a consumer's dgrad reduced for THIS layer, if ``dy`` is exactly that dgrad's
+    output (same tensor, never modified: a gradient summed from several consumers does not qualify)."""
+    pre = getattr(dy, "_tony_bnsums", None)
+    if pre is None or pre[0] is not getattr(ctx, "bnc_self", None) or dy._version != pre[2]:
+        return None
+    FUSED_REDUCE_HITS[0] += 1
+    return pre[1]
 
 
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride=1, padding=0, dst=None):
@@ -368,21 +418,21 @@ def _fwd(x, weight, stride, padding, stats):
         _miopen_fwd(x, weight, stride, padding, stats)
 
 
-def _dgrad(dy, weight, x_shape, stride, padding):
+def _dgrad(dy, weight, x_shape, stride, padding, bnr=None):
     key = ("dgrad", tuple(dy.shape), tuple(weight.shape), stride, padding)
     if fullcover(x_shape, weight.shape, stride, padding):
         _CHOICE.setdefault(key, "gemm")
         return _gemm_dgrad(dy, weight, x_shape)
     impl = _CHOICE.get(key)  # steady state: no candidate closures to build
     if impl == "tony":
-        return conv_dgrad(dy, weight, x_shape, stride, padding)
+        return conv_dgrad(dy, weight, x_shape, stride, padding, bnr=bnr)
     if impl == "miopen":
         return _miopen_dgrad(dy, weight, x_shape, stride, padding)
     cands = {"miopen": lambda: _miopen_dgrad(dy, weight, x_shape, stride, padding)}
     if dgrad_supported(x_shape, weight, stride, padding):
         cands["tony"] = lambda: conv_dgrad(dy, weight, x_shape, stride, padding)
     impl = _choose(key, cands)
-    return conv_dgrad(dy, weight, x_shape, stride, padding) if impl == "tony" else \
+    return conv_dgrad(dy, weight, x_shape, stride, padding, bnr=bnr) if impl == "tony" else \
         _miopen_dgrad(dy, weight, x_shape, stride, padding)
 
 
@@ -454,6 +504,7 @@ class _ConvFn(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         ctx.params = (weight,)
         ctx.stride, ctx.padding = stride, padding
+        ctx.bnc_in = getattr(x, "_tony_bnr", None)
         return y
 
     @staticmethod
@@ -461,7 +512,7 @@ class _ConvFn(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         dy = _as_rows(dy)[0]
         dw = _wgrad(dy, x, weight, ctx.stride, ctx.padding)  # first: overlaps the dgrad on the side stream
-        dx = _dgrad(dy, weight, x.shape, ctx.stride, ctx.padding) if ctx.needs_input_grad[0] else None
+        dx = _dgrad_fused_bn(ctx, dy, weight, x.shape, ctx.stride, ctx.padding) if ctx.needs_input_grad[0] else None
         streams.keep(dx)  # may be consumed on another (branch) stream
         _lib.report_inplace(ctx.params, (dw,))
         return dx, dw, None, None
@@ -510,6 +561,11 @@ class _ConvBNActFn(torch.autograd.Function):
         ctx.save_for_backward(x, weight, gamma, beta, mean, invstd, Z)
         ctx.params = (weight, gamma, beta)
         ctx.cfg = (stride, padding, relu, pb)
+        ctx.bnc_in = getattr(x, "_tony_bnr", None)
+        ctx.bnc_self = None
+        if training and slot is None:  # a consumer conv's dgrad may reduce this layer's BN backward
+            ctx.bnc_self = BnCtx(Z, ldz, mean, invstd, gamma, beta, pb, relu)
+            y._tony_bnr = ctx.bnc_self
         return y
 
     @staticmethod
@@ -526,17 +582,18 @@ def _conv_bn_backward(ctx, x, weight, gamma, beta, mean, invstd, Z, dy):
     stride, padding, relu, pb = ctx.cfg
     dev = x.device
     M, co, ldz = _rows_view(Z)
+    presums = _bn_presums(ctx, dy)  # reduced by the consumer's dgrad epilogue
     dy, (_, _, lddy) = _as_rows(dy)
     dZ = torch.empty_like(Z)
-    ws = zeros_f32(_lib.bn_bwd_ws_floats(co), dev)
+    ws = None if presums is not None else zeros_f32(_lib.bn_bwd_ws_floats(co), dev)
     gg, gb = _lib.grad_slot(ctx.params[1]), _lib.grad_slot(ctx.params[2])
     inplace = gg is not None and gb is not None
     dgamma = gg if inplace else torch.empty_like(gamma)
     dbeta = gb if inplace else torch.empty_like(beta)
     _lib.bn_bwd(Z, ldz, dy, lddy, dZ, ldz, M, co, mean, invstd, gamma, beta, pb, relu, ws, dgamma, dbeta, inplace,
-                dev)
+                dev, sums=presums)
     dw = _wgrad(dZ, x, weight, stride, padding)  # first: overlaps the dgrad on the side stream
-    dx = _dgrad(dZ, weight, x.shape, stride, padding) if ctx.needs_input_grad[0] else None
+    dx = _dgrad_fused_bn(ctx, dZ, weight, x.shape, stride, padding) if ctx.needs_input_grad[0] else None
     streams.keep(dx)  # may be consumed on another (branch) stream
     if inplace:
         dgamma = dbeta = None
@@ -575,6 +632,7 @@ class _ConvBNActPoolFn(torch.autograd.Function):
         ctx.params = (weight, gamma, beta)
         ctx.cfg = (stride, padding, True, pb)
         ctx.pool = (k, s)
+        ctx.bnc_in = getattr(x, "_tony_bnr", None)
         return y
 
     @staticmethod

@@ -107,12 +107,98 @@ __device__ __forceinline__ void store_rows(uint16_t* lds, const uint4* regs) {
 // reduced filter.  The A operand is the usual flipped-tap gather of dY (Gather over the taps (a, b));
 // B rows are read straight out of the full transposed filter Wt [Ci][R][S][Co] at the class's taps
 // (no per-class weight copies), and the epilogue scatters GEMM rows back to the class's pixels.
+// BatchNorm-backward reduction fused into a backward-data epilogue.  The dgrad of conv L+1 produces
+// dY_L, the output gradient of layer L's BN(+ReLU), whose backward first reduces
+//   dsum[c] = sum dY', dsumx[c] = sum dY' * xhat,  xhat = (Z - mean) * invstd,
+//   dY' = dY masked by ReLU(gamma * xhat + beta) > 0 (relu)
+// over every pixel (csrc/bn_act.hip bn_bwd_reduce_kernel).  When layer L's output feeds ONLY conv
+// L+1, the dgrad epilogue has every dY tile at hand: it reads the matching Z tile, accumulates the two
+// sums (from the bf16-rounded dY it stores, as the reduce kernel would read it) and adds them into
+// the sharded [dsum | dsumx] buffer -- the separate 2-pass reduce over Z and dY disappears.
+struct BnRed {
+  const uint16_t* z = nullptr;  // Z of layer L (rows = the dgrad's output pixels), nullptr = off
+  int64_t ldz = 0;
+  const float* mean = nullptr;
+  const float* invstd = nullptr;
+  const void* gamma = nullptr;
+  const void* beta = nullptr;
+  int pb = 0;                   // gamma / beta are bf16
+  int relu = 0;
+  float* dsum = nullptr;        // [dsum C | dsumx C], kStatShards copies sstride floats apart (zeroed)
+  int64_t sstride = 0;
+  int done = 0;                 // host side: set by the launcher when the chosen kernel reduced
+};
+
+__device__ __forceinline__ float bnr_param(const void* p, int c, int pb, float dflt) {
+  if (p == nullptr) return dflt;
+  return pb ? bf2f(static_cast<const uint16_t*>(p)[c]) : static_cast<const float*>(p)[c];
+}
+
+// per-channel (xhat = z*p0 + p1, pre-activation = z*p2 + p3) of channel c
+__device__ __forceinline__ void bnr_coef(const BnRed& br, int c, float& p0, float& p1, float& p2, float& p3) {
+  const float mu = br.mean[c], is = br.invstd[c];
+  const float g = bnr_param(br.gamma, c, br.pb, 1.f), be = bnr_param(br.beta, c, br.pb, 0.f);
+  p0 = is;
+  p1 = -mu * is;
+  p2 = g * is;
+  p3 = be - g * is * mu;
+}
+
 struct Phase {
   int R, S;      // taps of the full filter: Wt row layout [R][S][Co]
   int r0, s0;    // the class's first tap
   int tsy, tsx;  // tap step (= conv stride)
   RowMap rows;   // GEMM row -> dX pixel
+  BnRed bnr;     // fused BN-backward reduction of the dgrad output (any dgrad, strided or not)
 };
+
+// The BN-backward reduction over a finished NT-epilogue tile (bf16 dY in Cs, rows x BN, row pitch
+// BN + 8): thread t owns 8 channels (t % (BN/8)) of every (256/(BN/8))-th row, its partial sums meet
+// in LDS behind the C tile, one sharded atomic per column and workgroup.
+template <int BM, int BN>
+__device__ void bnred_tile(const uint16_t* Cs, float* red, int M, int N, int m0, int n0, const RowMap& rm,
+                           const BnRed& br, int shard) {
+  constexpr int LDC = BN + 8, NCH = BN / 8, RSTEP = kThreads / NCH;
+  const int ch = threadIdx.x % NCH, rsub = threadIdx.x / NCH;
+  const int gcol = n0 + ch * 8;
+  float a[8], b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = b[j] = 0.f;
+  if (rsub < RSTEP && gcol < N) {
+    float p0[8], p1[8], p2[8], p3[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bnr_coef(br, gcol + j, p0[j], p1[j], p2[j], p3[j]);
+    for (int row = rsub; row < BM && m0 + row < M; row += RSTEP) {
+      float d[8], z[8];
+      bf16x8 dv, zv;
+      dv.raw = *reinterpret_cast<const uint4*>(Cs + row * LDC + ch * 8);
+      zv.raw = *reinterpret_cast<const uint4*>(br.z + rm.pixel(m0 + row) * br.ldz + gcol);
+      dv.to_float(d);
+      zv.to_float(z);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = (br.relu && fmaf(z[j], p2[j], p3[j]) <= 0.f) ? 0.f : d[j];
+        a[j] += v;
+        b[j] = fmaf(v, fmaf(z[j], p0[j], p1[j]), b[j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[j * kThreads + threadIdx.x] = a[j];
+    red[(8 + j) * kThreads + threadIdx.x] = b[j];
+  }
+  __syncthreads();
+  float* ds = br.dsum + shard_off(shard, br.sstride);
+  for (int q = threadIdx.x; q < 2 * BN; q += kThreads) {
+    const int which = q / BN, c = q - which * BN;
+    if (n0 + c >= N) continue;
+    const int cg = c / 8, j = c % 8;
+    float sum = 0.f;
+    for (int r = 0; r < RSTEP; ++r) sum += red[(which * 8 + j) * kThreads + r * NCH + cg];
+    atomicAdd(ds + which * N + n0 + c, sum);
+  }
+}
 
 // B rows [row0, row0 + ROWS) x this thread's K chunk, where the K position is the thread's A tap
 // (the A and B chunk columns of conv_nt_kernel coincide: both are threadIdx.x & 7)
@@ -224,6 +310,12 @@ __global__ __launch_bounds__(kThreads) void conv_nt_kernel(Gather g, const uint1
   nt_epilogue<BM, BN, TM, TN>(acc, smem, C, ldc, M, N, m0, n0,
                                (epi & 1) ? stats + shard_off(tm, sstride) : nullptr,
                                (epi & 2) ? stats : nullptr, (epi & 4) != 0, PH ? ph.rows : RowMap{});
+  if (ph.bnr.z != nullptr) {  // uniform: the C tile is still in LDS, the fold area lies behind it
+    constexpr int CS_ELEMS = (BM * (BN + 8) + 7) / 8 * 8;
+    static_assert(CS_ELEMS * 2 + 16 * kThreads * 4 <= 2 * (BM + BN) * BK * 2, "BN-reduce fold area fits");
+    bnred_tile<BM, BN>(smem, reinterpret_cast<float*>(smem + CS_ELEMS), M, N, m0, n0, PH ? ph.rows : RowMap{},
+                       ph.bnr, tm);
+  }
 }
 
 template <int BM, int BN, bool PH>
@@ -472,20 +564,28 @@ struct DirectCfg {
   static constexpr int PB = WPX / 16, CB = CO / 16;
   static constexpr int HCH = HH * HW * (CS / 8);  // 16-byte chunks of a halo
   static constexpr int PFN = (HCH + kThreads - 1) / kThreads;
-  static constexpr size_t kLds = static_cast<size_t>(HALO + WTS) * sizeof(uint16_t);
+  static constexpr size_t kLds = static_cast<size_t>(HALO + WTS) * sizeof(uint16_t) + CO * 4 * sizeof(float);
 };
 
 template <int CS, int CO, int TW>
 __global__ __launch_bounds__(kThreads) void conv_direct_kernel(Gather g, const uint16_t* __restrict__ B,
                                                               uint16_t* __restrict__ C, int64_t ldc,
                                                               float* __restrict__ stats, int64_t sstride,
-                                                              int tiles_x, int tiles_y, int ntiles) {
+                                                              int tiles_x, int tiles_y, int ntiles, BnRed bnr) {
   using D = DirectCfg<CS, CO, TW>;
   extern __shared__ __attribute__((aligned(16))) uint16_t dsm[];
   uint16_t* halo = dsm;
   uint16_t* wts = dsm + D::HALO;
+  // the fused BN-backward reduction (dgrad): per channel xhat = z*p0 + p1, pre-activation z*p2 + p3
+  float4* coef = reinterpret_cast<float4*>(dsm + D::HALO + D::WTS);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int kq = lane >> 4;
+  if (bnr.z != nullptr)
+    for (int c = threadIdx.x; c < CO; c += kThreads) {
+      float4 q;
+      bnr_coef(bnr, c, q.x, q.y, q.z, q.w);
+      coef[c] = q;
+    }
 
   // weight panel [CO][K] -> LDS rows of KP (once per workgroup)
   for (int v = threadIdx.x; v < CO * (D::K / 8); v += kThreads) {
@@ -596,11 +696,27 @@ __global__ __launch_bounds__(kThreads) void conv_direct_kernel(Gather g, const u
             ssum[c][r] += a[r];
             ssq[c][r] = fmaf(a[r], a[r], ssq[c][r]);
           }
+        } else if (bnr.z != nullptr) {  // dY' and dY' * xhat of the bf16 values just stored
+          const uint2 zr = *reinterpret_cast<const uint2*>(
+              bnr.z + ((static_cast<int64_t>(n) * g.OH + oy) * g.OW + ox) * bnr.ldz + c * 16 + kq * 4);
+          const float zf[4] = {__uint_as_float(zr.x << 16), __uint_as_float(zr.x & 0xffff0000u),
+                               __uint_as_float(zr.y << 16), __uint_as_float(zr.y & 0xffff0000u)};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float4 q = coef[c * 16 + kq * 4 + r];
+            const float d = (bnr.relu && fmaf(zf[r], q.z, q.w) <= 0.f) ? 0.f : bf2f(f2bf(a[r]));
+            ssum[c][r] += d;
+            ssq[c][r] = fmaf(d, fmaf(zf[r], q.x, q.y), ssq[c][r]);
+          }
         }
       }
     }
   }
-  if (stats == nullptr) return;
+  if (stats == nullptr && bnr.z == nullptr) return;
+  if (stats == nullptr) {  // BN-backward reduction: [dsum | dsumx] of this workgroup's pixels
+    stats = bnr.dsum;
+    sstride = bnr.sstride;
+  }
   float* st = stats + shard_off(blockIdx.x, sstride);
 #pragma unroll
   for (int c = 0; c < D::CB; ++c)
@@ -621,7 +737,7 @@ __global__ __launch_bounds__(kThreads) void conv_direct_kernel(Gather g, const u
 
 // The direct kernel for this shape, or -3 when it does not apply.
 int run_direct(const Gather& g, const void* B, void* C, int64_t ldc, int64_t N, int epi, float* st, int64_t sstride,
-               hipStream_t stream) {
+               hipStream_t stream, const BnRed& bnr = BnRed{}) {
   if (g.R != 3 || g.S != 3 || g.sh != 1 || g.sw != 1 || (epi & 6) || (ldc % 4) || g.halo_images <= 0 ||
       (reinterpret_cast<uintptr_t>(C) & 7) || (reinterpret_cast<uintptr_t>(B) & 15))
     return -3;
@@ -648,7 +764,7 @@ int run_direct(const Gather& g, const void* B, void* C, int64_t ldc, int64_t N, 
     const int grid = static_cast<int>(std::min<int64_t>(ntiles, static_cast<int64_t>(per_cu) * cus));
     conv_direct_kernel<CS, CO, TW><<<grid, kThreads, D::kLds, stream>>>(
         g, static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), ldc, st, sstride, tiles_x, tiles_y,
-        static_cast<int>(ntiles));
+        static_cast<int>(ntiles), bnr);
     TONY_LAUNCH_CHECK();
     return 0;
   };
@@ -663,7 +779,7 @@ int run_direct(const Gather& g, const void* B, void* C, int64_t ldc, int64_t N, 
 }
 
 int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, int flags, float* stats,
-           int64_t sstride, hipStream_t stream) {
+           int64_t sstride, hipStream_t stream, const Phase& bph = Phase{}) {
   // flags bit0: statistics accumulated into stats (the caller zeroes it, ops/arena.py);
   // bit1: stats = [scale | shift] of the folded inference BN, bit2: ReLU after it (H5)
   const int epi = flags & 7;
@@ -671,19 +787,19 @@ int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int6
   if ((epi & 3) && stats == nullptr) return -1;
   float* st = stats;
   const int v = (flags >> 8) & 0xff;
-  if (v == kHaloVariant) return run_halo(g, B, C, ldc, N, epi, st, sstride, stream);
-  if (v == kDirectVariant) return run_direct(g, B, C, ldc, N, epi, st, sstride, stream);
+  if (v == kHaloVariant) return bph.bnr.z != nullptr ? -3 : run_halo(g, B, C, ldc, N, epi, st, sstride, stream);
+  if (v == kDirectVariant) return run_direct(g, B, C, ldc, N, epi, st, sstride, stream, bph.bnr);
   if (v >= kNumNtVariants) return -1;
   if (v == 0) {
     const int64_t bn = pick_bn(N, 192);
-    return bn <= 64 ? launch_nt_bm<256>(g, B, C, ldc, M, N, st, sstride, epi, bn, stream)
-                    : launch_nt_bm<128>(g, B, C, ldc, M, N, st, sstride, epi, bn, stream);
+    return bn <= 64 ? launch_nt_bm<256>(g, B, C, ldc, M, N, st, sstride, epi, bn, stream, bph)
+                    : launch_nt_bm<128>(g, B, C, ldc, M, N, st, sstride, epi, bn, stream, bph);
   }
   const int64_t bn = pick_bn(N, kNtVariants[v].cap);
   switch (kNtVariants[v].bm) {
-    case 64: return launch_nt_bm<64>(g, B, C, ldc, M, N, st, sstride, epi, bn, stream);
-    case 128: return launch_nt_bm<128>(g, B, C, ldc, M, N, st, sstride, epi, bn, stream);
-    default: return launch_nt_bm<256>(g, B, C, ldc, M, N, st, sstride, epi, bn, stream);
+    case 64: return launch_nt_bm<64>(g, B, C, ldc, M, N, st, sstride, epi, bn, stream, bph);
+    case 128: return launch_nt_bm<128>(g, B, C, ldc, M, N, st, sstride, epi, bn, stream, bph);
+    default: return launch_nt_bm<256>(g, B, C, ldc, M, N, st, sstride, epi, bn, stream, bph);
   }
 }
 
@@ -1066,13 +1182,27 @@ TONY_API int tony_conv_fwd(const void* x, int N, int H, int W, int C, int64_t ld
 // Wt = W permuted to [C][R][S][Co].  flags bits 8..15: tile variant (run_nt).
 TONY_API int tony_conv_dgrad(const void* dy, int N, int OH, int OW, int Co, int64_t lddy, const void* wt, int C,
                              int R, int S, int ph, int pw, void* dx, int H, int W, int64_t lddx, int flags,
-                             hipStream_t stream) {
+                             BnRed* bnr, hipStream_t stream) {
   if (bad_geom(Co, lddy, dy) || (reinterpret_cast<uintptr_t>(wt) & 15) || C <= 0) return -1;
   if (OH != H + 2 * ph - R + 1 || OW != W + 2 * pw - S + 1) return -1;  // stride 1 only
   const int64_t M = static_cast<int64_t>(N) * H * W;
   if (M > 0x7fffffff || static_cast<int64_t>(N) * OH * OW > 0x7fffffff) return -1;
   Gather g{static_cast<const uint16_t*>(dy), lddy, OH, OW, Co, H, W, R, S, 1, 1, ph, pw, -1, R * S * Co, N};
-  return run_nt(g, wt, dx, lddx, M, C, flags & 0xff00, nullptr, 0, stream);
+  Phase bph{};
+  if (bnr != nullptr) {
+    bnr->done = 0;
+    if (bnr->z != nullptr) {
+      if (bnr->mean == nullptr || bnr->invstd == nullptr || bnr->dsum == nullptr || (bnr->ldz % 8) ||
+          (reinterpret_cast<uintptr_t>(bnr->z) & 15) || (C % 8))
+        return -1;
+      bph.bnr = *bnr;
+    }
+  }
+  const int rc = run_nt(g, wt, dx, lddx, M, C, flags & 0xff00, nullptr, 0, stream, bph);
+  if (rc == -3 && bph.bnr.z != nullptr)  // the chosen variant has no fused reduction: plain dgrad
+    return run_nt(g, wt, dx, lddx, M, C, flags & 0xff00, nullptr, 0, stream);
+  if (rc == 0 && bph.bnr.z != nullptr) bnr->done = 1;
+  return rc;
 }
 
 // dX[N*H*W, C] (row stride lddx) of a STRIDED conv (stride sh x sw, padding ph, pw): one MFMA
@@ -1082,10 +1212,20 @@ TONY_API int tony_conv_dgrad(const void* dy, int N, int OH, int OW, int Co, int6
 // tile variant (run_nt_phase).
 TONY_API int tony_conv_dgrad_strided(const void* dy, int N, int OH, int OW, int Co, int64_t lddy, const void* wt,
                                      int C, int R, int S, int sh, int sw, int ph, int pw, void* dx, int H, int W,
-                                     int64_t lddx, int flags, hipStream_t stream) {
+                                     int64_t lddx, int flags, BnRed* bnr, hipStream_t stream) {
   if (bad_geom(Co, lddy, dy) || (reinterpret_cast<uintptr_t>(wt) & 15) || C <= 0 || C % 8 || (lddx % 8) ||
       (reinterpret_cast<uintptr_t>(dx) & 15))
     return -1;
+  BnRed br{};
+  if (bnr != nullptr) {
+    bnr->done = 0;
+    if (bnr->z != nullptr) {
+      if (bnr->mean == nullptr || bnr->invstd == nullptr || bnr->dsum == nullptr || (bnr->ldz % 8) ||
+          (reinterpret_cast<uintptr_t>(bnr->z) & 15))
+        return -1;
+      br = *bnr;  // every residue class adds its pixels' sums
+    }
+  }
   if (sh < 1 || sw < 1 || sh > 4 || sw > 4 || ph < 0 || pw < 0 || ph >= R || pw >= S) return -1;
   if (OH != (H + 2 * ph - R) / sh + 1 || OW != (W + 2 * pw - S) / sw + 1 || OH <= 0 || OW <= 0) return -1;
   if (static_cast<int64_t>(N) * H * W > 0x7fffffff || static_cast<int64_t>(N) * OH * OW > 0x7fffffff) return -1;
@@ -1110,10 +1250,12 @@ TONY_API int tony_conv_dgrad_strided(const void* dy, int N, int OH, int OW, int 
       phz.rows.sx = sw;
       phz.rows.y0 = py;
       phz.rows.x0 = px;
+      phz.bnr = br;
       const int rc = run_nt_phase(g, wt, dx, lddx, M, C, v, phz, stream);
       if (rc != 0) return rc;
     }
   }
+  if (br.z != nullptr) bnr->done = 1;
   return 0;
 }
 

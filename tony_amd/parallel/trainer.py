@@ -10,6 +10,7 @@ replay always uses the current learning rate.
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Callable
 
@@ -19,6 +20,10 @@ from ..ops import streams, wt_cache
 from ..ops.arena import for_device
 from ..utils.tracing import heartbeat, trace_range
 from .ps import ParameterServer
+
+# Opt-in: measured slower on MI355X (bench 16.9 vs 15.7 ms/step; the compute queue's gaps grew from
+# 3.3 to 5.9 ms under rocprofv3), so the step stays on the caller's stream by default.
+PRIO_STREAM = os.environ.get("TONY_PRIO_STREAM", "0") == "1"
 
 
 class Trainer:
@@ -47,6 +52,7 @@ class Trainer:
         self.static_y = None
         self.static_loss = None
         self._eager_steps = 0
+        self._prio = None
         dev = ps.flat.device
         # one zero-fill per step for every fused kernel's fp32 accumulators (ops/arena.py)
         self.arena = for_device(dev) if dev.type == "cuda" else None
@@ -121,10 +127,35 @@ class Trainer:
         heartbeat()
         return loss.detach()
 
+    def _compute_stream(self):
+        """The high-priority stream the step's critical chain runs on (None: the caller's stream).
+
+        The weight gradients and the bucketed communication run on their own default-priority
+        streams.  At equal priority the command processor hands freed CUs to whichever queue
+        dispatched first, so a wide split-K wgrad grid issued just before a data-gradient kernel
+        (the side stream forks at every layer) occupies the CUs that dgrad -- the critical path --
+        waits for (rocprofv3: 50-100 us gaps on the compute queue after each BN backward).  With the
+        compute queue at the higher priority, the side stream's workgroups only fill what it leaves
+        idle.  Opt-in (``TONY_PRIO_STREAM=1``): it measured slower (see PRIO_STREAM)."""
+        if not PRIO_STREAM or self.ps.flat.device.type != "cuda":
+            return None
+        if self._prio is None:
+            lo, hi = torch.cuda.Stream.priority_range()  # (lowest, highest): e.g. (0, -1)
+            self._prio = torch.cuda.Stream(device=self.ps.flat.device, priority=hi) if hi != lo else False
+        return self._prio or None
+
     def step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         wt_cache.activate(self.wt)
         try:
-            return self._step(x, y)
+            s = self._compute_stream()
+            if s is None:
+                return self._step(x, y)
+            cur = torch.cuda.current_stream(s.device)
+            s.wait_stream(cur)  # inputs written on the caller's stream
+            with torch.cuda.stream(s):
+                loss = self._step(x, y)
+            cur.wait_stream(s)  # the caller may read the loss / parameters on its stream
+            return loss
         finally:
             wt_cache.activate(None)
 

@@ -52,6 +52,15 @@ def per_queue(rows, ngaps):
         span = iv[-1][1] - iv[0][0]
         print(f"    {key} {q}: {len(iv)} kernels, busy {busy / 1e6:.2f} ms over {span / 1e6:.2f} ms"
               + ("  <- busiest" if q == main_q else ""))
+    for q, ivs in qs.items():
+        by = {}
+        for s_, e_, name in ivs:
+            k = name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:70]
+            t, c = by.get(k, (0, 0))
+            by[k] = (t + e_ - s_, c + 1)
+        print(f"    top kernels of {key} {q}:")
+        for k, (t, c) in sorted(by.items(), key=lambda kv: -kv[1][0])[:14]:
+            print(f"      {t / 1e3:8.1f} us {c:4d}x  {k}")
     iv = sorted(qs[main_q])
     gaps = sorted(((b[0] - a[1], a[2][:60], b[2][:60]) for a, b in zip(iv, iv[1:])), reverse=True)
     tot = sum(g for g, _, _ in gaps if g > 0)
