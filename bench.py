@@ -67,7 +67,8 @@ def parse():
     ap.add_argument("--no-wgrad-stream", action="store_true",
                     help="serial backward (no weight gradients on a second stream)")
     ap.add_argument("--no-branch-streams", action="store_true",
-                    help="Inception branches on one stream (branch streams are opt-in: TONY_BRANCH_STREAMS=1)")
+                    help="Inception branches on one stream (branch streams are on by default; TONY_BRANCH_STREAMS=0 "
+                         "also turns them off)")
     ap.add_argument("--tune-cache", default=None,
                     help="JSON of kernel-choice decisions: loaded when it exists (no autotuning for those "
                          "shapes), written after setup otherwise (reproducible profiles, faster startup)")

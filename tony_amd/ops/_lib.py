@@ -73,20 +73,20 @@ _SIGNATURES = {
     "tony_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64,
                        c_int, c_void_p, c_int64, c_void_p],
     "tony_gemm_tn_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64,
-                          c_void_p, c_int64, c_int_p, c_int, c_void_p, c_void_p, c_int, c_void_p],
+                          c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p],
     "tony_splitk_reduce": [c_void_p, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_void_p],
     "tony_conv_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int,
                       c_int, c_int, c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_int64, c_void_p],
     "tony_stem_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                       c_int, c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_int64, c_int, c_void_p],
     "tony_stem_wgrad": [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                        c_int, c_int, c_int, c_int, c_void_p, c_int64, c_int_p, c_int, c_void_p],
+                        c_int, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_int, c_void_p],
     "tony_conv_dgrad": [c_void_p, c_int, c_int, c_int, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int,
                         c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_void_p],
     "tony_conv_dgrad_strided": [c_void_p, c_int, c_int, c_int, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_int,
                                 c_int, c_int, c_int, c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_void_p],
     "tony_conv_wgrad": [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int, c_int, c_int, c_int,
-                        c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_int_p, c_int, c_void_p,
+                        c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_void_p,
                         c_void_p, c_int, c_void_p],
     "tony_avgpool3_s1p1": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
     "tony_maxpool_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
@@ -135,6 +135,17 @@ class _SignedLib:
             fn.argtypes = argtypes
             fn.restype = c_int
             setattr(self, name, fn)
+        # the generated METH_FASTCALL wrappers (ops/fastcall.py) replace the ctypes calls where built
+        self.fastcall = 0
+        if os.environ.get("TONY_FASTCALL", "1") != "0":
+            try:
+                from . import _tony_fastcall, fastcall
+            except ImportError:
+                _tony_fastcall = None
+            if _tony_fastcall is not None:
+                for name, w in fastcall.bind_all(_tony_fastcall, h, _SIGNATURES).items():
+                    setattr(self, name, w)
+                    self.fastcall += 1
 
     def __getattr__(self, name):
         raise KernelError(f"{name}: not exported by {SO_PATH} or missing from _lib._SIGNATURES")

@@ -8,6 +8,8 @@ Two shared objects are produced next to their Python loaders:
   ``libamdhip64.so`` without a SONAME; linking to ``/opt/rocm``'s
   ``libamdhip64.so.7`` would put a second HIP runtime in the process and stream
   handles would not be shared).
+* ``tony_amd/ops/_tony_fastcall*.so`` -- generated CPython METH_FASTCALL wrappers of the kernel
+  entry points (ops/fastcall.py), ~20x cheaper per launch than ctypes.
 * ``tony_amd/native/_tony_native.so`` -- host-only C++ runtime pieces (process
   launcher / gang spawner, port reservation, amd-smi GPU inventory + metrics).
 
@@ -104,6 +106,27 @@ def build_kernels(verbose: bool = False, force: bool = False) -> str:
     return KERNELS_SO
 
 
+def build_fastcall(verbose: bool = False, force: bool = False) -> str:
+    """Generate (ops/fastcall.py) and compile the CPython fast-call wrappers of the kernel entry points."""
+    import sysconfig
+
+    from . import fastcall
+    from ._lib import _SIGNATURES
+
+    out = os.path.join(HERE, "_tony_fastcall" + sysconfig.get_config_var("EXT_SUFFIX"))
+    src = os.path.join(BUILD_DIR, "_tony_fastcall.c")
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    code = fastcall.generate(_SIGNATURES)
+    old = open(src).read() if os.path.exists(src) else None
+    if old != code:
+        with open(src, "w") as fh:
+            fh.write(code)
+    if force or old != code or _newer(out, [src]):
+        cmd = ["gcc", "-O2", "-fPIC", "-shared", "-Wall", f"-I{sysconfig.get_paths()['include']}", src, "-o", out]
+        _run(cmd, verbose)
+    return out
+
+
 def build_native(verbose: bool = False, force: bool = False) -> str:
     ndir = os.path.join(PKG, "native")
     srcs = sorted(glob.glob(os.path.join(ndir, "*.cpp")))
@@ -125,7 +148,9 @@ def build_native(verbose: bool = False, force: bool = False) -> str:
 
 
 def build_all(verbose: bool = False, force: bool = False):
-    return build_kernels(verbose, force), build_native(verbose, force)
+    kernels = build_kernels(verbose, force)
+    build_fastcall(verbose, force)
+    return kernels, build_native(verbose, force)
 
 
 if __name__ == "__main__":

@@ -162,7 +162,7 @@ def stem_wgrad(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride=1, paddin
     splits = ctypes.c_int(0)
     st = _lib.stream_ptr(dev)
     rc = L.tony_stem_wgrad(dy.data_ptr(), lddy, x.data_ptr(), n, h, w, c, co, r, s, sh, sw, ph, pw, dy.shape[2],
-                           dy.shape[3], slab.data_ptr(), slab.numel(), ctypes.byref(splits), cus, st)
+                           dy.shape[3], slab.data_ptr(), slab.numel(), ctypes.addressof(splits), cus, st)
     _lib.check(rc, "tony_stem_wgrad")
     out = dst if dst is not None else torch.empty(nel, dtype=torch.float32, device=dev)
     rc = L.tony_splitk_reduce(slab.data_ptr(), splits.value, nel, out.data_ptr(), int(out.dtype == _BF16),
@@ -198,7 +198,7 @@ def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, paddin
     if (sh, sw) == (1, 1):
         def launch(vf, br=None):
             return L.tony_conv_dgrad(dy.data_ptr(), n, dy.shape[2], dy.shape[3], co, lddy, wt.data_ptr(), c, r, s, ph,
-                                     pw, dx.data_ptr(), h, w, c, vf, None if br is None else ctypes.byref(br), st)
+                                     pw, dx.data_ptr(), h, w, c, vf, None if br is None else ctypes.addressof(br), st)
         name = "tony_conv_dgrad"
     else:
         def launch(vf, br=None):
@@ -206,7 +206,7 @@ def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, paddin
                 return -3
             return L.tony_conv_dgrad_strided(dy.data_ptr(), n, dy.shape[2], dy.shape[3], co, lddy, wt.data_ptr(), c,
                                              r, s, sh, sw, ph, pw, dx.data_ptr(), h, w, c, vf,
-                                             None if br is None else ctypes.byref(br), st)
+                                             None if br is None else ctypes.addressof(br), st)
         name = "tony_conv_dgrad_strided"
 
     # variants are timed without the fused reduction (it must run exactly once)

@@ -84,10 +84,10 @@ def splitk_combine(launch, n: int, ntiles: int, device, dst: torch.Tensor | None
     flags = int(out.dtype == torch.bfloat16) | (2 if dst is not None else 0)
     if SPLITK_FOLD:
         counters = zeros_f32(ntiles, device)  # zero bits = zero uint32 arrival counters
-        _lib.check(launch(slab.data_ptr(), slab.numel(), ctypes.byref(splits), counters.data_ptr(), out.data_ptr(),
+        _lib.check(launch(slab.data_ptr(), slab.numel(), ctypes.addressof(splits), counters.data_ptr(), out.data_ptr(),
                           flags), "split-K wgrad (fold)")
         return None if dst is not None else out
-    _lib.check(launch(slab.data_ptr(), slab.numel(), ctypes.byref(splits), 0, 0, 0), "split-K wgrad")
+    _lib.check(launch(slab.data_ptr(), slab.numel(), ctypes.addressof(splits), 0, 0, 0), "split-K wgrad")
     rc = _lib.lib().tony_splitk_reduce(slab.data_ptr(), splits.value, n, out.data_ptr(), int(out.dtype == torch.bfloat16),
                                        int(dst is not None), cus, _lib.stream_ptr(device))
     _lib.check(rc, "tony_splitk_reduce")

@@ -55,7 +55,10 @@ def _side(device: torch.device) -> torch.cuda.Stream:
 # independent conv chains of an Inception block execute concurrently; autograd then replays each
 # branch's backward on the stream its forward ran on.  Tensors that cross streams are kept
 # referenced until ``end()`` (``keep``), which joins every stream used into the current one.
-BRANCHES_ENABLED = os.environ.get("TONY_BRANCH_STREAMS", "0") == "1"  # measured: no gain (GPU already full), +1.5 ms host
+# On by default since round 2: with the faster kernels the Inception step is no longer host-bound, and
+# branch streams measured 15.05 vs 15.66 ms/step (alternating A/B on MI355X,
+# profiles/r2s3_branch_streams_ab.log).  TONY_BRANCH_STREAMS=0 runs every branch on one stream.
+BRANCHES_ENABLED = os.environ.get("TONY_BRANCH_STREAMS", "1") != "0"
 _branch_pool: Dict[int, List[torch.cuda.Stream]] = {}
 _branches_on = [False]
 _used: Dict[int, torch.cuda.Stream] = {}

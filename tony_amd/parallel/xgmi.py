@@ -98,7 +98,7 @@ class XgmiComm:
                                     int(inp.dtype == torch.bfloat16), root, float(scale),
                                     self.epoch & 0xFFFFFFFF, self.grid(nbytes), stream)
         _lib.check(rc, "tony_xgmi_collective")
-        _lib.check(L.tony_xgmi_error_async(ctypes.c_void_p(self.window), self._err_host.data_ptr(), stream),
+        _lib.check(L.tony_xgmi_error_async(self.window, self._err_host.data_ptr(), stream),
                    "tony_xgmi_error_async")
 
     @staticmethod
@@ -204,7 +204,7 @@ class XgmiComm:
         dist.barrier(group=self.group)  # no peer may still be reading this rank's window
         L = _lib.lib()
         for p in self.peers:
-            L.tony_xgmi_close(ctypes.c_void_p(p))
-        L.tony_xgmi_free(ctypes.c_void_p(self.window))
+            L.tony_xgmi_close(p)
+        L.tony_xgmi_free(self.window)
         self.window = None
         self.peers = []
