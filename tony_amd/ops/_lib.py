@@ -46,6 +46,17 @@ _SIGNATURES = {
     "tony_bn_apply": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p,
                       c_void_p, c_int, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
                       c_void_p],
+    "tony_bn_apply_segs": [c_void_p, c_int64, c_int, c_int64, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                           c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int64,
+                           c_void_p, c_void_p, c_int, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                           c_float, c_void_p],
+    "tony_bn_bwd_reduce_segs": [c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int, c_void_p, c_void_p,
+                                c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p],
+    "tony_bn_bwd_apply_segs": [c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                               c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p, c_int64, c_int64, c_int,
+                               c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int64,
+                               c_void_p, c_void_p, c_int, c_void_p],
     "tony_bn_relu_maxpool": [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_float,
                              c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_int64, c_void_p, c_int,
                              c_int, c_int, c_int, c_int, c_int, c_void_p],

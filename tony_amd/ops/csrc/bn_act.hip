@@ -37,6 +37,25 @@ struct RowMap {
   }
 };
 
+// Column segments of a multi-output BN pass -- the 1x1 splits of a fused Inception head (ops/fused.py):
+// columns [end[s-1], end[s]) of the [M, C] tensor live in tensor p[s] (its column 0) with row stride
+// ld[s], so ONE launch normalises (or back-propagates) every split.  n == 0: the plain pointer.
+struct Segs {
+  int n = 0;
+  int end[4] = {0, 0, 0, 0};
+  uint16_t* p[4] = {nullptr, nullptr, nullptr, nullptr};
+  int64_t ld[4] = {0, 0, 0, 0};
+  __device__ __forceinline__ void resolve(int col, uint16_t*& base, int64_t& ld_out) const {
+    int s = 0, start = 0;
+    while (s + 1 < n && col >= end[s]) {
+      start = end[s];
+      ++s;
+    }
+    base = p[s] + (col - start);
+    ld_out = ld[s];
+  }
+};
+
 __device__ __forceinline__ float load_param(const void* p, int idx, int is_bf16, float dflt) {
   if (p == nullptr) return dflt;
   return is_bf16 ? bf2f(static_cast<const uint16_t*>(p)[idx]) : static_cast<const float*>(p)[idx];
@@ -130,7 +149,7 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
     uint16_t* __restrict__ y, int64_t ldy, const float* __restrict__ sum, const float* __restrict__ sumsq,
     int64_t sstride, const void* gamma, const void* beta, int param_bf16, float eps, int relu, int mode,
     float* __restrict__ save_mean, float* __restrict__ save_invstd,
-    float* __restrict__ running_mean, float* __restrict__ running_var, float momentum) {
+    float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, Segs segs) {
   __shared__ float scale[kMaxC];
   __shared__ float shift[kMaxC];
   const float inv_m = 1.f / static_cast<float>(M);
@@ -171,6 +190,9 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
   const int64_t r1 = min(M, r0 + rows_per_block);
   const int64_t step = rm.RPI;
   int64_t r = r0 + rm.rsub;
+  uint16_t* yb = y + rm.cg * 8;
+  int64_t ldyt = ldy;
+  if (segs.n > 0) segs.resolve(rm.cg * 8, yb, ldyt);
   auto body = [&](const bf16x8& v, const bf16x8& rv, int64_t row) {
     float f[8], q[8];
     v.to_float(f);
@@ -181,7 +203,7 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
       if (RES) t += q[j];
       f[j] = relu ? fmaxf(t, 0.f) : t;
     }
-    store8(y + row * ldy + rm.cg * 8, bf16x8::from_float(f));
+    store8(yb + row * ldyt, bf16x8::from_float(f));
   };
   bf16x8 none{};
   for (; r + 3 * step < r1; r += 4 * step) {
@@ -209,7 +231,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     const uint16_t* __restrict__ ym, int64_t ldym,
     int64_t M, int C, int64_t rows_per_block, const float* __restrict__ mean,
     const float* __restrict__ invstd, const void* gamma, const void* beta, int param_bf16,
-    int relu, float* __restrict__ dsum, float* __restrict__ dsumx, int64_t sstride) {
+    int relu, float* __restrict__ dsum, float* __restrict__ dsumx, int64_t sstride, Segs segs) {
   __shared__ float red[kMaxC * 4];  // coefficient table [4][C] first, then the block reduction
   for (int c = threadIdx.x; c < C; c += kThreads) {
     const float mu = mean[c], is = invstd[c];
@@ -256,21 +278,27 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
       }
     };
     bf16x8 none{};
+    const uint16_t* db = dy + rm.cg * 8;
+    int64_t lddt = lddy;
+    if (segs.n > 0) {
+      uint16_t* b;
+      segs.resolve(rm.cg * 8, b, lddt);
+      db = b;
+    }
     int64_t r = r0 + rm.rsub;
     for (; r + 3 * step < r1; r += 4 * step) {
       bf16x8 xv[4], gv[4], yv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         xv[u] = load8(x + (r + u * step) * ldx + rm.cg * 8);
-        gv[u] = load8(dy + (r + u * step) * lddy + rm.cg * 8);
+        gv[u] = load8(db + (r + u * step) * lddt);
         if (YMASK) yv[u] = load8(ym + (r + u * step) * ldym + rm.cg * 8);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) body(xv[u], gv[u], YMASK ? yv[u] : none);
     }
     for (; r < r1; r += step)
-      body(load8(x + r * ldx + rm.cg * 8), load8(dy + r * lddy + rm.cg * 8),
-           YMASK ? load8(ym + r * ldym + rm.cg * 8) : none);
+      body(load8(x + r * ldx + rm.cg * 8), load8(db + r * lddt), YMASK ? load8(ym + r * ldym + rm.cg * 8) : none);
   }
   const int64_t so = shard_off(blockIdx.x, sstride);
   block_reduce_add(red, rm, C, a, b, dsum + so, dsumx + so);
@@ -286,7 +314,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     uint16_t* __restrict__ dx, int64_t lddx, int64_t M, int C, int64_t rows_per_block,
     const float* __restrict__ mean, const float* __restrict__ invstd, const void* gamma,
     const void* beta, int param_bf16, int relu, const float* __restrict__ dsum,
-    const float* __restrict__ dsumx, int64_t sstride, void* dgamma, void* dbeta, int accumulate) {
+    const float* __restrict__ dsumx, int64_t sstride, void* dgamma, void* dbeta, int accumulate, Segs segs) {
   __shared__ float tab[5][kMaxC];
   const float inv_m = 1.f / static_cast<float>(M);
   for (int c = threadIdx.x; c < C; c += kThreads) {
@@ -341,21 +369,27 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     if (YMASK && dres != nullptr) store8(dres + row * lddr + rm.cg * 8, bf16x8::from_float(gf));
   };
   bf16x8 none{};
+  const uint16_t* db = dy + rm.cg * 8;
+  int64_t lddt = lddy;
+  if (segs.n > 0) {
+    uint16_t* b;
+    segs.resolve(rm.cg * 8, b, lddt);
+    db = b;
+  }
   int64_t r = r0 + rm.rsub;
   for (; r + 3 * step < r1; r += 4 * step) {
     bf16x8 xv[4], gv[4], yv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       xv[u] = load8(x + (r + u * step) * ldx + rm.cg * 8);
-      gv[u] = load8(dy + (r + u * step) * lddy + rm.cg * 8);
+      gv[u] = load8(db + (r + u * step) * lddt);
       if (YMASK) yv[u] = load8(ym + (r + u * step) * ldym + rm.cg * 8);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) body(xv[u], gv[u], YMASK ? yv[u] : none, r + u * step);
   }
   for (; r < r1; r += step)
-    body(load8(x + r * ldx + rm.cg * 8), load8(dy + r * lddy + rm.cg * 8),
-         YMASK ? load8(ym + r * ldym + rm.cg * 8) : none, r);
+    body(load8(x + r * ldx + rm.cg * 8), load8(db + r * lddt), YMASK ? load8(ym + r * ldym + rm.cg * 8) : none, r);
 }
 
 // ---- one-launch BN(+ReLU) backward: reduce -> grid barrier -> apply ------------------------------
@@ -639,7 +673,7 @@ TONY_API int tony_bn_apply(const void* x, int64_t M, int C, int64_t ldx, void* y
   plan_rows(M, C, 4, 8192, &rpb, &grid);
   bn_fwd_apply_kernel<false><<<grid, kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), M, C, ldx, rpb, nullptr, 0, static_cast<uint16_t*>(y), ldy, sum, sumsq,
-      sstride, gamma, beta, param_bf16, eps, relu, mode, save_mean, save_invstd, running_mean, running_var, momentum);
+      sstride, gamma, beta, param_bf16, eps, relu, mode, save_mean, save_invstd, running_mean, running_var, momentum, Segs{});
   TONY_LAUNCH_CHECK();
   return 0;
 }
@@ -657,7 +691,7 @@ TONY_API int tony_bn_apply_res(const void* x, int64_t M, int C, int64_t ldx, con
   bn_fwd_apply_kernel<true><<<grid, kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), M, C, ldx, rpb, static_cast<const uint16_t*>(res), ldr,
       static_cast<uint16_t*>(y), ldy, sum, sumsq, sstride, gamma, beta, param_bf16, eps, relu, mode, save_mean,
-      save_invstd, running_mean, running_var, momentum);
+      save_invstd, running_mean, running_var, momentum, Segs{});
   TONY_LAUNCH_CHECK();
   return 0;
 }
@@ -672,7 +706,7 @@ TONY_API int tony_bn_bwd_reduce(const void* x, int64_t ldx, const void* dy, int6
   plan_rows(M, C, 8, 512, &rpb, &grid, true);  // few WGs: C atomics per WG contend per channel
   bn_bwd_reduce_kernel<false><<<grid, kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, nullptr, 0, M, C, rpb, mean,
-      invstd, gamma, beta, param_bf16, relu, dsum, dsumx, sstride);
+      invstd, gamma, beta, param_bf16, relu, dsum, dsumx, sstride, Segs{});
   TONY_LAUNCH_CHECK();
   return 0;
 }
@@ -688,7 +722,91 @@ TONY_API int tony_bn_bwd_apply(const void* x, int64_t ldx, const void* dy, int64
   bn_bwd_apply_kernel<false><<<grid, kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, nullptr, 0, nullptr, 0,
       static_cast<uint16_t*>(dx), lddx, M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsum, dsumx, sstride,
-      dgamma, dbeta, accumulate);
+      dgamma, dbeta, accumulate, Segs{});
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---- multi-output forms: the splits of a fused Inception head (ops/fused.py) in ONE launch ------
+// Segment s covers columns [e[s-1], e[s]) of the [M, C] BN tensor x (C = e[n-1]); its output (apply)
+// / input gradient (backward) lives at p[s] with row stride l[s].  n = 1..4, every e[s] % 8 == 0,
+// every p[s] 16-byte aligned and every l[s] % 8 == 0.
+namespace {
+bool make_segs(Segs& sg, int C, int n, int e0, int e1, int e2, int e3, void* p0, void* p1, void* p2, void* p3,
+               int64_t l0, int64_t l1, int64_t l2, int64_t l3) {
+  if (n < 1 || n > 4) return false;
+  const int e[4] = {e0, e1, e2, e3};
+  void* p[4] = {p0, p1, p2, p3};
+  const int64_t l[4] = {l0, l1, l2, l3};
+  int prev = 0;
+  sg.n = n;
+  for (int s = 0; s < n; ++s) {
+    if (e[s] <= prev || (e[s] % 8) || p[s] == nullptr || (reinterpret_cast<uintptr_t>(p[s]) & 15) || (l[s] % 8) ||
+        l[s] < e[s] - prev)
+      return false;
+    sg.end[s] = e[s];
+    sg.p[s] = static_cast<uint16_t*>(p[s]);
+    sg.ld[s] = l[s];
+    prev = e[s];
+  }
+  return prev == C;
+}
+}  // namespace
+
+TONY_API int tony_bn_apply_segs(const void* x, int64_t M, int C, int64_t ldx, int n, int e0, int e1, int e2, int e3,
+                                void* p0, void* p1, void* p2, void* p3, int64_t l0, int64_t l1, int64_t l2, int64_t l3,
+                                const float* sum, const float* sumsq, int64_t sstride, const void* gamma,
+                                const void* beta, int param_bf16, float eps, int relu, int mode, float* save_mean,
+                                float* save_invstd, float* running_mean, float* running_var, float momentum,
+                                hipStream_t stream) {
+  Segs sg;
+  if (bad_c(C) || (ldx % 8) || sstride < 0 || !make_segs(sg, C, n, e0, e1, e2, e3, p0, p1, p2, p3, l0, l1, l2, l3))
+    return -1;
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 4, 8192, &rpb, &grid);
+  bn_fwd_apply_kernel<false><<<grid, kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), M, C, ldx, rpb, nullptr, 0, sg.p[0], sg.ld[0], sum, sumsq, sstride, gamma, beta,
+      param_bf16, eps, relu, mode, save_mean, save_invstd, running_mean, running_var, momentum, sg);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+TONY_API int tony_bn_bwd_reduce_segs(const void* x, int64_t ldx, int n, int e0, int e1, int e2, int e3, void* p0,
+                                     void* p1, void* p2, void* p3, int64_t l0, int64_t l1, int64_t l2, int64_t l3,
+                                     int64_t M, int C, const float* mean, const float* invstd, const void* gamma,
+                                     const void* beta, int param_bf16, int relu, float* dsum, float* dsumx,
+                                     int64_t sstride, hipStream_t stream) {
+  Segs sg;
+  if (bad_c(C) || (ldx % 8) || sstride < 0 || !make_segs(sg, C, n, e0, e1, e2, e3, p0, p1, p2, p3, l0, l1, l2, l3))
+    return -1;
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 8, 512, &rpb, &grid, true);
+  bn_bwd_reduce_kernel<false><<<grid, kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), ldx, sg.p[0], sg.ld[0], nullptr, 0, M, C, rpb, mean, invstd, gamma, beta,
+      param_bf16, relu, dsum, dsumx, sstride, sg);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+TONY_API int tony_bn_bwd_apply_segs(const void* x, int64_t ldx, int n, int e0, int e1, int e2, int e3, void* p0,
+                                    void* p1, void* p2, void* p3, int64_t l0, int64_t l1, int64_t l2, int64_t l3,
+                                    void* dx, int64_t lddx, int64_t M, int C, const float* mean, const float* invstd,
+                                    const void* gamma, const void* beta, int param_bf16, int relu, const float* dsum,
+                                    const float* dsumx, int64_t sstride, void* dgamma, void* dbeta, int accumulate,
+                                    hipStream_t stream) {
+  Segs sg;
+  if (bad_c(C) || (ldx % 8) || (lddx % 8) || sstride < 0 ||
+      !make_segs(sg, C, n, e0, e1, e2, e3, p0, p1, p2, p3, l0, l1, l2, l3))
+    return -1;
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 4, 8192, &rpb, &grid);
+  bn_bwd_apply_kernel<false><<<grid, kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(x), ldx, sg.p[0], sg.ld[0], nullptr, 0, nullptr, 0, static_cast<uint16_t*>(dx),
+      lddx, M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsum, dsumx, sstride, dgamma, dbeta, accumulate,
+      sg);
   TONY_LAUNCH_CHECK();
   return 0;
 }
@@ -758,13 +876,13 @@ TONY_API int tony_bn_bwd_res(const void* x, int64_t ldx, const void* dy, int64_t
   plan_rows(M, C, 8, 512, &rpb, &grid);
   bn_bwd_reduce_kernel<true><<<grid, kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, static_cast<const uint16_t*>(y),
-      ldy, M, C, rpb, mean, invstd, gamma, beta, param_bf16, 1, dsums_ws, dsums_ws + C, ss);
+      ldy, M, C, rpb, mean, invstd, gamma, beta, param_bf16, 1, dsums_ws, dsums_ws + C, ss, Segs{});
   TONY_LAUNCH_CHECK();
   plan_rows(M, C, 4, 8192, &rpb, &grid);
   bn_bwd_apply_kernel<true><<<grid, kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, static_cast<const uint16_t*>(y),
       ldy, static_cast<uint16_t*>(dres), lddr, static_cast<uint16_t*>(dx), lddx, M, C, rpb, mean, invstd, gamma, beta,
-      param_bf16, 1, dsums_ws, dsums_ws + C, ss, dgamma, dbeta, accumulate);
+      param_bf16, 1, dsums_ws, dsums_ws + C, ss, dgamma, dbeta, accumulate, Segs{});
   TONY_LAUNCH_CHECK();
   return 0;
 }

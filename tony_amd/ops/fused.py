@@ -27,6 +27,7 @@ A single-split head is simply conv1x1 + BN + ReLU with epilogue statistics.
 """
 from __future__ import annotations
 
+import os
 from typing import Sequence
 
 import torch
@@ -46,6 +47,26 @@ def _cl_empty(n, c, h, w, device, dtype=_BF16):
 
 def _off(t: torch.Tensor, elems: int) -> int:
     return t.data_ptr() + elems * t.element_size()
+
+
+# TONY_BN_SEGS=0: one BN apply / reduce / apply launch per head split instead of one per head
+SEGS = os.environ.get("TONY_BN_SEGS", "1") != "0"
+
+
+def _seg_ends(splits):
+    """Cumulative column ends of up to 4 splits, padded to 4 values (the C ABI's fixed arity)."""
+    ends, e = [], 0
+    for c in splits:
+        e += c
+        ends.append(e)
+    return ends + [0] * (4 - len(ends))
+
+
+def _seg_args(tensors):
+    """(4 data pointers, 4 row strides) of up to 4 per-split row tensors, zero-padded."""
+    ptr = [t.data_ptr() for t in tensors] + [0] * (4 - len(tensors))
+    ld = [_rows_view(t)[2] for t in tensors] + [0] * (4 - len(tensors))
+    return ptr, ld
 
 
 class _HeadFn(torch.autograd.Function):
@@ -79,20 +100,31 @@ class _HeadFn(torch.autograd.Function):
             invstd = torch.rsqrt(running_var.float() + eps)
         mode = 0 if training else 1
         outs = []
-        c0 = 0
         slots = slots or ()
         for k, ci in enumerate(splits):
             # a final branch output goes straight into the block's concat buffer (ops/concat.py)
             y = concat.take(slots[k] if k < len(slots) else None, n, ci, h, w, x)
             if y is None:
                 y = _cl_empty(n, ci, h, w, dev)
-            ldy = _rows_view(y)[2]
-            rc = L.tony_bn_apply(_off(Z, c0), M, ci, ctot, y.data_ptr(), ldy, _off(stats, c0), _off(stats, ctot + c0),
-                                 ss, _off(gamma, c0), _off(beta, c0), pb, float(eps), 1, mode,
-                                 _off(mean, c0) if training else 0, _off(invstd, c0) if training else 0,
-                                 _off(running_mean, c0), _off(running_var, c0), float(momentum), stream)
-            _lib.check(rc, "tony_bn_apply")
             outs.append(y)
+        # every split normalised by ONE launch (csrc/bn_act.hip segment table), else one per split
+        csum = sum(splits)
+        rc = -1
+        if SEGS and 1 <= len(splits) <= 4:
+            ptr, ld = _seg_args(outs)
+            ends = _seg_ends(splits)
+            rc = L.tony_bn_apply_segs(Z.data_ptr(), M, csum, ctot, len(splits), *ends, *ptr, *ld, stats.data_ptr(),
+                                      _off(stats, ctot), ss, gamma.data_ptr(), beta.data_ptr(), pb, float(eps), 1,
+                                      mode, mean.data_ptr() if training else 0, invstd.data_ptr() if training else 0,
+                                      _lib.ptr(running_mean), _lib.ptr(running_var), float(momentum), stream)
+        c0 = 0
+        for y, ci in zip(outs, splits):
+            if rc != 0:
+                rc2 = L.tony_bn_apply(_off(Z, c0), M, ci, ctot, y.data_ptr(), _rows_view(y)[2], _off(stats, c0),
+                                      _off(stats, ctot + c0), ss, _off(gamma, c0), _off(beta, c0), pb, float(eps), 1,
+                                      mode, _off(mean, c0) if training else 0, _off(invstd, c0) if training else 0,
+                                      _off(running_mean, c0), _off(running_var, c0), float(momentum), stream)
+                _lib.check(rc2, "tony_bn_apply")
             c0 += ci
         P = None
         if npool:
@@ -143,19 +175,37 @@ class _HeadFn(torch.autograd.Function):
         acc = int(inplace)
         dgamma = gg if inplace else torch.empty_like(gamma)
         dbeta = gb if inplace else torch.empty_like(beta)
+        dys = [_as_rows(dy)[0] for dy in douts[:len(ctx.splits)]]
+        rc = -1
+        if SEGS and 1 <= len(ctx.splits) <= 4:  # every split's reduce / apply in ONE launch each
+            ptr, ld = _seg_args(dys)
+            ends = _seg_ends(ctx.splits)
+            csum = sum(ctx.splits)
+            rc = L.tony_bn_bwd_reduce_segs(Z.data_ptr(), ctot, len(ctx.splits), *ends, *ptr, *ld, M, csum,
+                                           mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), pb,
+                                           1, dsum.data_ptr(), _off(dsum, ctot), ss, stream)
+            if rc == 0:
+                rc = L.tony_bn_bwd_apply_segs(Z.data_ptr(), ctot, len(ctx.splits), *ends, *ptr, *ld, dZ.data_ptr(),
+                                              ctot, M, csum, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
+                                              beta.data_ptr(), pb, 1, dsum.data_ptr(), _off(dsum, ctot), ss,
+                                              dgamma.data_ptr(), dbeta.data_ptr(), acc, stream)
+                _lib.check(rc, "tony_bn_bwd_apply_segs")
         c0 = 0
-        for ci, dy in zip(ctx.splits, douts):
-            dy, (_, _, lddy) = _as_rows(dy)
-            rc = L.tony_bn_bwd_reduce(_off(Z, c0), ctot, dy.data_ptr(), lddy, M, ci, _off(mean, c0), _off(invstd, c0),
-                                      _off(gamma, c0), _off(beta, c0), pb, 1, _off(dsum, c0), _off(dsum, ctot + c0),
-                                      ss, stream)
-            _lib.check(rc, "tony_bn_bwd_reduce")
-            rc = L.tony_bn_bwd_apply(_off(Z, c0), ctot, dy.data_ptr(), lddy, _off(dZ, c0), ctot, M, ci,
-                                     _off(mean, c0), _off(invstd, c0), _off(gamma, c0), _off(beta, c0), pb, 1,
-                                     _off(dsum, c0), _off(dsum, ctot + c0), ss, _off(dgamma, c0), _off(dbeta, c0),
-                                     acc, stream)
-            _lib.check(rc, "tony_bn_bwd_apply")
+        for ci, dy in zip(ctx.splits, dys):
+            if rc == 0:
+                break
+            lddy = _rows_view(dy)[2]
+            rc2 = L.tony_bn_bwd_reduce(_off(Z, c0), ctot, dy.data_ptr(), lddy, M, ci, _off(mean, c0),
+                                       _off(invstd, c0), _off(gamma, c0), _off(beta, c0), pb, 1, _off(dsum, c0),
+                                       _off(dsum, ctot + c0), ss, stream)
+            _lib.check(rc2, "tony_bn_bwd_reduce")
+            rc2 = L.tony_bn_bwd_apply(_off(Z, c0), ctot, dy.data_ptr(), lddy, _off(dZ, c0), ctot, M, ci,
+                                      _off(mean, c0), _off(invstd, c0), _off(gamma, c0), _off(beta, c0), pb, 1,
+                                      _off(dsum, c0), _off(dsum, ctot + c0), ss, _off(dgamma, c0), _off(dbeta, c0),
+                                      acc, stream)
+            _lib.check(rc2, "tony_bn_bwd_apply")
             c0 += ci
+        c0 = sum(ctx.splits)  # the pool branch's columns follow the splits
         if ctx.npool:
             npool = ctx.npool
             dy, (_, _, lddy) = _as_rows(douts[len(ctx.splits)])
