@@ -272,19 +272,19 @@ __global__ __launch_bounds__(kThreads) void stem_fwd_kernel(StemGeom g, const ui
 }
 
 // ------------------------------------------------------------------------------ weight grad --
-// Each wave reduces 64 pixels of a 256-pixel chunk into the full CO x 64 tile of its column group
-// (blockIdx.y: GEMM columns [64 y, 64 y + 64) of K).  dY rows sit in LDS with a (CO + 4)-element
+// Each wave reduces 64 pixels of a 256-pixel chunk into the full CO x KW tile of its column group
+// (blockIdx.y: GEMM columns [KW y, KW y + KW) of K, KW = 16 KB).  dY rows sit in LDS with a (CO + 4)-element
 // pitch: the 8 rows a lane reads for one A fragment are 8 x pitch apart, which puts the four lane
 // quarters on disjoint bank ranges (conflict-free ds_read_u16).  The next chunk's dY rows and input
 // rows are loaded into registers while the current chunk computes.
-template <int CO>
+template <int CO, int KB>
 __global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(StemGeom g, const uint16_t* __restrict__ dy,
                                                               int64_t lddy, float* __restrict__ slab, int64_t n) {
   constexpr int PD = CO + 4;
   constexpr int CB = CO / 16;       // 16-row blocks of dW (output channels)
-  constexpr int KB = 4;             // 16-column blocks of dW per column group
+  constexpr int KW = KB * 16;       // dW columns per column group (blockIdx.y)
   constexpr int DYL = kBM * PD;     // dY staging elements
-  constexpr int RED = CO * 64;      // fp32 fold tile
+  constexpr int RED = CO * KW;      // fp32 fold tile
   constexpr int DV = kBM * CO / 8 / kThreads;  // 16-byte dY pieces per thread and chunk
   static_assert(RED * 4 <= (DYL + kPatch) * 2, "the fold tile reuses the staging buffers");
   __shared__ __attribute__((aligned(16))) uint16_t smem[DYL + kPatch];
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(StemGeom g, const 
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int kq = lane >> 4;
-  const int kcol0 = blockIdx.y * 64;
+  const int kcol0 = blockIdx.y * KW;
   const int kbn = min(KB, (g.K - kcol0 + 15) / 16);  // column blocks of this group inside K
   uint32_t tp[KB];  // this lane's B column per block is fixed for the whole kernel
 #pragma unroll
@@ -383,12 +383,12 @@ __global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(StemGeom g, const 
     for (int j = 0; j < KB; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (j < kbn) atomicAdd(red + (i * 16 + kq * 4 + r) * 64 + j * 16 + (lane & 15), acc[i][j][r]);
+        if (j < kbn) atomicAdd(red + (i * 16 + kq * 4 + r) * KW + j * 16 + (lane & 15), acc[i][j][r]);
   __syncthreads();
   float* out = slab + static_cast<int64_t>(blockIdx.x) * n;
-  const int kend = min(g.K, kcol0 + 64);
+  const int kend = min(g.K, kcol0 + KW);
   for (int v = threadIdx.x; v < RED; v += kThreads) {
-    const int co = v / 64, k = kcol0 + (v - co * 64);
+    const int co = v / KW, k = kcol0 + (v - co * KW);
     if (k < kend) out[static_cast<int64_t>(co) * g.K + k] = red[v];
   }
 }
@@ -463,13 +463,33 @@ TONY_API int tony_stem_wgrad(const void* dy, int64_t lddy, const void* x, int N,
     return -1;
   const int64_t n = static_cast<int64_t>(Co) * g.K;
   const int nchunks = ceil_div(g.M, kBM);
-  const int gx = min(nchunks, 2 * num_cus);
+  const bool k5 = Co == 64 && g.K > 64 && g.K <= 160;
+  // persistent grid = the resident workgroups (occupancy query; <= 2 per CU): a second wave of
+  // workgroups would only start when the first finishes its whole share of the chunks
+  static int occ[3] = {0, 0, 0};
+  const int which = k5 ? 2 : (Co == 64);
+  if (occ[which] == 0) {
+    const void* fn = k5 ? reinterpret_cast<const void*>(&stem_wgrad_kernel<64, 5>)
+                        : Co == 64 ? reinterpret_cast<const void*>(&stem_wgrad_kernel<64, 4>)
+                                   : reinterpret_cast<const void*>(&stem_wgrad_kernel<32, 4>);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[which], fn, kThreads, 0) != hipSuccess || occ[which] <= 0)
+      occ[which] = 1;
+  }
+  const int gx = min(nchunks, min(2, occ[which]) * num_cus);
   if (static_cast<int64_t>(gx) * n > slab_cap) return -1;
-  const dim3 grid(gx, ceil_div(g.K, 64));
-  if (Co == 32)
-    stem_wgrad_kernel<32><<<grid, kThreads, 0, stream>>>(g, static_cast<const uint16_t*>(dy), lddy, slab, n);
-  else
-    stem_wgrad_kernel<64><<<grid, kThreads, 0, stream>>>(g, static_cast<const uint16_t*>(dy), lddy, slab, n);
+  // column groups of 64 (Inception's K = 27 fits one); a 7x7 RGB stem (K = 147) takes its 160 padded
+  // columns in two groups of 5 blocks, so dY and the image are streamed twice instead of three times
+  // (one group of 10 blocks spills: 160 accumulator registers)
+  if (k5) {
+    stem_wgrad_kernel<64, 5><<<dim3(gx, ceil_div(g.K, 80)), kThreads, 0, stream>>>(
+        g, static_cast<const uint16_t*>(dy), lddy, slab, n);
+  } else {
+    const dim3 grid(gx, ceil_div(g.K, 64));
+    if (Co == 32)
+      stem_wgrad_kernel<32, 4><<<grid, kThreads, 0, stream>>>(g, static_cast<const uint16_t*>(dy), lddy, slab, n);
+    else
+      stem_wgrad_kernel<64, 4><<<grid, kThreads, 0, stream>>>(g, static_cast<const uint16_t*>(dy), lddy, slab, n);
+  }
   TONY_LAUNCH_CHECK();
   *splits = gx;
   return 0;
