@@ -385,7 +385,8 @@ def test_bn_reduce_fused_into_dgrad(cuda):
     bs = [torch.empty(co, device=cuda).uniform_(-0.2, 0.2).to(torch.bfloat16) for _, co, _, _ in dims]
 
     def run(fused, fp32=False):
-        C.FUSED_REDUCE = fused  # opt-in path (off by default, measured slower end to end)
+        C.FUSED_REDUCE = fused  # every eligible layer (the default fuses only >= 64 MB layers)
+        C.FUSED_REDUCE_MIN_BYTES = 0
         params = [t.detach().clone().float() if fp32 else t.detach().clone() for t in ws + gs + bs]
         for p in params:
             p.requires_grad_(True)
@@ -404,7 +405,7 @@ def test_bn_reduce_fused_into_dgrad(cuda):
         return [p.grad.float() for p in params]
 
     _lib.set_inplace_grads(False)
-    saved = C.FUSED_REDUCE
+    saved = C.FUSED_REDUCE, C.FUSED_REDUCE_MIN_BYTES
     try:
         hits0 = C.FUSED_REDUCE_HITS[0]
         fused = run(True)
@@ -414,7 +415,7 @@ def test_bn_reduce_fused_into_dgrad(cuda):
         plain = run(False)
         ref = run(False, fp32=True)
     finally:
-        C.FUSED_REDUCE = saved
+        C.FUSED_REDUCE, C.FUSED_REDUCE_MIN_BYTES = saved
         _lib.set_inplace_grads(True)
     for i, (a, b, r) in enumerate(zip(fused, plain, ref)):
         assert _rel(a, b) < 2e-3, f"param {i}: fused vs unfused {_rel(a, b):.2e}"

@@ -227,13 +227,21 @@ class BnCtx:
         self.gamma, self.beta, self.pb, self.relu, self.C = gamma, beta, pb, int(relu), Z.shape[1]
 
 
-# Opt-in (TONY_BN_FUSED_REDUCE=1).  Measured on MI355X it is a net loss: 24 of the 96 Inception-v3
-# reductions fuse (branch heads are _HeadFn layers, whose BN output no conv ctx reaches), the dgrad
-# epilogues grow by the Z reads + fold (+0.55 ms), and the apply pass no longer finds Z / dY warm in
-# the caches behind the reduce (+0.5 ms): 15.88 vs 15.60 ms/step, alternating A/B in one box session
-# (profiles/r2s3_rejected_bn_reduce_in_dgrad_ab.log).
-FUSED_REDUCE = os.environ.get("TONY_BN_FUSED_REDUCE", "0") == "1"
-FUSED_REDUCE_HITS = [0]  # BN backward passes that used a dgrad-fused reduction (tests, bench record)
+# TONY_BN_FUSED_REDUCE = 1 (every eligible layer) | 0 (never) | auto (default: layers whose Z is at
+# least FUSED_REDUCE_MIN_BYTES).  Fusing every eligible layer measured a net loss on MI355X: the
+# dgrad epilogues grow by the Z reads + fold, and for the small 35x35 / 17x17 layers the separate
+# apply pass loses the warm caches the reduce leaves (Z + dY fit the 256 MB Infinity Cache):
+# 15.88 vs 15.60 ms/step (profiles/r2s3_rejected_bn_reduce_in_dgrad_ab.log).  The stem layers' Z
+# (85-182 MB, twice that with dY) does not stay cached, so there the fused form saves a full pass.
+# Measured again with the "auto" threshold + the fused pool backward: 15.34 / 15.05 vs 14.98 / 14.98
+# ms/step (profiles/r2s3_rejected_bn_reduce_in_dgrad_ab.log): off by default.
+_FR = os.environ.get("TONY_BN_FUSED_REDUCE", "0").lower()
+FUSED_REDUCE = _FR != "0"
+FUSED_REDUCE_MIN_BYTES = 0 if _FR == "1" else int(os.environ.get("TONY_BN_FUSED_REDUCE_MIN_MB", "64")) << 20
+FUSED_REDUCE_HITS = [0]
+# TONY_POOL_BNRED=1: the stem max-pool backward also reduces the BN-backward sums (one kernel
+# instead of two); opt-in, measured no faster end to end (see _FR above)
+POOL_BNRED = os.environ.get("TONY_POOL_BNRED", "0") == "1"  # BN backward passes that used a dgrad-fused reduction (tests, bench record)
 
 
 def _dgrad_fused_bn(ctx, dy, weight, x_shape, stride, padding):
@@ -241,7 +249,8 @@ def _dgrad_fused_bn(ctx, dy, weight, x_shape, stride, padding):
     also reduces that layer's BN-backward sums and tags dX with them (``_tony_bnsums``): if autograd
     hands dX unchanged to that layer's backward, it skips its reduce kernel (``_bn_presums``)."""
     bnc = getattr(ctx, "bnc_in", None)
-    if bnc is None or not FUSED_REDUCE or tuple(bnc.Z.shape) != tuple(x_shape):
+    if (bnc is None or not FUSED_REDUCE or tuple(bnc.Z.shape) != tuple(x_shape)
+            or bnc.Z.numel() * bnc.Z.element_size() < FUSED_REDUCE_MIN_BYTES):
         return _dgrad(dy, weight, x_shape, stride, padding)
     sums = zeros_f32(_lib.stat_floats(bnc.C), dy.device)
     br = _lib.BnRed(bnc.Z.data_ptr(), bnc.ldz, bnc.mean.data_ptr(), bnc.invstd.data_ptr(), _lib.ptr(bnc.gamma),
@@ -575,14 +584,16 @@ class _ConvBNActFn(torch.autograd.Function):
         return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None
 
 
-def _conv_bn_backward(ctx, x, weight, gamma, beta, mean, invstd, Z, dy):
+def _conv_bn_backward(ctx, x, weight, gamma, beta, mean, invstd, Z, dy, presums=None):
     """BN(+ReLU) backward from Z (the ReLU mask is recomputed from it), then the conv's wgrad (side
-    stream when active) and dgrad; parameter gradients go straight into their flat slots."""
+    stream when active) and dgrad; parameter gradients go straight into their flat slots.
+    ``presums``: the BN reduction already computed by the kernel that produced dy."""
     L = _lib.lib()
     stride, padding, relu, pb = ctx.cfg
     dev = x.device
     M, co, ldz = _rows_view(Z)
-    presums = _bn_presums(ctx, dy)  # reduced by the consumer's dgrad epilogue
+    if presums is None:
+        presums = _bn_presums(ctx, dy)  # reduced by the consumer's dgrad epilogue
     dy, (_, _, lddy) = _as_rows(dy)
     dZ = torch.empty_like(Z)
     ws = None if presums is not None else zeros_f32(_lib.bn_bwd_ws_floats(co), dev)
@@ -642,10 +653,22 @@ class _ConvBNActPoolFn(torch.autograd.Function):
         n, co, h, w = Z.shape
         dyp, (_, _, lddy) = _as_rows(dyp)
         dy = _cl_empty(n, co, h, w, Z.device)
-        rc = _lib.lib().tony_maxpool_bwd(dyp.data_ptr(), arg.data_ptr(), dy.data_ptr(), n, h, w, co, k, s, lddy, co,
-                                         _lib.stream_ptr(Z.device))
-        _lib.check(rc, "tony_maxpool_bwd")
-        dx, dw, dgamma, dbeta = _conv_bn_backward(ctx, x, weight, gamma, beta, mean, invstd, Z, dy)
+        if not POOL_BNRED:
+            rc = _lib.lib().tony_maxpool_bwd(dyp.data_ptr(), arg.data_ptr(), dy.data_ptr(), n, h, w, co, k, s, lddy,
+                                             co, _lib.stream_ptr(Z.device))
+            _lib.check(rc, "tony_maxpool_bwd")
+            dx, dw, dgamma, dbeta = _conv_bn_backward(ctx, x, weight, gamma, beta, mean, invstd, Z, dy)
+            return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None
+        # the pool backward also reduces the BN backward sums (csrc/pool.hip maxpool_bwd_bnred_kernel):
+        # the separate two-pass reduce over Z and dY (354 / 155 MB each at the Inception stem) disappears
+        _, _, ldz = _rows_view(Z)
+        sums = zeros_f32(_lib.stat_floats(co), Z.device)
+        rc = _lib.lib().tony_maxpool_bwd_bnred(dyp.data_ptr(), arg.data_ptr(), dy.data_ptr(), n, h, w, co, k, s,
+                                               lddy, co, Z.data_ptr(), ldz, mean.data_ptr(), invstd.data_ptr(),
+                                               gamma.data_ptr(), beta.data_ptr(), ctx.cfg[3], 1, sums.data_ptr(),
+                                               2 * co, _lib.num_cus(Z.device), _lib.stream_ptr(Z.device))
+        _lib.check(rc, "tony_maxpool_bwd_bnred")
+        dx, dw, dgamma, dbeta = _conv_bn_backward(ctx, x, weight, gamma, beta, mean, invstd, Z, dy, presums=sums)
         return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None
 
 

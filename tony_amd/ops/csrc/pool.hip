@@ -11,6 +11,8 @@
 // A lane owns one (n, h, w) site x 8 channels; neighbouring lanes own the next
 // channel groups of the same site, so every wavefront access is a contiguous
 // span of the NHWC image and the 3x3 neighbourhood re-reads hit L1/L2.
+#include <algorithm>
+
 #include "common.h"
 
 using namespace tony;
@@ -139,6 +141,96 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd_kernel(const uint16_t* _
   }
 }
 
+// Max-pool backward fused with the BatchNorm-backward reduction of the layer that fed the pool
+// (Inception's stem: conv -> BN -> ReLU -> maxpool 3x3/2 at 147x147x64 and 71x71x192, whose BN
+// backward then needs dsum[c] = sum dY', dsumx[c] = sum dY' xhat over 354 / 155 MB of Z and dY).
+// The pool backward produces every dY element anyway: reading Z beside it and reducing there
+// replaces the separate reduce kernel's two full passes by one.  Workgroup-contiguous site ranges,
+// one fixed 8-channel group per thread (the BN kernels' RowMap), partial sums folded in LDS and
+// added once per workgroup into the sharded [dsum | dsumx] buffer.
+__global__ __launch_bounds__(kThreads) void maxpool_bwd_bnred_kernel(
+    const uint16_t* __restrict__ dy, const uint8_t* __restrict__ arg, uint16_t* __restrict__ dx, int N, int H,
+    int W, int C, int OH, int OW, int K, int S, int64_t lddy, int64_t lddx, int64_t sites_per_block,
+    const uint16_t* __restrict__ z, int64_t ldz, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const void* gamma, const void* beta, int pb, int relu, float* __restrict__ dsum, int64_t sstride) {
+  __shared__ float red[2 * kThreads * 8];
+  const int CG = C >> 3, RPI = kThreads / CG;
+  const int cg = threadIdx.x % CG, rsub = threadIdx.x / CG;
+  const bool active = rsub < RPI;
+  float a[8], b[8], p0[8], p1[8], p2[8], p3[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] = b[j] = 0.f;
+    const int c = cg * 8 + j;
+    const float mu = mean[c], is = invstd[c];
+    const float g = gamma == nullptr ? 1.f : pb ? bf2f(static_cast<const uint16_t*>(gamma)[c])
+                                                : static_cast<const float*>(gamma)[c];
+    const float be = beta == nullptr ? 0.f : pb ? bf2f(static_cast<const uint16_t*>(beta)[c])
+                                                : static_cast<const float*>(beta)[c];
+    p0[j] = is;
+    p1[j] = -mu * is;
+    p2[j] = g * is;
+    p3[j] = be - g * is * mu;
+  }
+  const int64_t total = static_cast<int64_t>(N) * H * W;
+  const int64_t s0 = static_cast<int64_t>(blockIdx.x) * sites_per_block;
+  const int64_t s1 = min(total, s0 + sites_per_block);
+  if (active) {
+    for (int64_t site = s0 + rsub; site < s1; site += RPI) {
+      const int w = static_cast<int>(site % W);
+      const int64_t nh = site / W;
+      const int h = static_cast<int>(nh % H);
+      const int64_t n = nh / H;
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      const int oh_lo = h >= K ? (h - K + S) / S : 0;
+      const int oh_hi = min(OH - 1, h / S);
+      const int ow_lo = w >= K ? (w - K + S) / S : 0;
+      const int ow_hi = min(OW - 1, w / S);
+      for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+        for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+          const int local = (h - oh * S) * K + (w - ow * S);
+          const int64_t osite = (n * OH + oh) * OW + ow;
+          const uint2 packed = *reinterpret_cast<const uint2*>(arg + osite * C + cg * 8);
+          float g[8];
+          load8(dy + osite * lddy + cg * 8).to_float(g);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const uint32_t word = j < 4 ? packed.x : packed.y;
+            if (((word >> (8 * (j & 3))) & 0xff) == static_cast<uint32_t>(local)) acc[j] += g[j];
+          }
+        }
+      }
+      const bf16x8 o = bf16x8::from_float(acc);
+      store8(dx + site * lddx + cg * 8, o);
+      float d[8], zf[8];
+      o.to_float(d);  // the stored bf16 values, as a separate reduce kernel would read them
+      load8(z + site * ldz + cg * 8).to_float(zf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = (relu && fmaf(zf[j], p2[j], p3[j]) <= 0.f) ? 0.f : d[j];
+        a[j] += v;
+        b[j] = fmaf(v, fmaf(zf[j], p0[j], p1[j]), b[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[rsub * C + cg * 8 + j] = a[j];
+      red[kThreads * 8 + rsub * C + cg * 8 + j] = b[j];
+    }
+  }
+  __syncthreads();
+  float* ds = dsum + shard_off(blockIdx.x, sstride);
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    float sa = 0.f, sb = 0.f;
+    for (int k = 0; k < RPI; ++k) {
+      sa += red[k * C + c];
+      sb += red[kThreads * 8 + k * C + c];
+    }
+    atomicAdd(ds + c, sa);
+    atomicAdd(ds + C + c, sb);
+  }
+}
+
 // avg KxK, stride S, no padding (Inception aux head 5x5/s3; K = H = W is the global average pool).
 __global__ __launch_bounds__(kThreads) void avgpool_fwd_kernel(const uint16_t* __restrict__ x,
                                                                uint16_t* __restrict__ y, int N, int H, int W, int C,
@@ -243,6 +335,29 @@ TONY_API int tony_maxpool_bwd(const void* dy, const void* argmax, void* dx, int 
   maxpool_bwd_kernel<<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(dy), static_cast<const uint8_t*>(argmax), static_cast<uint16_t*>(dx), N, H, W, C,
       OH, OW, K, S, lddy, lddx);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// tony_maxpool_bwd + the BN-backward reduction of Z (the pool input's BN input, rows = dX pixels):
+// [dsum | dsumx] (kStatShards copies sstride floats apart, zeroed) accumulate sum dY', sum dY' xhat.
+TONY_API int tony_maxpool_bwd_bnred(const void* dy, const void* argmax, void* dx, int N, int H, int W, int C, int K,
+                                    int S, int64_t lddy, int64_t lddx, const void* z, int64_t ldz, const float* mean,
+                                    const float* invstd, const void* gamma, const void* beta, int pb, int relu,
+                                    float* dsum, int64_t sstride, int num_cus, hipStream_t stream) {
+  if (C % 8 || C > 2048 || lddy % 8 || lddx % 8 || ldz % 8 || H < K || W < K || z == nullptr || mean == nullptr ||
+      invstd == nullptr || dsum == nullptr || (reinterpret_cast<uintptr_t>(z) & 15) || sstride < 0)
+    return -1;
+  const int64_t total = static_cast<int64_t>(N) * H * W;
+  if (total * (C / 8) > 0x7fffffff) return -1;
+  const int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
+  const int64_t blocks = std::min<int64_t>(4 * static_cast<int64_t>(num_cus > 0 ? num_cus : 256),
+                                           (total + 63) / 64);
+  const int64_t per = (total + blocks - 1) / blocks;
+  maxpool_bwd_bnred_kernel<<<static_cast<int>((total + per - 1) / per), kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(dy), static_cast<const uint8_t*>(argmax), static_cast<uint16_t*>(dx), N, H, W, C,
+      OH, OW, K, S, lddy, lddx, per, static_cast<const uint16_t*>(z), ldz, mean, invstd, gamma, beta, pb, relu, dsum,
+      sstride);
   TONY_LAUNCH_CHECK();
   return 0;
 }
