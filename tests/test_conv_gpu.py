@@ -370,6 +370,38 @@ def test_conv_direct_variant(cuda, shape):
     assert _rel(dx, xr.grad) < 1e-2
 
 
+# (N, Cin, H, W, Cout, (R, S), padding): LDS-DMA kernel shapes -- partial row / column tiles, K not a
+# multiple of 64, Cin < 64 (several taps per K-step), 1x1
+GLDS_SHAPES = [(2, 64, 35, 35, 96, (3, 3), (1, 1)), (2, 48, 17, 19, 64, (5, 5), (2, 2)),
+               (2, 160, 17, 17, 192, (1, 7), (0, 3)), (3, 448, 8, 8, 384, (3, 3), (1, 1)),
+               (2, 88, 13, 11, 40, (1, 1), (0, 0)), (1, 32, 9, 9, 32, (3, 3), (0, 0))]
+
+
+@pytest.mark.parametrize("v", range(11, 16))
+@pytest.mark.parametrize("shape", GLDS_SHAPES, ids=[f"{s[1]}->{s[4]}_{s[2]}x{s[3]}k{s[5][0]}{s[5][1]}" for s in GLDS_SHAPES])
+def test_conv_glds_variants(cuda, shape, v):
+    """csrc/conv.hip conv_glds_kernel (variants 11-15): forward + BN statistics, stride-1 backward-data."""
+    from tony_amd.ops import _lib
+    from tony_amd.ops.conv import conv_dgrad, conv_fwd
+
+    n, c, h, w, co, (r, s), p = shape
+    torch.manual_seed(v)
+    x = _nhwc(torch.randn(n, c, h, w, device=cuda)).to(torch.bfloat16)
+    wt = _nhwc(torch.randn(co, c, r, s, device=cuda) / (c * r * s) ** 0.5).to(torch.bfloat16)
+    stats = torch.zeros(_lib.stat_floats(co), device=cuda)
+    y = conv_fwd(x, wt, 1, p, stats, vflags=v << 8)
+    xr = x.float().requires_grad_(True)
+    ref = torch.nn.functional.conv2d(xr, wt.float(), None, 1, p)
+    assert _rel(y, ref) < 1e-2
+    st = _lib.fold_stats(stats, co)
+    torch.testing.assert_close(st[:co], ref.detach().sum((0, 2, 3)), rtol=2e-3, atol=ref.numel() / co * 2e-4)
+    torch.testing.assert_close(st[co:], (ref.detach() ** 2).sum((0, 2, 3)), rtol=2e-3, atol=1e-1)
+    dy = _nhwc(torch.randn_like(ref)).to(torch.bfloat16)
+    ref.backward(dy.float())
+    dx = conv_dgrad(dy, wt, x.shape, 1, p, vflags=v << 8)
+    assert _rel(dx, xr.grad) < 1e-2
+
+
 def test_bn_reduce_fused_into_dgrad(cuda):
     """A chain conv-BN-ReLU -> conv-BN-ReLU (strided) -> conv-BN-ReLU: each BN backward's reduction
     comes from the next conv's dgrad epilogue (csrc/conv.hip BnRed: NT kernel, strided residue classes,

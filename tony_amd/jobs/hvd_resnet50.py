@@ -1,8 +1,8 @@
 """ResNet-50 bf16 data-parallel training through the Horovod API (BASELINE.json config
 "horovod-on-tony ResNet-50 ring-allreduce bf16 on 8xMI355X").
 
-Per rank: the fused-kernel ResNet-50 (NHWC bf16, tony_amd conv/BN/GEMM/residual HIP kernels; MIOpen
-only for the 3-channel 7x7 stem), synthetic ImageNet batches generated on the device, SGD-momentum
+Per rank: the fused-kernel ResNet-50 (NHWC bf16, tony_amd conv/BN/GEMM/residual HIP kernels, the
+3-channel 7x7 stem included: ops/csrc/stem.hip), synthetic ImageNet batches generated on the device, SGD-momentum
 through ``hvd.DistributedOptimizer``: its bucketed all-reduce (RCCL over xGMI) overlaps the backward
 pass and the update is one fused HIP SGD launch per flat buffer.  Reports images/sec over all ranks.
 

@@ -238,10 +238,10 @@ class BnCtx:
 _FR = os.environ.get("TONY_BN_FUSED_REDUCE", "0").lower()
 FUSED_REDUCE = _FR != "0"
 FUSED_REDUCE_MIN_BYTES = 0 if _FR == "1" else int(os.environ.get("TONY_BN_FUSED_REDUCE_MIN_MB", "64")) << 20
-FUSED_REDUCE_HITS = [0]
+FUSED_REDUCE_HITS = [0]  # BN backward passes that used a dgrad-fused reduction (tests, bench record)
 # TONY_POOL_BNRED=1: the stem max-pool backward also reduces the BN-backward sums (one kernel
 # instead of two); opt-in, measured no faster end to end (see _FR above)
-POOL_BNRED = os.environ.get("TONY_POOL_BNRED", "0") == "1"  # BN backward passes that used a dgrad-fused reduction (tests, bench record)
+POOL_BNRED = os.environ.get("TONY_POOL_BNRED", "0") == "1"
 
 
 def _dgrad_fused_bn(ctx, dy, weight, x_shape, stride, padding):

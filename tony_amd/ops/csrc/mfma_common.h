@@ -173,7 +173,7 @@ struct RowMap {
 // acc layout of 16x16 MFMA: col = lane&15, row = (lane>>4)*4 + r.
 // With ``aff`` ([scale N | shift N] fp32, the folded inference BatchNorm) the stored value is
 // act(acc * scale[col] + shift[col]) (act = ReLU when ``relu``): conv + BN + ReLU in one pass (H5).
-template <int BM, int BN, int TM, int TN>
+template <int BM, int BN, int TM, int TN, int LDS_ELEMS = 2 * (BM + BN) * BK>
 __device__ __forceinline__ void nt_epilogue(f32x4 (&acc)[TM][TN], uint16_t* smem, uint16_t* __restrict__ C,
                                             int64_t ldc, int M, int N, int m0, int n0, float* __restrict__ stats,
                                             const float* __restrict__ aff = nullptr, bool relu = false,
@@ -206,7 +206,7 @@ __device__ __forceinline__ void nt_epilogue(f32x4 (&acc)[TM][TN], uint16_t* smem
     }
   }
   constexpr int LDC = BN + 8;
-  static_assert(BM * LDC <= 2 * (BM + BN) * BK, "C staging tile must fit in the LDS buffers");
+  static_assert(BM * LDC <= LDS_ELEMS, "C staging tile must fit in the LDS buffers");
   uint16_t* Cs = smem;  // the K loop ended with a barrier: both buffers are free
   if (aff != nullptr) {
 #pragma unroll

@@ -17,8 +17,10 @@ from typing import Callable, Dict, Hashable
 import torch
 
 AUTOTUNE = os.environ.get("TONY_CONV_AUTOTUNE", "1") != "0"
-NT_VARIANTS = tuple(range(11))  # csrc/mfma_common.h kNtVariants (0-8) + 9: conv.hip halo-tile 3x3 path,
-# 10: conv.hip persistent direct 3x3 kernel (32/64 channels)
+# csrc/mfma_common.h kNtVariants (0-8) + 9: conv.hip halo-tile 3x3 path, 10: conv.hip persistent
+# direct 3x3 kernel (32/64 channels), 11-15: conv.hip LDS-DMA kernels (kGldsVariants; TONY_CONV_GLDS=0
+# leaves them out of the search)
+NT_VARIANTS = tuple(range(16 if os.environ.get("TONY_CONV_GLDS", "1") != "0" else 11))
 _CACHE: Dict[Hashable, int] = {}
 
 

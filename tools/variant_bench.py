@@ -16,19 +16,26 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 STEM = [(32, 149, 149, 32, (3, 3), 1, (0, 0)), (32, 147, 147, 64, (3, 3), 1, (1, 1)),
         (80, 73, 73, 192, (3, 3), 1, (0, 0)), (64, 35, 35, 96, (3, 3), 1, (1, 1)),
         (192, 17, 17, 192, (1, 7), 1, (0, 3)), (288, 35, 35, 384, (3, 3), 2, (0, 0))]
+# the other heavy Inception-v3 spatial convs (the 1x1s run through gemm.hip)
+MIXED = [(96, 35, 35, 96, (3, 3), 1, (1, 1)), (48, 35, 35, 64, (5, 5), 1, (2, 2)),
+         (128, 17, 17, 128, (1, 7), 1, (0, 3)), (160, 17, 17, 160, (7, 1), 1, (3, 0)),
+         (192, 17, 17, 320, (3, 3), 2, (0, 0)), (384, 8, 8, 384, (1, 3), 1, (0, 1)),
+         (448, 8, 8, 384, (3, 3), 1, (1, 1))]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--shapes", choices=("stem", "mixed", "all"), default="all")
     args = ap.parse_args()
     from tony_amd.ops import _lib, tune
     from tony_amd.ops import conv as C
 
     dev = torch.device("cuda", 0)
     cl = torch.channels_last
-    for cin, h, w, co, (r, s), st, pad in STEM:
+    shapes = {"stem": STEM, "mixed": MIXED, "all": STEM + MIXED}[args.shapes]
+    for cin, h, w, co, (r, s), st, pad in shapes:
         x = torch.randn(args.batch, cin, h, w, device=dev).to(torch.bfloat16).contiguous(memory_format=cl)
         wt = (0.05 * torch.randn(co, cin, r, s, device=dev)).to(torch.bfloat16).contiguous(memory_format=cl)
         y = C.conv_fwd(x, wt, st, pad)
@@ -37,7 +44,7 @@ def main():
         oh, ow = y.shape[2], y.shape[3]
         flop = 2.0 * args.batch * oh * ow * co * cin * r * s
         print(f"{args.batch}x{cin}x{h}x{w}->{co} k{r}x{s} s{st} p{pad}  ({flop / 1e9:.0f} GFLOP)")
-        for v in range(11):
+        for v in range(16):
             row = []
             for name, fn in (("fwd", lambda: C.conv_fwd(x, wt, st, pad, None, v << 8)),
                              ("fwd+stats", lambda: C.conv_fwd(x, wt, st, pad, stats, v << 8)),
