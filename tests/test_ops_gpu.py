@@ -71,8 +71,10 @@ def test_bn_act_strided_slice_and_eval(cuda):
     _close(y, ref, 2e-2, 2e-2, "bn eval on slice")
 
 
-@pytest.mark.parametrize("mnk", [(1000, 64, 192), (4096, 80, 64), (777, 320, 1280), (128, 1000, 2048), (33, 48, 256)])
-def test_gemm_nt(cuda, mnk):
+@pytest.mark.parametrize("v", [0, 11, 12, 13, 14, 15])  # heuristic register-staged tiles; LDS-DMA kernels (igemm.h)
+@pytest.mark.parametrize("mnk", [(1000, 64, 192), (4096, 80, 64), (777, 320, 1280), (128, 1000, 2048), (33, 48, 256),
+                                 (517, 200, 40)])
+def test_gemm_nt(cuda, mnk, v):
     from tony_amd.ops.gemm import gemm_nt
 
     m, n, k = mnk
@@ -80,7 +82,7 @@ def test_gemm_nt(cuda, mnk):
     a = torch.randn(m, k, device=cuda).to(torch.bfloat16)
     b = torch.randn(n, k, device=cuda).to(torch.bfloat16)
     stats = torch.empty(2 * n, device=cuda)
-    c = gemm_nt(a, b, stats=stats)
+    c = gemm_nt(a, b, stats=stats, vflags=v << 8)
     ref = a.float() @ b.float().t()
     _close(c, ref, 2e-2, 0.02 * (k ** 0.5), "gemm")
     _close(stats[:n], ref.sum(0), 1e-2, 1e-2 * m ** 0.5 * k ** 0.5, "gemm col sum")

@@ -18,53 +18,12 @@
 #include <cstdlib>
 #include <type_traits>
 
-#include "mfma_common.h"
+#include "igemm.h"
 
 using namespace tony;
 using namespace tony::mfma;
 
 namespace {
-
-struct Gather {
-  const uint16_t* src;  // source image, pixel-major: pixel p at src + p * ld
-  int64_t ld;           // elements per pixel row (>= Cs; a channel slice of a concat buffer is fine)
-  int Hs, Ws, Cs;       // source spatial dims and channels
-  int OH, OW;           // the GEMM row space: m -> (n, oy, ox) over [N][OH][OW]
-  int R, S;             // filter taps
-  int sh, sw;           // stride of the output grid in source pixels
-  int offh, offw;       // source coord = o*stride + off + sign*tap
-  int sign;             // +1 convolution, -1 transposed (dgrad)
-  int K;                // R * S * Cs
-  int halo_images;      // batch count N (the halo-tile path walks images x tile rows x tile columns)
-};
-
-struct RowState {
-  int pix;   // n * Hs * Ws
-  int iy0;   // oy*sh + offh
-  int ix0;   // ox*sw + offw
-  bool ok;   // row < M
-};
-
-// position of a K chunk: channel c of tap (r, s)
-struct TapPos {
-  int c, r, s;
-  __device__ __forceinline__ void init(int k, const Gather& g) {
-    c = k % g.Cs;
-    const int tap = k / g.Cs;
-    r = tap / g.S;
-    s = tap - r * g.S;
-  }
-  __device__ __forceinline__ void advance(int dk, const Gather& g) {
-    c += dk;
-    while (c >= g.Cs) {
-      c -= g.Cs;
-      if (++s == g.S) {
-        s = 0;
-        ++r;
-      }
-    }
-  }
-};
 
 __device__ __forceinline__ uint4 gather16(const Gather& g, const RowState& rs, const TapPos& t) {
   const int iy = rs.iy0 + g.sign * t.r, ix = rs.ix0 + g.sign * t.s;
@@ -778,235 +737,6 @@ int run_direct(const Gather& g, const void* B, void* C, int64_t ldc, int64_t N, 
   return -3;
 }
 
-// ---- forward / stride-1 dgrad with LDS-DMA staging and wide wave tiles (variants 11..15) -------
-// conv_nt_kernel stages both operands through VGPRs (global_load -> ds_write_b128) and its 32x48
-// wave tiles read 5 fragments per 6 MFMAs: per 64-deep K-step the LDS array carries ~420 cycles
-// (the 13-cycle ds_write_b128 transfer dominates) against 192 MFMA cycles per SIMD.  Here
-//   * every 16-byte chunk goes global -> LDS by global_load_lds_dwordx4 (no VGPR round trip, no
-//     ds_write): a wave instruction fills 1 KB of LDS rows (8 rows of 128 B at KB = 64, 16 rows of
-//     64 B at KB = 32) lane-linearly; the LDS swizzle is applied on the SOURCE side -- the lane that
-//     lands on physical chunk p of row r fetches logical chunk p ^ swz(r) -- so the fragment reads
-//     stay conflict-free;
-//   * padding taps, rows past M and columns past N / K fetch the 16 zero bytes of kZeroChunk;
-//   * ST stages ring in LDS, ST - 1 of them in flight behind the MFMAs; completion is one counted
-//     `s_waitcnt vmcnt` + s_barrier per K-step (hipcc does not see the DMAs, see glds16);
-//   * 2x2 waves of (BM/2) x (BN/2): 64x64 wave tiles read 8 fragments per 16 MFMAs.
-// Measured on MI355X (tools/variant_bench.py): what matters most is resident waves -- a 3-stage
-// 96 KB ring at one workgroup per CU ran 1.5x slower than a 2-stage 64 KB one at two -- so the
-// 32-deep K-steps (KB = 32) exist to keep 2-3 stages in flight at 2-3 workgroups per CU.
-// Each thread owns one K chunk column for the whole loop, so the tap walk (TapPos) is per thread,
-// as in conv_nt_kernel.  Row groups that do not divide evenly over the 4 waves are re-fetched by a
-// wave with a spare instruction slot (identical bytes to the same LDS row: benign, and it keeps the
-// per-wave DMA count a compile-time constant for the vmcnt wait).
-constexpr int kGldsFirst = 11;
-struct GldsVariant {
-  int bm, cap, stages, kb;
-};
-constexpr GldsVariant kGldsVariants[] = {
-    {128, 128, 2, 64}, {128, 128, 3, 32}, {128, 128, 4, 32}, {128, 192, 3, 32}, {64, 128, 4, 32}};
-constexpr int kNumGlds = sizeof(kGldsVariants) / sizeof(kGldsVariants[0]);
-
-template <int N>
-__device__ __forceinline__ void glds_wait_barrier() {  // this thread's DMAs but the last N landed, then all waves
-  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
-}
-
-// LDS layout of a KB-deep operand tile: row r holds KB bf16 (KB / 8 chunks of 16 B); logical chunk c
-// sits at physical chunk c ^ swz(r).  KB = 64: lds_off's (r & 7).  KB = 32 (4 chunks, 4 rows per
-// 256-B bank period): s[(r >> 2) & 3] with s = {0, 2, 3, 1} puts the 16 (row, chunk) pairs of every
-// ds_read_b128 lane group ({0-3,12-15,20-27}, ...) on 16 distinct 16-B bank slots.
-template <int KB>
-__device__ __forceinline__ int gswz(int row) {
-  if constexpr (KB == 64) return row & 7;
-  else return (0x1320 >> (((row >> 2) & 3) * 4)) & 3;  // {0, 2, 3, 1}
-}
-template <int KB>
-__device__ __forceinline__ int goff(int row, int ch) {
-  return row * KB + ((ch ^ gswz<KB>(row)) << 3);
-}
-
-template <int BM, int BN, int ST, int KB>
-__global__ __launch_bounds__(kThreads) void conv_glds_kernel(Gather g, const uint16_t* __restrict__ B,
-                                                             uint16_t* __restrict__ C, int64_t ldc, int M, int N,
-                                                             float* __restrict__ stats, int64_t sstride, int epi,
-                                                             int tiles_n) {
-  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
-  constexpr int CPR = KB / 8;                // 16-B chunks per LDS row
-  constexpr int RPI = 64 / CPR;              // rows per DMA instruction (1 KB)
-  constexpr int AG = BM / RPI, BG = BN / RPI;  // row groups per operand tile
-  constexpr int AI = (AG + 3) / 4, BI = (BG + 3) / 4;  // DMA instructions per wave and stage
-  constexpr int STAGE = (BM + BN) * KB;      // elements
-  constexpr int KSUB = KB / 32;              // MFMA K-steps per stage
-  static_assert(BM % RPI == 0 && BN % RPI == 0 && BN % 32 == 0 && ST >= 2 && (KB == 32 || KB == 64), "tile shape");
-  static_assert(BM * (BN + 8) <= ST * STAGE, "the epilogue's C tile fits in the ring");
-  __shared__ __attribute__((aligned(16))) uint16_t smem[ST * STAGE];
-
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = wg / tiles_n, tn = wg % tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int K = g.K;
-  const int rin = lane / CPR;                     // row within the instruction's row group
-  const int ck = (lane % CPR) ^ gswz<KB>(rin);    // logical K chunk this lane fetches (row groups are
-                                                  // RPI-aligned, so swz(row) == swz(rin))
-
-  RowState rs[AI];
-  int agrp[AI];
-  const int ohw = g.OH * g.OW;
-#pragma unroll
-  for (int i = 0; i < AI; ++i) {
-    agrp[i] = min(wave + 4 * i, AG - 1);
-    const int m = m0 + agrp[i] * RPI + rin;
-    rs[i].ok = m < M;
-    const int mm = rs[i].ok ? m : 0;
-    const int n = mm / ohw, rem = mm - n * ohw;
-    const int oy = rem / g.OW, ox = rem - oy * g.OW;
-    rs[i].pix = n * g.Hs * g.Ws;
-    rs[i].iy0 = oy * g.sh + g.offh;
-    rs[i].ix0 = ox * g.sw + g.offw;
-  }
-  const uint16_t* brow[BI];
-  bool bok[BI];
-  int bgrp[BI];
-#pragma unroll
-  for (int i = 0; i < BI; ++i) {
-    bgrp[i] = min(wave + 4 * i, BG - 1);
-    const int n = n0 + bgrp[i] * RPI + rin;
-    bok[i] = n < N;
-    brow[i] = B + static_cast<int64_t>(bok[i] ? n : 0) * K;
-  }
-  TapPos tp;
-  tp.init(ck * 8, g);
-  int kb = ck * 8;  // this thread's K column of the next stage to issue
-  const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(smem));
-  constexpr uint32_t kGroupB = RPI * KB * 2;  // bytes per row group
-  constexpr uint32_t kStageB = STAGE * 2, kBOff = BM * KB * 2;
-  uint32_t aoff[AI], boff[BI];  // wave-uniform byte offsets of this wave's row groups
-#pragma unroll
-  for (int i = 0; i < AI; ++i) aoff[i] = __builtin_amdgcn_readfirstlane(agrp[i] * kGroupB);
-#pragma unroll
-  for (int i = 0; i < BI; ++i) boff[i] = __builtin_amdgcn_readfirstlane(kBOff + bgrp[i] * kGroupB);
-
-  auto issue = [&](int slot) {
-    const uint32_t st0 = base + slot * kStageB;
-    const void* z = &kZeroChunk;
-#pragma unroll
-    for (int i = 0; i < AI; ++i) {
-      const int iy = rs[i].iy0 + g.sign * tp.r, ix = rs[i].ix0 + g.sign * tp.s;
-      const bool ok = rs[i].ok & (tp.r < g.R) & (static_cast<unsigned>(iy) < static_cast<unsigned>(g.Hs)) &
-                      (static_cast<unsigned>(ix) < static_cast<unsigned>(g.Ws));
-      const uint16_t* src = g.src + (static_cast<int64_t>(rs[i].pix) + iy * g.Ws + ix) * g.ld + tp.c;
-      glds16(ok ? static_cast<const void*>(src) : z, st0 + aoff[i]);
-    }
-    const bool kok = kb < K;
-#pragma unroll
-    for (int i = 0; i < BI; ++i) glds16(kok & bok[i] ? static_cast<const void*>(brow[i] + kb) : z, st0 + boff[i]);
-    tp.advance(KB, g);
-    kb += KB;
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int nk = (K + KB - 1) / KB;
-#pragma unroll
-  for (int s = 0; s < ST - 1; ++s) issue(s);
-  int slot = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    // stage kt has landed everywhere and every wave is done reading stage kt - 1, whose slot takes
-    // stage kt + ST - 1 (past the end: zero fills, which keeps the per-thread DMA count uniform)
-    glds_wait_barrier<(ST - 2) * (AI + BI)>();
-    issue(slot == 0 ? ST - 1 : slot - 1);
-    const uint16_t* As = smem + slot * STAGE;
-    const uint16_t* Bs = As + BM * KB;
-#pragma unroll
-    for (int kk = 0; kk < KSUB; ++kk) {
-      const int ch = kk * 4 + (lane >> 4);
-      bf16x8_t af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8_t*>(As + goff<KB>(wm * WM + i * 16 + (lane & 15), ch));
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8_t*>(Bs + goff<KB>(wn * WN + j * 16 + (lane & 15), ch));
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    slot = slot + 1 == ST ? 0 : slot + 1;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's zero fills land before LDS is reused
-  __syncthreads();
-  nt_epilogue<BM, BN, TM, TN, ST * STAGE>(acc, smem, C, ldc, M, N, m0, n0,
-                                           (epi & 1) ? stats + shard_off(tm, sstride) : nullptr,
-                                           (epi & 2) ? stats : nullptr, (epi & 4) != 0);
-}
-
-int run_glds(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, int epi, float* st,
-             int64_t sstride, int v, hipStream_t stream) {
-  if ((ldc % 8) || (reinterpret_cast<uintptr_t>(C) & 15) || (reinterpret_cast<uintptr_t>(B) & 15) ||
-      (g.ld % 8) || (g.K % 8))
-    return -3;
-  const GldsVariant gv = kGldsVariants[v - kGldsFirst];
-  const int64_t bn = pick_bn(N, gv.cap);
-  using std::integral_constant;
-  const auto launch = [&](auto bm, auto bnc, auto st_, auto kb) -> int {
-    constexpr int BM = decltype(bm)::value, BN = decltype(bnc)::value, ST = decltype(st_)::value;
-    constexpr int KB = decltype(kb)::value;
-    if constexpr (BN % (64 / (KB / 8)) != 0) {
-      return -3;
-    } else {
-      const int tiles_m = ceil_div(M, BM), tiles_n = ceil_div(N, BN);
-      const int64_t tiles = static_cast<int64_t>(tiles_m) * tiles_n;
-      if (tiles > 0x7fffffff) return -2;
-      conv_glds_kernel<BM, BN, ST, KB><<<static_cast<int>(tiles), kThreads, 0, stream>>>(
-          g, static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), ldc, static_cast<int>(M),
-          static_cast<int>(N), st, sstride, epi, tiles_n);
-      TONY_LAUNCH_CHECK();
-      return 0;
-    }
-  };
-  const auto by_bn = [&](auto bm, auto st_, auto kb, auto cap) -> int {
-    constexpr int CAP = decltype(cap)::value;
-    switch (bn) {
-      case 32: return launch(bm, integral_constant<int, 32>{}, st_, kb);
-      case 64: return launch(bm, integral_constant<int, 64>{}, st_, kb);
-      case 96: return launch(bm, integral_constant<int, 96>{}, st_, kb);
-      case 128: return launch(bm, integral_constant<int, 128>{}, st_, kb);
-      case 160:
-        if constexpr (CAP >= 160) return launch(bm, integral_constant<int, 160>{}, st_, kb);
-        break;
-      case 192:
-        if constexpr (CAP >= 192) return launch(bm, integral_constant<int, 192>{}, st_, kb);
-        break;
-      default: break;
-    }
-    return -3;
-  };
-  using I2 = integral_constant<int, 2>;
-  using I3 = integral_constant<int, 3>;
-  using I4 = integral_constant<int, 4>;
-  using K32 = integral_constant<int, 32>;
-  using K64 = integral_constant<int, 64>;
-  using M64 = integral_constant<int, 64>;
-  using M128 = integral_constant<int, 128>;
-  using C128 = integral_constant<int, 128>;
-  using C192 = integral_constant<int, 192>;
-  switch (v - kGldsFirst) {
-    case 0: return by_bn(M128{}, I2{}, K64{}, C128{});
-    case 1: return by_bn(M128{}, I3{}, K32{}, C128{});
-    case 2: return by_bn(M128{}, I4{}, K32{}, C128{});
-    case 3: return by_bn(M128{}, I3{}, K32{}, C192{});
-    case 4: return by_bn(M64{}, I4{}, K32{}, C128{});
-    default: return -3;
-  }
-}
-
 int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, int flags, float* stats,
            int64_t sstride, hipStream_t stream, const Phase& bph = Phase{}) {
   // flags bit0: statistics accumulated into stats (the caller zeroes it, ops/arena.py);
@@ -1019,7 +749,7 @@ int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int6
   if (v == kHaloVariant) return bph.bnr.z != nullptr ? -3 : run_halo(g, B, C, ldc, N, epi, st, sstride, stream);
   if (v == kDirectVariant) return run_direct(g, B, C, ldc, N, epi, st, sstride, stream, bph.bnr);
   if (v >= kGldsFirst && v < kGldsFirst + kNumGlds)
-    return bph.bnr.z != nullptr ? -3 : run_glds(g, B, C, ldc, M, N, epi, st, sstride, v, stream);
+    return bph.bnr.z != nullptr ? -3 : run_glds(g, B, g.K, C, ldc, M, N, epi, st, sstride, v, stream);
   if (v >= kNumNtVariants) return -1;
   if (v == 0) {
     const int64_t bn = pick_bn(N, 192);

@@ -19,7 +19,7 @@
 //    an A row-panel) are dispatched onto the same XCD and hit its private L2.
 #include <cstdlib>
 
-#include "mfma_common.h"
+#include "igemm.h"
 
 using namespace tony;
 using namespace tony::mfma;
@@ -179,6 +179,8 @@ TONY_API int tony_gemm_bf16(const void* A, const void* B, void* C, int64_t M, in
   if ((epi & 3) && stats == nullptr) return -1;
   float* st = stats;
   const int v = (flags >> 8) & 0xff;
+  if (v >= kGldsFirst && v < kGldsFirst + kNumGlds)  // LDS-DMA kernel on A as a 1x1 "conv" (igemm.h)
+    return run_glds(gemm_gather(A, lda, M, K), B, ldb, C, ldc, M, N, epi, st, sstride, v, stream);
   if (v >= kNumNtVariants) return -1;
   if (v == 0) {
     if (N <= 64) return launch<256, 64>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, epi, stream);

@@ -19,8 +19,10 @@ from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 
 
-def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, stats: torch.Tensor | None = None):
-    """out[M,N] = a[M,K] @ b[N,K]^T for bf16 CUDA 2-D tensors with unit inner stride."""
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, stats: torch.Tensor | None = None,
+            vflags: int = 0):
+    """out[M,N] = a[M,K] @ b[N,K]^T for bf16 CUDA 2-D tensors with unit inner stride (``vflags``: tile
+    variant bits, ops/tune.py; 0 = the built-in heuristic)."""
     if not (a.is_cuda and b.is_cuda) or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
         raise TypeError("gemm_nt takes bf16 CUDA tensors")
     if a.stride(1) != 1:
@@ -37,7 +39,8 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, s
         stats.zero_()  # the epilogue accumulates into it
     rc = _lib.lib().tony_gemm_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0) if M > 1 else K,
                                    b.stride(0) if N > 1 else K, out.stride(0) if M > 1 else N,
-                                   1 if stats is not None else 0, _lib.ptr(stats), 0, _lib.stream_ptr(a.device))
+                                   (1 if stats is not None else 0) | vflags, _lib.ptr(stats), 0,
+                                   _lib.stream_ptr(a.device))
     _lib.check(rc, "tony_gemm_bf16")
     return out
 
@@ -52,7 +55,11 @@ def _gemm_rows(a_ptr, lda, b, M, N, K, out_ptr, ldc, device):
 # them occ x the real CU count keeps more splits in flight per CU (bigger slab, more latency hiding,
 # more combine traffic).  The best occ depends on the shape (tools/conv_bench.py --tony: 4 beats 1
 # on the 147x147 stem, changes nothing at 17x17), so it is autotuned per shape (ops/tune.py).
-WGRAD_OCC = (1, 2, 4, 8)
+# In the training step the wgrads run on a side stream beside the BN passes, and more splits also
+# mean more fp32 partials through HBM (~1 GB of slab per step at the tuned 2-4x): restricting the
+# search to occ = 1 measured 14.43 / 14.47 vs 14.55 / 14.62 ms of GPU time per step
+# (profiles/r2s3_wgrad_occ_ab.log).  TONY_WGRAD_OCC=1,2,4,8 restores the isolated-speed search.
+WGRAD_OCC = tuple(int(o) for o in os.environ.get("TONY_WGRAD_OCC", "1").split(","))
 
 
 def wgrad_cus(device, occ: int = 1) -> int:

@@ -1,7 +1,10 @@
-"""tony_amd MFMA GEMMs vs hipBLASLt (torch.matmul) on the conv-shaped problems of Inception-v3 (bs128).
+"""Per-variant timing of the NT GEMM (csrc/gemm.hip: register-staged tiles 1-8, LDS-DMA kernels 11-15
+from igemm.h) on the Inception-v3 1x1-conv shapes at batch 128: the fused-head forwards (N = the
+concatenated 1x1 outputs of a block) and their backward-data GEMMs.
 
-NT (forward / dgrad of 1x1 convs): C[M,N] = A[M,K] B[N,K]^T ; TN (wgrad): C[N1,N2] = A[M,N1]^T B[M,N2].
+usage: python tools/gemm_bench.py [--iters 10]
 """
+import argparse
 import os
 import sys
 
@@ -9,45 +12,43 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from tony_amd.ops.gemm import gemm_nt, gemm_tn  # noqa: E402
-
-NT = [(156800, 64, 192), (156800, 352, 192), (156800, 192, 352), (36992, 768, 768), (36992, 192, 768),
-      (36992, 768, 192), (8192, 1280, 1280), (8192, 2048, 1280), (682112, 80, 64), (156800, 64, 64)]
-TN = [(156800, 352, 192), (36992, 768, 768), (36992, 192, 768), (8192, 1280, 1280), (682112, 80, 64)]
-
-
-def t(fn, iters=20):
-    fn()
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        fn()
-    e.record()
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / iters
+# (M, N, K, label)
+SHAPES = [(128 * 35 * 35, 176, 192, "Mixed_5b head fwd"), (128 * 35 * 35, 192, 176, "Mixed_5b head dgrad"),
+          (128 * 35 * 35, 176, 288, "Mixed_5d head fwd"), (128 * 17 * 17, 768, 768, "Mixed_6c head fwd"),
+          (128 * 17 * 17, 768, 768, "Mixed_6c head dgrad"), (128 * 8 * 8, 1344, 1280, "Mixed_7b head fwd"),
+          (128 * 8 * 8, 1280, 1344, "Mixed_7b head dgrad"), (128 * 73 * 73, 80, 64, "Conv2d_3b fwd"),
+          (128 * 73 * 73, 64, 80, "Conv2d_3b dgrad"), (128 * 8 * 8, 1344, 2048, "Mixed_7c head fwd")]
+VARIANTS = list(range(9)) + list(range(11, 16))
 
 
 def main():
-    dev = torch.device("cuda")
-    print("| NT M,N,K | tony ms (TF/s) | hipBLASLt ms (TF/s) |")
-    print("|---|---|---|")
-    for m, n, k in NT:
-        a = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
-        b = torch.randn(n, k, device=dev, dtype=torch.bfloat16)
-        f = 2.0 * m * n * k
-        t1 = t(lambda: gemm_nt(a, b))
-        t2 = t(lambda: a @ b.t())
-        print(f"| {m},{n},{k} | {t1:.3f} ({f / t1 / 1e9:.0f}) | {t2:.3f} ({f / t2 / 1e9:.0f}) |")
-    print("\n| TN M,N1,N2 | tony ms (TF/s) | hipBLASLt ms (TF/s) |")
-    print("|---|---|---|")
-    for m, n1, n2 in TN:
-        a = torch.randn(m, n1, device=dev, dtype=torch.bfloat16)
-        b = torch.randn(m, n2, device=dev, dtype=torch.bfloat16)
-        f = 2.0 * m * n1 * n2
-        t1 = t(lambda: gemm_tn(a, b))
-        t2 = t(lambda: a.t() @ b)
-        print(f"| {m},{n1},{n2} | {t1:.3f} ({f / t1 / 1e9:.0f}) | {t2:.3f} ({f / t2 / 1e9:.0f}) |")
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=10)
+    args = ap.parse_args()
+    from tony_amd.ops import _lib, tune
+
+    dev = torch.device("cuda", 0)
+    L = _lib.lib()
+    st = _lib.stream_ptr(dev)
+    for m, n, k, label in SHAPES:
+        a = torch.randn(m, k, device=dev).to(torch.bfloat16)
+        b = (0.05 * torch.randn(n, k, device=dev)).to(torch.bfloat16)
+        c = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+        stats = torch.zeros(_lib.stat_floats(n), device=dev)
+        flop = 2.0 * m * n * k
+        row = []
+        for v in VARIANTS:
+            def run(v=v):
+                return L.tony_gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), m, n, k, k, k, n, 1 | (v << 8),
+                                        stats.data_ptr(), 2 * n, st)
+            if run() != 0:
+                continue
+            ms = tune.time_ms(run, args.iters)
+            row.append((ms, v))
+        best = min(row)
+        print(f"{label:22s} M={m:7d} N={n:5d} K={k:5d}  best v{best[1]:2d} {best[0] * 1e3:7.1f} us "
+              f"({flop / best[0] / 1e9:4.0f} TF/s) | " +
+              " ".join(f"v{v}:{ms * 1e3:.0f}" for ms, v in row), flush=True)
 
 
 if __name__ == "__main__":
