@@ -370,6 +370,29 @@ def test_conv_direct_variant(cuda, shape):
     assert _rel(dx, xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("shape", DIRECT_SHAPES + [(2, 64, 21, 40, 64, (2, 2)), (1, 32, 3, 3, 64, (1, 1))],
+                         ids=lambda s: f"{s[1]}->{s[4]}_{s[2]}x{s[3]}p{s[5][0]}")
+def test_conv_wgrad_direct(cuda, shape):
+    """csrc/conv.hip conv_wgrad_direct_kernel (3x3 stride 1, C / Co in {32, 64}) vs fp32, returned and
+    added into a bf16 gradient slot."""
+    from tony_amd.ops.conv import conv_wgrad
+
+    n, c, h, w, co, p = shape
+    torch.manual_seed(12)
+    x = _nhwc(torch.randn(n, c, h, w, device=cuda)).to(torch.bfloat16)
+    wt = _nhwc(0.1 * torch.randn(co, c, 3, 3, device=cuda)).to(torch.bfloat16)
+    xr, wr = x.float(), wt.float().requires_grad_(True)
+    ref = torch.nn.functional.conv2d(xr, wr, None, 1, p)
+    dy = _nhwc(torch.randn_like(ref)).to(torch.bfloat16)
+    ref.backward(dy.float())
+    dw = conv_wgrad(dy, x, wt.shape, 1, p, impl="direct")
+    assert _rel(dw, wr.grad) < 5e-3, f"direct wgrad rel {_rel(dw, wr.grad):.5f}"
+    slot = torch.full((co * 9 * c,), 0.5, device=cuda, dtype=torch.bfloat16)
+    assert conv_wgrad(dy, x, wt.shape, 1, p, dst=slot, impl="direct") is None
+    want = 0.5 + wr.grad.permute(0, 2, 3, 1).reshape(-1)
+    assert _rel(slot, want) < 1e-2
+
+
 # (N, Cin, H, W, Cout, (R, S), padding): LDS-DMA kernel shapes -- partial row / column tiles, K not a
 # multiple of 64, Cin < 64 (several taps per K-step), 1x1
 GLDS_SHAPES = [(2, 64, 35, 35, 96, (3, 3), (1, 1)), (2, 48, 17, 19, 64, (5, 5), (2, 2)),

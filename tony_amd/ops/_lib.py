@@ -99,6 +99,8 @@ _SIGNATURES = {
     "tony_conv_wgrad": [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int, c_int, c_int, c_int,
                         c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_void_p,
                         c_void_p, c_int, c_void_p],
+    "tony_conv_wgrad_direct": [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int, c_int, c_int,
+                               c_int, c_int, c_void_p, c_int64, c_void_p, c_int, c_void_p],
     "tony_avgpool3_s1p1": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
     "tony_maxpool_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
                          c_void_p],

@@ -271,7 +271,37 @@ def _bn_presums(ctx, dy):
     return pre[1]
 
 
-def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride=1, padding=0, dst=None):
+# csrc/conv.hip conv_wgrad_direct_kernel: 3x3 stride-1 convs with 32 / 64 channels in and out (the
+# 147x147 / 149x149 stem layers); a candidate of the per-shape wgrad choice (TONY_WGRAD_DIRECT=0: never)
+WGRAD_DIRECT = os.environ.get("TONY_WGRAD_DIRECT", "1") != "0"
+
+
+def wgrad_direct_supported(c, co, r, s, sh, sw) -> bool:
+    return c in (32, 64) and co in (32, 64) and (r, s) == (3, 3) and (sh, sw) == (1, 1)
+
+
+def _wgrad_direct(dy, lddy, x, ldx, co, ph, pw, dst=None):
+    """dW of a 3x3 stride-1 conv by the direct kernel: [Co][3][3][C] fp32 partials per workgroup,
+    summed by tony_splitk_reduce into ``dst`` (added; returns None) or a new fp32 tensor."""
+    n, c, h, w = x.shape
+    L, dev = _lib.lib(), x.device
+    cus = _lib.num_cus(dev)
+    nel = co * 9 * c
+    slab = torch.empty(2 * cus * nel, dtype=torch.float32, device=dev)
+    splits = ctypes.c_int(0)
+    st = _lib.stream_ptr(dev)
+    rc = L.tony_conv_wgrad_direct(dy.data_ptr(), lddy, x.data_ptr(), n, h, w, c, ldx, co, ph, pw, dy.shape[2],
+                                  dy.shape[3], slab.data_ptr(), slab.numel(), ctypes.addressof(splits), cus, st)
+    _lib.check(rc, "tony_conv_wgrad_direct")
+    out = dst if dst is not None else torch.empty(nel, dtype=torch.float32, device=dev)
+    rc = L.tony_splitk_reduce(slab.data_ptr(), splits.value, nel, out.data_ptr(), int(out.dtype == _BF16),
+                              int(dst is not None), cus, st)
+    _lib.check(rc, "tony_splitk_reduce")
+    return None if dst is not None else out
+
+
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride=1, padding=0, dst=None,
+               impl: str | None = None):
     """fp32 dW with memory [Co][R][S][Ci] (returned as a [Co, Ci, R, S] channels_last view), or, with
     ``dst`` (a gradient slot in [Co][R][S][Ci] memory order), dW added into dst (returns None).
 
@@ -287,14 +317,22 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride=1, paddin
     ntiles = -(-co // tbm) * -(-(r * s * c) // 128)
 
     def run(occ, dst_=None):
+        if occ == "direct":
+            return _wgrad_direct(dy, lddy, x, ldx, co, ph, pw, dst_)
         return splitk_combine(
             lambda slab, cap, sp, fc, fd, ff: L.tony_conv_wgrad(
                 dy.data_ptr(), lddy, x.data_ptr(), n, h, w, c, ldx, co, r, s, sh, sw, ph, pw, dy.shape[2],
                 dy.shape[3], 0, slab, cap, sp, wgrad_cus(dev, occ), fc, fd, ff, _lib.stream_ptr(dev)),
             co * r * s * c, ntiles, dev, dst_, occ)
 
-    occ = tune.pick_choice(("wgrad_occ", tuple(dy.shape), lddy, tuple(x.shape), ldx, tuple(weight_shape), sh, sw,
-                            ph, pw), WGRAD_OCC, run)
+    choices = WGRAD_OCC
+    if WGRAD_DIRECT and wgrad_direct_supported(c, co, r, s, sh, sw):
+        choices = ("direct",) + tuple(WGRAD_OCC)
+    if impl is not None:  # tests: a fixed path ("direct" or an occupancy)
+        occ = impl
+    else:
+        occ = tune.pick_choice(("wgrad_occ", tuple(dy.shape), lddy, tuple(x.shape), ldx, tuple(weight_shape), sh,
+                                sw, ph, pw), choices, run)
     out = run(occ, dst)
     return None if out is None else out.view(co, r, s, c).permute(0, 3, 1, 2)
 

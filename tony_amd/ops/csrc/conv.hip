@@ -1080,6 +1080,151 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_glds_kernel(const uint16_
                                 fold);
 }
 
+// ---- 3x3 stride-1 weight gradient with 32 / 64 channels on both sides: persistent direct kernel --
+// The implicit-GEMM wgrad (above) gathers the im2col rows of X through L2 for each of the 9 taps and,
+// with Cout = 32 / 64, runs 16-row MFMA tiles with a thin A panel: Inception's 149x149 / 147x147
+// stem layers (51 / 102 GFLOP) ran at ~100 TF/s, serialised at the very end of the backward pass.
+// Here a persistent workgroup walks 8 x 16 output-pixel tiles (b, b + grid, ...), stages the tile's
+// dY [128 px][CO] and the (8+2) x (16+2) input halo [px][CS] in LDS ONCE (the next tile's in flight
+// in registers), and computes every tap's dW_t[co][ci] = sum_px dY[px][co] X[px + t][ci] from LDS:
+// MFMA A = dY^T (co x 32 px), B = the tap-shifted halo pixels (32 px x ci), both read with the
+// transposing ds_read_b64_tr_b16 (rows = pixels).  The 9 * CS/16 (tap, ci-block) pairs are dealt to
+// the 4 waves; each pair's CO/16 accumulator blocks stay in registers over all the workgroup's tiles,
+// and the workgroup stores its [CO][9][CS] partial once (tony_splitk_reduce sums the workgroups).
+// LDS rows are CS / CO bf16 = 2 or 4 blocks of 16 columns, block b of row r at b ^ wd_swz(r): any 8
+// rows {r0..r0+3, r0+8..r0+11} a transposing read touches land on 8 distinct 32-B bank slots.
+constexpr int kWdH = 8, kWdW = 16, kWdPix = kWdH * kWdW;
+
+template <int NCB>
+__device__ __forceinline__ int wd_swz(int row) {
+  if constexpr (NCB == 2) return (row >> 3) & 1;
+  else return ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+}
+template <int C>
+__device__ __forceinline__ int wd_off(int row, int col) {  // element offset of (row, col), col % 4 == 0
+  return row * C + ((((col >> 4) ^ wd_swz<C / 16>(row))) << 4) + (col & 15);
+}
+// MFMA operand of 8 consecutive LDS rows (row0 + 0..7 of this lane's k-group) x 16 columns
+template <int C>
+__device__ __forceinline__ bf16x8_t wd_frag(const uint16_t* lds, int row0, int col0, int lane) {
+  const int q = (lane & 15) >> 2, p = lane & 3;
+  const int col = col0 + 4 * p;
+  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(lds + wd_off<C>(row0 + q, col)));
+  v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(lds + wd_off<C>(row0 + 4 + q, col)));
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  v8i16 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, r);
+}
+
+template <int CS, int CO>
+struct WdCfg {
+  static constexpr int HH = kWdH + 2, HW = kWdW + 2;
+  static constexpr int HALO = HH * HW * CS;         // elements
+  static constexpr int DYT = kWdPix * CO;
+  static constexpr int HV = (HH * HW * CS / 8 + kThreads - 1) / kThreads;  // 16-B chunks per thread
+  static constexpr int DV = kWdPix * CO / 8 / kThreads;
+  static constexpr int NP = 9 * (CS / 16);          // (tap, ci block) pairs
+  static constexpr int PPW = (NP + 3) / 4;          // pairs per wave
+  static constexpr int CB = CO / 16;
+};
+
+template <int CS, int CO>
+__global__ __launch_bounds__(kThreads) void conv_wgrad_direct_kernel(const uint16_t* __restrict__ dY, int64_t lddy,
+                                                                     Gather g, float* __restrict__ slab,
+                                                                     int tiles_x, int tiles_y, int ntiles) {
+  using D = WdCfg<CS, CO>;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[D::HALO + D::DYT];
+  uint16_t* halo = smem;
+  uint16_t* dyl = smem + D::HALO;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kq = lane >> 4;
+
+  f32x4 acc[D::PPW][D::CB];
+#pragma unroll
+  for (int i = 0; i < D::PPW; ++i)
+#pragma unroll
+    for (int j = 0; j < D::CB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 hv[D::HV], dv[D::DV];
+  auto fetch = [&](int tile) {
+    const int tx = tile % tiles_x, rest = tile / tiles_x;
+    const int ty = rest % tiles_y, img = rest / tiles_y;
+    const int oy0 = ty * kWdH, ox0 = tx * kWdW;
+#pragma unroll
+    for (int i = 0; i < D::HV; ++i) {
+      const int v = threadIdx.x + i * kThreads;
+      const int hp = v / (CS / 8), c8 = v % (CS / 8);
+      const int hy = hp / D::HW, hx = hp - hy * D::HW;
+      const int iy = oy0 + hy + g.offh, ix = ox0 + hx + g.offw;
+      hv[i] = (hp < D::HH * D::HW && static_cast<unsigned>(iy) < static_cast<unsigned>(g.Hs) &&
+               static_cast<unsigned>(ix) < static_cast<unsigned>(g.Ws))
+                  ? *reinterpret_cast<const uint4*>(
+                        g.src + ((static_cast<int64_t>(img) * g.Hs + iy) * g.Ws + ix) * g.ld + c8 * 8)
+                  : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int i = 0; i < D::DV; ++i) {
+      const int v = threadIdx.x + i * kThreads;
+      const int px = v / (CO / 8), c8 = v % (CO / 8);
+      const int oy = oy0 + px / kWdW, ox = ox0 + px % kWdW;
+      dv[i] = (oy < g.OH && ox < g.OW)
+                  ? *reinterpret_cast<const uint4*>(
+                        dY + ((static_cast<int64_t>(img) * g.OH + oy) * g.OW + ox) * lddy + c8 * 8)
+                  : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+
+  if (static_cast<int>(blockIdx.x) < ntiles) fetch(blockIdx.x);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    __syncthreads();  // every wave is done with the previous tile's LDS
+#pragma unroll
+    for (int i = 0; i < D::HV; ++i) {
+      const int v = threadIdx.x + i * kThreads;
+      const int hp = v / (CS / 8), c8 = v % (CS / 8);
+      if (hp < D::HH * D::HW) *reinterpret_cast<uint4*>(halo + wd_off<CS>(hp, c8 * 8)) = hv[i];
+    }
+#pragma unroll
+    for (int i = 0; i < D::DV; ++i) {
+      const int v = threadIdx.x + i * kThreads;
+      *reinterpret_cast<uint4*>(dyl + wd_off<CO>(v / (CO / 8), (v % (CO / 8)) * 8)) = dv[i];
+    }
+    __syncthreads();
+    if (tile + static_cast<int>(gridDim.x) < ntiles) fetch(tile + gridDim.x);
+#pragma unroll
+    for (int ks = 0; ks < kWdPix / 32; ++ks) {
+      const int p0 = ks * 32 + kq * 8;       // this lane's 8 pixels: one half row of the tile
+      const int py = p0 / kWdW, px = p0 % kWdW;
+      bf16x8_t af[D::CB];
+#pragma unroll
+      for (int i = 0; i < D::CB; ++i) af[i] = wd_frag<CO>(dyl, p0, i * 16, lane);
+#pragma unroll
+      for (int pp = 0; pp < D::PPW; ++pp) {
+        const int pair = wave + 4 * pp;
+        if (pair >= D::NP) break;  // wave-uniform
+        const int t = pair / (CS / 16), j = pair % (CS / 16);
+        const int r = t / 3, sx = t - r * 3;
+        const bf16x8_t bfr = wd_frag<CS>(halo, (py + r) * D::HW + px + sx, j * 16, lane);
+#pragma unroll
+        for (int i = 0; i < D::CB; ++i) acc[pp][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[pp][i], 0, 0, 0);
+      }
+    }
+  }
+  // this workgroup's partial dW [CO][9][CS] (every (tap, ci block, co block) has one owner wave)
+  constexpr int K = 9 * CS;
+  float* out = slab + static_cast<int64_t>(blockIdx.x) * CO * K;
+#pragma unroll
+  for (int pp = 0; pp < D::PPW; ++pp) {
+    const int pair = wave + 4 * pp;
+    if (pair >= D::NP) break;
+    const int t = pair / (CS / 16), j = pair % (CS / 16);
+#pragma unroll
+    for (int i = 0; i < D::CB; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        out[static_cast<int64_t>(i * 16 + kq * 4 + rr) * K + t * CS + j * 16 + (lane & 15)] = acc[pp][i][rr];
+  }
+}
+
 bool wgrad_glds_enabled() {
   static const bool on = [] {
     const char* e = getenv("TONY_WGRAD_GLDS");
@@ -1243,4 +1388,40 @@ TONY_API int tony_conv_wgrad(const void* dy, int64_t lddy, const void* x, int N,
   if (Co <= 32) return launch_wgrad<32>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream);
   if (Co <= 64) return launch_wgrad<64>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream);
   return launch_wgrad<128>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream);
+}
+
+// dW (fp32 partials, [grid][Co][3][3][C]) of a 3x3 stride-1 conv with C, Co in {32, 64} by the
+// persistent direct kernel; *splits = the workgroup count (tony_splitk_reduce sums them).  -3: the
+// shape is not one it takes.
+TONY_API int tony_conv_wgrad_direct(const void* dy, int64_t lddy, const void* x, int N, int H, int W, int C,
+                                    int64_t ldx, int Co, int ph, int pw, int OH, int OW, float* slab,
+                                    int64_t slab_cap, int* splits, int num_cus, hipStream_t stream) {
+  if (bad_geom(C, ldx, x) || (lddy % 8) || (reinterpret_cast<uintptr_t>(dy) & 15) || slab == nullptr) return -1;
+  if ((C != 32 && C != 64) || (Co != 32 && Co != 64) || ph < 0 || pw < 0 || ph > 2 || pw > 2) return -3;
+  if (OH != H + 2 * ph - 2 || OW != W + 2 * pw - 2 || OH <= 0 || OW <= 0) return -1;
+  if (static_cast<int64_t>(N) * H * W > 0x7fffffff || static_cast<int64_t>(N) * OH * OW > 0x7fffffff) return -1;
+  Gather g{static_cast<const uint16_t*>(x), ldx, H, W, C, OH, OW, 3, 3, 1, 1, -ph, -pw, 1, 9 * C, N};
+  const int tiles_x = ceil_div(OW, kWdW), tiles_y = ceil_div(OH, kWdH);
+  const int64_t nt = static_cast<int64_t>(N) * tiles_x * tiles_y;
+  if (nt > 0x7fffffff) return -1;
+  const auto launch = [&](auto cs, auto co) -> int {
+    constexpr int CS = decltype(cs)::value, CO = decltype(co)::value;
+    const void* fn = reinterpret_cast<const void*>(&conv_wgrad_direct_kernel<CS, CO>);
+    static int per_cu = 0;  // per instance: resident workgroups per CU
+    if (per_cu == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kThreads, 0) != hipSuccess ||
+                        per_cu <= 0))
+      per_cu = 1;
+    const int grid = static_cast<int>(std::min<int64_t>(nt, static_cast<int64_t>(std::min(per_cu, 2)) *
+                                                                (num_cus > 0 ? num_cus : 256)));
+    if (static_cast<int64_t>(grid) * CO * 9 * CS > slab_cap) return -4;
+    conv_wgrad_direct_kernel<CS, CO><<<grid, kThreads, 0, stream>>>(static_cast<const uint16_t*>(dy), lddy, g, slab,
+                                                                    tiles_x, tiles_y, static_cast<int>(nt));
+    TONY_LAUNCH_CHECK();
+    *splits = grid;
+    return 0;
+  };
+  using I32 = std::integral_constant<int, 32>;
+  using I64 = std::integral_constant<int, 64>;
+  if (C == 32) return Co == 32 ? launch(I32{}, I32{}) : launch(I32{}, I64{});
+  return Co == 32 ? launch(I64{}, I32{}) : launch(I64{}, I64{});
 }

@@ -163,12 +163,25 @@ def _flush(side: torch.cuda.Stream) -> None:
         torch.cuda.set_stream(cur)
 
 
+# The last TAIL weight gradients of a backward pass run on the current stream instead.  The
+# backward ends with the stem layers (147x147 / 149x149 maps: the largest wgrads of the step) while
+# the data-gradient chain has almost nothing left to do; queued behind the side stream's backlog
+# they would run alone after it, with the compute stream idle until the join.  The count is taken
+# from the previous step (the backward order is fixed); TONY_WGRAD_TAIL=0 keeps all on the side.
+TAIL = int(os.environ.get("TONY_WGRAD_TAIL", "0"))
+_tail_from = [-1]  # index of the first weight gradient of a step that runs inline (-1: none)
+
+
 def run(fn: Callable[[], object], *keep: torch.Tensor):
     """Run ``fn`` (which must write its result in place and return None) on the side stream when one
     is active -- possibly deferred to the next batch flush or ``end()`` -- else right here.  ``keep``:
     tensors ``fn`` reads that the caller may drop."""
     side = _active[0]
     if side is None:
+        return fn()
+    if 0 <= _tail_from[0] <= _issued[0]:  # the step's tail: on the current stream
+        with _lock:
+            _issued[0] += 1
         return fn()
     with _lock:
         _pending.append(fn)
@@ -211,4 +224,5 @@ def end() -> int:
     with _lock:
         _keep.clear()
         n, _issued[0] = _issued[0], 0
+    _tail_from[0] = n - TAIL if 0 < TAIL < n else -1
     return n
