@@ -287,15 +287,17 @@ def main():
     # untimed: GPU time per step with the host far ahead (a spin kernel holds the GPU while the host
     # enqueues the steps): equal to ms_per_step when the step is GPU-bound, lower when host launch
     # overhead leaves the GPU waiting
-    gpu_ahead = None
+    gpu_ahead = host_free = None
     if world == 1 and trainer.use_graph is False:
         n_ahead = 6
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda._sleep(int(2.4e6 * 16 * n_ahead))  # ~2.4 GHz x 16 ms x n_ahead
         e0.record()
+        th = time.perf_counter()
         for _ in range(n_ahead):
             loss = trainer.step(x, y)
+        host_free = (time.perf_counter() - th) / n_ahead  # issue cost while the GPU is still spinning
         e1.record()
         e1.synchronize()
         gpu_ahead = round(e0.elapsed_time(e1) / n_ahead, 3)
@@ -361,6 +363,7 @@ def main():
                     dict(zip(("forward", "backward", "exposed_ps_push_apply_pull"), [round(v, 3) for v in phases])),
                 "host_ms_per_step": round(1000.0 * host / args.steps, 3),
                 "gpu_ms_per_step_host_ahead": gpu_ahead,
+                "host_ms_per_step_unblocked": None if host_free is None else round(1000.0 * host_free, 3),
                 "host_fwd_bwd_ms_last_eager_step": [round(1000.0 * trainer.host_fwd_s, 3),
                                                     round(1000.0 * trainer.host_bwd_s, 3)],
                 "kernels": "tony_amd HIP" if fused else "stock PyTorch-ROCm (MIOpen / hipBLASLt)",

@@ -121,7 +121,10 @@ def active() -> bool:
 # Work is handed to the side stream in batches of BATCH ops: one fork (event record + stream wait,
 # ~10 us of host time) and one stream switch per batch instead of per op.  A batch forks from the
 # current stream's position at flush time -- later than each op needs, never earlier.
-BATCH = int(os.environ.get("TONY_WGRAD_BATCH", "1"))  # measured: 1 (16.34 ms) beats 4 (16.77 ms)
+# Measured: 1 (16.34 ms) beat 4 (16.77 ms) while the step was GPU-bound at 16 ms (round 1); with the
+# GPU at 14 ms the host issue cost matters: 2 measured 13.90 / 13.89 ms/step vs 14.1-15.1 at 1
+# (profiles/r2s3_host_levers_ab.log)
+BATCH = int(os.environ.get("TONY_WGRAD_BATCH", "2"))
 _pending: List[Callable[[], object]] = []
 
 
