@@ -22,7 +22,8 @@ from torch import nn
 
 from ..ops.concat import Slot, assemble, concat_buffer
 from ..ops.pool import avg_pool, avg_pool3x3_s1, global_avg_pool, max_pool
-from ..ops import streams
+from ..ops import conv as conv_ops
+from ..ops import streams, tape
 from ..ops.fused import FusedHead
 from ..ops.linear import Linear
 from .layers import ConvBNAct, conv_bn_act_maxpool, init_weights
@@ -238,18 +239,44 @@ class InceptionV3(nn.Module):
         self.fc = (Linear if fused else nn.Linear)(2048, num_classes)
         self.fused = fused
 
-    def forward(self, x):
-        # stem: the last conv of each group feeds a 3x3/2 max pool; fused training runs BN + ReLU + pool
-        # as one kernel there (models/layers.py conv_bn_act_maxpool)
+    def _stem_fwd(self, x):
+        # the last conv of each group feeds a 3x3/2 max pool; fused training runs BN + ReLU + pool as
+        # one kernel there (models/layers.py conv_bn_act_maxpool)
         for m in self.stem[:-1]:
             x = m(x)
         x = conv_bn_act_maxpool(self.stem[-1], x, 3, 2)
         for m in self.stem2[:-1]:
             x = m(x)
-        x = conv_bn_act_maxpool(self.stem2[-1], x, 3, 2)
-        x = self.mixed_6(self.mixed_6a(self.mixed_5(x)))
-        aux = self.aux(x) if (self.aux is not None and self.training) else None
-        x = self.mixed_7(x)
+        return conv_bn_act_maxpool(self.stem2[-1], x, 3, 2)
+
+    def _segments(self):
+        """(callable, params) per tape segment: the stem, then every Inception block (ops/tape.py)."""
+        segs = getattr(self, "_tape_segs", None)
+        if segs is None:
+            stem = (self.stem, self.stem2)
+            segs = [(self._stem_fwd, [p for m in stem for p in m.parameters()], [b for m in stem for b in m.buffers()])]
+            for blk in (*self.mixed_5, self.mixed_6a, *self.mixed_6):
+                segs.append((blk, list(blk.parameters()), list(blk.buffers())))
+            tail = [(blk, list(blk.parameters()), list(blk.buffers())) for blk in self.mixed_7]
+            segs = self._tape_segs = (segs, tail)
+        return segs
+
+    def forward(self, x):
+        # tape segments need every op of a block on the tony kernels: the 8x8 convs are at batch >= 32
+        if (self.fused and self.training and x.is_cuda and tape.ENABLED and torch.is_grad_enabled()
+                and x.shape[0] * 64 >= conv_ops.MIN_ROWS):
+            # each block = one autograd node replaying its ops' backward from a tape (ops/tape.py)
+            head, tail = self._segments()
+            for run, params, bufs in head:
+                x = tape.segment(run, x, params, bufs)
+            aux = self.aux(x) if self.aux is not None else None
+            for run, params, bufs in tail:
+                x = tape.segment(run, x, params, bufs)
+        else:
+            x = self._stem_fwd(x)
+            x = self.mixed_6(self.mixed_6a(self.mixed_5(x)))
+            aux = self.aux(x) if (self.aux is not None and self.training) else None
+            x = self.mixed_7(x)
         x = global_avg_pool(x) if self.fused else torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1)
         logits = self.fc(self.dropout(x))
         return (logits, aux) if aux is not None else logits

@@ -14,6 +14,7 @@ from torch import nn
 import os
 
 from ..ops import conv as conv_ops
+from ..ops import tape
 from ..ops.bn import BatchNormAct2d
 from ..ops.fused import _HeadFn
 
@@ -54,7 +55,7 @@ class ConvBNAct(nn.Module):
         if self.fused and self.is_1x1 and self.bn.relu and x.is_cuda:
             # MFMA GEMM with BN statistics in its epilogue + fused apply (ops/fused.py)
             bn = self.bn
-            return _HeadFn.apply(x, self.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+            return tape.apply(_HeadFn, x, self.conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                  (self.conv.out_channels,), 0, self.training, bn.momentum, bn.eps,
                                  (slot,) if slot is not None else None)[0]
         if self.fused and x.is_cuda and USE_TONY_CONV and (
@@ -80,7 +81,8 @@ def conv_bn_act_maxpool(layer: "ConvBNAct", x, k: int = 3, s: int = 2):
 
     c, bn = layer.conv, layer.bn
     if (layer.fused and layer.training and x.is_cuda and bn.relu and not layer.is_1x1 and USE_TONY_CONV
-            and torch.is_grad_enabled() and conv_ops.supported(x, c.weight, c.stride, c.padding)):
+            and (torch.is_grad_enabled() or tape.recording())
+            and conv_ops.supported(x, c.weight, c.stride, c.padding)):
         return conv_ops.conv_bn_act_pool(x, c.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, c.stride,
                                          c.padding, bn.momentum, bn.eps, k, s)
     y = layer(x)

@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import torch
 
-from . import _lib
+from . import _lib, tape
 from .arena import zeros_f32
 
 
@@ -123,7 +123,7 @@ def bn_act(x, weight, bias, running_mean, running_var, training=True, momentum=0
     if x.is_cuda:
         if x.dtype != torch.bfloat16:
             raise TypeError(f"bn_act HIP kernel takes bf16 activations, got {x.dtype}")
-        return _BNActFn.apply(x, weight, bias, running_mean, running_var, training, momentum, eps, relu)
+        return tape.apply(_BNActFn, x, weight, bias, running_mean, running_var, training, momentum, eps, relu)
     return bn_act_reference(x, weight, bias, running_mean, running_var, training, momentum, eps, relu)
 
 

@@ -19,6 +19,8 @@ from typing import Optional, Sequence
 
 import torch
 
+from . import tape
+
 
 class Slot:
     """Channel slice [c0, c0 + c) of a channels_last concat buffer, as a destination for a kernel."""
@@ -78,4 +80,4 @@ class _AssembleFn(torch.autograd.Function):
 
 def assemble(buf: torch.Tensor, parts: Sequence[torch.Tensor]) -> torch.Tensor:
     """The block output ``buf`` (= cat(parts, 1)), with the parts already written into it in place."""
-    return _AssembleFn.apply(Slot(buf, 0), *parts)
+    return tape.apply(_AssembleFn, Slot(buf, 0), *parts)

@@ -25,7 +25,7 @@ from typing import Callable, Dict, Tuple
 
 import torch
 
-from . import _lib, concat, streams, tune, wt_cache
+from . import _lib, concat, streams, tape, tune, wt_cache
 from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 from .gemm import WGRAD_OCC, splitk_combine, wgrad_cus, wgrad_tn
@@ -567,7 +567,7 @@ class _ConvFn(torch.autograd.Function):
 
 def conv2d(x, weight, stride=1, padding=0):
     if supported(x, weight, stride, padding):
-        return _ConvFn.apply(x, weight, _pair(stride), _pair(padding))
+        return tape.apply(_ConvFn, x, weight, _pair(stride), _pair(padding))
     if x.is_cuda:
         _record_unsupported("fwd", x.shape, weight.shape, stride, padding)
     return torch.nn.functional.conv2d(x, weight, None, stride, padding)
@@ -713,7 +713,7 @@ class _ConvBNActPoolFn(torch.autograd.Function):
 def conv_bn_act_pool(x, weight, gamma, beta, running_mean, running_var, stride=1, padding=0, momentum=0.1,
                      eps=1e-3, k=3, s=2):
     """max_pool2d(relu(batch_norm(conv2d(x))), k, s) in training mode, fused (see _ConvBNActPoolFn)."""
-    return _ConvBNActPoolFn.apply(x, weight, gamma, beta, running_mean, running_var, _pair(stride), _pair(padding),
+    return tape.apply(_ConvBNActPoolFn, x, weight, gamma, beta, running_mean, running_var, _pair(stride), _pair(padding),
                                   momentum, eps, k, s)
 
 
@@ -721,7 +721,7 @@ def conv_bn_act(x, weight, gamma, beta, running_mean, running_var, stride=1, pad
                 momentum=0.1, eps=1e-3, relu=True, slot=None):
     """relu(bn(conv(x))); with a ``concat.Slot`` the result is written into that channel slice."""
     if supported(x, weight, stride, padding) or (STEM and stem_supported(x, weight, stride, padding)):
-        return _ConvBNActFn.apply(x, weight, gamma, beta, running_mean, running_var, _pair(stride), _pair(padding),
+        return tape.apply(_ConvBNActFn, x, weight, gamma, beta, running_mean, running_var, _pair(stride), _pair(padding),
                                   training, momentum, eps, relu, slot)
     if x.is_cuda:
         _record_unsupported("fwd", x.shape, weight.shape, stride, padding)

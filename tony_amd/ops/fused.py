@@ -33,7 +33,7 @@ from typing import Sequence
 import torch
 from torch import nn
 
-from . import _lib, concat, streams, tune, wt_cache
+from . import _lib, concat, streams, tape, tune, wt_cache
 from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 from .gemm import wgrad_tn
@@ -282,5 +282,5 @@ class FusedHead(nn.Module):
         if x.is_cuda:
             if x.dtype != _BF16:
                 raise TypeError("FusedHead HIP path takes bf16 activations")
-            return _HeadFn.apply(*args, tuple(slots) if slots else None)
+            return tape.apply(_HeadFn, *args, tuple(slots) if slots else None)
         return head_reference(*args)

@@ -14,7 +14,7 @@ import os
 
 import torch
 
-from . import _lib, tune
+from . import _lib, tape, tune
 from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 
@@ -167,5 +167,5 @@ def conv1x1(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     if x.is_cuda:
         if x.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16:
             raise TypeError("conv1x1 MFMA path takes bf16 activations and weights")
-        return _Conv1x1Fn.apply(x, weight)
+        return tape.apply(_Conv1x1Fn, x, weight)
     return torch.nn.functional.conv2d(x, weight)

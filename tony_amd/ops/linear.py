@@ -19,7 +19,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
-from . import _lib
+from . import _lib, tape
 from .gemm import wgrad_tn
 
 _BF16 = torch.bfloat16
@@ -97,7 +97,7 @@ class _LinearFn(torch.autograd.Function):
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
     """``F.linear`` on the MFMA GEMMs when ``supported``, else PyTorch's."""
     if supported(x, weight):
-        return _LinearFn.apply(x, weight, bias)
+        return tape.apply(_LinearFn, x, weight, bias)
     return nn.functional.linear(x, weight, bias)
 
 

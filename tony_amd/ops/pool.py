@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import torch
 
-from . import _lib, concat, streams
+from . import _lib, concat, streams, tape
 from .bn import _as_rows, _rows_view
 
 
@@ -90,7 +90,7 @@ class _AvgPoolFn(torch.autograd.Function):
 def avg_pool(x: torch.Tensor, k: int, s: int) -> torch.Tensor:
     """avg_pool2d(x, k, s) (no padding) on channels_last bf16; k = H = W is the global average pool."""
     if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0:
-        return _AvgPoolFn.apply(x, k, s)
+        return tape.apply(_AvgPoolFn, x, k, s)
     return torch.nn.functional.avg_pool2d(x, k, s)
 
 
@@ -104,12 +104,12 @@ def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
 def avg_pool3x3_s1(x: torch.Tensor) -> torch.Tensor:
     """avg_pool2d(x, 3, 1, 1, count_include_pad=True) on channels_last bf16."""
     if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0:
-        return _AvgPool3Fn.apply(x)
+        return tape.apply(_AvgPool3Fn, x)
     return torch.nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=True)
 
 
 def max_pool(x: torch.Tensor, k: int = 3, s: int = 2, slot=None) -> torch.Tensor:
     """max_pool2d(x, k, s) (no padding) on channels_last bf16 (into a concat.Slot when given)."""
     if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0:
-        return _MaxPoolFn.apply(x, k, s, slot)
+        return tape.apply(_MaxPoolFn, x, k, s, slot)
     return torch.nn.functional.max_pool2d(x, k, s)

@@ -17,7 +17,7 @@ from __future__ import annotations
 
 import torch
 
-from . import _lib, streams, tune, wt_cache
+from . import _lib, streams, tape, tune, wt_cache
 from .arena import zeros_f32
 from .bn import _as_rows, _empty_like_rows, _rows_view
 from .fused import _cl_empty
@@ -165,7 +165,7 @@ def bn_add_relu(z, res, gamma, beta, running_mean, running_var, training=True, m
     if z.is_cuda:
         if z.dtype != _BF16:
             raise TypeError("bn_add_relu HIP kernel takes bf16 activations")
-        return _BNAddReLUFn.apply(z, res, gamma, beta, running_mean, running_var, training, momentum, eps)
+        return tape.apply(_BNAddReLUFn, z, res, gamma, beta, running_mean, running_var, training, momentum, eps)
     return bn_add_relu_reference(z, res, gamma, beta, running_mean, running_var, training, momentum, eps)
 
 
@@ -174,7 +174,7 @@ def conv1x1_bn_add_relu(x, weight, res, gamma, beta, running_mean, running_var, 
     if x.is_cuda:
         if x.dtype != _BF16:
             raise TypeError("conv1x1_bn_add_relu HIP path takes bf16 activations")
-        return _Conv1x1BNAddReLUFn.apply(x, weight, res, gamma, beta, running_mean, running_var, training, momentum,
+        return tape.apply(_Conv1x1BNAddReLUFn, x, weight, res, gamma, beta, running_mean, running_var, training, momentum,
                                          eps)
     z = torch.nn.functional.conv2d(x, weight)
     return bn_add_relu_reference(z, res, gamma, beta, running_mean, running_var, training, momentum, eps)
