@@ -191,6 +191,10 @@ def main():
     model = model.to(dev).to(memory_format=torch.channels_last)
     model.train()
     ps_kw = {} if args.bucket_mb is None else {"bucket_mb": args.bucket_mb}
+    if os.environ.get("TONY_BUCKETED_SINGLE", "0") == "1":
+        # one rank: the bucket engine applies each bucket as soon as backward has written it (the
+        # optimizer overlaps the backward tail) instead of one apply after the join
+        ps_kw["bucketed_single"] = True
     ps = ParameterServer(model, optimizer=args.optimizer, lr=0.045 if args.model == "inception_v3" else 0.1,
                          momentum=0.9, weight_decay=4e-5, mode=args.ps_mode, ps_ranks=(0,), dtype=dtype, device=dev,
                          wire_dtype=grad_dtype, **ps_kw)

@@ -16,6 +16,8 @@
 // Thread map: one 16-byte (8-channel) vector per lane; a 256-thread workgroup
 // covers RPI = 256/(C/8) rows per iteration, so a wavefront always reads a
 // contiguous 1 KiB span of the row-major image (fully coalesced for any C%8==0).
+#include <algorithm>
+
 #include "common.h"
 
 using namespace tony;
@@ -24,6 +26,15 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kMaxC = 2048;
+// Per-channel tables and block reductions live in dynamic LDS sized to the layer's C (not kMaxC):
+// a 17x17 / 35x35 layer's BN kernel then takes ~1-16 KB instead of 16-40 KB, so it co-resides with
+// the LDS-heavy MFMA kernels of the other streams (wgrad 144 KB per CU) and runs at full occupancy.
+extern __shared__ __attribute__((aligned(16))) float bn_dyn[];
+inline size_t bn_lds_table(int C, int rows) { return static_cast<size_t>(rows) * C * sizeof(float); }
+inline size_t bn_lds_reduce(int C) {  // block_reduce_add: [2][RPI][C]
+  return static_cast<size_t>(2) * (kThreads / (C / 8)) * C * sizeof(float);
+}
+inline size_t bn_lds_bred(int C) { return std::max(bn_lds_table(C, 4), bn_lds_reduce(C)); }
 
 struct RowMap {
   int CG, RPI, cg, rsub;
@@ -81,7 +92,7 @@ __device__ __forceinline__ void block_reduce_add(float* red, const RowMap& rm, i
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       red[rm.rsub * C + rm.cg * 8 + j] = a[j];
-      red[kMaxC + rm.rsub * C + rm.cg * 8 + j] = b[j];
+      red[rm.RPI * C + rm.rsub * C + rm.cg * 8 + j] = b[j];
     }
   }
   __syncthreads();
@@ -89,7 +100,7 @@ __device__ __forceinline__ void block_reduce_add(float* red, const RowMap& rm, i
     float sa = 0.f, sb = 0.f;
     for (int k = 0; k < rm.RPI; ++k) {
       sa += red[k * C + c];
-      sb += red[kMaxC + k * C + c];
+      sb += red[rm.RPI * C + k * C + c];
     }
     atomicAdd(out_a + c, sa);
     atomicAdd(out_b + c, sb);
@@ -99,7 +110,7 @@ __device__ __forceinline__ void block_reduce_add(float* red, const RowMap& rm, i
 __global__ __launch_bounds__(kThreads) void bn_fwd_stats_kernel(
     const uint16_t* __restrict__ x, int64_t M, int C, int64_t ldx, int64_t rows_per_block,
     float* __restrict__ sum, float* __restrict__ sumsq, int64_t sstride) {
-  __shared__ float red[kMaxC * 2];
+  float* red = bn_dyn;  // bn_lds_reduce(C) bytes
   RowMap rm(C);
   float s[8], q[8];
 #pragma unroll
@@ -150,8 +161,8 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
     int64_t sstride, const void* gamma, const void* beta, int param_bf16, float eps, int relu, int mode,
     float* __restrict__ save_mean, float* __restrict__ save_invstd,
     float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, Segs segs) {
-  __shared__ float scale[kMaxC];
-  __shared__ float shift[kMaxC];
+  float* scale = bn_dyn;  // [C] then shift [C]: bn_lds_table(C, 2) bytes
+  float* shift = bn_dyn + C;
   const float inv_m = 1.f / static_cast<float>(M);
   for (int c = threadIdx.x; c < C; c += kThreads) {
     float mean, invstd;
@@ -232,14 +243,14 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     int64_t M, int C, int64_t rows_per_block, const float* __restrict__ mean,
     const float* __restrict__ invstd, const void* gamma, const void* beta, int param_bf16,
     int relu, float* __restrict__ dsum, float* __restrict__ dsumx, int64_t sstride, Segs segs) {
-  __shared__ float red[kMaxC * 4];  // coefficient table [4][C] first, then the block reduction
+  float* red = bn_dyn;  // coefficient table [4][C] first, then the block reduction (bn_lds_bred)
   for (int c = threadIdx.x; c < C; c += kThreads) {
     const float mu = mean[c], is = invstd[c];
     const float g = load_param(gamma, c, param_bf16, 1.f), be = load_param(beta, c, param_bf16, 0.f);
     red[c] = is;
-    red[kMaxC + c] = -mu * is;
-    red[2 * kMaxC + c] = g * is;
-    red[3 * kMaxC + c] = be - g * is * mu;
+    red[C + c] = -mu * is;
+    red[2 * C + c] = g * is;
+    red[3 * C + c] = be - g * is * mu;
   }
   __syncthreads();
   RowMap rm(C);
@@ -250,9 +261,9 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     a[j] = b[j] = 0.f;
     const int c = (rm.active ? rm.cg * 8 : 0) + j;
     p0[j] = red[c];
-    p1[j] = red[kMaxC + c];
-    p2[j] = red[2 * kMaxC + c];
-    p3[j] = red[3 * kMaxC + c];
+    p1[j] = red[C + c];
+    p2[j] = red[2 * C + c];
+    p3[j] = red[3 * C + c];
   }
   __syncthreads();  // the table is dead: red is reused by block_reduce_add
   if (rm.active) {
@@ -315,7 +326,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     const float* __restrict__ mean, const float* __restrict__ invstd, const void* gamma,
     const void* beta, int param_bf16, int relu, const float* __restrict__ dsum,
     const float* __restrict__ dsumx, int64_t sstride, void* dgamma, void* dbeta, int accumulate, Segs segs) {
-  __shared__ float tab[5][kMaxC];
+  float* tab = bn_dyn;  // [5][C]: bn_lds_table(C, 5) bytes
   const float inv_m = 1.f / static_cast<float>(M);
   for (int c = threadIdx.x; c < C; c += kThreads) {
     const float g = load_param(gamma, c, param_bf16, 1.f), be = load_param(beta, c, param_bf16, 0.f);
@@ -323,11 +334,11 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     const float mu = mean[c], is = invstd[c];
     const float k = g * is, am = ds * inv_m, bm = dsx * inv_m;
     // dx = k*(d - am - (x - mu)*is*bm)
-    tab[0][c] = k;
-    tab[1][c] = -k * bm * is;
-    tab[2][c] = k * (bm * is * mu - am);
-    tab[3][c] = k;               // pre-activation = x*k + (be - k*mu)
-    tab[4][c] = be - k * mu;
+    tab[0 * C + c] = k;
+    tab[1 * C + c] = -k * bm * is;
+    tab[2 * C + c] = k * (bm * is * mu - am);
+    tab[3 * C + c] = k;               // pre-activation = x*k + (be - k*mu)
+    tab[4 * C + c] = be - k * mu;
     if (blockIdx.x == 0) {
       store_param(dbeta, c, param_bf16, ds, accumulate);
       store_param(dgamma, c, param_bf16, dsx, accumulate);
@@ -340,11 +351,11 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = rm.cg * 8 + j;
-    q0[j] = tab[0][c];
-    q1[j] = tab[1][c];
-    q2[j] = tab[2][c];
-    q3[j] = tab[3][c];
-    q4[j] = tab[4][c];
+    q0[j] = tab[0 * C + c];
+    q1[j] = tab[1 * C + c];
+    q2[j] = tab[2 * C + c];
+    q3[j] = tab[3 * C + c];
+    q4[j] = tab[4 * C + c];
   }
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
   const int64_t r1 = min(M, r0 + rows_per_block);
@@ -571,8 +582,8 @@ __global__ __launch_bounds__(kThreads) void bn_relu_maxpool_kernel(
     float* __restrict__ save_mean, float* __restrict__ save_invstd, float* __restrict__ running_mean,
     float* __restrict__ running_var, float momentum, uint16_t* __restrict__ y, int64_t ldy,
     uint8_t* __restrict__ arg, int N, int H, int W, int C, int OH, int OW, int K, int S) {
-  __shared__ float scale[kMaxC];
-  __shared__ float shift[kMaxC];
+  float* scale = bn_dyn;  // [C] then shift [C]: bn_lds_table(C, 2) bytes
+  float* shift = bn_dyn + C;
   const int64_t M = static_cast<int64_t>(N) * H * W;
   const float inv_m = 1.f / static_cast<float>(M);
   for (int c = threadIdx.x; c < C; c += kThreads) {
@@ -655,7 +666,7 @@ TONY_API int tony_bn_stats(const void* x, int64_t M, int C, int64_t ldx, float* 
   int64_t rpb;
   int grid;
   plan_rows(M, C, 8, 512, &rpb, &grid);  // few WGs: C atomics per WG contend per channel
-  bn_fwd_stats_kernel<<<grid, kThreads, 0, stream>>>(static_cast<const uint16_t*>(x), M, C, ldx, rpb, sum, sumsq,
+  bn_fwd_stats_kernel<<<grid, kThreads, bn_lds_reduce(C), stream>>>(static_cast<const uint16_t*>(x), M, C, ldx, rpb, sum, sumsq,
                                                       sstride);
   TONY_LAUNCH_CHECK();
   return 0;
@@ -671,7 +682,7 @@ TONY_API int tony_bn_apply(const void* x, int64_t M, int C, int64_t ldx, void* y
   int64_t rpb;
   int grid;
   plan_rows(M, C, 4, 8192, &rpb, &grid);
-  bn_fwd_apply_kernel<false><<<grid, kThreads, 0, stream>>>(
+  bn_fwd_apply_kernel<false><<<grid, kThreads, bn_lds_table(C, 2), stream>>>(
       static_cast<const uint16_t*>(x), M, C, ldx, rpb, nullptr, 0, static_cast<uint16_t*>(y), ldy, sum, sumsq,
       sstride, gamma, beta, param_bf16, eps, relu, mode, save_mean, save_invstd, running_mean, running_var, momentum, Segs{});
   TONY_LAUNCH_CHECK();
@@ -688,7 +699,7 @@ TONY_API int tony_bn_apply_res(const void* x, int64_t M, int C, int64_t ldx, con
   int64_t rpb;
   int grid;
   plan_rows(M, C, 4, 8192, &rpb, &grid);
-  bn_fwd_apply_kernel<true><<<grid, kThreads, 0, stream>>>(
+  bn_fwd_apply_kernel<true><<<grid, kThreads, bn_lds_table(C, 2), stream>>>(
       static_cast<const uint16_t*>(x), M, C, ldx, rpb, static_cast<const uint16_t*>(res), ldr,
       static_cast<uint16_t*>(y), ldy, sum, sumsq, sstride, gamma, beta, param_bf16, eps, relu, mode, save_mean,
       save_invstd, running_mean, running_var, momentum, Segs{});
@@ -704,7 +715,7 @@ TONY_API int tony_bn_bwd_reduce(const void* x, int64_t ldx, const void* dy, int6
   int64_t rpb;
   int grid;
   plan_rows(M, C, 8, 512, &rpb, &grid, true);  // few WGs: C atomics per WG contend per channel
-  bn_bwd_reduce_kernel<false><<<grid, kThreads, 0, stream>>>(
+  bn_bwd_reduce_kernel<false><<<grid, kThreads, bn_lds_bred(C), stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, nullptr, 0, M, C, rpb, mean,
       invstd, gamma, beta, param_bf16, relu, dsum, dsumx, sstride, Segs{});
   TONY_LAUNCH_CHECK();
@@ -719,7 +730,7 @@ TONY_API int tony_bn_bwd_apply(const void* x, int64_t ldx, const void* dy, int64
   int64_t rpb;
   int grid;
   plan_rows(M, C, 4, 8192, &rpb, &grid);
-  bn_bwd_apply_kernel<false><<<grid, kThreads, 0, stream>>>(
+  bn_bwd_apply_kernel<false><<<grid, kThreads, bn_lds_table(C, 5), stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, nullptr, 0, nullptr, 0,
       static_cast<uint16_t*>(dx), lddx, M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsum, dsumx, sstride,
       dgamma, dbeta, accumulate, Segs{});
@@ -765,7 +776,7 @@ TONY_API int tony_bn_apply_segs(const void* x, int64_t M, int C, int64_t ldx, in
   int64_t rpb;
   int grid;
   plan_rows(M, C, 4, 8192, &rpb, &grid);
-  bn_fwd_apply_kernel<false><<<grid, kThreads, 0, stream>>>(
+  bn_fwd_apply_kernel<false><<<grid, kThreads, bn_lds_table(C, 2), stream>>>(
       static_cast<const uint16_t*>(x), M, C, ldx, rpb, nullptr, 0, sg.p[0], sg.ld[0], sum, sumsq, sstride, gamma, beta,
       param_bf16, eps, relu, mode, save_mean, save_invstd, running_mean, running_var, momentum, sg);
   TONY_LAUNCH_CHECK();
@@ -783,7 +794,7 @@ TONY_API int tony_bn_bwd_reduce_segs(const void* x, int64_t ldx, int n, int e0, 
   int64_t rpb;
   int grid;
   plan_rows(M, C, 8, 512, &rpb, &grid, true);
-  bn_bwd_reduce_kernel<false><<<grid, kThreads, 0, stream>>>(
+  bn_bwd_reduce_kernel<false><<<grid, kThreads, bn_lds_bred(C), stream>>>(
       static_cast<const uint16_t*>(x), ldx, sg.p[0], sg.ld[0], nullptr, 0, M, C, rpb, mean, invstd, gamma, beta,
       param_bf16, relu, dsum, dsumx, sstride, sg);
   TONY_LAUNCH_CHECK();
@@ -803,7 +814,7 @@ TONY_API int tony_bn_bwd_apply_segs(const void* x, int64_t ldx, int n, int e0, i
   int64_t rpb;
   int grid;
   plan_rows(M, C, 4, 8192, &rpb, &grid);
-  bn_bwd_apply_kernel<false><<<grid, kThreads, 0, stream>>>(
+  bn_bwd_apply_kernel<false><<<grid, kThreads, bn_lds_table(C, 5), stream>>>(
       static_cast<const uint16_t*>(x), ldx, sg.p[0], sg.ld[0], nullptr, 0, nullptr, 0, static_cast<uint16_t*>(dx),
       lddx, M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsum, dsumx, sstride, dgamma, dbeta, accumulate,
       sg);
@@ -874,12 +885,12 @@ TONY_API int tony_bn_bwd_res(const void* x, int64_t ldx, const void* dy, int64_t
   int64_t rpb;
   int grid;
   plan_rows(M, C, 8, 512, &rpb, &grid);
-  bn_bwd_reduce_kernel<true><<<grid, kThreads, 0, stream>>>(
+  bn_bwd_reduce_kernel<true><<<grid, kThreads, bn_lds_bred(C), stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, static_cast<const uint16_t*>(y),
       ldy, M, C, rpb, mean, invstd, gamma, beta, param_bf16, 1, dsums_ws, dsums_ws + C, ss, Segs{});
   TONY_LAUNCH_CHECK();
   plan_rows(M, C, 4, 8192, &rpb, &grid);
-  bn_bwd_apply_kernel<true><<<grid, kThreads, 0, stream>>>(
+  bn_bwd_apply_kernel<true><<<grid, kThreads, bn_lds_table(C, 5), stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, static_cast<const uint16_t*>(y),
       ldy, static_cast<uint16_t*>(dres), lddr, static_cast<uint16_t*>(dx), lddx, M, C, rpb, mean, invstd, gamma, beta,
       param_bf16, 1, dsums_ws, dsums_ws + C, ss, dgamma, dbeta, accumulate, Segs{});
@@ -901,7 +912,7 @@ TONY_API int tony_bn_relu_maxpool(const void* z, int64_t ldz, const float* sum, 
   int64_t work = static_cast<int64_t>(N) * OH * OW * (C / 8);
   int64_t grid = (work + kThreads - 1) / kThreads;
   if (grid > 16384) grid = 16384;
-  bn_relu_maxpool_kernel<<<static_cast<int>(grid < 1 ? 1 : grid), kThreads, 0, stream>>>(
+  bn_relu_maxpool_kernel<<<static_cast<int>(grid < 1 ? 1 : grid), kThreads, bn_lds_table(C, 2), stream>>>(
       static_cast<const uint16_t*>(z), ldz, sum, sumsq, sstride, gamma, beta, param_bf16, eps, save_mean, save_invstd,
       running_mean, running_var, momentum, static_cast<uint16_t*>(y), ldy, static_cast<uint8_t*>(argmax), N, H, W, C,
       OH, OW, K, S);

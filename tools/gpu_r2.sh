@@ -33,7 +33,7 @@ for s in "$@"; do
           python3 tools/prof_summary.py gpurun_out/prof --skip 6 > gpurun_out/prof_summary.md; find gpurun_out/prof -name '*trace*' -delete ;;
     trace) export TMPDIR=/tmp; R=$(pwd)
           step trace 900 rocprofv3 --kernel-trace -d "$R/gpurun_out/trace" -o run --output-format csv -- python3 "$R/bench.py" --steps 3 --warmup 5 --mode eager ${BENCH_ARGS:-}
-          python3 tools/step_union.py gpurun_out/trace --per-queue > gpurun_out/trace_union.txt; find gpurun_out/trace -name '*trace*.csv' -delete ;;
+          python3 tools/step_union.py gpurun_out/trace --per-queue > gpurun_out/trace_union.txt; ${KEEP_TRACE:+true} find gpurun_out/trace -name "*trace*.csv" -delete ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
   esac
 done

@@ -25,7 +25,7 @@ def classify(name):
     if "gemm_nt_kernel" in n or "gemm_tn_splitk" in n or "gemm_tn_glds" in n:
         return "tony HIP: MFMA GEMM (1x1 conv fwd/dgrad/wgrad)"
     if "conv_nt_kernel" in n or "conv_wgrad_kernel" in n or "conv_wgrad_glds" in n or "conv_halo" in n \
-            or "conv_direct_kernel" in n:
+            or "conv_direct_kernel" in n or "conv_glds_kernel" in n or "conv_wgrad_direct" in n:
         return "tony HIP: implicit-GEMM conv (fwd/dgrad/wgrad)"
     if "stem_fwd_kernel" in n or "stem_wgrad_kernel" in n:
         return "tony HIP: MFMA image-stem conv (fwd/wgrad)"
@@ -86,7 +86,8 @@ def main():
         return 1
     t0, t1 = opt_ends[skip - 1], opt_ends[-1]
     steps = len(opt_ends) - skip
-    win = [(s, e, n) for s, e, n in ks if s > t0 and e <= t1]
+    # the harness's spin kernels (bench.py host-ahead window, tune.time_ms) are not step work
+    win = [(s, e, n) for s, e, n in ks if s > t0 and e <= t1 and "spin_kernel" not in n]
     if "--sequence" in sys.argv:
         # one steady-state step in dispatch order: index, start offset, duration, gap to previous end
         one = [(s, e, n) for s, e, n in ks if s > opt_ends[-2] and e <= t1]
