@@ -17,6 +17,7 @@
 // covers RPI = 256/(C/8) rows per iteration, so a wavefront always reads a
 // contiguous 1 KiB span of the row-major image (fully coalesced for any C%8==0).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -569,6 +570,16 @@ void plan_rows(int64_t M, int C, int min_iters, int max_blocks, int64_t* rpb, in
 
 bool bad_c(int C) { return C <= 0 || C % 8 != 0 || C > kMaxC; }
 
+// workgroup cap of the backward reduction (TONY_BN_RED_WGS, default 512 = 2 per CU)
+int red_wgs() {
+  static const int v = [] {
+    const char* e = getenv("TONY_BN_RED_WGS");
+    const int n = e != nullptr ? atoi(e) : 0;
+    return n > 0 ? n : 512;
+  }();
+  return v;
+}
+
 // Training BN + ReLU fused with the KxK / stride-S max pool that follows it (Inception's stem:
 // conv -> BN -> ReLU -> maxpool 3x3/2 at 147x147 and 71x71).  The full-resolution activation is
 // never written: each lane normalises the 9 window inputs of its 8 channels on the fly (scale /
@@ -714,7 +725,7 @@ TONY_API int tony_bn_bwd_reduce(const void* x, int64_t ldx, const void* dy, int6
   if (bad_c(C) || (ldx % 8) || (lddy % 8) || sstride < 0) return -1;
   int64_t rpb;
   int grid;
-  plan_rows(M, C, 8, 512, &rpb, &grid, true);  // few WGs: C atomics per WG contend per channel
+  plan_rows(M, C, 8, red_wgs(), &rpb, &grid, true);  // few WGs: C atomics per WG contend per channel
   bn_bwd_reduce_kernel<false><<<grid, kThreads, bn_lds_bred(C), stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, nullptr, 0, M, C, rpb, mean,
       invstd, gamma, beta, param_bf16, relu, dsum, dsumx, sstride, Segs{});
@@ -793,7 +804,7 @@ TONY_API int tony_bn_bwd_reduce_segs(const void* x, int64_t ldx, int n, int e0, 
     return -1;
   int64_t rpb;
   int grid;
-  plan_rows(M, C, 8, 512, &rpb, &grid, true);
+  plan_rows(M, C, 8, red_wgs(), &rpb, &grid, true);
   bn_bwd_reduce_kernel<false><<<grid, kThreads, bn_lds_bred(C), stream>>>(
       static_cast<const uint16_t*>(x), ldx, sg.p[0], sg.ld[0], nullptr, 0, M, C, rpb, mean, invstd, gamma, beta,
       param_bf16, relu, dsum, dsumx, sstride, sg);
