@@ -24,6 +24,9 @@ SHAPES = [
     (2, 256, 56, 56, 512, (1, 1), 2, (0, 0)),      # ResNet downsample: odd classes get no taps (zeros)
     (2, 64, 57, 57, 64, (3, 3), 2, (1, 1)),        # odd size + padding
     (2, 32, 20, 20, 48, (5, 5), 3, (2, 2)),        # stride 3: nine classes
+    # tiny output images (OH * OW < 32 + OW): the wgrad's general row walk, not the incremental one
+    (5, 128, 5, 5, 128, (3, 3), 1, (0, 0)),
+    (3, 128, 12, 9, 160, (3, 3), 2, (1, 1)),
 ]
 
 
@@ -397,7 +400,11 @@ def test_conv_wgrad_direct(cuda, shape):
 # multiple of 64, Cin < 64 (several taps per K-step), 1x1
 GLDS_SHAPES = [(2, 64, 35, 35, 96, (3, 3), (1, 1)), (2, 48, 17, 19, 64, (5, 5), (2, 2)),
                (2, 160, 17, 17, 192, (1, 7), (0, 3)), (3, 448, 8, 8, 384, (3, 3), (1, 1)),
-               (2, 88, 13, 11, 40, (1, 1), (0, 0)), (1, 32, 9, 9, 32, (3, 3), (0, 0))]
+               (2, 88, 13, 11, 40, (1, 1), (0, 0)), (1, 32, 9, 9, 32, (3, 3), (0, 0)),
+               # channel counts that are multiples of both K-step depths (the uniform-tap loop of
+               # igemm.h: every lane crosses into the next tap at the same step) incl. a 1x1
+               (2, 64, 17, 19, 64, (5, 5), (2, 2)), (3, 128, 9, 7, 192, (1, 1), (0, 0)),
+               (2, 192, 11, 13, 128, (3, 1), (1, 0))]
 
 
 @pytest.mark.parametrize("v", range(11, 16))

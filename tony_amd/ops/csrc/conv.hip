@@ -971,11 +971,24 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __
 // `s_waitcnt vmcnt(4)` + a raw s_barrier per stage (a __syncthreads() would drain the ring).
 constexpr int kWgStages = 3;
 
-template <int TBM>
-__global__ __launch_bounds__(kThreads) void conv_wgrad_glds_kernel(const uint16_t* __restrict__ dY, int64_t lddy,
+// INC: the im2col row walk is incremental.  The general walk re-derives every row's source address
+// per stage (MRow's wrap loop + 64-bit (n * Hs * Ws + iy * Ws + ix) * ld products): ~24 quarter-rate
+// v_mul_lo_u32 / v_mad_u64_u32 per stage against 16 MFMAs, so the loop was VALU-bound.  With INC
+// each row keeps its source coordinates (ix, iy) and 32-bit element offset e; a WK-row advance adds
+// wave-uniform deltas (WkStep) -- at most one output-row carry and one image carry per stage when
+// OH * OW >= WK + OW -- and the dY rows advance by a pointer add: no multiply in the loop.
+struct WkStep {
+  int dx, dy, de;      // base advance: (WK % OW) columns, (WK / OW) rows
+  int cx, cy, ce;      // extra when the column wraps (ox >= OW)
+  int img_y, img_e;    // extra when the row wraps past the image (oy >= OH)
+};
+
+template <int TBM, bool INC>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wgrad_glds_kernel(const uint16_t* __restrict__ dY, int64_t lddy,
                                                                    Gather g, int64_t M, int Co, int tiles_n2,
                                                                    int ntiles, int64_t rows_per_split,
-                                                                   float* __restrict__ slab, SplitFold fold) {
+                                                                   float* __restrict__ slab, SplitFold fold,
+                                                                   WkStep ws) {
   constexpr int TM = TBM / 32;
   constexpr int TILE = WK * 128;           // elements per staged operand (32 rows x 256 B)
   constexpr int STAGE = 2 * TILE;          // A then B
@@ -1008,9 +1021,54 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_glds_kernel(const uint16_
   const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(smem) + (4 * wave) * 256);
   constexpr uint32_t kRow16 = 16 * 256, kStageB = STAGE * 2, kTileB = TILE * 2;
 
+  // INC state: rows r0 and r0 + 16 of the next stage
+  int ix[2], iy[2], ie[2];
+  const int xlim = g.OW * g.sw + g.offw + tp.s, ylim = g.OH * g.sh + g.offh + tp.r;  // carry thresholds
+  const uint16_t* ap = dY + (m_begin + r0) * lddy + acol;
+  int am32 = static_cast<int>(m_begin) + r0;
+  const int mend32 = static_cast<int>(m_end);
+  if constexpr (INC) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const MRow& q = mr[i];
+      ix[i] = q.ox * g.sw + g.offw + tp.s;
+      iy[i] = q.oy * g.sh + g.offh + tp.r;
+      ie[i] = ((q.n * g.Hs + iy[i]) * g.Ws + ix[i]) * static_cast<int>(g.ld) + tp.c;
+    }
+  }
+
   auto issue = [&](int slot) {
     const uint32_t As = base + slot * kStageB, Bs = As + kTileB;
     const void* z = &kZeroChunk;
+    if constexpr (INC) {
+      const int64_t row16 = 16 * lddy;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool ok = acol_ok & (am32 + 16 * i < mend32);
+        glds16(ok ? static_cast<const void*>(ap + i * row16) : z, As + i * kRow16);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool ok = kok & (am32 + 16 * i < mend32) & (static_cast<unsigned>(iy[i]) < static_cast<unsigned>(g.Hs)) &
+                        (static_cast<unsigned>(ix[i]) < static_cast<unsigned>(g.Ws));
+        glds16(ok ? static_cast<const void*>(g.src + ie[i]) : z, Bs + i * kRow16);
+        ix[i] += ws.dx;
+        iy[i] += ws.dy;
+        ie[i] += ws.de;
+        if (ix[i] >= xlim) {
+          ix[i] += ws.cx;
+          iy[i] += ws.cy;
+          ie[i] += ws.ce;
+        }
+        if (iy[i] >= ylim) {
+          iy[i] += ws.img_y;
+          ie[i] += ws.img_e;
+        }
+      }
+      am32 += WK;
+      ap += WK * lddy;
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int64_t m = am + 16 * i;
@@ -1233,6 +1291,14 @@ bool wgrad_glds_enabled() {
   return on;
 }
 
+bool wgrad_inc_enabled() {  // TONY_WGRAD_INC=0: the general row walk (A/B measurements)
+  static const bool on = [] {
+    const char* e = getenv("TONY_WGRAD_INC");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
 template <int TBM>
 int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, float* slab, int64_t slab_cap,
                  int* splits_out, int64_t M, int Co, int num_cus, const SplitFold& fold, hipStream_t stream) {
@@ -1253,10 +1319,31 @@ int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, float
   if (splits_out != nullptr) *splits_out = static_cast<int>(splits);
   // LDS-DMA staging pays for the 128-row Cout tiles only (measured: Cout <= 64 tiles, whose A rows
   // are half / quarter zero chunks, run 4-8 % slower than the register-staged kernel)
-  if (TBM == 128 && slab != nullptr && wgrad_glds_enabled())
-    conv_wgrad_glds_kernel<TBM><<<static_cast<int>(grid), kThreads, 0, stream>>>(
-        static_cast<const uint16_t*>(dy), lddy, g, M, Co, tiles_n2, ntiles, rows, slab, fold);
-  else
+  if (TBM == 128 && slab != nullptr && wgrad_glds_enabled()) {
+    // the incremental row walk needs int32 element offsets / row indices and at most one image
+    // carry per WK-row stage
+    const int64_t images = M / (static_cast<int64_t>(g.OH) * g.OW) + 1;
+    const int64_t src_elems = images * g.Hs * g.Ws * g.ld;
+    const bool inc = wgrad_inc_enabled() && src_elems < (int64_t{1} << 30) && M < (int64_t{1} << 30) &&
+                     static_cast<int64_t>(g.OH) * g.OW >= WK + g.OW;
+    WkStep ws{};
+    if (inc) {
+      const int q = WK / g.OW, rem = WK % g.OW, ld = static_cast<int>(g.ld);
+      ws.dx = rem * g.sw;
+      ws.dy = q * g.sh;
+      ws.de = (rem * g.sw + q * g.sh * g.Ws) * ld;
+      ws.cx = -g.OW * g.sw;
+      ws.cy = g.sh;
+      ws.ce = (g.sh * g.Ws - g.OW * g.sw) * ld;
+      ws.img_y = -g.OH * g.sh;
+      ws.img_e = (g.Hs - g.OH * g.sh) * g.Ws * ld;
+      conv_wgrad_glds_kernel<TBM, true><<<static_cast<int>(grid), kThreads, 0, stream>>>(
+          static_cast<const uint16_t*>(dy), lddy, g, M, Co, tiles_n2, ntiles, rows, slab, fold, ws);
+    } else {
+      conv_wgrad_glds_kernel<TBM, false><<<static_cast<int>(grid), kThreads, 0, stream>>>(
+          static_cast<const uint16_t*>(dy), lddy, g, M, Co, tiles_n2, ntiles, rows, slab, fold, ws);
+    }
+  } else
     conv_wgrad_kernel<TBM><<<static_cast<int>(grid), kThreads, 0, stream>>>(
         static_cast<const uint16_t*>(dy), lddy, g, dw, M, Co, tiles_n2, ntiles, rows, slab, fold);
   TONY_LAUNCH_CHECK();

@@ -7,6 +7,8 @@
 #pragma once
 
 #include <algorithm>
+#include <cstdlib>
+#include <tuple>
 #include <type_traits>
 
 #include "mfma_common.h"
@@ -84,6 +86,14 @@ inline Gather gemm_gather(const void* A, int64_t lda, int64_t M, int64_t K) {
 // wave with a spare instruction slot (identical bytes to the same LDS row: benign, and it keeps the
 // per-wave DMA count a compile-time constant for the vmcnt wait).
 constexpr int kGldsFirst = 11;
+// TONY_GLDS_UNI=0 in the environment keeps the general loop for every shape (A/B measurements)
+inline bool glds_uni_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("TONY_GLDS_UNI");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  return on;
+}
 struct GldsVariant {
   int bm, cap, stages, kb;
 };
@@ -110,7 +120,13 @@ __device__ __forceinline__ int goff(int row, int ch) {
   return row * KB + ((ch ^ gswz<KB>(row)) << 3);
 }
 
-template <int BM, int BN, int ST, int KB>
+// UNI (Cs % KB == 0, every Inception / ResNet layer past the stem): each lane's channel walk
+// crosses into the next filter tap at the same K-step, so the tap (r, s) is wave-uniform.  A DMA's
+// source then only moves KB channels per step (one 64-bit add; zero-fill lanes point at kZeroChunk
+// with a zero increment) and its bounds are re-derived once per tap in a scalar branch, instead of
+// the per-step TapPos walk + im2col address + bounds math: the general loop spends ~65 VALU
+// instructions per K-step against 12-24 MFMAs, more VALU issue than the MFMAs leave free.
+template <int BM, int BN, int ST, int KB, bool UNI>
 __global__ __launch_bounds__(kThreads) void conv_glds_kernel(Gather g, const uint16_t* __restrict__ B, int64_t ldb,
                                                              uint16_t* __restrict__ C, int64_t ldc, int M, int N,
                                                              float* __restrict__ stats, int64_t sstride, int epi,
@@ -173,8 +189,61 @@ __global__ __launch_bounds__(kThreads) void conv_glds_kernel(Gather g, const uin
 #pragma unroll
   for (int i = 0; i < BI; ++i) boff[i] = __builtin_amdgcn_readfirstlane(kBOff + bgrp[i] * kGroupB);
 
+  const uint16_t* zc = reinterpret_cast<const uint16_t*>(&kZeroChunk);
+  const uint16_t* ap[AI];
+  const uint16_t* bp[BI];
+  int ainc[AI], binc[BI];
+  int ur = 0, us = 0, uleft = 0;
+  auto set_tap = [&]() {  // UNI: sources of tap (ur, us) for this thread's DMAs
+    const bool tap_ok = ur < g.R;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int iy = rs[i].iy0 + g.sign * ur, ix = rs[i].ix0 + g.sign * us;
+      const bool ok = tap_ok & rs[i].ok & (static_cast<unsigned>(iy) < static_cast<unsigned>(g.Hs)) &
+                      (static_cast<unsigned>(ix) < static_cast<unsigned>(g.Ws));
+      ap[i] = ok ? g.src + (static_cast<int64_t>(rs[i].pix) + iy * g.Ws + ix) * g.ld + ck * 8 : zc;
+      ainc[i] = ok ? KB : 0;
+    }
+    if (!tap_ok) {  // K is exhausted (K = R * S * Cs): the ring's tail stages fetch zeros
+#pragma unroll
+      for (int i = 0; i < BI; ++i) {
+        bp[i] = zc;
+        binc[i] = 0;
+      }
+    }
+    uleft = g.Cs / KB;
+  };
+  if constexpr (UNI) {
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      bp[i] = bok[i] ? brow[i] + ck * 8 : zc;
+      binc[i] = bok[i] ? KB : 0;
+    }
+    set_tap();
+  }
+
   auto issue = [&](int slot) {
     const uint32_t st0 = base + slot * kStageB;
+    if constexpr (UNI) {
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        glds16(ap[i], st0 + aoff[i]);
+        ap[i] += ainc[i];
+      }
+#pragma unroll
+      for (int i = 0; i < BI; ++i) {
+        glds16(bp[i], st0 + boff[i]);
+        bp[i] += binc[i];
+      }
+      if (--uleft == 0) {
+        if (++us == g.S) {
+          us = 0;
+          ++ur;
+        }
+        set_tap();
+      }
+      return;
+    }
     const void* z = &kZeroChunk;
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
@@ -250,9 +319,12 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
       const int tiles_m = ceil_div(M, BM), tiles_n = ceil_div(N, BN);
       const int64_t tiles = static_cast<int64_t>(tiles_m) * tiles_n;
       if (tiles > 0x7fffffff) return -2;
-      conv_glds_kernel<BM, BN, ST, KB><<<static_cast<int>(tiles), kThreads, 0, stream>>>(
-          g, static_cast<const uint16_t*>(B), ldb, static_cast<uint16_t*>(C), ldc, static_cast<int>(M),
-          static_cast<int>(N), st, sstride, epi, tiles_n);
+      const auto args = std::make_tuple(g, static_cast<const uint16_t*>(B), ldb, static_cast<uint16_t*>(C), ldc,
+                                        static_cast<int>(M), static_cast<int>(N), st, sstride, epi, tiles_n);
+      if (g.Cs % KB == 0 && glds_uni_enabled())
+        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true><<<static_cast<int>(tiles), kThreads, 0, stream>>>(a...); }, args);
+      else
+        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, false><<<static_cast<int>(tiles), kThreads, 0, stream>>>(a...); }, args);
       TONY_LAUNCH_CHECK();
       return 0;
     }
