@@ -25,11 +25,11 @@ using namespace tony::mfma;
 
 namespace {
 
-__device__ __forceinline__ uint4 gather16(const Gather& g, const RowState& rs, const TapPos& t) {
+__device__ __forceinline__ uint4 gather16(const Gather& g, const RowState& rs, const TapPos& t, int toff) {
   const int iy = rs.iy0 + g.sign * t.r, ix = rs.ix0 + g.sign * t.s;
   if (rs.ok && t.r < g.R && static_cast<unsigned>(iy) < static_cast<unsigned>(g.Hs) &&
       static_cast<unsigned>(ix) < static_cast<unsigned>(g.Ws))
-    return *reinterpret_cast<const uint4*>(g.src + (static_cast<int64_t>(rs.pix) + iy * g.Ws + ix) * g.ld + t.c);
+    return *reinterpret_cast<const uint4*>(rs.base + toff);  // toff = t.off(g)
   return make_uint4(0, 0, 0, 0);
 }
 
@@ -165,14 +165,16 @@ template <int ROWS>
 __device__ __forceinline__ void load_rows_phase(uint4* regs, const uint16_t* __restrict__ B, const Phase& ph,
                                                 const Gather& g, const TapPos& t, int row0, int nrows) {
   constexpr int VEC = ROWS * BK / 8 / kThreads;
-  const int64_t ldb = static_cast<int64_t>(ph.R) * ph.S * g.Cs;
-  const int64_t koff = (static_cast<int64_t>(ph.r0 + ph.tsy * t.r) * ph.S + ph.s0 + ph.tsx * t.s) * g.Cs + t.c;
+  // 32-bit offsets (the filter has far fewer than 2^31 elements): no 64-bit products per K-step
+  const int ldb = ph.R * ph.S * g.Cs;
+  const int koff = ((ph.r0 + ph.tsy * t.r) * ph.S + ph.s0 + ph.tsx * t.s) * g.Cs + t.c;
   const bool kok = t.r < g.R;
+  const uint16_t* Bk = B + koff;
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
     const int gr = row0 + ((threadIdx.x + i * kThreads) >> 3);
     if (kok && gr < nrows)
-      regs[i] = *reinterpret_cast<const uint4*>(B + static_cast<int64_t>(gr) * ldb + koff);
+      regs[i] = *reinterpret_cast<const uint4*>(Bk + gr * ldb);
     else
       regs[i] = make_uint4(0, 0, 0, 0);
   }
@@ -209,6 +211,7 @@ __global__ __launch_bounds__(kThreads) void conv_nt_kernel(Gather g, const uint1
     rs[i].pix = n * g.Hs * g.Ws;
     rs[i].iy0 = oy * g.sh + g.offh;
     rs[i].ix0 = ox * g.sw + g.offw;
+    rs[i].set_base(g);
   }
   TapPos tp;
   tp.init((threadIdx.x & 7) * 8, g);
@@ -221,8 +224,11 @@ __global__ __launch_bounds__(kThreads) void conv_nt_kernel(Gather g, const uint1
 
   uint4 ra[AV], rb[BV];
   const int nk = (K + BK - 1) / BK;
+  {
+    const int toff = tp.off(g);
 #pragma unroll
-  for (int i = 0; i < AV; ++i) ra[i] = gather16(g, rs[i], tp);
+    for (int i = 0; i < AV; ++i) ra[i] = gather16(g, rs[i], tp, toff);
+  }
   if constexpr (PH)
     load_rows_phase<BN>(rb, B, ph, g, tp, n0, N);
   else
@@ -237,8 +243,9 @@ __global__ __launch_bounds__(kThreads) void conv_nt_kernel(Gather g, const uint1
     const bool more = kt + 1 < nk;
     if (more) {
       tp.advance(BK, g);
+      const int toff = tp.off(g);
 #pragma unroll
-      for (int i = 0; i < AV; ++i) ra[i] = gather16(g, rs[i], tp);
+      for (int i = 0; i < AV; ++i) ra[i] = gather16(g, rs[i], tp, toff);
       if constexpr (PH)
         load_rows_phase<BN>(rb, B, ph, g, tp, n0, N);
       else
@@ -816,11 +823,60 @@ struct MRow {
 // 256-B LDS rows and read with the transposing ds_read (tr_frag).
 constexpr int WK = 32;  // 64-row stages measured slower: 2x LDS + VGPRs halve the waves hiding the gather
 
-template <int TBM>
+// INC: the im2col row walk is incremental.  The general walk re-derives every row's source address
+// per stage (MRow's wrap loop + 64-bit (n * Hs * Ws + iy * Ws + ix) * ld products): ~24 quarter-rate
+// v_mul_lo_u32 / v_mad_u64_u32 per stage against 16 MFMAs, so the loop was VALU-bound.  With INC
+// each row keeps its source coordinates (ix, iy) and 32-bit element offset e; a WK-row advance adds
+// wave-uniform deltas (WkStep) -- at most one output-row carry and one image carry per stage when
+// OH * OW >= WK + OW -- and the dY rows advance by a pointer add: no multiply in the loop.
+struct WkStep {
+  int dx, dy, de;      // base advance: (WK % OW) columns, (WK / OW) rows
+  int cx, cy, ce;      // extra when the column wraps (ox >= OW)
+  int img_y, img_e;    // extra when the row wraps past the image (oy >= OH)
+};
+
+// the two rows (r, r + 16) of a WK-row stage that one thread fetches, walked incrementally
+struct IncRows {
+  int ix[2], iy[2], ie[2];  // source coordinates and element offset (pixel * ld + c) per row
+  int xlim, ylim;           // carry thresholds: ix >= xlim <=> ox >= OW, iy >= ylim <=> oy >= OH
+  __device__ __forceinline__ void init(const MRow* mr, const Gather& g, const TapPos& tp) {
+    xlim = g.OW * g.sw + g.offw + tp.s;
+    ylim = g.OH * g.sh + g.offh + tp.r;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      ix[i] = mr[i].ox * g.sw + g.offw + tp.s;
+      iy[i] = mr[i].oy * g.sh + g.offh + tp.r;
+      ie[i] = ((mr[i].n * g.Hs + iy[i]) * g.Ws + ix[i]) * static_cast<int>(g.ld) + tp.c;
+    }
+  }
+  __device__ __forceinline__ bool in_image(int i, const Gather& g) const {
+    return (static_cast<unsigned>(iy[i]) < static_cast<unsigned>(g.Hs)) &
+           (static_cast<unsigned>(ix[i]) < static_cast<unsigned>(g.Ws));
+  }
+  __device__ __forceinline__ void advance(const WkStep& ws) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      ix[i] += ws.dx;
+      iy[i] += ws.dy;
+      ie[i] += ws.de;
+      if (ix[i] >= xlim) {
+        ix[i] += ws.cx;
+        iy[i] += ws.cy;
+        ie[i] += ws.ce;
+      }
+      if (iy[i] >= ylim) {
+        iy[i] += ws.img_y;
+        ie[i] += ws.img_e;
+      }
+    }
+  }
+};
+
+template <int TBM, bool INC>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __restrict__ dY, int64_t lddy,
                                                               Gather g, float* __restrict__ C, int64_t M, int Co,
                                                               int tiles_n2, int ntiles, int64_t rows_per_split,
-                                                              float* __restrict__ slab, SplitFold fold) {
+                                                              float* __restrict__ slab, SplitFold fold, WkStep ws) {
   constexpr int TM = TBM / 32;                 // 16-row MFMA tiles per wave along Cout (2 waves)
   constexpr int A_CH = TBM / 8;                // 16-B chunks per dY row in the tile
   constexpr int AV = (WK * A_CH + kThreads - 1) / kThreads;
@@ -849,8 +905,21 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __
   for (int i = 0; i < BV; ++i) mr[i].init(m_begin + brow + 16 * i, g);
   // A (dY): chunk v = tid + 256 i -> row v / A_CH, chunk v % A_CH
   int64_t arow_m = m_begin;
+  static_assert(!INC || BV == 2, "IncRows walks two rows per thread");
+  IncRows inc;
+  if constexpr (INC) inc.init(mr, g, tp);
 
   auto load_b = [&](uint4* regs) {
+    if constexpr (INC) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if (kok && mr[0].m + 16 * i < m_end && inc.in_image(i, g))
+          regs[i] = *reinterpret_cast<const uint4*>(g.src + inc.ie[i]);
+        else
+          regs[i] = make_uint4(0, 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < BV; ++i) {
       const MRow& q = mr[i];
@@ -908,8 +977,13 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __
     const uint16_t* Bs = As + TILE;
     const bool more = kt + 1 < nk;
     if (more) {
+      if constexpr (INC) {
+        mr[0].m += WK;  // only the row index is read in INC mode
+        inc.advance(ws);
+      } else {
 #pragma unroll
-      for (int i = 0; i < BV; ++i) mr[i].advance(WK, g);
+        for (int i = 0; i < BV; ++i) mr[i].advance(WK, g);
+      }
       arow_m += WK;
       load_a(ra);
       load_b(rb);
@@ -971,18 +1045,6 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __
 // `s_waitcnt vmcnt(4)` + a raw s_barrier per stage (a __syncthreads() would drain the ring).
 constexpr int kWgStages = 3;
 
-// INC: the im2col row walk is incremental.  The general walk re-derives every row's source address
-// per stage (MRow's wrap loop + 64-bit (n * Hs * Ws + iy * Ws + ix) * ld products): ~24 quarter-rate
-// v_mul_lo_u32 / v_mad_u64_u32 per stage against 16 MFMAs, so the loop was VALU-bound.  With INC
-// each row keeps its source coordinates (ix, iy) and 32-bit element offset e; a WK-row advance adds
-// wave-uniform deltas (WkStep) -- at most one output-row carry and one image carry per stage when
-// OH * OW >= WK + OW -- and the dY rows advance by a pointer add: no multiply in the loop.
-struct WkStep {
-  int dx, dy, de;      // base advance: (WK % OW) columns, (WK / OW) rows
-  int cx, cy, ce;      // extra when the column wraps (ox >= OW)
-  int img_y, img_e;    // extra when the row wraps past the image (oy >= OH)
-};
-
 template <int TBM, bool INC>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wgrad_glds_kernel(const uint16_t* __restrict__ dY, int64_t lddy,
                                                                    Gather g, int64_t M, int Co, int tiles_n2,
@@ -1022,20 +1084,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
   constexpr uint32_t kRow16 = 16 * 256, kStageB = STAGE * 2, kTileB = TILE * 2;
 
   // INC state: rows r0 and r0 + 16 of the next stage
-  int ix[2], iy[2], ie[2];
-  const int xlim = g.OW * g.sw + g.offw + tp.s, ylim = g.OH * g.sh + g.offh + tp.r;  // carry thresholds
+  IncRows inc;
   const uint16_t* ap = dY + (m_begin + r0) * lddy + acol;
   int am32 = static_cast<int>(m_begin) + r0;
   const int mend32 = static_cast<int>(m_end);
-  if constexpr (INC) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const MRow& q = mr[i];
-      ix[i] = q.ox * g.sw + g.offw + tp.s;
-      iy[i] = q.oy * g.sh + g.offh + tp.r;
-      ie[i] = ((q.n * g.Hs + iy[i]) * g.Ws + ix[i]) * static_cast<int>(g.ld) + tp.c;
-    }
-  }
+  if constexpr (INC) inc.init(mr, g, tp);
 
   auto issue = [&](int slot) {
     const uint32_t As = base + slot * kStageB, Bs = As + kTileB;
@@ -1049,22 +1102,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const bool ok = kok & (am32 + 16 * i < mend32) & (static_cast<unsigned>(iy[i]) < static_cast<unsigned>(g.Hs)) &
-                        (static_cast<unsigned>(ix[i]) < static_cast<unsigned>(g.Ws));
-        glds16(ok ? static_cast<const void*>(g.src + ie[i]) : z, Bs + i * kRow16);
-        ix[i] += ws.dx;
-        iy[i] += ws.dy;
-        ie[i] += ws.de;
-        if (ix[i] >= xlim) {
-          ix[i] += ws.cx;
-          iy[i] += ws.cy;
-          ie[i] += ws.ce;
-        }
-        if (iy[i] >= ylim) {
-          iy[i] += ws.img_y;
-          ie[i] += ws.img_e;
-        }
+        const bool ok = kok & (am32 + 16 * i < mend32) & inc.in_image(i, g);
+        glds16(ok ? static_cast<const void*>(g.src + inc.ie[i]) : z, Bs + i * kRow16);
       }
+      inc.advance(ws);
       am32 += WK;
       ap += WK * lddy;
       return;
@@ -1299,6 +1340,26 @@ bool wgrad_inc_enabled() {  // TONY_WGRAD_INC=0: the general row walk (A/B measu
   return on;
 }
 
+// the WK-row advance of the incremental im2col walk; false when the walk does not apply (element
+// offsets or rows past int32, or images so small that one stage can wrap more than one image)
+bool wgrad_inc_step(const Gather& g, int64_t M, WkStep* ws) {
+  const int64_t images = M / (static_cast<int64_t>(g.OH) * g.OW) + 1;
+  const int64_t src_elems = images * g.Hs * g.Ws * g.ld;
+  if (!wgrad_inc_enabled() || src_elems >= (int64_t{1} << 30) || M >= (int64_t{1} << 30) ||
+      static_cast<int64_t>(g.OH) * g.OW < WK + g.OW)
+    return false;
+  const int q = WK / g.OW, rem = WK % g.OW, ld = static_cast<int>(g.ld);
+  ws->dx = rem * g.sw;
+  ws->dy = q * g.sh;
+  ws->de = (rem * g.sw + q * g.sh * g.Ws) * ld;
+  ws->cx = -g.OW * g.sw;
+  ws->cy = g.sh;
+  ws->ce = (g.sh * g.Ws - g.OW * g.sw) * ld;
+  ws->img_y = -g.OH * g.sh;
+  ws->img_e = (g.Hs - g.OH * g.sh) * g.Ws * ld;
+  return true;
+}
+
 template <int TBM>
 int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, float* slab, int64_t slab_cap,
                  int* splits_out, int64_t M, int Co, int num_cus, const SplitFold& fold, hipStream_t stream) {
@@ -1319,33 +1380,23 @@ int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, float
   if (splits_out != nullptr) *splits_out = static_cast<int>(splits);
   // LDS-DMA staging pays for the 128-row Cout tiles only (measured: Cout <= 64 tiles, whose A rows
   // are half / quarter zero chunks, run 4-8 % slower than the register-staged kernel)
+  WkStep ws{};
+  const bool inc = wgrad_inc_step(g, M, &ws);
+  const auto* dyp = static_cast<const uint16_t*>(dy);
   if (TBM == 128 && slab != nullptr && wgrad_glds_enabled()) {
-    // the incremental row walk needs int32 element offsets / row indices and at most one image
-    // carry per WK-row stage
-    const int64_t images = M / (static_cast<int64_t>(g.OH) * g.OW) + 1;
-    const int64_t src_elems = images * g.Hs * g.Ws * g.ld;
-    const bool inc = wgrad_inc_enabled() && src_elems < (int64_t{1} << 30) && M < (int64_t{1} << 30) &&
-                     static_cast<int64_t>(g.OH) * g.OW >= WK + g.OW;
-    WkStep ws{};
-    if (inc) {
-      const int q = WK / g.OW, rem = WK % g.OW, ld = static_cast<int>(g.ld);
-      ws.dx = rem * g.sw;
-      ws.dy = q * g.sh;
-      ws.de = (rem * g.sw + q * g.sh * g.Ws) * ld;
-      ws.cx = -g.OW * g.sw;
-      ws.cy = g.sh;
-      ws.ce = (g.sh * g.Ws - g.OW * g.sw) * ld;
-      ws.img_y = -g.OH * g.sh;
-      ws.img_e = (g.Hs - g.OH * g.sh) * g.Ws * ld;
+    if (inc)
       conv_wgrad_glds_kernel<TBM, true><<<static_cast<int>(grid), kThreads, 0, stream>>>(
-          static_cast<const uint16_t*>(dy), lddy, g, M, Co, tiles_n2, ntiles, rows, slab, fold, ws);
-    } else {
+          dyp, lddy, g, M, Co, tiles_n2, ntiles, rows, slab, fold, ws);
+    else
       conv_wgrad_glds_kernel<TBM, false><<<static_cast<int>(grid), kThreads, 0, stream>>>(
-          static_cast<const uint16_t*>(dy), lddy, g, M, Co, tiles_n2, ntiles, rows, slab, fold, ws);
-    }
-  } else
-    conv_wgrad_kernel<TBM><<<static_cast<int>(grid), kThreads, 0, stream>>>(
-        static_cast<const uint16_t*>(dy), lddy, g, dw, M, Co, tiles_n2, ntiles, rows, slab, fold);
+          dyp, lddy, g, M, Co, tiles_n2, ntiles, rows, slab, fold, ws);
+  } else if (inc) {
+    conv_wgrad_kernel<TBM, true><<<static_cast<int>(grid), kThreads, 0, stream>>>(
+        dyp, lddy, g, dw, M, Co, tiles_n2, ntiles, rows, slab, fold, ws);
+  } else {
+    conv_wgrad_kernel<TBM, false><<<static_cast<int>(grid), kThreads, 0, stream>>>(
+        dyp, lddy, g, dw, M, Co, tiles_n2, ntiles, rows, slab, fold, ws);
+  }
   TONY_LAUNCH_CHECK();
   return 0;
 }

@@ -36,11 +36,23 @@ struct RowState {
   int iy0;   // oy*sh + offh
   int ix0;   // ox*sw + offw
   bool ok;   // row < M
+  const uint16_t* base;  // src + (pix + iy0 * Ws + ix0) * ld: the row's source at tap (0, 0), channel 0
+                         // (outside the image for padded rows; only dereferenced with a tap in bounds)
+  __device__ __forceinline__ void set_base(const struct Gather& g);
 };
+
+__device__ __forceinline__ void RowState::set_base(const Gather& g) {
+  base = g.src + (static_cast<int64_t>(pix) + static_cast<int64_t>(iy0) * g.Ws + ix0) * g.ld;
+}
 
 // position of a K chunk: channel c of tap (r, s)
 struct TapPos {
   int c, r, s;
+  // element offset of this chunk from a row's tap-(0, 0) source (RowState::base): one product per
+  // K-step shared by all of a thread's rows instead of a 64-bit (pix + iy * Ws + ix) * ld per row
+  __device__ __forceinline__ int off(const struct Gather& g) const {
+    return g.sign * (r * g.Ws + s) * static_cast<int>(g.ld) + c;
+  }
   __device__ __forceinline__ void init(int k, const Gather& g) {
     c = k % g.Cs;
     const int tap = k / g.Cs;
@@ -166,6 +178,7 @@ __global__ __launch_bounds__(kThreads) void conv_glds_kernel(Gather g, const uin
     rs[i].pix = n * g.Hs * g.Ws;
     rs[i].iy0 = oy * g.sh + g.offh;
     rs[i].ix0 = ox * g.sw + g.offw;
+    rs[i].set_base(g);
   }
   const uint16_t* brow[BI];
   bool bok[BI];
@@ -245,12 +258,13 @@ __global__ __launch_bounds__(kThreads) void conv_glds_kernel(Gather g, const uin
       return;
     }
     const void* z = &kZeroChunk;
+    const int toff = tp.off(g);
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const int iy = rs[i].iy0 + g.sign * tp.r, ix = rs[i].ix0 + g.sign * tp.s;
       const bool ok = rs[i].ok & (tp.r < g.R) & (static_cast<unsigned>(iy) < static_cast<unsigned>(g.Hs)) &
                       (static_cast<unsigned>(ix) < static_cast<unsigned>(g.Ws));
-      const uint16_t* src = g.src + (static_cast<int64_t>(rs[i].pix) + iy * g.Ws + ix) * g.ld + tp.c;
+      const uint16_t* src = rs[i].base + toff;
       glds16(ok ? static_cast<const void*>(src) : z, st0 + aoff[i]);
     }
     const bool kok = kb < K;
