@@ -101,6 +101,7 @@ def _ps_reference(workers, steps, lr=0.1, mu=0.9):
     ("colocated", 3, [0, 1, 2], 0.0003, (0,), True),       # several buckets, 3-way split, launched in backward
     ("dedicated", 3, [1, 2], 32, (0,), False),
     ("dedicated", 4, [2, 3], 0.0003, (0, 1), True),        # 2 ps tasks own alternate buckets
+    ("colocated", 8, list(range(8)), 0.0003, (0,), True),  # the driver's 8-GPU layout: 8 shards per bucket
 ])
 def test_parameter_server_sync(mode, world, workers, bucket_mb, ps_ranks, overlap):
     port, steps = _port(), 3
