@@ -1139,16 +1139,20 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int nk = static_cast<int>((m_end - m_begin + WK - 1) / WK);
   issue(0);
   issue(1);
-  for (int kt = 0; kt < nk; ++kt) {
+  // one K-step on ring slot SLOT (= kt % 3).  The loop is unrolled by the ring length so that the
+  // slot is a compile-time constant: the fragment reads then address LDS as a per-lane offset (loop
+  // invariant) plus an immediate, instead of re-deriving 16 addresses from the slot every step.
+  const int kgrp = lane >> 4;
+  auto step = [&](auto slot_c) {
+    constexpr int SLOT = decltype(slot_c)::value;
     // stage kt has landed in this wave (4 DMAs per stage; stage kt+1's 4 may still fly) and, after
     // the barrier, in every wave; every wave is also done reading stage kt-1, whose slot is refilled
     // with stage kt+2 (past the end: zero / unread fills, which keeps the count uniform)
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    issue((kt + 2) % kWgStages);
-    const uint16_t* As = smem + (kt % kWgStages) * STAGE;
+    issue((SLOT + 2) % kWgStages);
+    const uint16_t* As = smem + SLOT * STAGE;
     const uint16_t* Bs = As + TILE;
-    const int kgrp = lane >> 4;
     bf16x8_t af[TM], bfr[4];
 #pragma unroll
     for (int i = 0; i < TM; ++i) af[i] = tr_frag(As, kgrp, wm * (TBM / 2) + i * 16, lane);
@@ -1159,7 +1163,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  };
+  static_assert(kWgStages == 3, "the K loop is unrolled by the ring length");
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  using S2 = std::integral_constant<int, 2>;
+  int kt = 0;
+  for (; kt + 3 <= nk; kt += 3) {
+    step(S0{});
+    step(S1{});
+    step(S2{});
   }
+  if (kt < nk) step(S0{});
+  if (kt + 1 < nk) step(S1{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup retires
   float* dst = slab + static_cast<int64_t>(split) * Co * K;
 #pragma unroll

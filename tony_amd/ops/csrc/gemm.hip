@@ -17,6 +17,7 @@
 //    of `lds_off`.
 //  * Workgroup ids are remapped so that consecutive output tiles (which share
 //    an A row-panel) are dispatched onto the same XCD and hit its private L2.
+#include <type_traits>
 #include <cstdlib>
 
 #include "igemm.h"
@@ -246,7 +247,7 @@ __device__ __forceinline__ void tn_store(uint16_t* lds, const uint4* regs) {
 // fetches logical chunk (l & 15) ^ tr_swz(row)).  Slab mode only.
 constexpr int kTnStages = 3;
 
-__global__ __launch_bounds__(kThreads) void gemm_tn_glds_kernel(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_tn_glds_kernel(
     const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ B, int64_t ldb, int64_t M, int N1,
     int N2, int tiles_n2, int ntiles, int64_t rows_per_split, float* __restrict__ slab, SplitFold fold) {
   constexpr int TILE = TBK * 128, STAGE = 2 * TILE;
@@ -265,7 +266,12 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_glds_kernel(
   const bool aok = n1_0 + ch * 8 < N1, bok = n2_0 + ch * 8 < N2;
   const uint16_t* ap = A + n1_0 + ch * 8;
   const uint16_t* bp = B + n2_0 + ch * 8;
-  int64_t am = m_begin + r0;
+  // row pointers advance by TBK rows per stage (no 64-bit m * ld product per DMA)
+  int am = static_cast<int>(m_begin) + r0;
+  const int mend = static_cast<int>(m_end);
+  const uint16_t* apm = ap + (m_begin + r0) * lda;
+  const uint16_t* bpm = bp + (m_begin + r0) * ldb;
+  const int64_t astep = TBK * lda, bstep = TBK * ldb;
   const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(smem) + (4 * wave) * 256);
   constexpr uint32_t kRow16 = 16 * 256, kStageB = STAGE * 2, kTileB = TILE * 2;
   auto issue = [&](int slot) {
@@ -273,12 +279,13 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_glds_kernel(
     const void* z = &kZeroChunk;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int64_t m = am + 16 * i;
-      const bool mok = m < m_end;
-      glds16(aok & mok ? static_cast<const void*>(ap + m * lda) : z, As + i * kRow16);
-      glds16(bok & mok ? static_cast<const void*>(bp + m * ldb) : z, Bs + i * kRow16);
+      const bool mok = am + 16 * i < mend;
+      glds16(aok & mok ? static_cast<const void*>(apm + i * 16 * lda) : z, As + i * kRow16);
+      glds16(bok & mok ? static_cast<const void*>(bpm + i * 16 * ldb) : z, Bs + i * kRow16);
     }
     am += TBK;
+    apm += astep;
+    bpm += bstep;
   };
 
   f32x4 acc[4][4];
@@ -290,15 +297,17 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_glds_kernel(
   const int nk = static_cast<int>((m_end - m_begin + TBK - 1) / TBK);
   issue(0);
   issue(1);
-  for (int kt = 0; kt < nk; ++kt) {
+  const int kgrp = lane >> 4;
+  // unrolled by the ring length: compile-time slots, so the fragment reads use immediate offsets
+  auto step = [&](auto slot_c) {
+    constexpr int SLOT = decltype(slot_c)::value;
     // stage kt landed here (4 DMAs per stage, stage kt+1's may still fly) and, after the barrier,
     // everywhere; stage kt-1's slot is free for stage kt+2 (zero fills past the end)
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    issue((kt + 2) % kTnStages);
-    const uint16_t* As = smem + (kt % kTnStages) * STAGE;
+    issue((SLOT + 2) % kTnStages);
+    const uint16_t* As = smem + SLOT * STAGE;
     const uint16_t* Bs = As + TILE;
-    const int kgrp = lane >> 4;
     bf16x8_t af[4], bfr[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) af[i] = tr_frag(As, kgrp, wm * 64 + i * 16, lane);
@@ -308,7 +317,16 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_glds_kernel(
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  };
+  static_assert(kTnStages == 3, "the K loop is unrolled by the ring length");
+  int kt = 0;
+  for (; kt + 3 <= nk; kt += 3) {
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{});
   }
+  if (kt < nk) step(std::integral_constant<int, 0>{});
+  if (kt + 1 < nk) step(std::integral_constant<int, 1>{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   float* dst = slab + static_cast<int64_t>(split) * N1 * N2;
 #pragma unroll
