@@ -8,18 +8,18 @@ tensor of another dtype is an error, not a silent fallback.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib, tape
 from .arena import zeros_f32
 
 
-def _rows_view(t: torch.Tensor):
-    """Return (M, C, ld) when ``t``'s memory is M rows of C channels with row
-    stride ``ld`` (channels_last 4D, a channel slice of one, or 2D [M, C])."""
-    if t.dim() == 4:
-        n, c, h, w = t.shape
-        sn, sc, sh, sw = t.stride()
+def _rows_view_uncached(shape, stride):
+    if len(shape) == 4:
+        n, c, h, w = shape
+        sn, sc, sh, sw = stride
         if sc != 1 and c > 1:
             return None
         # strides of size-1 dims are arbitrary: derive the row stride from the
@@ -37,12 +37,33 @@ def _rows_view(t: torch.Tensor):
         if ld < c:
             return None
         return n * h * w, c, ld
-    if t.dim() == 2:
-        m, c = t.shape
-        if t.stride(1) != 1:
+    if len(shape) == 2:
+        m, c = shape
+        if stride[1] != 1:
             return None
-        return m, c, t.stride(0) if m > 1 else c
+        return m, c, stride[0] if m > 1 else c
     return None
+
+
+# The row view depends only on (shape, strides): memoised, since every fused op asks it for each
+# operand on every call (~600 times per Inception step; the uncached walk is ~2 us of Python).
+# TONY_HOST_MEMO=0 turns the host-side memos of ops/ off (A/B of the host issue time).
+HOST_MEMO = os.environ.get("TONY_HOST_MEMO", "1") != "0"
+_RV_CACHE: dict = {}
+
+
+def _rows_view(t: torch.Tensor):
+    """Return (M, C, ld) when ``t``'s memory is M rows of C channels with row
+    stride ``ld`` (channels_last 4D, a channel slice of one, or 2D [M, C])."""
+    if not HOST_MEMO:
+        return _rows_view_uncached(t.shape, t.stride())
+    key = (t.shape, t.stride())
+    r = _RV_CACHE.get(key, _RV_CACHE)
+    if r is _RV_CACHE:
+        if len(_RV_CACHE) > 4096:
+            _RV_CACHE.clear()
+        r = _RV_CACHE[key] = _rows_view_uncached(*key)
+    return r
 
 
 def _as_rows(t: torch.Tensor):
