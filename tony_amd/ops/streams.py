@@ -126,6 +126,13 @@ def active() -> bool:
 # (profiles/r2s3_host_levers_ab.log)
 BATCH = int(os.environ.get("TONY_WGRAD_BATCH", "2"))
 _pending: List[Callable[[], object]] = []
+# ...except for big operands: a batch forks from the current stream when it is flushed, so a pending
+# op waits for whatever the compute stream was given in between (the next layer's BN backward and
+# data gradient).  At the end of an Inception backward that is the serial stem chain: the 149x149
+# layer's wgrad sat behind the 147x147 layer's BN backward, and the optimizer waited ~350 us on it
+# (profiles/r2s4_step_tail_trace.txt).  Ops whose first kept operand (the conv-output gradient) is at
+# least URGENT_BYTES are issued at once.  TONY_WGRAD_URGENT_MB=0 turns this off.
+URGENT_BYTES = int(os.environ.get("TONY_WGRAD_URGENT_MB", "64")) << 20
 
 
 # A fork costs host time on every weight gradient (~66 per Inception step), so it avoids the
@@ -186,11 +193,12 @@ def run(fn: Callable[[], object], *keep: torch.Tensor):
         with _lock:
             _issued[0] += 1
         return fn()
+    urgent = URGENT_BYTES > 0 and bool(keep) and keep[0].numel() * keep[0].element_size() >= URGENT_BYTES
     with _lock:
         _pending.append(fn)
         _keep.extend(keep)
         _issued[0] += 1
-        full = len(_pending) >= BATCH
+        full = len(_pending) >= BATCH or urgent
     if full:
         _flush(side)
     return None
