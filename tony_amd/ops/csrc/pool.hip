@@ -56,6 +56,9 @@ __global__ __launch_bounds__(kThreads) void box3_kernel(const uint16_t* __restri
   }
 }
 
+// KT = 3: the window's 9 loads are issued before the first is consumed (the runtime-K loop waits on
+// each in turn); 0: any K
+template <int KT>
 __global__ __launch_bounds__(kThreads) void maxpool_fwd_kernel(const uint16_t* __restrict__ x,
                                                                uint16_t* __restrict__ y, uint8_t* __restrict__ arg,
                                                                int N, int H, int W, int C, int OH, int OW, int K,
@@ -77,19 +80,33 @@ __global__ __launch_bounds__(kThreads) void maxpool_fwd_kernel(const uint16_t* _
       best[j] = -INFINITY;
       bi[j] = 0;
     }
-    for (int kh = 0; kh < K; ++kh) {
-      const int hh = oh * S + kh;
-      for (int kw = 0; kw < K; ++kw) {
-        const int ww = ow * S + kw;
-        float f[8];
-        load8(x + ((n * H + hh) * W + ww) * ldx + cg * 8).to_float(f);
-        const uint8_t idx = static_cast<uint8_t>(kh * K + kw);
+    auto take = [&](const bf16x8& raw, uint8_t idx) {
+      float f[8];
+      raw.to_float(f);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          if (f[j] > best[j] || (f[j] != f[j])) {  // NaN propagates like torch
-            best[j] = f[j];
-            bi[j] = idx;
-          }
+      for (int j = 0; j < 8; ++j) {
+        if (f[j] > best[j] || (f[j] != f[j])) {  // NaN propagates like torch
+          best[j] = f[j];
+          bi[j] = idx;
+        }
+      }
+    };
+    if constexpr (KT > 0) {
+      const uint16_t* base = x + ((n * H + oh * S) * W + ow * S) * ldx + cg * 8;
+      const int64_t row = static_cast<int64_t>(W) * ldx;
+      bf16x8 raw[KT * KT];
+#pragma unroll
+      for (int kh = 0; kh < KT; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < KT; ++kw) raw[kh * KT + kw] = load8(base + kh * row + kw * ldx);
+#pragma unroll
+      for (int k = 0; k < KT * KT; ++k) take(raw[k], static_cast<uint8_t>(k));
+    } else {
+      for (int kh = 0; kh < K; ++kh) {
+        const int hh = oh * S + kh;
+        for (int kw = 0; kw < K; ++kw) {
+          const int ww = ow * S + kw;
+          take(load8(x + ((n * H + hh) * W + ww) * ldx + cg * 8), static_cast<uint8_t>(kh * K + kw));
         }
       }
     }
@@ -320,7 +337,7 @@ TONY_API int tony_maxpool_fwd(const void* x, void* y, void* argmax, int N, int H
   if (C % 8 || ldx % 8 || ldy % 8 || K * K > 255 || H < K || W < K) return -1;
   if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
   const int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
-  maxpool_fwd_kernel<<<grid_for(static_cast<int64_t>(N) * OH * OW * (C / 8)), kThreads, 0, stream>>>(
+  (K == 3 ? maxpool_fwd_kernel<3> : maxpool_fwd_kernel<0>)<<<grid_for(static_cast<int64_t>(N) * OH * OW * (C / 8)), kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), static_cast<uint8_t*>(argmax), N, H, W, C, OH, OW,
       K, S, ldx, ldy);
   TONY_LAUNCH_CHECK();
