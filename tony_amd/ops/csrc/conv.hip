@@ -561,6 +561,18 @@ __global__ __launch_bounds__(kThreads) void conv_direct_kernel(Gather g, const u
   }
 
   uint4 pf[D::PFN];
+  // tile-invariant part of each prefetch chunk: halo (row, column) packed in one word and the element
+  // offset from the halo origin -- per tile only a wave-uniform base pointer changes (no 64-bit
+  // (pix + iy * Ws + ix) * ld product per chunk and tile)
+  int pyx[D::PFN], poff[D::PFN];
+#pragma unroll
+  for (int i = 0; i < D::PFN; ++i) {
+    const int v = i * kThreads + threadIdx.x;
+    const int hp = v / (CS / 8), c8 = v - hp * (CS / 8);
+    const int hy = hp / D::HW, hx = hp - hy * D::HW;
+    pyx[i] = v < D::HCH ? (hy << 16) | hx : 0x7fff0000;  // past the halo: never in bounds
+    poff[i] = (hy * g.Ws + hx) * static_cast<int>(g.ld) + c8 * 8;
+  }
   auto tile_origin = [&](int t, int& n, int& oy0, int& ox0) {
     const int tx = t % tiles_x, rest = t / tiles_x;
     const int ty = rest % tiles_y;
@@ -573,17 +585,13 @@ __global__ __launch_bounds__(kThreads) void conv_direct_kernel(Gather g, const u
     tile_origin(t, n, oy0, ox0);
     const int hy0 = oy0 + g.offh - (g.sign < 0 ? D::R - 1 : 0);
     const int hx0 = ox0 + g.offw - (g.sign < 0 ? D::S - 1 : 0);
-    const int64_t pix0 = static_cast<int64_t>(n) * g.Hs * g.Ws;
+    const uint16_t* hb = g.src + ((static_cast<int64_t>(n) * g.Hs + hy0) * g.Ws + hx0) * g.ld;
 #pragma unroll
     for (int i = 0; i < D::PFN; ++i) {
-      const int v = i * kThreads + threadIdx.x;
-      const int hp = v / (CS / 8), c8 = v - hp * (CS / 8);
-      const int hy = hp / D::HW, hx = hp - hy * D::HW;
-      const int iy = hy0 + hy, ix = hx0 + hx;
+      const int iy = hy0 + (pyx[i] >> 16), ix = hx0 + (pyx[i] & 0xffff);
       pf[i] = make_uint4(0u, 0u, 0u, 0u);
-      if (v < D::HCH && static_cast<unsigned>(iy) < static_cast<unsigned>(g.Hs) &&
-          static_cast<unsigned>(ix) < static_cast<unsigned>(g.Ws))
-        pf[i] = *reinterpret_cast<const uint4*>(g.src + (pix0 + iy * g.Ws + ix) * g.ld + c8 * 8);
+      if (static_cast<unsigned>(iy) < static_cast<unsigned>(g.Hs) && static_cast<unsigned>(ix) < static_cast<unsigned>(g.Ws))
+        pf[i] = *reinterpret_cast<const uint4*>(hb + poff[i]);
     }
   };
 
