@@ -20,6 +20,7 @@
 // with the MFMA (A = dY^T: 8 pixels of one channel per lane, B = the same im2col gather as the
 // forward), the four waves fold their tiles with LDS float adds at the end, and each workgroup
 // stores one partial into the split-K slab that csrc/splitk.hip sums into the gradient slot.
+#include <type_traits>
 #include "mfma_common.h"
 
 using namespace tony;
@@ -41,7 +42,18 @@ struct StemGeom {
   int M;                 // N * OH * OW
   int K;                 // R * S * C
   int64_t total;         // N * H * W * C
+  float inv_ohw, inv_ow; // 1 / (OH * OW), 1 / OW: pixel index -> (n, oy, ox) without integer division
 };
+
+// q = a / b for 0 <= a < 2^24 (exact in fp32): the fp32 quotient is off by at most one, fixed up with
+// 24-bit integer products (full rate; a runtime integer division is a ~30-instruction sequence)
+__device__ __forceinline__ int fast_div(int a, int b, float inv_b) {
+  int q = static_cast<int>(static_cast<float>(a) * inv_b);
+  const int r = a - static_cast<int>(__umul24(q, b));
+  if (r < 0) --q;
+  else if (r >= b) ++q;
+  return q;
+}
 
 // Element range [e0, e1) of x covering every in-image tap of output pixels m_first..m_last
 // (consecutive in m).  e0 is 8-aligned (16-byte loads).  False if it does not fit the patch.
@@ -96,15 +108,20 @@ struct Pix {
   __device__ __forceinline__ void set(const StemGeom& g, int64_t e0) {
     iy0 = oy * g.sh - g.ph;
     ix0 = ox * g.sw - g.pw;
-    base = ((static_cast<int64_t>(n) * g.H + iy0) * g.W + ix0) * g.C - e0;
+    // unsigned 24-bit products (full rate) on the unpadded coordinates oy * sh, ox * sw >= 0: the pixel
+    // index stays below N * H * W < 2^24 (make_geom) and times C below 2^31; the padding offset is
+    // subtracted afterwards
+    const unsigned pix = __umul24(__umul24(static_cast<unsigned>(n), g.H) + static_cast<unsigned>(iy0 + g.ph), g.W) +
+                         static_cast<unsigned>(ix0 + g.pw);
+    base = static_cast<int64_t>(__umul24(pix, g.C)) - (static_cast<int64_t>(g.ph) * g.W + g.pw) * g.C - e0;
   }
   __device__ __forceinline__ void init(const StemGeom& g, int m, int64_t e0) {
     ok = m < g.M;
     const int mm = ok ? m : 0;
     const int ohw = g.OH * g.OW;
-    n = mm / ohw;
+    n = fast_div(mm, ohw, g.inv_ohw);  // make_geom guarantees M < 2^24
     const int rem = mm - n * ohw;
-    oy = rem / g.OW;
+    oy = fast_div(rem, g.OW, g.inv_ow);
     ox = rem - oy * g.OW;
     set(g, e0);
   }
@@ -133,7 +150,12 @@ __device__ __forceinline__ uint32_t tap_word(const StemGeom& g, int k) {
   return static_cast<uint32_t>(off) | (static_cast<uint32_t>(r) << 20) | (static_cast<uint32_t>(s) << 26);
 }
 
+// NP (no padding): every tap of an output pixel lies inside the image, so the gather is one add and
+// one load; the K-padding columns (k >= K) read the pixel's own tap-(0, 0) value, which the zero
+// weight columns (forward) cancel and the weight gradient never stores.
+template <bool NP>
 __device__ __forceinline__ uint16_t tap_value(const StemGeom& g, const uint16_t* src, const Pix& p, uint32_t t) {
+  if constexpr (NP) return p.ok ? src[p.base + static_cast<int>(t & 0xfffffu)] : static_cast<uint16_t>(0);
   const int r = (t >> 20) & 63, s = t >> 26;
   const bool in = p.ok && static_cast<unsigned>(p.iy0 + r) < static_cast<unsigned>(g.H) &&
                   static_cast<unsigned>(p.ix0 + s) < static_cast<unsigned>(g.W);
@@ -152,7 +174,7 @@ __device__ __forceinline__ bf16x8_t pack8(const uint16_t (&v)[8]) {
 // of a 256-pixel tile (no duplicated gathers).  The weight fragments (bf16, MFMA-B order) and the
 // per-column tap table are built in LDS once per workgroup.  BN statistics accumulate in
 // registers over all the workgroup's tiles and are added once (one sharded atomic per column).
-template <int BN>
+template <int BN, bool NP>
 __global__ __launch_bounds__(kThreads) void stem_fwd_kernel(StemGeom g, const uint16_t* __restrict__ wk,
                                                             uint16_t* __restrict__ y, int64_t ldy,
                                                             float* __restrict__ stats, int64_t sstride) {
@@ -221,7 +243,7 @@ __global__ __launch_bounds__(kThreads) void stem_fwd_kernel(StemGeom g, const ui
         for (int i = 0; i < TM; ++i) {
           uint16_t v[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = tap_value(g, src, px[i], tp[e]);
+          for (int e = 0; e < 8; ++e) v[e] = tap_value<NP>(g, src, px[i], tp[e]);
           const bf16x8_t af = pack8(v);
 #pragma unroll
           for (int j = 0; j < TN; ++j)
@@ -277,7 +299,7 @@ __global__ __launch_bounds__(kThreads) void stem_fwd_kernel(StemGeom g, const ui
 // pitch: the 8 rows a lane reads for one A fragment are 8 x pitch apart, which puts the four lane
 // quarters on disjoint bank ranges (conflict-free ds_read_u16).  The next chunk's dY rows and input
 // rows are loaded into registers while the current chunk computes.
-template <int CO, int KB>
+template <int CO, int KB, bool NP>
 __global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(StemGeom g, const uint16_t* __restrict__ dy,
                                                               int64_t lddy, float* __restrict__ slab, int64_t n) {
   constexpr int PD = CO + 4;
@@ -358,7 +380,7 @@ __global__ __launch_bounds__(kThreads) void stem_wgrad_kernel(StemGeom g, const 
           if (j >= kbn) break;  // wave-uniform: column blocks past K
           uint16_t v[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = tap_value(g, src, px[e], tp[j]);
+          for (int e = 0; e < 8; ++e) v[e] = tap_value<NP>(g, src, px[e], tp[j]);
           const bf16x8_t bfr = pack8(v);
 #pragma unroll
           for (int i = 0; i < CB; ++i)
@@ -400,11 +422,13 @@ bool make_geom(StemGeom& g, const void* x, int N, int H, int W, int C, int Co, i
   if (R <= 0 || S <= 0 || sh <= 0 || sw <= 0 || ph < 0 || pw < 0 || ph >= R || pw >= S) return false;
   if (OH != (H + 2 * ph - R) / sh + 1 || OW != (W + 2 * pw - S) / sw + 1 || OH <= 0 || OW <= 0) return false;
   const int64_t M = static_cast<int64_t>(N) * OH * OW;
-  if (M > 0x7fffffff - kBM) return false;  // 32-bit pixel index in the kernels
+  if (M >= (1 << 24) - kBM) return false;  // pixel indices exact in fp32 (fast_div)
+  if (static_cast<int64_t>(N) * H * W >= (1 << 24)) return false;  // 24-bit pixel products (Pix::set)
   if (static_cast<int64_t>(R) * S * C > kMaxKSteps * 32 || (static_cast<int64_t>(R) * W + S) * C >= (1 << 20))
     return false;
   g = StemGeom{static_cast<const uint16_t*>(x), H, W, C, R, S, sh, sw, ph, pw, OH, OW, static_cast<int>(M),
-               R * S * C, static_cast<int64_t>(N) * H * W * C};
+               R * S * C, static_cast<int64_t>(N) * H * W * C, 1.f / static_cast<float>(OH * OW),
+               1.f / static_cast<float>(OW)};
   return true;
 }
 
@@ -437,15 +461,19 @@ TONY_API int tony_stem_fwd(const void* x, int N, int H, int W, int C, const void
       per_cu = 2;
     return min(ceil_div(g.M, kBM), per_cu * (num_cus > 0 ? num_cus : 256));
   };
-  if (Co == 32) {
-    const size_t b = lds(32);
-    stem_fwd_kernel<32><<<grid_for(reinterpret_cast<const void*>(&stem_fwd_kernel<32>), b), kThreads, b, stream>>>(
-        g, static_cast<const uint16_t*>(w), static_cast<uint16_t*>(y), ldy, st, sstride);
-  } else {
-    const size_t b = lds(64);
-    stem_fwd_kernel<64><<<grid_for(reinterpret_cast<const void*>(&stem_fwd_kernel<64>), b), kThreads, b, stream>>>(
-        g, static_cast<const uint16_t*>(w), static_cast<uint16_t*>(y), ldy, st, sstride);
-  }
+  const bool np = ph == 0 && pw == 0;
+  const auto launch = [&](auto bn_c, auto np_c) {
+    constexpr int BN = decltype(bn_c)::value;
+    constexpr bool NP = decltype(np_c)::value;
+    const size_t b = lds(BN);
+    stem_fwd_kernel<BN, NP><<<grid_for(reinterpret_cast<const void*>(&stem_fwd_kernel<BN, NP>), b), kThreads, b,
+                               stream>>>(g, static_cast<const uint16_t*>(w), static_cast<uint16_t*>(y), ldy, st, sstride);
+  };
+  using std::integral_constant;
+  if (Co == 32)
+    np ? launch(integral_constant<int, 32>{}, std::true_type{}) : launch(integral_constant<int, 32>{}, std::false_type{});
+  else
+    np ? launch(integral_constant<int, 64>{}, std::true_type{}) : launch(integral_constant<int, 64>{}, std::false_type{});
   TONY_LAUNCH_CHECK();
   return 0;
 }
@@ -469,9 +497,9 @@ TONY_API int tony_stem_wgrad(const void* dy, int64_t lddy, const void* x, int N,
   static int occ[3] = {0, 0, 0};
   const int which = k5 ? 2 : (Co == 64);
   if (occ[which] == 0) {
-    const void* fn = k5 ? reinterpret_cast<const void*>(&stem_wgrad_kernel<64, 5>)
-                        : Co == 64 ? reinterpret_cast<const void*>(&stem_wgrad_kernel<64, 4>)
-                                   : reinterpret_cast<const void*>(&stem_wgrad_kernel<32, 4>);
+    const void* fn = k5 ? reinterpret_cast<const void*>(&stem_wgrad_kernel<64, 5, false>)
+                        : Co == 64 ? reinterpret_cast<const void*>(&stem_wgrad_kernel<64, 4, false>)
+                                   : reinterpret_cast<const void*>(&stem_wgrad_kernel<32, 4, false>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[which], fn, kThreads, 0) != hipSuccess || occ[which] <= 0)
       occ[which] = 1;
   }
@@ -480,16 +508,22 @@ TONY_API int tony_stem_wgrad(const void* dy, int64_t lddy, const void* x, int N,
   // column groups of 64 (Inception's K = 27 fits one); a 7x7 RGB stem (K = 147) takes its 160 padded
   // columns in two groups of 5 blocks, so dY and the image are streamed twice instead of three times
   // (one group of 10 blocks spills: 160 accumulator registers)
-  if (k5) {
-    stem_wgrad_kernel<64, 5><<<dim3(gx, ceil_div(g.K, 80)), kThreads, 0, stream>>>(
-        g, static_cast<const uint16_t*>(dy), lddy, slab, n);
-  } else {
-    const dim3 grid(gx, ceil_div(g.K, 64));
-    if (Co == 32)
-      stem_wgrad_kernel<32, 4><<<grid, kThreads, 0, stream>>>(g, static_cast<const uint16_t*>(dy), lddy, slab, n);
-    else
-      stem_wgrad_kernel<64, 4><<<grid, kThreads, 0, stream>>>(g, static_cast<const uint16_t*>(dy), lddy, slab, n);
-  }
+  const bool np = ph == 0 && pw == 0;
+  const auto launch = [&](auto co_c, auto kb_c, auto np_c, int gy) {
+    stem_wgrad_kernel<decltype(co_c)::value, decltype(kb_c)::value, decltype(np_c)::value>
+        <<<dim3(gx, gy), kThreads, 0, stream>>>(g, static_cast<const uint16_t*>(dy), lddy, slab, n);
+  };
+  using std::integral_constant;
+  using I4 = integral_constant<int, 4>;
+  if (k5)
+    np ? launch(integral_constant<int, 64>{}, integral_constant<int, 5>{}, std::true_type{}, ceil_div(g.K, 80))
+       : launch(integral_constant<int, 64>{}, integral_constant<int, 5>{}, std::false_type{}, ceil_div(g.K, 80));
+  else if (Co == 32)
+    np ? launch(integral_constant<int, 32>{}, I4{}, std::true_type{}, ceil_div(g.K, 64))
+       : launch(integral_constant<int, 32>{}, I4{}, std::false_type{}, ceil_div(g.K, 64));
+  else
+    np ? launch(integral_constant<int, 64>{}, I4{}, std::true_type{}, ceil_div(g.K, 64))
+       : launch(integral_constant<int, 64>{}, I4{}, std::false_type{}, ceil_div(g.K, 64));
   TONY_LAUNCH_CHECK();
   *splits = gx;
   return 0;
