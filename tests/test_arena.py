@@ -66,3 +66,28 @@ def test_tune_cache_roundtrip(tmp_path):
         tune._CACHE.update(saved_t)
         conv._CHOICE.clear()
         conv._CHOICE.update(saved_c)
+
+
+def test_rows_view_memo_matches_uncached_walk():
+    """ops/bn.py memoises the (shape, strides) -> (M, C, ld) row view: every layout the fused ops see
+    (channels_last, channel slices of a concat buffer, 2D, size-1 dims, non-row layouts) must give
+    the uncached answer, on the first (miss) and second (hit) call."""
+    import torch
+
+    from tony_amd.ops import bn
+
+    cl = torch.channels_last
+    base = torch.empty(3, 24, 5, 7).contiguous(memory_format=cl)
+    cases = [base, base[:, 8:16], base[:, :8], torch.empty(4, 16, 1, 1).contiguous(memory_format=cl),
+             torch.empty(1, 8, 1, 9).contiguous(memory_format=cl), torch.empty(2, 8, 3, 3),  # NCHW: no row view
+             torch.empty(6, 40), torch.empty(6, 40)[:, :16], torch.empty(6, 40).t()]
+    for t in cases:
+        want = bn._rows_view_uncached(t.shape, t.stride())
+        assert bn._rows_view(t) == want
+        assert bn._rows_view(t) == want
+
+
+def test_conv_pair_fast_path():
+    from tony_amd.ops.conv import _pair
+
+    assert _pair(3) == (3, 3) and _pair((1, 2)) == (1, 2) and _pair([2, 1]) == (2, 1)
