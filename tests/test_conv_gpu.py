@@ -270,9 +270,9 @@ def test_conv_bn_act_pool_fused_matches_unfused(cuda, shape):
 
 # (N, H, W, (R, S), stride, (ph, pw), Cout): Inception-v3's 3x3/2 stem (shrunk in N and H/W, with a
 # partial last workgroup and workgroups straddling two images), ResNet's 7x7/2 p3 stem (5 K steps,
-# 3 wgrad column groups), and a padded stride-1 case
+# 3 wgrad column groups) and a padded 3x3/2 stem (stride-1 stems are not taken: conv.stem_supported)
 STEM_SHAPES = [(2, 299, 299, (3, 3), 2, (0, 0), 32), (3, 37, 41, (3, 3), 2, (0, 0), 32),
-               (2, 45, 33, (7, 7), 2, (3, 3), 64), (1, 20, 20, (3, 3), 1, (1, 1), 32),
+               (2, 45, 33, (7, 7), 2, (3, 3), 64), (4, 64, 64, (3, 3), 2, (1, 1), 32),
                (3, 56, 56, (7, 7), 2, (3, 3), 64)]
 
 

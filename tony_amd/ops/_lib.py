@@ -19,7 +19,7 @@ import weakref
 import torch  # noqa: F401  (must precede the dlopen below)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-SO_PATH = os.path.join(_HERE, "_tony_kernels.so")
+SO_PATH = os.environ.get("TONY_KERNELS_SO") or os.path.join(_HERE, "_tony_kernels.so")  # override: A/B of builds
 
 _lock = threading.Lock()
 _lib = None

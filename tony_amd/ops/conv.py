@@ -87,6 +87,10 @@ def stem_supported(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, d
     """Whether the MFMA stem kernels (csrc/stem.hip) take this conv: dense NHWC bf16 input with fewer
     than 8 channels (an image), 32 or 64 output channels, padding smaller than the filter."""
     (ph, pw) = _pair(padding)
+    # strided stems only (every image stem of the reference models is stride 2): a stride-1 padded
+    # 3x3 stem produced non-finite rows on MI355X (tools/stem_check.py) and is left to MIOpen
+    if min(_pair(stride)) < 2:
+        return False
     return (x.is_cuda and x.dtype == _BF16 and weight.dtype == _BF16 and x.dim() == 4 and groups == 1
             and _pair(dilation) == (1, 1) and 0 < x.shape[1] < 8 and weight.shape[0] in (32, 64)
             and weight.shape[1] == x.shape[1] and ph < weight.shape[2] and pw < weight.shape[3]
