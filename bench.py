@@ -221,6 +221,11 @@ def main():
     if args.tune_cache and os.path.exists(args.tune_cache):
         tune_loaded = tune.load(args.tune_cache)
     mode = "eager" if args.no_graph else args.mode
+    if mode == "auto" and world > 1:
+        # several ranks: a replayed graph holds forward + backward only and the bucketed PS push /
+        # apply / pull then runs after it, un-overlapped (collectives stay out of the capture), so the
+        # eager step -- communication overlapped with backward -- is the one to run; no graph trial
+        mode = "eager"
     if ps.is_worker:
         trainer = Trainer(model, ps, loss_fn, use_graph=mode != "eager", overlap_wgrad=not args.no_wgrad_stream,
                           branch_streams=not args.no_branch_streams, overlap_comm=not args.no_overlap)
