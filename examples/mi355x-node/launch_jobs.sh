@@ -33,12 +33,12 @@ if [ "$TINY" = 1 ]; then
       "--ps-mode colocated --batch-size 2 --steps 1 --warmup 1" tony.ps.instances=1 tony.worker.instances=2
 else
   run "Inception-v3 TF-PS, 1 ps + 4 workers" inception_ps.py "--steps 20" \
-      tony.ps.instances=1 tony.worker.instances=4 tony.worker.gpus=1
+      tony.ps.instances=1 tony.worker.instances=4 tony.worker.gpus=1 tony.worker.memory=32g
   run "Horovod ResNet-50 bf16, 8 workers" hvd_resnet50.py "--steps 20" \
-      tony.application.framework=horovod tony.ps.instances=0 tony.worker.instances=8 tony.worker.gpus=1
+      tony.application.framework=horovod tony.ps.instances=0 tony.worker.instances=8 tony.worker.gpus=1 tony.worker.memory=32g
 fi
 run "MNIST PyTorch DDP, $W workers" mnist_pytorch_ddp.py "--steps-per-epoch 20" \
-    tony.application.framework=pytorch tony.ps.instances=0 tony.worker.instances=$W tony.worker.gpus=1
+    tony.application.framework=pytorch tony.ps.instances=0 tony.worker.instances=$W tony.worker.gpus=1 tony.worker.memory=32g
 run "MXNet linreg dist_sync, 1 server + $W workers" mxnet_linreg.py "--kvstore dist_sync --epochs 1" \
     tony.application.framework=mxnet tony.scheduler.instances=1 tony.server.instances=1 \
     tony.worker.instances=$W tony.ps.instances=0

@@ -7,7 +7,7 @@ through ``hvd.DistributedOptimizer``: its bucketed all-reduce (RCCL over xGMI) o
 pass and the update is one fused HIP SGD launch per flat buffer.  Reports images/sec over all ranks.
 
   tony --src_dir tony_amd/jobs --executes hvd_resnet50.py --conf tony.application.framework=horovod \
-       --conf tony.worker.instances=8 --conf tony.worker.gpus=1
+       --conf tony.worker.instances=8 --conf tony.worker.gpus=1 --conf tony.worker.memory=32g
 """
 from __future__ import annotations
 

@@ -22,7 +22,7 @@ resumes from the newest step complete on every rank.  ``--fail-at-step S`` is a 
 first session, worker 1 exits at step S (the TEST_WORKER_TERMINATION idea, mid-training).
 
   tony --src_dir tony_amd/jobs --executes inception_ps.py --conf tony.ps.instances=1 \
-       --conf tony.worker.instances=4 --conf tony.worker.gpus=1
+       --conf tony.worker.instances=4 --conf tony.worker.gpus=1 --conf tony.worker.memory=32g
 """
 from __future__ import annotations
 

@@ -9,7 +9,8 @@ in one flat buffer, bucketed all-reduce launched from the backward hooks, so com
 the rest of the backward), SGD-momentum.  Reports images/sec over all ranks.
 
   tony --src_dir tony_amd/jobs --executes resnet50_ddp.py --conf tony.application.framework=pytorch \
-       --conf tony.worker.instances=8 --conf tony.worker.gpus=1 --conf tony.ps.instances=0
+       --conf tony.worker.instances=8 --conf tony.worker.gpus=1 --conf tony.ps.instances=0 \
+       --conf tony.worker.memory=32g
 """
 from __future__ import annotations
 
