@@ -150,6 +150,11 @@ def main(argv=None) -> int:
                start_step=start, steps=total)
     log(f"{float(rate):.1f} images/sec total over {workers} workers ({mode} PS)")
     dist.barrier()
+    # orderly shutdown: drain the device (side streams included) and tear the process group down before
+    # interpreter exit -- one run of this job aborted (exit 134) after reporting, during teardown
+    if on_gpu:
+        torch.cuda.synchronize()
+    dist.destroy_process_group()
     return 0
 
 
