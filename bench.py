@@ -12,8 +12,11 @@ One process per GPU (torch.distributed.run, RCCL over xGMI).  Two PS topologies:
     (parallel/buckets.py).
 ``--ps-mode dedicated``
     the paper topology: rank 0 is the ps task (owns the fp32 variables, runs no model), ranks
-    1..N-1 are workers; per bucket push = reduce to the ps, apply on the ps, pull = broadcast.
-    Images/sec counts the N-1 workers' images only.
+    1..N-1 are workers.  Data plane (parallel/ps_plane.py): workers store each bucket's gradient
+    straight into the ps GPU's receive window as backward produces it, the ps applies the fused
+    optimizer as the rows land and stores the new variables straight into every worker's landing
+    window (TONY_PS_PLANE=rccl: reduce / apply / broadcast per bucket instead).  Images/sec counts
+    the N-1 workers' images only.
 
 Compute is bf16 NHWC with the tony_amd HIP kernels (fused BN+ReLU, MFMA implicit-GEMM convs, fused
 heads, fused softmax-xent, fused optimizer); the step is issued eagerly (weight gradients on a side
@@ -123,11 +126,43 @@ def diagnose(world: int, rank: int, dev, backend: str, shared_ok: bool) -> dict:
     allp = [None] * world
     dist.all_gather_object(allp, me)
     info["devices"] = [a["bdf"] for a in allp]
+    # RCCL's transport per rank (P2P over xGMI vs SHM / NET fallbacks), from its INIT,P2P debug log:
+    # the channels of the ring/tree are connected by the collectives above
+    tr = _rccl_transport()
+    allt = [None] * world
+    dist.all_gather_object(allt, tr)
+    info["transport"] = allt
     if len({a["bdf"] for a in allp}) != world and not shared_ok:
         raise SystemExit(fail(f"ranks share a GPU ({info['devices']}): each rank must own one device"))
     if backend != "nccl" and not shared_ok:
         raise SystemExit(fail(f"process group backend is {backend!r}, not RCCL"))
     return info
+
+
+_RCCL_LOG = [None]
+
+
+def _rccl_debug_env(world: int) -> None:
+    """Ask RCCL for its INIT,P2P log in a private file (unless the user set NCCL_DEBUG themselves)."""
+    if world > 1 and "NCCL_DEBUG" not in os.environ:
+        path = f"/tmp/tony_rccl_{os.getpid()}.log"
+        os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_SUBSYS="INIT,P2P", NCCL_DEBUG_FILE=path)
+        _RCCL_LOG[0] = path
+
+
+def _rccl_transport() -> dict:
+    """{transport: channel connections} parsed from RCCL's "... via P2P/IPC" lines (None: no log)."""
+    path = _RCCL_LOG[0]
+    if path is None or not os.path.exists(path):
+        return {}
+    out = {}
+    with open(path, errors="replace") as f:
+        for line in f:
+            if " via " not in line:
+                continue
+            kind = line.split(" via ", 1)[1].split()[0] if line.split(" via ", 1)[1].split() else "?"
+            out[kind] = out.get(kind, 0) + 1
+    return out
 
 
 def _heartbeat(t0: float, every_s: float = 45.0) -> None:
@@ -165,6 +200,8 @@ def main():
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
     diag = {}
+    if world > 1 and backend == "nccl":
+        _rccl_debug_env(world)
     if world > 1:
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
         diag = diagnose(world, rank, dev, dist.get_backend(), rehearsal)
@@ -333,7 +370,7 @@ def main():
         if args.ps_mode == "colocated":
             par = f"ps-colocated-sharded dp{world} (1 PS shard + 1 worker per GPU, sync)"
         else:
-            par = f"ps-dedicated 1 ps + {n_workers} workers (sync)"
+            par = f"ps-dedicated 1 ps + {n_workers} workers (sync, {ps.plane_kind} data plane)"
         rec = {
             "metric": "images/sec (whole node) Inception-v3 TF-PS" if args.model == "inception_v3"
             else "images/sec (whole node) ResNet-50",
@@ -388,6 +425,8 @@ def main():
     rc = 0
     if os.environ.get("TONY_COLLECTIVE", "rccl").lower() in ("hip", "xgmi") and fallbacks:
         rc = fail(f"TONY_COLLECTIVE=xgmi requested but {fallbacks} collectives fell back to RCCL")
+    if ps.plane is not None:
+        ps.plane.close()
     if world > 1:
         dist.destroy_process_group()
     return rc

@@ -89,7 +89,11 @@ def run(rank, world, port, q, kind, bucket_mb):
         dist.barrier()
         dist.destroy_process_group()
         # by value: a tensor would travel as a shared-memory handle that dies with this process
-        q.put((rank, {k: {kk: vv.numpy() if isinstance(vv, torch.Tensor) else vv for kk, vv in v.items()}
-                      for k, v in out.items()}))
+        from tony_amd.parallel import collectives as coll
+
+        res = {k: {kk: vv.numpy() if isinstance(vv, torch.Tensor) else vv for kk, vv in v.items()}
+               for k, v in out.items()}
+        res["fallbacks"] = coll.fallback_count()
+        q.put((rank, res))
     except Exception:  # noqa: BLE001 - reported to the parent
         q.put((rank, {"error": traceback.format_exc()}))

@@ -652,3 +652,68 @@ def test_task_monitor_memory_limit(monkeypatch):
                         memory_limit_bytes=256 << 20)
     mon.refresh()
     assert len(faults) == 1 and "memory limit" in faults[0] and mon.fault_code == C.EXIT_MEMORY_LIMIT
+
+
+def test_flat_sgd_resync_reseeds_master_from_changed_compute_copy():
+    """FlatSGD(resync=True): elements of the bf16 compute copy changed outside the optimizer re-seed the
+    fp32 master before the update (the CPU form of csrc/optim.hip's resync); untouched ones keep it."""
+    import torch
+
+    from tony_amd.ops.optim import FlatSGD
+
+    master = torch.linspace(-1, 1, 16)
+    opt = FlatSGD(master.clone(), lr=0.5, momentum=0.0, resync=True)
+    cur = opt.w.to(torch.bfloat16)
+    cur[3] = 7.0  # e.g. load_state_dict into the module
+    g = torch.ones(16)
+    before = opt.w.clone()
+    opt.step(g, out_bf16=cur)
+    assert opt.w[3].item() == 7.0 - 0.5
+    keep = [i for i in range(16) if i != 3]
+    assert torch.allclose(opt.w[keep], before[keep] - 0.5)
+
+
+def test_gpu_pinning_env_modes():
+    """what each visible-devices mode exports.  none (default) keeps every GPU visible for
+    RCCL P2P / peer-memory mapping and names the task's GPUs by HIP ordinal; hip / rocr hide the rest."""
+    from tony_amd.cluster.coordinator import gpu_pinning_env
+    from tony_amd.conf import Configuration
+    from tony_amd.conf import keys as K
+    from tony_amd.native import GpuDevice
+
+    assert Configuration().get(K.AMD_VISIBLE_DEVICES_MODE) == "none"
+    devs = [GpuDevice(i, bdf=f"0000:{0x10 * (i + 1):02x}:00.0", numa_node=0, fake=True) for i in range(8)]
+    hip_ord = {0: 3, 1: 2, 2: 1, 3: 0, 4: 4, 5: 5, 6: 6, 7: 7}  # amd-smi order != HIP order
+    e = gpu_pinning_env("none", [1], hip_ord, devs)
+    assert e["TONY_HIP_ORDINALS"] == "2" and e["TONY_GPU_BDFS"] == "0000:20:00.0" and e["TONY_VISIBLE_MODE"] == "none"
+    assert "HIP_VISIBLE_DEVICES" not in e and "ROCR_VISIBLE_DEVICES" not in e
+    e = gpu_pinning_env("hip", [0, 5], hip_ord, devs)
+    assert e["HIP_VISIBLE_DEVICES"] == "3,5" and "ROCR_VISIBLE_DEVICES" not in e
+    e = gpu_pinning_env("rocr", [2], hip_ord, devs)
+    assert e["ROCR_VISIBLE_DEVICES"] == "1" and "HIP_VISIBLE_DEVICES" not in e
+    with pytest.raises(ValueError):
+        gpu_pinning_env("cuda", [0], hip_ord, devs)
+
+
+def test_verify_visible_device_in_all_visible_mode(monkeypatch):
+    """visible-devices-mode none: the task's device is TONY_HIP_ORDINALS[0]; picking any other ordinal, or
+    an ordinal whose BDF is not the allocated GPU's, raises."""
+    from types import SimpleNamespace
+
+    import torch
+
+    from tony_amd.gpu.inventory import verify_visible_device
+
+    props = {2: SimpleNamespace(pci_domain_id=0, pci_bus_id=0x20, pci_device_id=0),
+             5: SimpleNamespace(pci_domain_id=0, pci_bus_id=0x60, pci_device_id=0)}
+    monkeypatch.setattr(torch.cuda, "get_device_properties", lambda i: props[i])
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    monkeypatch.setenv("TONY_VISIBLE_MODE", "none")
+    monkeypatch.setenv("TONY_HIP_ORDINALS", "2")
+    monkeypatch.setenv("TONY_GPU_BDFS", "0000:20:00.0")
+    assert verify_visible_device(2) == "0000:20:00.0"
+    with pytest.raises(RuntimeError, match="not among this task's GPUs"):
+        verify_visible_device(5)
+    monkeypatch.setenv("TONY_GPU_BDFS", "0000:21:00.0")
+    with pytest.raises(RuntimeError, match="does not select the allocated GPU"):
+        verify_visible_device(2)

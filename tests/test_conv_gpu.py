@@ -270,10 +270,14 @@ def test_conv_bn_act_pool_fused_matches_unfused(cuda, shape):
 
 # (N, H, W, (R, S), stride, (ph, pw), Cout): Inception-v3's 3x3/2 stem (shrunk in N and H/W, with a
 # partial last workgroup and workgroups straddling two images), ResNet's 7x7/2 p3 stem (5 K steps,
-# 3 wgrad column groups) and a padded 3x3/2 stem (stride-1 stems are not taken: conv.stem_supported)
+# 3 wgrad column groups) at 45x33 / 56x56 / 64x64 (the whole-model test's shape) / 224x224, and
+# padded 3x3 stems at stride 2 and stride 1.  Images taller than 63 rows with padding are the case
+# the round-2 K-padding-column bug read outside the staged rows (csrc/stem.hip tap_word).
 STEM_SHAPES = [(2, 299, 299, (3, 3), 2, (0, 0), 32), (3, 37, 41, (3, 3), 2, (0, 0), 32),
                (2, 45, 33, (7, 7), 2, (3, 3), 64), (4, 64, 64, (3, 3), 2, (1, 1), 32),
-               (3, 56, 56, (7, 7), 2, (3, 3), 64)]
+               (3, 56, 56, (7, 7), 2, (3, 3), 64), (4, 64, 64, (7, 7), 2, (3, 3), 64),
+               (2, 224, 224, (7, 7), 2, (3, 3), 64), (4, 64, 64, (3, 3), 1, (1, 1), 32),
+               (2, 80, 72, (3, 3), 1, (1, 1), 64)]
 
 
 @pytest.mark.parametrize("shape", STEM_SHAPES, ids=[f"{s[1]}x{s[2]}k{s[3][0]}s{s[4]}c{s[6]}" for s in STEM_SHAPES])
@@ -305,6 +309,55 @@ def test_stem_fwd_wgrad_mfma(cuda, shape):
     slot = _nhwc(torch.ones_like(wt))
     assert stem_wgrad(dy, x, wt.shape, s, p, dst=slot) is None
     assert _rel(slot.float() - 1.0, wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("shape", STEM_SHAPES[3:], ids=[f"{s[1]}x{s[2]}k{s[3][0]}s{s[4]}p{s[5][0]}" for s in STEM_SHAPES[3:]])
+def test_stem_ignores_nan_outside_the_image(cuda, shape):
+    """Regression for the round-2 stem bug: the padded stem must never read an element outside the image.
+    The image sits inside a NaN-filled allocation (global memory around it is NaN) and an all-NaN image
+    of the same shape runs first (the staged-row LDS of every CU is left full of NaN).  Any read outside
+    the input's in-image taps then shows up as a non-finite output row or statistic."""
+    from tony_amd.ops import _lib
+    from tony_amd.ops.conv import stem_fwd, stem_wgrad
+
+    n, h, w, k, s, p, co = shape
+    torch.manual_seed(5)
+    numel = n * h * w * 3
+    pad = 64 * 1024  # elements of NaN on each side (more than the widest tap reach)
+    buf = torch.full((numel + 2 * pad,), float("nan"), dtype=torch.bfloat16, device=cuda)
+    x = buf[pad:pad + numel].view(n, h, w, 3).permute(0, 3, 1, 2)  # channels_last view inside the NaN sea
+    x.copy_(torch.randn(n, 3, h, w, device=cuda))
+    assert x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0
+    wt = _nhwc(0.2 * torch.randn(co, 3, *k, device=cuda)).to(torch.bfloat16)
+    poison = torch.full_like(x, float("nan")).contiguous(memory_format=torch.channels_last)
+    stem_fwd(poison, wt, s, p, torch.zeros(_lib.stat_floats(co), device=cuda))  # NaN into the LDS staging
+    stats = torch.zeros(_lib.stat_floats(co), device=cuda)
+    y = stem_fwd(x, wt, s, p, stats)
+    torch.cuda.synchronize()
+    assert torch.isfinite(y.float()).all(), "stem forward read outside the image"
+    assert torch.isfinite(stats).all(), "stem statistics read outside the image"
+    ref = torch.nn.functional.conv2d(x.float(), wt.float(), None, s, p)
+    assert _rel(y, ref) < 1e-2
+    dy = _nhwc(torch.randn_like(ref)).to(torch.bfloat16)
+    stem_wgrad(dy, poison, wt.shape, s, p)  # NaN into the wgrad kernel's LDS
+    dw = stem_wgrad(dy, x, wt.shape, s, p)
+    assert torch.isfinite(dw).all(), "stem weight gradient read outside the image"
+    wr = wt.float().requires_grad_(True)
+    torch.nn.functional.conv2d(x.float(), wr, None, s, p).backward(dy.float())
+    assert _rel(dw, wr.grad) < 1e-2
+
+
+def test_fused_relu_propagates_nan(cuda):
+    """The fused BN+ReLU keeps a NaN a NaN (torch.relu semantics): an upstream NaN must surface as a
+    non-finite activation, not as the silent all-zero output fmaxf(NaN, 0) = 0 produced in round 2."""
+    from tony_amd.ops.bn import bn_act
+
+    x = _nhwc(torch.randn(2, 16, 4, 4, device=cuda)).to(torch.bfloat16)
+    x[0, 3, 1, 1] = float("nan")
+    g, b = torch.ones(16, device=cuda), torch.zeros(16, device=cuda)
+    y = bn_act(x, g, b, None, None, True, 0.1, 1e-5, True)
+    assert torch.isnan(y[:, 3].float()).all(), "NaN in channel 3's statistics must reach its outputs"
+    assert torch.isfinite(y[:, 2].float()).all()
 
 
 def test_stem_conv_bn_act_layer_fwd_bwd(cuda):

@@ -145,6 +145,18 @@ def test_inception_ps_colocated_tiny(conf):
     assert len(ms) == 1 and ms[0]["workers"] == 2 and ms[0]["ps_mode"] == "colocated"
 
 
+def test_inception_ps_dedicated_tiny(conf):
+    """The paper topology (1 ps + 2 workers, the ps owning the variables) through the launcher.  The ps
+    task and the workers must issue matching collective sequences (per-step bucket reduce / broadcast,
+    the timing barrier, the rate all-reduce): a mismatch hangs or corrupts the gloo group."""
+    rc, client, h = run_job(conf, "inception_ps.py", ["tony.ps.instances=1", "tony.worker.instances=2"],
+                            "--ps-mode dedicated --batch-size 2 --image-size 299 --steps 2 --warmup 1")
+    assert rc == 0, _diag(client)
+    ms = _metrics(client)
+    assert len(ms) == 1 and ms[0]["workers"] == 2 and ms[0]["ps_mode"] == "dedicated"
+    assert ms[0]["images_per_sec"] > 0
+
+
 def test_cluster_discovery(conf):
     rc, client, _ = run_job(conf, "cluster_discovery.py", ["tony.head.instances=1", "tony.worker.instances=1",
                                                            "tony.ps.instances=0"])

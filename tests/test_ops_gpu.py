@@ -413,11 +413,37 @@ def test_resnet50_fused_matches_stock(cuda):
     ref.load_state_dict({k: v.float() for k, v in sd.items()})
     stock16.load_state_dict(sd)
     x = _nhwc(torch.randn(4, 3, 64, 64, device=cuda))
+    # per-layer outputs (stem, every bottleneck), so that a failure names the first layer that diverged
+    acts = {}
+
+    def hook(tag, name):
+        def f(_m, _inp, out):
+            acts.setdefault(tag, {})[name] = out.detach().float()
+        return f
+
+    handles = []
+    for tag, m in (("k", fused), ("r", ref), ("s", stock16)):
+        handles.append(m.stem.register_forward_hook(hook(tag, "stem")))
+        for i, b in enumerate(m.blocks):
+            handles.append(b.register_forward_hook(hook(tag, f"block{i}")))
     yk, yr, ys = fused(x.to(torch.bfloat16)), ref(x), stock16(x.to(torch.bfloat16))
+    for h in handles:
+        h.remove()
+
+    def layer_report():
+        rows = []
+        for name, r in acts["r"].items():
+            k, s_ = acts["k"][name], acts["s"][name]
+            rows.append(f"{name}: |k|={k.norm():.3g} |ref|={r.norm():.3g} finite={bool(torch.isfinite(k).all())} "
+                        f"rel_k={((k - r).norm() / r.norm()).item():.3f} rel_s={((s_ - r).norm() / r.norm()).item():.3f}")
+        return "\n".join(rows)
+
+    for name, k in acts["k"].items():
+        assert torch.isfinite(k).all(), f"non-finite fused output at {name}\n{layer_report()}"
     assert torch.isfinite(yk.float()).all()
     rel_k = ((yk.float() - yr).norm() / yr.norm()).item()
     rel_s = ((ys.float() - yr).norm() / yr.norm()).item()
-    assert rel_k < 1.5 * rel_s + 0.02, f"fused {rel_k:.3f} vs stock-bf16 {rel_s:.3f} (rel err to fp32)"
+    assert rel_k < 1.5 * rel_s + 0.02, f"fused {rel_k:.3f} vs stock-bf16 {rel_s:.3f} (rel err to fp32)\n{layer_report()}"
     for m, y in ((fused, yk), (ref, yr), (stock16, ys)):
         y.float().sum().backward()
     gr = ref.stem.conv.weight.grad

@@ -42,9 +42,14 @@ def test_ps_overlap_one_rank_matches_serial(cuda, kind):
     assert log.index("launch:0") < max(i for i, e in enumerate(log) if e.startswith("ready:"))
 
 
-@pytest.mark.parametrize("kind", ["A"])
-def test_two_ranks_overlap_ps_and_ddp(cuda, kind):
+@pytest.mark.parametrize("kind,collective", [("A", "rccl"), ("A", "hip")], ids=["gloo", "xgmi-kernels"])
+def test_two_ranks_overlap_ps_and_ddp(cuda, kind, collective, monkeypatch):
+    """collective=hip: the colocated PS push / pull and DDP's bucket all-reduce run on the xGMI
+    peer-memory kernels (TONY_COLLECTIVE=hip routes every data plane through parallel/collectives.py;
+    gloo then only carries the window-handle exchange)."""
     import overlap_worker as W
+
+    monkeypatch.setenv("TONY_COLLECTIVE", collective)
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -62,6 +67,8 @@ def test_two_ranks_overlap_ps_and_ddp(cuda, kind):
     for r in range(world):
         assert "error" not in out[r], out[r]["error"]
         for v in out[r].values():
+            if not isinstance(v, dict):
+                continue
             for k in ("params", "grad"):
                 if k in v:
                     v[k] = torch.from_numpy(v[k])
@@ -77,3 +84,5 @@ def test_two_ranks_overlap_ps_and_ddp(cuda, kind):
     assert d0["launches"] == d0["n_buckets"] and d0["overlapped"] >= d0["n_buckets"] - 1
     assert torch.equal(d0["grad"], d1["grad"])                    # averaged gradients identical on both ranks
     assert d0["grad"].abs().sum().item() > 0
+    if collective == "hip":
+        assert out[0]["fallbacks"] == 0 and out[1]["fallbacks"] == 0, "a collective fell back to gloo"

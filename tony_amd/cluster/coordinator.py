@@ -67,6 +67,30 @@ def _default_history_root(conf, staging_root: str) -> str:
     return loc
 
 
+def gpu_pinning_env(mode: str, gpus, hip_ordinal, devices) -> dict:
+    """Environment that pins a task to its GPUs (SURVEY §7.4 hard part 6: isolation vs P2P).
+
+    ``none`` (default): every GPU stays visible, so RCCL keeps its xGMI P2P transport and the tony_amd
+    data planes can map peer memory (hipIpcOpenMemHandle needs the peer device in the process);
+    the task's GPUs are named by their HIP ordinals in TONY_HIP_ORDINALS and parallel/bootstrap.py
+    selects the first one (``torch.cuda.set_device``).  ``hip`` / ``rocr``: HIP_VISIBLE_DEVICES /
+    ROCR_VISIBLE_DEVICES hide every other GPU (hard isolation; a data plane that needs a peer's
+    memory cannot run).  Either way TONY_GPU_BDFS lets the task verify it got the GPU it was
+    allocated (gpu/inventory.verify_visible_device)."""
+    mode = (mode or "none").lower()
+    if mode not in ("none", "hip", "rocr"):
+        raise ValueError(f"tony.amd.visible-devices-mode must be none, hip or rocr, not {mode!r}")
+    ordinals = ",".join(str(hip_ordinal.get(g, g)) for g in gpus)
+    devs = {d.index: d for d in devices}
+    env = {"TONY_GPU_BDFS": ",".join(devs[g].bdf for g in gpus if g in devs), "TONY_VISIBLE_MODE": mode,
+           "TONY_HIP_ORDINALS": ordinals}
+    if mode == "hip":
+        env[C.HIP_VISIBLE_DEVICES] = ordinals
+    elif mode == "rocr":
+        env[C.ROCR_VISIBLE_DEVICES] = ordinals
+    return env
+
+
 class Coordinator:
     def __init__(self, conf_path: str, job_dir: str, app_id: str, started_ms: Optional[int] = None):
         self.conf_path = conf_path
@@ -398,6 +422,8 @@ class Coordinator:
             env[C.TONY_TOKEN_FILE] = os.path.join(self.job_dir, "token")
         # data-plane collectives of the tony_amd jobs: RCCL or the xGMI peer-memory kernels
         env["TONY_COLLECTIVE"] = c.get(K.AMD_COLLECTIVE, "rccl").lower()
+        # whether the ps tasks own GPUs (the Inception PS job picks its topology from it on every task)
+        env["TONY_PS_GPUS"] = str(c.get_int("tony.ps.gpus", 0))
         if slot is not None and slot.gpus:
             ids = ",".join(str(g) for g in slot.gpus)
             task.gpus = list(slot.gpus)
@@ -406,14 +432,8 @@ class Coordinator:
             env[C.TONY_NUMA_NODE] = str(slot.numa_node)
             if slot.cpus and c.get_bool(K.AMD_NUMA_BIND, True):
                 env["TONY_CPUS"] = ",".join(str(x) for x in slot.cpus)
-            mode = c.get(K.AMD_VISIBLE_DEVICES_MODE, "hip").lower()
-            ordinals = ",".join(str(self.hip_ordinal.get(g, g)) for g in slot.gpus)
-            devs = {d.index: d for d in self.allocator.devices}
-            env["TONY_GPU_BDFS"] = ",".join(devs[g].bdf for g in slot.gpus if g in devs)
-            if mode == "hip":
-                env[C.HIP_VISIBLE_DEVICES] = ordinals
-            elif mode == "rocr":
-                env[C.ROCR_VISIBLE_DEVICES] = ordinals
+            env.update(gpu_pinning_env(c.get(K.AMD_VISIBLE_DEVICES_MODE, "none"), slot.gpus, self.hip_ordinal,
+                                       self.allocator.devices))
             task.info.gpus = ids
         if c.get_bool(K.DOCKER_ENABLED, False):
             image = c.get(K.docker_image_key(task.job_name)) or c.get(K.DOCKER_CONTAINERS_IMAGE, "")

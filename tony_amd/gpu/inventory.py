@@ -119,16 +119,30 @@ def verify_visible_device(device_index: int = 0) -> Optional[str]:
     """In a task: the BDF torch/HIP sees for ``device_index`` vs the one the coordinator pinned
     (TONY_GPU_BDFS, same order as HIP_VISIBLE_DEVICES).  Returns the BDF; raises on a mismatch."""
     want = [b for b in os.environ.get("TONY_GPU_BDFS", "").split(",") if b]
-    if not want or os.environ.get("HIP_VISIBLE_DEVICES") is None:
+    if not want:
+        return None
+    mode = os.environ.get("TONY_VISIBLE_MODE") or ("hip" if os.environ.get("HIP_VISIBLE_DEVICES") is not None
+                                                   else "")
+    if mode in ("hip", "rocr"):
+        pos = device_index  # the task sees only its GPUs, in allocation order
+    elif mode == "none":   # every GPU visible: the task's GPUs are the ordinals the coordinator named
+        ords = [int(o) for o in os.environ.get("TONY_HIP_ORDINALS", "").split(",") if o.strip()]
+        if device_index not in ords:
+            raise RuntimeError(f"HIP device {device_index} is not among this task's GPUs {ords} "
+                               "(TONY_HIP_ORDINALS)")
+        pos = ords.index(device_index)
+    else:
+        return None
+    if pos >= len(want):
         return None
     import torch
 
     p = torch.cuda.get_device_properties(device_index)
     got = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
-    exp = _norm_bdf(want[device_index])
+    exp = _norm_bdf(want[pos])
     if exp.rsplit(".", 1)[0] != got.rsplit(".", 1)[0]:
         raise RuntimeError(f"HIP device {device_index} is {got} but the coordinator pinned {exp}: "
-                           "HIP_VISIBLE_DEVICES does not select the allocated GPU")
+                           f"the {mode} pinning does not select the allocated GPU")
     return got
 
 

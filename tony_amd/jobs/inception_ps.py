@@ -9,8 +9,13 @@ variables and apply the optimizer, workers push gradients and pull variables eve
     = the fused HIP SGD on the shard's fp32 master copy, pull = all-gather.  The ``ps`` tasks of
     the cluster spec do what a TF ps does once the graph is placed -- ``server.join()`` -- and are
     stopped by the coordinator when training ends (ps is untracked by default).
-``--ps-mode dedicated``
-    The ps task(s) join the group and own the variables (give them GPUs: tony.ps.gpus=1).
+``--ps-mode dedicated`` (default when the ps tasks have a GPU: ``tony.ps.gpus`` >= 1, exported to
+    every task as TONY_PS_GPUS)
+    The ps task(s) join the group and own the variables.  On GPUs the data plane is the xGMI one of
+    parallel/ps_plane.py: workers store gradients straight into the ps GPU's receive windows, the ps
+    applies the fused optimizer as they land and stores the new variables straight into every
+    worker's landing window.  ``--async`` gives TF's default asynchronous PS (each push applied on
+    arrival).
 
 The step (forward, loss, backward, push/apply/pull) runs eagerly with the bucketed push/apply/pull
 overlapped with backward, or replayed as a HIP graph (``--graph``).
@@ -56,12 +61,15 @@ def main(argv=None) -> int:
     ap.add_argument("--checkpoint-dir", default=None, help="default: <job dir>/inception_ps")
     ap.add_argument("--save-steps", type=int, default=0, help="checkpoint every K steps (0: never)")
     ap.add_argument("--fail-at-step", type=int, default=-1, help="test hook (session 0, worker 1)")
+    ap.add_argument("--async", dest="async_ps", action="store_true",
+                    help="asynchronous PS (dedicated mode): every worker push applied on its own on arrival")
     a = ap.parse_args(argv)
     tc = TFConfig.from_env()
     on_gpu = torch.cuda.is_available()
     mode = a.ps_mode
     if mode == "auto":  # every task must decide the same way: only from the shared conf / env
-        mode = os.environ.get("TONY_PS_MODE", "colocated" if on_gpu else "dedicated")
+        ps_gpus = int(os.environ.get("TONY_PS_GPUS", "0") or 0)
+        mode = os.environ.get("TONY_PS_MODE") or ("dedicated" if ps_gpus > 0 or not on_gpu else "colocated")
     if mode == "colocated":
         if tc.task_type == "ps":
             log("colocated PS: variables are sharded over the worker GPUs; ps task joins (waits) until stopped")
@@ -78,7 +86,10 @@ def main(argv=None) -> int:
         torch.backends.cudnn.benchmark = True
     model = cast_model(inception_v3(fused=on_gpu, seed=0), dtype, dev).to(memory_format=torch.channels_last)
     ps = ParameterServer(model, optimizer="sgd", lr=0.045, momentum=0.9, weight_decay=4e-5, mode=mode,
-                         ps_ranks=tc.ps_ranks if mode == "dedicated" else (0,), dtype=dtype, device=dev)
+                         ps_ranks=tc.ps_ranks if mode == "dedicated" else (0,), dtype=dtype, device=dev,
+                         sync=not (a.async_ps and mode == "dedicated"))
+    if mode == "dedicated" and not ps.sync and ps.plane is None:
+        raise SystemExit("--async needs the xGMI PS data plane (GPU ranks)")
 
     def loss_fn(out, y):
         logits, aux = out if isinstance(out, tuple) else (out, None)
@@ -109,15 +120,31 @@ def main(argv=None) -> int:
             st["rng_cuda"] = torch.cuda.get_rng_state(dev)
         ckpt.save(step, st, force=force)
 
+    # Every rank issues the same sequence of collectives on the default group: the per-step PS
+    # collectives (RCCL plane: each bucket's reduce / broadcast), ONE barrier at the first timed
+    # step, then the rate all-reduce and the closing barrier.  (The ps task used to run only the
+    # per-step collectives and one barrier: its sequence did not match the workers'.)
+    timed_from = max(start, a.warmup)
     if mode == "dedicated" and ps.is_ps and not ps.is_worker:
-        for s in range(start, total):  # the ps task: reduce -> apply -> broadcast, bucket by bucket
+        for s in range(start, total):  # the ps task: apply bucket by bucket as the pushes land
+            if s == timed_from:
+                dist.barrier()
             ps.step()
             if ckpt.should_save(s + 1):
                 save(s + 1)
         if a.save_steps:
             save(total, force=True)
             ckpt.wait()
+        if on_gpu:
+            torch.cuda.synchronize()
+        if ps.plane is not None:
+            ps.plane.check_error()
+        rate = torch.zeros(1, dtype=torch.float64, device=dev if on_gpu else "cpu")
+        dist.all_reduce(rate)  # the workers' images/sec sum (the ps adds none)
         dist.barrier()
+        if ps.plane is not None:
+            ps.plane.close()
+        dist.destroy_process_group()
         return 0
 
     trainer = Trainer(model, ps, loss_fn, use_graph=on_gpu and a.graph)
@@ -130,7 +157,7 @@ def main(argv=None) -> int:
                 and tc.task_index == 1:
             log(f"test hook: worker 1 fails at step {s}")
             os._exit(17)
-        if s == max(start, a.warmup):
+        if s == timed_from:
             dist.barrier()
             tp.start()
         loss = trainer.step(x, y)
@@ -154,6 +181,9 @@ def main(argv=None) -> int:
     # interpreter exit -- one run of this job aborted (exit 134) after reporting, during teardown
     if on_gpu:
         torch.cuda.synchronize()
+    if ps.plane is not None:
+        ps.plane.check_error()
+        ps.plane.close()
     dist.destroy_process_group()
     return 0
 

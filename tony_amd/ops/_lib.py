@@ -113,6 +113,20 @@ _SIGNATURES = {
     "tony_avgpool_bwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
     "tony_transpose_desc_bytes": [],
     "tony_transpose_batch": [c_void_p, c_int, c_int, c_void_p],
+    # parameter-server data plane over xGMI windows (csrc/ps_plane.hip, parallel/ps_plane.py)
+    "tony_ps_header_bytes": [],
+    "tony_ps_max_buckets": [],
+    "tony_ps_max_blocks": [],
+    "tony_ps_land_entry_bytes": [],
+    "tony_ps_window_alloc": [c_int64, c_void_pp, c_u8_p],
+    "tony_ps_push": [c_void_p, c_int, c_void_p, c_int64, c_int, c_int64, c_int, c_int, ctypes.c_uint32, c_int,
+                     c_void_p],
+    "tony_ps_apply": [c_void_p, c_int64, c_int64, c_int, c_int, c_int64, c_int64, c_void_p, c_void_p, c_void_p,
+                      c_void_p, c_int, c_u64_p, c_void_p, c_int, c_int, ctypes.c_uint32, c_int, ctypes.c_double,
+                      c_int, c_void_p],
+    "tony_ps_land": [c_void_p, c_void_p, c_int, c_void_p, c_int, ctypes.c_uint32, ctypes.c_double, c_void_p],
+    "tony_ps_error_async": [c_void_p, c_void_p, c_void_p],
+    "tony_ps_error": [c_void_p, c_int_p],
     # xGMI peer-memory collectives (csrc/xgmi.hip, parallel/xgmi.py)
     "tony_xgmi_max_ranks": [],
     "tony_xgmi_handle_bytes": [],

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 from typing import Callable, Dict, Tuple
 
 import torch
@@ -55,7 +56,7 @@ def supported(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, dilati
     """Whether the tony kernels take this conv (``min_rows``: fewest output pixels, default MIN_ROWS)."""
     if not HOST_MEMO:
         return _supported(x, weight, stride, padding, dilation, groups, min_rows)
-    key = (x.shape, x.dtype, x.device.type, weight.shape, weight.dtype, _pair(stride), _pair(padding), _pair(dilation),
+    key = (x.shape, x.dtype, x.device, weight.shape, weight.dtype, _pair(stride), _pair(padding), _pair(dilation),
            groups, min_rows)
     r = _SUP_CACHE.get(key)
     if r is None:
@@ -87,10 +88,6 @@ def stem_supported(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, d
     """Whether the MFMA stem kernels (csrc/stem.hip) take this conv: dense NHWC bf16 input with fewer
     than 8 channels (an image), 32 or 64 output channels, padding smaller than the filter."""
     (ph, pw) = _pair(padding)
-    # strided stems only (every image stem of the reference models is stride 2): a stride-1 padded
-    # 3x3 stem produced non-finite rows on MI355X (tools/stem_check.py) and is left to MIOpen
-    if min(_pair(stride)) < 2:
-        return False
     return (x.is_cuda and x.dtype == _BF16 and weight.dtype == _BF16 and x.dim() == 4 and groups == 1
             and _pair(dilation) == (1, 1) and 0 < x.shape[1] < 8 and weight.shape[0] in (32, 64)
             and weight.shape[1] == x.shape[1] and ph < weight.shape[2] and pw < weight.shape[3]
@@ -124,7 +121,8 @@ def conv_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: 
     """Y = conv(x, w); with ``stats`` (zeroed, ``_lib.stat_floats(Cout)`` floats) the epilogue accumulates
     [sum | sumsq] of Y into its STAT_SHARDS copies.  ``vflags``: tile variant bits (None: autotuned)."""
     if HOST_MEMO and vflags is None:  # steady state: the shape's geometry and tuned variant are memoised
-        plan = _FWD_PLAN.get((x.shape, x.stride(), weight.shape, stride, padding, stats is not None))
+        plan = _FWD_PLAN.get((x.shape, x.stride(), x.dtype, x.device, weight.shape, weight.stride(), weight.dtype,
+                              stride, padding, stats is not None))
         if plan is not None and x.data_ptr() % 16 == 0:
             n, h, w, C, ldx, co, r, s, sh, sw, ph, pw, oh, ow, vf = plan
             y = _cl_empty(n, co, oh, ow, x.device)
@@ -136,7 +134,8 @@ def conv_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: 
             return y
     if x.shape[1] < 8:  # image stem (csrc/stem.hip)
         return stem_fwd(x, weight, stride, padding, stats)
-    key0 = (x.shape, x.stride(), weight.shape, stride, padding, stats is not None)
+    key0 = (x.shape, x.stride(), x.dtype, x.device, weight.shape, weight.stride(), weight.dtype, stride, padding,
+            stats is not None)
     x, (_, C, ldx) = _as_rows(x)
     n, _, h, w = x.shape
     co, _, r, s = weight.shape
@@ -157,13 +156,16 @@ def conv_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: 
         if vflags is None:  # first call of this shape: time the variants (statistics into a scratch buffer)
             scratch = torch.zeros(_lib.stat_floats(co), device=x.device) if stats is not None else None
             vflags = tune.pick(key, lambda vf: launch(vf, scratch))
-        if HOST_MEMO and key0[1] == x.stride() and not torch.cuda.is_current_stream_capturing():
+        if (HOST_MEMO and key0[1] == x.stride() and x.dtype == _BF16 and weight.dtype == _BF16
+                and not torch.cuda.is_current_stream_capturing()):
             _FWD_PLAN[key0] = (n, h, w, C, ldx, co, r, s, sh, sw, ph, pw, oh, ow, vflags)
     _lib.check(launch(vflags, stats), "tony_conv_fwd")
     return y
 
 
-_FWD_PLAN: Dict[Tuple, Tuple] = {}  # conv_fwd: (x shape, x strides, w shape, stride, padding, stats) -> launch geometry
+# conv_fwd: (x shape / strides / dtype / device, w shape / strides / dtype, stride, padding, stats) -> launch
+# geometry.  Everything the geometry or the kernel's operand contract depends on is in the key.
+_FWD_PLAN: Dict[Tuple, Tuple] = {}
 
 
 def stem_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: torch.Tensor | None = None):
@@ -770,21 +772,21 @@ def conv_bn_act(x, weight, gamma, beta, running_mean, running_var, stride=1, pad
 
 
 # ------------------------------------------------------------------------------ inference --
-_AFF: Dict[int, Tuple] = {}
+_AFF: "weakref.WeakKeyDictionary[torch.Tensor, Tuple]" = weakref.WeakKeyDictionary()
 
 
 def folded_bn(gamma, beta, running_mean, running_var, eps) -> torch.Tensor:
-    """[scale | shift] fp32 of an inference BatchNorm (y = z * scale + shift), cached until any of
-    the four tensors changes (their version counters)."""
-    key = id(gamma)
-    ver = (gamma._version, beta._version, running_mean._version, running_var._version, float(eps),
-           gamma.data_ptr(), running_var.data_ptr())
-    hit = _AFF.get(key)
-    if hit is not None and hit[0] == ver:
+    """[scale | shift] fp32 of an inference BatchNorm (y = z * scale + shift), cached per gamma TENSOR
+    (weak key: a new module's gamma never hits an old entry, even at a recycled id / address) until
+    any of the four tensors changes (the identity of the other three and all version counters)."""
+    ver = (beta._version, running_mean._version, running_var._version, gamma._version, float(eps),
+           id(beta), id(running_mean), id(running_var), gamma.data_ptr(), running_var.data_ptr())
+    hit = _AFF.get(gamma)
+    if hit is not None and hit[0] == ver and hit[2]() is beta and hit[3]() is running_var:
         return hit[1]
     scale = gamma.float() * torch.rsqrt(running_var.float() + eps)
     aff = torch.cat([scale, beta.float() - running_mean.float() * scale]).contiguous()
-    _AFF[key] = (ver, aff)
+    _AFF[gamma] = (ver, aff, weakref.ref(beta), weakref.ref(running_var))
     return aff
 
 

@@ -213,7 +213,7 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
     for (int j = 0; j < 8; ++j) {
       float t = fmaf(f[j], sc[j], sh[j]);
       if (RES) t += q[j];
-      f[j] = relu ? fmaxf(t, 0.f) : t;
+      f[j] = relu ? relu_f(t) : t;
     }
     store8(yb + row * ldyt, bf16x8::from_float(f));
   };
@@ -645,7 +645,7 @@ __global__ __launch_bounds__(kThreads) void bn_relu_maxpool_kernel(
       raw.to_float(f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float v = bf2f(f2bf(fmaxf(fmaf(f[j], sc[j], sh[j]), 0.f)));  // the bf16 activation
+        const float v = bf2f(f2bf(relu_f(fmaf(f[j], sc[j], sh[j]))));  // the bf16 activation
         if (v > best[j] || (v != v)) {
           best[j] = v;
           bi[j] = idx;

@@ -36,6 +36,10 @@ __device__ __forceinline__ int64_t shard_off(int idx, int64_t sstride) {
   return sstride == 0 ? 0 : static_cast<int64_t>(idx % kStatShards) * sstride;
 }
 
+// ReLU that keeps a NaN a NaN (torch.relu semantics).  fmaxf(NaN, 0) is 0 on CDNA (IEEE maxNum), which
+// once turned a NaN produced upstream into a silently all-zero activation instead of a visible error.
+__device__ __forceinline__ float relu_f(float t) { return t < 0.f ? 0.f : t; }
+
 __device__ __forceinline__ float bf2f(uint16_t v) {
   return __uint_as_float(static_cast<uint32_t>(v) << 16);
 }

@@ -220,7 +220,7 @@ __device__ __forceinline__ void nt_epilogue(f32x4 (&acc)[TM][TN], uint16_t* smem
         for (int r = 0; r < 4; ++r) {
           const int row = wm * WM + i * 16 + (lane >> 4) * 4 + r;
           const float v = fmaf(acc[i][j][r], sc, sh);
-          Cs[row * LDC + col] = f2bf(relu ? fmaxf(v, 0.f) : v);
+          Cs[row * LDC + col] = f2bf(relu ? relu_f(v) : v);
         }
     }
   } else {

@@ -9,9 +9,14 @@
 //
 // Hyper-parameters live in a small device array `hp` (not kernel arguments) so
 // a captured HIP graph replays with the current learning rate / step.
-//   SGD  hp = [lr, momentum, weight_decay, grad_scale, nesterov]
+//   SGD  hp = [lr, momentum, weight_decay, grad_scale, nesterov, resync]
+//        resync != 0 (with a bf16 compute copy): an element whose compute copy no longer equals
+//        bf16(master) was overwritten outside the optimizer (load_state_dict, a Horovod
+//        broadcast_parameters from rank 0, a checkpoint restore into the module) and its master is
+//        re-seeded from it before the update -- one extra 2-byte read per parameter
 //   Adam hp = [lr, beta1, beta2, eps, weight_decay, grad_scale, bias_corr1, bias_corr2, decoupled]
 #include "common.h"
+#include "optim_math.h"
 
 using namespace tony;
 
@@ -50,6 +55,7 @@ __global__ __launch_bounds__(kThreads) void sgd_kernel(float* __restrict__ w, fl
                                                        const float* __restrict__ hp) {
   const float lr = hp[0], mu = hp[1], wd = hp[2], gs = hp[3];
   const bool nesterov = hp[4] != 0.f;
+  const bool resync = hp[5] != 0.f && w_bf16 != nullptr;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
   for (int64_t q = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; q < n4; q += stride) {
     const int64_t i = q * 4;
@@ -59,13 +65,15 @@ __global__ __launch_bounds__(kThreads) void sgd_kernel(float* __restrict__ w, fl
     float4 vv = *reinterpret_cast<float4*>(v + i);
     float wf[4] = {wv.x, wv.y, wv.z, wv.w};
     float vf[4] = {vv.x, vv.y, vv.z, vv.w};
+    if (resync) {
+      const uint2 cv = *reinterpret_cast<const uint2*>(w_bf16 + i);
+      const uint16_t cur[4] = {static_cast<uint16_t>(cv.x & 0xffffu), static_cast<uint16_t>(cv.x >> 16),
+                               static_cast<uint16_t>(cv.y & 0xffffu), static_cast<uint16_t>(cv.y >> 16)};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const float gk = fmaf(gf[k], gs, wd * wf[k]);
-      vf[k] = fmaf(mu, vf[k], gk);
-      const float upd = nesterov ? fmaf(mu, vf[k], gk) : vf[k];
-      wf[k] = fmaf(-lr, upd, wf[k]);
+      for (int k = 0; k < 4; ++k)
+        if (cur[k] != f2bf(wf[k])) wf[k] = bf2f(cur[k]);
     }
+    sgd_update4(wf, vf, gf, lr, mu, wd, gs, nesterov);
     *reinterpret_cast<float4*>(w + i) = make_float4(wf[0], wf[1], wf[2], wf[3]);
     *reinterpret_cast<float4*>(v + i) = make_float4(vf[0], vf[1], vf[2], vf[3]);
     if (w_bf16 != nullptr) store_bf16x4(w_bf16 + i, wf);
@@ -94,18 +102,7 @@ __global__ __launch_bounds__(kThreads) void adam_kernel(float* __restrict__ w, f
     float wf[4] = {wv.x, wv.y, wv.z, wv.w};
     float mf[4] = {mv.x, mv.y, mv.z, mv.w};
     float vf[4] = {vv.x, vv.y, vv.z, vv.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float gk = gf[k] * gs;
-      if (decoupled)
-        wf[k] *= (1.f - lr * wd);
-      else
-        gk = fmaf(wd, wf[k], gk);
-      mf[k] = fmaf(b1, mf[k], (1.f - b1) * gk);
-      vf[k] = fmaf(b2, vf[k], (1.f - b2) * gk * gk);
-      const float denom = sqrtf(vf[k]) * inv_sqrt_bc2 + eps;
-      wf[k] = fmaf(-step_size, mf[k] / denom, wf[k]);
-    }
+    adam_update4(wf, mf, vf, gf, lr, b1, b2, eps, wd, gs, step_size, inv_sqrt_bc2, decoupled);
     *reinterpret_cast<float4*>(w + i) = make_float4(wf[0], wf[1], wf[2], wf[3]);
     *reinterpret_cast<float4*>(m + i) = make_float4(mf[0], mf[1], mf[2], mf[3]);
     *reinterpret_cast<float4*>(v + i) = make_float4(vf[0], vf[1], vf[2], vf[3]);

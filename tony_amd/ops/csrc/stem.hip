@@ -140,9 +140,16 @@ struct Pix {
 };
 
 // GEMM column k inside a pixel's receptive field, packed in one word: element offset (bits 0-19),
-// tap row r (20-25), tap column s (26-31); r = 63 marks a padding column (k >= K).
+// tap row r (20-25), tap column s (26-31).  A K-padding column (k >= K) aliases tap (0, 0): it
+// passes the same image-bounds check as a real tap, so it reads either a real, finite input
+// element (which the zero weight column cancels) or nothing.  It used to be marked r = 63 and
+// skipped only when iy0 + 63 >= H -- for images taller than 63 rows with padding that let pixels of
+// the first output rows read the element at input row -ph, outside the staged LDS range (or before
+// x), and a NaN found there survived the zero weight (NaN * 0 = NaN) into the BN statistics; the
+// fused BN + ReLU then turned the whole activation into zeros (fmaxf(NaN, 0) = 0): the round-2
+// "fused ResNet-50 forward collapses to 0" failure of tests/test_ops_gpu.py.
 __device__ __forceinline__ uint32_t tap_word(const StemGeom& g, int k) {
-  if (k >= g.K) return 63u << 20;
+  if (k >= g.K) return 0u;
   const int sc = g.S * g.C;
   const int r = k / sc, rem = k - r * sc;
   const int s = rem / g.C;
@@ -151,8 +158,8 @@ __device__ __forceinline__ uint32_t tap_word(const StemGeom& g, int k) {
 }
 
 // NP (no padding): every tap of an output pixel lies inside the image, so the gather is one add and
-// one load; the K-padding columns (k >= K) read the pixel's own tap-(0, 0) value, which the zero
-// weight columns (forward) cancel and the weight gradient never stores.
+// one load.  Either way the K-padding columns (k >= K) read the pixel's own tap-(0, 0) value, which
+// the zero weight columns (forward) cancel and the weight gradient never stores.
 template <bool NP>
 __device__ __forceinline__ uint16_t tap_value(const StemGeom& g, const uint16_t* src, const Pix& p, uint32_t t) {
   if constexpr (NP) return p.ok ? src[p.base + static_cast<int>(t & 0xfffffu)] : static_cast<uint16_t>(0);

@@ -126,7 +126,9 @@ __device__ __forceinline__ void copy16(uint8_t* dst, const uint8_t* src, int64_t
     reinterpret_cast<uint4*>(dst)[v] = reinterpret_cast<const uint4*>(src)[v];
 }
 
-// dst vectors [v0,v1) = scale * (own[v] + sum over peers p of row p of this rank's slot at off)
+// dst vectors [v0,v1) = scale * (sum over ranks p of row p of this rank's slot at off, own input for
+// p == rank).  The terms are added in rank order on every rank, so a one-shot all-reduce gives
+// bit-identical results everywhere (data-parallel replicas must not drift apart).
 template <bool BF16>
 __device__ void reduce_rows(const Comm& c, uint32_t epoch, const uint8_t* own, int64_t row_bytes, int64_t off,
                             uint8_t* dst, int64_t v0, int64_t v1, float scale) {
@@ -134,10 +136,10 @@ __device__ void reduce_rows(const Comm& c, uint32_t epoch, const uint8_t* own, i
   const uint8_t* base = slot(c, c.rank, 0, epoch) + off;
   for (int64_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
     float acc[E::kVec], f[E::kVec];
-    E::load(own + v * 16, acc);
+#pragma unroll
+    for (int j = 0; j < E::kVec; ++j) acc[j] = 0.f;
     for (int p = 0; p < c.nranks; ++p) {
-      if (p == c.rank) continue;
-      E::load(base + p * row_bytes + v * 16, f);
+      E::load(p == c.rank ? own + v * 16 : base + p * row_bytes + v * 16, f);
 #pragma unroll
       for (int j = 0; j < E::kVec; ++j) acc[j] += f[j];
     }

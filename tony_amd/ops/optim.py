@@ -70,16 +70,21 @@ class _FlatOptimizer:
 class FlatSGD(_FlatOptimizer):
     """SGD with (Nesterov) momentum: v = mu*v + g + wd*w ; w -= lr*v (TF MomentumOptimizer semantics)."""
 
-    n_hp = 5
+    n_hp = 6
 
-    def __init__(self, master, lr, momentum=0.9, weight_decay=0.0, nesterov=False):
+    def __init__(self, master, lr, momentum=0.9, weight_decay=0.0, nesterov=False, resync=False):
         super().__init__(master, lr, weight_decay)
         self.momentum = float(momentum)
         self.nesterov = bool(nesterov)
+        # resync: the bf16 compute copy (``out_bf16``) is the parameters users see and may overwrite
+        # (load_state_dict, broadcast_parameters); elements changed there re-seed the fp32 master
+        # before the update (csrc/optim.hip sgd_kernel).  Off for the PS, whose masters are the truth.
+        self.resync = bool(resync)
         self.v = torch.zeros_like(master)
 
     def _hp_values(self):
-        return [self.lr, self.momentum, self.weight_decay, self.grad_scale, 1.0 if self.nesterov else 0.0]
+        return [self.lr, self.momentum, self.weight_decay, self.grad_scale, 1.0 if self.nesterov else 0.0,
+                1.0 if self.resync else 0.0]
 
     def apply_range(self, grad: torch.Tensor, lo: int = 0, out_bf16: torch.Tensor | None = None):
         """Update master elements [lo, lo + grad.numel()) (one bucket of a sharded PS) with ``grad``;
@@ -94,6 +99,9 @@ class FlatSGD(_FlatOptimizer):
             _lib.check(rc, "tony_sgd_step")
             return
         w, v = self.w[lo:lo + n], self.v[lo:lo + n]
+        if self.resync and out_bf16 is not None:
+            changed = out_bf16 != w.to(out_bf16.dtype)
+            w.copy_(torch.where(changed, out_bf16.float(), w))
         g = grad.float() * self.grad_scale + self.weight_decay * w
         v.mul_(self.momentum).add_(g)
         upd = g + self.momentum * v if self.nesterov else v

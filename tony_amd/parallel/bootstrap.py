@@ -34,11 +34,17 @@ def default_backend() -> str:
 
 
 def pick_device(local_rank: int) -> torch.device:
-    """The task's GPU.  With per-task HIP_VISIBLE_DEVICES the task sees one device (index 0)."""
+    """The task's GPU: the first of TONY_HIP_ORDINALS when the launcher pinned it with every GPU
+    visible (visible-devices-mode none, the default), else ``local_rank`` (index 0 under a per-task
+    HIP_VISIBLE_DEVICES, or torchrun's LOCAL_RANK)."""
     if not torch.cuda.is_available():
         return torch.device("cpu")
     n = torch.cuda.device_count()
-    dev = torch.device("cuda", local_rank % n)
+    ords = [int(o) for o in os.environ.get("TONY_HIP_ORDINALS", "").split(",") if o.strip()]
+    if ords and os.environ.get("TONY_VISIBLE_MODE", "none") == "none" and ords[0] < n:
+        dev = torch.device("cuda", ords[0])
+    else:
+        dev = torch.device("cuda", local_rank % n)
     torch.cuda.set_device(dev)
     from ..gpu.inventory import verify_visible_device
 

@@ -233,12 +233,24 @@ class GradBucketEngine:
             if h is not None:
                 h.remove()
 
-    def end(self) -> None:
-        """Launch the remaining buckets in order and make the current stream wait for all of them."""
+    def end(self, finish: Optional[Callable[[], None]] = None) -> None:
+        """Launch the remaining buckets in order, then ``finish`` (enqueued on the communication stream
+        after every bucket: e.g. the PS plane's landing of the new variables), and make the current
+        stream wait for all of it."""
         self._drop_inplace_hooks()
         for b in self.buckets:
             if not b.launched:
                 self._launch(b)
         self.armed = False
+        if finish is not None:
+            if self.comm is None:
+                finish()
+            else:
+                cur = torch.cuda.current_stream(self.device)
+                torch.cuda.set_stream(self.comm)
+                try:
+                    finish()
+                finally:
+                    torch.cuda.set_stream(cur)
         if self.comm is not None:
             torch.cuda.current_stream(self.device).wait_stream(self.comm)

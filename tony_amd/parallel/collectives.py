@@ -93,12 +93,23 @@ def all_gather_flat(out: torch.Tensor, inp: torch.Tensor, group=None, async_op=F
     return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
 
 
-def all_reduce(t: torch.Tensor, op=None, group=None, async_op=False):
+def all_reduce(t: torch.Tensor, op=None, group=None, async_op=False, average: bool = False):
+    """Sum (``average``: mean) of ``t`` over the ranks, in place.  TONY_COLLECTIVE=hip runs it on the
+    xGMI kernels (one launch; the average is a scale inside the reduction), else RCCL (AVG op) / gloo
+    (SUM, then a scale)."""
     if world(group) == 1:
         return None
     x = _xgmi(t, group) if op in (None, dist.ReduceOp.SUM) else None
     if x is not None and t.is_contiguous():
-        x.all_reduce(t)
+        x.all_reduce(t, average=average)
+        return None
+    if average:
+        if op not in (None, dist.ReduceOp.SUM):
+            raise ValueError("average=True is a SUM scaled by 1/world")
+        if not _is_gloo(group):
+            return dist.all_reduce(t, op=dist.ReduceOp.AVG, group=group, async_op=async_op)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        t.mul_(1.0 / world(group))
         return None
     return dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=group, async_op=async_op)
 

@@ -30,7 +30,6 @@ import contextlib
 from typing import List, Optional
 
 import torch
-import torch.distributed as dist
 
 from . import collectives as coll
 from .buckets import DEFAULT_BUCKET_MB, Bucket, GradBucketEngine, make_buckets
@@ -80,20 +79,21 @@ class BucketedAllReduce:
         self.engine.begin(overlap=self._active)
         torch.autograd.Variable._execution_engine.queue_callback(self.finish)
 
-    def _scale_needed(self) -> bool:
-        return self.average and (dist.get_backend(self.group) != "nccl" or self.predivide != 1.0)
-
     def _launch(self, b: Bucket) -> None:
-        """Enqueue bucket b's all-reduce (the communication stream is current on the GPU)."""
+        """Enqueue bucket b's all-reduce (the communication stream is current on the GPU).  Goes through
+        parallel/collectives.py, so TONY_COLLECTIVE=hip (tony.amd.collective) runs it on the xGMI
+        kernels and RCCL stays the A/B baseline; a fallback to RCCL is counted there."""
         g = self.flat.grad[b.lo:b.hi]
         wire = g.to(self.compression) if self.compression is not None and g.dtype != self.compression else g
-        op = dist.ReduceOp.AVG if self.average and not self._scale_needed() else dist.ReduceOp.SUM
         if self.predivide != 1.0:
             if wire is g:
                 wire = g.clone()
             wire.mul_(1.0 / self.predivide)
-        dist.all_reduce(wire, op=op, group=self.group, async_op=True).wait()  # the comm stream waits, not the host
-        if self._scale_needed():
+        plain_avg = self.average and self.predivide == 1.0
+        work = coll.all_reduce(wire, group=self.group, async_op=True, average=plain_avg)
+        if work is not None:
+            work.wait()  # the comm stream waits, not the host
+        if self.average and not plain_avg:
             wire.mul_(self.predivide / self.world)
         if wire is not g:
             g.copy_(wire)

@@ -381,8 +381,18 @@ class _DistributedOptimizer:
 
             g = optimizer.param_groups[0]
             for flat, _ in self.groups:
-                self._fused.append((flat, FlatSGD(flat.data.float().clone(), g["lr"], momentum=g["momentum"],
-                                                  weight_decay=g["weight_decay"], nesterov=g["nesterov"])))
+                # an fp32 flat buffer IS the master (nothing to keep in sync); a bf16 one gets an fp32
+                # master that re-seeds from any element changed behind the optimizer's back (resync)
+                master = flat.data if flat.data.dtype == torch.float32 else flat.data.float().clone()
+                self._fused.append((flat, FlatSGD(master, g["lr"], momentum=g["momentum"],
+                                                  weight_decay=g["weight_decay"], nesterov=g["nesterov"],
+                                                  resync=master is not flat.data)))
+            # torch-SGD state index of every parameter -> (flat buffer, slot)
+            slot_of = {}
+            for fi, (flat, _) in enumerate(self.groups):
+                for slot, p in zip(flat.slots, flat.params):
+                    slot_of[id(p)] = (fi, slot)
+            self._slots = [slot_of.get(id(p)) for p in optimizer.param_groups[0]["params"]]
 
     # torch.optim.Optimizer surface
     @property
@@ -394,10 +404,42 @@ class _DistributedOptimizer:
         return self.optimizer.state
 
     def state_dict(self):
-        return self.optimizer.state_dict()
+        """torch.optim.SGD's state_dict format; with the fused apply the momentum buffers are views of
+        the flat fp32 momentum (the wrapped optimizer never steps, so its own state is empty)."""
+        sd = self.optimizer.state_dict()
+        if not self._fused:
+            return sd
+        state = {}
+        for i, fs in enumerate(self._slots):
+            if fs is None:  # a frozen parameter: no state
+                continue
+            fi, slot = fs
+            opt = self._fused[fi][1]
+            if opt.step_count and self.optimizer.param_groups[0]["momentum"]:
+                state[i] = {"momentum_buffer": slot.view(opt.v).clone()}
+        sd["state"] = state
+        return sd
 
     def load_state_dict(self, sd):
         self.optimizer.load_state_dict(sd)
+        if not self._fused:
+            return
+        g = self.optimizer.param_groups[0]
+        for fi, (_, opt) in enumerate(self._fused):
+            opt.v.zero_()
+            opt.lr, opt.momentum, opt.weight_decay = g["lr"], g["momentum"], g["weight_decay"]
+        for i, st in sd.get("state", {}).items():
+            buf = st.get("momentum_buffer") if isinstance(st, dict) else None
+            if buf is None:
+                continue
+            fs = self._slots[int(i)]
+            if fs is None:
+                continue
+            fi, slot = fs
+            opt = self._fused[fi][1]
+            with torch.no_grad():
+                slot.view(opt.v).copy_(buf.to(device=opt.v.device, dtype=torch.float32))
+            opt.step_count = max(opt.step_count, 1)
 
     def zero_grad(self, set_to_none: bool = False):  # noqa: ARG002 - grads are views of the flat buffers
         for flat, _ in self.groups:
@@ -415,11 +457,10 @@ class _DistributedOptimizer:
         g = self.optimizer.param_groups[0]  # lr schedules edit the wrapped optimizer's group
         for flat, opt in self._fused:
             opt.lr, opt.momentum, opt.weight_decay = g["lr"], g["momentum"], g["weight_decay"]
-            if flat.data.dtype == torch.bfloat16:
-                opt.step(flat.grad, out_bf16=flat.data)
+            if opt.w is flat.data:
+                opt.step(flat.grad)  # fp32: updated in place
             else:
-                opt.step(flat.grad)
-                flat.data.copy_(opt.w)
+                opt.step(flat.grad, out_bf16=flat.data)
         return loss
 
     def __getattr__(self, name):

@@ -23,11 +23,16 @@ Only the last bucket (the stem's gradients) is exposed after backward.
     pull  = in-place ``all_gather`` of the bucket's pieces into every worker's flat parameters.
 ``mode="dedicated"``
     The paper topology (1 ps + N workers).  PS ranks own the variables and run no model; bucket b
-    belongs to ps task ``b % n_ps`` (round-robin placement, ``replica_device_setter``).  Per
-    bucket: push = ``reduce`` of the bucket to its owner, apply on the owner, pull = ``broadcast``
-    from the owner.  ``sync=False`` gives TF's default *asynchronous* PS: each worker's push is
-    applied on arrival (point-to-point send/recv, the PS polls the outstanding receives) and the
-    worker pulls the post-apply variables.
+    belongs to ps task ``b % n_ps`` (round-robin placement, ``replica_device_setter``).
+    ``plane="xgmi"`` (default on GPUs, parallel/ps_plane.py + csrc/ps_plane.hip): per bucket the
+    workers store their gradients straight into the owner's IPC-mapped receive rows (push), the
+    owner GPU applies the fused optimizer chunk by chunk as the rows land and stores the new
+    variables straight into every worker's landing window (apply + pull in one kernel), and each
+    worker copies its landing window into its parameters after backward.  ``sync=False`` gives TF's
+    default *asynchronous* PS on the same plane: every worker's push is applied on its own as it
+    arrives and lands only in that worker's window.  ``plane="rccl"`` (and CPU / gloo runs): push =
+    ``reduce`` to the owner, apply, pull = ``broadcast``; async = point-to-point send/recv of the
+    whole flat gradient with the PS polling the outstanding receives.
 
 Gradients are averaged over workers (TF SyncReplicasOptimizer semantics) by the optimizer's
 ``grad_scale``.  ``wire_dtype=torch.float32`` pushes and sums fp32 gradients (the reference TF job
@@ -36,6 +41,7 @@ is fp32 end to end) even when the gradient buffer the kernels accumulate into is
 from __future__ import annotations
 
 import math
+import os
 import time
 from typing import Dict, List, Optional
 
@@ -71,7 +77,8 @@ class ParameterServer:
     def __init__(self, model: torch.nn.Module, optimizer: str = "sgd", lr: float = 0.1, momentum: float = 0.9,
                  weight_decay: float = 0.0, mode: str = "colocated", sync: bool = True, ps_ranks=(0,),
                  group=None, dtype=torch.bfloat16, device=None, wire_dtype: Optional[torch.dtype] = None,
-                 bucket_mb: float = DEFAULT_BUCKET_MB, bucketed_single: bool = False, **opt_kw):
+                 bucket_mb: float = DEFAULT_BUCKET_MB, bucketed_single: bool = False, plane: str = "auto",
+                 **opt_kw):
         self.mode = mode
         self.sync = sync
         self.group = group
@@ -136,15 +143,32 @@ class ParameterServer:
             if self.is_ps:
                 opt = make_optimizer(optimizer, f.data.float().clone(), lr, momentum, weight_decay, **opt_kw)
                 self.optimizers[self.rank] = opt
+        if plane == "auto":
+            plane = os.environ.get("TONY_PS_PLANE", "xgmi" if f.device.type == "cuda" else "rccl")
+        self.plane_kind = plane if mode == "dedicated" and self.world > 1 else "rccl"
+        if self.plane_kind not in ("xgmi", "rccl"):
+            raise ValueError(f"unknown PS data plane {plane!r}")
+        if self.plane_kind == "xgmi" and f.device.type != "cuda":
+            raise ValueError("the xGMI PS data plane needs GPU tensors")
+        self.plane = None
+        if self.plane_kind == "xgmi":
+            from .ps_plane import XgmiPSPlane
+
+            if not sync:
+                for opt in self.optimizers.values():
+                    opt.grad_scale = 1.0  # async: every push is applied on its own
+            self.plane = XgmiPSPlane(f, self.buckets, self._owner, self.ps_ranks, self.worker_ranks, self.rank,
+                                     self.wire_dtype, group=group, sync=sync)
         self._wire = None
-        if self.world > 1 and self.wire_dtype != f.grad.dtype:
+        if self.world > 1 and self.wire_dtype != f.grad.dtype and self.plane is None:
             self._wire = torch.zeros(f.numel, dtype=self.wire_dtype, device=f.device)
         self.engine = GradBucketEngine(f, self.buckets, self._launch)
         # one rank: nothing to communicate, so nothing to overlap -- the step is ONE fused apply over
         # the whole shard after backward, with no per-parameter readiness bookkeeping on the host
         # (``bucketed_single`` keeps the bucket engine: tests of the overlap machinery on one GPU)
         self.single = mode == "colocated" and self.world == 1 and not bucketed_single
-        if (mode == "colocated" or sync) and not self.single:
+        if (mode == "colocated" or sync or self.plane is not None) and not self.single and \
+                not (self.plane is not None and not self.is_worker):
             self.engine.attach()
 
     # -- helpers ---------------------------------------------------------------
@@ -166,6 +190,10 @@ class ParameterServer:
     def begin_step(self, overlap: bool = True):
         """Arm the bucket engine before the forward: with ``overlap`` each bucket's push/apply/pull is
         enqueued as soon as backward completes its gradients."""
+        if self.plane is not None:
+            if self.is_worker:
+                self.engine.begin(overlap)  # pushes launch from backward; the ps's hp go out in step()
+            return
         if self.mode == "dedicated" and not self.sync:
             return
         for opt in self.optimizers.values():
@@ -180,6 +208,10 @@ class ParameterServer:
 
     def step(self):
         """Finish push (gradients) -> apply (fused optimizer on the PS) -> pull (variables)."""
+        if self.plane is not None:
+            self._step_plane()
+            self.steps += 1
+            return
         if self.mode == "dedicated" and not self.sync:
             self._step_dedicated_async_worker()
             self.steps += 1
@@ -202,6 +234,29 @@ class ParameterServer:
         """Buckets of the last step whose communication was issued while backward was running."""
         return self.engine.launched_during_backward
 
+    def _step_plane(self):
+        """One step on the xGMI data plane.  Worker: the remaining pushes, then the landing of every
+        bucket's new variables (on the communication stream), joined into the compute stream.  PS:
+        the previous step's applies must be done before this step's hyper-parameters go to the
+        device (Adam's bias corrections change every step), then one apply per owned bucket, in
+        bucket order -- each waits on the GPU for its rows, so the host is not in the loop."""
+        pl = self.plane
+        if self.is_worker:
+            if not self.engine.armed:
+                self.engine.begin(False)
+            self.engine.end(finish=lambda: pl.land(self.steps))
+            return
+        torch.cuda.current_stream(self.flat.device).synchronize()
+        opt = self.optimizers.get(self.rank)
+        if opt is None:
+            return
+        opt.begin_step()
+        for b in self.buckets:
+            if self._owner(b) == self.rank:
+                m, _ = self._master_range[b.index]
+                pl.apply(b, self.steps, opt, m, local_params=self.flat.data)
+        pl.end_step()
+
     def _wire_grad(self, b: Bucket) -> torch.Tensor:
         g = self.flat.grad[b.lo:b.hi]
         if self._wire is not None:
@@ -213,6 +268,9 @@ class ParameterServer:
     def _launch(self, b: Bucket):
         """Enqueue bucket b's push / apply / pull (the communication stream is current)."""
         f = self.flat
+        if self.plane is not None:  # worker: straight into the owner's receive rows (push)
+            self.plane.push(b, self.steps)
+            return
         opt = self.optimizers.get(self.rank)
         if self.mode == "colocated":
             m, p = self._master_range[b.index]
@@ -308,7 +366,10 @@ class ParameterServer:
         return sd
 
     def load_state_dict(self, sd):
-        if sd.get("layout") is not None and sd["layout"] != self.layout():
+        if sd.get("layout") is None:
+            raise ValueError("PS checkpoint has no 'layout' record (an older format whose shard order cannot be "
+                             "verified): refusing to load it")
+        if sd["layout"] != self.layout():
             raise ValueError(f"PS checkpoint layout {sd['layout']} does not match this job's {self.layout()}")
         self.steps = int(sd["steps"])
         self.flat.data.copy_(sd["flat"])
