@@ -717,3 +717,23 @@ def test_verify_visible_device_in_all_visible_mode(monkeypatch):
     monkeypatch.setenv("TONY_GPU_BDFS", "0000:21:00.0")
     with pytest.raises(RuntimeError, match="does not select the allocated GPU"):
         verify_visible_device(2)
+
+
+def test_gpu_task_memory_sized_when_left_at_default():
+    """a GPU jobtype whose memory is the 2g default gets 32g per GPU (a PyTorch-ROCm rank alone
+    exceeds 2 GB RSS and the agent enforces the limit); explicit values and CPU jobtypes are untouched."""
+    from tony_amd.conf import Configuration
+    from tony_amd.utils import core as U
+
+    c = Configuration()
+    c.set("tony.worker.instances", "2")
+    c.set("tony.worker.gpus", "2")
+    c.set("tony.ps.instances", "1")
+    c.set("tony.evaluator.instances", "1")
+    c.set("tony.evaluator.gpus", "1")
+    c.set("tony.evaluator.memory", "8g")
+    changed = U.size_gpu_task_memory(c)
+    assert changed == {"worker": 65536}
+    reqs = U.parse_container_requests(c)
+    assert reqs["worker"].memory_mb == 65536 and reqs["ps"].memory_mb == 2048 and reqs["evaluator"].memory_mb == 8192
+    assert "<name>tony.worker.memory</name>" in c.to_xml()

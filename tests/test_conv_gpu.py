@@ -360,6 +360,46 @@ def test_fused_relu_propagates_nan(cuda):
     assert torch.isfinite(y[:, 2].float()).all()
 
 
+@pytest.mark.parametrize("shape", [(4, 64, 64), (2, 224, 224)], ids=["64", "224"])
+def test_resnet_stem_conv_bn_relu_padded_pool_fused(cuda, shape):
+    """ResNet's stem as ONE conv + BN + ReLU + 3x3/2 p1 max-pool fusion (MFMA stem kernel + the padded
+    bn_relu_maxpool kernel) == conv_bn_act then the padded max pool (outputs, running stats, gradients)."""
+    from tony_amd.ops import _lib
+    from tony_amd.ops.conv import conv_bn_act, conv_bn_act_pool
+    from tony_amd.ops.pool import max_pool
+
+    n, h, w = shape
+    co = 64
+    torch.manual_seed(9)
+    x0 = _nhwc(torch.randn(n, 3, h, w, device=cuda)).to(torch.bfloat16)
+    w0 = _nhwc(torch.randn(co, 3, 7, 7, device=cuda) / (3 * 49) ** 0.5).to(torch.bfloat16)
+    g0 = (torch.rand(co, device=cuda) + 0.5)
+    b0 = torch.randn(co, device=cuda) * 0.1
+
+    def run(fused):
+        _lib.set_inplace_grads(False)
+        wt = torch.nn.Parameter(w0.clone())
+        g, b = torch.nn.Parameter(g0.clone()), torch.nn.Parameter(b0.clone())
+        rm, rv = torch.zeros(co, device=cuda), torch.ones(co, device=cuda)
+        if fused:
+            y = conv_bn_act_pool(x0, wt, g, b, rm, rv, 2, 3, 0.1, 1e-5, 3, 2, 1)
+        else:
+            y = max_pool(conv_bn_act(x0, wt, g, b, rm, rv, 2, 3, True, 0.1, 1e-5, True), 3, 2, padding=1)
+        gy = torch.randn(y.shape, device=cuda, generator=torch.Generator(device=cuda).manual_seed(3))
+        (y.float() * gy).sum().backward()
+        _lib.set_inplace_grads(True)
+        return y.detach().float(), rm, rv, wt.grad.float(), g.grad.float(), b.grad.float()
+
+    fu, ref = run(True), run(False)
+    assert fu[0].shape == (n, co, (h // 2 + 1) // 2, (w // 2 + 1) // 2)
+    assert torch.isfinite(fu[0]).all()
+    assert torch.equal(fu[0], ref[0]), "pooled outputs differ"
+    torch.testing.assert_close(fu[1], ref[1], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(fu[2], ref[2], rtol=1e-5, atol=1e-6)
+    for a, b, what in zip(fu[3:], ref[3:], ("dw", "dgamma", "dbeta")):
+        assert _rel(a, b) < 2e-2, f"{what} rel {_rel(a, b):.4f}"
+
+
 def test_stem_conv_bn_act_layer_fwd_bwd(cuda):
     """The fused ConvBNAct layer on a 3-channel input (MFMA stem forward + wgrad, no MIOpen) vs fp32."""
     from tony_amd.ops import _lib

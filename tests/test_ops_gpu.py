@@ -242,6 +242,25 @@ def test_maxpool(cuda, shape):
     _close(x.grad, xr.grad, 1e-2, 1e-2, "maxpool bwd")
 
 
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (2, 64, 56, 56), (3, 16, 9, 7), (2, 8, 4, 4)])
+def test_maxpool_padded(cuda, shape):
+    """max_pool2d(x, 3, 2, padding=1) (ResNet's stem pool) on the tony kernel: forward bit-exact against
+    torch (padded taps never win), backward through the argmax."""
+    from tony_amd.ops.pool import max_pool
+
+    torch.manual_seed(8)
+    x = _nhwc(torch.randn(shape, device=cuda)).to(torch.bfloat16)
+    x = _nhwc(x).requires_grad_(True)
+    y = max_pool(x, 3, 2, padding=1)
+    xr = x.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.max_pool2d(xr, 3, 2, 1)
+    assert y.shape == yr.shape and torch.equal(y.float(), yr)
+    dy = _nhwc(torch.randn(yr.shape, device=cuda)).to(torch.bfloat16)
+    y.backward(dy)
+    yr.backward(dy.float())
+    _close(x.grad, xr.grad, 1e-2, 1e-2, "padded maxpool bwd")
+
+
 @pytest.mark.parametrize("cfg", [((4, 768, 17, 17), 5, 3), ((3, 2048, 8, 8), 8, 1), ((2, 16, 9, 7), 3, 2),
                                  ((2, 64, 1, 1), 1, 1)])
 def test_avgpool_kxk(cuda, cfg):

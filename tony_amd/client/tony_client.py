@@ -209,6 +209,7 @@ class TonyClient:
         version.inject(conf)
 
     def validate_tony_conf(self, conf: Configuration) -> bool:
+        U.size_gpu_task_memory(conf)
         try:
             requests = U.parse_container_requests(conf)
         except (ValueError, RuntimeError) as e:

@@ -119,6 +119,7 @@ AMD_CLIENT_POLL_MS = AMD + "client-poll-ms"                # client app-status p
 AMD_STAGING_DIR = AMD + "staging-dir"                      # job dirs (YARN app dir equivalent)
 AMD_PROFILE = AMD + "profile"                              # wrap tasks in rocprofv3 --kernel-trace --stats
 AMD_PROFILE_JOBTYPES = AMD + "profile.jobtypes"
+AMD_GPU_TASK_MEMORY = AMD + "gpu-task-memory-per-gpu"    # memory of a GPU task left at the 2g default
 AMD_MEMORY_ENFORCED = AMD + "memory-enforced"              # stop tasks whose RSS exceeds tony.<job>.memory
 AMD_GPU_FAULT_STOPS_TASK = AMD + "gpu-fault-stops-task"    # new uncorrectable ECC errors stop the task
 

@@ -74,19 +74,22 @@ class ConvBNAct(nn.Module):
         return self.act(self.bn(y))
 
 
-def conv_bn_act_maxpool(layer: "ConvBNAct", x, k: int = 3, s: int = 2):
-    """max_pool(layer(x), k, s); in fused training on the tony conv path one kernel does BN + ReLU +
-    pool, so the full-resolution activation is never materialised (ops/conv.py conv_bn_act_pool)."""
+def conv_bn_act_maxpool(layer: "ConvBNAct", x, k: int = 3, s: int = 2, padding: int = 0):
+    """max_pool(layer(x), k, s, padding); in fused training on the tony conv path (implicit GEMM, or the
+    MFMA image stem) one kernel does BN + ReLU + pool, so the full-resolution activation is never
+    materialised (ops/conv.py conv_bn_act_pool) -- Inception's stem pools and ResNet's 7x7 stem + 3x3/2 p1
+    pool alike."""
     from ..ops.pool import max_pool
 
     c, bn = layer.conv, layer.bn
     if (layer.fused and layer.training and x.is_cuda and bn.relu and not layer.is_1x1 and USE_TONY_CONV
             and (torch.is_grad_enabled() or tape.recording())
-            and conv_ops.supported(x, c.weight, c.stride, c.padding)):
+            and (conv_ops.supported(x, c.weight, c.stride, c.padding)
+                 or (conv_ops.STEM and conv_ops.stem_supported(x, c.weight, c.stride, c.padding)))):
         return conv_ops.conv_bn_act_pool(x, c.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, c.stride,
-                                         c.padding, bn.momentum, bn.eps, k, s)
+                                         c.padding, bn.momentum, bn.eps, k, s, padding)
     y = layer(x)
-    return max_pool(y, k, s) if layer.fused else nn.functional.max_pool2d(y, k, s)
+    return max_pool(y, k, s, padding=padding) if layer.fused else nn.functional.max_pool2d(y, k, s, padding)
 
 
 def cast_model(model: nn.Module, dtype: torch.dtype, device=None) -> nn.Module:

@@ -11,7 +11,8 @@ conv3  1x1 s1      MFMA GEMM (+stats) -> ONE pass: BN apply + identity add + ReL
 downsample         1x1 s1|s2 conv (tony_amd implicit GEMM; strided dgrad per residue class) -> fused BN
 
 Architecture: torchvision's resnet50 (stride on the 3x3, "v1.5"); layer
-widths 64/128/256/512 x4, blocks [3, 4, 6, 3], 7x7/s2 stem + 3x3/s2 max pool,
+widths 64/128/256/512 x4, blocks [3, 4, 6, 3], 7x7/s2 stem + 3x3/s2 p1 max pool (fused with the stem's
+BN + ReLU in one kernel when training, ops/conv.py conv_bn_act_pool),
 global average pool, 1000-way FC (MFMA GEMMs, ops/linear.py).  The 7x7/s2 stem runs on the
 MFMA stem kernels (csrc/stem.hip).  ``fused=False`` is the stock PyTorch
 module graph (the comparator and the CPU path).
@@ -25,7 +26,7 @@ from ..ops.bn import BatchNormAct2d
 from ..ops.linear import Linear
 from ..ops.pool import global_avg_pool
 from ..ops.residual import bn_add_relu, conv1x1_bn_add_relu
-from .layers import ConvBNAct, init_weights
+from .layers import ConvBNAct, conv_bn_act_maxpool, init_weights
 
 
 class Bottleneck(nn.Module):
@@ -74,8 +75,12 @@ class ResNet(nn.Module):
         self.fc = (Linear if fused else nn.Linear)(cin, num_classes)
 
     def forward(self, x):
-        x = self.stem(x)
-        x = torch.nn.functional.max_pool2d(x, 3, 2, 1)
+        if self.fused:
+            # one kernel: BN + ReLU + 3x3/2 p1 max pool over the stem conv's output (training), the
+            # padded tony max pool otherwise -- no stock pooling kernel on the fused path
+            x = conv_bn_act_maxpool(self.stem, x, 3, 2, padding=1)
+        else:
+            x = torch.nn.functional.max_pool2d(self.stem(x), 3, 2, 1)
         x = self.blocks(x)
         x = global_avg_pool(x) if self.fused else x.mean((2, 3))
         return self.fc(x)

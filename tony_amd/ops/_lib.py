@@ -59,7 +59,7 @@ _SIGNATURES = {
                                c_void_p, c_void_p, c_int, c_void_p],
     "tony_bn_relu_maxpool": [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_float,
                              c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_int64, c_void_p, c_int,
-                             c_int, c_int, c_int, c_int, c_int, c_void_p],
+                             c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "tony_bn_bwd_reduce": [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p,
                            c_void_p, c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p],
     "tony_bn_bwd_apply": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p,
@@ -102,9 +102,9 @@ _SIGNATURES = {
     "tony_conv_wgrad_direct": [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int, c_int, c_int,
                                c_int, c_int, c_void_p, c_int64, c_void_p, c_int, c_void_p],
     "tony_avgpool3_s1p1": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
-    "tony_maxpool_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
+    "tony_maxpool_fwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
                          c_void_p],
-    "tony_maxpool_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
+    "tony_maxpool_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
                          c_void_p],
     "tony_maxpool_bwd_bnred": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64,
                                c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,

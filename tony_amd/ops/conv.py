@@ -45,7 +45,12 @@ def _pair(v):
 # Image stems (3-channel input) run on the MFMA stem kernels of csrc/stem.hip: forward with the BN
 # statistics epilogue and the split-K weight gradient.  TONY_STEM=0 sends them back to MIOpen (A/B).
 STEM = os.environ.get("TONY_STEM", "1") != "0"
-MIN_ROWS = 2048  # below this many output pixels a tile grid cannot fill 256 CUs: leave it to MIOpen
+# Fewest output pixels a conv needs to run on the tony kernels.  Every shape does (1): small-M layers
+# (ResNet's 7x7 maps at per-GPU batch 16, the whole-model tests at 64x64) pick their tile variant by
+# autotuning like every other shape (64-row variants for few rows), so no conv falls to MIOpen --
+# runtime multi-backend dispatch on the hot path.  TONY_CONV_MIN_ROWS=2048 restores the round-2
+# MIOpen cutoff for A/B runs.
+MIN_ROWS = int(os.environ.get("TONY_CONV_MIN_ROWS", "1"))
 
 
 _SUP_CACHE: dict = {}
@@ -698,7 +703,7 @@ class _ConvBNActPoolFn(torch.autograd.Function):
     the saved argmax, then the BN + conv backward of _ConvBNActFn."""
 
     @staticmethod
-    def forward(ctx, x, weight, gamma, beta, running_mean, running_var, stride, padding, momentum, eps, k, s):
+    def forward(ctx, x, weight, gamma, beta, running_mean, running_var, stride, padding, momentum, eps, k, s, p=0):
         L = _lib.lib()
         _lib.check_f32_stats(running_mean, running_var)
         dev = x.device
@@ -707,7 +712,7 @@ class _ConvBNActPoolFn(torch.autograd.Function):
         Z = _fwd(x, weight, stride, padding, stats)
         _, _, ldz = _rows_view(Z)
         n, _, h, w = Z.shape
-        oh, ow = (h - k) // s + 1, (w - k) // s + 1
+        oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
         y = _cl_empty(n, co, oh, ow, dev)
         arg = torch.empty((n, oh, ow, co), dtype=torch.uint8, device=dev)
         mean = torch.empty(co, dtype=torch.float32, device=dev)
@@ -716,28 +721,28 @@ class _ConvBNActPoolFn(torch.autograd.Function):
         rc = L.tony_bn_relu_maxpool(Z.data_ptr(), ldz, stats.data_ptr(), stats.data_ptr() + 4 * co, 2 * co,
                                     gamma.data_ptr(), beta.data_ptr(), pb, float(eps), mean.data_ptr(),
                                     invstd.data_ptr(), _lib.ptr(running_mean), _lib.ptr(running_var), float(momentum),
-                                    y.data_ptr(), co, arg.data_ptr(), n, h, w, co, k, s, _lib.stream_ptr(dev))
+                                    y.data_ptr(), co, arg.data_ptr(), n, h, w, co, k, s, p, _lib.stream_ptr(dev))
         _lib.check(rc, "tony_bn_relu_maxpool")
         ctx.save_for_backward(x, weight, gamma, beta, mean, invstd, Z, arg)
         ctx.params = (weight, gamma, beta)
         ctx.cfg = (stride, padding, True, pb)
-        ctx.pool = (k, s)
+        ctx.pool = (k, s, p)
         ctx.bnc_in = getattr(x, "_tony_bnr", None)
         return y
 
     @staticmethod
     def backward(ctx, dyp):
         x, weight, gamma, beta, mean, invstd, Z, arg = ctx.saved_tensors
-        k, s = ctx.pool
+        k, s, p = ctx.pool
         n, co, h, w = Z.shape
         dyp, (_, _, lddy) = _as_rows(dyp)
         dy = _cl_empty(n, co, h, w, Z.device)
-        if not POOL_BNRED:
-            rc = _lib.lib().tony_maxpool_bwd(dyp.data_ptr(), arg.data_ptr(), dy.data_ptr(), n, h, w, co, k, s, lddy,
+        if not POOL_BNRED or p:  # the fused bnred pool backward has no padding
+            rc = _lib.lib().tony_maxpool_bwd(dyp.data_ptr(), arg.data_ptr(), dy.data_ptr(), n, h, w, co, k, s, p, lddy,
                                              co, _lib.stream_ptr(Z.device))
             _lib.check(rc, "tony_maxpool_bwd")
             dx, dw, dgamma, dbeta = _conv_bn_backward(ctx, x, weight, gamma, beta, mean, invstd, Z, dy)
-            return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None
+            return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None
         # the pool backward also reduces the BN backward sums (csrc/pool.hip maxpool_bwd_bnred_kernel):
         # the separate two-pass reduce over Z and dY (354 / 155 MB each at the Inception stem) disappears
         _, _, ldz = _rows_view(Z)
@@ -748,14 +753,15 @@ class _ConvBNActPoolFn(torch.autograd.Function):
                                                2 * co, _lib.num_cus(Z.device), _lib.stream_ptr(Z.device))
         _lib.check(rc, "tony_maxpool_bwd_bnred")
         dx, dw, dgamma, dbeta = _conv_bn_backward(ctx, x, weight, gamma, beta, mean, invstd, Z, dy, presums=sums)
-        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None
+        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None
 
 
 def conv_bn_act_pool(x, weight, gamma, beta, running_mean, running_var, stride=1, padding=0, momentum=0.1,
-                     eps=1e-3, k=3, s=2):
-    """max_pool2d(relu(batch_norm(conv2d(x))), k, s) in training mode, fused (see _ConvBNActPoolFn)."""
+                     eps=1e-3, k=3, s=2, pool_padding=0):
+    """max_pool2d(relu(batch_norm(conv2d(x))), k, s, pool_padding) in training mode, fused (see
+    _ConvBNActPoolFn)."""
     return tape.apply(_ConvBNActPoolFn, x, weight, gamma, beta, running_mean, running_var, _pair(stride), _pair(padding),
-                                  momentum, eps, k, s)
+                                  momentum, eps, k, s, pool_padding)
 
 
 def conv_bn_act(x, weight, gamma, beta, running_mean, running_var, stride=1, padding=0, training=True,

@@ -597,7 +597,7 @@ __global__ __launch_bounds__(kThreads) void bn_relu_maxpool_kernel(
     int64_t sstride, const void* gamma, const void* beta, int param_bf16, float eps,
     float* __restrict__ save_mean, float* __restrict__ save_invstd, float* __restrict__ running_mean,
     float* __restrict__ running_var, float momentum, uint16_t* __restrict__ y, int64_t ldy,
-    uint8_t* __restrict__ arg, int N, int H, int W, int C, int OH, int OW, int K, int S) {
+    uint8_t* __restrict__ arg, int N, int H, int W, int C, int OH, int OW, int K, int S, int P) {
   float* scale = bn_dyn;  // [C] then shift [C]: bn_lds_table(C, 2) bytes
   float* shift = bn_dyn + C;
   const int64_t M = static_cast<int64_t>(N) * H * W;
@@ -652,21 +652,43 @@ __global__ __launch_bounds__(kThreads) void bn_relu_maxpool_kernel(
         }
       }
     };
+    // P > 0 (ResNet's 3x3/2 p1 stem pool): out-of-image taps are skipped -- every window holds an
+    // in-image tap (P < K) and the ReLU outputs are >= 0, so a padded tap could never win anyway
+    const int h0 = oh * S - P, w0 = ow * S - P;
     if constexpr (KT > 0) {
-      const uint16_t* base = z + ((n * H + oh * S) * W + ow * S) * ldz + cg * 8;
-      const int64_t row = static_cast<int64_t>(W) * ldz;
-      bf16x8 raw[KT * KT];
+      if (P == 0) {
+        const uint16_t* base = z + ((n * H + h0) * W + w0) * ldz + cg * 8;
+        const int64_t row = static_cast<int64_t>(W) * ldz;
+        bf16x8 raw[KT * KT];
 #pragma unroll
-      for (int kh = 0; kh < KT; ++kh)
+        for (int kh = 0; kh < KT; ++kh)
 #pragma unroll
-        for (int kw = 0; kw < KT; ++kw) raw[kh * KT + kw] = load8(base + kh * row + kw * ldz);
+          for (int kw = 0; kw < KT; ++kw) raw[kh * KT + kw] = load8(base + kh * row + kw * ldz);
 #pragma unroll
-      for (int k = 0; k < KT * KT; ++k) take(raw[k], static_cast<uint8_t>(k));
+        for (int k = 0; k < KT * KT; ++k) take(raw[k], static_cast<uint8_t>(k));
+      } else {
+        bf16x8 raw[KT * KT];
+        bool ok[KT * KT];
+#pragma unroll
+        for (int kh = 0; kh < KT; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < KT; ++kw) {
+            const int hh = h0 + kh, ww = w0 + kw;
+            ok[kh * KT + kw] = static_cast<unsigned>(hh) < static_cast<unsigned>(H) &&
+                               static_cast<unsigned>(ww) < static_cast<unsigned>(W);
+            if (ok[kh * KT + kw]) raw[kh * KT + kw] = load8(z + ((n * H + hh) * W + ww) * ldz + cg * 8);
+          }
+#pragma unroll
+        for (int k = 0; k < KT * KT; ++k)
+          if (ok[k]) take(raw[k], static_cast<uint8_t>(k));
+      }
     } else {
       for (int kh = 0; kh < K; ++kh) {
-        const int hh = oh * S + kh;
+        const int hh = h0 + kh;
+        if (static_cast<unsigned>(hh) >= static_cast<unsigned>(H)) continue;
         for (int kw = 0; kw < K; ++kw) {
-          const int ww = ow * S + kw;
+          const int ww = w0 + kw;
+          if (static_cast<unsigned>(ww) >= static_cast<unsigned>(W)) continue;
           take(load8(z + ((n * H + hh) * W + ww) * ldz + cg * 8), static_cast<uint8_t>(kh * K + kw));
         }
       }
@@ -935,10 +957,12 @@ TONY_API int tony_bn_relu_maxpool(const void* z, int64_t ldz, const float* sum, 
                                   const void* gamma, const void* beta, int param_bf16, float eps, float* save_mean,
                                   float* save_invstd, float* running_mean, float* running_var, float momentum,
                                   void* y, int64_t ldy, void* argmax, int N, int H, int W, int C, int K, int S,
-                                  hipStream_t stream) {
-  if (bad_c(C) || (ldz % 8) || (ldy % 8) || sstride < 0 || K * K > 255 || H < K || W < K || S < 1) return -1;
+                                  int P, hipStream_t stream) {
+  if (bad_c(C) || (ldz % 8) || (ldy % 8) || sstride < 0 || K * K > 255 || P < 0 || 2 * P >= K + 1 ||
+      H + 2 * P < K || W + 2 * P < K || S < 1)
+    return -1;
   if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
-  const int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
+  const int OH = (H + 2 * P - K) / S + 1, OW = (W + 2 * P - K) / S + 1;
   int64_t work = static_cast<int64_t>(N) * OH * OW * (C / 8);
   int64_t grid = (work + kThreads - 1) / kThreads;
   if (grid > 16384) grid = 16384;
@@ -946,7 +970,7 @@ TONY_API int tony_bn_relu_maxpool(const void* z, int64_t ldz, const float* sum, 
   kern<<<static_cast<int>(grid < 1 ? 1 : grid), kThreads, bn_lds_table(C, 2), stream>>>(
       static_cast<const uint16_t*>(z), ldz, sum, sumsq, sstride, gamma, beta, param_bf16, eps, save_mean, save_invstd,
       running_mean, running_var, momentum, static_cast<uint16_t*>(y), ldy, static_cast<uint8_t*>(argmax), N, H, W, C,
-      OH, OW, K, S);
+      OH, OW, K, S, P);
   TONY_LAUNCH_CHECK();
   return 0;
 }

@@ -58,11 +58,13 @@ __global__ __launch_bounds__(kThreads) void box3_kernel(const uint16_t* __restri
 
 // KT = 3: the window's 9 loads are issued before the first is consumed (the runtime-K loop waits on
 // each in turn); 0: any K
+// P: zero-padding of the window (torch's max_pool2d padding: padded taps never win; ResNet's stem pool
+// is 3x3/2 p1).  With P > 0 each tap is bounds-checked and an out-of-image tap is skipped.
 template <int KT>
 __global__ __launch_bounds__(kThreads) void maxpool_fwd_kernel(const uint16_t* __restrict__ x,
                                                                uint16_t* __restrict__ y, uint8_t* __restrict__ arg,
                                                                int N, int H, int W, int C, int OH, int OW, int K,
-                                                               int S, int64_t ldx, int64_t ldy) {
+                                                               int S, int P, int64_t ldx, int64_t ldy) {
   const uint32_t CG = C >> 3;
   const uint32_t total = static_cast<uint32_t>(N) * OH * OW * CG;
   const uint32_t stride = gridDim.x * kThreads;
@@ -91,21 +93,41 @@ __global__ __launch_bounds__(kThreads) void maxpool_fwd_kernel(const uint16_t* _
         }
       }
     };
+    const int h0 = oh * S - P, w0 = ow * S - P;
     if constexpr (KT > 0) {
-      const uint16_t* base = x + ((n * H + oh * S) * W + ow * S) * ldx + cg * 8;
-      const int64_t row = static_cast<int64_t>(W) * ldx;
-      bf16x8 raw[KT * KT];
+      if (P == 0) {
+        const uint16_t* base = x + ((n * H + h0) * W + w0) * ldx + cg * 8;
+        const int64_t row = static_cast<int64_t>(W) * ldx;
+        bf16x8 raw[KT * KT];
 #pragma unroll
-      for (int kh = 0; kh < KT; ++kh)
+        for (int kh = 0; kh < KT; ++kh)
 #pragma unroll
-        for (int kw = 0; kw < KT; ++kw) raw[kh * KT + kw] = load8(base + kh * row + kw * ldx);
+          for (int kw = 0; kw < KT; ++kw) raw[kh * KT + kw] = load8(base + kh * row + kw * ldx);
 #pragma unroll
-      for (int k = 0; k < KT * KT; ++k) take(raw[k], static_cast<uint8_t>(k));
+        for (int k = 0; k < KT * KT; ++k) take(raw[k], static_cast<uint8_t>(k));
+        } else {  // padded: the in-image taps' loads all issued up front, then consumed
+        bf16x8 raw[KT * KT];
+        bool ok[KT * KT];
+#pragma unroll
+        for (int kh = 0; kh < KT; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < KT; ++kw) {
+            const int hh = h0 + kh, ww = w0 + kw;
+            ok[kh * KT + kw] = static_cast<unsigned>(hh) < static_cast<unsigned>(H) &&
+                               static_cast<unsigned>(ww) < static_cast<unsigned>(W);
+            if (ok[kh * KT + kw]) raw[kh * KT + kw] = load8(x + ((n * H + hh) * W + ww) * ldx + cg * 8);
+          }
+#pragma unroll
+        for (int k = 0; k < KT * KT; ++k)
+          if (ok[k]) take(raw[k], static_cast<uint8_t>(k));
+      }
     } else {
       for (int kh = 0; kh < K; ++kh) {
-        const int hh = oh * S + kh;
+        const int hh = h0 + kh;
+        if (static_cast<unsigned>(hh) >= static_cast<unsigned>(H)) continue;
         for (int kw = 0; kw < K; ++kw) {
-          const int ww = ow * S + kw;
+          const int ww = w0 + kw;
+          if (static_cast<unsigned>(ww) >= static_cast<unsigned>(W)) continue;
           take(load8(x + ((n * H + hh) * W + ww) * ldx + cg * 8), static_cast<uint8_t>(kh * K + kw));
         }
       }
@@ -121,7 +143,7 @@ __global__ __launch_bounds__(kThreads) void maxpool_fwd_kernel(const uint16_t* _
 __global__ __launch_bounds__(kThreads) void maxpool_bwd_kernel(const uint16_t* __restrict__ dy,
                                                                const uint8_t* __restrict__ arg,
                                                                uint16_t* __restrict__ dx, int N, int H, int W, int C,
-                                                               int OH, int OW, int K, int S, int64_t lddy,
+                                                               int OH, int OW, int K, int S, int P, int64_t lddy,
                                                                int64_t lddx) {
   const uint32_t CG = C >> 3;
   const uint32_t total = static_cast<uint32_t>(N) * H * W * CG;
@@ -134,14 +156,15 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd_kernel(const uint16_t* _
     const int h = static_cast<int>(nh % H);
     const int64_t n = nh / H;
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    // windows oh with oh*S <= h <= oh*S + K - 1
-    const int oh_lo = h >= K ? (h - K + S) / S : 0;
-    const int oh_hi = min(OH - 1, h / S);
-    const int ow_lo = w >= K ? (w - K + S) / S : 0;
-    const int ow_hi = min(OW - 1, w / S);
+    // windows oh with oh*S - P <= h <= oh*S - P + K - 1 (hp = h + P: the padded coordinate)
+    const int hp = h + P, wp = w + P;
+    const int oh_lo = hp >= K ? (hp - K + S) / S : 0;
+    const int oh_hi = min(OH - 1, hp / S);
+    const int ow_lo = wp >= K ? (wp - K + S) / S : 0;
+    const int ow_hi = min(OW - 1, wp / S);
     for (int oh = oh_lo; oh <= oh_hi; ++oh) {
       for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-        const int local = (h - oh * S) * K + (w - ow * S);
+        const int local = (hp - oh * S) * K + (wp - ow * S);
         const int64_t osite = (n * OH + oh) * OW + ow;
         const uint2 packed = *reinterpret_cast<const uint2*>(arg + osite * C + cg * 8);
         float g[8];
@@ -332,26 +355,31 @@ TONY_API int tony_avgpool3_s1p1(const void* x, void* y, int N, int H, int W, int
   return 0;
 }
 
-TONY_API int tony_maxpool_fwd(const void* x, void* y, void* argmax, int N, int H, int W, int C, int K, int S,
+// Max pool KxK / stride S / zero-padding P (P < K: every window holds an in-image tap), NHWC bf16
+// with row strides; argmax: one byte per output element (the winning tap kh*K + kw).
+TONY_API int tony_maxpool_fwd(const void* x, void* y, void* argmax, int N, int H, int W, int C, int K, int S, int P,
                               int64_t ldx, int64_t ldy, hipStream_t stream) {
-  if (C % 8 || ldx % 8 || ldy % 8 || K * K > 255 || H < K || W < K) return -1;
+  if (C % 8 || ldx % 8 || ldy % 8 || K * K > 255 || P < 0 || 2 * P >= K + 1 || H + 2 * P < K || W + 2 * P < K ||
+      S < 1)
+    return -1;
   if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
-  const int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
+  const int OH = (H + 2 * P - K) / S + 1, OW = (W + 2 * P - K) / S + 1;
   (K == 3 ? maxpool_fwd_kernel<3> : maxpool_fwd_kernel<0>)<<<grid_for(static_cast<int64_t>(N) * OH * OW * (C / 8)), kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), static_cast<uint8_t*>(argmax), N, H, W, C, OH, OW,
-      K, S, ldx, ldy);
+      K, S, P, ldx, ldy);
   TONY_LAUNCH_CHECK();
   return 0;
 }
 
 TONY_API int tony_maxpool_bwd(const void* dy, const void* argmax, void* dx, int N, int H, int W, int C, int K, int S,
-                              int64_t lddy, int64_t lddx, hipStream_t stream) {
-  if (C % 8 || lddy % 8 || lddx % 8 || H < K || W < K) return -1;
+                              int P, int64_t lddy, int64_t lddx, hipStream_t stream) {
+  if (C % 8 || lddy % 8 || lddx % 8 || P < 0 || 2 * P >= K + 1 || H + 2 * P < K || W + 2 * P < K || S < 1)
+    return -1;
   if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
-  const int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
+  const int OH = (H + 2 * P - K) / S + 1, OW = (W + 2 * P - K) / S + 1;
   maxpool_bwd_kernel<<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(dy), static_cast<const uint8_t*>(argmax), static_cast<uint16_t*>(dx), N, H, W, C,
-      OH, OW, K, S, lddy, lddx);
+      OH, OW, K, S, P, lddy, lddx);
   TONY_LAUNCH_CHECK();
   return 0;
 }

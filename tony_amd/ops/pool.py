@@ -1,4 +1,4 @@
-"""NHWC pooling kernels (csrc/pool.hip): avg 3x3/s1/p1 and max KxK/sS."""
+"""NHWC pooling kernels (csrc/pool.hip): avg 3x3/s1/p1, avg KxK/sS and max KxK/sS with zero padding."""
 from __future__ import annotations
 
 import torch
@@ -35,32 +35,32 @@ class _AvgPool3Fn(torch.autograd.Function):
 
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k, s, slot=None):
+    def forward(ctx, x, k, s, slot=None, p=0):
         x, (_, c, ld) = _as_rows(x)
         n, _, h, w = x.shape
-        oh, ow = (h - k) // s + 1, (w - k) // s + 1
+        oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
         y = concat.take(slot, n, c, oh, ow, x)  # straight into the block's concat buffer
         if y is None:
             y = _nhwc_empty(n, c, oh, ow, x)
         arg = torch.empty((n, oh, ow, c), dtype=torch.uint8, device=x.device)
-        rc = _lib.lib().tony_maxpool_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), n, h, w, c, k, s, ld,
+        rc = _lib.lib().tony_maxpool_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), n, h, w, c, k, s, p, ld,
                                          _rows_view(y)[2], _lib.stream_ptr(x.device))
         _lib.check(rc, "tony_maxpool_fwd")
         ctx.save_for_backward(arg)
-        ctx.shape = (n, c, h, w, k, s)
+        ctx.shape = (n, c, h, w, k, s, p)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         (arg,) = ctx.saved_tensors
-        n, c, h, w, k, s = ctx.shape
+        n, c, h, w, k, s, p = ctx.shape
         dy, (_, _, lddy) = _as_rows(dy)
         dx = _nhwc_empty(n, c, h, w, dy)
-        rc = _lib.lib().tony_maxpool_bwd(dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), n, h, w, c, k, s, lddy, c,
+        rc = _lib.lib().tony_maxpool_bwd(dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), n, h, w, c, k, s, p, lddy, c,
                                          _lib.stream_ptr(dy.device))
         _lib.check(rc, "tony_maxpool_bwd")
         streams.keep(dx)  # may be consumed on another (branch) stream
-        return dx, None, None, None
+        return dx, None, None, None, None
 
 
 class _AvgPoolFn(torch.autograd.Function):
@@ -108,8 +108,9 @@ def avg_pool3x3_s1(x: torch.Tensor) -> torch.Tensor:
     return torch.nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=True)
 
 
-def max_pool(x: torch.Tensor, k: int = 3, s: int = 2, slot=None) -> torch.Tensor:
-    """max_pool2d(x, k, s) (no padding) on channels_last bf16 (into a concat.Slot when given)."""
-    if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0:
-        return tape.apply(_MaxPoolFn, x, k, s, slot)
-    return torch.nn.functional.max_pool2d(x, k, s)
+def max_pool(x: torch.Tensor, k: int = 3, s: int = 2, slot=None, padding: int = 0) -> torch.Tensor:
+    """max_pool2d(x, k, s, padding) on channels_last bf16 (into a concat.Slot when given); padded taps
+    never win (torch semantics), e.g. ResNet's 3x3/2 p1 stem pool."""
+    if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0 and 2 * padding <= k:
+        return tape.apply(_MaxPoolFn, x, k, s, slot, padding)
+    return torch.nn.functional.max_pool2d(x, k, s, padding)

@@ -251,6 +251,30 @@ def ensure_staged_tasks_integrity(prepare: List[str], training: List[str], all_t
             f"job types, but {len(all_types)} job types in total")
 
 
+def size_gpu_task_memory(conf) -> Dict[str, int]:
+    """MI355X-sized memory for GPU jobtypes whose ``tony.<job>.memory`` was left at tony-default.xml's
+    YARN-era 2g.  A PyTorch-ROCm rank alone exceeds 2 GB of RSS, and the task agent enforces the limit
+    (tony.amd.memory-enforced, like YARN's pmem check), so such a job used to be SIGKILLed.  Such a
+    jobtype gets ``tony.amd.gpu-task-memory-per-gpu`` (default 32g) x its GPUs, set explicitly in the conf
+    (and so in tony-final.xml); an explicit user value is never changed.  Returns {job: MB} changed."""
+    changed = {}
+    per_gpu = parse_memory_string(conf.get(K.AMD_GPU_TASK_MEMORY, "32g"))
+    for job in get_all_job_types(conf):
+        key = K.resource_key(job, C.MEMORY)
+        gpus = conf.get_int(K.resource_key(job, C.GPUS), 0)
+        src = conf.get_source(key)
+        if gpus <= 0 or per_gpu <= 0 or (src is not None and src != "tony-default.xml"):
+            continue
+        cur = parse_memory_string(conf.get(key, K.DEFAULT_MEMORY))
+        want = gpus * per_gpu
+        if want > cur:
+            conf.set(key, f"{want}m", source=f"{K.AMD_GPU_TASK_MEMORY} x {gpus} GPU(s)")
+            changed[job] = want
+            LOG.info("tony.%s.memory left at the default %d MB for a %d-GPU task: using %d MB (%s)", job, cur, gpus,
+                     want, K.AMD_GPU_TASK_MEMORY)
+    return changed
+
+
 def parse_container_requests(conf, gpus_available: Optional[int] = None) -> Dict[str, JobContainerRequest]:
     """Job types -> requests with unique priorities and prepare->training stage dependencies."""
     job_types = get_all_job_types(conf)
