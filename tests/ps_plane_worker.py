@@ -19,6 +19,16 @@ def _grad_value(step, widx, i):
     return float((widx + 1) * (step % 3 + 1)) * 0.25 + (i % 4) * 0.125
 
 
+def _master_flat(ps):
+    """The ps's fp32 masters (stored bucket by bucket) back in flat-buffer order."""
+    master = ps.optimizers[ps.rank].w.cpu()
+    out = torch.zeros(ps.flat.numel)
+    for b in ps.buckets:
+        m, n = ps._master_range[b.index]
+        out[b.lo:b.hi] = master[m:m + n]
+    return out
+
+
 def run(rank, world, port, q, sync=True, wire=None, steps=4):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     try:
@@ -28,7 +38,7 @@ def run(rank, world, port, q, sync=True, wire=None, steps=4):
         from tony_amd.parallel.ps import ParameterServer
 
         torch.manual_seed(0)
-        net = _Net([3000, 517 * 8, 12345 * 8, 64])
+        net = _Net([11000, 12000, 4136, 13000, 3000, 11008, 64])
         with torch.no_grad():
             for p in net.ps:
                 p.copy_(torch.randn(p.shape).mul_(0.5))
@@ -67,14 +77,12 @@ def run(rank, world, port, q, sync=True, wire=None, steps=4):
             got = ps.flat.data.float().cpu()
             res["params_match"] = bool(torch.allclose(got, exp, rtol=1e-2, atol=2e-2))
             if ps.is_ps:
-                master = ps.optimizers[ps.rank].w.cpu()
-                res["master_match"] = bool(torch.allclose(master, exp, rtol=1e-5, atol=1e-4))
+                res["master_match"] = bool(torch.allclose(_master_flat(ps), exp, rtol=1e-5, atol=1e-4))
         else:
             # async, momentum 0: updates commute -> the ps ends at w0 - lr * (every push); a worker's last
             # landing includes all of its own pushes and a subset of the others'
             if ps.is_ps:
-                master = ps.optimizers[ps.rank].w.cpu()
-                res["master_match"] = bool(torch.allclose(master, w0 - lr * tot, rtol=1e-5, atol=1e-3))
+                res["master_match"] = bool(torch.allclose(_master_flat(ps), w0 - lr * tot, rtol=1e-5, atol=1e-3))
             else:
                 applied = (w0 - ps.flat.data.float().cpu()) / lr
                 res["own_included"] = bool((applied >= own * 0.99 - 0.1).all())

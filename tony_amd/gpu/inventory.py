@@ -119,8 +119,8 @@ def verify_visible_device(device_index: int = 0) -> Optional[str]:
     """In a task: the BDF torch/HIP sees for ``device_index`` vs the one the coordinator pinned
     (TONY_GPU_BDFS, same order as HIP_VISIBLE_DEVICES).  Returns the BDF; raises on a mismatch."""
     want = [b for b in os.environ.get("TONY_GPU_BDFS", "").split(",") if b]
-    if not want:
-        return None
+    if not want or any(b.startswith("fake") for b in want):
+        return None  # local mode's fake inventory (tony.amd.fake-gpus): nothing real to verify against
     mode = os.environ.get("TONY_VISIBLE_MODE") or ("hip" if os.environ.get("HIP_VISIBLE_DEVICES") is not None
                                                    else "")
     if mode in ("hip", "rocr"):

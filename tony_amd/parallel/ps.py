@@ -139,10 +139,12 @@ class ParameterServer:
                 opt = make_optimizer(optimizer, master, lr, momentum, weight_decay, **opt_kw)
                 opt.grad_scale = 1.0 / len(self.worker_ranks)
                 self.optimizers[self.rank] = opt
-        else:  # asynchronous: the single ps task owns the whole buffer
+        else:  # asynchronous: the single ps task owns the whole buffer (masters in flat order)
             if self.is_ps:
                 opt = make_optimizer(optimizer, f.data.float().clone(), lr, momentum, weight_decay, **opt_kw)
                 self.optimizers[self.rank] = opt
+                for b in self.buckets:
+                    self._master_range[b.index] = (b.lo, b.numel)
         if plane == "auto":
             plane = os.environ.get("TONY_PS_PLANE", "xgmi" if f.device.type == "cuda" else "rccl")
         self.plane_kind = plane if mode == "dedicated" and self.world > 1 else "rccl"

@@ -131,7 +131,7 @@ class XgmiPSPlane:
     def check_error(self) -> None:
         torch.cuda.synchronize(self.device)
         err = ctypes.c_int(0)
-        _lib.check(_lib.lib().tony_ps_error(ctypes.c_void_p(self.window), ctypes.byref(err)), "tony_ps_error")
+        _lib.check(_lib.lib().tony_ps_error(self.window, ctypes.byref(err)), "tony_ps_error")
         self._err_host.zero_()
         if err.value:
             raise PSPlaneError(f"rank {self.rank}: a peer of the parameter-server plane never arrived within "
@@ -142,8 +142,9 @@ class XgmiPSPlane:
         """Worker: bucket b's gradient into its row of the owner's window (current stream)."""
         g = self.flat.grad[b.lo:b.hi]
         owner = self.owner[b.index]
+        row = self.widx * self.row_stride[owner] + self.row_off[b.index]  # this worker's row of bucket b
         rc = _lib.lib().tony_ps_push(g.data_ptr(), int(g.dtype == torch.bfloat16), self.mapped[owner],
-                                     self.row_off[b.index], int(self.wire_dtype == torch.bfloat16), b.numel, b.index,
+                                     row, int(self.wire_dtype == torch.bfloat16), b.numel, b.index,
                                      self.widx, (step + 1) & 0xFFFFFFFF, self.blocks[b.index],
                                      _lib.stream_ptr(self.device))
         _lib.check(rc, "tony_ps_push")
@@ -186,7 +187,7 @@ class XgmiPSPlane:
         dist.barrier(group=self.group)  # nobody writes into a window after this
         L = _lib.lib()
         for p in self._opened:
-            L.tony_xgmi_close(ctypes.c_void_p(p))
-        L.tony_xgmi_free(ctypes.c_void_p(self.window))
+            L.tony_xgmi_close(p)
+        L.tony_xgmi_free(self.window)
         self.window = None
         self._opened = []

@@ -1,0 +1,40 @@
+#!/bin/bash
+# Round-3 GPU session steps.  Each step runs under its own time limit; the session stops at the
+# first failing step (a GPU fault / abort / timeout must not be followed by more GPU work).
+set -u
+mkdir -p gpurun_out
+step() {  # step <name> <timeout_s> <cmd...>
+  local name=$1 to=$2; shift 2
+  echo "== $name: $*" >&2
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" >&2
+  tail -4 "gpurun_out/$name.log" >&2
+  if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)" >&2; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    plane) step plane 500 python -u -m pytest tests/test_ps_plane_gpu.py tests/test_hvd_gpu.py tests/test_overlap_gpu.py -x -v --timeout 240 --timeout-method thread ;;
+    tests) step gpu_suite 800 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread ;;
+    bench) step bench 400 python bench.py --steps 20 --warmup 6 ;;
+    bench_r50) step bench_r50 400 python bench.py --model resnet50 --steps 20 --warmup 6 ;;
+    bench_r50_b16) step bench_r50_b16 400 python bench.py --model resnet50 --batch 16 --steps 20 --warmup 6 --mode eager ;;
+    host) step host_layer 300 python tools/host_layer_bench.py ;;
+    hostprof) step host_prof_fwd 300 python tools/host_profile.py --steps 5
+              step host_prof_bwd 300 python tools/host_profile.py --steps 5 --bwd ;;
+    # 1 ps + 2 workers, three processes on the box's one GPU (gloo only exchanges the window handles):
+    # the dedicated PS on the xGMI data plane with the real Inception-v3 step
+    bench3_ded) step bench3_ded 600 env TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 3 --master-addr 127.0.0.1 --master-port 29521 bench.py --gpus 3 --steps 4 --warmup 2 --batch 32 --mode eager --ps-mode dedicated ;;
+    # the same topology through the launcher (bin/tony: coordinator -> task agents -> TF_CONFIG)
+    ps_job) step ps_job 600 bash bin/tony --src_dir tony_amd/jobs --executes inception_ps.py \
+              --task_params "--ps-mode dedicated --batch-size 32 --steps 6 --warmup 2" \
+              --conf tony.ps.instances=1 --conf tony.worker.instances=2 --conf tony.ps.gpus=1 \
+              --conf tony.worker.gpus=1 --conf tony.amd.fake-gpus=3 --conf tony.application.security.enabled=false \
+              --shell_env TONY_DIST_BACKEND=gloo ;;
+    prof) export TMPDIR=/tmp; R=$(pwd)
+          step prof 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 5 --mode eager ${BENCH_ARGS:-}
+          python3 tools/prof_summary.py gpurun_out/prof --skip 6 > gpurun_out/prof_summary.md; find gpurun_out/prof -name '*trace*' -delete ;;
+    *) echo "unknown step $s" >&2; exit 2 ;;
+  esac
+done
