@@ -108,7 +108,7 @@ def run_overlap(rank, world, port, q):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
-        from tony_amd.models.layers import ConvBNAct, init_weights
+        from tony_amd.models.layers import ConvBNAct, cast_model, init_weights
         from tony_amd.ops import cross_entropy
         from tony_amd.ops.pool import global_avg_pool
         from tony_amd.parallel.ps import ParameterServer
@@ -125,14 +125,23 @@ def run_overlap(rank, world, port, q):
             def forward(self, x):
                 return self.fc(global_avg_pool(self.c3(self.c2(self.c1(x)))))
 
-        model = init_weights(Net(), seed=1).to(dev).to(torch.bfloat16).to(memory_format=torch.channels_last)
+        model = cast_model(init_weights(Net(), seed=1), torch.bfloat16, dev).to(memory_format=torch.channels_last)
         ps = ParameterServer(model, optimizer="sgd", lr=0.05, momentum=0.9, mode="dedicated", ps_ranks=(0,),
                              dtype=torch.bfloat16, device=dev, bucket_mb=0.05, plane="xgmi")
         res = {}
         steps = 5
+        import sys
+        import time
+
+        t0 = time.time()
+
+        def say(msg):
+            print(f"[rank {rank} t={time.time() - t0:.1f}s] {msg}", file=sys.stderr, flush=True)
+
         if ps.is_ps:
-            for _ in range(steps):
+            for s_ in range(steps):
                 ps.step()
+                say(f"ps step {s_} issued")
         else:
             trainer = Trainer(model, ps, lambda out, y: cross_entropy(out, y), use_graph=False)
             g = torch.Generator(device=dev).manual_seed(rank)
@@ -140,8 +149,27 @@ def run_overlap(rank, world, port, q):
                 memory_format=torch.channels_last)
             y = torch.randint(0, 16, (16,), generator=g, device=dev)
             overl = []
-            for _ in range(steps):
+            if os.environ.get("TONY_PS_PLANE_TRACE"):
+                # progress of the first step, phase by phase (diagnostics for a stalled rehearsal)
+                orig_step, orig_bwd = ps.step, torch.Tensor.backward
+
+                def traced_step():
+                    say("ps.step (pushes + land) issuing")
+                    orig_step()
+                    say("ps.step issued")
+
+                def traced_bwd(t, *a, **k):
+                    say("backward start")
+                    orig_bwd(t, *a, **k)
+                    say("backward issued")
+
+                ps.step = traced_step
+                torch.Tensor.backward = traced_bwd
+            for s_ in range(steps):
+                say(f"worker step {s_} start")
                 loss = trainer.step(x, y)
+                torch.cuda.synchronize()
+                say(f"worker step {s_} done (overlapped buckets {ps.overlapped_buckets} of {len(ps.buckets)})")
                 overl.append(ps.overlapped_buckets)
             res["loss_finite"] = bool(torch.isfinite(loss).item())
             res["overlapped"] = max(overl) > 0

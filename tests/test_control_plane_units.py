@@ -737,3 +737,22 @@ def test_gpu_task_memory_sized_when_left_at_default():
     reqs = U.parse_container_requests(c)
     assert reqs["worker"].memory_mb == 65536 and reqs["ps"].memory_mb == 2048 and reqs["evaluator"].memory_mb == 8192
     assert "<name>tony.worker.memory</name>" in c.to_xml()
+
+
+def test_ps_checkpoint_without_layout_is_refused():
+    """a PS shard checkpoint without its 'layout' record (older format, shard order
+    unverifiable) must be refused, not loaded into a possibly different bucket order."""
+    import torch
+
+    from tony_amd.parallel.ps import ParameterServer
+
+    net = torch.nn.Sequential(torch.nn.Linear(8, 8), torch.nn.Linear(8, 4))
+    ps = ParameterServer(net, optimizer="sgd", lr=0.1, dtype=torch.float32, device="cpu")
+    sd = ps.state_dict()
+    ps.load_state_dict(sd)  # round trip with the layout record works
+    del sd["layout"]
+    with pytest.raises(ValueError, match="no 'layout' record"):
+        ps.load_state_dict(sd)
+    sd["layout"] = dict(ps.layout(), world=2)
+    with pytest.raises(ValueError, match="does not match"):
+        ps.load_state_dict(sd)

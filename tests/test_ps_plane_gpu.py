@@ -37,8 +37,8 @@ def _spawn(target, world, *args):
             p.join(timeout=30)
             if p.is_alive():
                 p.kill()
-    for r in range(world):
-        assert "error" not in out[r], out[r]["error"]
+    errors = {r: out[r]["error"] for r in range(world) if "error" in out[r]}
+    assert not errors, "\n".join(f"rank {r}: {e}" for r, e in errors.items())
     return out
 
 
@@ -57,7 +57,9 @@ def test_ps_plane_push_apply_land(world, sync, wire, monkeypatch):
     assert out[0]["pushed"] == 0 and all(out[r]["pushed"] > 0 for r in range(1, world))
 
 
-def test_ps_plane_trainer_overlap():
+def test_ps_plane_trainer_overlap(monkeypatch):
+    monkeypatch.setenv("TONY_PS_SPIN_S", "20")
+    monkeypatch.setenv("TONY_PS_PLANE_TRACE", "1")
     out = _spawn(__import__("ps_plane_worker").run_overlap, 3)
     for r in range(1, 3):
         assert out[r]["loss_finite"] and out[r]["overlapped"], out[r]

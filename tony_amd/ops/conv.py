@@ -778,21 +778,25 @@ def conv_bn_act(x, weight, gamma, beta, running_mean, running_var, stride=1, pad
 
 
 # ------------------------------------------------------------------------------ inference --
-_AFF: "weakref.WeakKeyDictionary[torch.Tensor, Tuple]" = weakref.WeakKeyDictionary()
+_AFF: Dict[int, Tuple] = {}
 
 
 def folded_bn(gamma, beta, running_mean, running_var, eps) -> torch.Tensor:
     """[scale | shift] fp32 of an inference BatchNorm (y = z * scale + shift), cached per gamma TENSOR
-    (weak key: a new module's gamma never hits an old entry, even at a recycled id / address) until
-    any of the four tensors changes (the identity of the other three and all version counters)."""
-    ver = (beta._version, running_mean._version, running_var._version, gamma._version, float(eps),
-           id(beta), id(running_mean), id(running_var), gamma.data_ptr(), running_var.data_ptr())
-    hit = _AFF.get(gamma)
-    if hit is not None and hit[0] == ver and hit[2]() is beta and hit[3]() is running_var:
+    (keyed by id, but a hit requires the entry's weak references to still be these very tensors: a
+    new module's gamma at a recycled id / address never hits an old entry) until any of the four
+    tensors changes (version counters)."""
+    ver = (beta._version, running_mean._version, running_var._version, gamma._version, float(eps))
+    hit = _AFF.get(id(gamma))
+    if (hit is not None and hit[0] == ver and hit[2]() is gamma and hit[3]() is beta
+            and hit[4]() is running_mean and hit[5]() is running_var):
         return hit[1]
     scale = gamma.float() * torch.rsqrt(running_var.float() + eps)
     aff = torch.cat([scale, beta.float() - running_mean.float() * scale]).contiguous()
-    _AFF[gamma] = (ver, aff, weakref.ref(beta), weakref.ref(running_var))
+    if len(_AFF) > 4096:
+        _AFF.clear()
+    _AFF[id(gamma)] = (ver, aff, weakref.ref(gamma), weakref.ref(beta), weakref.ref(running_mean),
+                       weakref.ref(running_var))
     return aff
 
 

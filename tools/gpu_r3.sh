@@ -20,7 +20,8 @@ for s in "$@"; do
     bench) step bench 400 python bench.py --steps 20 --warmup 6 ;;
     bench_r50) step bench_r50 400 python bench.py --model resnet50 --steps 20 --warmup 6 ;;
     bench_r50_b16) step bench_r50_b16 400 python bench.py --model resnet50 --batch 16 --steps 20 --warmup 6 --mode eager ;;
-    host) step host_layer 300 python tools/host_layer_bench.py ;;
+    host) step host_layer 300 python tools/host_layer_bench.py
+          step host_micro 300 python tools/host_micro.py ;;
     hostprof) step host_prof_fwd 300 python tools/host_profile.py --steps 5
               step host_prof_bwd 300 python tools/host_profile.py --steps 5 --bwd ;;
     # 1 ps + 2 workers, three processes on the box's one GPU (gloo only exchanges the window handles):
@@ -35,6 +36,9 @@ for s in "$@"; do
     prof) export TMPDIR=/tmp; R=$(pwd)
           step prof 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 5 --mode eager ${BENCH_ARGS:-}
           python3 tools/prof_summary.py gpurun_out/prof --skip 6 > gpurun_out/prof_summary.md; find gpurun_out/prof -name '*trace*' -delete ;;
+    trace) export TMPDIR=/tmp; R=$(pwd)
+          step trace 600 rocprofv3 --kernel-trace -d "$R/gpurun_out/trace" -o run --output-format csv -- python3 "$R/bench.py" --steps 3 --warmup 5 --mode eager ${BENCH_ARGS:-}
+          python3 tools/step_union.py gpurun_out/trace --per-queue > gpurun_out/trace_union.txt; find gpurun_out/trace -name "*trace*.csv" -delete ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
   esac
 done
