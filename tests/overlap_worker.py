@@ -44,13 +44,16 @@ def ps_run(rank, kind, overlap, bucket_mb, steps=3):
                          bucketed_single=True)
     tr = Trainer(model, ps, lambda o, y: cross_entropy(o, y), overlap_comm=overlap)
     x, y = _data(rank, kind, dev)
+    from tony_amd.parallel import collectives as coll
+
+    fb0 = coll.fallback_count()
     for s in range(steps):
         if s == steps - 1:
             ps.engine.log = []
         tr.step(x, y)
     torch.cuda.synchronize()
     return {"params": ps.flat.data.float().cpu(), "log": ps.engine.log, "n_buckets": len(ps.buckets),
-            "overlapped": ps.overlapped_buckets}
+            "overlapped": ps.overlapped_buckets, "train_fallbacks": coll.fallback_count() - fb0}
 
 
 def ddp_run(rank, kind, bucket_mb):
@@ -63,11 +66,15 @@ def ddp_run(rank, kind, bucket_mb):
         p.data = p.data.to(torch.bfloat16)
     ddp = DistributedDataParallel(model, bucket_mb=bucket_mb, device=dev)
     x, y = _data(rank, kind, dev)
+    from tony_amd.parallel import collectives as coll
+
+    fb0 = coll.fallback_count()  # init-time broadcasts of small / int64 buffers may fall back; buckets may not
     ddp.zero_grad()
     cross_entropy(ddp(x), y).backward()
     torch.cuda.synchronize()
     return {"grad": ddp.flat.grad.float().cpu(), "n_buckets": len(ddp.reducer.buckets),
-            "overlapped": ddp.reducer.overlapped_buckets, "launches": ddp.reducer.launches}
+            "overlapped": ddp.reducer.overlapped_buckets, "launches": ddp.reducer.launches,
+            "train_fallbacks": coll.fallback_count() - fb0}
 
 
 def run(rank, world, port, q, kind, bucket_mb):

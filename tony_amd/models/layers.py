@@ -42,9 +42,43 @@ class ConvBNAct(nn.Module):
             self.bn = nn.BatchNorm2d(cout, eps=eps, momentum=momentum)
             self.act = nn.ReLU(inplace=True) if relu else nn.Identity()
 
+    # training hot path: the route (fused head / implicit-GEMM conv + BN) and the op's arguments are
+    # resolved once per input layout (~6 us of support checks and module attribute lookups per call,
+    # ~94 layers per Inception step); _apply (to / cuda / cast_model replace buffers) drops them
+    _ROUTE_HEAD, _ROUTE_CONV = 1, 2
+
+    def _apply(self, fn, *a, **k):
+        self.__dict__.pop("_routes", None)
+        return super()._apply(fn, *a, **k)
+
+    def _route(self, x):
+        c, bn = self.conv, self.bn
+        if self.is_1x1 and bn.relu:
+            return (self._ROUTE_HEAD, (c.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                       (c.out_channels,), 0))
+        if USE_TONY_CONV and (conv_ops.supported(x, c.weight, c.stride, c.padding)
+                              or (conv_ops.STEM and conv_ops.stem_supported(x, c.weight, c.stride, c.padding))):
+            return (self._ROUTE_CONV, (c.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                       conv_ops._pair(c.stride), conv_ops._pair(c.padding)))
+        return None
+
     def forward(self, x, slot=None):
         """``slot`` (ops/concat.Slot): write the output into a block's concat buffer when the fused
         kernels run (ignored on the stock / CPU path, where the block copies it in)."""
+        if self.training and self.fused and x.is_cuda:
+            routes = self.__dict__.get("_routes")
+            if routes is None:
+                routes = self.__dict__["_routes"] = {}
+            key = (x.shape, x.stride(), x.dtype, x.data_ptr() % 16 == 0)
+            r = routes.get(key, routes)
+            if r is routes:
+                r = routes[key] = self._route(x)
+            if r is not None:
+                bn = self.bn
+                if r[0] == self._ROUTE_HEAD:
+                    return tape.apply(_HeadFn, x, *r[1], True, bn.momentum, bn.eps,
+                                      (slot,) if slot is not None else None)[0]
+                return tape.apply(conv_ops._ConvBNActFn, x, *r[1], True, bn.momentum, bn.eps, bn.relu, slot)
         if (self.fused and x.is_cuda and not self.training and not torch.is_grad_enabled()
                 and conv_ops.supported(x, self.conv.weight, self.conv.stride, self.conv.padding, min_rows=1)
                 and (self.is_1x1 or USE_TONY_CONV)):

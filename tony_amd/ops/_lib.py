@@ -15,6 +15,7 @@ import ctypes
 import os
 import threading
 import weakref
+from typing import Dict
 
 import torch  # noqa: F401  (must precede the dlopen below)
 
@@ -113,6 +114,9 @@ _SIGNATURES = {
     "tony_avgpool_bwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
     "tony_transpose_desc_bytes": [],
     "tony_transpose_batch": [c_void_p, c_int, c_int, c_void_p],
+    # cross-stream forks / joins of the eager step (csrc/streams.hip, ops/streams.py)
+    "tony_event_pool": [c_int, c_u64_p],
+    "tony_fork": [c_void_p, c_void_p, c_void_p],
     # parameter-server data plane over xGMI windows (csrc/ps_plane.hip, parallel/ps_plane.py)
     "tony_ps_header_bytes": [],
     "tony_ps_max_buckets": [],
@@ -312,16 +316,27 @@ def set_inplace_grads(enabled: bool) -> None:
     _INPLACE_GRADS[0] = bool(enabled)
 
 
+_SLOT_OK: Dict[int, tuple] = {}  # id(param) -> (weakref to its .grad, whether that tensor passed the checks)
+
+
 def grad_slot(param):
-    """The tensor to accumulate ``param``'s gradient into, or None."""
+    """The tensor to accumulate ``param``'s gradient into, or None.  The dtype / shape / layout checks
+    of a given ``.grad`` tensor are memoised (~200 lookups per Inception step): a hit requires the
+    very same gradient tensor object (FlatParams' slot views are rebound, never mutated in place)."""
     if not _INPLACE_GRADS[0] or param is None or not isinstance(param, torch.nn.Parameter):
         return None
     g = param.grad
-    if g is None or g.dtype != param.dtype or g.shape != param.shape:
+    if g is None:
         return None
-    if not (g.is_contiguous() or (g.dim() == 4 and g.is_contiguous(memory_format=torch.channels_last))):
-        return None
-    return g
+    hit = _SLOT_OK.get(id(param))
+    if hit is not None and hit[0]() is g:
+        return g if hit[1] else None
+    ok = (g.dtype == param.dtype and g.shape == param.shape
+          and (g.is_contiguous() or (g.dim() == 4 and g.is_contiguous(memory_format=torch.channels_last))))
+    if len(_SLOT_OK) > 65536:
+        _SLOT_OK.clear()
+    _SLOT_OK[id(param)] = (weakref.ref(g), ok)  # weak: never keeps a dropped gradient buffer alive
+    return g if ok else None
 
 
 _GRAD_LISTENERS: "weakref.WeakSet" = weakref.WeakSet()

@@ -31,6 +31,8 @@ from typing import Callable, Dict, List, Optional
 
 import torch
 
+from . import _lib
+
 ENABLED = os.environ.get("TONY_WGRAD_STREAM", "1") != "0"
 
 _lock = threading.Lock()
@@ -99,17 +101,20 @@ def parallel(*thunks):
     """Results of the independent ``thunks``; concurrently on branch streams when branches are on."""
     if not _branches_on[0] or len(thunks) < 2:
         return [f() for f in thunks]
-    main = torch.cuda.current_stream()
+    main = current(torch.cuda.current_device())
     side = _branch_streams(main.device, len(thunks) - 1)
     outs = [None] * len(thunks)
     for i, (f, s) in enumerate(zip(thunks[1:], side), 1):
-        s.wait_stream(main)
-        with torch.cuda.stream(s):
+        fork(main, s)
+        torch.cuda.set_stream(s)
+        try:
             outs[i] = f()
+        finally:
+            torch.cuda.set_stream(main)
         _used[id(s)] = s
     outs[0] = thunks[0]()
     for s in side:
-        main.wait_stream(s)
+        fork(s, main)
     keep(*[o for o in outs if isinstance(o, torch.Tensor)])
     return outs
 
@@ -135,23 +140,55 @@ _pending: List[Callable[[], object]] = []
 URGENT_BYTES = int(os.environ.get("TONY_WGRAD_URGENT_MB", "64")) << 20
 
 
-# A fork costs host time on every weight gradient (~66 per Inception step), so it avoids the
-# convenience wrappers: Stream.wait_stream() creates a new HIP event per call and the stream()
-# context manager re-resolves the device; here a ring of pre-created events is re-recorded (a
-# recorded event may be recorded again once the wait on it is enqueued) and the current stream is
-# switched with the raw setter.
-_EVENTS: Dict[int, List] = {}
+# A fork costs host time on every weight gradient, branch and bucket (~150 per Inception step), so it
+# avoids the convenience wrappers: Stream.wait_stream() creates a new HIP event per call, and even a
+# pooled torch.cuda.Event's record + wait_event is ~7.6 us of host time (tools/host_micro.py).  Here
+# ONE fast-call (csrc/streams.hip tony_fork) records a pooled timing-free HIP event on the producer
+# and makes the consumer wait on it (a recorded event may be recorded again once the wait on it is
+# enqueued); the current stream is switched with the raw setter.
 _ev_next = [0]
 _EV_RING = 256
+_RAW: Dict[int, List[int]] = {}
+_FORK = [None]
 
 
-def _fork_event(device_index: int):
-    ring = _EVENTS.get(device_index)
+def _raw_ring(device_index: int) -> List[int]:
+    ring = _RAW.get(device_index)
     if ring is None:
-        ring = _EVENTS[device_index] = [torch.cuda.Event() for _ in range(_EV_RING)]
-    ev = ring[_ev_next[0] % _EV_RING]
-    _ev_next[0] += 1
-    return ev
+        import ctypes
+
+        buf = (ctypes.c_uint64 * _EV_RING)()
+        with torch.cuda.device(device_index):
+            _lib.check(_lib.lib().tony_event_pool(_EV_RING, buf), "tony_event_pool")
+        ring = _RAW[device_index] = list(buf)
+        _FORK[0] = _lib.lib().tony_fork
+    return ring
+
+
+_BY_HANDLE: Dict[int, torch.cuda.Stream] = {}
+
+
+def current(device_index: int) -> torch.cuda.Stream:
+    """torch.cuda.current_stream(device) without its ~2.6 us of host time (tools/host_micro.py): the
+    raw current handle (one C call) maps to the Stream object seen the first time (torch never
+    destroys its pooled streams, so a handle names one stream for the whole process)."""
+    h = _lib._RAW_STREAM(device_index) if _lib._RAW_STREAM is not None else None
+    s = _BY_HANDLE.get(h) if h is not None else None
+    if s is None:
+        s = torch.cuda.current_stream(device_index)
+        if h is not None:
+            _BY_HANDLE[h] = s
+    return s
+
+
+def fork(producer: torch.cuda.Stream, consumer: torch.cuda.Stream) -> None:
+    """``consumer`` waits for everything enqueued on ``producer`` so far (no host block)."""
+    ring = _RAW.get(producer.device_index) or _raw_ring(producer.device_index)
+    i = _ev_next[0]
+    _ev_next[0] = i + 1
+    rc = _FORK[0](ring[i % _EV_RING], producer.cuda_stream, consumer.cuda_stream)
+    if rc:
+        _lib.check(rc, "tony_fork")
 
 
 def _flush(side: torch.cuda.Stream) -> None:
@@ -160,10 +197,8 @@ def _flush(side: torch.cuda.Stream) -> None:
         _pending.clear()
     if not work:
         return
-    cur = torch.cuda.current_stream(side.device)
-    ev = _fork_event(side.device_index)
-    ev.record(cur)
-    side.wait_event(ev)
+    cur = current(side.device_index)
+    fork(cur, side)
     torch.cuda.set_stream(side)
     try:
         for fn in work:
@@ -214,9 +249,7 @@ def fence_into(stream: torch.cuda.Stream) -> None:
     for s in [side, *_used.values()]:
         if s is stream:
             continue
-        ev = _fork_event(s.device_index)
-        ev.record(s)
-        stream.wait_event(ev)
+        fork(s, stream)
 
 
 def end() -> int:
@@ -227,10 +260,10 @@ def end() -> int:
     _branches_on[0] = False
     if side is not None:
         _flush(side)
-        cur = torch.cuda.current_stream(side.device)
-        cur.wait_stream(side)
+        cur = current(side.device_index)
+        fork(side, cur)
         for s in _used.values():  # backward kernels of branch nodes ran on these
-            cur.wait_stream(s)
+            fork(s, cur)
         _used.clear()
     with _lock:
         _keep.clear()

@@ -177,9 +177,7 @@ class _Ref:
 def _wait(stream: Optional[torch.cuda.Stream], producer: Optional[torch.cuda.Stream]) -> None:
     if stream is None or producer is None or producer is stream:
         return
-    ev = streams._fork_event(stream.device_index)
-    ev.record(producer)
-    stream.wait_event(ev)
+    streams.fork(producer, stream)
 
 
 def recording() -> bool:

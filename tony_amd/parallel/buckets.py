@@ -108,8 +108,10 @@ class GradBucketEngine:
         self._seen: List[bool] = [False] * len(flat.slots)
         self.device = flat.device
         self.comm: Optional[torch.cuda.Stream] = None
+        self._dev_index = -1
         if self.device.type == "cuda":
             self.comm = torch.cuda.Stream(device=self.device)
+            self._dev_index = self.comm.device_index
         self._hooks: Dict[int, object] = {}
         self._inplace = [False] * len(flat.slots)  # reported by a fused op: its AccumulateGrad hook is dropped
         esz = flat.grad.element_size()
@@ -214,10 +216,8 @@ class GradBucketEngine:
         if self.comm is None:
             self.launch_fn(b)
             return
-        cur = torch.cuda.current_stream(self.device)
-        ev = streams._fork_event(self.device.index)
-        ev.record(cur)
-        self.comm.wait_event(ev)
+        cur = streams.current(self._dev_index)
+        streams.fork(cur, self.comm)
         streams.fence_into(self.comm)  # the weight-gradient side stream's writes, too
         torch.cuda.set_stream(self.comm)
         try:
@@ -253,4 +253,4 @@ class GradBucketEngine:
                 finally:
                     torch.cuda.set_stream(cur)
         if self.comm is not None:
-            torch.cuda.current_stream(self.device).wait_stream(self.comm)
+            streams.fork(self.comm, streams.current(self._dev_index))

@@ -73,6 +73,10 @@ def main():
         s.wait_event(ev)
 
     out["event_fork_us"] = bench(fork, a.iters)
+    main = torch.cuda.current_stream()
+    out["native_fork_us"] = bench(lambda: streams.fork(main, s), a.iters)
+    out["set_stream_pair_us"] = bench(lambda: (torch.cuda.set_stream(s), torch.cuda.set_stream(main)), a.iters)
+    out["current_stream_us"] = bench(lambda: torch.cuda.current_stream(), a.iters)
     ar = arena.for_device(dev)
     ar.begin_step()
     out["arena_slice_us"] = bench(lambda: arena.zeros_f32(128, dev), 2000)
