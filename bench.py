@@ -334,7 +334,7 @@ def main():
     # enqueues the steps): equal to ms_per_step when the step is GPU-bound, lower when host launch
     # overhead leaves the GPU waiting
     gpu_ahead = host_free = None
-    if world == 1 and trainer.use_graph is False:
+    if world == 1 and (trainer.use_graph is False or getattr(trainer, "plan", None) is not None):
         n_ahead = 6
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -397,8 +397,10 @@ def main():
                 "grad_dtype": "fp32" if grad_dtype == torch.float32 else "bf16",
                 "variables": f"fp32 master on the PS, {args.dtype} compute copy",
                 "optimizer": "fused SGD-momentum (HIP)" if args.optimizer == "sgd" else args.optimizer,
-                "hip_graph": mode == "graph",
-                "step_mode": mode,
+                "hip_graph": mode == "graph" and getattr(trainer, "replay_kind", None) == "graph",
+                # plan: the step captured once and re-issued natively (ops/plan.py, csrc/plan.hip)
+                "step_mode": "plan" if mode == "graph" and getattr(trainer, "replay_kind", None) == "plan" else mode,
+                "plan_stats": trainer.plan.stats if getattr(trainer, "plan", None) is not None else None,
                 "mode_setup_ms": setup or None,
                 "tune_cache_loaded": tune_loaded,
                 "wgrad_stream": not args.no_wgrad_stream,

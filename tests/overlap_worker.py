@@ -33,7 +33,7 @@ def _data(rank, kind, dev):
     return x.contiguous(memory_format=torch.channels_last), torch.randint(0, 10, (8,), generator=g, device=dev)
 
 
-def ps_run(rank, kind, overlap, bucket_mb, steps=3):
+def ps_run(rank, kind, overlap, bucket_mb, steps=3, graph=False):
     from tony_amd.ops import cross_entropy
     from tony_amd.parallel.ps import ParameterServer
     from tony_amd.parallel.trainer import Trainer
@@ -42,7 +42,9 @@ def ps_run(rank, kind, overlap, bucket_mb, steps=3):
     model = _model(kind, dev)
     ps = ParameterServer(model, optimizer="sgd", lr=0.05, momentum=0.9, device=dev, bucket_mb=bucket_mb,
                          bucketed_single=True)
-    tr = Trainer(model, ps, lambda o, y: cross_entropy(o, y), overlap_comm=overlap)
+    # graph: the step captured once and replayed natively (ops/plan.py) -- with several ranks the
+    # buckets' collectives are issued between plan segments (parallel/trainer.py _replay_overlapped)
+    tr = Trainer(model, ps, lambda o, y: cross_entropy(o, y), overlap_comm=overlap, use_graph=graph, warmup_eager=1)
     x, y = _data(rank, kind, dev)
     from tony_amd.parallel import collectives as coll
 
@@ -53,7 +55,8 @@ def ps_run(rank, kind, overlap, bucket_mb, steps=3):
         tr.step(x, y)
     torch.cuda.synchronize()
     return {"params": ps.flat.data.float().cpu(), "log": ps.engine.log, "n_buckets": len(ps.buckets),
-            "overlapped": ps.overlapped_buckets, "train_fallbacks": coll.fallback_count() - fb0}
+            "overlapped": ps.overlapped_buckets, "train_fallbacks": coll.fallback_count() - fb0,
+            "replay": tr.replay_kind, "plan_buckets": tr.plan_buckets, "plan_error": tr.plan_error}
 
 
 def ddp_run(rank, kind, bucket_mb):
@@ -89,6 +92,7 @@ def run(rank, world, port, q, kind, bucket_mb):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         out = {}
         for name, fn in (("ps_overlap", lambda: ps_run(rank, kind, True, bucket_mb)),
+                         ("ps_plan", lambda: ps_run(rank, kind, True, bucket_mb, graph=True)),
                          ("ps_serial", lambda: ps_run(rank, kind, False, bucket_mb)),
                          ("ddp", lambda: ddp_run(rank, kind, bucket_mb))):
             print(f"rank {rank}: {name}", file=trace, flush=True)

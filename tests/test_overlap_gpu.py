@@ -80,11 +80,18 @@ def test_two_ranks_overlap_ps_and_ddp(cuda, kind, collective, monkeypatch):
     assert torch.equal(o0["params"], o1["params"])               # every rank pulled the same variables
     err = (o0["params"] - out[0]["ps_serial"]["params"]).abs().max().item()
     assert err < 1e-2, err
+    # the natively replayed step (ops/plan.py) with the buckets issued between plan segments
+    p0, p1 = out[0]["ps_plan"], out[1]["ps_plan"]
+    assert p0["replay"] == "plan" and p0["plan_buckets"], p0["plan_error"]
+    assert p0["overlapped"] >= p0["n_buckets"] - 1, (p0["overlapped"], p0["n_buckets"])
+    assert torch.equal(p0["params"], p1["params"])
+    err = (p0["params"] - out[0]["ps_serial"]["params"]).abs().max().item()
+    assert err < 1e-2, err
     d0, d1 = out[0]["ddp"], out[1]["ddp"]
     assert d0["launches"] == d0["n_buckets"] and d0["overlapped"] >= d0["n_buckets"] - 1
     assert torch.equal(d0["grad"], d1["grad"])                    # averaged gradients identical on both ranks
     assert d0["grad"].abs().sum().item() > 0
     if collective == "hip":  # every bucket push / pull / all-reduce ran on the xGMI kernels
         for r in range(world):
-            for name in ("ps_overlap", "ps_serial", "ddp"):
+            for name in ("ps_overlap", "ps_plan", "ps_serial", "ddp"):
                 assert out[r][name]["train_fallbacks"] == 0, (r, name, "a bucket collective fell back to gloo")

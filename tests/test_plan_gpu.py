@@ -1,0 +1,142 @@
+"""Native step replay (ops/plan.py, csrc/plan.hip): a captured multi-stream step re-issued from C++
+must compute exactly what the eager issue computes, keep cross-stream dependencies, and train like
+the eager and hipGraph-replayed steps."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _capture(fn):
+    g = torch.cuda.CUDAGraph(keep_graph=True)
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g):
+        out = fn()
+    return g, out
+
+
+def _streams(n):
+    return [torch.cuda.Stream() for _ in range(n)]
+
+
+def test_plan_replays_forked_streams(cuda):
+    from tony_amd.ops import streams
+    from tony_amd.ops.plan import StepPlan
+
+    dev = torch.device("cuda", 0)
+    x = torch.randn(1 << 20, device=dev)
+    side = _streams(2)
+
+    def body():
+        cur = torch.cuda.current_stream()
+        y = x * 2.0
+        outs = []
+        for s, k in zip(side, (1.0, 5.0)):
+            streams.fork(cur, s)
+            with torch.cuda.stream(s):
+                t = y + k
+                t = t * t  # a chain of two kernels on the branch stream
+            outs.append(t)
+        w = y * 3.0
+        for s in side:
+            streams.fork(s, cur)
+        return outs[0] + outs[1] + w
+
+    g, out = _capture(body)
+    plan = StepPlan(g, [torch.cuda.current_stream(), *_streams(3)])
+    st = plan.stats
+    assert st["kernels"] == 8 and st["memsets"] == 0 and st["markers"] == 0, st
+    assert st["false_deps"] == 0, st
+    assert st["waits"] >= 2 and st["streams_used"] >= 2, st  # the branches run on their own streams
+    for trial in range(3):
+        x.copy_(torch.randn_like(x))
+        plan.replay()
+        y = x * 2.0
+        t1, t2 = y + 1.0, y + 5.0
+        ref = t1 * t1 + t2 * t2 + y * 3.0
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), trial
+    plan.close()
+
+
+def test_plan_segments_fork_into_side_stream(cuda):
+    """A marker splits the plan; the host's work on the side stream follows the marker and the
+    second segment reads what the host wrote there only through its own dependencies."""
+    from tony_amd.ops.plan import StepPlan, mark
+
+    dev = torch.device("cuda", 0)
+    x = torch.randn(1 << 18, device=dev)
+
+    def body():
+        a = x + 1.0
+        mark(0)
+        b = a * 2.0
+        return a, b
+
+    g, (a, b) = _capture(body)
+    plan = StepPlan(g, [torch.cuda.current_stream(), *_streams(2)])
+    assert plan.segments == 2 and plan.stats["markers"] == 1
+    kinds = [k for k, _, _ in plan.ops()]
+    assert kinds.count(5) == 1 and kinds.count(0) == 2
+    comm = torch.cuda.Stream()
+    seen = torch.empty_like(x)
+    for _ in range(2):
+        x.copy_(torch.randn_like(x))
+        plan.replay(0, comm)
+        with torch.cuda.stream(comm):
+            seen.copy_(a)  # host-issued work after the marker sees segment 0's result
+        plan.replay(1)
+        torch.cuda.current_stream().wait_stream(comm)
+        torch.cuda.synchronize()
+        assert torch.equal(seen, x + 1.0)
+        assert torch.equal(b, (x + 1.0) * 2.0)
+    plan.close()
+
+
+def _train(replay, kind, monkeypatch, steps=5):
+    import tony_amd.parallel.trainer as trainer_mod
+    from tony_amd.models import inception_v3 as iv3
+    from tony_amd.models.layers import init_weights
+    from tony_amd.ops import cross_entropy
+    from tony_amd.ops.pool import global_avg_pool
+    from tony_amd.parallel.ps import ParameterServer
+
+    class Net(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.block = {"A": lambda: iv3.InceptionA(64, 32), "C": lambda: iv3.InceptionC(64, 32)}[kind]()
+            self.fc = torch.nn.Linear(self.block.out_channels, 10)
+
+        def forward(self, x):
+            return self.fc(global_avg_pool(self.block(x)))
+
+    monkeypatch.setattr(trainer_mod, "REPLAY", replay or "plan")
+    dev = torch.device("cuda", 0)
+    hw = 35 if kind == "A" else 17
+    model = init_weights(Net(), seed=0).to(dev).to(memory_format=torch.channels_last).train()
+    ps = ParameterServer(model, optimizer="sgd", lr=0.05, momentum=0.9, device=dev)
+    tr = trainer_mod.Trainer(model, ps, lambda o, y: cross_entropy(o, y), use_graph=replay is not None,
+                             warmup_eager=1, graph_collectives=True if replay else None)
+    g = torch.Generator(device=dev).manual_seed(7)
+    x = torch.randn((16, 64, hw, hw), generator=g, device=dev).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (16,), generator=g, device=dev)
+    losses = [float(tr.step(x, y).float().item()) for _ in range(steps)]
+    torch.cuda.synchronize()
+    return losses, ps.flat.data.float().clone(), tr
+
+
+@pytest.mark.parametrize("kind", ["A", "C"])
+def test_trainer_plan_matches_eager_and_graph(cuda, kind, monkeypatch):
+    le, pe, _ = _train(None, kind, monkeypatch)
+    lp, pp, tp = _train("plan", kind, monkeypatch)
+    lg, pg, tg = _train("graph", kind, monkeypatch)
+    assert tp.replay_kind == "plan", tp.plan_error
+    assert tg.replay_kind == "graph"
+    st = tp.plan.stats
+    assert st["kernels"] > 20 and st["streams_used"] >= 2, st  # branches + weight-gradient stream kept
+    for ref, lv, pv in ((le, lp, pp), (lg, lp, pp)):
+        for a, b in zip(lv, ref):
+            assert abs(a - b) <= 2e-2 * max(1.0, abs(b)), (lv, ref)
+    assert (pp - pe).abs().max().item() < 2e-2
+    assert (pp - pg).abs().max().item() < 2e-2

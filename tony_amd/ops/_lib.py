@@ -117,6 +117,13 @@ _SIGNATURES = {
     # cross-stream forks / joins of the eager step (csrc/streams.hip, ops/streams.py)
     "tony_event_pool": [c_int, c_u64_p],
     "tony_fork": [c_void_p, c_void_p, c_void_p],
+    # native replay of a captured step (csrc/plan.hip, ops/plan.py)
+    "tony_plan_mark": [c_int, c_void_p],
+    "tony_plan_build": [c_void_p, c_u64_p, c_int, c_u64_p, c_int_p],
+    "tony_plan_replay": [c_void_p, c_int, c_void_p],
+    "tony_plan_segments": [c_void_p],
+    "tony_plan_ops": [c_void_p, c_int_p, c_int],
+    "tony_plan_destroy": [c_void_p],
     # parameter-server data plane over xGMI windows (csrc/ps_plane.hip, parallel/ps_plane.py)
     "tony_ps_header_bytes": [],
     "tony_ps_max_buckets": [],

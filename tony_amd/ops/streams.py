@@ -74,6 +74,14 @@ def _branch_streams(device: torch.device, n: int) -> List[torch.cuda.Stream]:
     return pool[:n]
 
 
+def plan_streams(device, branches: int = 3) -> List[torch.cuda.Stream]:
+    """The side streams a natively replayed step may use (ops/plan.py): the weight-gradient stream
+    and ``branches`` branch streams -- the same streams (and so the same hardware queues) as the
+    eager step's."""
+    device = torch.device(device)
+    return [_side(device), *_branch_streams(device, branches)]
+
+
 def begin(device, branches: bool = False) -> bool:
     """Route in-place weight gradients to the side stream (and, with ``branches``, model branches to
     branch streams) until ``end()``; False when disabled."""

@@ -118,6 +118,11 @@ class GradBucketEngine:
         self._slot_ptr = [flat.grad.data_ptr() + s.offset * esz for s in flat.slots]
         self.armed = False
         self.overlap = False
+        # native step replay (ops/plan.py): during the capture of a step each bucket's launch point is
+        # captured as a plan marker instead; replays then issue the plan segment by segment and the
+        # bucket's collective after each (``replay_launch``), in ``marked`` order
+        self.capture_markers = False
+        self.marked: List[int] = []
         self._next = 0
         self.launches = 0
         self.launched_during_backward = 0  # buckets issued before end() (the overlap actually happened)
@@ -142,15 +147,46 @@ class GradBucketEngine:
         self._hooks = {}
 
     # -- per step -------------------------------------------------------------------------------
-    def begin(self, overlap: bool = True) -> None:
-        """Arm for one backward pass; with ``overlap`` False nothing launches before ``end()``."""
+    def begin(self, overlap: bool = True, markers: bool = False) -> None:
+        """Arm for one backward pass; with ``overlap`` False nothing launches before ``end()``.
+        ``markers`` (inside a step capture only): record each bucket's launch point as a plan marker."""
         for b in self.buckets:
             b.pending, b.launched, b.work = len(b.params), False, None
         self._seen = [False] * len(self.flat.slots)
         self._next = 0
         self.launched_during_backward = 0
         self.armed = True
-        self.overlap = bool(overlap) and not (self.device.type == "cuda" and torch.cuda.is_current_stream_capturing())
+        capturing = self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()
+        self.capture_markers = bool(markers) and capturing and self.comm is not None
+        if self.capture_markers:
+            self.marked = []
+        self.overlap = (bool(overlap) and not capturing) or self.capture_markers
+
+    def end_capture(self) -> None:
+        """Close a marker capture: join the communication stream back (the capture must end joined)
+        and disarm without launching anything; ``marked`` keeps the bucket of each marker."""
+        if not self.capture_markers:
+            return
+        self.capture_markers = False
+        self.armed = False
+        self._drop_inplace_hooks()
+        streams.fork(self.comm, streams.current(self._dev_index))
+
+    def replay_launch(self, b: Bucket) -> None:
+        """Launch bucket ``b`` on the communication stream after a plan segment (the plan already
+        forked the marker's stream into it)."""
+        b.launched = True
+        self._next = max(self._next, b.index + 1)
+        self.launches += 1
+        self.launched_during_backward += 1
+        if self.log is not None:
+            self.log.append(f"launch:{b.index}")
+        cur = streams.current(self._dev_index)
+        torch.cuda.set_stream(self.comm)
+        try:
+            self.launch_fn(b)
+        finally:
+            torch.cuda.set_stream(cur)
 
     def cancel(self) -> None:
         """Disarm without launching anything (a gradient-accumulation pass)."""
@@ -219,6 +255,12 @@ class GradBucketEngine:
         cur = streams.current(self._dev_index)
         streams.fork(cur, self.comm)
         streams.fence_into(self.comm)  # the weight-gradient side stream's writes, too
+        if self.capture_markers:  # step capture: the launch point becomes a plan marker
+            from ..ops import plan
+
+            plan.mark(len(self.marked), self.comm)
+            self.marked.append(b.index)
+            return
         torch.cuda.set_stream(self.comm)
         try:
             self.launch_fn(b)

@@ -32,6 +32,11 @@ from .ps import ParameterServer
 GC_MODE = os.environ.get("TONY_GC", "freeze").lower()
 GC_EVERY = int(os.environ.get("TONY_GC_EVERY", "200"))
 
+# How a captured step is re-issued: "plan" (default) walks the captured hipGraph once and replays it
+# from C++ onto the eager step's streams (ops/plan.py, csrc/plan.hip); "graph" instantiates it and
+# calls hipGraphLaunch.  A graph the native replay cannot issue falls back to "graph".
+REPLAY = os.environ.get("TONY_REPLAY", "plan").lower()
+
 # Opt-in: measured slower on MI355X (bench 16.9 vs 15.7 ms/step; the compute queue's gaps grew from
 # 3.3 to 5.9 ms under rocprofv3), so the step stays on the caller's stream by default.
 PRIO_STREAM = os.environ.get("TONY_PRIO_STREAM", "0") == "1"
@@ -59,6 +64,10 @@ class Trainer:
         self.side_ops = 0
         self.host_fwd_s = self.host_bwd_s = 0.0
         self.graph = None
+        self.plan = None
+        self.plan_error = None
+        self.plan_buckets = False
+        self.replay_kind = None
         self.static_x = None
         self.static_y = None
         self.static_loss = None
@@ -205,7 +214,14 @@ class Trainer:
         if y.data_ptr() != self.static_y.data_ptr():
             self.static_y.copy_(y, non_blocking=True)
         self._refresh_hp()
-        self.graph.replay()
+        if self.plan is not None and self.plan_buckets:
+            self._replay_overlapped()
+            heartbeat()
+            return self.static_loss
+        if self.plan is not None:
+            self.plan.replay()
+        else:
+            self.graph.replay()
         if self.graph_collectives:
             self.ps.steps += 1
             for opt in self.ps.optimizers.values():
@@ -214,6 +230,18 @@ class Trainer:
             self._ps_step()  # eager push/apply/pull; ps.step() advances the counters itself
         heartbeat()
         return self.static_loss
+
+    def _replay_overlapped(self):
+        """Several ranks: the plan segment by segment, each gradient bucket's push / apply / pull
+        issued on the communication stream right after the segment that completes it -- the eager
+        step's overlap of communication with backward, at the plan's host cost."""
+        eng = self.ps.engine
+        self.ps.begin_step(overlap=True)
+        for k, bi in enumerate(eng.marked):
+            self.plan.replay(k, eng.comm)
+            eng.replay_launch(eng.buckets[bi])
+        self.plan.replay(len(eng.marked))
+        self._ps_step()  # the buckets not complete before the end of backward, the join, the weight cache
 
     def _refresh_hp(self):
         for opt in self.ps.optimizers.values():
@@ -225,20 +253,56 @@ class Trainer:
         self.static_x = x
         self.static_y = y
         torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
+        native = REPLAY == "plan"
+        g = torch.cuda.CUDAGraph(keep_graph=True) if native else torch.cuda.CUDAGraph()
         self._refresh_hp()
         inside = self.graph_collectives
+        # several ranks + native replay: the buckets' launch points are captured as plan markers, so
+        # replays can overlap the collectives (which stay outside the graph) with backward
+        eng = getattr(self.ps, "engine", None)
+        markers = native and not inside and self.overlap_comm and eng is not None and eng.comm is not None \
+            and bool(eng._hooks)
+
+        def body():
+            if markers:
+                eng.begin(overlap=True, markers=True)
+            out = self._body(self.static_x, self.static_y, ps_step=inside)
+            if markers:
+                eng.end_capture()
+            return out
+
         with torch.cuda.graph(g):
             if self.arena is not None:
                 with self.arena:  # its one fill is a node of the graph; the slices keep their addresses
-                    loss = self._body(self.static_x, self.static_y, ps_step=inside)
+                    loss = body()
             else:
-                loss = self._body(self.static_x, self.static_y, ps_step=inside)
+                loss = body()
             self.static_loss = loss.detach()
         if inside:
             self.ps.steps -= 1  # the capture itself did not train
             for opt in self.ps.optimizers.values():
                 opt.step_count -= 1
         self.graph = g
+        self.plan = None
+        self.plan_buckets = False
+        self.replay_kind = "graph"
+        if native:
+            from ..ops.plan import PlanUnsupported, StepPlan
+
+            dev = self.ps.flat.device
+            try:
+                # the compute stream the step is issued on, then the weight-gradient side stream and
+                # the branch streams: the streams the eager step runs on
+                self.plan = StepPlan(g, [streams.current(dev.index), *streams.plan_streams(dev)])
+                self.replay_kind = "plan"
+                if markers:
+                    ids = [m for k, _, m in self.plan.ops() if k == 5]
+                    self.plan_buckets = ids == list(range(len(eng.marked))) and \
+                        self.plan.segments == len(eng.marked) + 1
+                    if not self.plan_buckets:  # markers out of order: replay whole, buckets after
+                        self.plan_error = f"plan markers {ids} vs buckets {eng.marked}"
+            except PlanUnsupported as e:
+                self.plan_error = str(e)
+                g.instantiate()
         if self.wt is not None:
             self.wt.frozen = True  # the captured refresh() holds the current work list

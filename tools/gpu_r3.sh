@@ -16,6 +16,9 @@ step() {  # step <name> <timeout_s> <cmd...>
 for s in "$@"; do
   case $s in
     plane) step plane 500 python -u -m pytest tests/test_ps_plane_gpu.py tests/test_hvd_gpu.py tests/test_overlap_gpu.py -x -v --timeout 240 --timeout-method thread ;;
+    plan) step plan_tests 400 python -u -m pytest tests/test_plan_gpu.py tests/test_trainer_gpu.py -x -v --timeout 240 --timeout-method thread ;;
+    bench_plan) step bench_plan 400 python bench.py --steps 20 --warmup 6 --mode graph ;;
+    bench_graph) step bench_graph 400 env TONY_REPLAY=graph python bench.py --steps 20 --warmup 6 --mode graph ;;
     tests) step gpu_suite 800 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread ;;
     bench) step bench 400 python bench.py --steps 20 --warmup 6 ;;
     bench_r50) step bench_r50 400 python bench.py --model resnet50 --steps 20 --warmup 6 ;;
