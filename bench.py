@@ -216,10 +216,13 @@ def main():
     fp32 = args.dtype == "fp32"
     dtype = torch.float32 if fp32 else torch.bfloat16
     grad_dtype = {"bf16": torch.bfloat16, "fp32": torch.float32, None: dtype}[args.grad_dtype]
-    fused = not (args.stock or fp32)  # the tony kernels are bf16; fp32 = stock MIOpen / hipBLASLt layers
+    # fp32 (the reference's precision): Inception-v3 on the x3-split kernels (ops/x3.py: fp32 tensors,
+    # bf16-MFMA products of hi/lo operand planes); --stock: the stock MIOpen / hipBLASLt comparator
+    x3 = fp32 and not args.stock and args.model == "inception_v3"
+    fused = not (args.stock or fp32)
     if args.model == "inception_v3":
         from tony_amd.models.inception_v3 import inception_v3
-        model = inception_v3(fused=fused, seed=0)
+        model = inception_v3(fused=fused, seed=0, precision="fp32" if x3 else "bf16")
         res, aux_w = 299, 0.4
     else:
         from tony_amd.models.resnet import resnet50
@@ -237,7 +240,7 @@ def main():
                          wire_dtype=grad_dtype, **ps_kw)
     n_workers = len(ps.worker_ranks)
 
-    if fused:
+    if fused or x3:
         xent = cross_entropy
     else:
         def xent(logits, y):
@@ -401,6 +404,7 @@ def main():
                 # plan: the step captured once and re-issued natively (ops/plan.py, csrc/plan.hip)
                 "step_mode": "plan" if mode == "graph" and getattr(trainer, "replay_kind", None) == "plan" else mode,
                 "plan_stats": trainer.plan.stats if getattr(trainer, "plan", None) is not None else None,
+                "plan_error": getattr(trainer, "plan_error", None),
                 "mode_setup_ms": setup or None,
                 "tune_cache_loaded": tune_loaded,
                 "wgrad_stream": not args.no_wgrad_stream,
@@ -414,7 +418,9 @@ def main():
                 "host_ms_per_step_unblocked": None if host_free is None else round(1000.0 * host_free, 3),
                 "host_fwd_bwd_ms_last_eager_step": [round(1000.0 * trainer.host_fwd_s, 3),
                                                     round(1000.0 * trainer.host_bwd_s, 3)],
-                "kernels": "tony_amd HIP" if fused else "stock PyTorch-ROCm (MIOpen / hipBLASLt)",
+                "kernels": "tony_amd HIP" if fused else (
+                    "tony_amd HIP, fp32 via x3-split bf16 MFMA products (ops/x3.py)" if x3
+                    else "stock PyTorch-ROCm (MIOpen / hipBLASLt)"),
                 "conv_impl": _conv_impl_counts(),
                 "collective": "hip-xgmi" if os.environ.get("TONY_COLLECTIVE", "rccl").lower() in ("hip", "xgmi")
                 else ("rccl" if dist.is_initialized() and dist.get_backend() == "nccl" else None),

@@ -1,0 +1,145 @@
+"""The fp32 step on the x3-split kernels (ops/x3.py, csrc/x3.hip): every pass against a float64
+reference of the same op (CPU), and the whole Inception-v3 fp32 model against the stock fp32 graph."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def test_split_planes_reconstruct_fp32(cuda):
+    from tony_amd.ops import x3
+
+    x = torch.randn(1000, 40, device=DEV) * torch.logspace(-3, 3, 40, device=DEV)
+    p = x3.split_rows(x, 1000, 40, 40, x3.ACT)
+    assert p.shape == (1000, 3 * 40)
+    hi, lo, hi2 = p[:, :40].float(), p[:, 40:80].float(), p[:, 80:120].float()
+    assert torch.equal(hi, hi2)
+    err = ((hi + lo) - x).abs() / x.abs()
+    assert err.max().item() < 2 ** -16, err.max().item()
+    w = x3.split_rows(x, 1000, 40, 40, x3.WGT)
+    assert torch.equal(w[:, :40], w[:, 40:80]) and torch.equal(w[:, 80:].float(), lo)
+    # odd channel count: planes padded to 8, zero-filled
+    y = torch.randn(10, 3, device=DEV)
+    q = x3.split_rows(y, 10, 3, 3, x3.ACT)
+    assert q.shape == (10, 24) and q[:, 3:8].abs().sum().item() == 0
+
+
+SHAPES = [  # (N, C, H, W, Co, k, stride, padding)
+    (2, 32, 17, 17, 64, (3, 3), 1, 1),
+    (2, 64, 17, 17, 48, (1, 1), 1, 0),
+    (2, 32, 17, 17, 64, (3, 3), 2, 0),
+    (2, 48, 17, 17, 64, (1, 7), 1, (0, 3)),
+    (2, 3, 35, 35, 32, (3, 3), 2, 0),      # the image stem: 3 channels, planes padded to 8
+    (2, 80, 9, 9, 192, (3, 3), 1, 0),
+]
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=lambda s: f"{s[1]}x{s[2]}-{s[4]}-k{s[5]}-s{s[6]}")
+def test_conv_bn_relu_x3_matches_float64(cuda, shape):
+    """Forward output and every gradient of conv -> BN (batch stats) -> ReLU within 1e-4 of float64."""
+    from tony_amd.ops.x3 import ConvBNActX3
+
+    n, c, h, w, co, k, s, p = shape
+    torch.manual_seed(0)
+    layer = ConvBNActX3(c, co, k, s, p).to(DEV).to(memory_format=torch.channels_last).train()
+    with torch.no_grad():
+        layer.bn.weight.uniform_(0.5, 1.5)
+        layer.bn.bias.uniform_(-0.2, 0.2)
+    x = _cl(torch.randn(n, c, h, w, device=DEV)).requires_grad_(c % 8 == 0)
+    y = layer(x)
+    g = _cl(torch.randn_like(y))
+    y.backward(g)
+
+    xd = x.detach().double().cpu().requires_grad_(c % 8 == 0)
+    wd = layer.conv.weight.detach().double().cpu().requires_grad_()
+    gd = layer.bn.weight.detach().double().cpu().requires_grad_()
+    bd = layer.bn.bias.detach().double().cpu().requires_grad_()
+    z = F.conv2d(xd, wd, None, layer.conv.stride, layer.conv.padding)
+    yd = torch.relu(F.batch_norm(z, None, None, gd, bd, True, 0.0, layer.bn.eps))
+    yd.backward(g.double().cpu())
+    assert _rel(y.detach(), yd.detach()) < 1e-4
+    assert _rel(layer.conv.weight.grad, wd.grad) < 1e-4
+    assert _rel(layer.bn.weight.grad, gd.grad) < 1e-4
+    assert _rel(layer.bn.bias.grad, bd.grad) < 1e-4
+    if c % 8 == 0:
+        assert _rel(x.grad, xd.grad) < 1e-4
+    # running statistics updated like torch's
+    assert _rel(layer.bn.running_mean, 0.9 * 0 + 0.1 * z.detach().mean((0, 2, 3))) < 1e-4
+
+
+def test_linear_x3_matches_float64(cuda):
+    from tony_amd.ops.x3 import LinearX3
+
+    torch.manual_seed(1)
+    fc = LinearX3(2048, 1000).to(DEV)
+    x = torch.randn(16, 2048, device=DEV, requires_grad=True)
+    y = fc(x)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xd = x.detach().double().cpu().requires_grad_()
+    wd = fc.weight.detach().double().cpu().requires_grad_()
+    bd = fc.bias.detach().double().cpu().requires_grad_()
+    yd = F.linear(xd, wd, bd)
+    yd.backward(g.double().cpu())
+    assert _rel(y.detach(), yd.detach()) < 1e-4
+    assert _rel(x.grad, xd.grad) < 1e-4
+    assert _rel(fc.weight.grad, wd.grad) < 1e-4
+    assert _rel(fc.bias.grad, bd.grad) < 1e-5
+
+
+@pytest.mark.parametrize("op", ["max", "avg3", "avg5s3"])
+def test_fp32_pools_match_torch(cuda, op):
+    from tony_amd.ops.pool import avg_pool, avg_pool3x3_s1, max_pool
+
+    x = _cl(torch.randn(4, 64, 17, 17, device=DEV)).requires_grad_()
+    fn, ref = {"max": (lambda t: max_pool(t, 3, 2), lambda t: F.max_pool2d(t, 3, 2)),
+               "avg3": (avg_pool3x3_s1, lambda t: F.avg_pool2d(t, 3, 1, 1, count_include_pad=True)),
+               "avg5s3": (lambda t: avg_pool(t, 5, 3), lambda t: F.avg_pool2d(t, 5, 3))}[op]
+    y = fn(x)
+    g = _cl(torch.randn_like(y))
+    y.backward(g)
+    xr = x.detach().clone().requires_grad_()
+    yr = ref(xr)
+    yr.backward(g)
+    assert _rel(y.detach(), yr.detach()) < 1e-6
+    assert _rel(x.grad, xr.grad) < 1e-6
+
+
+def test_inception_fp32_step_matches_stock_fp32(cuda):
+    """One training step of the whole fp32 Inception-v3 (x3 kernels) against the stock fp32 graph
+    (MIOpen / hipBLASLt fp32) with the same weights: loss, logits and every parameter gradient."""
+    from tony_amd.models.inception_v3 import inception_v3
+    from tony_amd.ops import cross_entropy
+
+    torch.manual_seed(0)
+    ours = inception_v3(precision="fp32", seed=3).to(DEV).to(memory_format=torch.channels_last).train()
+    ref = inception_v3(fused=False, seed=3).to(DEV).to(memory_format=torch.channels_last).train()
+    ours.dropout.p = ref.dropout.p = 0.0
+    x = _cl(torch.randn(4, 3, 299, 299, device=DEV))
+    y = torch.randint(0, 1000, (4,), device=DEV)
+    lo, ao = ours(x)
+    lr_, ar = ref(x)
+    loss_o = cross_entropy(lo, y) + 0.4 * cross_entropy(ao, y)
+    loss_r = F.cross_entropy(lr_, y) + 0.4 * F.cross_entropy(ar, y)
+    loss_o.backward()
+    loss_r.backward()
+    assert abs(loss_o.item() - loss_r.item()) < 1e-4 * max(1.0, abs(loss_r.item()))
+    assert _rel(lo.detach(), lr_.detach()) < 1e-3
+    worst = []
+    for (name, po), pr in zip(ours.named_parameters(), ref.parameters()):
+        assert po.shape == pr.shape, name
+        worst.append((_rel(po.grad, pr.grad), name))
+    worst.sort(reverse=True)
+    assert worst[0][0] < 2e-3, worst[:5]

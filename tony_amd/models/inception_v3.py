@@ -26,6 +26,7 @@ from ..ops import conv as conv_ops
 from ..ops import streams, tape
 from ..ops.fused import FusedHead
 from ..ops.linear import Linear
+from ..ops.x3 import ConvBNActX3, LinearX3
 from .layers import ConvBNAct, conv_bn_act_maxpool, init_weights
 
 
@@ -46,25 +47,33 @@ def _slots(buf, widths):
 
 
 class _Block(nn.Module):
-    """A set of parallel branches whose outputs are concatenated on channels."""
+    """A set of parallel branches whose outputs are concatenated on channels.  ``x3``: the fp32 model
+    (ops/x3.py) -- the textbook graph with every conv + BN + ReLU, pool and classifier on the fp32 /
+    x3-split kernels."""
 
-    def __init__(self, fused):
+    def __init__(self, fused, x3=False):
         super().__init__()
-        self.fused = fused
+        self.fused = fused and not x3
+        self.x3 = x3
 
     def avgpool(self, x):
-        return avg_pool3x3_s1(x) if self.fused else nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=True)
+        if self.fused or self.x3:
+            return avg_pool3x3_s1(x)
+        return nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=True)
 
     def maxpool(self, x):
-        return max_pool(x, 3, 2) if self.fused else nn.functional.max_pool2d(x, 3, 2)
+        return max_pool(x, 3, 2) if (self.fused or self.x3) else nn.functional.max_pool2d(x, 3, 2)
 
     def c(self, cin, cout, k, s=1, p=0):
+        if self.x3:
+            return ConvBNActX3(cin, cout, k, s, p, eps=1e-3)
         return ConvBNAct(cin, cout, k, s, p, eps=1e-3, fused=self.fused)
 
 
 class InceptionA(_Block):
-    def __init__(self, cin, pool_ch, fused=True):
-        super().__init__(fused)
+    def __init__(self, cin, pool_ch, fused=True, x3=False):
+        super().__init__(fused, x3)
+        fused = self.fused
         if fused:
             # b1 1x1/64, b5 1x1/48, b3 1x1/64 and the pool branch's 1x1 share one GEMM
             self.head = FusedHead(cin, (64, 48, 64), pool_cout=pool_ch)
@@ -92,8 +101,8 @@ class InceptionA(_Block):
 
 
 class InceptionB(_Block):  # 35x35 -> 17x17 reduction
-    def __init__(self, cin, fused=True):
-        super().__init__(fused)
+    def __init__(self, cin, fused=True, x3=False):
+        super().__init__(fused, x3)
         self.b3 = self.c(cin, 384, 3, s=2)
         self.bd = nn.Sequential(self.c(cin, 64, 1), self.c(64, 96, 3, p=1), self.c(96, 96, 3, s=2))
         self.out_channels = 384 + 96 + cin
@@ -111,8 +120,9 @@ class InceptionB(_Block):  # 35x35 -> 17x17 reduction
 
 
 class InceptionC(_Block):  # 17x17 with factorised 7x7
-    def __init__(self, cin, c7, fused=True):
-        super().__init__(fused)
+    def __init__(self, cin, c7, fused=True, x3=False):
+        super().__init__(fused, x3)
+        fused = self.fused
         if fused:
             self.head = FusedHead(cin, (192, c7, c7), pool_cout=192)
             self.b7 = nn.Sequential(self.c(c7, c7, (1, 7), p=(0, 3)), self.c(c7, 192, (7, 1), p=(3, 0)))
@@ -142,8 +152,9 @@ class InceptionC(_Block):  # 17x17 with factorised 7x7
 
 
 class InceptionD(_Block):  # 17x17 -> 8x8 reduction
-    def __init__(self, cin, fused=True):
-        super().__init__(fused)
+    def __init__(self, cin, fused=True, x3=False):
+        super().__init__(fused, x3)
+        fused = self.fused
         if fused:
             self.head = FusedHead(cin, (192, 192))
             self.b3 = self.c(192, 320, 3, s=2)
@@ -169,8 +180,9 @@ class InceptionD(_Block):  # 17x17 -> 8x8 reduction
 
 
 class InceptionE(_Block):  # 8x8 with split 1x3 / 3x1 branches
-    def __init__(self, cin, fused=True):
-        super().__init__(fused)
+    def __init__(self, cin, fused=True, x3=False):
+        super().__init__(fused, x3)
+        fused = self.fused
         if fused:
             self.head = FusedHead(cin, (320, 384, 448), pool_cout=192)
         else:
@@ -209,35 +221,41 @@ class InceptionE(_Block):  # 8x8 with split 1x3 / 3x1 branches
 
 
 class InceptionAux(_Block):
-    def __init__(self, cin, num_classes, fused=True):
-        super().__init__(fused)
+    def __init__(self, cin, num_classes, fused=True, x3=False):
+        super().__init__(fused, x3)
         self.conv0 = self.c(cin, 128, 1)
         self.conv1 = self.c(128, 768, 5)
-        self.fc = (Linear if fused else nn.Linear)(768, num_classes)
+        self.fc = (LinearX3 if x3 else Linear if self.fused else nn.Linear)(768, num_classes)
 
     def forward(self, x):
-        x = avg_pool(x, 5, 3) if self.fused else nn.functional.avg_pool2d(x, 5, 3)
+        tony = self.fused or self.x3
+        x = avg_pool(x, 5, 3) if tony else nn.functional.avg_pool2d(x, 5, 3)
         x = self.conv1(self.conv0(x))
-        x = global_avg_pool(x) if self.fused else torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1)
+        x = global_avg_pool(x) if tony else torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)
 
 
 class InceptionV3(nn.Module):
-    def __init__(self, num_classes=1000, aux_logits=True, dropout=0.5, fused=True):
+    def __init__(self, num_classes=1000, aux_logits=True, dropout=0.5, fused=True, x3=False):
         super().__init__()
-        c = lambda cin, cout, k, s=1, p=0: ConvBNAct(cin, cout, k, s, p, eps=1e-3, fused=fused)  # noqa: E731
+        fused = fused and not x3
+        if x3:
+            c = lambda cin, cout, k, s=1, p=0: ConvBNActX3(cin, cout, k, s, p, eps=1e-3)  # noqa: E731
+        else:
+            c = lambda cin, cout, k, s=1, p=0: ConvBNAct(cin, cout, k, s, p, eps=1e-3, fused=fused)  # noqa: E731
+        kw = {"fused": fused, "x3": x3}
         self.stem = nn.ModuleList([c(3, 32, 3, s=2), c(32, 32, 3), c(32, 64, 3, p=1)])
         self.stem2 = nn.ModuleList([c(64, 80, 1), c(80, 192, 3)])
-        self.mixed_5 = nn.Sequential(InceptionA(192, 32, fused), InceptionA(256, 64, fused),
-                                     InceptionA(288, 64, fused))
-        self.mixed_6a = InceptionB(288, fused)
-        self.mixed_6 = nn.Sequential(InceptionC(768, 128, fused), InceptionC(768, 160, fused),
-                                     InceptionC(768, 160, fused), InceptionC(768, 192, fused))
-        self.aux = InceptionAux(768, num_classes, fused) if aux_logits else None
-        self.mixed_7 = nn.Sequential(InceptionD(768, fused), InceptionE(1280, fused), InceptionE(2048, fused))
+        self.mixed_5 = nn.Sequential(InceptionA(192, 32, **kw), InceptionA(256, 64, **kw), InceptionA(288, 64, **kw))
+        self.mixed_6a = InceptionB(288, **kw)
+        self.mixed_6 = nn.Sequential(InceptionC(768, 128, **kw), InceptionC(768, 160, **kw),
+                                     InceptionC(768, 160, **kw), InceptionC(768, 192, **kw))
+        self.aux = InceptionAux(768, num_classes, **kw) if aux_logits else None
+        self.mixed_7 = nn.Sequential(InceptionD(768, **kw), InceptionE(1280, **kw), InceptionE(2048, **kw))
         self.dropout = nn.Dropout(dropout)
-        self.fc = (Linear if fused else nn.Linear)(2048, num_classes)
+        self.fc = (LinearX3 if x3 else Linear if fused else nn.Linear)(2048, num_classes)
         self.fused = fused
+        self.x3 = x3
 
     def _stem_fwd(self, x):
         # the last conv of each group feeds a 3x3/2 max pool; fused training runs BN + ReLU + pool as
@@ -277,10 +295,17 @@ class InceptionV3(nn.Module):
             x = self.mixed_6(self.mixed_6a(self.mixed_5(x)))
             aux = self.aux(x) if (self.aux is not None and self.training) else None
             x = self.mixed_7(x)
-        x = global_avg_pool(x) if self.fused else torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1)
+        if self.fused or self.x3:
+            x = global_avg_pool(x)
+        else:
+            x = torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1)
         logits = self.fc(self.dropout(x))
         return (logits, aux) if aux is not None else logits
 
 
-def inception_v3(num_classes=1000, aux_logits=True, fused=True, seed=0) -> InceptionV3:
-    return init_weights(InceptionV3(num_classes, aux_logits, fused=fused), seed)
+def inception_v3(num_classes=1000, aux_logits=True, fused=True, seed=0, precision: str = "bf16") -> InceptionV3:
+    """``precision="fp32"``: the fp32 model on the x3-split kernels (ops/x3.py); "bf16": the bf16 model
+    (``fused`` picks the tony kernels or the stock comparator)."""
+    if precision not in ("bf16", "fp32"):
+        raise ValueError(f"precision must be bf16 or fp32, not {precision!r}")
+    return init_weights(InceptionV3(num_classes, aux_logits, fused=fused, x3=precision == "fp32"), seed)

@@ -123,7 +123,8 @@ def conv_bn_act_maxpool(layer: "ConvBNAct", x, k: int = 3, s: int = 2, padding: 
         return conv_ops.conv_bn_act_pool(x, c.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, c.stride,
                                          c.padding, bn.momentum, bn.eps, k, s, padding)
     y = layer(x)
-    return max_pool(y, k, s, padding=padding) if layer.fused else nn.functional.max_pool2d(y, k, s, padding)
+    tony_pool = layer.fused or getattr(layer, "x3", False)
+    return max_pool(y, k, s, padding=padding) if tony_pool else nn.functional.max_pool2d(y, k, s, padding)
 
 
 def cast_model(model: nn.Module, dtype: torch.dtype, device=None) -> nn.Module:

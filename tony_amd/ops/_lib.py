@@ -117,6 +117,25 @@ _SIGNATURES = {
     # cross-stream forks / joins of the eager step (csrc/streams.hip, ops/streams.py)
     "tony_event_pool": [c_int, c_u64_p],
     "tony_fork": [c_void_p, c_void_p, c_void_p],
+    # fp32 forms of the BN / pool kernels and the x3 operand split (csrc/x3.hip, ops/x3.py)
+    "tony_bn_stats_f32": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_void_p, c_int64, c_void_p],
+    "tony_bn_apply_f32": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p,
+                      c_void_p, c_int, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_float,
+                      c_void_p],
+    "tony_bn_bwd_reduce_f32": [c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p,
+                           c_void_p, c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p],
+    "tony_bn_bwd_apply_f32": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p,
+                          c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p,
+                          c_void_p, c_int, c_void_p],
+    "tony_avgpool3_s1p1_f32": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
+    "tony_maxpool_fwd_f32": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
+                         c_void_p],
+    "tony_maxpool_bwd_f32": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
+                         c_void_p],
+    "tony_avgpool_fwd_f32": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
+    "tony_avgpool_bwd_f32": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
+    "tony_x3_split": [c_void_p, c_int64, c_int64, c_int, c_int, c_void_p, c_int64, c_int, c_void_p],
+    "tony_x3_weights_t": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
     # native replay of a captured step (csrc/plan.hip, ops/plan.py)
     "tony_plan_mark": [c_int, c_void_p],
     "tony_plan_build": [c_void_p, c_u64_p, c_int, c_u64_p, c_int_p],

@@ -55,15 +55,16 @@ struct RowMap {
 struct Segs {
   int n = 0;
   int end[4] = {0, 0, 0, 0};
-  uint16_t* p[4] = {nullptr, nullptr, nullptr, nullptr};
+  void* p[4] = {nullptr, nullptr, nullptr, nullptr};
   int64_t ld[4] = {0, 0, 0, 0};
-  __device__ __forceinline__ void resolve(int col, uint16_t*& base, int64_t& ld_out) const {
+  template <class T>
+  __device__ __forceinline__ void resolve(int col, T*& base, int64_t& ld_out) const {
     int s = 0, start = 0;
     while (s + 1 < n && col >= end[s]) {
       start = end[s];
       ++s;
     }
-    base = p[s] + (col - start);
+    base = static_cast<T*>(p[s]) + (col - start);
     ld_out = ld[s];
   }
 };
@@ -108,8 +109,9 @@ __device__ __forceinline__ void block_reduce_add(float* red, const RowMap& rm, i
   }
 }
 
+template <class T>
 __global__ __launch_bounds__(kThreads) void bn_fwd_stats_kernel(
-    const uint16_t* __restrict__ x, int64_t M, int C, int64_t ldx, int64_t rows_per_block,
+    const T* __restrict__ x, int64_t M, int C, int64_t ldx, int64_t rows_per_block,
     float* __restrict__ sum, float* __restrict__ sumsq, int64_t sstride) {
   float* red = bn_dyn;  // bn_lds_reduce(C) bytes
   RowMap rm(C);
@@ -119,13 +121,13 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_stats_kernel(
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
   const int64_t r1 = min(M, r0 + rows_per_block);
   if (rm.active) {
-    const uint16_t* base = x + rm.cg * 8;
+    const T* base = x + rm.cg * 8;
     int64_t r = r0 + rm.rsub;
     const int64_t step = rm.RPI;
     for (; r + 3 * step < r1; r += 4 * step) {
-      bf16x8 v[4];
+      V8<T> v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = load8(base + (r + u * step) * ldx);
+      for (int u = 0; u < 4; ++u) v[u] = V8<T>::load(base + (r + u * step) * ldx);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         float f[8];
@@ -139,7 +141,7 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_stats_kernel(
     }
     for (; r < r1; r += step) {
       float f[8];
-      load8(base + r * ldx).to_float(f);
+      V8<T>::load(base + r * ldx).to_float(f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         s[j] += f[j];
@@ -154,11 +156,11 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_stats_kernel(
 // mode 0: training (stats from sums, saves mean/invstd, updates running stats)
 // mode 1: inference (stats from running_mean / running_var)
 // RES: y = act(bn(x) + res)  (ResNet bottleneck tail: BN + identity add + ReLU in one pass)
-template <bool RES>
+template <bool RES, class T = uint16_t>
 __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
-    const uint16_t* __restrict__ x, int64_t M, int C, int64_t ldx, int64_t rows_per_block,
-    const uint16_t* __restrict__ res, int64_t ldr,
-    uint16_t* __restrict__ y, int64_t ldy, const float* __restrict__ sum, const float* __restrict__ sumsq,
+    const T* __restrict__ x, int64_t M, int C, int64_t ldx, int64_t rows_per_block,
+    const T* __restrict__ res, int64_t ldr,
+    T* __restrict__ y, int64_t ldy, const float* __restrict__ sum, const float* __restrict__ sumsq,
     int64_t sstride, const void* gamma, const void* beta, int param_bf16, float eps, int relu, int mode,
     float* __restrict__ save_mean, float* __restrict__ save_invstd,
     float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, Segs segs) {
@@ -202,10 +204,10 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
   const int64_t r1 = min(M, r0 + rows_per_block);
   const int64_t step = rm.RPI;
   int64_t r = r0 + rm.rsub;
-  uint16_t* yb = y + rm.cg * 8;
+  T* yb = y + rm.cg * 8;
   int64_t ldyt = ldy;
   if (segs.n > 0) segs.resolve(rm.cg * 8, yb, ldyt);
-  auto body = [&](const bf16x8& v, const bf16x8& rv, int64_t row) {
+  auto body = [&](const V8<T>& v, const V8<T>& rv, int64_t row) {
     float f[8], q[8];
     v.to_float(f);
     if (RES) rv.to_float(q);
@@ -215,21 +217,21 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
       if (RES) t += q[j];
       f[j] = relu ? relu_f(t) : t;
     }
-    store8(yb + row * ldyt, bf16x8::from_float(f));
+    V8<T>::from_float(f).store(yb + row * ldyt);
   };
-  bf16x8 none{};
+  V8<T> none{};
   for (; r + 3 * step < r1; r += 4 * step) {
-    bf16x8 v[4], rv[4];
+    V8<T> v[4], rv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      v[u] = load8(x + (r + u * step) * ldx + rm.cg * 8);
-      if (RES) rv[u] = load8(res + (r + u * step) * ldr + rm.cg * 8);
+      v[u] = V8<T>::load(x + (r + u * step) * ldx + rm.cg * 8);
+      if (RES) rv[u] = V8<T>::load(res + (r + u * step) * ldr + rm.cg * 8);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) body(v[u], RES ? rv[u] : none, r + u * step);
   }
   for (; r < r1; r += step)
-    body(load8(x + r * ldx + rm.cg * 8), RES ? load8(res + r * ldr + rm.cg * 8) : none, r);
+    body(V8<T>::load(x + r * ldx + rm.cg * 8), RES ? V8<T>::load(res + r * ldr + rm.cg * 8) : none, r);
 }
 
 // Backward reduction: dsums[c] = sum(dy'), dsums[C+c] = sum(dy' * xhat),
@@ -237,10 +239,10 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
 // residual form where the ReLU followed an add -- masked by the saved output y.
 // Per-channel coefficients are built once per workgroup in LDS (xhat = x*p0 + p1,
 // pre-activation = x*p2 + p3), so no lane waits on scattered parameter loads.
-template <bool YMASK>
+template <bool YMASK, class T = uint16_t>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
-    const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __restrict__ dy, int64_t lddy,
-    const uint16_t* __restrict__ ym, int64_t ldym,
+    const T* __restrict__ x, int64_t ldx, const T* __restrict__ dy, int64_t lddy,
+    const T* __restrict__ ym, int64_t ldym,
     int64_t M, int C, int64_t rows_per_block, const float* __restrict__ mean,
     const float* __restrict__ invstd, const void* gamma, const void* beta, int param_bf16,
     int relu, float* __restrict__ dsum, float* __restrict__ dsumx, int64_t sstride, Segs segs) {
@@ -271,7 +273,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
     const int64_t r1 = min(M, r0 + rows_per_block);
     const int64_t step = rm.RPI;
-    auto body = [&](const bf16x8& xv, const bf16x8& gv, const bf16x8& yv) {
+    auto body = [&](const V8<T>& xv, const V8<T>& gv, const V8<T>& yv) {
       float xf[8], gf[8], yf[8];
       xv.to_float(xf);
       gv.to_float(gf);
@@ -289,28 +291,28 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
         b[j] = fmaf(d, xh, b[j]);
       }
     };
-    bf16x8 none{};
-    const uint16_t* db = dy + rm.cg * 8;
+    V8<T> none{};
+    const T* db = dy + rm.cg * 8;
     int64_t lddt = lddy;
     if (segs.n > 0) {
-      uint16_t* b;
+      T* b;
       segs.resolve(rm.cg * 8, b, lddt);
       db = b;
     }
     int64_t r = r0 + rm.rsub;
     for (; r + 3 * step < r1; r += 4 * step) {
-      bf16x8 xv[4], gv[4], yv[4];
+      V8<T> xv[4], gv[4], yv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        xv[u] = load8(x + (r + u * step) * ldx + rm.cg * 8);
-        gv[u] = load8(db + (r + u * step) * lddt);
-        if (YMASK) yv[u] = load8(ym + (r + u * step) * ldym + rm.cg * 8);
+        xv[u] = V8<T>::load(x + (r + u * step) * ldx + rm.cg * 8);
+        gv[u] = V8<T>::load(db + (r + u * step) * lddt);
+        if (YMASK) yv[u] = V8<T>::load(ym + (r + u * step) * ldym + rm.cg * 8);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) body(xv[u], gv[u], YMASK ? yv[u] : none);
     }
     for (; r < r1; r += step)
-      body(load8(x + r * ldx + rm.cg * 8), load8(db + r * lddt), YMASK ? load8(ym + r * ldym + rm.cg * 8) : none);
+      body(V8<T>::load(x + r * ldx + rm.cg * 8), V8<T>::load(db + r * lddt), YMASK ? V8<T>::load(ym + r * ldym + rm.cg * 8) : none);
   }
   const int64_t so = shard_off(blockIdx.x, sstride);
   block_reduce_add(red, rm, C, a, b, dsum + so, dsumx + so);
@@ -319,11 +321,11 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
 // dx = k*(dy' - dsum/M - xhat*dsumx/M) folded per channel into dx = dy'*q0 + x*q1 + q2 (LDS table,
 // with the ReLU test x*q3 + q4 > 0).  YMASK: mask dy by the saved output y and also write the
 // masked dy -- the gradient of the residual branch -- to dres (when non-null).
-template <bool YMASK>
+template <bool YMASK, class T = uint16_t>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
-    const uint16_t* __restrict__ x, int64_t ldx, const uint16_t* __restrict__ dy, int64_t lddy,
-    const uint16_t* __restrict__ ym, int64_t ldym, uint16_t* __restrict__ dres, int64_t lddr,
-    uint16_t* __restrict__ dx, int64_t lddx, int64_t M, int C, int64_t rows_per_block,
+    const T* __restrict__ x, int64_t ldx, const T* __restrict__ dy, int64_t lddy,
+    const T* __restrict__ ym, int64_t ldym, T* __restrict__ dres, int64_t lddr,
+    T* __restrict__ dx, int64_t lddx, int64_t M, int C, int64_t rows_per_block,
     const float* __restrict__ mean, const float* __restrict__ invstd, const void* gamma,
     const void* beta, int param_bf16, int relu, const float* __restrict__ dsum,
     const float* __restrict__ dsumx, int64_t sstride, void* dgamma, void* dbeta, int accumulate, Segs segs) {
@@ -361,7 +363,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
   const int64_t r1 = min(M, r0 + rows_per_block);
   const int64_t step = rm.RPI;
-  auto body = [&](const bf16x8& xv, const bf16x8& gv, const bf16x8& yv, int64_t row) {
+  auto body = [&](const V8<T>& xv, const V8<T>& gv, const V8<T>& yv, int64_t row) {
     float xf[8], gf[8], yf[8], o[8];
     xv.to_float(xf);
     gv.to_float(gf);
@@ -377,31 +379,31 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
       }
       o[j] = fmaf(d, q0[j], fmaf(xf[j], q1[j], q2[j]));
     }
-    store8(dx + row * lddx + rm.cg * 8, bf16x8::from_float(o));
-    if (YMASK && dres != nullptr) store8(dres + row * lddr + rm.cg * 8, bf16x8::from_float(gf));
+    V8<T>::from_float(o).store(dx + row * lddx + rm.cg * 8);
+    if (YMASK && dres != nullptr) V8<T>::from_float(gf).store(dres + row * lddr + rm.cg * 8);
   };
-  bf16x8 none{};
-  const uint16_t* db = dy + rm.cg * 8;
+  V8<T> none{};
+  const T* db = dy + rm.cg * 8;
   int64_t lddt = lddy;
   if (segs.n > 0) {
-    uint16_t* b;
+    T* b;
     segs.resolve(rm.cg * 8, b, lddt);
     db = b;
   }
   int64_t r = r0 + rm.rsub;
   for (; r + 3 * step < r1; r += 4 * step) {
-    bf16x8 xv[4], gv[4], yv[4];
+    V8<T> xv[4], gv[4], yv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      xv[u] = load8(x + (r + u * step) * ldx + rm.cg * 8);
-      gv[u] = load8(db + (r + u * step) * lddt);
-      if (YMASK) yv[u] = load8(ym + (r + u * step) * ldym + rm.cg * 8);
+      xv[u] = V8<T>::load(x + (r + u * step) * ldx + rm.cg * 8);
+      gv[u] = V8<T>::load(db + (r + u * step) * lddt);
+      if (YMASK) yv[u] = V8<T>::load(ym + (r + u * step) * ldym + rm.cg * 8);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) body(xv[u], gv[u], YMASK ? yv[u] : none, r + u * step);
   }
   for (; r < r1; r += step)
-    body(load8(x + r * ldx + rm.cg * 8), load8(db + r * lddt), YMASK ? load8(ym + r * ldym + rm.cg * 8) : none, r);
+    body(V8<T>::load(x + r * ldx + rm.cg * 8), V8<T>::load(db + r * lddt), YMASK ? V8<T>::load(ym + r * ldym + rm.cg * 8) : none, r);
 }
 
 // ---- one-launch BN(+ReLU) backward: reduce -> grid barrier -> apply ------------------------------
@@ -718,7 +720,7 @@ TONY_API int tony_bn_stats(const void* x, int64_t M, int C, int64_t ldx, float* 
   int64_t rpb;
   int grid;
   plan_rows(M, C, 8, 512, &rpb, &grid);  // few WGs: C atomics per WG contend per channel
-  bn_fwd_stats_kernel<<<grid, kThreads, bn_lds_reduce(C), stream>>>(static_cast<const uint16_t*>(x), M, C, ldx, rpb, sum, sumsq,
+  bn_fwd_stats_kernel<uint16_t><<<grid, kThreads, bn_lds_reduce(C), stream>>>(static_cast<const uint16_t*>(x), M, C, ldx, rpb, sum, sumsq,
                                                       sstride);
   TONY_LAUNCH_CHECK();
   return 0;
@@ -734,7 +736,7 @@ TONY_API int tony_bn_apply(const void* x, int64_t M, int C, int64_t ldx, void* y
   int64_t rpb;
   int grid;
   plan_rows(M, C, 4, 8192, &rpb, &grid);
-  bn_fwd_apply_kernel<false><<<grid, kThreads, bn_lds_table(C, 2), stream>>>(
+  bn_fwd_apply_kernel<false, uint16_t><<<grid, kThreads, bn_lds_table(C, 2), stream>>>(
       static_cast<const uint16_t*>(x), M, C, ldx, rpb, nullptr, 0, static_cast<uint16_t*>(y), ldy, sum, sumsq,
       sstride, gamma, beta, param_bf16, eps, relu, mode, save_mean, save_invstd, running_mean, running_var, momentum, Segs{});
   TONY_LAUNCH_CHECK();
@@ -751,7 +753,7 @@ TONY_API int tony_bn_apply_res(const void* x, int64_t M, int C, int64_t ldx, con
   int64_t rpb;
   int grid;
   plan_rows(M, C, 4, 8192, &rpb, &grid);
-  bn_fwd_apply_kernel<true><<<grid, kThreads, bn_lds_table(C, 2), stream>>>(
+  bn_fwd_apply_kernel<true, uint16_t><<<grid, kThreads, bn_lds_table(C, 2), stream>>>(
       static_cast<const uint16_t*>(x), M, C, ldx, rpb, static_cast<const uint16_t*>(res), ldr,
       static_cast<uint16_t*>(y), ldy, sum, sumsq, sstride, gamma, beta, param_bf16, eps, relu, mode, save_mean,
       save_invstd, running_mean, running_var, momentum, Segs{});
@@ -767,7 +769,7 @@ TONY_API int tony_bn_bwd_reduce(const void* x, int64_t ldx, const void* dy, int6
   int64_t rpb;
   int grid;
   plan_rows(M, C, 8, red_wgs(), &rpb, &grid, true);  // few WGs: C atomics per WG contend per channel
-  bn_bwd_reduce_kernel<false><<<grid, kThreads, bn_lds_bred(C), stream>>>(
+  bn_bwd_reduce_kernel<false, uint16_t><<<grid, kThreads, bn_lds_bred(C), stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, nullptr, 0, M, C, rpb, mean,
       invstd, gamma, beta, param_bf16, relu, dsum, dsumx, sstride, Segs{});
   TONY_LAUNCH_CHECK();
@@ -782,7 +784,7 @@ TONY_API int tony_bn_bwd_apply(const void* x, int64_t ldx, const void* dy, int64
   int64_t rpb;
   int grid;
   plan_rows(M, C, 4, 8192, &rpb, &grid);
-  bn_bwd_apply_kernel<false><<<grid, kThreads, bn_lds_table(C, 5), stream>>>(
+  bn_bwd_apply_kernel<false, uint16_t><<<grid, kThreads, bn_lds_table(C, 5), stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, nullptr, 0, nullptr, 0,
       static_cast<uint16_t*>(dx), lddx, M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsum, dsumx, sstride,
       dgamma, dbeta, accumulate, Segs{});
@@ -808,7 +810,7 @@ bool make_segs(Segs& sg, int C, int n, int e0, int e1, int e2, int e3, void* p0,
         l[s] < e[s] - prev)
       return false;
     sg.end[s] = e[s];
-    sg.p[s] = static_cast<uint16_t*>(p[s]);
+    sg.p[s] = p[s];
     sg.ld[s] = l[s];
     prev = e[s];
   }
@@ -828,8 +830,8 @@ TONY_API int tony_bn_apply_segs(const void* x, int64_t M, int C, int64_t ldx, in
   int64_t rpb;
   int grid;
   plan_rows(M, C, 4, 8192, &rpb, &grid);
-  bn_fwd_apply_kernel<false><<<grid, kThreads, bn_lds_table(C, 2), stream>>>(
-      static_cast<const uint16_t*>(x), M, C, ldx, rpb, nullptr, 0, sg.p[0], sg.ld[0], sum, sumsq, sstride, gamma, beta,
+  bn_fwd_apply_kernel<false, uint16_t><<<grid, kThreads, bn_lds_table(C, 2), stream>>>(
+      static_cast<const uint16_t*>(x), M, C, ldx, rpb, nullptr, 0, static_cast<uint16_t*>(sg.p[0]), sg.ld[0], sum, sumsq, sstride, gamma, beta,
       param_bf16, eps, relu, mode, save_mean, save_invstd, running_mean, running_var, momentum, sg);
   TONY_LAUNCH_CHECK();
   return 0;
@@ -846,8 +848,8 @@ TONY_API int tony_bn_bwd_reduce_segs(const void* x, int64_t ldx, int n, int e0, 
   int64_t rpb;
   int grid;
   plan_rows(M, C, 8, red_wgs(), &rpb, &grid, true);
-  bn_bwd_reduce_kernel<false><<<grid, kThreads, bn_lds_bred(C), stream>>>(
-      static_cast<const uint16_t*>(x), ldx, sg.p[0], sg.ld[0], nullptr, 0, M, C, rpb, mean, invstd, gamma, beta,
+  bn_bwd_reduce_kernel<false, uint16_t><<<grid, kThreads, bn_lds_bred(C), stream>>>(
+      static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(sg.p[0]), sg.ld[0], nullptr, 0, M, C, rpb, mean, invstd, gamma, beta,
       param_bf16, relu, dsum, dsumx, sstride, sg);
   TONY_LAUNCH_CHECK();
   return 0;
@@ -866,10 +868,69 @@ TONY_API int tony_bn_bwd_apply_segs(const void* x, int64_t ldx, int n, int e0, i
   int64_t rpb;
   int grid;
   plan_rows(M, C, 4, 8192, &rpb, &grid);
-  bn_bwd_apply_kernel<false><<<grid, kThreads, bn_lds_table(C, 5), stream>>>(
-      static_cast<const uint16_t*>(x), ldx, sg.p[0], sg.ld[0], nullptr, 0, nullptr, 0, static_cast<uint16_t*>(dx),
+  bn_bwd_apply_kernel<false, uint16_t><<<grid, kThreads, bn_lds_table(C, 5), stream>>>(
+      static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(sg.p[0]), sg.ld[0], nullptr, 0, nullptr, 0, static_cast<uint16_t*>(dx),
       lddx, M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsum, dsumx, sstride, dgamma, dbeta, accumulate,
       sg);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---- fp32 forms (the x3 fp32 step, ops/x3.py): same kernels on float rows, same arguments -------
+TONY_API int tony_bn_stats_f32(const void* x, int64_t M, int C, int64_t ldx, float* sum, float* sumsq,
+                               int64_t sstride, hipStream_t stream) {
+  if (bad_c(C) || (ldx % 4) || sstride < 0) return -1;
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 8, 512, &rpb, &grid);
+  bn_fwd_stats_kernel<float><<<grid, kThreads, bn_lds_reduce(C), stream>>>(static_cast<const float*>(x), M, C, ldx,
+                                                                           rpb, sum, sumsq, sstride);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+TONY_API int tony_bn_apply_f32(const void* x, int64_t M, int C, int64_t ldx, void* y, int64_t ldy, const float* sum,
+                               const float* sumsq, int64_t sstride, const void* gamma, const void* beta, int param_bf16,
+                               float eps, int relu, int mode, float* save_mean, float* save_invstd,
+                               float* running_mean, float* running_var, float momentum, hipStream_t stream) {
+  if (bad_c(C) || (ldx % 4) || (ldy % 4) || sstride < 0) return -1;
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 4, 8192, &rpb, &grid);
+  bn_fwd_apply_kernel<false, float><<<grid, kThreads, bn_lds_table(C, 2), stream>>>(
+      static_cast<const float*>(x), M, C, ldx, rpb, nullptr, 0, static_cast<float*>(y), ldy, sum, sumsq, sstride,
+      gamma, beta, param_bf16, eps, relu, mode, save_mean, save_invstd, running_mean, running_var, momentum, Segs{});
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+TONY_API int tony_bn_bwd_reduce_f32(const void* x, int64_t ldx, const void* dy, int64_t lddy, int64_t M, int C,
+                                    const float* mean, const float* invstd, const void* gamma, const void* beta,
+                                    int param_bf16, int relu, float* dsum, float* dsumx, int64_t sstride,
+                                    hipStream_t stream) {
+  if (bad_c(C) || (ldx % 4) || (lddy % 4) || sstride < 0) return -1;
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 8, red_wgs(), &rpb, &grid, true);
+  bn_bwd_reduce_kernel<false, float><<<grid, kThreads, bn_lds_bred(C), stream>>>(
+      static_cast<const float*>(x), ldx, static_cast<const float*>(dy), lddy, nullptr, 0, M, C, rpb, mean, invstd,
+      gamma, beta, param_bf16, relu, dsum, dsumx, sstride, Segs{});
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+TONY_API int tony_bn_bwd_apply_f32(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx, int64_t lddx,
+                                   int64_t M, int C, const float* mean, const float* invstd, const void* gamma,
+                                   const void* beta, int param_bf16, int relu, const float* dsum, const float* dsumx,
+                                   int64_t sstride, void* dgamma, void* dbeta, int accumulate, hipStream_t stream) {
+  if (bad_c(C) || (ldx % 4) || (lddy % 4) || (lddx % 4) || sstride < 0) return -1;
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 4, 8192, &rpb, &grid);
+  bn_bwd_apply_kernel<false, float><<<grid, kThreads, bn_lds_table(C, 5), stream>>>(
+      static_cast<const float*>(x), ldx, static_cast<const float*>(dy), lddy, nullptr, 0, nullptr, 0,
+      static_cast<float*>(dx), lddx, M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsum, dsumx, sstride,
+      dgamma, dbeta, accumulate, Segs{});
   TONY_LAUNCH_CHECK();
   return 0;
 }
@@ -937,12 +998,12 @@ TONY_API int tony_bn_bwd_res(const void* x, int64_t ldx, const void* dy, int64_t
   int64_t rpb;
   int grid;
   plan_rows(M, C, 8, 512, &rpb, &grid);
-  bn_bwd_reduce_kernel<true><<<grid, kThreads, bn_lds_bred(C), stream>>>(
+  bn_bwd_reduce_kernel<true, uint16_t><<<grid, kThreads, bn_lds_bred(C), stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, static_cast<const uint16_t*>(y),
       ldy, M, C, rpb, mean, invstd, gamma, beta, param_bf16, 1, dsums_ws, dsums_ws + C, ss, Segs{});
   TONY_LAUNCH_CHECK();
   plan_rows(M, C, 4, 8192, &rpb, &grid);
-  bn_bwd_apply_kernel<true><<<grid, kThreads, bn_lds_table(C, 5), stream>>>(
+  bn_bwd_apply_kernel<true, uint16_t><<<grid, kThreads, bn_lds_table(C, 5), stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, static_cast<const uint16_t*>(y),
       ldy, static_cast<uint16_t*>(dres), lddr, static_cast<uint16_t*>(dx), lddx, M, C, rpb, mean, invstd, gamma, beta,
       param_bf16, 1, dsums_ws, dsums_ws + C, ss, dgamma, dbeta, accumulate, Segs{});

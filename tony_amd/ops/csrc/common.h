@@ -82,6 +82,36 @@ __device__ __forceinline__ void store8(uint16_t* p, const bf16x8& v) {
   *reinterpret_cast<uint4*>(p) = v.raw;
 }
 
+// 8 consecutive elements of a bf16 (uint16_t) or fp32 tensor as 8 floats: the element-type
+// abstraction of the kernels that serve both the bf16 step and the fp32 x3 step (ops/x3.py)
+template <class T>
+struct V8;
+template <>
+struct V8<uint16_t> {
+  bf16x8 b;
+  __device__ __forceinline__ static V8 load(const uint16_t* p) { return V8{load8(p)}; }
+  __device__ __forceinline__ void store(uint16_t* p) const { store8(p, b); }
+  __device__ __forceinline__ void to_float(float* f) const { b.to_float(f); }
+  __device__ __forceinline__ static V8 from_float(const float* f) { return V8{bf16x8::from_float(f)}; }
+};
+template <>
+struct V8<float> {
+  float4 lo, hi;
+  __device__ __forceinline__ static V8 load(const float* p) {
+    return V8{*reinterpret_cast<const float4*>(p), *reinterpret_cast<const float4*>(p + 4)};
+  }
+  __device__ __forceinline__ void store(float* p) const {
+    *reinterpret_cast<float4*>(p) = lo;
+    *reinterpret_cast<float4*>(p + 4) = hi;
+  }
+  __device__ __forceinline__ void to_float(float* f) const {
+    f[0] = lo.x, f[1] = lo.y, f[2] = lo.z, f[3] = lo.w, f[4] = hi.x, f[5] = hi.y, f[6] = hi.z, f[7] = hi.w;
+  }
+  __device__ __forceinline__ static V8 from_float(const float* f) {
+    return V8{make_float4(f[0], f[1], f[2], f[3]), make_float4(f[4], f[5], f[6], f[7])};
+  }
+};
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);

@@ -275,7 +275,7 @@ __global__ __launch_bounds__(kThreads) void conv_nt_kernel(Gather g, const uint1
   // inference BN (H5), bit2: ReLU after it
   nt_epilogue<BM, BN, TM, TN>(acc, smem, C, ldc, M, N, m0, n0,
                                (epi & 1) ? stats + shard_off(tm, sstride) : nullptr,
-                               (epi & 2) ? stats : nullptr, (epi & 4) != 0, PH ? ph.rows : RowMap{});
+                               (epi & 2) ? stats : nullptr, (epi & 4) != 0, PH ? ph.rows : RowMap{}, (epi & 8) != 0);
   if (ph.bnr.z != nullptr) {  // uniform: the C tile is still in LDS, the fold area lies behind it
     constexpr int CS_ELEMS = (BM * (BN + 8) + 7) / 8 * 8;
     static_assert(CS_ELEMS * 2 + 16 * kThreads * 4 <= 2 * (BM + BN) * BK * 2, "BN-reduce fold area fits");
@@ -756,11 +756,13 @@ int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int6
            int64_t sstride, hipStream_t stream, const Phase& bph = Phase{}) {
   // flags bit0: statistics accumulated into stats (the caller zeroes it, ops/arena.py);
   // bit1: stats = [scale | shift] of the folded inference BN, bit2: ReLU after it (H5)
-  const int epi = flags & 7;
+  // bit3: fp32 output (the x3 path, ops/x3.py): only the variants whose epilogue is nt_epilogue
+  const int epi = flags & 15;
   if ((epi & 1) && (epi & 2)) return -1;
   if ((epi & 3) && stats == nullptr) return -1;
   float* st = stats;
   const int v = (flags >> 8) & 0xff;
+  if ((epi & 8) && (v == kHaloVariant || v == kDirectVariant)) return -3;
   if (v == kHaloVariant) return bph.bnr.z != nullptr ? -3 : run_halo(g, B, C, ldc, N, epi, st, sstride, stream);
   if (v == kDirectVariant) return run_direct(g, B, C, ldc, N, epi, st, sstride, stream, bph.bnr);
   if (v >= kGldsFirst && v < kGldsFirst + kNumGlds)
@@ -781,18 +783,18 @@ int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int6
 
 // One residue class of a strided dgrad with tile variant v (flags bits 8..15 of tony_conv_dgrad_strided).
 int run_nt_phase(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, int v, const Phase& ph,
-                 hipStream_t stream) {
+                 hipStream_t stream, int epi = 0) {
   if (v == kHaloVariant || v == kDirectVariant || v >= kNumNtVariants) return -1;
   if (v == 0) {
     const int64_t bn = pick_bn(N, 192);
-    return bn <= 64 ? launch_nt_bm<256, true>(g, B, C, ldc, M, N, nullptr, 0, 0, bn, stream, ph)
-                    : launch_nt_bm<128, true>(g, B, C, ldc, M, N, nullptr, 0, 0, bn, stream, ph);
+    return bn <= 64 ? launch_nt_bm<256, true>(g, B, C, ldc, M, N, nullptr, 0, epi, bn, stream, ph)
+                    : launch_nt_bm<128, true>(g, B, C, ldc, M, N, nullptr, 0, epi, bn, stream, ph);
   }
   const int64_t bn = pick_bn(N, kNtVariants[v].cap);
   switch (kNtVariants[v].bm) {
-    case 64: return launch_nt_bm<64, true>(g, B, C, ldc, M, N, nullptr, 0, 0, bn, stream, ph);
-    case 128: return launch_nt_bm<128, true>(g, B, C, ldc, M, N, nullptr, 0, 0, bn, stream, ph);
-    default: return launch_nt_bm<256, true>(g, B, C, ldc, M, N, nullptr, 0, 0, bn, stream, ph);
+    case 64: return launch_nt_bm<64, true>(g, B, C, ldc, M, N, nullptr, 0, epi, bn, stream, ph);
+    case 128: return launch_nt_bm<128, true>(g, B, C, ldc, M, N, nullptr, 0, epi, bn, stream, ph);
+    default: return launch_nt_bm<256, true>(g, B, C, ldc, M, N, nullptr, 0, epi, bn, stream, ph);
   }
 }
 
@@ -1466,9 +1468,10 @@ TONY_API int tony_conv_dgrad(const void* dy, int N, int OH, int OW, int Co, int6
       bph.bnr = *bnr;
     }
   }
-  const int rc = run_nt(g, wt, dx, lddx, M, C, flags & 0xff00, nullptr, 0, stream, bph);
+  const int fl = flags & 0xff08;  // variant + fp32 output (bit3)
+  const int rc = run_nt(g, wt, dx, lddx, M, C, fl, nullptr, 0, stream, bph);
   if (rc == -3 && bph.bnr.z != nullptr)  // the chosen variant has no fused reduction: plain dgrad
-    return run_nt(g, wt, dx, lddx, M, C, flags & 0xff00, nullptr, 0, stream);
+    return run_nt(g, wt, dx, lddx, M, C, fl, nullptr, 0, stream);
   if (rc == 0 && bph.bnr.z != nullptr) bnr->done = 1;
   return rc;
 }
@@ -1519,7 +1522,7 @@ TONY_API int tony_conv_dgrad_strided(const void* dy, int N, int OH, int OW, int 
       phz.rows.y0 = py;
       phz.rows.x0 = px;
       phz.bnr = br;
-      const int rc = run_nt_phase(g, wt, dx, lddx, M, C, v, phz, stream);
+      const int rc = run_nt_phase(g, wt, dx, lddx, M, C, v, phz, stream, flags & 8);
       if (rc != 0) return rc;
     }
   }

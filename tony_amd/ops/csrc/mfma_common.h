@@ -173,11 +173,13 @@ struct RowMap {
 // acc layout of 16x16 MFMA: col = lane&15, row = (lane>>4)*4 + r.
 // With ``aff`` ([scale N | shift N] fp32, the folded inference BatchNorm) the stored value is
 // act(acc * scale[col] + shift[col]) (act = ReLU when ``relu``): conv + BN + ReLU in one pass (H5).
+// ``f32out`` (the fp32 "x3" path, ops/x3.py): C is an fp32 [M, ldc] matrix and the accumulators are
+// stored as they are -- 4 rows x 16 columns (64 contiguous bytes per row) per store instruction.
 template <int BM, int BN, int TM, int TN, int LDS_ELEMS = 2 * (BM + BN) * BK>
 __device__ __forceinline__ void nt_epilogue(f32x4 (&acc)[TM][TN], uint16_t* smem, uint16_t* __restrict__ C,
                                             int64_t ldc, int M, int N, int m0, int n0, float* __restrict__ stats,
                                             const float* __restrict__ aff = nullptr, bool relu = false,
-                                            const RowMap rm = RowMap{}) {
+                                            const RowMap rm = RowMap{}, bool f32out = false) {
   constexpr int WM = BM / 2, WN = BN / 2;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -204,6 +206,29 @@ __device__ __forceinline__ void nt_epilogue(f32x4 (&acc)[TM][TN], uint16_t* smem
         atomicAdd(stats + N + col, q);
       }
     }
+  }
+  if (f32out) {
+    float* Cf = reinterpret_cast<float*>(C);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * WN + j * 16 + (lane & 15);
+      float sc = 1.f, sh = 0.f;
+      if (aff != nullptr) {
+        sc = aff[min(col, N - 1)];
+        sh = aff[N + min(col, N - 1)];
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+          if (row >= M || col >= N) continue;
+          float v = acc[i][j][r];
+          if (aff != nullptr) v = fmaf(v, sc, sh);
+          Cf[rm.pixel(row) * ldc + col] = relu ? relu_f(v) : v;
+        }
+    }
+    return;
   }
   constexpr int LDC = BN + 8;
   static_assert(BM * LDC <= LDS_ELEMS, "C staging tile must fit in the LDS buffers");

@@ -36,7 +36,7 @@ __global__ void plan_marker_kernel(int) {}
 
 constexpr int kMaxStreams = 8;
 
-enum OpKind : int { kKernel = 0, kMemset = 1, kMemcpy = 2, kWait = 3, kRecord = 4, kMarker = 5 };
+enum OpKind : int { kKernel = 0, kMemset = 1, kMemcpy = 2, kWait = 3, kRecord = 4, kMarker = 5, kGraph = 6 };
 
 struct Op {
   int kind;
@@ -47,6 +47,7 @@ struct Op {
   hipFunction_t fn;  // the device function (resolved once from the captured host stub)
   hipMemsetParams ms;
   hipMemcpy3DParms mc;
+  hipGraphExec_t ex;  // kGraph: a one-node executable graph (nodes without a direct re-issue call)
 };
 
 struct Plan {
@@ -57,7 +58,7 @@ struct Plan {
   int used[kMaxStreams] = {};
   std::vector<int> tails;            // per stream: event recorded after its last op (joined at the end)
   std::vector<int> seg_end;          // op index one past each marker (segment k = [seg_end[k-1], seg_end[k]))
-  int stats[10] = {};
+  int stats[11] = {};
 };
 
 int new_event(Plan& p) {
@@ -69,7 +70,29 @@ int new_event(Plan& p) {
 
 void destroy(Plan* p) {
   for (hipEvent_t e : p->events) (void)hipEventDestroy(e);
+  for (Op& o : p->ops)
+    if (o.kind == kGraph && o.ex != nullptr) (void)hipGraphExecDestroy(o.ex);
   delete p;
+}
+
+// A node without a direct re-issue call (a copy captured from hipMemcpyAsync is a 1D node whose
+// parameters no getter returns) becomes a one-node executable graph: the captured graph cloned, every
+// other node removed, instantiated.  Launched with hipGraphLaunch on the node's stream.
+hipGraphExec_t single_node_exec(hipGraph_t g, hipGraphNode_t node) {
+  hipGraph_t clone = nullptr;
+  if (hipGraphClone(&clone, g) != hipSuccess) return nullptr;
+  hipGraphNode_t target = nullptr;
+  hipGraphExec_t ex = nullptr;
+  size_t cn = 0;
+  if (hipGraphNodeFindInClone(&target, node, clone) == hipSuccess && hipGraphGetNodes(clone, nullptr, &cn) == hipSuccess) {
+    std::vector<hipGraphNode_t> all(cn);
+    bool ok = cn == 0 || hipGraphGetNodes(clone, all.data(), &cn) == hipSuccess;
+    for (size_t i = 0; ok && i < cn; ++i)
+      if (all[i] != target) ok = hipGraphDestroyNode(all[i]) == hipSuccess;
+    if (ok && hipGraphInstantiate(&ex, clone, nullptr, nullptr, 0) != hipSuccess) ex = nullptr;
+  }
+  (void)hipGraphDestroy(clone);
+  return ex;
 }
 
 hipError_t issue(const Plan& p, const Op& o, hipStream_t side) {
@@ -94,6 +117,8 @@ hipError_t issue(const Plan& p, const Op& o, hipStream_t side) {
       return hipStreamWaitEvent(s, p.events[o.event], 0);
     case kRecord:
       return hipEventRecord(p.events[o.event], s);
+    case kGraph:
+      return hipGraphLaunch(o.ex, s);
     case kMarker: {
       hipError_t e = hipEventRecord(p.events[o.event], s);
       if (e == hipSuccess && side != nullptr) e = hipStreamWaitEvent(side, p.events[o.event], 0);
@@ -116,7 +141,7 @@ TONY_API int tony_plan_mark(int id, hipStream_t stream) {
 // Build a replay plan from a captured graph.  streams[0] must be the stream the replay is issued on
 // (the capture's origin stream); streams[1..n) are side streams the plan may use (n <= 8).
 // stats (10 ints): kernels, memsets, memcpys, waits, records, streams used, markers, graph nodes,
-// placements that had to take a false dependency, empty nodes folded.
+// placements that had to take a false dependency, empty nodes folded, nodes issued as one-node graphs.
 // Returns 0 and the handle in *out; negative: unsupported graph (the caller keeps its own path).
 TONY_API int tony_plan_build(void* graph, const uint64_t* streams, int nstreams, uint64_t* out, int* stats) {
   if (graph == nullptr || streams == nullptr || out == nullptr || nstreams < 1 || nstreams > kMaxStreams) return -1;
@@ -145,13 +170,12 @@ TONY_API int tony_plan_build(void* graph, const uint64_t* streams, int nstreams,
       deps[i].push_back(it->second);
     }
     switch (type[i]) {
-      case hipGraphNodeTypeKernel:
-      case hipGraphNodeTypeMemset:
-      case hipGraphNodeTypeMemcpy:
-      case hipGraphNodeTypeEmpty:
-        break;
+      case hipGraphNodeTypeGraph:
+      case hipGraphNodeTypeMemAlloc:
+      case hipGraphNodeTypeMemFree:
+        return -3 - 100 * static_cast<int>(type[i]);  // a child graph / graph-owned memory: not replayed here
       default:
-        return -3 - 100 * static_cast<int>(type[i]);  // host / child graph / external events...
+        break;
     }
   }
   // Kahn, lowest node index first (= capture order)
@@ -212,7 +236,7 @@ TONY_API int tony_plan_build(void* graph, const uint64_t* streams, int nstreams,
   int known[kMaxStreams][kMaxStreams];
   for (auto& row : known)
     for (int& x : row) x = 0;
-  int tick = 0, forced = 0, empties = 0;
+  int tick = 0, forced = 0, empties = 0, graphs = 0;
   std::vector<int> at_pos[kMaxStreams];  // node at each position of each stream
   // which nodes need an event recorded after them (a dependent lands on another stream): decided
   // as dependents are placed, so records are appended lazily -- an op list position per node
@@ -317,19 +341,29 @@ TONY_API int tony_plan_build(void* graph, const uint64_t* streams, int nstreams,
           return fail(-7);
       }
     } else if (type[v] == hipGraphNodeTypeMemset) {
+      // (a memset node's parameters are always readable)
       o.kind = kMemset;
       if (hipGraphMemsetNodeGetParams(nodes[v], &o.ms) != hipSuccess) return fail(-2);
     } else {
-      // a copy captured from hipMemcpyAsync is a 1D node whose 3D parameter block is not filled in
-      // (no 1D getter exists): only a copy with a complete 3D description is re-issued
-      o.kind = kMemcpy;
-      if (hipGraphMemcpyNodeGetParams(nodes[v], &o.mc) != hipSuccess) return fail(-9);
-      const hipMemcpy3DParms& m = o.mc;
-      const bool src_ok = m.srcArray != nullptr || m.srcPtr.ptr != nullptr;
-      const bool dst_ok = m.dstArray != nullptr || m.dstPtr.ptr != nullptr;
-      if (!src_ok || !dst_ok || m.extent.width == 0 || m.extent.height == 0 || m.extent.depth == 0 ||
-          static_cast<int>(m.kind) < 0 || static_cast<int>(m.kind) > 4)
-        return fail(-9);
+      // copies: a fully described 3D copy is re-issued directly, anything else (1D copies captured
+      // from hipMemcpyAsync carry no readable parameters) as a one-node executable graph
+      bool direct = false;
+      if (type[v] == hipGraphNodeTypeMemcpy && hipGraphMemcpyNodeGetParams(nodes[v], &o.mc) == hipSuccess) {
+        const hipMemcpy3DParms& m = o.mc;
+        const bool src_ok = m.srcArray != nullptr || m.srcPtr.ptr != nullptr;
+        const bool dst_ok = m.dstArray != nullptr || m.dstPtr.ptr != nullptr;
+        direct = src_ok && dst_ok && m.extent.width > 0 && m.extent.height > 0 && m.extent.depth > 0 &&
+                 static_cast<int>(m.kind) >= 0 && static_cast<int>(m.kind) <= 4;
+      }
+      (void)hipGetLastError();
+      if (direct) {
+        o.kind = kMemcpy;
+      } else {
+        o.kind = kGraph;
+        o.ex = single_node_exec(g, nodes[v]);
+        if (o.ex == nullptr) return fail(-9);
+        ++graphs;
+      }
     }
     ops.push_back(o);
     op_after[v] = static_cast<int>(ops.size()) - 1;
@@ -387,6 +421,7 @@ TONY_API int tony_plan_build(void* graph, const uint64_t* streams, int nstreams,
   st[7] = static_cast<int>(n);
   st[8] = forced;
   st[9] = empties;
+  st[10] = graphs;
   if (stats != nullptr) std::memcpy(stats, st, sizeof(p->stats));
   *out = reinterpret_cast<uint64_t>(p);
   return 0;

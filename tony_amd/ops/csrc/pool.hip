@@ -21,7 +21,8 @@ namespace {
 
 constexpr int kThreads = 256;
 
-__global__ __launch_bounds__(kThreads) void box3_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+template <class T>
+__global__ __launch_bounds__(kThreads) void box3_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                         int N, int H, int W, int C, int64_t ldx, int64_t ldy) {
   // 32-bit index math (the host checks the element count fits): 64-bit div/mod are long
   // instruction sequences and made these memory-bound kernels ALU-bound
@@ -45,14 +46,14 @@ __global__ __launch_bounds__(kThreads) void box3_kernel(const uint16_t* __restri
         const int ww = w + dw;
         if (ww < 0 || ww >= W) continue;
         float f[8];
-        load8(x + ((n * H + hh) * W + ww) * ldx + cg * 8).to_float(f);
+        V8<T>::load(x + ((n * H + hh) * W + ww) * ldx + cg * 8).to_float(f);
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] += f[j];
       }
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] *= (1.f / 9.f);
-    store8(y + static_cast<int64_t>(site) * ldy + cg * 8, bf16x8::from_float(acc));
+    V8<T>::from_float(acc).store(y + static_cast<int64_t>(site) * ldy + cg * 8);
   }
 }
 
@@ -60,9 +61,9 @@ __global__ __launch_bounds__(kThreads) void box3_kernel(const uint16_t* __restri
 // each in turn); 0: any K
 // P: zero-padding of the window (torch's max_pool2d padding: padded taps never win; ResNet's stem pool
 // is 3x3/2 p1).  With P > 0 each tap is bounds-checked and an out-of-image tap is skipped.
-template <int KT>
-__global__ __launch_bounds__(kThreads) void maxpool_fwd_kernel(const uint16_t* __restrict__ x,
-                                                               uint16_t* __restrict__ y, uint8_t* __restrict__ arg,
+template <int KT, class T = uint16_t>
+__global__ __launch_bounds__(kThreads) void maxpool_fwd_kernel(const T* __restrict__ x,
+                                                               T* __restrict__ y, uint8_t* __restrict__ arg,
                                                                int N, int H, int W, int C, int OH, int OW, int K,
                                                                int S, int P, int64_t ldx, int64_t ldy) {
   const uint32_t CG = C >> 3;
@@ -82,7 +83,7 @@ __global__ __launch_bounds__(kThreads) void maxpool_fwd_kernel(const uint16_t* _
       best[j] = -INFINITY;
       bi[j] = 0;
     }
-    auto take = [&](const bf16x8& raw, uint8_t idx) {
+    auto take = [&](const V8<T>& raw, uint8_t idx) {
       float f[8];
       raw.to_float(f);
 #pragma unroll
@@ -96,17 +97,17 @@ __global__ __launch_bounds__(kThreads) void maxpool_fwd_kernel(const uint16_t* _
     const int h0 = oh * S - P, w0 = ow * S - P;
     if constexpr (KT > 0) {
       if (P == 0) {
-        const uint16_t* base = x + ((n * H + h0) * W + w0) * ldx + cg * 8;
+        const T* base = x + ((n * H + h0) * W + w0) * ldx + cg * 8;
         const int64_t row = static_cast<int64_t>(W) * ldx;
-        bf16x8 raw[KT * KT];
+        V8<T> raw[KT * KT];
 #pragma unroll
         for (int kh = 0; kh < KT; ++kh)
 #pragma unroll
-          for (int kw = 0; kw < KT; ++kw) raw[kh * KT + kw] = load8(base + kh * row + kw * ldx);
+          for (int kw = 0; kw < KT; ++kw) raw[kh * KT + kw] = V8<T>::load(base + kh * row + kw * ldx);
 #pragma unroll
         for (int k = 0; k < KT * KT; ++k) take(raw[k], static_cast<uint8_t>(k));
         } else {  // padded: the in-image taps' loads all issued up front, then consumed
-        bf16x8 raw[KT * KT];
+        V8<T> raw[KT * KT];
         bool ok[KT * KT];
 #pragma unroll
         for (int kh = 0; kh < KT; ++kh)
@@ -115,7 +116,7 @@ __global__ __launch_bounds__(kThreads) void maxpool_fwd_kernel(const uint16_t* _
             const int hh = h0 + kh, ww = w0 + kw;
             ok[kh * KT + kw] = static_cast<unsigned>(hh) < static_cast<unsigned>(H) &&
                                static_cast<unsigned>(ww) < static_cast<unsigned>(W);
-            if (ok[kh * KT + kw]) raw[kh * KT + kw] = load8(x + ((n * H + hh) * W + ww) * ldx + cg * 8);
+            if (ok[kh * KT + kw]) raw[kh * KT + kw] = V8<T>::load(x + ((n * H + hh) * W + ww) * ldx + cg * 8);
           }
 #pragma unroll
         for (int k = 0; k < KT * KT; ++k)
@@ -128,11 +129,11 @@ __global__ __launch_bounds__(kThreads) void maxpool_fwd_kernel(const uint16_t* _
         for (int kw = 0; kw < K; ++kw) {
           const int ww = w0 + kw;
           if (static_cast<unsigned>(ww) >= static_cast<unsigned>(W)) continue;
-          take(load8(x + ((n * H + hh) * W + ww) * ldx + cg * 8), static_cast<uint8_t>(kh * K + kw));
+          take(V8<T>::load(x + ((n * H + hh) * W + ww) * ldx + cg * 8), static_cast<uint8_t>(kh * K + kw));
         }
       }
     }
-    store8(y + static_cast<int64_t>(site) * ldy + cg * 8, bf16x8::from_float(best));
+    V8<T>::from_float(best).store(y + static_cast<int64_t>(site) * ldy + cg * 8);
     uint2 packed;
     packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (static_cast<uint32_t>(bi[3]) << 24);
     packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (static_cast<uint32_t>(bi[7]) << 24);
@@ -140,9 +141,10 @@ __global__ __launch_bounds__(kThreads) void maxpool_fwd_kernel(const uint16_t* _
   }
 }
 
-__global__ __launch_bounds__(kThreads) void maxpool_bwd_kernel(const uint16_t* __restrict__ dy,
+template <class T>
+__global__ __launch_bounds__(kThreads) void maxpool_bwd_kernel(const T* __restrict__ dy,
                                                                const uint8_t* __restrict__ arg,
-                                                               uint16_t* __restrict__ dx, int N, int H, int W, int C,
+                                                               T* __restrict__ dx, int N, int H, int W, int C,
                                                                int OH, int OW, int K, int S, int P, int64_t lddy,
                                                                int64_t lddx) {
   const uint32_t CG = C >> 3;
@@ -168,7 +170,7 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd_kernel(const uint16_t* _
         const int64_t osite = (n * OH + oh) * OW + ow;
         const uint2 packed = *reinterpret_cast<const uint2*>(arg + osite * C + cg * 8);
         float g[8];
-        load8(dy + osite * lddy + cg * 8).to_float(g);
+        V8<T>::load(dy + osite * lddy + cg * 8).to_float(g);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const uint32_t word = j < 4 ? packed.x : packed.y;
@@ -177,7 +179,7 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd_kernel(const uint16_t* _
         }
       }
     }
-    store8(dx + static_cast<int64_t>(site) * lddx + cg * 8, bf16x8::from_float(acc));
+    V8<T>::from_float(acc).store(dx + static_cast<int64_t>(site) * lddx + cg * 8);
   }
 }
 
@@ -272,8 +274,9 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd_bnred_kernel(
 }
 
 // avg KxK, stride S, no padding (Inception aux head 5x5/s3; K = H = W is the global average pool).
-__global__ __launch_bounds__(kThreads) void avgpool_fwd_kernel(const uint16_t* __restrict__ x,
-                                                               uint16_t* __restrict__ y, int N, int H, int W, int C,
+template <class T>
+__global__ __launch_bounds__(kThreads) void avgpool_fwd_kernel(const T* __restrict__ x,
+                                                               T* __restrict__ y, int N, int H, int W, int C,
                                                                int OH, int OW, int K, int S, int64_t ldx,
                                                                int64_t ldy) {
   const uint32_t CG = C >> 3;
@@ -292,20 +295,21 @@ __global__ __launch_bounds__(kThreads) void avgpool_fwd_kernel(const uint16_t* _
       const int64_t row = (n * H + oh * S + r) * W + ow * S;
       for (int s = 0; s < K; ++s) {
         float v[8];
-        load8(x + (row + s) * ldx + cg * 8).to_float(v);
+        V8<T>::load(x + (row + s) * ldx + cg * 8).to_float(v);
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] += v[j];
       }
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] *= inv;
-    store8(y + static_cast<int64_t>(site) * ldy + cg * 8, bf16x8::from_float(acc));
+    V8<T>::from_float(acc).store(y + static_cast<int64_t>(site) * ldy + cg * 8);
   }
 }
 
 // dx[h, w] = (1/K^2) * sum of dy over the <= ceil(K/S)^2 windows covering (h, w): a gather, no atomics
-__global__ __launch_bounds__(kThreads) void avgpool_bwd_kernel(const uint16_t* __restrict__ dy,
-                                                               uint16_t* __restrict__ dx, int N, int H, int W, int C,
+template <class T>
+__global__ __launch_bounds__(kThreads) void avgpool_bwd_kernel(const T* __restrict__ dy,
+                                                               T* __restrict__ dx, int N, int H, int W, int C,
                                                                int OH, int OW, int K, int S, int64_t lddy,
                                                                int64_t lddx) {
   const uint32_t CG = C >> 3;
@@ -327,13 +331,13 @@ __global__ __launch_bounds__(kThreads) void avgpool_bwd_kernel(const uint16_t* _
     for (int oh = oh_lo; oh <= oh_hi; ++oh)
       for (int ow = ow_lo; ow <= ow_hi; ++ow) {
         float g[8];
-        load8(dy + ((n * OH + oh) * OW + ow) * lddy + cg * 8).to_float(g);
+        V8<T>::load(dy + ((n * OH + oh) * OW + ow) * lddy + cg * 8).to_float(g);
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] += g[j];
       }
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] *= inv;
-    store8(dx + static_cast<int64_t>(site) * lddx + cg * 8, bf16x8::from_float(acc));
+    V8<T>::from_float(acc).store(dx + static_cast<int64_t>(site) * lddx + cg * 8);
   }
 }
 
@@ -349,7 +353,7 @@ int grid_for(int64_t work) {
 TONY_API int tony_avgpool3_s1p1(const void* x, void* y, int N, int H, int W, int C, int64_t ldx, int64_t ldy,
                                 hipStream_t stream) {
   if (C % 8 || ldx % 8 || ldy % 8 || static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
-  box3_kernel<<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+  box3_kernel<uint16_t><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, ldx, ldy);
   TONY_LAUNCH_CHECK();
   return 0;
@@ -364,7 +368,7 @@ TONY_API int tony_maxpool_fwd(const void* x, void* y, void* argmax, int N, int H
     return -1;
   if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
   const int OH = (H + 2 * P - K) / S + 1, OW = (W + 2 * P - K) / S + 1;
-  (K == 3 ? maxpool_fwd_kernel<3> : maxpool_fwd_kernel<0>)<<<grid_for(static_cast<int64_t>(N) * OH * OW * (C / 8)), kThreads, 0, stream>>>(
+  (K == 3 ? maxpool_fwd_kernel<3, uint16_t> : maxpool_fwd_kernel<0, uint16_t>)<<<grid_for(static_cast<int64_t>(N) * OH * OW * (C / 8)), kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), static_cast<uint8_t*>(argmax), N, H, W, C, OH, OW,
       K, S, P, ldx, ldy);
   TONY_LAUNCH_CHECK();
@@ -377,7 +381,7 @@ TONY_API int tony_maxpool_bwd(const void* dy, const void* argmax, void* dx, int 
     return -1;
   if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
   const int OH = (H + 2 * P - K) / S + 1, OW = (W + 2 * P - K) / S + 1;
-  maxpool_bwd_kernel<<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+  maxpool_bwd_kernel<uint16_t><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(dy), static_cast<const uint8_t*>(argmax), static_cast<uint16_t*>(dx), N, H, W, C,
       OH, OW, K, S, P, lddy, lddx);
   TONY_LAUNCH_CHECK();
@@ -412,7 +416,7 @@ TONY_API int tony_avgpool_fwd(const void* x, void* y, int N, int H, int W, int C
   if (C % 8 || ldx % 8 || ldy % 8 || K < 1 || S < 1 || H < K || W < K) return -1;
   if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
   const int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
-  avgpool_fwd_kernel<<<grid_for(static_cast<int64_t>(N) * OH * OW * (C / 8)), kThreads, 0, stream>>>(
+  avgpool_fwd_kernel<uint16_t><<<grid_for(static_cast<int64_t>(N) * OH * OW * (C / 8)), kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), N, H, W, C, OH, OW, K, S, ldx, ldy);
   TONY_LAUNCH_CHECK();
   return 0;
@@ -423,8 +427,67 @@ TONY_API int tony_avgpool_bwd(const void* dy, void* dx, int N, int H, int W, int
   if (C % 8 || lddy % 8 || lddx % 8 || K < 1 || S < 1 || H < K || W < K) return -1;
   if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
   const int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
-  avgpool_bwd_kernel<<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+  avgpool_bwd_kernel<uint16_t><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(dy), static_cast<uint16_t*>(dx), N, H, W, C, OH, OW, K, S, lddy, lddx);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---- fp32 forms (the x3 fp32 step, ops/x3.py): the same kernels on float rows ----------------------
+TONY_API int tony_avgpool3_s1p1_f32(const void* x, void* y, int N, int H, int W, int C, int64_t ldx, int64_t ldy,
+                                    hipStream_t stream) {
+  if (C % 8 || ldx % 4 || ldy % 4 || static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
+  box3_kernel<float><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+      static_cast<const float*>(x), static_cast<float*>(y), N, H, W, C, ldx, ldy);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+TONY_API int tony_maxpool_fwd_f32(const void* x, void* y, void* argmax, int N, int H, int W, int C, int K, int S,
+                                  int P, int64_t ldx, int64_t ldy, hipStream_t stream) {
+  if (C % 8 || ldx % 4 || ldy % 4 || K * K > 255 || P < 0 || 2 * P >= K + 1 || H + 2 * P < K || W + 2 * P < K ||
+      S < 1)
+    return -1;
+  if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
+  const int OH = (H + 2 * P - K) / S + 1, OW = (W + 2 * P - K) / S + 1;
+  (K == 3 ? maxpool_fwd_kernel<3, float> : maxpool_fwd_kernel<0, float>)<<<grid_for(static_cast<int64_t>(N) * OH * OW * (C / 8)), kThreads, 0, stream>>>(
+      static_cast<const float*>(x), static_cast<float*>(y), static_cast<uint8_t*>(argmax), N, H, W, C, OH, OW, K, S,
+      P, ldx, ldy);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+TONY_API int tony_maxpool_bwd_f32(const void* dy, const void* argmax, void* dx, int N, int H, int W, int C, int K,
+                                  int S, int P, int64_t lddy, int64_t lddx, hipStream_t stream) {
+  if (C % 8 || lddy % 4 || lddx % 4 || P < 0 || 2 * P >= K + 1 || H + 2 * P < K || W + 2 * P < K || S < 1)
+    return -1;
+  if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
+  const int OH = (H + 2 * P - K) / S + 1, OW = (W + 2 * P - K) / S + 1;
+  maxpool_bwd_kernel<float><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+      static_cast<const float*>(dy), static_cast<const uint8_t*>(argmax), static_cast<float*>(dx), N, H, W, C, OH, OW,
+      K, S, P, lddy, lddx);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+TONY_API int tony_avgpool_fwd_f32(const void* x, void* y, int N, int H, int W, int C, int K, int S, int64_t ldx,
+                                  int64_t ldy, hipStream_t stream) {
+  if (C % 8 || ldx % 4 || ldy % 4 || K < 1 || S < 1 || H < K || W < K) return -1;
+  if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
+  const int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
+  avgpool_fwd_kernel<float><<<grid_for(static_cast<int64_t>(N) * OH * OW * (C / 8)), kThreads, 0, stream>>>(
+      static_cast<const float*>(x), static_cast<float*>(y), N, H, W, C, OH, OW, K, S, ldx, ldy);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+TONY_API int tony_avgpool_bwd_f32(const void* dy, void* dx, int N, int H, int W, int C, int K, int S, int64_t lddy,
+                                  int64_t lddx, hipStream_t stream) {
+  if (C % 8 || lddy % 4 || lddx % 4 || K < 1 || S < 1 || H < K || W < K) return -1;
+  if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
+  const int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
+  avgpool_bwd_kernel<float><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+      static_cast<const float*>(dy), static_cast<float*>(dx), N, H, W, C, OH, OW, K, S, lddy, lddx);
   TONY_LAUNCH_CHECK();
   return 0;
 }

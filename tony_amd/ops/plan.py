@@ -28,7 +28,7 @@ import torch
 from . import _lib
 
 STAT_KEYS = ("kernels", "memsets", "memcpys", "waits", "records", "streams_used", "markers", "graph_nodes",
-             "false_deps", "empty_nodes")
+             "false_deps", "empty_nodes", "node_graphs")
 
 
 class PlanUnsupported(RuntimeError):
@@ -66,7 +66,7 @@ class StepPlan:
 
     def ops(self) -> List[tuple]:
         """(kind, stream, event-or-marker) per issued op: kinds 0 kernel, 1 memset, 2 memcpy, 3 wait,
-        4 record, 5 marker (tests / tracing)."""
+        4 record, 5 marker, 6 one-node graph (tests / tracing)."""
         L = _lib.lib()
         n = L.tony_plan_ops(self.handle, None, 0)
         buf = (ctypes.c_int * (3 * max(n, 1)))()

@@ -11,10 +11,19 @@ def _nhwc_empty(n, c, h, w, like):
     return torch.empty((n, c, h, w), dtype=like.dtype, device=like.device, memory_format=torch.channels_last)
 
 
+def _fn(name: str, t: torch.Tensor):
+    """The bf16 entry point or its fp32 form (``_f32``: the x3 fp32 step, ops/x3.py) for ``t``'s dtype."""
+    return getattr(_lib.lib(), name + "_f32" if t.dtype == torch.float32 else name)
+
+
+def _ok(x: torch.Tensor) -> bool:
+    return x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and x.shape[1] % 8 == 0
+
+
 def _box3(src, n, c, h, w, ld_src):
     out = _nhwc_empty(n, c, h, w, src)
-    rc = _lib.lib().tony_avgpool3_s1p1(src.data_ptr(), out.data_ptr(), n, h, w, c, ld_src, c,
-                                       _lib.stream_ptr(src.device))
+    rc = _fn("tony_avgpool3_s1p1", src)(src.data_ptr(), out.data_ptr(), n, h, w, c, ld_src, c,
+                                        _lib.stream_ptr(src.device))
     _lib.check(rc, "tony_avgpool3_s1p1")
     return out
 
@@ -43,7 +52,7 @@ class _MaxPoolFn(torch.autograd.Function):
         if y is None:
             y = _nhwc_empty(n, c, oh, ow, x)
         arg = torch.empty((n, oh, ow, c), dtype=torch.uint8, device=x.device)
-        rc = _lib.lib().tony_maxpool_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), n, h, w, c, k, s, p, ld,
+        rc = _fn("tony_maxpool_fwd", x)(x.data_ptr(), y.data_ptr(), arg.data_ptr(), n, h, w, c, k, s, p, ld,
                                          _rows_view(y)[2], _lib.stream_ptr(x.device))
         _lib.check(rc, "tony_maxpool_fwd")
         ctx.save_for_backward(arg)
@@ -56,7 +65,7 @@ class _MaxPoolFn(torch.autograd.Function):
         n, c, h, w, k, s, p = ctx.shape
         dy, (_, _, lddy) = _as_rows(dy)
         dx = _nhwc_empty(n, c, h, w, dy)
-        rc = _lib.lib().tony_maxpool_bwd(dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), n, h, w, c, k, s, p, lddy, c,
+        rc = _fn("tony_maxpool_bwd", dy)(dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), n, h, w, c, k, s, p, lddy, c,
                                          _lib.stream_ptr(dy.device))
         _lib.check(rc, "tony_maxpool_bwd")
         streams.keep(dx)  # may be consumed on another (branch) stream
@@ -70,7 +79,7 @@ class _AvgPoolFn(torch.autograd.Function):
         n, _, h, w = x.shape
         oh, ow = (h - k) // s + 1, (w - k) // s + 1
         y = _nhwc_empty(n, c, oh, ow, x)
-        rc = _lib.lib().tony_avgpool_fwd(x.data_ptr(), y.data_ptr(), n, h, w, c, k, s, ld, c,
+        rc = _fn("tony_avgpool_fwd", x)(x.data_ptr(), y.data_ptr(), n, h, w, c, k, s, ld, c,
                                          _lib.stream_ptr(x.device))
         _lib.check(rc, "tony_avgpool_fwd")
         ctx.shape = (n, c, h, w, k, s)
@@ -81,15 +90,15 @@ class _AvgPoolFn(torch.autograd.Function):
         n, c, h, w, k, s = ctx.shape
         dy, (_, _, lddy) = _as_rows(dy)
         dx = _nhwc_empty(n, c, h, w, dy)
-        rc = _lib.lib().tony_avgpool_bwd(dy.data_ptr(), dx.data_ptr(), n, h, w, c, k, s, lddy, c,
+        rc = _fn("tony_avgpool_bwd", dy)(dy.data_ptr(), dx.data_ptr(), n, h, w, c, k, s, lddy, c,
                                          _lib.stream_ptr(dy.device))
         _lib.check(rc, "tony_avgpool_bwd")
         return dx, None, None
 
 
 def avg_pool(x: torch.Tensor, k: int, s: int) -> torch.Tensor:
-    """avg_pool2d(x, k, s) (no padding) on channels_last bf16; k = H = W is the global average pool."""
-    if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0:
+    """avg_pool2d(x, k, s) (no padding) on channels_last bf16 / fp32; k = H = W is the global average pool."""
+    if _ok(x):
         return tape.apply(_AvgPoolFn, x, k, s)
     return torch.nn.functional.avg_pool2d(x, k, s)
 
@@ -102,8 +111,8 @@ def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
 
 
 def avg_pool3x3_s1(x: torch.Tensor) -> torch.Tensor:
-    """avg_pool2d(x, 3, 1, 1, count_include_pad=True) on channels_last bf16."""
-    if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0:
+    """avg_pool2d(x, 3, 1, 1, count_include_pad=True) on channels_last bf16 / fp32."""
+    if _ok(x):
         return tape.apply(_AvgPool3Fn, x)
     return torch.nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=True)
 
@@ -111,6 +120,6 @@ def avg_pool3x3_s1(x: torch.Tensor) -> torch.Tensor:
 def max_pool(x: torch.Tensor, k: int = 3, s: int = 2, slot=None, padding: int = 0) -> torch.Tensor:
     """max_pool2d(x, k, s, padding) on channels_last bf16 (into a concat.Slot when given); padded taps
     never win (torch semantics), e.g. ResNet's 3x3/2 p1 stem pool."""
-    if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0 and 2 * padding <= k:
+    if _ok(x) and 2 * padding <= k:
         return tape.apply(_MaxPoolFn, x, k, s, slot, padding)
     return torch.nn.functional.max_pool2d(x, k, s, padding)

@@ -1,0 +1,316 @@
+"""fp32 training on the bf16 matrix cores: the x3 operand split (csrc/x3.hip).
+
+The reference's TF-PS job trains in fp32 (``tony-examples/mnist-tensorflow/mnist_distributed.py:64-124``).
+MI355X's matrix cores are bf16/fp8 machines (fp32 MFMA runs at 1/16 of the bf16 rate), so the fp32
+step keeps every tensor -- activations, gradients, BN statistics, variables -- in fp32 and only the
+convolution / GEMM *products* go through the bf16 MFMAs, each fp32 operand split as hi + lo:
+
+    x * w  ~=  hi_x*hi_w + lo_x*hi_w + hi_x*lo_w        (lo_x*lo_w <= 2^-16 |x w| dropped)
+
+With activations laid out as channel planes [hi | lo | hi] and weights as [hi | hi | lo] (``split``),
+that sum is ONE implicit GEMM over 3x the channels on the same tuned kernels as the bf16 step, with
+the fp32 epilogue (flag bit 3 of tony_conv_fwd / tony_conv_dgrad / tony_gemm_bf16).  Weight gradients
+are the three plane pairs through the bf16 split-K wgrad kernels, summed in fp32.  BatchNorm, pooling
+and the loss run on fp32 rows (the ``*_f32`` entry points of csrc/bn_act.hip, csrc/pool.hip,
+csrc/loss.hip).  Products are accurate to ~2^-16 relative (fp32: 2^-24; the TF32 that TensorFlow's
+fp32 convolutions default to on tensor-core GPUs: 2^-11); accumulation is fp32 throughout.
+
+``ConvBNActX3`` is the layer (conv + BN + ReLU); ``inception_v3(precision="fp32")`` builds the whole
+model from it (models/inception_v3.py).
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+
+from . import _lib, tune
+from .bn import _as_rows
+
+ACT = 0b010  # activation / gradient planes: [hi | lo | hi]
+WGT = 0b100  # weight planes:                [hi | hi | lo]
+_F32 = torch.float32
+_BF16 = torch.bfloat16
+
+
+def cp_of(c: int) -> int:
+    """Channels per plane: C rounded up to 8 (16-byte aligned planes; the 3-channel image: 8)."""
+    return (c + 7) // 8 * 8
+
+
+def _pair(v):
+    return (v, v) if isinstance(v, int) else tuple(v)
+
+
+def split_rows(src: torch.Tensor, rows: int, c: int, ld: int, pattern: int) -> torch.Tensor:
+    """bf16 [rows, 3 * cp] planes of the fp32 rows ``src`` ([rows][c] at row stride ld)."""
+    cp = cp_of(c)
+    out = torch.empty((rows, 3 * cp), dtype=_BF16, device=src.device)
+    rc = _lib.lib().tony_x3_split(src.data_ptr(), ld, rows, c, cp, out.data_ptr(), 3 * cp, pattern,
+                                  _lib.stream_ptr(src.device))
+    _lib.check(rc, "tony_x3_split")
+    return out
+
+
+def split_act(x: torch.Tensor) -> Tuple[torch.Tensor, int]:
+    """fp32 NHWC activation (channels_last 4D, a channel slice of one, or [M, C]) -> bf16 planes as a
+    channels_last [N, 3cp, H, W] tensor (2D input: [M, 3cp]); also returns cp."""
+    x, (m, c, ld) = _rows4(x)
+    out = split_rows(x, m, c, ld, ACT)
+    cp = cp_of(c)
+    if x.dim() == 4:
+        n, _, h, w = x.shape
+        out = out.view(n, h, w, 3 * cp).permute(0, 3, 1, 2)
+    return out, cp
+
+
+def _rows4(x: torch.Tensor):
+    if x.dtype != _F32:
+        raise TypeError(f"x3 path: fp32 activations expected, got {x.dtype}")
+    return _as_rows(x)  # (rows, (M, C, ld)); the RGB image (C = 3): dense channels_last, ld = 3
+
+
+def split_weight(w: torch.Tensor) -> torch.Tensor:
+    """fp32 conv weight [Co, C, R, S] -> bf16 [Co][R][S][3cp] planes [hi | hi | lo] (KRSC memory)."""
+    co, c, r, s = w.shape
+    wk = w.permute(0, 2, 3, 1)
+    wk = wk if wk.is_contiguous() else wk.contiguous()
+    return split_rows(wk, co * r * s, c, c, WGT)
+
+
+def split_weight_t(w: torch.Tensor) -> torch.Tensor:
+    """fp32 conv weight [Co, C, R, S] -> bf16 [C][R][S][3Co] planes [hi | hi | lo] (the dgrad operand)."""
+    co, c, r, s = w.shape
+    wk = w.permute(0, 2, 3, 1)
+    wk = wk if wk.is_contiguous() else wk.contiguous()
+    out = torch.empty((c, r, s, 3 * co), dtype=_BF16, device=w.device)
+    rc = _lib.lib().tony_x3_weights_t(wk.data_ptr(), co, r * s, c, out.data_ptr(), _lib.stream_ptr(w.device))
+    _lib.check(rc, "tony_x3_weights_t")
+    return out
+
+
+def _cl(n, c, h, w, dev, dtype=_F32):
+    return torch.empty((n, c, h, w), dtype=dtype, device=dev, memory_format=torch.channels_last)
+
+
+# ---- convolution passes ---------------------------------------------------------------------------
+def conv_fwd(x3: torch.Tensor, cp: int, w3: torch.Tensor, wshape, stride, padding, stats=None) -> torch.Tensor:
+    """fp32 Z = conv(x, w) from the planes x3 [N, 3cp, H, W] and w3 [Co][R][S][3cp]; with ``stats``
+    (zeroed, _lib.stat_floats(Co)) the epilogue adds the BN [sum | sumsq] of Z."""
+    n, _, h, w = x3.shape
+    co, _, r, s = wshape
+    (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
+    oh, ow = (h + 2 * ph - r) // sh + 1, (w + 2 * pw - s) // sw + 1
+    z = _cl(n, co, oh, ow, x3.device)
+    ldx = 3 * cp  # dense planes (split_act)
+    L, st = _lib.lib(), _lib.stream_ptr(x3.device)
+    base = 8 | (1 if stats is not None else 0)
+
+    def launch(vf, stats_t):
+        return L.tony_conv_fwd(x3.data_ptr(), n, h, w, 3 * cp, ldx, w3.data_ptr(), co, r, s, sh, sw, ph, pw,
+                               z.data_ptr(), oh, ow, co, (base if stats_t is not None else 8) | vf,
+                               _lib.ptr(stats_t), 2 * co, st)
+
+    key = ("x3_fwd", tuple(x3.shape), ldx, tuple(wshape), (sh, sw), (ph, pw), stats is not None)
+    vf = tune.cached(key)
+    if vf is None:
+        scratch = torch.zeros(_lib.stat_floats(co), device=x3.device) if stats is not None else None
+        vf = tune.pick(key, lambda v: launch(v, scratch))
+    _lib.check(launch(vf, stats), "tony_conv_fwd (x3)")
+    return z
+
+
+def conv_dgrad(d3: torch.Tensor, wt3: torch.Tensor, co: int, x_shape, wshape, stride, padding) -> torch.Tensor:
+    """fp32 dX from the dZ planes d3 [N, 3Co, OH, OW] and wt3 [C][R][S][3Co]."""
+    n, c, h, w = x_shape
+    _, _, r, s = wshape
+    (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
+    _, _, oh, ow = d3.shape
+    dx = _cl(n, c, h, w, d3.device)
+    L, st = _lib.lib(), _lib.stream_ptr(d3.device)
+    ldd = 3 * co
+    if (sh, sw) == (1, 1):
+        def launch(vf):
+            return L.tony_conv_dgrad(d3.data_ptr(), n, oh, ow, 3 * co, ldd, wt3.data_ptr(), c, r, s, ph, pw,
+                                     dx.data_ptr(), h, w, c, 8 | vf, None, st)
+        name = "tony_conv_dgrad (x3)"
+    else:
+        def launch(vf):
+            return L.tony_conv_dgrad_strided(d3.data_ptr(), n, oh, ow, 3 * co, ldd, wt3.data_ptr(), c, r, s, sh, sw,
+                                             ph, pw, dx.data_ptr(), h, w, c, 8 | vf, None, st)
+        name = "tony_conv_dgrad_strided (x3)"
+    key = ("x3_dgrad", tuple(d3.shape), tuple(x_shape), tuple(wshape), (sh, sw), (ph, pw))
+    variants = tuple(v for v in tune.NT_VARIANTS if v not in (9, 10))  # fp32 epilogue: NT / LDS-DMA kernels
+    vf = tune.cached(key)
+    if vf is None:
+        vf = tune.pick(key, launch, variants)
+    _lib.check(launch(vf), name)
+    return dx
+
+
+def conv_wgrad(d3: torch.Tensor, x3: torch.Tensor, cp: int, wshape, stride, padding) -> torch.Tensor:
+    """fp32 dW [Co, C, R, S] (channels_last memory [Co][R][S][C]) = the three plane products
+    hi_d*hi_x + hi_d*lo_x + lo_d*hi_x, each a bf16 split-K implicit-GEMM wgrad summed in fp32."""
+    from .conv import conv_wgrad as wgrad_bf16
+
+    co, c, r, s = wshape
+    dev = d3.device
+    acc = torch.zeros(co * r * s * cp, dtype=_F32, device=dev)
+    dh, dl = d3[:, 0:co], d3[:, co:2 * co]
+    xh, xl = x3[:, 0:cp], x3[:, cp:2 * cp]
+    for dd, xx in ((dh, xh), (dh, xl), (dl, xh)):
+        wgrad_bf16(dd, xx, (co, cp, r, s), stride, padding, dst=acc)
+    dw = acc.view(co, r, s, cp)
+    if cp != c:
+        dw = dw[..., :c].contiguous()
+    return dw.permute(0, 3, 1, 2)
+
+
+# ---- BatchNorm on fp32 rows -------------------------------------------------------------------------
+def bn_apply(z: torch.Tensor, stats, gamma, beta, rmean, rvar, eps, momentum, relu, training):
+    """y = act(BN(z)) in fp32; training: batch statistics from ``stats`` (sharded [sum | sumsq]),
+    running statistics updated.  Returns (y, mean, invstd)."""
+    n, co, oh, ow = z.shape
+    m = n * oh * ow
+    y = _cl(n, co, oh, ow, z.device)
+    mean = torch.empty(co, dtype=_F32, device=z.device)
+    invstd = torch.empty(co, dtype=_F32, device=z.device)
+    L = _lib.lib()
+    rc = L.tony_bn_apply_f32(z.data_ptr(), m, co, co, y.data_ptr(), co, _lib.ptr(stats),
+                             None if stats is None else stats.data_ptr() + 4 * co, 2 * co if stats is not None else 0,
+                             gamma.data_ptr(), beta.data_ptr(), 0, float(eps), int(relu), 0 if training else 1,
+                             mean.data_ptr(), invstd.data_ptr(), _lib.ptr(rmean), _lib.ptr(rvar), float(momentum),
+                             _lib.stream_ptr(z.device))
+    _lib.check(rc, "tony_bn_apply_f32")
+    return y, mean, invstd
+
+
+def bn_backward(z, dy, mean, invstd, gamma, beta, relu):
+    """(dZ, dgamma, dbeta) of y = act(BN(z)) on fp32 rows."""
+    n, co, oh, ow = z.shape
+    m = n * oh * ow
+    dy, (_, _, lddy) = _as_rows(dy)
+    dev = z.device
+    sums = torch.zeros(_lib.stat_floats(co), dtype=_F32, device=dev)
+    dz = _cl(n, co, oh, ow, dev)
+    dgamma = torch.empty(co, dtype=_F32, device=dev)
+    dbeta = torch.empty(co, dtype=_F32, device=dev)
+    L, st = _lib.lib(), _lib.stream_ptr(dev)
+    rc = L.tony_bn_bwd_reduce_f32(z.data_ptr(), co, dy.data_ptr(), lddy, m, co, mean.data_ptr(), invstd.data_ptr(),
+                                  gamma.data_ptr(), beta.data_ptr(), 0, int(relu), sums.data_ptr(),
+                                  sums.data_ptr() + 4 * co, 2 * co, st)
+    _lib.check(rc, "tony_bn_bwd_reduce_f32")
+    rc = L.tony_bn_bwd_apply_f32(z.data_ptr(), co, dy.data_ptr(), lddy, dz.data_ptr(), co, m, co, mean.data_ptr(),
+                                 invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), 0, int(relu), sums.data_ptr(),
+                                 sums.data_ptr() + 4 * co, 2 * co, dgamma.data_ptr(), dbeta.data_ptr(), 0, st)
+    _lib.check(rc, "tony_bn_bwd_apply_f32")
+    return dz, dgamma, dbeta
+
+
+class _ConvBNActX3Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, rmean, rvar, stride, padding, training, momentum, eps, relu):
+        x3, cp = split_act(x)
+        w3 = split_weight(weight)
+        co = weight.shape[0]
+        stats = torch.zeros(_lib.stat_floats(co), dtype=_F32, device=x.device) if training else None
+        z = conv_fwd(x3, cp, w3, weight.shape, stride, padding, stats)
+        y, mean, invstd = bn_apply(z, stats, gamma, beta, rmean, rvar, eps, momentum, relu, training)
+        ctx.save_for_backward(x3, weight, gamma, beta, z, mean, invstd)
+        ctx.conf = (cp, tuple(x.shape), stride, padding, relu, x.requires_grad)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x3, weight, gamma, beta, z, mean, invstd = ctx.saved_tensors
+        cp, x_shape, stride, padding, relu, need_dx = ctx.conf
+        dz, dgamma, dbeta = bn_backward(z, dy, mean, invstd, gamma, beta, relu)
+        d3, _ = split_act(dz)
+        dw = conv_wgrad(d3, x3, cp, weight.shape, stride, padding)
+        dx = None
+        if need_dx and ctx.needs_input_grad[0]:
+            dx = conv_dgrad(d3, split_weight_t(weight), weight.shape[0], x_shape, weight.shape, stride, padding)
+        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None
+
+
+def conv_bn_act(x, weight, gamma, beta, rmean, rvar, stride=1, padding=0, training=True, momentum=0.1, eps=1e-3,
+                relu=True):
+    return _ConvBNActX3Fn.apply(x, weight, gamma, beta, rmean, rvar, stride, padding, training, momentum, eps, relu)
+
+
+# ---- the classifier: an x3 GEMM --------------------------------------------------------------------
+class _LinearX3Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        n, k = x.shape
+        out_f = weight.shape[0]
+        x3 = split_rows(x.contiguous(), n, k, k, ACT)
+        w3 = split_rows(weight.contiguous(), out_f, k, k, WGT)
+        kp = 3 * cp_of(k)
+        y = torch.empty((n, out_f), dtype=_F32, device=x.device)
+        rc = _lib.lib().tony_gemm_bf16(x3.data_ptr(), w3.data_ptr(), y.data_ptr(), n, out_f, kp, kp, kp, out_f, 8, None,
+                                       0, _lib.stream_ptr(x.device))
+        _lib.check(rc, "tony_gemm_bf16 (x3 linear)")
+        if bias is not None:
+            y += bias
+        ctx.save_for_backward(x3, weight)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x3, weight = ctx.saved_tensors
+        out_f, k = weight.shape
+        n = dy.shape[0]
+        dev = dy.device
+        L, st = _lib.lib(), _lib.stream_ptr(dev)
+        dy = dy.contiguous().float()
+        d3 = split_rows(dy, n, out_f, out_f, ACT)
+        cpo = cp_of(out_f)
+        # dX [n, k] = dY [n, out] . W [out, k]: B = W^T planes [k][3 out]
+        wt3 = split_rows(weight.t().contiguous(), k, out_f, out_f, WGT)
+        dx = torch.empty((n, k), dtype=_F32, device=dev)
+        rc = L.tony_gemm_bf16(d3.data_ptr(), wt3.data_ptr(), dx.data_ptr(), n, k, 3 * cpo, 3 * cpo, 3 * cpo, k, 8,
+                              None, 0, st)
+        _lib.check(rc, "tony_gemm_bf16 (x3 linear dgrad)")
+        # dW [out, k] = dY^T X: the three plane products through the split-K TN GEMM
+        from .gemm import wgrad_tn
+
+        cpk = cp_of(k)
+        acc = torch.zeros(out_f * cpk, dtype=_F32, device=dev)
+        for do, xo in ((0, 0), (0, cpk), (cpo, 0)):
+            wgrad_tn(d3.data_ptr() + 2 * do, 3 * cpo, x3.data_ptr() + 2 * xo, 3 * cpk, n, out_f, cpk, dev, dst=acc)
+        dw = acc.view(out_f, cpk)[:, :k]
+        db = dy.sum(0) if ctx.has_bias else None
+        return dx, dw, db
+
+
+class LinearX3(torch.nn.Linear):
+    """fp32 nn.Linear whose products run as an x3 bf16 GEMM (the classifier of the fp32 model)."""
+
+    def forward(self, x):
+        return _LinearX3Fn.apply(x, self.weight, self.bias)
+
+
+class ConvBNActX3(torch.nn.Module):
+    """Conv2d (no bias) + BatchNorm2d + ReLU, fp32, on the x3 split kernels (same parameters and
+    state-dict keys as models/layers.ConvBNAct)."""
+
+    fused = False  # models/layers.conv_bn_act_maxpool: no fused BN + pool kernel on this path
+    x3 = True
+
+    def __init__(self, cin, cout, k, stride=1, padding=0, eps=1e-3, momentum=0.1, relu=True):
+        super().__init__()
+        kk = _pair(k)
+        self.conv = torch.nn.Conv2d(cin, cout, kk, stride, padding, bias=False)
+        self.bn = torch.nn.BatchNorm2d(cout, eps=eps, momentum=momentum)
+        self.relu = relu
+        self.is_1x1 = kk == (1, 1) and _pair(stride) == (1, 1) and _pair(padding) == (0, 0)
+
+    def forward(self, x):
+        c, bn = self.conv, self.bn
+        return conv_bn_act(x, c.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, c.stride, c.padding,
+                           self.training, bn.momentum, bn.eps, self.relu)
+
+
+__all__ = ["ConvBNActX3", "LinearX3", "conv_bn_act", "split_act", "split_weight", "split_weight_t", "cp_of"]

@@ -19,6 +19,8 @@ for s in "$@"; do
     plan) step plan_tests 400 python -u -m pytest tests/test_plan_gpu.py tests/test_trainer_gpu.py -x -v --timeout 240 --timeout-method thread ;;
     bench_plan) step bench_plan 400 python bench.py --steps 20 --warmup 6 --mode graph ;;
     bench_graph) step bench_graph 400 env TONY_REPLAY=graph python bench.py --steps 20 --warmup 6 --mode graph ;;
+    x3) step x3_tests 400 python -u -m pytest tests/test_x3_gpu.py -x -v --timeout 240 --timeout-method thread ;;
+    bench_fp32) step bench_fp32 600 python bench.py --steps 10 --warmup 3 --dtype fp32 --mode eager ;;
     tests) step gpu_suite 800 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread ;;
     bench) step bench 400 python bench.py --steps 20 --warmup 6 ;;
     bench_r50) step bench_r50 400 python bench.py --model resnet50 --steps 20 --warmup 6 ;;
