@@ -215,7 +215,7 @@ def test_avgpool3(cuda, shape):
     x = _nhwc(x).requires_grad_(True)
     y = avg_pool3x3_s1(x)
     # fp32 reference on the CPU: the GPU channels_last avg_pool2d backward of this
-    # PyTorch-ROCm build returns wrong gradients (see tools/debug_pool2.py)
+    # PyTorch-ROCm build returns wrong gradients (max relative error ~1.2 on 4x64x17x17)
     xr = x.detach().float().cpu().requires_grad_(True)
     yr = torch.nn.functional.avg_pool2d(xr, 3, 1, 1, count_include_pad=True)
     _close(y, yr, 1e-2, 1e-2, "avgpool fwd")

@@ -110,9 +110,11 @@ def test_fp32_pools_match_torch(cuda, op):
     y = fn(x)
     g = _cl(torch.randn_like(y))
     y.backward(g)
-    xr = x.detach().clone().requires_grad_()
+    # float64 reference on the CPU: this PyTorch-ROCm build's channels_last GPU avg_pool2d backward
+    # returns wrong gradients (the bf16 pool tests in test_ops_gpu.py reference the CPU for the same reason)
+    xr = x.detach().double().cpu().requires_grad_()
     yr = ref(xr)
-    yr.backward(g)
+    yr.backward(g.double().cpu())
     assert _rel(y.detach(), yr.detach()) < 1e-6
     assert _rel(x.grad, xr.grad) < 1e-6
 
@@ -125,12 +127,20 @@ def test_inception_fp32_step_matches_stock_fp32(cuda):
 
     torch.manual_seed(0)
     ours = inception_v3(precision="fp32", seed=3).to(DEV).to(memory_format=torch.channels_last).train()
-    ref = inception_v3(fused=False, seed=3).to(DEV).to(memory_format=torch.channels_last).train()
+    # the stock graph runs NCHW: this PyTorch-ROCm build's channels_last GPU avg_pool2d backward is wrong
+    # (test_fp32_pools_match_torch references the CPU for that reason), and with it every gradient
+    # upstream of an Inception pool branch
+    ref = inception_v3(fused=False, seed=3).to(DEV).train()
     ours.dropout.p = ref.dropout.p = 0.0
     x = _cl(torch.randn(4, 3, 299, 299, device=DEV))
     y = torch.randint(0, 1000, (4,), device=DEV)
+    t = torch.randn(2, 8, 9, 9, device=DEV, dtype=torch.float64, requires_grad=True)
+    F.avg_pool2d(t, 3, 1, 1, count_include_pad=True).pow(2).sum().backward()
+    tc = t.detach().cpu().requires_grad_()
+    F.avg_pool2d(tc, 3, 1, 1, count_include_pad=True).pow(2).sum().backward()
+    assert _rel(t.grad, tc.grad) < 1e-12, "NCHW GPU avg_pool2d backward is wrong too: no stock reference"
     lo, ao = ours(x)
-    lr_, ar = ref(x)
+    lr_, ar = ref(x.contiguous())
     loss_o = cross_entropy(lo, y) + 0.4 * cross_entropy(ao, y)
     loss_r = F.cross_entropy(lr_, y) + 0.4 * F.cross_entropy(ar, y)
     loss_o.backward()

@@ -32,6 +32,10 @@ for s in "$@"; do
     # 1 ps + 2 workers, three processes on the box's one GPU (gloo only exchanges the window handles):
     # the dedicated PS on the xGMI data plane with the real Inception-v3 step
     bench3_ded) step bench3_ded 600 env TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 3 --master-addr 127.0.0.1 --master-port 29521 bench.py --gpus 3 --steps 4 --warmup 2 --batch 32 --mode eager --ps-mode dedicated ;;
+    # 2 colocated ranks on the box's one GPU (gloo): --mode auto now also times the native plan with
+    # per-bucket segments at N > 1; bench2_plan forces it (and the xGMI kernels for the buckets)
+    bench2_auto) step bench2_auto 600 env TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29523 bench.py --gpus 2 --steps 6 --warmup 3 --batch 32 ;;
+    bench2_plan) step bench2_plan 600 env TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29524 bench.py --gpus 2 --steps 6 --warmup 3 --batch 32 --mode graph --collective hip ;;
     # the same topology through the launcher (bin/tony: coordinator -> task agents -> TF_CONFIG)
     ps_job) step ps_job 600 bash bin/tony --src_dir tony_amd/jobs --executes inception_ps.py \
               --task_params "--ps-mode dedicated --batch-size 32 --steps 6 --warmup 2" \
@@ -42,8 +46,8 @@ for s in "$@"; do
           step prof 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 5 --mode eager ${BENCH_ARGS:-}
           python3 tools/prof_summary.py gpurun_out/prof --skip 6 > gpurun_out/prof_summary.md; find gpurun_out/prof -name '*trace*' -delete ;;
     trace) export TMPDIR=/tmp; R=$(pwd)
-          step trace 600 rocprofv3 --kernel-trace -d "$R/gpurun_out/trace" -o run --output-format csv -- python3 "$R/bench.py" --steps 3 --warmup 5 --mode eager ${BENCH_ARGS:-}
-          python3 tools/step_union.py gpurun_out/trace --per-queue > gpurun_out/trace_union.txt; find gpurun_out/trace -name "*trace*.csv" -delete ;;
+          step trace 600 rocprofv3 --kernel-trace -d "$R/gpurun_out/trace" -o run --output-format csv -- python3 "$R/bench.py" --steps 3 --warmup 5 --mode ${TRACE_MODE:-graph} ${BENCH_ARGS:-}
+          python3 tools/step_union.py gpurun_out/trace --per-queue > gpurun_out/trace_union.txt; python3 tools/crit_path.py $(find gpurun_out/trace -name "*kernel_trace.csv" | head -1) > gpurun_out/crit_path.txt 2>&1 || true; find gpurun_out/trace -name "*trace*.csv" -delete ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
   esac
 done
