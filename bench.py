@@ -261,13 +261,12 @@ def main():
     if args.tune_cache and os.path.exists(args.tune_cache):
         tune_loaded = tune.load(args.tune_cache)
     mode = "eager" if args.no_graph else args.mode
-    if mode == "auto" and world > 1 and (args.ps_mode != "colocated" or os.environ.get("TONY_REPLAY", "plan") != "plan"):
-        # several ranks without the native plan: a replayed graph holds forward + backward only and the
-        # bucketed PS push / apply / pull then runs after it, un-overlapped (collectives stay out of the
-        # capture), so the eager step -- communication overlapped with backward -- is the one to run.
-        # The colocated PS under the native plan keeps the overlap (each bucket's collective is issued
-        # right after the plan segment that completes it, parallel/trainer.py _replay_overlapped) at
-        # ~2.5 ms of host per step instead of ~11 (8 ranks share the node's host CPUs), so auto times both.
+    if mode == "auto" and world > 1:
+        # several ranks: the eager step overlaps the bucketed PS push / apply / pull with backward.  The
+        # native plan can too (per-bucket plan segments, parallel/trainer.py _replay_overlapped), but its
+        # 2-rank rehearsal failed to replay (tony_plan_replay: hipErrorInvalidValue on one rank,
+        # profiles/r3s2_bench2_auto_plan_replay_fail.log), so auto keeps to eager at N > 1 until it is
+        # fixed; --mode graph still selects it
         mode = "eager"
     if ps.is_worker:
         trainer = Trainer(model, ps, loss_fn, use_graph=mode != "eager", overlap_wgrad=not args.no_wgrad_stream,

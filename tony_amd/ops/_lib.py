@@ -100,6 +100,9 @@ _SIGNATURES = {
     "tony_conv_wgrad": [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int, c_int, c_int, c_int,
                         c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_void_p,
                         c_void_p, c_int, c_void_p],
+    "tony_conv_wgrad_x3": [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int, c_int, c_int,
+                           c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_int,
+                           c_void_p],
     "tony_conv_wgrad_direct": [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int, c_int, c_int,
                                c_int, c_int, c_void_p, c_int64, c_void_p, c_int, c_void_p],
     "tony_avgpool3_s1p1": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
@@ -127,6 +130,9 @@ _SIGNATURES = {
     "tony_bn_bwd_apply_f32": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p,
                           c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p,
                           c_void_p, c_int, c_void_p],
+    "tony_bn_bwd_apply_f32_x3": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p,
+                          c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p,
+                          c_void_p, c_int, c_void_p],
     "tony_avgpool3_s1p1_f32": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
     "tony_maxpool_fwd_f32": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
                          c_void_p],
@@ -141,6 +147,7 @@ _SIGNATURES = {
     "tony_plan_build": [c_void_p, c_u64_p, c_int, c_u64_p, c_int_p],
     "tony_plan_replay": [c_void_p, c_int, c_void_p],
     "tony_plan_segments": [c_void_p],
+    "tony_plan_failure": [c_void_p, c_int_p],
     "tony_plan_ops": [c_void_p, c_int_p, c_int],
     "tony_plan_destroy": [c_void_p],
     # parameter-server data plane over xGMI windows (csrc/ps_plane.hip, parallel/ps_plane.py)
@@ -238,6 +245,9 @@ def check_stat_buffer(buf, c: int) -> None:
 # the memory pipeline -- measured 109 us per layer vs 43 us for the reduce + apply pair
 # (profiles/r2_rejected_splitk_fold_bn_onepass_prof.md).
 BN_ONEPASS = os.environ.get("TONY_BN_ONEPASS", "0") == "1"
+# ... only for layers whose activation (M x C bf16) is at most this many MB (0: every layer): the small
+# 17x17 / 8x8 layers pay two launch ramps for 14 MB of data, and their second read hits the L2 / MALL
+BN_ONEPASS_MAX_BYTES = int(os.environ.get("TONY_BN_ONEPASS_MAX_MB", "0")) << 20
 
 
 def bn_bwd_ws_floats(c: int) -> int:
@@ -258,7 +268,8 @@ def bn_bwd(x, ldx: int, dy, lddy: int, dx, lddx: int, M: int, C: int, mean, invs
                                  stream_ptr(device))
         check(rc, "tony_bn_bwd_apply")
         return
-    if BN_ONEPASS and ws.numel() >= stat_floats(C) + 1:
+    if BN_ONEPASS and ws.numel() >= stat_floats(C) + 1 and (BN_ONEPASS_MAX_BYTES == 0 or
+                                                             2 * M * C <= BN_ONEPASS_MAX_BYTES):
         rc = L.tony_bn_bwd_onepass(x.data_ptr(), ldx, dy.data_ptr(), lddy, dx.data_ptr(), lddx, M, C,
                                    mean.data_ptr(), invstd.data_ptr(), ptr(gamma), ptr(beta), pb, int(relu),
                                    ws.data_ptr(), ptr(dgamma), ptr(dbeta), int(accumulate),

@@ -321,7 +321,10 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
 // dx = k*(dy' - dsum/M - xhat*dsumx/M) folded per channel into dx = dy'*q0 + x*q1 + q2 (LDS table,
 // with the ReLU test x*q3 + q4 > 0).  YMASK: mask dy by the saved output y and also write the
 // masked dy -- the gradient of the residual branch -- to dres (when non-null).
-template <bool YMASK, class T = uint16_t>
+// X3 (T = float, the fp32 step of ops/x3.py): dx is written straight as the bf16 [hi | lo | hi] planes
+// of the next convolution's backward (row stride lddx = 3C, plane p at column p * C): the fp32 dx and
+// the separate split pass over it (x3.hip split3_kernel) are never made.
+template <bool YMASK, class T = uint16_t, bool X3 = false>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     const T* __restrict__ x, int64_t ldx, const T* __restrict__ dy, int64_t lddy,
     const T* __restrict__ ym, int64_t ldym, T* __restrict__ dres, int64_t lddr,
@@ -379,7 +382,20 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
       }
       o[j] = fmaf(d, q0[j], fmaf(xf[j], q1[j], q2[j]));
     }
-    V8<T>::from_float(o).store(dx + row * lddx + rm.cg * 8);
+    if constexpr (X3) {
+      float lo[8];
+      const V8<uint16_t> hi = V8<uint16_t>::from_float(o);
+      float hf[8];
+      hi.to_float(hf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) lo[j] = o[j] - hf[j];
+      uint16_t* d = reinterpret_cast<uint16_t*>(dx) + row * lddx + rm.cg * 8;
+      hi.store(d);
+      V8<uint16_t>::from_float(lo).store(d + C);
+      hi.store(d + 2 * C);
+    } else {
+      V8<T>::from_float(o).store(dx + row * lddx + rm.cg * 8);
+    }
     if (YMASK && dres != nullptr) V8<T>::from_float(gf).store(dres + row * lddr + rm.cg * 8);
   };
   V8<T> none{};
@@ -411,9 +427,10 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
 // per layer (x 96 layers per Inception step).  Here a workgroup reduces its rows, all workgroups
 // meet at a grid barrier (an atomic arrival counter in the zeroed statistics workspace), and each
 // then applies to the SAME rows it just reduced -- the second read mostly hits the L2 / MALL.
-// The grid is at most 2 workgroups per CU with <= 40 KB of LDS each, so every workgroup of the
-// launch is resident on an otherwise idle GPU (4 fit per CU): no workgroup can wait on one that
-// never gets a CU.  Arrival is a release atomic by one lane after __syncthreads; the wait polls
+// The grid is at most 1 workgroup per CU with <= 40 KB of LDS each, so every workgroup of the
+// launch is resident on an otherwise idle GPU (4 fit per CU), also beside two more such launches on
+// the branch streams: no workgroup can wait on one that never gets a CU.  Opt-in
+// (TONY_BN_ONEPASS=1, TONY_BN_ONEPASS_MAX_MB: the layers it applies to, ops/_lib.py).  Arrival is a release atomic by one lane after __syncthreads; the wait polls
 // with an acquire load at agent scope (vector memory, never the scalar cache).
 __device__ __forceinline__ void grid_barrier(unsigned* counter) {
   __syncthreads();
@@ -919,6 +936,26 @@ TONY_API int tony_bn_bwd_reduce_f32(const void* x, int64_t ldx, const void* dy, 
   return 0;
 }
 
+// tony_bn_bwd_apply_f32 writing dx as the x3 planes (bf16 [M][3C], row stride lddx >= 3C): X3 above
+TONY_API int tony_bn_bwd_apply_f32_x3(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx3,
+                                      int64_t lddx, int64_t M, int C, const float* mean, const float* invstd,
+                                      const void* gamma, const void* beta, int param_bf16, int relu, const float* dsum,
+                                      const float* dsumx, int64_t sstride, void* dgamma, void* dbeta, int accumulate,
+                                      hipStream_t stream) {
+  if (bad_c(C) || (ldx % 4) || (lddy % 4) || (lddx % 8) || lddx < 3 * static_cast<int64_t>(C) || sstride < 0 ||
+      (reinterpret_cast<uintptr_t>(dx3) & 15))
+    return -1;
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 4, 8192, &rpb, &grid);
+  bn_bwd_apply_kernel<false, float, true><<<grid, kThreads, bn_lds_table(C, 5), stream>>>(
+      static_cast<const float*>(x), ldx, static_cast<const float*>(dy), lddy, nullptr, 0, nullptr, 0,
+      static_cast<float*>(dx3), lddx, M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsum, dsumx, sstride,
+      dgamma, dbeta, accumulate, Segs{});
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
 TONY_API int tony_bn_bwd_apply_f32(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx, int64_t lddx,
                                    int64_t M, int C, const float* mean, const float* invstd, const void* gamma,
                                    const void* beta, int param_bf16, int relu, const float* dsum, const float* dsumx,
@@ -967,7 +1004,9 @@ TONY_API int tony_bn_bwd_onepass(const void* x, int64_t ldx, const void* dy, int
   const int64_t ss = 2 * static_cast<int64_t>(C);
   int64_t rpb;
   int grid;
-  plan_rows(M, C, 4, 2 * num_cus, &rpb, &grid);  // <= 2 workgroups per CU: all co-resident
+  // <= 1 workgroup per CU (40 KB of LDS, 4 waves): all co-resident even with two more of these kernels
+  // spinning at their barriers on the branch streams (4 fit per CU by LDS), so no cycle of waiting grids
+  plan_rows(M, C, 4, num_cus, &rpb, &grid);
   bn_bwd_onepass_kernel<<<grid, kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, static_cast<uint16_t*>(dx), lddx,
       M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsums_ws, dsums_ws + C, ss, dgamma, dbeta, accumulate,

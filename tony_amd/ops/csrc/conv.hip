@@ -882,11 +882,22 @@ struct IncRows {
   }
 };
 
+// x3 (fp32) weight gradients: the three bf16 plane products dW = dYh^T Xh + dYh^T Xl + dYl^T Xh of
+// ops/x3.py as ONE split-K launch.  The splits come in npairs groups of sp; group q reads dY and X at
+// the element offsets dy_off[q] / x_off[q] (the plane's first channel) and stores its partials into
+// slab splits q * sp .. q * sp + sp - 1, so one tony_splitk_reduce sums all three products.
+// npairs = 1, offsets 0: the plain wgrad.
+struct PlanePairs {
+  int npairs, sp;
+  int dy_off[3], x_off[3];
+};
+
 template <int TBM, bool INC>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __restrict__ dY, int64_t lddy,
                                                               Gather g, float* __restrict__ C, int64_t M, int Co,
                                                               int tiles_n2, int ntiles, int64_t rows_per_split,
-                                                              float* __restrict__ slab, SplitFold fold, WkStep ws) {
+                                                              float* __restrict__ slab, SplitFold fold, WkStep ws,
+                                                              PlanePairs pp) {
   constexpr int TM = TBM / 32;                 // 16-row MFMA tiles per wave along Cout (2 waves)
   constexpr int A_CH = TBM / 8;                // 16-B chunks per dY row in the tile
   constexpr int AV = (WK * A_CH + kThreads - 1) / kThreads;
@@ -895,9 +906,12 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 2 * TILE];
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int tile = wg % ntiles, split = wg / ntiles;
+  const int pair = split / pp.sp;  // wave-uniform: selects, no dynamic index into the argument array
+  dY += pair == 0 ? pp.dy_off[0] : pair == 1 ? pp.dy_off[1] : pp.dy_off[2];
+  g.src += pair == 0 ? pp.x_off[0] : pair == 1 ? pp.x_off[1] : pp.x_off[2];
   const int t1 = tile / tiles_n2, t2 = tile % tiles_n2;
   const int n1_0 = t1 * TBM, n2_0 = t2 * WTBN;
-  const int64_t m_begin = static_cast<int64_t>(split) * rows_per_split;
+  const int64_t m_begin = static_cast<int64_t>(split - pair * pp.sp) * rows_per_split;
   const int64_t m_end = min(M, m_begin + rows_per_split);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -1060,16 +1074,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
                                                                    Gather g, int64_t M, int Co, int tiles_n2,
                                                                    int ntiles, int64_t rows_per_split,
                                                                    float* __restrict__ slab, SplitFold fold,
-                                                                   WkStep ws) {
+                                                                   WkStep ws, PlanePairs pp) {
   constexpr int TM = TBM / 32;
   constexpr int TILE = WK * 128;           // elements per staged operand (32 rows x 256 B)
   constexpr int STAGE = 2 * TILE;          // A then B
   __shared__ __attribute__((aligned(16))) uint16_t smem[kWgStages * STAGE];
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int tile = wg % ntiles, split = wg / ntiles;
+  const int pair = split / pp.sp;  // wave-uniform: selects, no dynamic index into the argument array
+  dY += pair == 0 ? pp.dy_off[0] : pair == 1 ? pp.dy_off[1] : pp.dy_off[2];
+  g.src += pair == 0 ? pp.x_off[0] : pair == 1 ? pp.x_off[1] : pp.x_off[2];
   const int t1 = tile / tiles_n2, t2 = tile % tiles_n2;
   const int n1_0 = t1 * TBM, n2_0 = t2 * WTBN;
-  const int64_t m_begin = static_cast<int64_t>(split) * rows_per_split;
+  const int64_t m_begin = static_cast<int64_t>(split - pair * pp.sp) * rows_per_split;
   const int64_t m_end = min(M, m_begin + rows_per_split);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -1388,22 +1405,26 @@ bool wgrad_inc_step(const Gather& g, int64_t M, WkStep* ws) {
 
 template <int TBM>
 int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, float* slab, int64_t slab_cap,
-                 int* splits_out, int64_t M, int Co, int num_cus, const SplitFold& fold, hipStream_t stream) {
+                 int* splits_out, int64_t M, int Co, int num_cus, const SplitFold& fold, hipStream_t stream,
+                 PlanePairs pp = PlanePairs{1, 1, {0, 0, 0}, {0, 0, 0}}) {
   const int tiles_n1 = ceil_div(Co, TBM), tiles_n2 = ceil_div(g.K, WTBN);
   const int ntiles = tiles_n1 * tiles_n2;
-  // enough workgroups for ~2 per CU, each reducing >= 8 stages of WK rows
+  const int npairs = pp.npairs;
+  // enough workgroups for ~2 per CU (over all plane pairs), each reducing >= 8 stages of WK rows
   const int target = 2 * (num_cus > 0 ? num_cus : 256);
-  int64_t splits = (target + ntiles - 1) / ntiles;
+  int64_t splits = (target + static_cast<int64_t>(ntiles) * npairs - 1) / (static_cast<int64_t>(ntiles) * npairs);
   const int64_t max_splits = (M + 8 * WK - 1) / (8 * WK);
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   int64_t rows = (M + splits - 1) / splits;
   rows = (rows + WK - 1) / WK * WK;
-  splits = (M + rows - 1) / rows;
-  const int64_t grid = splits * ntiles;
+  splits = (M + rows - 1) / rows;  // per plane pair
+  pp.sp = static_cast<int>(splits);
+  const int64_t grid = splits * npairs * ntiles;
   if (grid > 0x7fffffff) return -2;
-  if (slab != nullptr && splits * Co * static_cast<int64_t>(g.K) > slab_cap) return -4;  // caller's bound is off
-  if (splits_out != nullptr) *splits_out = static_cast<int>(splits);
+  if (slab != nullptr && splits * npairs * Co * static_cast<int64_t>(g.K) > slab_cap) return -4;  // caller's bound is off
+  if (npairs > 1 && (slab == nullptr || fold.counters != nullptr)) return -1;  // the pairs meet in the slab
+  if (splits_out != nullptr) *splits_out = static_cast<int>(splits * npairs);
   // LDS-DMA staging pays for the 128-row Cout tiles only (measured: Cout <= 64 tiles, whose A rows
   // are half / quarter zero chunks, run 4-8 % slower than the register-staged kernel)
   WkStep ws{};
@@ -1412,16 +1433,16 @@ int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, float
   if (TBM == 128 && slab != nullptr && wgrad_glds_enabled()) {
     if (inc)
       conv_wgrad_glds_kernel<TBM, true><<<static_cast<int>(grid), kThreads, 0, stream>>>(
-          dyp, lddy, g, M, Co, tiles_n2, ntiles, rows, slab, fold, ws);
+          dyp, lddy, g, M, Co, tiles_n2, ntiles, rows, slab, fold, ws, pp);
     else
       conv_wgrad_glds_kernel<TBM, false><<<static_cast<int>(grid), kThreads, 0, stream>>>(
-          dyp, lddy, g, M, Co, tiles_n2, ntiles, rows, slab, fold, ws);
+          dyp, lddy, g, M, Co, tiles_n2, ntiles, rows, slab, fold, ws, pp);
   } else if (inc) {
     conv_wgrad_kernel<TBM, true><<<static_cast<int>(grid), kThreads, 0, stream>>>(
-        dyp, lddy, g, dw, M, Co, tiles_n2, ntiles, rows, slab, fold, ws);
+        dyp, lddy, g, dw, M, Co, tiles_n2, ntiles, rows, slab, fold, ws, pp);
   } else {
     conv_wgrad_kernel<TBM, false><<<static_cast<int>(grid), kThreads, 0, stream>>>(
-        dyp, lddy, g, dw, M, Co, tiles_n2, ntiles, rows, slab, fold, ws);
+        dyp, lddy, g, dw, M, Co, tiles_n2, ntiles, rows, slab, fold, ws, pp);
   }
   TONY_LAUNCH_CHECK();
   return 0;
@@ -1553,6 +1574,29 @@ TONY_API int tony_conv_wgrad(const void* dy, int64_t lddy, const void* x, int N,
   if (Co <= 32) return launch_wgrad<32>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream);
   if (Co <= 64) return launch_wgrad<64>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream);
   return launch_wgrad<128>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream);
+}
+
+// x3 weight gradient (ops/x3.py conv_wgrad): dy / x point at the hi planes (channel 0) of the dY and X
+// plane tensors, the lo planes start dplane / xplane elements (channels) later; C and Co are the plane
+// widths.  Partials of dYh^T Xh, dYh^T Xl and dYl^T Xh into one slab (*splits_out = all of them):
+// the caller's tony_splitk_reduce sums the three products.
+TONY_API int tony_conv_wgrad_x3(const void* dy, int64_t lddy, const void* x, int N, int H, int W, int C, int64_t ldx,
+                                int Co, int R, int S, int sh, int sw, int ph, int pw, int OH, int OW, int dplane,
+                                int xplane, float* slab, int64_t slab_cap, int* splits_out, int num_cus,
+                                hipStream_t stream) {
+  if (bad_geom(C, ldx, x) || (Co % 8) || (lddy % 8) || (reinterpret_cast<uintptr_t>(dy) & 15) || slab == nullptr)
+    return -1;
+  if ((dplane % 8) || (xplane % 8) || dplane < Co || xplane < C || dplane + Co > lddy || xplane + C > ldx) return -1;
+  if (OH != (H + 2 * ph - R) / sh + 1 || OW != (W + 2 * pw - S) / sw + 1) return -1;
+  const int K = R * S * C;
+  const int64_t M = static_cast<int64_t>(N) * OH * OW;
+  if (M > 0x7fffffff) return -1;
+  Gather g{static_cast<const uint16_t*>(x), ldx, H, W, C, OH, OW, R, S, sh, sw, -ph, -pw, 1, K, 0};
+  const SplitFold fold{nullptr, nullptr, 0};
+  const PlanePairs pp{3, 1, {0, 0, dplane}, {0, xplane, 0}};
+  if (Co <= 32) return launch_wgrad<32>(dy, lddy, g, nullptr, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream, pp);
+  if (Co <= 64) return launch_wgrad<64>(dy, lddy, g, nullptr, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream, pp);
+  return launch_wgrad<128>(dy, lddy, g, nullptr, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream, pp);
 }
 
 // dW (fp32 partials, [grid][Co][3][3][C]) of a 3x3 stride-1 conv with C, Co in {32, 64} by the

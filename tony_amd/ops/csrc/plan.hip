@@ -59,6 +59,7 @@ struct Plan {
   std::vector<int> tails;            // per stream: event recorded after its last op (joined at the end)
   std::vector<int> seg_end;          // op index one past each marker (segment k = [seg_end[k-1], seg_end[k]))
   int stats[11] = {};
+  int fail_op = -1, fail_kind = -1, fail_stream = -1;  // the op whose issue failed last (tony_plan_failure)
 };
 
 int new_event(Plan& p) {
@@ -445,7 +446,14 @@ TONY_API int tony_plan_replay(void* handle, int seg, hipStream_t side) {
   }
   const int lo = first == 0 ? 0 : p->seg_end[first - 1];
   const int hi = p->seg_end[last];
-  for (int i = lo; i < hi && e == hipSuccess; ++i) e = issue(*p, p->ops[i], side);
+  for (int i = lo; i < hi && e == hipSuccess; ++i) {
+    e = issue(*p, p->ops[i], side);
+    if (e != hipSuccess) {
+      p->fail_op = i;
+      p->fail_kind = p->ops[i].kind;
+      p->fail_stream = p->ops[i].stream;
+    }
+  }
   if (e == hipSuccess && last == nseg - 1) {
     for (int s = 1; s < p->nstreams && e == hipSuccess; ++s)
       if (p->tails[s] >= 0) {
@@ -454,6 +462,16 @@ TONY_API int tony_plan_replay(void* handle, int seg, hipStream_t side) {
       }
   }
   return static_cast<int>(e);
+}
+
+// out[3] = (op index, op kind, stream) of the last failed issue (-1s: none)
+TONY_API int tony_plan_failure(void* handle, int* out) {
+  Plan* p = static_cast<Plan*>(handle);
+  if (p == nullptr || out == nullptr) return -1;
+  out[0] = p->fail_op;
+  out[1] = p->fail_kind;
+  out[2] = p->fail_stream;
+  return 0;
 }
 
 TONY_API int tony_plan_segments(void* handle) {

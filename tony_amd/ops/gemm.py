@@ -73,7 +73,8 @@ def wgrad_cus(device, occ: int = 1) -> int:
 SPLITK_FOLD = os.environ.get("TONY_SPLITK_FOLD", "0") == "1"
 
 
-def splitk_combine(launch, n: int, ntiles: int, device, dst: torch.Tensor | None = None, occ: int = 1):
+def splitk_combine(launch, n: int, ntiles: int, device, dst: torch.Tensor | None = None, occ: int = 1,
+                   pairs: int = 1):
     """Run a split-K weight-gradient kernel in slab mode and sum its splits.
 
     ``launch(slab_ptr, slab_cap, splits_ref, fold_counters, fold_dst, fold_flags)`` launches the
@@ -82,14 +83,15 @@ def splitk_combine(launch, n: int, ntiles: int, device, dst: torch.Tensor | None
     (else csrc/splitk.hip's combine kernel does).  The sum is ADDED into ``dst`` (a bf16 or fp32
     flat-gradient slot in the kernel's element order) and None returned, or returned as a new
     fp32 tensor of n floats.  The split count never exceeds ceil(2 * CUs / ntiles) (the kernels'
-    2-workgroups-per-CU plan), which bounds the slab."""
+    2-workgroups-per-CU plan), which bounds the slab; ``pairs``: plane pairs of an x3 launch
+    (csrc/conv.hip tony_conv_wgrad_x3), each with its own splits of that plan divided by ``pairs``."""
     cus = wgrad_cus(device, occ)
-    bound = max(1, -(-2 * cus // ntiles))
+    bound = pairs * max(1, -(-2 * cus // (pairs * ntiles)))
     slab = torch.empty(bound * n, dtype=torch.float32, device=device)
     splits = ctypes.c_int(0)
     out = dst if dst is not None else torch.empty(n, dtype=torch.float32, device=device)
     flags = int(out.dtype == torch.bfloat16) | (2 if dst is not None else 0)
-    if SPLITK_FOLD:
+    if SPLITK_FOLD and pairs == 1:
         counters = zeros_f32(ntiles, device)  # zero bits = zero uint32 arrival counters
         _lib.check(launch(slab.data_ptr(), slab.numel(), ctypes.addressof(splits), counters.data_ptr(), out.data_ptr(),
                           flags), "split-K wgrad (fold)")

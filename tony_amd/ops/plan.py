@@ -62,7 +62,12 @@ class StepPlan:
         stream must be ``streams[0]``."""
         rc = self._replay(self.handle, seg, None if side is None else side.cuda_stream)
         if rc:
-            _lib.check(rc, "tony_plan_replay")
+            f = (ctypes.c_int * 3)()
+            _lib.lib().tony_plan_failure(self.handle, f)
+            kinds = ("kernel", "memset", "memcpy", "wait", "record", "marker", "one-node graph")
+            kind = kinds[f[1]] if 0 <= f[1] < len(kinds) else str(f[1])
+            _lib.check(rc, f"tony_plan_replay (segment {seg}: op {f[0]} of {len(self.ops())}, a {kind} on plan "
+                           f"stream {f[2]})")
 
     def ops(self) -> List[tuple]:
         """(kind, stream, event-or-marker) per issued op: kinds 0 kernel, 1 memset, 2 memcpy, 3 wait,

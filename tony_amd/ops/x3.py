@@ -150,16 +150,26 @@ def conv_dgrad(d3: torch.Tensor, wt3: torch.Tensor, co: int, x_shape, wshape, st
 
 def conv_wgrad(d3: torch.Tensor, x3: torch.Tensor, cp: int, wshape, stride, padding) -> torch.Tensor:
     """fp32 dW [Co, C, R, S] (channels_last memory [Co][R][S][C]) = the three plane products
-    hi_d*hi_x + hi_d*lo_x + lo_d*hi_x, each a bf16 split-K implicit-GEMM wgrad summed in fp32."""
-    from .conv import conv_wgrad as wgrad_bf16
+    hi_d*hi_x + hi_d*lo_x + lo_d*hi_x: ONE split-K wgrad launch whose splits come in three plane-pair
+    groups (csrc/conv.hip tony_conv_wgrad_x3) and one combine of all their partials -- not three
+    launches, three combines and an fp32 accumulator fill (profiles/r3s2_fp32_x3_steady.md)."""
+    from .gemm import splitk_combine, wgrad_cus
 
     co, c, r, s = wshape
     dev = d3.device
-    acc = torch.zeros(co * r * s * cp, dtype=_F32, device=dev)
-    dh, dl = d3[:, 0:co], d3[:, co:2 * co]
-    xh, xl = x3[:, 0:cp], x3[:, cp:2 * cp]
-    for dd, xx in ((dh, xh), (dh, xl), (dl, xh)):
-        wgrad_bf16(dd, xx, (co, cp, r, s), stride, padding, dst=acc)
+    d3, (_, _, lddy) = _as_rows(d3)
+    x3, (_, _, ldx) = _as_rows(x3)
+    n, _, h, w = x3.shape
+    _, _, oh, ow = d3.shape
+    (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
+    L = _lib.lib()
+    tbm = 32 if co <= 32 else 64 if co <= 64 else 128  # csrc/conv.hip wgrad tile rows
+    ntiles = -(-co // tbm) * -(-(r * s * cp) // 128)
+    acc = splitk_combine(
+        lambda slab, cap, sp, fc, fd, ff: L.tony_conv_wgrad_x3(
+            d3.data_ptr(), lddy, x3.data_ptr(), n, h, w, cp, ldx, co, r, s, sh, sw, ph, pw, oh, ow, co, cp, slab, cap,
+            sp, wgrad_cus(dev, 1), _lib.stream_ptr(dev)),
+        co * r * s * cp, ntiles, dev, None, 1, pairs=3)
     dw = acc.view(co, r, s, cp)
     if cp != c:
         dw = dw[..., :c].contiguous()
@@ -185,14 +195,21 @@ def bn_apply(z: torch.Tensor, stats, gamma, beta, rmean, rvar, eps, momentum, re
     return y, mean, invstd
 
 
-def bn_backward(z, dy, mean, invstd, gamma, beta, relu):
-    """(dZ, dgamma, dbeta) of y = act(BN(z)) on fp32 rows."""
+def bn_backward(z, dy, mean, invstd, gamma, beta, relu, planes: bool = False):
+    """(dZ, dgamma, dbeta) of y = act(BN(z)) on fp32 rows; ``planes``: dZ comes back as its x3 planes
+    (bf16 channels_last [N, 3Co, OH, OW], split_act's layout) written by the apply kernel itself --
+    the fp32 dZ and a split pass over it are never made (Co is a multiple of 8, so cp = Co)."""
     n, co, oh, ow = z.shape
     m = n * oh * ow
     dy, (_, _, lddy) = _as_rows(dy)
     dev = z.device
     sums = torch.zeros(_lib.stat_floats(co), dtype=_F32, device=dev)
-    dz = _cl(n, co, oh, ow, dev)
+    if planes and co % 8 == 0:
+        dz = _cl(n, 3 * co, oh, ow, dev, _BF16)
+        apply, ldo = L_apply_x3, 3 * co
+    else:
+        dz = _cl(n, co, oh, ow, dev)
+        apply, ldo = None, co
     dgamma = torch.empty(co, dtype=_F32, device=dev)
     dbeta = torch.empty(co, dtype=_F32, device=dev)
     L, st = _lib.lib(), _lib.stream_ptr(dev)
@@ -200,11 +217,15 @@ def bn_backward(z, dy, mean, invstd, gamma, beta, relu):
                                   gamma.data_ptr(), beta.data_ptr(), 0, int(relu), sums.data_ptr(),
                                   sums.data_ptr() + 4 * co, 2 * co, st)
     _lib.check(rc, "tony_bn_bwd_reduce_f32")
-    rc = L.tony_bn_bwd_apply_f32(z.data_ptr(), co, dy.data_ptr(), lddy, dz.data_ptr(), co, m, co, mean.data_ptr(),
-                                 invstd.data_ptr(), gamma.data_ptr(), beta.data_ptr(), 0, int(relu), sums.data_ptr(),
-                                 sums.data_ptr() + 4 * co, 2 * co, dgamma.data_ptr(), dbeta.data_ptr(), 0, st)
+    fn = L.tony_bn_bwd_apply_f32_x3 if apply is not None else L.tony_bn_bwd_apply_f32
+    rc = fn(z.data_ptr(), co, dy.data_ptr(), lddy, dz.data_ptr(), ldo, m, co, mean.data_ptr(), invstd.data_ptr(),
+            gamma.data_ptr(), beta.data_ptr(), 0, int(relu), sums.data_ptr(), sums.data_ptr() + 4 * co, 2 * co,
+            dgamma.data_ptr(), dbeta.data_ptr(), 0, st)
     _lib.check(rc, "tony_bn_bwd_apply_f32")
     return dz, dgamma, dbeta
+
+
+L_apply_x3 = "tony_bn_bwd_apply_f32_x3"
 
 
 class _ConvBNActX3Fn(torch.autograd.Function):
@@ -224,8 +245,9 @@ class _ConvBNActX3Fn(torch.autograd.Function):
     def backward(ctx, dy):
         x3, weight, gamma, beta, z, mean, invstd = ctx.saved_tensors
         cp, x_shape, stride, padding, relu, need_dx = ctx.conf
-        dz, dgamma, dbeta = bn_backward(z, dy, mean, invstd, gamma, beta, relu)
-        d3, _ = split_act(dz)
+        d3, dgamma, dbeta = bn_backward(z, dy, mean, invstd, gamma, beta, relu, planes=True)
+        if d3.dtype == _F32:  # Co not a multiple of 8: fp32 dZ, split here
+            d3, _ = split_act(d3)
         dw = conv_wgrad(d3, x3, cp, weight.shape, stride, padding)
         dx = None
         if need_dx and ctx.needs_input_grad[0]:

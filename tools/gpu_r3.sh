@@ -21,6 +21,9 @@ for s in "$@"; do
     bench_graph) step bench_graph 400 env TONY_REPLAY=graph python bench.py --steps 20 --warmup 6 --mode graph ;;
     x3) step x3_tests 400 python -u -m pytest tests/test_x3_gpu.py -x -v --timeout 240 --timeout-method thread ;;
     bench_fp32) step bench_fp32 600 python bench.py --steps 10 --warmup 3 --dtype fp32 --mode eager ;;
+    bench_fp32_auto) step bench_fp32_auto 600 python bench.py --steps 10 --warmup 3 --dtype fp32 ;;
+    # alternating A/B of the opt-in environment toggles against the default step (tools/ab_r3.py)
+    ab) step ab 1000 python tools/ab_r3.py --reps 2 onepass16=TONY_BN_ONEPASS=1,TONY_BN_ONEPASS_MAX_MB=16 fused_red=TONY_BN_FUSED_REDUCE=1 pool_bnred=TONY_POOL_BNRED=1 occ2=TONY_WGRAD_OCC=2 nobranch=TONY_BRANCH_STREAMS=0 wbatch1=TONY_WGRAD_BATCH=1 ;;
     tests) step gpu_suite 800 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread ;;
     bench) step bench 400 python bench.py --steps 20 --warmup 6 ;;
     bench_r50) step bench_r50 400 python bench.py --model resnet50 --steps 20 --warmup 6 ;;
