@@ -883,9 +883,9 @@ struct IncRows {
 };
 
 // x3 (fp32) weight gradients: the three bf16 plane products dW = dYh^T Xh + dYh^T Xl + dYl^T Xh of
-// ops/x3.py as ONE split-K launch.  The splits come in npairs groups of sp; group q reads dY and X at
-// the element offsets dy_off[q] / x_off[q] (the plane's first channel) and stores its partials into
-// slab splits q * sp .. q * sp + sp - 1, so one tony_splitk_reduce sums all three products.
+// ops/x3.py as ONE split-K launch.  Split s covers rows (s / npairs) * rows_per_split.. of plane pair
+// q = s % npairs, reading dY and X at the element offsets dy_off[q] / x_off[q] (the plane's first
+// channel), and stores its partials into slab split s, so one tony_splitk_reduce sums all three.
 // npairs = 1, offsets 0: the plain wgrad.
 struct PlanePairs {
   int npairs, sp;
@@ -906,12 +906,16 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 2 * TILE];
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int tile = wg % ntiles, split = wg / ntiles;
-  const int pair = split / pp.sp;  // wave-uniform: selects, no dynamic index into the argument array
+  // the pairs of one row range are neighbours in the grid (pair = split % npairs), so the workgroups
+  // running together read the same dY / X rows (dYh is shared by pairs 0 and 1, Xh by 0 and 2) out of
+  // L2 instead of three planes' worth of distinct rows (the stem's 177 MB planes thrashed it: 577 vs
+  // 3 x 111 us as three launches).  Wave-uniform selects, no dynamic index into the argument array.
+  const int pair = split % pp.npairs;
   dY += pair == 0 ? pp.dy_off[0] : pair == 1 ? pp.dy_off[1] : pp.dy_off[2];
   g.src += pair == 0 ? pp.x_off[0] : pair == 1 ? pp.x_off[1] : pp.x_off[2];
   const int t1 = tile / tiles_n2, t2 = tile % tiles_n2;
   const int n1_0 = t1 * TBM, n2_0 = t2 * WTBN;
-  const int64_t m_begin = static_cast<int64_t>(split - pair * pp.sp) * rows_per_split;
+  const int64_t m_begin = static_cast<int64_t>(split / pp.npairs) * rows_per_split;
   const int64_t m_end = min(M, m_begin + rows_per_split);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -1081,12 +1085,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
   __shared__ __attribute__((aligned(16))) uint16_t smem[kWgStages * STAGE];
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int tile = wg % ntiles, split = wg / ntiles;
-  const int pair = split / pp.sp;  // wave-uniform: selects, no dynamic index into the argument array
+  // the pairs of one row range are neighbours in the grid (pair = split % npairs), so the workgroups
+  // running together read the same dY / X rows (dYh is shared by pairs 0 and 1, Xh by 0 and 2) out of
+  // L2 instead of three planes' worth of distinct rows (the stem's 177 MB planes thrashed it: 577 vs
+  // 3 x 111 us as three launches).  Wave-uniform selects, no dynamic index into the argument array.
+  const int pair = split % pp.npairs;
   dY += pair == 0 ? pp.dy_off[0] : pair == 1 ? pp.dy_off[1] : pp.dy_off[2];
   g.src += pair == 0 ? pp.x_off[0] : pair == 1 ? pp.x_off[1] : pp.x_off[2];
   const int t1 = tile / tiles_n2, t2 = tile % tiles_n2;
   const int n1_0 = t1 * TBM, n2_0 = t2 * WTBN;
-  const int64_t m_begin = static_cast<int64_t>(split - pair * pp.sp) * rows_per_split;
+  const int64_t m_begin = static_cast<int64_t>(split / pp.npairs) * rows_per_split;
   const int64_t m_end = min(M, m_begin + rows_per_split);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -1430,7 +1438,7 @@ int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, float
   WkStep ws{};
   const bool inc = wgrad_inc_step(g, M, &ws);
   const auto* dyp = static_cast<const uint16_t*>(dy);
-  if (TBM == 128 && slab != nullptr && wgrad_glds_enabled()) {
+  if (TBM >= 96 && slab != nullptr && wgrad_glds_enabled()) {
     if (inc)
       conv_wgrad_glds_kernel<TBM, true><<<static_cast<int>(grid), kThreads, 0, stream>>>(
           dyp, lddy, g, M, Co, tiles_n2, ntiles, rows, slab, fold, ws, pp);
@@ -1446,6 +1454,19 @@ int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, float
   }
   TONY_LAUNCH_CHECK();
   return 0;
+}
+
+// Cout tile rows of the split-K wgrad: 32 / 64 for thin layers; above, 96 where it pads Cout less than
+// 128 does (Inception's 160 / 192 / 288 / 448-channel layers: 25-37% of the 128-row tiles' MFMA rows
+// were zero padding at 160 / 192), else 128.  TONY_WGRAD_TBM96=0: always 128 (A/B).
+int wgrad_tbm(int Co) {
+  static const bool t96 = [] {
+    const char* e = getenv("TONY_WGRAD_TBM96");
+    return e == nullptr || e[0] != '0';
+  }();
+  if (Co <= 32) return 32;
+  if (Co <= 64) return 64;
+  return t96 && ceil_div(Co, 96) * 96 < ceil_div(Co, 128) * 128 ? 96 : 128;
 }
 
 bool bad_geom(int C, int64_t ld, const void* p) {
@@ -1571,9 +1592,12 @@ TONY_API int tony_conv_wgrad(const void* dy, int64_t lddy, const void* x, int N,
                                    (reinterpret_cast<uintptr_t>(fold_dst) & 7)))
     return -1;
   const SplitFold fold{fold_counters, fold_dst, fold_flags};
-  if (Co <= 32) return launch_wgrad<32>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream);
-  if (Co <= 64) return launch_wgrad<64>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream);
-  return launch_wgrad<128>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream);
+  switch (wgrad_tbm(Co)) {
+    case 32: return launch_wgrad<32>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream);
+    case 64: return launch_wgrad<64>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream);
+    case 96: return launch_wgrad<96>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream);
+    default: return launch_wgrad<128>(dy, lddy, g, dw, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream);
+  }
 }
 
 // x3 weight gradient (ops/x3.py conv_wgrad): dy / x point at the hi planes (channel 0) of the dY and X
@@ -1594,9 +1618,12 @@ TONY_API int tony_conv_wgrad_x3(const void* dy, int64_t lddy, const void* x, int
   Gather g{static_cast<const uint16_t*>(x), ldx, H, W, C, OH, OW, R, S, sh, sw, -ph, -pw, 1, K, 0};
   const SplitFold fold{nullptr, nullptr, 0};
   const PlanePairs pp{3, 1, {0, 0, dplane}, {0, xplane, 0}};
-  if (Co <= 32) return launch_wgrad<32>(dy, lddy, g, nullptr, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream, pp);
-  if (Co <= 64) return launch_wgrad<64>(dy, lddy, g, nullptr, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream, pp);
-  return launch_wgrad<128>(dy, lddy, g, nullptr, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream, pp);
+  switch (wgrad_tbm(Co)) {
+    case 32: return launch_wgrad<32>(dy, lddy, g, nullptr, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream, pp);
+    case 64: return launch_wgrad<64>(dy, lddy, g, nullptr, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream, pp);
+    case 96: return launch_wgrad<96>(dy, lddy, g, nullptr, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream, pp);
+    default: return launch_wgrad<128>(dy, lddy, g, nullptr, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream, pp);
+  }
 }
 
 // dW (fp32 partials, [grid][Co][3][3][C]) of a 3x3 stride-1 conv with C, Co in {32, 64} by the

@@ -24,7 +24,7 @@ from typing import Tuple
 
 import torch
 
-from . import _lib, tune
+from . import _lib, streams, tune
 from .bn import _as_rows
 
 ACT = 0b010  # activation / gradient planes: [hi | lo | hi]
@@ -54,13 +54,23 @@ def split_rows(src: torch.Tensor, rows: int, c: int, ld: int, pattern: int) -> t
 
 def split_act(x: torch.Tensor) -> Tuple[torch.Tensor, int]:
     """fp32 NHWC activation (channels_last 4D, a channel slice of one, or [M, C]) -> bf16 planes as a
-    channels_last [N, 3cp, H, W] tensor (2D input: [M, 3cp]); also returns cp."""
+    channels_last [N, 3cp, H, W] tensor (2D input: [M, 3cp]); also returns cp.  The planes are kept on
+    ``x`` (keyed by its version counter): an Inception block input feeds 3-4 branch heads, which then
+    share one split of it instead of making one each."""
+    hit = getattr(x, "_tony_x3", None)
+    if hit is not None and hit[0] == x._version:
+        return hit[1], hit[2]
+    src = x
     x, (m, c, ld) = _rows4(x)
     out = split_rows(x, m, c, ld, ACT)
     cp = cp_of(c)
     if x.dim() == 4:
         n, _, h, w = x.shape
         out = out.view(n, h, w, 3 * cp).permute(0, 3, 1, 2)
+    # only activations made inside the step (grad_fn set): a persistent input -- the trainer's static
+    # batch, refilled by copy_ between replays of a captured step -- must be split inside the capture
+    if x is src and src.grad_fn is not None:
+        src._tony_x3 = (src._version, out, cp)
     return out, cp
 
 
@@ -148,11 +158,13 @@ def conv_dgrad(d3: torch.Tensor, wt3: torch.Tensor, co: int, x_shape, wshape, st
     return dx
 
 
-def conv_wgrad(d3: torch.Tensor, x3: torch.Tensor, cp: int, wshape, stride, padding) -> torch.Tensor:
+def conv_wgrad(d3: torch.Tensor, x3: torch.Tensor, cp: int, wshape, stride, padding, dst=None):
     """fp32 dW [Co, C, R, S] (channels_last memory [Co][R][S][C]) = the three plane products
     hi_d*hi_x + hi_d*lo_x + lo_d*hi_x: ONE split-K wgrad launch whose splits come in three plane-pair
     groups (csrc/conv.hip tony_conv_wgrad_x3) and one combine of all their partials -- not three
-    launches, three combines and an fp32 accumulator fill (profiles/r3s2_fp32_x3_steady.md)."""
+    launches, three combines and an fp32 accumulator fill (profiles/r3s2_fp32_x3_steady.md).
+    ``dst``: an fp32 gradient slot in [Co][R][S][C] memory (C a multiple of 8) that the combine adds
+    dW into; returns None then."""
     from .gemm import splitk_combine, wgrad_cus
 
     co, c, r, s = wshape
@@ -169,11 +181,17 @@ def conv_wgrad(d3: torch.Tensor, x3: torch.Tensor, cp: int, wshape, stride, padd
         lambda slab, cap, sp, fc, fd, ff: L.tony_conv_wgrad_x3(
             d3.data_ptr(), lddy, x3.data_ptr(), n, h, w, cp, ldx, co, r, s, sh, sw, ph, pw, oh, ow, co, cp, slab, cap,
             sp, wgrad_cus(dev, 1), _lib.stream_ptr(dev)),
-        co * r * s * cp, ntiles, dev, None, 1, pairs=3)
+        co * r * s * cp, ntiles, dev, dst if cp == c else None, 1, pairs=3)
+    if acc is None:
+        return None
     dw = acc.view(co, r, s, cp)
     if cp != c:
         dw = dw[..., :c].contiguous()
-    return dw.permute(0, 3, 1, 2)
+    dw = dw.permute(0, 3, 1, 2)
+    if dst is not None:  # the stem's padded planes: add the unpadded dW into the slot
+        dst.add_(dw)
+        return None
+    return dw
 
 
 # ---- BatchNorm on fp32 rows -------------------------------------------------------------------------
@@ -195,10 +213,11 @@ def bn_apply(z: torch.Tensor, stats, gamma, beta, rmean, rvar, eps, momentum, re
     return y, mean, invstd
 
 
-def bn_backward(z, dy, mean, invstd, gamma, beta, relu, planes: bool = False):
+def bn_backward(z, dy, mean, invstd, gamma, beta, relu, planes: bool = False, dgamma=None, dbeta=None):
     """(dZ, dgamma, dbeta) of y = act(BN(z)) on fp32 rows; ``planes``: dZ comes back as its x3 planes
     (bf16 channels_last [N, 3Co, OH, OW], split_act's layout) written by the apply kernel itself --
-    the fp32 dZ and a split pass over it are never made (Co is a multiple of 8, so cp = Co)."""
+    the fp32 dZ and a split pass over it are never made (Co is a multiple of 8, so cp = Co).
+    ``dgamma`` / ``dbeta``: fp32 gradient slots the kernel adds into (returned as None then)."""
     n, co, oh, ow = z.shape
     m = n * oh * ow
     dy, (_, _, lddy) = _as_rows(dy)
@@ -210,8 +229,10 @@ def bn_backward(z, dy, mean, invstd, gamma, beta, relu, planes: bool = False):
     else:
         dz = _cl(n, co, oh, ow, dev)
         apply, ldo = None, co
-    dgamma = torch.empty(co, dtype=_F32, device=dev)
-    dbeta = torch.empty(co, dtype=_F32, device=dev)
+    slots = dgamma is not None and dbeta is not None
+    if not slots:
+        dgamma = torch.empty(co, dtype=_F32, device=dev)
+        dbeta = torch.empty(co, dtype=_F32, device=dev)
     L, st = _lib.lib(), _lib.stream_ptr(dev)
     rc = L.tony_bn_bwd_reduce_f32(z.data_ptr(), co, dy.data_ptr(), lddy, m, co, mean.data_ptr(), invstd.data_ptr(),
                                   gamma.data_ptr(), beta.data_ptr(), 0, int(relu), sums.data_ptr(),
@@ -220,9 +241,9 @@ def bn_backward(z, dy, mean, invstd, gamma, beta, relu, planes: bool = False):
     fn = L.tony_bn_bwd_apply_f32_x3 if apply is not None else L.tony_bn_bwd_apply_f32
     rc = fn(z.data_ptr(), co, dy.data_ptr(), lddy, dz.data_ptr(), ldo, m, co, mean.data_ptr(), invstd.data_ptr(),
             gamma.data_ptr(), beta.data_ptr(), 0, int(relu), sums.data_ptr(), sums.data_ptr() + 4 * co, 2 * co,
-            dgamma.data_ptr(), dbeta.data_ptr(), 0, st)
+            dgamma.data_ptr(), dbeta.data_ptr(), int(slots), st)
     _lib.check(rc, "tony_bn_bwd_apply_f32")
-    return dz, dgamma, dbeta
+    return (dz, None, None) if slots else (dz, dgamma, dbeta)
 
 
 L_apply_x3 = "tony_bn_bwd_apply_f32_x3"
@@ -245,13 +266,25 @@ class _ConvBNActX3Fn(torch.autograd.Function):
     def backward(ctx, dy):
         x3, weight, gamma, beta, z, mean, invstd = ctx.saved_tensors
         cp, x_shape, stride, padding, relu, need_dx = ctx.conf
-        d3, dgamma, dbeta = bn_backward(z, dy, mean, invstd, gamma, beta, relu, planes=True)
+        # in-place gradient slots (the trainer's flat fp32 gradients): BN's dgamma / dbeta are added by
+        # the apply kernel, dW by the wgrad combine -- on the weight-gradient side stream when one is
+        # active (ops/streams.py), overlapped with the data-gradient chain as in the bf16 step
+        gw, gg, gb = _lib.grad_slot(weight), _lib.grad_slot(gamma), _lib.grad_slot(beta)
+        gw = gw if gw is not None and gw.dtype == _F32 and gw.is_contiguous(memory_format=torch.channels_last) \
+            else None
+        bn_slots = gg is not None and gb is not None and gg.dtype == _F32 and gb.dtype == _F32
+        d3, dgamma, dbeta = bn_backward(z, dy, mean, invstd, gamma, beta, relu, planes=True,
+                                        dgamma=gg if bn_slots else None, dbeta=gb if bn_slots else None)
         if d3.dtype == _F32:  # Co not a multiple of 8: fp32 dZ, split here
             d3, _ = split_act(d3)
-        dw = conv_wgrad(d3, x3, cp, weight.shape, stride, padding)
+        if gw is not None:
+            dw = streams.run(lambda: conv_wgrad(d3, x3, cp, weight.shape, stride, padding, dst=gw), d3, x3)
+        else:
+            dw = conv_wgrad(d3, x3, cp, weight.shape, stride, padding)
         dx = None
         if need_dx and ctx.needs_input_grad[0]:
             dx = conv_dgrad(d3, split_weight_t(weight), weight.shape[0], x_shape, weight.shape, stride, padding)
+        _lib.report_inplace((weight, gamma, beta), (dw, dgamma, dbeta))
         return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None
 
 

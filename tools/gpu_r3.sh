@@ -38,6 +38,7 @@ for s in "$@"; do
     # 2 colocated ranks on the box's one GPU (gloo): --mode auto now also times the native plan with
     # per-bucket segments at N > 1; bench2_plan forces it (and the xGMI kernels for the buckets)
     bench2_auto) step bench2_auto 600 env TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29523 bench.py --gpus 2 --steps 6 --warmup 3 --batch 32 ;;
+    bench2_plan_gloo) step bench2_plan_gloo 600 env TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29525 bench.py --gpus 2 --steps 6 --warmup 3 --batch 32 --mode graph ;;
     bench2_plan) step bench2_plan 600 env TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29524 bench.py --gpus 2 --steps 6 --warmup 3 --batch 32 --mode graph --collective hip ;;
     # the same topology through the launcher (bin/tony: coordinator -> task agents -> TF_CONFIG)
     ps_job) step ps_job 600 bash bin/tony --src_dir tony_amd/jobs --executes inception_ps.py \
