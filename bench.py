@@ -21,8 +21,9 @@ One process per GPU (torch.distributed.run, RCCL over xGMI).  Two PS topologies:
 Compute is bf16 NHWC with the tony_amd HIP kernels (fused BN+ReLU, MFMA implicit-GEMM convs, fused
 heads, fused softmax-xent, fused optimizer); the step is issued eagerly (weight gradients on a side
 stream) or replayed as a HIP graph, whichever measured faster in setup (``--mode auto``).
-``--dtype fp32`` runs the reference-precision row (TF's Inception-v3 PS job is fp32): stock
-PyTorch-ROCm layers (MIOpen / hipBLASLt) in fp32 with fp32 variables and fp32 pushed gradients.
+``--dtype fp32`` runs the reference-precision row (TF's Inception-v3 PS job is fp32): fp32
+activations, variables and pushed gradients, each conv / GEMM product as an x3 split over the bf16
+MFMA kernels (ops/x3.py); ``--stock --dtype fp32``: the stock MIOpen / hipBLASLt fp32 comparator.
 ``--grad-dtype fp32`` keeps bf16 compute but pushes and sums fp32 gradients.
 
 Data is synthetic (ImageNet-shaped 299x299x3 images, random labels) and weights are random-init --
@@ -56,7 +57,7 @@ def parse():
     ap.add_argument("--ps-mode", default="colocated", choices=["colocated", "dedicated"],
                     help="colocated: one PS shard per GPU; dedicated: rank 0 = the ps task, the rest are workers")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
-                    help="compute dtype; fp32 = the reference-precision row (stock layers, fp32 variables)")
+                    help="compute dtype; fp32 = the reference-precision row (x3-split MFMA products, fp32 variables)")
     ap.add_argument("--grad-dtype", default=None, choices=["bf16", "fp32"],
                     help="dtype of the pushed / summed gradients (default: the compute dtype)")
     ap.add_argument("--bucket-mb", type=float, default=None, help="gradient bucket size (default 8 MB)")

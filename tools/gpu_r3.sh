@@ -22,6 +22,10 @@ for s in "$@"; do
     x3) step x3_tests 400 python -u -m pytest tests/test_x3_gpu.py -x -v --timeout 240 --timeout-method thread ;;
     bench_fp32) step bench_fp32 600 python bench.py --steps 10 --warmup 3 --dtype fp32 --mode eager ;;
     bench_fp32_auto) step bench_fp32_auto 600 python bench.py --steps 10 --warmup 3 --dtype fp32 ;;
+    conv_tests) step conv_tests 400 python -u -m pytest tests/test_conv_gpu.py tests/test_x3_gpu.py -x -q --timeout 240 --timeout-method thread ;;
+    tbm) step tbm_diag 400 bash tools/diag/wgrad_tbm.sh ;;
+    ab_tbm) step ab_tbm 600 python tools/ab_r3.py --reps 3 tbm128=TONY_WGRAD_TBM96=0 ;;
+    ab_tbm_fp32) step ab_tbm_fp32 600 python tools/ab_r3.py --reps 2 --steps 10 --bench-args "--dtype fp32" tbm128=TONY_WGRAD_TBM96=0 ;;
     # alternating A/B of the opt-in environment toggles against the default step (tools/ab_r3.py)
     ab) step ab 1000 python tools/ab_r3.py --reps 2 onepass16=TONY_BN_ONEPASS=1,TONY_BN_ONEPASS_MAX_MB=16 fused_red=TONY_BN_FUSED_REDUCE=1 pool_bnred=TONY_POOL_BNRED=1 occ2=TONY_WGRAD_OCC=2 nobranch=TONY_BRANCH_STREAMS=0 wbatch1=TONY_WGRAD_BATCH=1 ;;
     tests) step gpu_suite 800 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread ;;
