@@ -262,12 +262,12 @@ def main():
     if args.tune_cache and os.path.exists(args.tune_cache):
         tune_loaded = tune.load(args.tune_cache)
     mode = "eager" if args.no_graph else args.mode
-    if mode == "auto" and world > 1:
+    if mode == "auto" and world > 1 and os.environ.get("TONY_BENCH_AUTO_PLAN", "0") != "1":
         # several ranks: the eager step overlaps the bucketed PS push / apply / pull with backward.  The
         # native plan can too (per-bucket plan segments, parallel/trainer.py _replay_overlapped), but its
         # 2-rank rehearsal failed to replay (tony_plan_replay: hipErrorInvalidValue on one rank,
         # profiles/r3s2_bench2_auto_plan_replay_fail.log), so auto keeps to eager at N > 1 until it is
-        # fixed; --mode graph still selects it
+        # fixed; --mode graph still selects it (TONY_BENCH_AUTO_PLAN=1: time both, for rehearsals)
         mode = "eager"
     if ps.is_worker:
         trainer = Trainer(model, ps, loss_fn, use_graph=mode != "eager", overlap_wgrad=not args.no_wgrad_stream,
