@@ -1,0 +1,41 @@
+"""ResNet identity blocks: conv1's dgrad adds its dX into the identity path's gradient in its
+epilogue (ops/residual.py GradJoin, csrc/mfma_common.h nt_epilogue accum) instead of autograd's add
+kernel -- the block input gradient must match the unjoined graph's (to bf16 rounding: the BN
+statistics are summed with atomics, so two runs may differ in the last bit; a lost contribution
+of either consumer is off by far more)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+@pytest.mark.parametrize("shape", [(4, 256, 14, 14), (2, 512, 7, 9)])
+def test_identity_block_join_matches_autograd_sum(cuda, shape, monkeypatch):
+    from tony_amd.models import resnet
+    from tony_amd.models.layers import cast_model, init_weights
+
+    n, c, h, w = shape
+    torch.manual_seed(0)
+    blk = cast_model(init_weights(resnet.Bottleneck(c, c // 4), 5), torch.bfloat16, cuda)
+    blk = blk.to(memory_format=torch.channels_last).train()
+    torch.nn.init.constant_(blk.bn3.weight, 0.5)  # non-degenerate residual branch
+    x0 = _cl(torch.randn(n, c, h, w, device=cuda)).to(torch.bfloat16)
+    g = _cl(torch.randn(n, c, h, w, device=cuda)).to(torch.bfloat16)
+    grads = {}
+    for join in (False, True):
+        monkeypatch.setattr(resnet, "JOIN", join)
+        blk.zero_grad(set_to_none=True)
+        x = (x0 * 1).requires_grad_(True)  # a non-leaf copy per run (the join rides on the tensor)
+        x.retain_grad()
+        y = blk(x)
+        y.backward(g)
+        grads[join] = (x.grad.float().clone(), [p.grad.float().clone() for p in blk.parameters()])
+    torch.testing.assert_close(grads[True][0], grads[False][0], rtol=1e-2, atol=1e-2)
+    # parameter gradients by norm: between two runs a pre-activation within the atomically summed BN
+    # statistics' last bit of 0 may take the other side of a ReLU and move single dW elements
+    for a, b in zip(grads[True][1], grads[False][1]):
+        assert ((a - b).norm() / b.norm().clamp_min(1e-12)).item() < 2e-2

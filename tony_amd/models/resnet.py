@@ -19,14 +19,20 @@ module graph (the comparator and the CPU path).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 
 from ..ops.bn import BatchNormAct2d
 from ..ops.linear import Linear
 from ..ops.pool import global_avg_pool
-from ..ops.residual import bn_add_relu, conv1x1_bn_add_relu
+from ..ops.residual import GradJoin, bn_add_relu, conv1x1_bn_add_relu
 from .layers import ConvBNAct, conv_bn_act_maxpool, init_weights
+
+
+# TONY_RESNET_JOIN=0: let autograd sum the identity-block input gradients (A/B)
+JOIN = os.environ.get("TONY_RESNET_JOIN", "1") != "0"
 
 
 class Bottleneck(nn.Module):
@@ -47,6 +53,9 @@ class Bottleneck(nn.Module):
                 BatchNormAct2d(cout, eps=eps, relu=False) if fused else nn.BatchNorm2d(cout, eps=eps))
 
     def forward(self, x):
+        if self.fused and self.downsample is None and x.is_cuda and JOIN and torch.is_grad_enabled():
+            # x feeds conv1 and the identity add: their gradients meet in one tensor (GradJoin), no add
+            x._tony_join = GradJoin()
         identity = self.downsample(x) if self.downsample is not None else x
         out = self.conv2(self.conv1(x))
         bn = self.bn3

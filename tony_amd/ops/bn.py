@@ -74,6 +74,14 @@ def _as_rows(t: torch.Tensor):
     return t, rv
 
 
+def _accum_ok(t: torch.Tensor, x_shape) -> bool:
+    """``t`` can take a dgrad epilogue's accumulating store: bf16, x's shape, dense channels_last rows."""
+    if t.dtype != torch.bfloat16 or tuple(t.shape) != tuple(x_shape) or t.data_ptr() % 16:
+        return False
+    rv = _rows_view(t)
+    return rv is not None and rv[2] == t.shape[1]
+
+
 def _empty_like_rows(x: torch.Tensor) -> torch.Tensor:
     if x.dim() == 4:
         return torch.empty(x.shape, dtype=x.dtype, device=x.device, memory_format=torch.channels_last)

@@ -28,7 +28,7 @@ import torch
 
 from . import _lib, concat, streams, tape, tune, wt_cache
 from .arena import zeros_f32
-from .bn import HOST_MEMO, _as_rows, _rows_view
+from .bn import HOST_MEMO, _accum_ok, _as_rows, _rows_view
 from .gemm import WGRAD_OCC, splitk_combine, wgrad_cus, wgrad_tn
 
 _BF16 = torch.bfloat16
@@ -225,11 +225,14 @@ def dgrad_supported(x_shape, weight: torch.Tensor, stride=1, padding=0) -> bool:
 
 
 def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, padding=0,
-               vflags: int | None = None, bnr: "_lib.BnRed | None" = None) -> torch.Tensor:
+               vflags: int | None = None, bnr: "_lib.BnRed | None" = None,
+               accum: torch.Tensor | None = None) -> torch.Tensor:
     """dX of conv(x, w): stride 1 is one implicit-GEMM transposed conv; a strided conv is one
     launch per residue class of dX (csrc/conv.hip tony_conv_dgrad_strided, no MIOpen).  With ``bnr``
     the epilogue also accumulates the BN-backward reduction of the layer whose output x is
-    (``bnr.done`` tells whether the chosen kernel did)."""
+    (``bnr.done`` tells whether the chosen kernel did).  ``accum``: a bf16 channels_last gradient of
+    x's shape (dense rows) that dX is added into by the epilogue (flag bit 4) and returned -- the
+    separate add kernel of a tensor with two consumers (ResNet's identity path, ops/residual.py)."""
     if not dgrad_supported(x_shape, weight, stride, padding):
         raise ValueError(f"conv_dgrad: unsupported x={tuple(x_shape)} w={tuple(weight.shape)} stride={stride} "
                          f"padding={padding}")
@@ -258,8 +261,24 @@ def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, paddin
     # variants are timed without the fused reduction (it must run exactly once)
     vf = vflags if vflags is not None else tune.pick(("conv_dgrad", tuple(dy.shape), lddy, tuple(weight.shape),
                                                          (sh, sw), (ph, pw)), launch)
+    if accum is not None and bnr is None and (sh, sw) == (1, 1) and _accum_ok(accum, x_shape):
+        plain = dx
+        dx = accum
+        rc = launch(vf | 16)
+        if rc == 0:
+            return dx
+        if rc != -3:  # -3: the chosen tile variant has its own epilogue (halo / direct): add after
+            _lib.check(rc, name)
+        dx = plain
+        _lib.check(launch(vf), name)
+        accum.add_(dx)
+        return accum
     _lib.check(launch(vf, bnr), name)
+    if accum is not None:
+        accum.add_(dx)
+        return accum
     return dx
+
 
 
 class BnCtx:
@@ -511,7 +530,13 @@ def _fwd(x, weight, stride, padding, stats):
         _miopen_fwd(x, weight, stride, padding, stats)
 
 
-def _dgrad(dy, weight, x_shape, stride, padding, bnr=None):
+def _dgrad(dy, weight, x_shape, stride, padding, bnr=None, accum=None):
+    """dX (``accum``: added into that gradient and returned, see conv_dgrad)."""
+    if accum is not None:
+        impl = _CHOICE.get(("dgrad", tuple(dy.shape), tuple(weight.shape), stride, padding))
+        if impl == "tony":
+            return conv_dgrad(dy, weight, x_shape, stride, padding, accum=accum)
+        return accum.add_(_dgrad(dy, weight, x_shape, stride, padding))
     key = ("dgrad", tuple(dy.shape), tuple(weight.shape), stride, padding)
     if fullcover(x_shape, weight.shape, stride, padding):
         _CHOICE.setdefault(key, "gemm")
@@ -655,6 +680,7 @@ class _ConvBNActFn(torch.autograd.Function):
         ctx.params = (weight, gamma, beta)
         ctx.cfg = (stride, padding, relu, pb)
         ctx.bnc_in = getattr(x, "_tony_bnr", None)
+        ctx.join = getattr(x, "_tony_join", None)  # ops/residual.py GradJoin: x has a second consumer
         ctx.bnc_self = None
         if training and slot is None:  # a consumer conv's dgrad may reduce this layer's BN backward
             ctx.bnc_self = BnCtx(Z, ldz, mean, invstd, gamma, beta, pb, relu)
@@ -688,7 +714,13 @@ def _conv_bn_backward(ctx, x, weight, gamma, beta, mean, invstd, Z, dy, presums=
     _lib.bn_bwd(Z, ldz, dy, lddy, dZ, ldz, M, co, mean, invstd, gamma, beta, pb, relu, ws, dgamma, dbeta, inplace,
                 dev, sums=presums)
     dw = _wgrad(dZ, x, weight, stride, padding)  # first: overlaps the dgrad on the side stream
-    dx = _dgrad_fused_bn(ctx, dZ, weight, x.shape, stride, padding) if ctx.needs_input_grad[0] else None
+    join = getattr(ctx, "join", None)
+    pend = join.take() if join is not None else None
+    if pend is not None and ctx.needs_input_grad[0]:
+        # x's other consumer (the identity path) already wrote its gradient: dX is added into it
+        dx = _dgrad(dZ, weight, x.shape, stride, padding, accum=pend)
+    else:
+        dx = _dgrad_fused_bn(ctx, dZ, weight, x.shape, stride, padding) if ctx.needs_input_grad[0] else None
     streams.keep(dx)  # may be consumed on another (branch) stream
     if inplace:
         dgamma = dbeta = None

@@ -275,7 +275,8 @@ __global__ __launch_bounds__(kThreads) void conv_nt_kernel(Gather g, const uint1
   // inference BN (H5), bit2: ReLU after it
   nt_epilogue<BM, BN, TM, TN>(acc, smem, C, ldc, M, N, m0, n0,
                                (epi & 1) ? stats + shard_off(tm, sstride) : nullptr,
-                               (epi & 2) ? stats : nullptr, (epi & 4) != 0, PH ? ph.rows : RowMap{}, (epi & 8) != 0);
+                               (epi & 2) ? stats : nullptr, (epi & 4) != 0, PH ? ph.rows : RowMap{}, (epi & 8) != 0,
+                               (epi & 16) != 0);
   if (ph.bnr.z != nullptr) {  // uniform: the C tile is still in LDS, the fold area lies behind it
     constexpr int CS_ELEMS = (BM * (BN + 8) + 7) / 8 * 8;
     static_assert(CS_ELEMS * 2 + 16 * kThreads * 4 <= 2 * (BM + BN) * BK * 2, "BN-reduce fold area fits");
@@ -757,12 +758,14 @@ int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int6
   // flags bit0: statistics accumulated into stats (the caller zeroes it, ops/arena.py);
   // bit1: stats = [scale | shift] of the folded inference BN, bit2: ReLU after it (H5)
   // bit3: fp32 output (the x3 path, ops/x3.py): only the variants whose epilogue is nt_epilogue
-  const int epi = flags & 15;
+  // bit4: C += the product (nt_epilogue's accum: a dgrad adding into a gradient already written)
+  const int epi = flags & 31;
   if ((epi & 1) && (epi & 2)) return -1;
   if ((epi & 3) && stats == nullptr) return -1;
+  if ((epi & 16) && ((epi & 3) || bph.bnr.z != nullptr)) return -1;
   float* st = stats;
   const int v = (flags >> 8) & 0xff;
-  if ((epi & 8) && (v == kHaloVariant || v == kDirectVariant)) return -3;
+  if ((epi & 24) && (v == kHaloVariant || v == kDirectVariant)) return -3;
   if (v == kHaloVariant) return bph.bnr.z != nullptr ? -3 : run_halo(g, B, C, ldc, N, epi, st, sstride, stream);
   if (v == kDirectVariant) return run_direct(g, B, C, ldc, N, epi, st, sstride, stream, bph.bnr);
   if (v >= kGldsFirst && v < kGldsFirst + kNumGlds)
@@ -1510,7 +1513,8 @@ TONY_API int tony_conv_dgrad(const void* dy, int N, int OH, int OW, int Co, int6
       bph.bnr = *bnr;
     }
   }
-  const int fl = flags & 0xff08;  // variant + fp32 output (bit3)
+  const int fl = flags & 0xff18;  // variant + fp32 output (bit3) + accumulate into dx (bit4)
+  if ((fl & 16) && bph.bnr.z != nullptr) return -1;
   const int rc = run_nt(g, wt, dx, lddx, M, C, fl, nullptr, 0, stream, bph);
   if (rc == -3 && bph.bnr.z != nullptr)  // the chosen variant has no fused reduction: plain dgrad
     return run_nt(g, wt, dx, lddx, M, C, fl, nullptr, 0, stream);

@@ -127,7 +127,7 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(const uint16_t* __res
   // inference BN (H5), bit2: ReLU after it
   nt_epilogue<BM, BN, TM, TN>(acc, smem, C, ldc, M, N, m0, n0,
                                (epi & 1) ? stats + shard_off(tm, sstride) : nullptr,
-                               (epi & 2) ? stats : nullptr, (epi & 4) != 0, RowMap{}, (epi & 8) != 0);
+                               (epi & 2) ? stats : nullptr, (epi & 4) != 0, RowMap{}, (epi & 8) != 0, (epi & 16) != 0);
 }
 
 template <int BM, int BN>
@@ -175,8 +175,9 @@ TONY_API int tony_gemm_bf16(const void* A, const void* B, void* C, int64_t M, in
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -1;
   // bit0: st is accumulated into with atomics (the caller hands it over zeroed, ops/arena.py);
   // bit1: st = [scale | shift] of the folded inference BN, bit2: ReLU after it (H5)
-  const int epi = flags & 15;  // bit3: fp32 output (nt_epilogue)
+  const int epi = flags & 31;  // bit3: fp32 output; bit4: C += the product (nt_epilogue accum)
   if ((epi & 1) && (epi & 2)) return -1;
+  if ((epi & 16) && (epi & 3)) return -1;  // no statistics / folded BN on an accumulating store
   if ((epi & 3) && stats == nullptr) return -1;
   float* st = stats;
   const int v = (flags >> 8) & 0xff;

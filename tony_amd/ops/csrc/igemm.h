@@ -312,7 +312,8 @@ __global__ __launch_bounds__(kThreads) void conv_glds_kernel(Gather g, const uin
   __syncthreads();
   nt_epilogue<BM, BN, TM, TN, ST * STAGE>(acc, smem, C, ldc, M, N, m0, n0,
                                            (epi & 1) ? stats + shard_off(tm, sstride) : nullptr,
-                                           (epi & 2) ? stats : nullptr, (epi & 4) != 0, RowMap{}, (epi & 8) != 0);
+                                           (epi & 2) ? stats : nullptr, (epi & 4) != 0, RowMap{}, (epi & 8) != 0,
+                                           (epi & 16) != 0);
 }
 
 // B rows n = [K] at row stride ldb (the conv weights [Co][R][S][Ci]: ldb = K)

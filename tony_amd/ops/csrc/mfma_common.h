@@ -179,7 +179,10 @@ template <int BM, int BN, int TM, int TN, int LDS_ELEMS = 2 * (BM + BN) * BK>
 __device__ __forceinline__ void nt_epilogue(f32x4 (&acc)[TM][TN], uint16_t* smem, uint16_t* __restrict__ C,
                                             int64_t ldc, int M, int N, int m0, int n0, float* __restrict__ stats,
                                             const float* __restrict__ aff = nullptr, bool relu = false,
-                                            const RowMap rm = RowMap{}, bool f32out = false) {
+                                            const RowMap rm = RowMap{}, bool f32out = false, bool accum = false) {
+  // accum: C += the tile (bf16: the stored bf16 tile and C's old value summed in fp32 and rounded once,
+  // as the separate add kernel it replaces did) -- a backward-data GEMM adding its dX into the gradient
+  // another consumer of the same input already wrote (ResNet's identity path, ops/residual.py)
   constexpr int WM = BM / 2, WN = BN / 2;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -225,7 +228,8 @@ __device__ __forceinline__ void nt_epilogue(f32x4 (&acc)[TM][TN], uint16_t* smem
           if (row >= M || col >= N) continue;
           float v = acc[i][j][r];
           if (aff != nullptr) v = fmaf(v, sc, sh);
-          Cf[rm.pixel(row) * ldc + col] = relu ? relu_f(v) : v;
+          float* cp = Cf + rm.pixel(row) * ldc + col;
+          *cp = (relu ? relu_f(v) : v) + (accum ? *cp : 0.f);
         }
     }
     return;
@@ -269,9 +273,18 @@ __device__ __forceinline__ void nt_epilogue(f32x4 (&acc)[TM][TN], uint16_t* smem
     const uint16_t* src = Cs + row * LDC + ch * 8;
     uint16_t* dst = C + rm.pixel(grow) * ldc + gcol;
     if (gcol + 8 <= N && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
-      *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+      if (accum) {
+        float a[8], b[8];
+        load8(src).to_float(a);
+        load8(dst).to_float(b);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] += b[e];
+        store8(dst, bf16x8::from_float(a));
+      } else {
+        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+      }
     } else {
-      for (int e = 0; e < 8 && gcol + e < N; ++e) dst[e] = src[e];
+      for (int e = 0; e < 8 && gcol + e < N; ++e) dst[e] = accum ? f2bf(bf2f(src[e]) + bf2f(dst[e])) : src[e];
     }
   }
 }

@@ -35,7 +35,7 @@ from torch import nn
 
 from . import _lib, concat, streams, tape, tune, wt_cache
 from .arena import zeros_f32
-from .bn import _as_rows, _rows_view
+from .bn import _accum_ok, _as_rows, _rows_view
 from .gemm import wgrad_tn
 
 _BF16 = torch.bfloat16
@@ -77,6 +77,7 @@ class _HeadFn(torch.autograd.Function):
         _lib.check_f32_stats(running_mean, running_var)
         dev = x.device
         stream = _lib.stream_ptr(dev)
+        ctx.join = getattr(x, "_tony_join", None)  # ops/residual.py GradJoin: x has a second consumer
         x, (M, cin, ldx) = _as_rows(x)
         n, _, h, w = x.shape
         ctot = weight.shape[0]
@@ -225,12 +226,22 @@ class _HeadFn(torch.autograd.Function):
             # issued first so that it overlaps the dgrad GEMM on the weight-gradient stream
             streams.run(lambda: wgrad_tn(dZ.data_ptr(), ctot, x.data_ptr(), ldx, M, ctot, cin, dev, dst=gw), dZ, x)
         dx = None
+        join = getattr(ctx, "join", None)
+        pend = join.take() if join is not None else None
         if ctx.needs_input_grad[0]:
             wt = wt_cache.transposed(weight).reshape(cin, ctot)  # [Cin, Ctot]
             dx = _cl_empty(n, cin, h, w, dev)
+            vf = tune.gemm_flags(dZ, wt, dx, M, cin, ctot, ctot, False)  # timing runs write dx, never pend
+            if pend is not None and _accum_ok(pend, x.shape):
+                # x's other consumer (the identity path) already wrote its gradient: the epilogue adds
+                # dX into it (bit 4) -- no separate add kernel
+                dx = pend
+                vf |= 16
             rc = L.tony_gemm_bf16(dZ.data_ptr(), wt.data_ptr(), dx.data_ptr(), M, cin, ctot, ctot, ctot, cin,
-                                  tune.gemm_flags(dZ, wt, dx, M, cin, ctot, ctot, False), 0, 0, stream)
+                                  vf, 0, 0, stream)
             _lib.check(rc, "tony_gemm_bf16")
+            if pend is not None and dx is not pend:
+                dx = pend.add_(dx)
         if inplace:
             _lib.report_inplace(ctx.params, (None, None, None))
             return dx, None, None, None, None, None, None, None, None, None, None, None

@@ -26,6 +26,43 @@ from .gemm import wgrad_tn
 _BF16 = torch.bfloat16
 
 
+class GradJoin:
+    """The gradient meeting point of a tensor with two consumers: ResNet's identity block feeds its
+    input x to conv1 AND to the residual add.  Autograd would sum the two gradients with a separate
+    add kernel (3 passes over a 51-205 MB activation per block).  Instead the residual op's backward,
+    which runs first, parks d(identity) here and returns None for it; conv1's backward then adds its
+    dX into that tensor in the dgrad epilogue (csrc/mfma_common.h nt_epilogue accum) and returns the
+    sum.  Either order is correct: if conv1's backward comes first (``take`` finds nothing), the
+    residual op returns its gradient to autograd as usual.  Set by models/resnet.py on x as
+    ``_tony_join``; one per forward."""
+
+    __slots__ = ("pending", "stream", "consumed")
+
+    def __init__(self):
+        self.pending = None
+        self.stream = None
+        self.consumed = False
+
+    def park(self, grad: torch.Tensor) -> bool:
+        """Hold ``grad`` for the other consumer; False when it already ran (return grad to autograd)."""
+        if self.consumed:
+            return False
+        self.pending = grad
+        self.stream = torch.cuda.current_stream(grad.device) if grad.is_cuda else None
+        return True
+
+    def take(self):
+        """The parked gradient (ordered before the current stream's next work), or None."""
+        self.consumed = True
+        g, self.pending = self.pending, None
+        if g is not None and self.stream is not None:
+            cur = torch.cuda.current_stream(g.device)
+            if cur is not self.stream:
+                streams.fork(self.stream, cur)
+                streams.keep(g)
+        return g
+
+
 def _bn_stats_and_apply(L, z, ldz, M, C, res, ldr, y, ldy, gamma, beta, pb, eps, training, momentum, running_mean,
                         running_var, stats, stream):
     _lib.check_f32_stats(running_mean, running_var)
@@ -125,6 +162,7 @@ class _Conv1x1BNAddReLUFn(torch.autograd.Function):
         ctx.save_for_backward(x, weight, Z, y, gamma, beta, mean, invstd)
         ctx.params = (weight, gamma, beta)
         ctx.pb = pb
+        ctx.join = getattr(res, "_tony_join", None)
         return y
 
     @staticmethod
@@ -153,6 +191,8 @@ class _Conv1x1BNAddReLUFn(torch.autograd.Function):
             dw = wgrad_tn(dZ.data_ptr(), cout, x.data_ptr(), ldx, M, cout, cin, dev).to(weight.dtype)
             dw = dw.reshape(weight.shape)
         _lib.report_inplace(ctx.params, (dw, dg, db))
+        if ctx.join is not None and dres is not None and ctx.join.park(dres):
+            dres = None  # conv1's dgrad adds its dX into it (GradJoin)
         return dx, dw, dres, dg, db, None, None, None, None, None
 
 
