@@ -1,6 +1,6 @@
-"""ResNet identity blocks: conv1's dgrad adds its dX into the identity path's gradient in its
-epilogue (ops/residual.py GradJoin, csrc/mfma_common.h nt_epilogue accum) instead of autograd's add
-kernel -- the block input gradient must match the unjoined graph's (to bf16 rounding: the BN
+"""ResNet blocks: the consumer of the block input whose backward runs second adds its dX into the
+gradient the first one parked, in its dgrad epilogue (ops/residual.py GradJoin, csrc/mfma_common.h accum)
+instead of autograd's add kernel -- the block input gradient must match the unjoined graph's (to bf16 rounding: the BN
 statistics are summed with atomics, so two runs may differ in the last bit; a lost contribution
 of either consumer is off by far more)."""
 import pytest
@@ -13,21 +13,25 @@ def _cl(t):
     return t.contiguous(memory_format=torch.channels_last)
 
 
-@pytest.mark.parametrize("shape", [(4, 256, 14, 14), (2, 512, 7, 9)])
+@pytest.mark.parametrize("shape", [(4, 256, 14, 14, 1, 64), (2, 512, 7, 9, 1, 128), (4, 64, 16, 16, 1, 64),
+                                   (4, 256, 16, 16, 2, 128)],
+                         ids=["identity-256", "identity-512", "projection-s1", "projection-s2"])
 def test_identity_block_join_matches_autograd_sum(cuda, shape, monkeypatch):
     from tony_amd.models import resnet
     from tony_amd.models.layers import cast_model, init_weights
 
-    n, c, h, w = shape
+    n, c, h, w, stride, width = shape
     torch.manual_seed(0)
-    blk = cast_model(init_weights(resnet.Bottleneck(c, c // 4), 5), torch.bfloat16, cuda)
+    blk = cast_model(init_weights(resnet.Bottleneck(c, width, stride=stride), 5), torch.bfloat16, cuda)
     blk = blk.to(memory_format=torch.channels_last).train()
     torch.nn.init.constant_(blk.bn3.weight, 0.5)  # non-degenerate residual branch
     x0 = _cl(torch.randn(n, c, h, w, device=cuda)).to(torch.bfloat16)
-    g = _cl(torch.randn(n, c, h, w, device=cuda)).to(torch.bfloat16)
+    oh, ow = (h - 1) // stride + 1, (w - 1) // stride + 1
+    g = _cl(torch.randn(n, 4 * width, oh, ow, device=cuda)).to(torch.bfloat16)
     grads = {}
     for join in (False, True):
         monkeypatch.setattr(resnet, "JOIN", join)
+        monkeypatch.setattr(resnet, "DS_TONY", True)
         blk.zero_grad(set_to_none=True)
         x = (x0 * 1).requires_grad_(True)  # a non-leaf copy per run (the join rides on the tensor)
         x.retain_grad()

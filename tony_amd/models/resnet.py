@@ -24,6 +24,7 @@ import os
 import torch
 from torch import nn
 
+from ..ops import conv as conv_ops
 from ..ops.bn import BatchNormAct2d
 from ..ops.linear import Linear
 from ..ops.pool import global_avg_pool
@@ -31,8 +32,10 @@ from ..ops.residual import GradJoin, bn_add_relu, conv1x1_bn_add_relu
 from .layers import ConvBNAct, conv_bn_act_maxpool, init_weights
 
 
-# TONY_RESNET_JOIN=0: let autograd sum the identity-block input gradients (A/B)
+# TONY_RESNET_JOIN=0: let autograd sum the block input gradients (A/B)
 JOIN = os.environ.get("TONY_RESNET_JOIN", "1") != "0"
+# TONY_RESNET_DS_TONY=0: the projection shortcut as nn.Conv2d (MIOpen) + fused BN (A/B)
+DS_TONY = os.environ.get("TONY_RESNET_DS_TONY", "1") != "0"
 
 
 class Bottleneck(nn.Module):
@@ -53,10 +56,24 @@ class Bottleneck(nn.Module):
                 BatchNormAct2d(cout, eps=eps, relu=False) if fused else nn.BatchNorm2d(cout, eps=eps))
 
     def forward(self, x):
-        if self.fused and self.downsample is None and x.is_cuda and JOIN and torch.is_grad_enabled():
-            # x feeds conv1 and the identity add: their gradients meet in one tensor (GradJoin), no add
+        ds_tony = (self.downsample is not None and self.fused and x.is_cuda and self.training and DS_TONY
+                   and conv_ops.supported(x, self.downsample[0].weight, self.downsample[0].stride,
+                                          self.downsample[0].padding))
+        if (self.fused and x.is_cuda and self.training and JOIN and torch.is_grad_enabled()
+                and x.dtype == torch.bfloat16 and (self.downsample is None or ds_tony)):
+            # x feeds conv1 and the identity add (or the downsample conv), both join-aware fused ops:
+            # their gradients meet in one tensor (GradJoin), no add kernel
             x._tony_join = GradJoin()
-        identity = self.downsample(x) if self.downsample is not None else x
+        if self.downsample is None:
+            identity = x
+        elif ds_tony:
+            # the projection shortcut on the tony kernels: 1x1/s conv with the BN statistics in its
+            # epilogue + BN apply (no ReLU), strided dgrad per residue class -- not MIOpen
+            c, bn = self.downsample[0], self.downsample[1]
+            identity = conv_ops.conv_bn_act(x, c.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                            c.stride, c.padding, True, bn.momentum, bn.eps, relu=False)
+        else:
+            identity = self.downsample(x)
         out = self.conv2(self.conv1(x))
         bn = self.bn3
         if self.fused and out.is_cuda:

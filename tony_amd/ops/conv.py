@@ -714,13 +714,15 @@ def _conv_bn_backward(ctx, x, weight, gamma, beta, mean, invstd, Z, dy, presums=
     _lib.bn_bwd(Z, ldz, dy, lddy, dZ, ldz, M, co, mean, invstd, gamma, beta, pb, relu, ws, dgamma, dbeta, inplace,
                 dev, sums=presums)
     dw = _wgrad(dZ, x, weight, stride, padding)  # first: overlaps the dgrad on the side stream
-    join = getattr(ctx, "join", None)
+    join = getattr(ctx, "join", None) if ctx.needs_input_grad[0] else None
     pend = join.take() if join is not None else None
-    if pend is not None and ctx.needs_input_grad[0]:
-        # x's other consumer (the identity path) already wrote its gradient: dX is added into it
+    if pend is not None:
+        # x's other consumer already wrote its gradient: dX is added into it (ops/residual.py GradJoin)
         dx = _dgrad(dZ, weight, x.shape, stride, padding, accum=pend)
     else:
         dx = _dgrad_fused_bn(ctx, dZ, weight, x.shape, stride, padding) if ctx.needs_input_grad[0] else None
+        if join is not None:
+            dx = join.settle(dx)  # first of the two: parked for the other consumer
     streams.keep(dx)  # may be consumed on another (branch) stream
     if inplace:
         dgamma = dbeta = None

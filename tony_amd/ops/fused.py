@@ -226,7 +226,7 @@ class _HeadFn(torch.autograd.Function):
             # issued first so that it overlaps the dgrad GEMM on the weight-gradient stream
             streams.run(lambda: wgrad_tn(dZ.data_ptr(), ctot, x.data_ptr(), ldx, M, ctot, cin, dev, dst=gw), dZ, x)
         dx = None
-        join = getattr(ctx, "join", None)
+        join = getattr(ctx, "join", None) if ctx.needs_input_grad[0] else None
         pend = join.take() if join is not None else None
         if ctx.needs_input_grad[0]:
             wt = wt_cache.transposed(weight).reshape(cin, ctot)  # [Cin, Ctot]
@@ -242,6 +242,8 @@ class _HeadFn(torch.autograd.Function):
             _lib.check(rc, "tony_gemm_bf16")
             if pend is not None and dx is not pend:
                 dx = pend.add_(dx)
+            elif pend is None and join is not None:
+                dx = join.settle(dx)  # first of the two: parked for the other consumer
         if inplace:
             _lib.report_inplace(ctx.params, (None, None, None))
             return dx, None, None, None, None, None, None, None, None, None, None, None

@@ -27,40 +27,59 @@ _BF16 = torch.bfloat16
 
 
 class GradJoin:
-    """The gradient meeting point of a tensor with two consumers: ResNet's identity block feeds its
-    input x to conv1 AND to the residual add.  Autograd would sum the two gradients with a separate
-    add kernel (3 passes over a 51-205 MB activation per block).  Instead the residual op's backward,
-    which runs first, parks d(identity) here and returns None for it; conv1's backward then adds its
-    dX into that tensor in the dgrad epilogue (csrc/mfma_common.h nt_epilogue accum) and returns the
-    sum.  Either order is correct: if conv1's backward comes first (``take`` finds nothing), the
-    residual op returns its gradient to autograd as usual.  Set by models/resnet.py on x as
-    ``_tony_join``; one per forward."""
+    """The gradient meeting point of a tensor with two consumers: a ResNet block feeds its input x to
+    conv1 AND to the residual add (identity blocks) or the downsample conv (projection blocks).
+    Autograd would sum the two gradients with a separate add kernel (3 passes over a 51-205 MB
+    activation per block).  Instead the consumer whose backward runs first parks its gradient here and
+    returns None for x; the second one adds its dX into that tensor in the dgrad epilogue
+    (csrc/mfma_common.h nt_epilogue accum) and returns the sum.  Set by models/resnet.py on x as
+    ``_tony_join``, one per forward; both consumers of x are then join-aware:
 
-    __slots__ = ("pending", "stream", "consumed")
+    * the residual op (produces d(identity) with its own kernel): ``park(grad)`` -> what to return for x;
+    * a conv (ops/conv.py _conv_bn_backward, ops/fused.py _HeadFn): ``take()`` before its dgrad -- a
+      parked gradient to accumulate into, or None, and then ``settle(dx)`` -> what to return."""
+
+    __slots__ = ("pending", "stream", "ran")
 
     def __init__(self):
         self.pending = None
         self.stream = None
-        self.consumed = False
+        self.ran = 0  # consumers whose backward has started
 
-    def park(self, grad: torch.Tensor) -> bool:
-        """Hold ``grad`` for the other consumer; False when it already ran (return grad to autograd)."""
-        if self.consumed:
-            return False
+    def _hold(self, grad: torch.Tensor) -> None:
         self.pending = grad
         self.stream = torch.cuda.current_stream(grad.device) if grad.is_cuda else None
-        return True
 
-    def take(self):
-        """The parked gradient (ordered before the current stream's next work), or None."""
-        self.consumed = True
-        g, self.pending = self.pending, None
-        if g is not None and self.stream is not None:
+    def _ordered(self, g: torch.Tensor) -> torch.Tensor:
+        """``g`` (parked on self.stream) usable on the current stream."""
+        if self.stream is not None:
             cur = torch.cuda.current_stream(g.device)
             if cur is not self.stream:
                 streams.fork(self.stream, cur)
                 streams.keep(g)
         return g
+
+    def park(self, grad):
+        self.ran += 1
+        if self.pending is not None:  # a conv consumer ran first and parked its dX: the sum goes back
+            total = self._ordered(self.pending).add_(grad)
+            self.pending = None
+            return total
+        if grad is None or self.ran >= 2:
+            return grad
+        self._hold(grad)
+        return None
+
+    def take(self):
+        self.ran += 1
+        g, self.pending = self.pending, None
+        return self._ordered(g) if g is not None else None
+
+    def settle(self, dx):
+        if dx is None or self.ran >= 2:
+            return dx
+        self._hold(dx)
+        return None
 
 
 def _bn_stats_and_apply(L, z, ldz, M, C, res, ldr, y, ldy, gamma, beta, pb, eps, training, momentum, running_mean,
@@ -191,8 +210,8 @@ class _Conv1x1BNAddReLUFn(torch.autograd.Function):
             dw = wgrad_tn(dZ.data_ptr(), cout, x.data_ptr(), ldx, M, cout, cin, dev).to(weight.dtype)
             dw = dw.reshape(weight.shape)
         _lib.report_inplace(ctx.params, (dw, dg, db))
-        if ctx.join is not None and dres is not None and ctx.join.park(dres):
-            dres = None  # conv1's dgrad adds its dX into it (GradJoin)
+        if ctx.join is not None:  # conv1's dgrad adds its dX into it, or it already ran (GradJoin)
+            dres = ctx.join.park(dres)
         return dx, dw, dres, dg, db, None, None, None, None, None
 
 
