@@ -59,17 +59,17 @@ __device__ __forceinline__ bf16x8_t tr_frag(const uint16_t* lds, int kgrp, int c
 // 16 zero bytes of kZeroChunk.
 __device__ const uint4 kZeroChunk = {0u, 0u, 0u, 0u};
 
+// M0 is declared clobbered rather than saved and restored around every DMA: the compiler
+// re-materialises it only where it needs it, which the K loops do not (2 fewer SALU per DMA; a K-step
+// issues 4-6 of them beside 12-24 MFMAs).
 __device__ __forceinline__ void glds16(const void* src, uint32_t lds_wave_base) {
-  unsigned keep;
   asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
+      "s_mov_b32 m0, %1\n\t"
       "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
+      "global_load_lds_dwordx4 %0, off"
+      :
       : "v"(src), "s"(lds_wave_base)
-      : "memory");
+      : "memory", "m0");
 }
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {

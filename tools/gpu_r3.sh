@@ -29,6 +29,7 @@ for s in "$@"; do
     join_tests) step join_tests 400 python -u -m pytest tests/test_resnet_join_gpu.py tests/test_ops_gpu.py -x -q --timeout 240 --timeout-method thread -k "join or resnet or residual" ;;
     ab_join) step ab_join 600 python tools/ab_r3.py --reps 3 --bench-args "--model resnet50" nojoin=TONY_RESNET_JOIN=0 ds_miopen=TONY_RESNET_DS_TONY=0 ;;
     ab2) step ab2 700 python tools/ab_r3.py --reps 3 fr_auto=TONY_BN_FUSED_REDUCE=auto fr_auto32=TONY_BN_FUSED_REDUCE=auto,TONY_BN_FUSED_REDUCE_MIN_MB=32 urgent0=TONY_WGRAD_URGENT_MB=0 ;;
+    ab_so) step ab_so 700 python tools/ab_r3.py --reps 3 old_so=TONY_KERNELS_SO=$(pwd)/tony_amd/ops/_tony_kernels_ab.so ;;
     # alternating A/B of the opt-in environment toggles against the default step (tools/ab_r3.py)
     ab) step ab 1000 python tools/ab_r3.py --reps 2 onepass16=TONY_BN_ONEPASS=1,TONY_BN_ONEPASS_MAX_MB=16 fused_red=TONY_BN_FUSED_REDUCE=1 pool_bnred=TONY_POOL_BNRED=1 occ2=TONY_WGRAD_OCC=2 nobranch=TONY_BRANCH_STREAMS=0 wbatch1=TONY_WGRAD_BATCH=1 ;;
     tests) step gpu_suite 800 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread ;;
