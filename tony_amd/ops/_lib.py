@@ -69,9 +69,15 @@ _SIGNATURES = {
     "tony_bn_apply_res": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
                           c_void_p, c_int64, c_void_p, c_void_p, c_int, c_float, c_int, c_int, c_void_p, c_void_p,
                           c_void_p, c_void_p, c_float, c_void_p],
+    "tony_bn_apply_res_m": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
+                            c_void_p, c_int64, c_void_p, c_void_p, c_int, c_float, c_int, c_int, c_void_p, c_void_p,
+                            c_void_p, c_void_p, c_float, c_void_p, c_int64, c_void_p],
     "tony_bn_bwd_res": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
                         c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
                         c_int, c_void_p],
+    "tony_bn_bwd_res_m": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
+                          c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                          c_void_p, c_int, c_void_p],
     "tony_bn_bwd_onepass": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p,
                             c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
                             c_void_p, c_int, c_void_p],

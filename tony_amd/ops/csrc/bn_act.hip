@@ -156,6 +156,8 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_stats_kernel(
 // mode 0: training (stats from sums, saves mean/invstd, updates running stats)
 // mode 1: inference (stats from running_mean / running_var)
 // RES: y = act(bn(x) + res)  (ResNet bottleneck tail: BN + identity add + ReLU in one pass)
+// mask (RES form, optional): one byte per 8 channels of a row (bit j: y > 0 for channel 8 * cg + j,
+// row stride ldm bytes) -- the ReLU mask the backward needs, 1/16 of the bytes of re-reading y
 template <bool RES, class T = uint16_t>
 __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
     const T* __restrict__ x, int64_t M, int C, int64_t ldx, int64_t rows_per_block,
@@ -163,7 +165,8 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
     T* __restrict__ y, int64_t ldy, const float* __restrict__ sum, const float* __restrict__ sumsq,
     int64_t sstride, const void* gamma, const void* beta, int param_bf16, float eps, int relu, int mode,
     float* __restrict__ save_mean, float* __restrict__ save_invstd,
-    float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, Segs segs) {
+    float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, Segs segs,
+    uint8_t* __restrict__ mask = nullptr, int64_t ldm = 0) {
   float* scale = bn_dyn;  // [C] then shift [C]: bn_lds_table(C, 2) bytes
   float* shift = bn_dyn + C;
   const float inv_m = 1.f / static_cast<float>(M);
@@ -217,7 +220,16 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
       if (RES) t += q[j];
       f[j] = relu ? relu_f(t) : t;
     }
-    V8<T>::from_float(f).store(yb + row * ldyt);
+    const V8<T> out = V8<T>::from_float(f);
+    out.store(yb + row * ldyt);
+    if (RES && mask != nullptr) {  // the stored values' sign, exactly what re-reading y would test
+      float g[8];
+      out.to_float(g);
+      unsigned b = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) b |= (g[j] > 0.f ? 1u : 0u) << j;
+      mask[row * ldm + rm.cg] = static_cast<uint8_t>(b);
+    }
   };
   V8<T> none{};
   for (; r + 3 * step < r1; r += 4 * step) {
@@ -239,7 +251,9 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
 // residual form where the ReLU followed an add -- masked by the saved output y.
 // Per-channel coefficients are built once per workgroup in LDS (xhat = x*p0 + p1,
 // pre-activation = x*p2 + p3), so no lane waits on scattered parameter loads.
-template <bool YMASK, class T = uint16_t>
+// MB (with YMASK): ym is the forward's byte mask (bn_fwd_apply_kernel mask, row stride ldym bytes)
+// instead of y
+template <bool YMASK, class T = uint16_t, bool MB = false>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     const T* __restrict__ x, int64_t ldx, const T* __restrict__ dy, int64_t lddy,
     const T* __restrict__ ym, int64_t ldym,
@@ -273,16 +287,19 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
     const int64_t r1 = min(M, r0 + rows_per_block);
     const int64_t step = rm.RPI;
-    auto body = [&](const V8<T>& xv, const V8<T>& gv, const V8<T>& yv) {
+    const uint8_t* mbp = reinterpret_cast<const uint8_t*>(ym) + rm.cg;
+    auto body = [&](const V8<T>& xv, const V8<T>& gv, const V8<T>& yv, unsigned mbits) {
       float xf[8], gf[8], yf[8];
       xv.to_float(xf);
       gv.to_float(gf);
-      if (YMASK) yv.to_float(yf);
+      if (YMASK && !MB) yv.to_float(yf);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float xh = fmaf(xf[j], p0[j], p1[j]);
         float d = gf[j];
-        if (YMASK) {
+        if (YMASK && MB) {
+          if (!((mbits >> j) & 1u)) d = 0.f;
+        } else if (YMASK) {
           if (yf[j] <= 0.f) d = 0.f;
         } else if (relu && fmaf(xf[j], p2[j], p3[j]) <= 0.f) {
           d = 0.f;
@@ -302,17 +319,20 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
     int64_t r = r0 + rm.rsub;
     for (; r + 3 * step < r1; r += 4 * step) {
       V8<T> xv[4], gv[4], yv[4];
+      unsigned mb[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         xv[u] = V8<T>::load(x + (r + u * step) * ldx + rm.cg * 8);
         gv[u] = V8<T>::load(db + (r + u * step) * lddt);
-        if (YMASK) yv[u] = V8<T>::load(ym + (r + u * step) * ldym + rm.cg * 8);
+        if (YMASK && MB) mb[u] = mbp[(r + u * step) * ldym];
+        else if (YMASK) yv[u] = V8<T>::load(ym + (r + u * step) * ldym + rm.cg * 8);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) body(xv[u], gv[u], YMASK ? yv[u] : none);
+      for (int u = 0; u < 4; ++u) body(xv[u], gv[u], (YMASK && !MB) ? yv[u] : none, mb[u]);
     }
     for (; r < r1; r += step)
-      body(V8<T>::load(x + r * ldx + rm.cg * 8), V8<T>::load(db + r * lddt), YMASK ? V8<T>::load(ym + r * ldym + rm.cg * 8) : none);
+      body(V8<T>::load(x + r * ldx + rm.cg * 8), V8<T>::load(db + r * lddt),
+           (YMASK && !MB) ? V8<T>::load(ym + r * ldym + rm.cg * 8) : none, (YMASK && MB) ? mbp[r * ldym] : 0u);
   }
   const int64_t so = shard_off(blockIdx.x, sstride);
   block_reduce_add(red, rm, C, a, b, dsum + so, dsumx + so);
@@ -324,7 +344,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(
 // X3 (T = float, the fp32 step of ops/x3.py): dx is written straight as the bf16 [hi | lo | hi] planes
 // of the next convolution's backward (row stride lddx = 3C, plane p at column p * C): the fp32 dx and
 // the separate split pass over it (x3.hip split3_kernel) are never made.
-template <bool YMASK, class T = uint16_t, bool X3 = false>
+template <bool YMASK, class T = uint16_t, bool X3 = false, bool MB = false>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     const T* __restrict__ x, int64_t ldx, const T* __restrict__ dy, int64_t lddy,
     const T* __restrict__ ym, int64_t ldym, T* __restrict__ dres, int64_t lddr,
@@ -366,16 +386,17 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
   const int64_t r1 = min(M, r0 + rows_per_block);
   const int64_t step = rm.RPI;
-  auto body = [&](const V8<T>& xv, const V8<T>& gv, const V8<T>& yv, int64_t row) {
+  const uint8_t* mbp = reinterpret_cast<const uint8_t*>(ym) + rm.cg;
+  auto body = [&](const V8<T>& xv, const V8<T>& gv, const V8<T>& yv, int64_t row, unsigned mbits) {
     float xf[8], gf[8], yf[8], o[8];
     xv.to_float(xf);
     gv.to_float(gf);
-    if (YMASK) yv.to_float(yf);
+    if (YMASK && !MB) yv.to_float(yf);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float d = gf[j];
       if (YMASK) {
-        if (yf[j] <= 0.f) d = 0.f;
+        if (MB ? !((mbits >> j) & 1u) : yf[j] <= 0.f) d = 0.f;
         gf[j] = d;
       } else if (relu && fmaf(xf[j], q3[j], q4[j]) <= 0.f) {
         d = 0.f;
@@ -409,17 +430,20 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
   int64_t r = r0 + rm.rsub;
   for (; r + 3 * step < r1; r += 4 * step) {
     V8<T> xv[4], gv[4], yv[4];
+    unsigned mb[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       xv[u] = V8<T>::load(x + (r + u * step) * ldx + rm.cg * 8);
       gv[u] = V8<T>::load(db + (r + u * step) * lddt);
-      if (YMASK) yv[u] = V8<T>::load(ym + (r + u * step) * ldym + rm.cg * 8);
+      if (YMASK && MB) mb[u] = mbp[(r + u * step) * ldym];
+      else if (YMASK) yv[u] = V8<T>::load(ym + (r + u * step) * ldym + rm.cg * 8);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) body(xv[u], gv[u], YMASK ? yv[u] : none, r + u * step);
+    for (int u = 0; u < 4; ++u) body(xv[u], gv[u], (YMASK && !MB) ? yv[u] : none, r + u * step, mb[u]);
   }
   for (; r < r1; r += step)
-    body(V8<T>::load(x + r * ldx + rm.cg * 8), V8<T>::load(db + r * lddt), YMASK ? V8<T>::load(ym + r * ldym + rm.cg * 8) : none, r);
+    body(V8<T>::load(x + r * ldx + rm.cg * 8), V8<T>::load(db + r * lddt),
+         (YMASK && !MB) ? V8<T>::load(ym + r * ldym + rm.cg * 8) : none, r, (YMASK && MB) ? mbp[r * ldym] : 0u);
 }
 
 // ---- one-launch BN(+ReLU) backward: reduce -> grid barrier -> apply ------------------------------
@@ -778,6 +802,26 @@ TONY_API int tony_bn_apply_res(const void* x, int64_t M, int C, int64_t ldx, con
   return 0;
 }
 
+// tony_bn_apply_res that also writes the forward's ReLU byte mask (M x C/8 bytes, row stride ldm)
+TONY_API int tony_bn_apply_res_m(const void* x, int64_t M, int C, int64_t ldx, const void* res, int64_t ldr, void* y,
+                                 int64_t ldy, const float* sum, const float* sumsq, int64_t sstride, const void* gamma,
+                                 const void* beta, int param_bf16, float eps, int relu, int mode, float* save_mean,
+                                 float* save_invstd, float* running_mean, float* running_var, float momentum,
+                                 void* mask, int64_t ldm, hipStream_t stream) {
+  if (bad_c(C) || (ldx % 8) || (ldy % 8) || (ldr % 8) || res == nullptr || sstride < 0 || mask == nullptr ||
+      ldm < C / 8)
+    return -1;
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 4, 8192, &rpb, &grid);
+  bn_fwd_apply_kernel<true, uint16_t><<<grid, kThreads, bn_lds_table(C, 2), stream>>>(
+      static_cast<const uint16_t*>(x), M, C, ldx, rpb, static_cast<const uint16_t*>(res), ldr,
+      static_cast<uint16_t*>(y), ldy, sum, sumsq, sstride, gamma, beta, param_bf16, eps, relu, mode, save_mean,
+      save_invstd, running_mean, running_var, momentum, Segs{}, static_cast<uint8_t*>(mask), ldm);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
 TONY_API int tony_bn_bwd_reduce(const void* x, int64_t ldx, const void* dy, int64_t lddy, int64_t M, int C,
                                 const float* mean, const float* invstd, const void* gamma, const void* beta,
                                 int param_bf16, int relu, float* dsum, float* dsumx, int64_t sstride,
@@ -1045,6 +1089,30 @@ TONY_API int tony_bn_bwd_res(const void* x, int64_t ldx, const void* dy, int64_t
   bn_bwd_apply_kernel<true, uint16_t><<<grid, kThreads, bn_lds_table(C, 5), stream>>>(
       static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, static_cast<const uint16_t*>(y),
       ldy, static_cast<uint16_t*>(dres), lddr, static_cast<uint16_t*>(dx), lddx, M, C, rpb, mean, invstd, gamma, beta,
+      param_bf16, 1, dsums_ws, dsums_ws + C, ss, dgamma, dbeta, accumulate, Segs{});
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// tony_bn_bwd_res with the forward's byte mask (tony_bn_apply_res_m) in place of y
+TONY_API int tony_bn_bwd_res_m(const void* x, int64_t ldx, const void* dy, int64_t lddy, const void* mask, int64_t ldm,
+                               void* dx, int64_t lddx, void* dres, int64_t lddr, int64_t M, int C, const float* mean,
+                               const float* invstd, const void* gamma, const void* beta, int param_bf16,
+                               float* dsums_ws, void* dgamma, void* dbeta, int accumulate, hipStream_t stream) {
+  if (bad_c(C) || (ldx % 8) || (lddy % 8) || (lddx % 8) || (lddr % 8) || mask == nullptr || ldm < C / 8) return -1;
+  const int64_t ss = 2 * static_cast<int64_t>(C);
+  const auto* mb = static_cast<const uint16_t*>(mask);  // reinterpreted as bytes inside (MB)
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 8, 512, &rpb, &grid);
+  bn_bwd_reduce_kernel<true, uint16_t, true><<<grid, kThreads, bn_lds_bred(C), stream>>>(
+      static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, mb, ldm, M, C, rpb, mean, invstd,
+      gamma, beta, param_bf16, 1, dsums_ws, dsums_ws + C, ss, Segs{});
+  TONY_LAUNCH_CHECK();
+  plan_rows(M, C, 4, 8192, &rpb, &grid);
+  bn_bwd_apply_kernel<true, uint16_t, false, true><<<grid, kThreads, bn_lds_table(C, 5), stream>>>(
+      static_cast<const uint16_t*>(x), ldx, static_cast<const uint16_t*>(dy), lddy, mb, ldm,
+      static_cast<uint16_t*>(dres), lddr, static_cast<uint16_t*>(dx), lddx, M, C, rpb, mean, invstd, gamma, beta,
       param_bf16, 1, dsums_ws, dsums_ws + C, ss, dgamma, dbeta, accumulate, Segs{});
   TONY_LAUNCH_CHECK();
   return 0;

@@ -15,6 +15,8 @@ place into the flat gradient buffer when the trainer enabled it.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib, streams, tape, tune, wt_cache
@@ -82,8 +84,20 @@ class GradJoin:
         return None
 
 
+# TONY_RES_MASK=0: the residual BN backward re-reads y for its ReLU mask instead of the forward's byte
+# mask (1 bit per element: y is a 51-205 MB activation read twice per block backward)
+RES_MASK = os.environ.get("TONY_RES_MASK", "1") != "0"
+
+
+def _res_mask(M: int, C: int, dev):
+    """The byte mask of a residual BN forward (bit j of byte [m, c // 8]: y[m, c] > 0), or None."""
+    if not RES_MASK or C % 8:
+        return None
+    return torch.empty((M, C // 8), dtype=torch.uint8, device=dev)
+
+
 def _bn_stats_and_apply(L, z, ldz, M, C, res, ldr, y, ldy, gamma, beta, pb, eps, training, momentum, running_mean,
-                        running_var, stats, stream):
+                        running_var, stats, stream, mask=None):
     _lib.check_f32_stats(running_mean, running_var)
     dev = z.device
     if training:
@@ -92,18 +106,25 @@ def _bn_stats_and_apply(L, z, ldz, M, C, res, ldr, y, ldy, gamma, beta, pb, eps,
     else:
         mean = running_mean
         invstd = torch.rsqrt(running_var.float() + eps)
-    rc = L.tony_bn_apply_res(z.data_ptr(), M, C, ldz, res.data_ptr(), ldr, y.data_ptr(), ldy,
-                             _lib.ptr(stats) if training else 0, _lib.ptr(stats) + 4 * C if training else 0,
-                             2 * C if training else 0, _lib.ptr(gamma), _lib.ptr(beta), pb, float(eps), 1, 0 if training else 1,
-                             _lib.ptr(mean) if training else 0, _lib.ptr(invstd) if training else 0,
-                             _lib.ptr(running_mean), _lib.ptr(running_var), float(momentum), stream)
+    args = (z.data_ptr(), M, C, ldz, res.data_ptr(), ldr, y.data_ptr(), ldy,
+            _lib.ptr(stats) if training else 0, _lib.ptr(stats) + 4 * C if training else 0,
+            2 * C if training else 0, _lib.ptr(gamma), _lib.ptr(beta), pb, float(eps), 1, 0 if training else 1,
+            _lib.ptr(mean) if training else 0, _lib.ptr(invstd) if training else 0,
+            _lib.ptr(running_mean), _lib.ptr(running_var), float(momentum))
+    if mask is not None:
+        rc = L.tony_bn_apply_res_m(*args, mask.data_ptr(), C // 8, stream)
+    else:
+        rc = L.tony_bn_apply_res(*args, stream)
     _lib.check(rc, "tony_bn_apply_res")
     return mean, invstd
 
 
 def _bwd_res(L, z, ldz, dy, y, M, C, mean, invstd, gamma, beta, pb, params, stream, want_dres=True):
+    """``y``: the forward output, or its byte mask (uint8 [M, C/8], _res_mask) for the ReLU test."""
     dev = z.device
     dy, (_, _, lddy) = _as_rows(dy)
+    if y.dtype == torch.uint8:
+        return _bwd_res_mask(L, z, ldz, dy, lddy, y, M, C, mean, invstd, gamma, beta, pb, params, stream, want_dres)
     _, _, ldy = _rows_view(y)
     dz = _empty_like_rows(y)
     _, _, lddz = _rows_view(dz)
@@ -118,6 +139,24 @@ def _bwd_res(L, z, ldz, dy, y, M, C, mean, invstd, gamma, beta, pb, params, stre
                            _lib.ptr(beta), pb, ws.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), int(inplace),
                            stream)
     _lib.check(rc, "tony_bn_bwd_res")
+    return dz, dres, (None, None) if inplace else (dgamma, dbeta)
+
+
+def _bwd_res_mask(L, z, ldz, dy, lddy, mask, M, C, mean, invstd, gamma, beta, pb, params, stream, want_dres):
+    dev = z.device
+    n, _, h, w = z.shape
+    dz = _cl_empty(n, C, h, w, dev)
+    dres = _cl_empty(n, C, h, w, dev) if want_dres else None
+    ws = zeros_f32(_lib.stat_floats(C), dev)
+    gg, gb = _lib.grad_slot(params[0]), _lib.grad_slot(params[1])
+    inplace = gg is not None and gb is not None
+    dgamma = gg if inplace else torch.empty_like(gamma)
+    dbeta = gb if inplace else torch.empty_like(beta)
+    rc = L.tony_bn_bwd_res_m(z.data_ptr(), ldz, dy.data_ptr(), lddy, mask.data_ptr(), C // 8, dz.data_ptr(), C,
+                             _lib.ptr(dres), C, M, C, mean.data_ptr(), invstd.data_ptr(), _lib.ptr(gamma),
+                             _lib.ptr(beta), pb, ws.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), int(inplace),
+                             stream)
+    _lib.check(rc, "tony_bn_bwd_res_m")
     return dz, dres, (None, None) if inplace else (dgamma, dbeta)
 
 
@@ -137,9 +176,10 @@ class _BNAddReLUFn(torch.autograd.Function):
             rc = L.tony_bn_stats(z.data_ptr(), M, C, ldz, stats.data_ptr(), stats.data_ptr() + 4 * C, 2 * C,
                                  stream)
             _lib.check(rc, "tony_bn_stats")
+        mask = _res_mask(M, C, z.device) if training and ldz == C else None
         mean, invstd = _bn_stats_and_apply(L, z, ldz, M, C, res, ldr, y, ldy, gamma, beta, pb, eps, training,
-                                           momentum, running_mean, running_var, stats, stream)
-        ctx.save_for_backward(z, y, gamma, beta, mean, invstd)
+                                           momentum, running_mean, running_var, stats, stream, mask)
+        ctx.save_for_backward(z, y if mask is None else mask, gamma, beta, mean, invstd)
         ctx.params = (gamma, beta)
         ctx.pb = pb
         return y
@@ -176,9 +216,10 @@ class _Conv1x1BNAddReLUFn(torch.autograd.Function):
         _lib.check(rc, "tony_gemm_bf16")
         y = _cl_empty(n, cout, h, w, dev)
         pb = int(gamma.dtype == _BF16)
+        mask = _res_mask(M, cout, dev) if training else None
         mean, invstd = _bn_stats_and_apply(L, Z, cout, M, cout, res, ldr, y, cout, gamma, beta, pb, eps, training,
-                                           momentum, running_mean, running_var, stats, stream)
-        ctx.save_for_backward(x, weight, Z, y, gamma, beta, mean, invstd)
+                                           momentum, running_mean, running_var, stats, stream, mask)
+        ctx.save_for_backward(x, weight, Z, y if mask is None else mask, gamma, beta, mean, invstd)
         ctx.params = (weight, gamma, beta)
         ctx.pb = pb
         ctx.join = getattr(res, "_tony_join", None)
