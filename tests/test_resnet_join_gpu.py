@@ -43,3 +43,31 @@ def test_identity_block_join_matches_autograd_sum(cuda, shape, monkeypatch):
     # statistics' last bit of 0 may take the other side of a ReLU and move single dW elements
     for a, b in zip(grads[True][1], grads[False][1]):
         assert ((a - b).norm() / b.norm().clamp_min(1e-12)).item() < 2e-2
+
+
+@pytest.mark.parametrize("block", ["B", "D", "E"])
+def test_inception_block_join_matches_autograd_sum(cuda, block, monkeypatch):
+    """Inception's reduction blocks (input -> 1x1 head / 3x3-s2 conv / max pool: 3 or 2 consumers) and
+    the E block's 1x3 / 3x1 splits: the joined input gradient matches autograd's sum."""
+    from tony_amd.models import inception_v3 as iv3
+    from tony_amd.models.layers import cast_model, init_weights
+
+    torch.manual_seed(0)
+    cin, hw, make = {"B": (288, 35, lambda: iv3.InceptionB(288)), "D": (768, 17, lambda: iv3.InceptionD(768)),
+                     "E": (1280, 8, lambda: iv3.InceptionE(1280))}[block]
+    blk = cast_model(init_weights(make(), 7), torch.bfloat16, cuda).to(memory_format=torch.channels_last).train()
+    x0 = _cl(torch.randn(8, cin, hw, hw, device=cuda)).to(torch.bfloat16)
+    grads = {}
+    for join in (False, True):
+        monkeypatch.setattr(iv3, "JOIN", join)
+        blk.zero_grad(set_to_none=True)
+        x = (x0 * 1).requires_grad_(True)
+        y = blk(x)
+        g = _cl(torch.randn(y.shape, device=cuda, generator=torch.Generator(device=cuda).manual_seed(1))).to(y.dtype)
+        y.backward(g)
+        torch.cuda.synchronize()
+        grads[join] = (x.grad.float().clone(), [p.grad.float().clone() for p in blk.parameters()])
+    a, b = grads[True][0], grads[False][0]
+    assert ((a - b).norm() / b.norm()).item() < 1e-2
+    for pa, pb in zip(grads[True][1], grads[False][1]):
+        assert ((pa - pb).norm() / pb.norm().clamp_min(1e-12)).item() < 2e-2

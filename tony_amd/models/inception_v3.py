@@ -17,6 +17,8 @@ aux head) is 27,161,264 either way.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 
@@ -25,9 +27,21 @@ from ..ops.pool import avg_pool, avg_pool3x3_s1, global_avg_pool, max_pool
 from ..ops import conv as conv_ops
 from ..ops import streams, tape
 from ..ops.fused import FusedHead
+from ..ops.residual import GradJoin
 from ..ops.linear import Linear
 from ..ops.x3 import ConvBNActX3, LinearX3
 from .layers import ConvBNAct, conv_bn_act_maxpool, init_weights
+
+
+# TONY_INCEPTION_JOIN=0: let autograd sum the gradients of tensors with several consumers (A/B)
+JOIN = os.environ.get("TONY_INCEPTION_JOIN", "1") != "0"
+
+
+def _join(t: torch.Tensor, n: int) -> None:
+    """``t`` feeds ``n`` join-aware fused ops (convs / heads / max pool): their input gradients meet in one
+    tensor, each added by its producer's epilogue (ops/residual.py GradJoin) -- no autograd add kernels."""
+    if JOIN and t.is_cuda and t.dtype == torch.bfloat16 and torch.is_grad_enabled() and t.requires_grad:
+        t._tony_join = GradJoin(n)
 
 
 def _seq(seq, x, slot):
@@ -112,6 +126,8 @@ class InceptionB(_Block):  # 35x35 -> 17x17 reduction
             n, c, h, w = x.shape
             buf = concat_buffer(n, self.out_channels, (h - 3) // 2 + 1, (w - 3) // 2 + 1, x)
             s3, sd, sp = _slots(buf, (384, 96, c))
+            if self.training:
+                _join(x, 3)  # the double-3x3 chain's 1x1 head, the 3x3/2 conv, the max pool
             od, o3, op = streams.parallel(lambda: _seq(self.bd, x, sd), lambda: self.b3(x, slot=s3),
                                           lambda: max_pool(x, 3, 2, slot=sp))
             streams.keep(x)
@@ -171,6 +187,8 @@ class InceptionD(_Block):  # 17x17 -> 8x8 reduction
             n, c, h, w = x.shape
             buf = concat_buffer(n, self.out_channels, (h - 3) // 2 + 1, (w - 3) // 2 + 1, x)
             s3, s7, sp = _slots(buf, (320, 192, c))
+            if self.training:
+                _join(x, 2)  # the fused 1x1 head and the max pool
             t3, t7 = self.head(x)
             o7, o3, op = streams.parallel(lambda: _seq(self.b7, t7, s7), lambda: self.b3(t3, slot=s3),
                                           lambda: max_pool(x, 3, 2, slot=sp))
@@ -204,9 +222,13 @@ class InceptionE(_Block):  # 8x8 with split 1x3 / 3x1 branches
             buf = concat_buffer(n, 2048, h, w, x)
             s1, sa, sb, sda, sdb, sp = _slots(buf, (320, 384, 384, 384, 384, 192))
             y1, t, d, yp = self.head(x, slots=(s1, None, None, sp))
+            if self.training:
+                _join(t, 2)  # the 1x3 and 3x1 splits
 
             def dbl():
                 dd = self.bd(d)
+                if self.training:
+                    _join(dd, 2)
                 return self.bda(dd, slot=sda), self.bdb(dd, slot=sdb)
 
             (oda, odb), oa, ob = streams.parallel(dbl, lambda: self.b3a(t, slot=sa), lambda: self.b3b(t, slot=sb))

@@ -146,7 +146,8 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd_kernel(const T* __restri
                                                                const uint8_t* __restrict__ arg,
                                                                T* __restrict__ dx, int N, int H, int W, int C,
                                                                int OH, int OW, int K, int S, int P, int64_t lddy,
-                                                               int64_t lddx) {
+                                                               int64_t lddx, int accum = 0) {
+  // accum: dx += the pooled gradient (a tensor with several consumers, ops/residual.py GradJoin)
   const uint32_t CG = C >> 3;
   const uint32_t total = static_cast<uint32_t>(N) * H * W * CG;
   const uint32_t stride = gridDim.x * kThreads;
@@ -179,7 +180,14 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd_kernel(const T* __restri
         }
       }
     }
-    V8<T>::from_float(acc).store(dx + static_cast<int64_t>(site) * lddx + cg * 8);
+    T* d = dx + static_cast<int64_t>(site) * lddx + cg * 8;
+    if (accum) {
+      float o[8];
+      V8<T>::load(d).to_float(o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += o[j];
+    }
+    V8<T>::from_float(acc).store(d);
   }
 }
 
@@ -384,6 +392,20 @@ TONY_API int tony_maxpool_bwd(const void* dy, const void* argmax, void* dx, int 
   maxpool_bwd_kernel<uint16_t><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(dy), static_cast<const uint8_t*>(argmax), static_cast<uint16_t*>(dx), N, H, W, C,
       OH, OW, K, S, P, lddy, lddx);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// tony_maxpool_bwd adding into dx (dx += the pooled gradient)
+TONY_API int tony_maxpool_bwd_acc(const void* dy, const void* argmax, void* dx, int N, int H, int W, int C, int K,
+                                  int S, int P, int64_t lddy, int64_t lddx, hipStream_t stream) {
+  if (C % 8 || lddy % 8 || lddx % 8 || P < 0 || 2 * P >= K + 1 || H + 2 * P < K || W + 2 * P < K || S < 1)
+    return -1;
+  if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
+  const int OH = (H + 2 * P - K) / S + 1, OW = (W + 2 * P - K) / S + 1;
+  maxpool_bwd_kernel<uint16_t><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+      static_cast<const uint16_t*>(dy), static_cast<const uint8_t*>(argmax), static_cast<uint16_t*>(dx), N, H, W, C,
+      OH, OW, K, S, P, lddy, lddx, 1);
   TONY_LAUNCH_CHECK();
   return 0;
 }

@@ -4,7 +4,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib, concat, streams, tape
-from .bn import _as_rows, _rows_view
+from .bn import _accum_ok, _as_rows, _rows_view
 
 
 def _nhwc_empty(n, c, h, w, like):
@@ -57,6 +57,7 @@ class _MaxPoolFn(torch.autograd.Function):
         _lib.check(rc, "tony_maxpool_fwd")
         ctx.save_for_backward(arg)
         ctx.shape = (n, c, h, w, k, s, p)
+        ctx.join = getattr(x, "_tony_join", None)  # ops/residual.py GradJoin: x has other consumers
         return y
 
     @staticmethod
@@ -64,10 +65,23 @@ class _MaxPoolFn(torch.autograd.Function):
         (arg,) = ctx.saved_tensors
         n, c, h, w, k, s, p = ctx.shape
         dy, (_, _, lddy) = _as_rows(dy)
-        dx = _nhwc_empty(n, c, h, w, dy)
-        rc = _fn("tony_maxpool_bwd", dy)(dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), n, h, w, c, k, s, p, lddy, c,
-                                         _lib.stream_ptr(dy.device))
-        _lib.check(rc, "tony_maxpool_bwd")
+        join = ctx.join if ctx.needs_input_grad[0] else None
+        pend = join.take() if join is not None else None
+        if pend is not None and dy.dtype == torch.bfloat16 and _accum_ok(pend, (n, c, h, w)):
+            # another consumer of x already wrote its gradient: the pool's is added into it in-kernel
+            rc = _lib.lib().tony_maxpool_bwd_acc(dy.data_ptr(), arg.data_ptr(), pend.data_ptr(), n, h, w, c, k, s, p,
+                                                 lddy, c, _lib.stream_ptr(dy.device))
+            _lib.check(rc, "tony_maxpool_bwd_acc")
+            dx = pend
+        else:
+            dx = _nhwc_empty(n, c, h, w, dy)
+            rc = _fn("tony_maxpool_bwd", dy)(dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), n, h, w, c, k, s, p, lddy,
+                                             c, _lib.stream_ptr(dy.device))
+            _lib.check(rc, "tony_maxpool_bwd")
+            if pend is not None:
+                dx = pend.add_(dx)
+        if join is not None:
+            dx = join.settle(dx)
         streams.keep(dx)  # may be consumed on another (branch) stream
         return dx, None, None, None, None
 

@@ -41,12 +41,13 @@ class GradJoin:
     * a conv (ops/conv.py _conv_bn_backward, ops/fused.py _HeadFn): ``take()`` before its dgrad -- a
       parked gradient to accumulate into, or None, and then ``settle(dx)`` -> what to return."""
 
-    __slots__ = ("pending", "stream", "ran")
+    __slots__ = ("pending", "stream", "ran", "n")
 
-    def __init__(self):
+    def __init__(self, n: int = 2):
         self.pending = None
         self.stream = None
         self.ran = 0  # consumers whose backward has started
+        self.n = n    # consumers of the tensor (Inception's reduction blocks: 3)
 
     def _hold(self, grad: torch.Tensor) -> None:
         self.pending = grad
@@ -63,11 +64,10 @@ class GradJoin:
 
     def park(self, grad):
         self.ran += 1
-        if self.pending is not None:  # a conv consumer ran first and parked its dX: the sum goes back
-            total = self._ordered(self.pending).add_(grad)
+        if self.pending is not None:  # a conv consumer ran first and parked its dX
+            grad = self._ordered(self.pending).add_(grad)
             self.pending = None
-            return total
-        if grad is None or self.ran >= 2:
+        if grad is None or self.ran >= self.n:
             return grad
         self._hold(grad)
         return None
@@ -78,7 +78,7 @@ class GradJoin:
         return self._ordered(g) if g is not None else None
 
     def settle(self, dx):
-        if dx is None or self.ran >= 2:
+        if dx is None or self.ran >= self.n:
             return dx
         self._hold(dx)
         return None
