@@ -66,6 +66,29 @@ def test_conv_fwd_dgrad_wgrad(cuda, shape):
     assert _rel(dw, wr.grad) < 1e-2, f"wgrad rel {_rel(dw, wr.grad):.4f}"
 
 
+ACC_SHAPES = [SHAPES[1], SHAPES[8], SHAPES[7], SHAPES[14], SHAPES[16], SHAPES[18]]
+
+
+@pytest.mark.parametrize("shape", ACC_SHAPES, ids=[f"{s[1]}x{s[2]}k{s[5][0]}{s[5][1]}s{s[6]}" for s in ACC_SHAPES])
+def test_conv_dgrad_accumulates_into_gradient(cuda, shape):
+    """conv_dgrad(accum=g) returns g + dX, summed in the epilogue (flag bit 4) -- stride 1 and the
+    strided per-residue-class launches, whose tap-less classes are then skipped (g kept there)."""
+    from tony_amd.ops.conv import conv_dgrad
+
+    n, ci, h, w, co, (r, s), st, (ph, pw) = shape
+    torch.manual_seed(1)
+    oh, ow = (h + 2 * ph - r) // st + 1, (w + 2 * pw - s) // st + 1
+    wt = _nhwc(torch.randn(co, ci, r, s, device=cuda) / (ci * r * s) ** 0.5).to(torch.bfloat16)
+    dy = _nhwc(torch.randn(n, co, oh, ow, device=cuda)).to(torch.bfloat16)
+    g = _nhwc(torch.randn(n, ci, h, w, device=cuda)).to(torch.bfloat16)
+    ref = g.float() + conv_dgrad(dy, wt, (n, ci, h, w), st, (ph, pw)).float()
+    ptr = g.data_ptr()
+    out = conv_dgrad(dy, wt, (n, ci, h, w), st, (ph, pw), accum=g)
+    assert out.data_ptr() == ptr
+    # one bf16 rounding of the fp32 sum vs the add of two bf16 tensors: within 2 bf16 ulps
+    torch.testing.assert_close(out.float(), ref, rtol=1.6e-2, atol=1.6e-2)
+
+
 def test_conv_on_channel_slice_input(cuda):
     """The input may be a channel slice of a concat buffer (pixel stride > C)."""
     from tony_amd.ops.conv import conv_fwd

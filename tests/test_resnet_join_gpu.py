@@ -13,6 +13,15 @@ def _cl(t):
     return t.contiguous(memory_format=torch.channels_last)
 
 
+def _close_but_flips(a, b):
+    """Elementwise within 1e-2, except where a ReLU of the block took the other side between the two
+    runs (its BN statistics are summed with atomics: a pre-activation within their last bit of 0
+    can flip) -- a handful of elements, against a lost consumer contribution that moves them all."""
+    bad = ~torch.isclose(a, b, rtol=1e-2, atol=1e-2)
+    assert bad.float().mean().item() < 1e-3, f"{int(bad.sum())} of {bad.numel()} elements differ"
+    assert ((a - b).norm() / b.norm()).item() < 5e-3
+
+
 @pytest.mark.parametrize("shape", [(4, 256, 14, 14, 1, 64), (2, 512, 7, 9, 1, 128), (4, 64, 16, 16, 1, 64),
                                    (4, 256, 16, 16, 2, 128)],
                          ids=["identity-256", "identity-512", "projection-s1", "projection-s2"])
@@ -38,7 +47,7 @@ def test_identity_block_join_matches_autograd_sum(cuda, shape, monkeypatch):
         y = blk(x)
         y.backward(g)
         grads[join] = (x.grad.float().clone(), [p.grad.float().clone() for p in blk.parameters()])
-    torch.testing.assert_close(grads[True][0], grads[False][0], rtol=1e-2, atol=1e-2)
+    _close_but_flips(grads[True][0], grads[False][0])
     # parameter gradients by norm: between two runs a pre-activation within the atomically summed BN
     # statistics' last bit of 0 may take the other side of a ReLU and move single dW elements
     for a, b in zip(grads[True][1], grads[False][1]):

@@ -261,7 +261,7 @@ def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, paddin
     # variants are timed without the fused reduction (it must run exactly once)
     vf = vflags if vflags is not None else tune.pick(("conv_dgrad", tuple(dy.shape), lddy, tuple(weight.shape),
                                                          (sh, sw), (ph, pw)), launch)
-    if accum is not None and bnr is None and (sh, sw) == (1, 1) and _accum_ok(accum, x_shape):
+    if accum is not None and bnr is None and _accum_ok(accum, x_shape):
         plain = dx
         dx = accum
         rc = launch(vf | 16)

@@ -1526,7 +1526,9 @@ TONY_API int tony_conv_dgrad(const void* dy, int N, int OH, int OW, int Co, int6
 // implicit-GEMM launch per residue class (iy % sh, ix % sw) of dX, each a stride-1 transposed conv
 // over the class's sub-grid with the class's taps of Wt = W permuted to [C][R][S][Co] (Phase).
 // Every dX pixel is written exactly once (classes with no taps write zeros).  flags bits 8..15:
-// tile variant (run_nt_phase).
+// tile variant (run_nt_phase); bit4: dX += the product (a projection shortcut's dgrad adding into the
+// gradient the block's first conv already wrote, ops/residual.py GradJoin) -- the classes with no
+// taps then add nothing and are not launched (3 of the 4 classes of a 1x1 / 2 shortcut).
 TONY_API int tony_conv_dgrad_strided(const void* dy, int N, int OH, int OW, int Co, int64_t lddy, const void* wt,
                                      int C, int R, int S, int sh, int sw, int ph, int pw, void* dx, int H, int W,
                                      int64_t lddx, int flags, BnRed* bnr, hipStream_t stream) {
@@ -1547,6 +1549,8 @@ TONY_API int tony_conv_dgrad_strided(const void* dy, int N, int OH, int OW, int 
   if (OH != (H + 2 * ph - R) / sh + 1 || OW != (W + 2 * pw - S) / sw + 1 || OH <= 0 || OW <= 0) return -1;
   if (static_cast<int64_t>(N) * H * W > 0x7fffffff || static_cast<int64_t>(N) * OH * OW > 0x7fffffff) return -1;
   const int v = (flags >> 8) & 0xff;
+  const int acc = flags & 16;
+  if (acc && br.z != nullptr) return -1;
   for (int py = 0; py < sh; ++py) {
     for (int px = 0; px < sw; ++px) {
       const int QH = H > py ? (H - py + sh - 1) / sh : 0, QW = W > px ? (W - px + sw - 1) / sw : 0;
@@ -1556,7 +1560,10 @@ TONY_API int tony_conv_dgrad_strided(const void* dy, int N, int OH, int OW, int 
       const int r0 = (py + ph) % sh, s0 = (px + pw) % sw;
       int Ra = r0 < R ? (R - r0 + sh - 1) / sh : 0, Sb = s0 < S ? (S - s0 + sw - 1) / sw : 0;
       const int cy = (py + ph - r0) / sh, cx = (px + pw - s0) / sw;
-      if (Ra == 0 || Sb == 0) Ra = 0, Sb = 1;  // no taps: the GEMM has K = 0 and writes zeros
+      if (Ra == 0 || Sb == 0) {
+        if (acc) continue;  // adds zero
+        Ra = 0, Sb = 1;     // no taps: the GEMM has K = 0 and writes zeros
+      }
       Gather g{static_cast<const uint16_t*>(dy), lddy, OH, OW, Co, QH, QW, Ra, Sb, 1, 1, cy, cx, -1, Ra * Sb * Co, N};
       Phase phz{R, S, r0, s0, sh, sw, RowMap{}};
       phz.rows.qw = QW;
@@ -1568,7 +1575,7 @@ TONY_API int tony_conv_dgrad_strided(const void* dy, int N, int OH, int OW, int 
       phz.rows.y0 = py;
       phz.rows.x0 = px;
       phz.bnr = br;
-      const int rc = run_nt_phase(g, wt, dx, lddx, M, C, v, phz, stream, flags & 8);
+      const int rc = run_nt_phase(g, wt, dx, lddx, M, C, v, phz, stream, flags & 24);
       if (rc != 0) return rc;
     }
   }

@@ -29,6 +29,9 @@ for s in "$@"; do
     join_tests) step join_tests 400 python -u -m pytest tests/test_resnet_join_gpu.py tests/test_ops_gpu.py -x -q --timeout 240 --timeout-method thread -k "join or resnet or residual or inception" ;;
     ab_join) step ab_join 600 python tools/ab_r3.py --reps 3 --bench-args "--model resnet50" nojoin=TONY_RESNET_JOIN=0 ds_miopen=TONY_RESNET_DS_TONY=0 ;;
     ab_ijoin) step ab_ijoin 600 python tools/ab_r3.py --reps 3 nojoin=TONY_INCEPTION_JOIN=0 ;;
+    acc_tests) step acc_tests 400 python -u -m pytest tests/test_conv_gpu.py tests/test_resnet_join_gpu.py -x -q --timeout 240 --timeout-method thread -k "accum or join" ;;
+    ab_red) step ab_red 700 python tools/ab_r3.py --reps 3 red1k=TONY_BN_RED_WGS=1024 red2k=TONY_BN_RED_WGS=2048 ;;
+    ab_red_r50) step ab_red_r50 700 python tools/ab_r3.py --reps 3 --bench-args "--model resnet50" red1k=TONY_BN_RED_WGS=1024 red2k=TONY_BN_RED_WGS=2048 ;;
     ab_mask) step ab_mask 600 python tools/ab_r3.py --reps 3 --bench-args "--model resnet50" nomask=TONY_RES_MASK=0 ;;
     ab2) step ab2 700 python tools/ab_r3.py --reps 3 fr_auto=TONY_BN_FUSED_REDUCE=auto fr_auto32=TONY_BN_FUSED_REDUCE=auto,TONY_BN_FUSED_REDUCE_MIN_MB=32 urgent0=TONY_WGRAD_URGENT_MB=0 ;;
     ab_so) step ab_so 700 python tools/ab_r3.py --reps 3 old_so=TONY_KERNELS_SO=$(pwd)/tony_amd/ops/_tony_kernels_ab.so ;;
