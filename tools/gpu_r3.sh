@@ -31,6 +31,8 @@ for s in "$@"; do
     ab_ijoin) step ab_ijoin 600 python tools/ab_r3.py --reps 3 nojoin=TONY_INCEPTION_JOIN=0 ;;
     acc_tests) step acc_tests 400 python -u -m pytest tests/test_conv_gpu.py tests/test_resnet_join_gpu.py -x -q --timeout 240 --timeout-method thread -k "accum or join" ;;
     ab_r50) step ab_r50 1000 python tools/ab_r3.py --reps 2 --bench-args "--model resnet50" fused_red=TONY_BN_FUSED_REDUCE=1 onepass16=TONY_BN_ONEPASS=1,TONY_BN_ONEPASS_MAX_MB=16 occ2=TONY_WGRAD_OCC=2 tbm128=TONY_WGRAD_TBM96=0 urgent0=TONY_WGRAD_URGENT_MB=0 ;;
+    gemm) step gemm_resnet 300 python tools/gemm_bench.py --resnet
+          step gemm_incep 300 python tools/gemm_bench.py ;;
     ab_red) step ab_red 700 python tools/ab_r3.py --reps 3 red1k=TONY_BN_RED_WGS=1024 red2k=TONY_BN_RED_WGS=2048 ;;
     ab_red_r50) step ab_red_r50 700 python tools/ab_r3.py --reps 3 --bench-args "--model resnet50" red1k=TONY_BN_RED_WGS=1024 red2k=TONY_BN_RED_WGS=2048 ;;
     ab_mask) step ab_mask 600 python tools/ab_r3.py --reps 3 --bench-args "--model resnet50" nomask=TONY_RES_MASK=0 ;;
