@@ -25,7 +25,8 @@ def _close_but_flips(a, b):
 @pytest.mark.parametrize("shape", [(4, 256, 14, 14, 1, 64), (2, 512, 7, 9, 1, 128), (4, 64, 16, 16, 1, 64),
                                    (4, 256, 16, 16, 2, 128)],
                          ids=["identity-256", "identity-512", "projection-s1", "projection-s2"])
-def test_identity_block_join_matches_autograd_sum(cuda, shape, monkeypatch):
+@pytest.mark.parametrize("masked", [True, False], ids=["masked", "dres"])
+def test_identity_block_join_matches_autograd_sum(cuda, shape, masked, monkeypatch):
     from tony_amd.models import resnet
     from tony_amd.models.layers import cast_model, init_weights
 
@@ -38,9 +39,20 @@ def test_identity_block_join_matches_autograd_sum(cuda, shape, monkeypatch):
     oh, ow = (h - 1) // stride + 1, (w - 1) // stride + 1
     g = _cl(torch.randn(n, 4 * width, oh, ow, device=cuda)).to(torch.bfloat16)
     grads = {}
+    from tony_amd.ops import residual
+
+    # the joined run parks the residual tail's dY + ReLU mask for conv1's dgrad epilogue (MaskedGrad),
+    # which must read them there: no materialised fallback
+    if masked:
+        from tony_amd.ops.bn import MaskedGrad
+
+        def _no_materialize(self):
+            raise AssertionError("MaskedGrad materialised: the dgrad epilogue did not take it")
+        monkeypatch.setattr(MaskedGrad, "materialize", _no_materialize)
     for join in (False, True):
         monkeypatch.setattr(resnet, "JOIN", join)
         monkeypatch.setattr(resnet, "DS_TONY", True)
+        monkeypatch.setattr(residual, "MASKED_JOIN", masked)
         blk.zero_grad(set_to_none=True)
         x = (x0 * 1).requires_grad_(True)  # a non-leaf copy per run (the join rides on the tensor)
         x.retain_grad()

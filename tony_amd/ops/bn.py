@@ -74,6 +74,33 @@ def _as_rows(t: torch.Tensor):
     return t, rv
 
 
+class MaskedGrad:
+    """A residual tail's d(identity) = dY * (y > 0) left unmaterialised: the dY rows (bf16, dense
+    channels_last) and the forward's ReLU byte mask (_res_mask).  The conv consumer that runs second
+    reads both in its dgrad epilogue (csrc/gemm.hip flags bit5) -- the tail's backward then writes dZ
+    only, one activation-sized store fewer per identity block -- and anything else materialises it."""
+
+    __slots__ = ("dy", "mask")
+
+    def __init__(self, dy: torch.Tensor, mask: torch.Tensor):
+        self.dy, self.mask = dy, mask
+
+    @property
+    def device(self):
+        return self.dy.device
+
+    @property
+    def is_cuda(self):
+        return self.dy.is_cuda
+
+    def materialize(self) -> torch.Tensor:
+        n, c, h, w = self.dy.shape
+        shifts = torch.arange(8, device=self.mask.device, dtype=torch.uint8)
+        bits = ((self.mask.unsqueeze(-1) >> shifts) & 1).reshape(n * h * w, c)  # channel 8 * j + e
+        rows = self.dy.permute(0, 2, 3, 1).reshape(n * h * w, c)
+        return (rows * bits.to(rows.dtype)).view(n, h, w, c).permute(0, 3, 1, 2)
+
+
 def _accum_ok(t: torch.Tensor, x_shape) -> bool:
     """``t`` can take a dgrad epilogue's accumulating store: bf16, x's shape, dense channels_last rows."""
     if t.dtype != torch.bfloat16 or tuple(t.shape) != tuple(x_shape) or t.data_ptr() % 16:

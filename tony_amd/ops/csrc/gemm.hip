@@ -125,9 +125,13 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(const uint16_t* __res
   // tile staged through LDS and written back with 16-byte coalesced stores.
   // epi bit0: BN statistics into stats (sharded); bit1: stats holds [scale | shift] for the folded
   // inference BN (H5), bit2: ReLU after it
+  // bit5: C = tile + (stats as bf16 rows) masked by (sstride as a byte-mask pointer), see tony_gemm_bf16
+  const bool am = (epi & 32) != 0;
   nt_epilogue<BM, BN, TM, TN>(acc, smem, C, ldc, M, N, m0, n0,
                                (epi & 1) ? stats + shard_off(tm, sstride) : nullptr,
-                               (epi & 2) ? stats : nullptr, (epi & 4) != 0, RowMap{}, (epi & 8) != 0, (epi & 16) != 0);
+                               (epi & 2) ? stats : nullptr, (epi & 4) != 0, RowMap{}, (epi & 8) != 0,
+                               (epi & 48) != 0, am ? reinterpret_cast<const uint16_t*>(stats) : nullptr,
+                               am ? reinterpret_cast<const uint8_t*>(sstride) : nullptr);
 }
 
 template <int BM, int BN>
@@ -166,7 +170,10 @@ int launch_bm(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, i
 
 // flags bit0: compute column statistics into stats[2N] (zero on entry; kStatShards copies sstride
 // floats apart when sstride > 0, common.h); bit1: C = bf16(acc * stats[col] + stats[N + col]) (folded
-// inference BN), bit2: ReLU after it; bits 8..15: tile variant (kNtVariants, mfma_common.h).
+// inference BN), bit2: ReLU after it; bit4: C += the product; bit5: C = the product + S masked by
+// Mk, with S = stats read as a bf16 [M, ldc] matrix and Mk = sstride read as the address of its ReLU
+// byte mask [M, ldc / 8] (ops/residual.py MaskedGrad: a residual tail's d(identity), never
+// materialised); bits 8..15: tile variant (kNtVariants, mfma_common.h).
 TONY_API int tony_gemm_bf16(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
                             int64_t ldb, int64_t ldc, int flags, float* stats, int64_t sstride, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || sstride < 0) return -1;
@@ -175,9 +182,12 @@ TONY_API int tony_gemm_bf16(const void* A, const void* B, void* C, int64_t M, in
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -1;
   // bit0: st is accumulated into with atomics (the caller hands it over zeroed, ops/arena.py);
   // bit1: st = [scale | shift] of the folded inference BN, bit2: ReLU after it (H5)
-  const int epi = flags & 31;  // bit3: fp32 output; bit4: C += the product (nt_epilogue accum)
+  const int epi = flags & 63;  // bit3: fp32 output; bit4: C += the product (nt_epilogue accum)
   if ((epi & 1) && (epi & 2)) return -1;
   if ((epi & 16) && (epi & 3)) return -1;  // no statistics / folded BN on an accumulating store
+  if ((epi & 32) && ((epi & 31) || stats == nullptr || sstride == 0 || (ldc % 8) ||
+                     (reinterpret_cast<uintptr_t>(stats) & 15)))
+    return -1;
   if ((epi & 3) && stats == nullptr) return -1;
   float* st = stats;
   const int v = (flags >> 8) & 0xff;

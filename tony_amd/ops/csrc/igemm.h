@@ -310,10 +310,12 @@ __global__ __launch_bounds__(kThreads) void conv_glds_kernel(Gather g, const uin
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's zero fills land before LDS is reused
   __syncthreads();
+  const bool am = (epi & 32) != 0;  // masked-source accumulate (tony_gemm_bf16 flags bit5)
   nt_epilogue<BM, BN, TM, TN, ST * STAGE>(acc, smem, C, ldc, M, N, m0, n0,
                                            (epi & 1) ? stats + shard_off(tm, sstride) : nullptr,
                                            (epi & 2) ? stats : nullptr, (epi & 4) != 0, RowMap{}, (epi & 8) != 0,
-                                           (epi & 16) != 0);
+                                           (epi & 48) != 0, am ? reinterpret_cast<const uint16_t*>(stats) : nullptr,
+                                           am ? reinterpret_cast<const uint8_t*>(sstride) : nullptr);
 }
 
 // B rows n = [K] at row stride ldb (the conv weights [Co][R][S][Ci]: ldb = K)

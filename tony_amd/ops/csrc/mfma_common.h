@@ -179,10 +179,15 @@ template <int BM, int BN, int TM, int TN, int LDS_ELEMS = 2 * (BM + BN) * BK>
 __device__ __forceinline__ void nt_epilogue(f32x4 (&acc)[TM][TN], uint16_t* smem, uint16_t* __restrict__ C,
                                             int64_t ldc, int M, int N, int m0, int n0, float* __restrict__ stats,
                                             const float* __restrict__ aff = nullptr, bool relu = false,
-                                            const RowMap rm = RowMap{}, bool f32out = false, bool accum = false) {
+                                            const RowMap rm = RowMap{}, bool f32out = false, bool accum = false,
+                                            const uint16_t* __restrict__ asrc = nullptr,
+                                            const uint8_t* __restrict__ amask = nullptr) {
   // accum: C += the tile (bf16: the stored bf16 tile and C's old value summed in fp32 and rounded once,
   // as the separate add kernel it replaces did) -- a backward-data GEMM adding its dX into the gradient
   // another consumer of the same input already wrote (ResNet's identity path, ops/residual.py)
+  // asrc / amask (bf16 C-shaped, row stride ldc, and its ReLU byte mask, row stride ldc / 8): C = the
+  // tile + asrc masked by amask -- the other consumer's gradient dY * (y > 0) of a residual tail read
+  // where it lies instead of materialised first (ops/residual.py MaskedGrad); C's old value is unused
   constexpr int WM = BM / 2, WN = BN / 2;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -276,13 +281,27 @@ __device__ __forceinline__ void nt_epilogue(f32x4 (&acc)[TM][TN], uint16_t* smem
       if (accum) {
         float a[8], b[8];
         load8(src).to_float(a);
-        load8(dst).to_float(b);
+        if (asrc != nullptr) {
+          const int64_t pix = rm.pixel(grow);
+          load8(asrc + pix * ldc + gcol).to_float(b);
+          const unsigned bits = amask[pix * (ldc >> 3) + (gcol >> 3)];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) a[e] += b[e];
+          for (int e = 0; e < 8; ++e) a[e] += ((bits >> e) & 1u) ? b[e] : 0.f;
+        } else {
+          load8(dst).to_float(b);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a[e] += b[e];
+        }
         store8(dst, bf16x8::from_float(a));
       } else {
         *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
       }
+    } else if (accum && asrc != nullptr) {
+      const int64_t pix = rm.pixel(grow);
+      const unsigned bits = amask[pix * (ldc >> 3) + (gcol >> 3)];
+      const uint16_t* as = asrc + pix * ldc + gcol;
+      for (int e = 0; e < 8 && gcol + e < N; ++e)
+        dst[e] = f2bf(bf2f(src[e]) + (((bits >> e) & 1u) ? bf2f(as[e]) : 0.f));
     } else {
       for (int e = 0; e < 8 && gcol + e < N; ++e) dst[e] = accum ? f2bf(bf2f(src[e]) + bf2f(dst[e])) : src[e];
     }

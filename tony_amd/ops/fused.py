@@ -35,7 +35,7 @@ from torch import nn
 
 from . import _lib, concat, streams, tape, tune, wt_cache
 from .arena import zeros_f32
-from .bn import _accum_ok, _as_rows, _rows_view
+from .bn import MaskedGrad, _accum_ok, _as_rows, _rows_view
 from .gemm import wgrad_tn
 
 _BF16 = torch.bfloat16
@@ -227,11 +227,23 @@ class _HeadFn(torch.autograd.Function):
             streams.run(lambda: wgrad_tn(dZ.data_ptr(), ctot, x.data_ptr(), ldx, M, ctot, cin, dev, dst=gw), dZ, x)
         dx = None
         join = getattr(ctx, "join", None) if ctx.needs_input_grad[0] else None
-        pend = join.take() if join is not None else None
+        pend = join.take(masked_ok=True) if join is not None else None
         if ctx.needs_input_grad[0]:
             wt = wt_cache.transposed(weight).reshape(cin, ctot)  # [Cin, Ctot]
             dx = _cl_empty(n, cin, h, w, dev)
             vf = tune.gemm_flags(dZ, wt, dx, M, cin, ctot, ctot, False)  # timing runs write dx, never pend
+            if isinstance(pend, MaskedGrad):
+                # the residual tail parked dY and its ReLU mask: the epilogue writes dX + dY * mask (bit 5;
+                # the source rows ride in the stats argument, the mask's address in sstride)
+                if tuple(pend.dy.shape) == tuple(x.shape) and pend.mask.shape == (M, cin // 8):
+                    rc = L.tony_gemm_bf16(dZ.data_ptr(), wt.data_ptr(), dx.data_ptr(), M, cin, ctot, ctot, ctot, cin,
+                                          vf | 32, pend.dy.data_ptr(), pend.mask.data_ptr(), stream)
+                    if rc == 0:
+                        pend = None
+                        vf = None
+                if pend is not None:
+                    pend = pend.materialize()
+        if ctx.needs_input_grad[0] and vf is not None:
             if pend is not None and _accum_ok(pend, x.shape):
                 # x's other consumer (the identity path) already wrote its gradient: the epilogue adds
                 # dX into it (bit 4) -- no separate add kernel

@@ -21,7 +21,7 @@ import torch
 
 from . import _lib, streams, tape, tune, wt_cache
 from .arena import zeros_f32
-from .bn import _as_rows, _empty_like_rows, _rows_view
+from .bn import MaskedGrad, _as_rows, _empty_like_rows, _rows_view
 from .fused import _cl_empty
 from .gemm import wgrad_tn
 
@@ -53,29 +53,47 @@ class GradJoin:
         self.pending = grad
         self.stream = torch.cuda.current_stream(grad.device) if grad.is_cuda else None
 
-    def _ordered(self, g: torch.Tensor) -> torch.Tensor:
+    def _ordered(self, g):
         """``g`` (parked on self.stream) usable on the current stream."""
         if self.stream is not None:
             cur = torch.cuda.current_stream(g.device)
             if cur is not self.stream:
                 streams.fork(self.stream, cur)
-                streams.keep(g)
+                if isinstance(g, MaskedGrad):
+                    streams.keep(g.dy, g.mask)
+                else:
+                    streams.keep(g)
         return g
+
+    def wants_masked(self) -> bool:
+        """The caller (a residual tail) runs first and another consumer follows: it may park a MaskedGrad."""
+        return MASKED_JOIN and self.pending is None and self.ran + 1 < self.n
+
+    def park_masked(self, dy: torch.Tensor, mask: torch.Tensor):
+        self.ran += 1
+        self._hold(MaskedGrad(dy, mask))
+        return None
 
     def park(self, grad):
         self.ran += 1
         if self.pending is not None:  # a conv consumer ran first and parked its dX
-            grad = self._ordered(self.pending).add_(grad)
+            p = self._ordered(self.pending)
+            grad = (p.materialize() if isinstance(p, MaskedGrad) else p).add_(grad)
             self.pending = None
         if grad is None or self.ran >= self.n:
             return grad
         self._hold(grad)
         return None
 
-    def take(self):
+    def take(self, masked_ok: bool = False):
+        """The parked gradient (None: this consumer is the first); a MaskedGrad only for ``masked_ok``
+        callers, materialised for the others."""
         self.ran += 1
         g, self.pending = self.pending, None
-        return self._ordered(g) if g is not None else None
+        if g is None:
+            return None
+        g = self._ordered(g)
+        return g.materialize() if isinstance(g, MaskedGrad) and not masked_ok else g
 
     def settle(self, dx):
         if dx is None or self.ran >= self.n:
@@ -83,6 +101,10 @@ class GradJoin:
         self._hold(dx)
         return None
 
+
+# TONY_MASKED_JOIN=0: the residual tail writes d(identity) for the GradJoin instead of parking dY and its
+# ReLU mask for the conv consumer's dgrad epilogue to read (MaskedGrad)
+MASKED_JOIN = os.environ.get("TONY_MASKED_JOIN", "1") != "0"
 
 # TONY_RES_MASK=0: the residual BN backward re-reads y for its ReLU mask instead of the forward's byte
 # mask (1 bit per element: y is a 51-205 MB activation read twice per block backward)
@@ -234,8 +256,12 @@ class _Conv1x1BNAddReLUFn(torch.autograd.Function):
         M, cin, ldx = _rows_view(x)
         n, _, h, w = x.shape
         cout = weight.shape[0]
+        masked = False
+        if ctx.join is not None and y.dtype == torch.uint8 and ctx.join.wants_masked():
+            dy, (_, _, lddy) = _as_rows(dy)
+            masked = lddy == cout and dy.data_ptr() % 16 == 0 and tuple(dy.shape) == (n, cout, h, w)
         dZ, dres, (dg, db) = _bwd_res(L, Z, cout, dy, y, M, cout, mean, invstd, gamma, beta, ctx.pb, ctx.params[1:],
-                                      stream)
+                                      stream, want_dres=not masked)
         gw = _lib.grad_slot(ctx.params[0])
         dw = None
         if gw is not None and dg is None:  # dW summed straight into the flat gradient slot (side stream)
@@ -251,7 +277,9 @@ class _Conv1x1BNAddReLUFn(torch.autograd.Function):
             dw = wgrad_tn(dZ.data_ptr(), cout, x.data_ptr(), ldx, M, cout, cin, dev).to(weight.dtype)
             dw = dw.reshape(weight.shape)
         _lib.report_inplace(ctx.params, (dw, dg, db))
-        if ctx.join is not None:  # conv1's dgrad adds its dX into it, or it already ran (GradJoin)
+        if masked:  # conv1's dgrad epilogue adds dY * mask to its dX (GradJoin, MaskedGrad)
+            dres = ctx.join.park_masked(dy, y)
+        elif ctx.join is not None:  # conv1's dgrad adds its dX into it, or it already ran (GradJoin)
             dres = ctx.join.park(dres)
         return dx, dw, dres, dg, db, None, None, None, None, None
 

@@ -33,6 +33,7 @@ for s in "$@"; do
     ab_r50) step ab_r50 1000 python tools/ab_r3.py --reps 2 --bench-args "--model resnet50" fused_red=TONY_BN_FUSED_REDUCE=1 onepass16=TONY_BN_ONEPASS=1,TONY_BN_ONEPASS_MAX_MB=16 occ2=TONY_WGRAD_OCC=2 tbm128=TONY_WGRAD_TBM96=0 urgent0=TONY_WGRAD_URGENT_MB=0 ;;
     gemm) step gemm_resnet 300 python tools/gemm_bench.py --resnet
           step gemm_incep 300 python tools/gemm_bench.py ;;
+    ab_masked) step ab_masked 700 python tools/ab_r3.py --reps 3 --bench-args "--model resnet50" dres=TONY_MASKED_JOIN=0 ;;
     ab_red) step ab_red 700 python tools/ab_r3.py --reps 3 red1k=TONY_BN_RED_WGS=1024 red2k=TONY_BN_RED_WGS=2048 ;;
     ab_red_r50) step ab_red_r50 700 python tools/ab_r3.py --reps 3 --bench-args "--model resnet50" red1k=TONY_BN_RED_WGS=1024 red2k=TONY_BN_RED_WGS=2048 ;;
     ab_mask) step ab_mask 600 python tools/ab_r3.py --reps 3 --bench-args "--model resnet50" nomask=TONY_RES_MASK=0 ;;
