@@ -256,11 +256,18 @@ def test_halo_tile_conv3x3(cuda, shape):
         assert _rel(dx, xr.grad) < 1e-2, f"halo dgrad rel {_rel(dx, xr.grad):.4f}"
 
 
+@pytest.mark.parametrize("mode", ["gather", "dy", "bnred"])
 @pytest.mark.parametrize("shape", [(2, 32, 37, 37, 64, 1), (2, 80, 35, 35, 192, 0)])  # M >= MIN_ROWS: both paths on tony kernels
-def test_conv_bn_act_pool_fused_matches_unfused(cuda, shape):
+def test_conv_bn_act_pool_fused_matches_unfused(cuda, shape, mode, monkeypatch):
     """conv -> BN -> ReLU -> maxpool 3x3/2 as one BN+ReLU+pool kernel == conv_bn_act then max_pool
-    (outputs, running statistics, input / weight / gamma / beta gradients)."""
+    (outputs, running statistics, input / weight / gamma / beta gradients).  Backward modes: the pooled
+    gradient gathered inside the BN reduce and apply (default), the full-resolution dY written by the
+    pool backward, and that dY with the BN reduction fused into the pool backward."""
+    from tony_amd.ops import conv as conv_mod
     from tony_amd.ops.conv import conv_bn_act, conv_bn_act_pool
+
+    monkeypatch.setattr(conv_mod, "POOL_BN_GATHER", mode == "gather")
+    monkeypatch.setattr(conv_mod, "POOL_BNRED", mode == "bnred")
     from tony_amd.ops.pool import max_pool
 
     n, ci, h, w, co, p = shape

@@ -116,9 +116,12 @@ _SIGNATURES = {
                          c_void_p],
     "tony_maxpool_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
                          c_void_p],
+    "tony_bn_bwd_pool_apply": [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                               c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                               c_void_p, c_int64, c_void_p, c_void_p, c_int, c_void_p],
     "tony_maxpool_bwd_acc": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
                          c_void_p],
-    "tony_maxpool_bwd_bnred": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64,
+    "tony_maxpool_bwd_bnred": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int64,
                                c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                c_void_p, c_int64, c_int, c_void_p],
     "tony_avgpool_fwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],

@@ -307,6 +307,13 @@ FUSED_REDUCE_HITS = [0]  # BN backward passes that used a dgrad-fused reduction 
 # TONY_POOL_BNRED=1: the stem max-pool backward also reduces the BN-backward sums (one kernel
 # instead of two); opt-in, measured no faster end to end (see _FR above)
 POOL_BNRED = os.environ.get("TONY_POOL_BNRED", "0") == "1"
+# TONY_POOL_BN_GATHER=1: the conv -> BN -> ReLU -> max-pool backward never writes the full-resolution dY:
+# the pooled gradient is gathered twice, in the BN reduction (csrc/pool.hip maxpool_bwd_bnred_kernel
+# without the store) and in the BN apply (csrc/bn_act.hip bn_bwd_pool_apply_kernel).  Opt-in: it saves
+# 3 passes over dY but the gathers are latency-bound -- 161 + 166 us vs 103 (pool backward) + 96
+# (reduce) + 107 (apply) at ResNet's 112x112x64 stem, end to end within noise on both models
+# (profiles/r3s2_rejected_pool_bn_gather.log)
+POOL_BN_GATHER = os.environ.get("TONY_POOL_BN_GATHER", "0") == "1"
 
 
 def _dgrad_fused_bn(ctx, dy, weight, x_shape, stride, padding):
@@ -694,25 +701,32 @@ class _ConvBNActFn(torch.autograd.Function):
         return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None
 
 
-def _conv_bn_backward(ctx, x, weight, gamma, beta, mean, invstd, Z, dy, presums=None):
-    """BN(+ReLU) backward from Z (the ReLU mask is recomputed from it), then the conv's wgrad (side
-    stream when active) and dgrad; parameter gradients go straight into their flat slots.
-    ``presums``: the BN reduction already computed by the kernel that produced dy."""
-    L = _lib.lib()
-    stride, padding, relu, pb = ctx.cfg
-    dev = x.device
-    M, co, ldz = _rows_view(Z)
-    if presums is None:
-        presums = _bn_presums(ctx, dy)  # reduced by the consumer's dgrad epilogue
-    dy, (_, _, lddy) = _as_rows(dy)
-    dZ = torch.empty_like(Z)
-    ws = None if presums is not None else zeros_f32(_lib.bn_bwd_ws_floats(co), dev)
+def _bn_grad_slots(ctx, gamma, beta):
+    """(dgamma, dbeta, inplace): the flat-buffer gradient slots when the trainer made them, else new."""
     gg, gb = _lib.grad_slot(ctx.params[1]), _lib.grad_slot(ctx.params[2])
     inplace = gg is not None and gb is not None
-    dgamma = gg if inplace else torch.empty_like(gamma)
-    dbeta = gb if inplace else torch.empty_like(beta)
-    _lib.bn_bwd(Z, ldz, dy, lddy, dZ, ldz, M, co, mean, invstd, gamma, beta, pb, relu, ws, dgamma, dbeta, inplace,
-                dev, sums=presums)
+    return (gg if inplace else torch.empty_like(gamma)), (gb if inplace else torch.empty_like(beta)), inplace
+
+
+def _conv_bn_backward(ctx, x, weight, gamma, beta, mean, invstd, Z, dy, presums=None, done=None):
+    """BN(+ReLU) backward from Z (the ReLU mask is recomputed from it), then the conv's wgrad (side
+    stream when active) and dgrad; parameter gradients go straight into their flat slots.
+    ``presums``: the BN reduction already computed by the kernel that produced dy.  ``done``: the BN
+    backward already ran (dZ, dgamma, dbeta, inplace), e.g. fused with a max-pool backward."""
+    stride, padding, relu, pb = ctx.cfg
+    dev = x.device
+    if done is not None:
+        dZ, dgamma, dbeta, inplace = done
+    else:
+        M, co, ldz = _rows_view(Z)
+        if presums is None:
+            presums = _bn_presums(ctx, dy)  # reduced by the consumer's dgrad epilogue
+        dy, (_, _, lddy) = _as_rows(dy)
+        dZ = torch.empty_like(Z)
+        ws = None if presums is not None else zeros_f32(_lib.bn_bwd_ws_floats(co), dev)
+        dgamma, dbeta, inplace = _bn_grad_slots(ctx, gamma, beta)
+        _lib.bn_bwd(Z, ldz, dy, lddy, dZ, ldz, M, co, mean, invstd, gamma, beta, pb, relu, ws, dgamma, dbeta, inplace,
+                    dev, sums=presums)
     dw = _wgrad(dZ, x, weight, stride, padding)  # first: overlaps the dgrad on the side stream
     join = getattr(ctx, "join", None) if ctx.needs_input_grad[0] else None
     pend = join.take() if join is not None else None
@@ -770,8 +784,30 @@ class _ConvBNActPoolFn(torch.autograd.Function):
         k, s, p = ctx.pool
         n, co, h, w = Z.shape
         dyp, (_, _, lddy) = _as_rows(dyp)
+        if POOL_BN_GATHER:
+            # the full-resolution dY is never made: the pool backward's gather runs twice, once reducing
+            # the BN sums beside Z (no store) and once inside the BN apply that writes dZ
+            L, dev = _lib.lib(), Z.device
+            _, _, ldz = _rows_view(Z)
+            stream = _lib.stream_ptr(dev)
+            sums = zeros_f32(_lib.stat_floats(co), dev)
+            rc = L.tony_maxpool_bwd_bnred(dyp.data_ptr(), arg.data_ptr(), None, n, h, w, co, k, s, p, lddy, co,
+                                          Z.data_ptr(), ldz, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
+                                          beta.data_ptr(), ctx.cfg[3], 1, sums.data_ptr(), 2 * co, _lib.num_cus(dev),
+                                          stream)
+            _lib.check(rc, "tony_maxpool_bwd_bnred")
+            dZ = torch.empty_like(Z)
+            dgamma, dbeta, inplace = _bn_grad_slots(ctx, gamma, beta)
+            rc = L.tony_bn_bwd_pool_apply(dyp.data_ptr(), lddy, arg.data_ptr(), n, h, w, co, k, s, p, Z.data_ptr(), ldz,
+                                          dZ.data_ptr(), ldz, mean.data_ptr(), invstd.data_ptr(), gamma.data_ptr(),
+                                          beta.data_ptr(), ctx.cfg[3], 1, sums.data_ptr(), 2 * co, dgamma.data_ptr(),
+                                          dbeta.data_ptr(), int(inplace), stream)
+            _lib.check(rc, "tony_bn_bwd_pool_apply")
+            dx, dw, dgamma, dbeta = _conv_bn_backward(ctx, x, weight, gamma, beta, mean, invstd, Z, None,
+                                                      done=(dZ, dgamma, dbeta, inplace))
+            return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None
         dy = _cl_empty(n, co, h, w, Z.device)
-        if not POOL_BNRED or p:  # the fused bnred pool backward has no padding
+        if not POOL_BNRED:
             rc = _lib.lib().tony_maxpool_bwd(dyp.data_ptr(), arg.data_ptr(), dy.data_ptr(), n, h, w, co, k, s, p, lddy,
                                              co, _lib.stream_ptr(Z.device))
             _lib.check(rc, "tony_maxpool_bwd")
@@ -781,7 +817,7 @@ class _ConvBNActPoolFn(torch.autograd.Function):
         # the separate two-pass reduce over Z and dY (354 / 155 MB each at the Inception stem) disappears
         _, _, ldz = _rows_view(Z)
         sums = zeros_f32(_lib.stat_floats(co), Z.device)
-        rc = _lib.lib().tony_maxpool_bwd_bnred(dyp.data_ptr(), arg.data_ptr(), dy.data_ptr(), n, h, w, co, k, s,
+        rc = _lib.lib().tony_maxpool_bwd_bnred(dyp.data_ptr(), arg.data_ptr(), dy.data_ptr(), n, h, w, co, k, s, p,
                                                lddy, co, Z.data_ptr(), ldz, mean.data_ptr(), invstd.data_ptr(),
                                                gamma.data_ptr(), beta.data_ptr(), ctx.cfg[3], 1, sums.data_ptr(),
                                                2 * co, _lib.num_cus(Z.device), _lib.stream_ptr(Z.device))

@@ -744,6 +744,99 @@ __global__ __launch_bounds__(kThreads) void bn_relu_maxpool_kernel(
   }
 }
 
+// BN(+ReLU) backward apply of the layer a KxK / stride-S max pool (padding P) read, with the pool's
+// backward gathered in: each lane's dY[site, 8 channels] is summed from the <= ceil(K/S)^2 windows
+// that cover the site and chose it (argmax byte == the site's window position), exactly as
+// csrc/pool.hip maxpool_bwd_kernel writes it, and goes straight into dZ = dY'*q0 + Z*q1 + q2 -- the
+// full-resolution dY (354 / 248 MB at Inception's two stem pools, 205 MB at ResNet's) is never
+// stored nor read back.  The sums come from the pool backward's fused reduction (pool.hip
+// maxpool_bwd_bnred_kernel with no dX store).  Rows per workgroup, thread map and the per-channel
+// coefficient table in LDS as in bn_bwd_apply_kernel.
+__global__ __launch_bounds__(kThreads) void bn_bwd_pool_apply_kernel(
+    const uint16_t* __restrict__ dyp, int64_t lddy, const uint8_t* __restrict__ arg, int N, int H, int W, int C,
+    int OH, int OW, int K, int S, int P, const uint16_t* __restrict__ z, int64_t ldz, uint16_t* __restrict__ dz,
+    int64_t lddz, int64_t rows_per_block, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const void* gamma, const void* beta, int param_bf16, int relu, const float* __restrict__ dsum, int64_t sstride,
+    void* dgamma, void* dbeta, int accumulate) {
+  const int64_t M = static_cast<int64_t>(N) * H * W;
+  const float inv_m = 1.f / static_cast<float>(M);
+  float* tab = bn_dyn;  // [5][C] per workgroup (bn_bwd_apply_kernel's table): the sharded sums are read
+                        // C times per workgroup, not 8 x 2 x kStatShards times per lane
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    const float g = load_param(gamma, c, param_bf16, 1.f), be = load_param(beta, c, param_bf16, 0.f);
+    const float ds = shard_sum(dsum, c, sstride), dsx = shard_sum(dsum + C, c, sstride);
+    const float mu = mean[c], is = invstd[c];
+    const float k = g * is, am = ds * inv_m, bm = dsx * inv_m;
+    tab[0 * C + c] = k;
+    tab[1 * C + c] = -k * bm * is;
+    tab[2 * C + c] = k * (bm * is * mu - am);
+    tab[3 * C + c] = k;
+    tab[4 * C + c] = be - k * mu;
+    if (blockIdx.x == 0) {
+      store_param(dbeta, c, param_bf16, ds, accumulate);
+      store_param(dgamma, c, param_bf16, dsx, accumulate);
+    }
+  }
+  __syncthreads();
+  RowMap rm(C);
+  if (!rm.active) return;
+  float q0[8], q1[8], q2[8], q3[8], q4[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = rm.cg * 8 + j;
+    q0[j] = tab[0 * C + c];
+    q1[j] = tab[1 * C + c];
+    q2[j] = tab[2 * C + c];
+    q3[j] = tab[3 * C + c];
+    q4[j] = tab[4 * C + c];
+  }
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  // (n, h, w) of the site walked incrementally: one 32-bit decomposition per lane, not four 64-bit
+  // divisions per row (emulated: they made this kernel ALU-bound at 1.9 TB/s)
+  const uint32_t first = static_cast<uint32_t>(r0 + rm.rsub);
+  int w = static_cast<int>(first % static_cast<uint32_t>(W));
+  const uint32_t nh0 = first / static_cast<uint32_t>(W);
+  int h = static_cast<int>(nh0 % static_cast<uint32_t>(H));
+  int64_t n = nh0 / static_cast<uint32_t>(H);
+  for (int64_t site = r0 + rm.rsub; site < r1; site += rm.RPI) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int hp = h + P, wp = w + P;  // windows oh with oh*S <= hp <= oh*S + K - 1
+    const int oh_lo = hp >= K ? (hp - K + S) / S : 0, oh_hi = min(OH - 1, hp / S);
+    const int ow_lo = wp >= K ? (wp - K + S) / S : 0, ow_hi = min(OW - 1, wp / S);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const uint32_t local = static_cast<uint32_t>((hp - oh * S) * K + (wp - ow * S));
+        const int64_t osite = (n * OH + oh) * OW + ow;
+        const uint2 packed = *reinterpret_cast<const uint2*>(arg + osite * C + rm.cg * 8);
+        float g[8];
+        V8<uint16_t>::load(dyp + osite * lddy + rm.cg * 8).to_float(g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t word = j < 4 ? packed.x : packed.y;
+          if (((word >> (8 * (j & 3))) & 0xffu) == local) acc[j] += g[j];
+        }
+      }
+    }
+    float d[8], xf[8], o[8];
+    V8<uint16_t>::from_float(acc).to_float(d);  // the bf16 dY the unfused pool backward would store
+    V8<uint16_t>::load(z + site * ldz + rm.cg * 8).to_float(xf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float dd = (relu && fmaf(xf[j], q3[j], q4[j]) <= 0.f) ? 0.f : d[j];
+      o[j] = fmaf(dd, q0[j], fmaf(xf[j], q1[j], q2[j]));
+    }
+    V8<uint16_t>::from_float(o).store(dz + site * lddz + rm.cg * 8);
+    for (w += rm.RPI; w >= W;) {
+      w -= W;
+      if (++h == H) {
+        h = 0;
+        ++n;
+      }
+    }
+  }
+}
+
 }  // namespace
 
 // ---- composable entry points (the fused conv heads call these on channel sub-ranges) ----
@@ -1139,6 +1232,32 @@ TONY_API int tony_bn_relu_maxpool(const void* z, int64_t ldz, const float* sum, 
       static_cast<const uint16_t*>(z), ldz, sum, sumsq, sstride, gamma, beta, param_bf16, eps, save_mean, save_invstd,
       running_mean, running_var, momentum, static_cast<uint16_t*>(y), ldy, static_cast<uint8_t*>(argmax), N, H, W, C,
       OH, OW, K, S, P);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// dZ of conv -> BN -> ReLU -> maxpool KxK/S (padding P) from the POOLED gradient dYp [N*OH*OW, C] (row
+// stride lddy) and the pool's argmax bytes (bn_bwd_pool_apply_kernel); dsum = [dsum | dsumx] from
+// pool.hip tony_maxpool_bwd_bnred (sharded, sstride floats apart); dgamma / dbeta stored (or added).
+TONY_API int tony_bn_bwd_pool_apply(const void* dyp, int64_t lddy, const void* argmax, int N, int H, int W, int C, int K,
+                                    int S, int P, const void* z, int64_t ldz, void* dz, int64_t lddz, const float* mean,
+                                    const float* invstd, const void* gamma, const void* beta, int param_bf16, int relu,
+                                    const float* dsum, int64_t sstride, void* dgamma, void* dbeta, int accumulate,
+                                    hipStream_t stream) {
+  if (bad_c(C) || (lddy % 8) || (ldz % 8) || (lddz % 8) || K < 1 || S < 1 || P < 0 || 2 * P >= K + 1 ||
+      H + 2 * P < K || W + 2 * P < K || z == nullptr || dz == nullptr || dyp == nullptr || argmax == nullptr ||
+      mean == nullptr || invstd == nullptr || dsum == nullptr || sstride < 0)
+    return -1;
+  const int64_t M = static_cast<int64_t>(N) * H * W;
+  if (M * (C / 8) > 0x7fffffff) return -1;
+  const int OH = (H + 2 * P - K) / S + 1, OW = (W + 2 * P - K) / S + 1;
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 4, 8192, &rpb, &grid);
+  bn_bwd_pool_apply_kernel<<<grid, kThreads, bn_lds_table(C, 5), stream>>>(
+      static_cast<const uint16_t*>(dyp), lddy, static_cast<const uint8_t*>(argmax), N, H, W, C, OH, OW, K, S, P,
+      static_cast<const uint16_t*>(z), ldz, static_cast<uint16_t*>(dz), lddz, rpb, mean, invstd, gamma, beta,
+      param_bf16, relu, dsum, sstride, dgamma, dbeta, accumulate);
   TONY_LAUNCH_CHECK();
   return 0;
 }

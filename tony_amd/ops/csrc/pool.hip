@@ -200,7 +200,7 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd_kernel(const T* __restri
 // added once per workgroup into the sharded [dsum | dsumx] buffer.
 __global__ __launch_bounds__(kThreads) void maxpool_bwd_bnred_kernel(
     const uint16_t* __restrict__ dy, const uint8_t* __restrict__ arg, uint16_t* __restrict__ dx, int N, int H,
-    int W, int C, int OH, int OW, int K, int S, int64_t lddy, int64_t lddx, int64_t sites_per_block,
+    int W, int C, int OH, int OW, int K, int S, int P, int64_t lddy, int64_t lddx, int64_t sites_per_block,
     const uint16_t* __restrict__ z, int64_t ldz, const float* __restrict__ mean, const float* __restrict__ invstd,
     const void* gamma, const void* beta, int pb, int relu, float* __restrict__ dsum, int64_t sstride) {
   __shared__ float red[2 * kThreads * 8];
@@ -226,19 +226,22 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd_bnred_kernel(
   const int64_t s0 = static_cast<int64_t>(blockIdx.x) * sites_per_block;
   const int64_t s1 = min(total, s0 + sites_per_block);
   if (active) {
+    // (n, h, w) walked incrementally (one 32-bit decomposition per lane: 64-bit divisions are emulated)
+    const uint32_t first = static_cast<uint32_t>(s0 + rsub);
+    int w = static_cast<int>(first % static_cast<uint32_t>(W));
+    const uint32_t nh0 = first / static_cast<uint32_t>(W);
+    int h = static_cast<int>(nh0 % static_cast<uint32_t>(H));
+    int64_t n = nh0 / static_cast<uint32_t>(H);
     for (int64_t site = s0 + rsub; site < s1; site += RPI) {
-      const int w = static_cast<int>(site % W);
-      const int64_t nh = site / W;
-      const int h = static_cast<int>(nh % H);
-      const int64_t n = nh / H;
       float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      const int oh_lo = h >= K ? (h - K + S) / S : 0;
-      const int oh_hi = min(OH - 1, h / S);
-      const int ow_lo = w >= K ? (w - K + S) / S : 0;
-      const int ow_hi = min(OW - 1, w / S);
+      const int hp = h + P, wp = w + P;  // the padded coordinate
+      const int oh_lo = hp >= K ? (hp - K + S) / S : 0;
+      const int oh_hi = min(OH - 1, hp / S);
+      const int ow_lo = wp >= K ? (wp - K + S) / S : 0;
+      const int ow_hi = min(OW - 1, wp / S);
       for (int oh = oh_lo; oh <= oh_hi; ++oh) {
         for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-          const int local = (h - oh * S) * K + (w - ow * S);
+          const int local = (hp - oh * S) * K + (wp - ow * S);
           const int64_t osite = (n * OH + oh) * OW + ow;
           const uint2 packed = *reinterpret_cast<const uint2*>(arg + osite * C + cg * 8);
           float g[8];
@@ -251,7 +254,7 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd_bnred_kernel(
         }
       }
       const bf16x8 o = bf16x8::from_float(acc);
-      store8(dx + site * lddx + cg * 8, o);
+      if (dx != nullptr) store8(dx + site * lddx + cg * 8, o);  // none: the BN apply gathers it again
       float d[8], zf[8];
       o.to_float(d);  // the stored bf16 values, as a separate reduce kernel would read them
       load8(z + site * ldz + cg * 8).to_float(zf);
@@ -260,6 +263,13 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd_bnred_kernel(
         const float v = (relu && fmaf(zf[j], p2[j], p3[j]) <= 0.f) ? 0.f : d[j];
         a[j] += v;
         b[j] = fmaf(v, fmaf(zf[j], p0[j], p1[j]), b[j]);
+      }
+      for (w += RPI; w >= W;) {
+        w -= W;
+        if (++h == H) {
+          h = 0;
+          ++n;
+        }
       }
     }
 #pragma unroll
@@ -412,22 +422,26 @@ TONY_API int tony_maxpool_bwd_acc(const void* dy, const void* argmax, void* dx, 
 
 // tony_maxpool_bwd + the BN-backward reduction of Z (the pool input's BN input, rows = dX pixels):
 // [dsum | dsumx] (kStatShards copies sstride floats apart, zeroed) accumulate sum dY', sum dY' xhat.
+// Padding P as tony_maxpool_bwd; dx == nullptr: the reduction only (bn_act.hip tony_bn_bwd_pool_apply
+// gathers dY again, so it is never stored).
 TONY_API int tony_maxpool_bwd_bnred(const void* dy, const void* argmax, void* dx, int N, int H, int W, int C, int K,
-                                    int S, int64_t lddy, int64_t lddx, const void* z, int64_t ldz, const float* mean,
-                                    const float* invstd, const void* gamma, const void* beta, int pb, int relu,
-                                    float* dsum, int64_t sstride, int num_cus, hipStream_t stream) {
-  if (C % 8 || C > 2048 || lddy % 8 || lddx % 8 || ldz % 8 || H < K || W < K || z == nullptr || mean == nullptr ||
-      invstd == nullptr || dsum == nullptr || (reinterpret_cast<uintptr_t>(z) & 15) || sstride < 0)
+                                    int S, int P, int64_t lddy, int64_t lddx, const void* z, int64_t ldz,
+                                    const float* mean, const float* invstd, const void* gamma, const void* beta, int pb,
+                                    int relu, float* dsum, int64_t sstride, int num_cus, hipStream_t stream) {
+  if (C % 8 || C > 2048 || lddy % 8 || lddx % 8 || ldz % 8 || P < 0 || 2 * P >= K + 1 || H + 2 * P < K ||
+      W + 2 * P < K || S < 1 || z == nullptr || mean == nullptr || invstd == nullptr || dsum == nullptr ||
+      (reinterpret_cast<uintptr_t>(z) & 15) || sstride < 0)
     return -1;
   const int64_t total = static_cast<int64_t>(N) * H * W;
   if (total * (C / 8) > 0x7fffffff) return -1;
-  const int OH = (H - K) / S + 1, OW = (W - K) / S + 1;
+  const int OH = (H + 2 * P - K) / S + 1, OW = (W + 2 * P - K) / S + 1;
+  // 4 workgroups per CU: 16 measured slower (187 vs 166 us at ResNet's 112x112x64 stem)
   const int64_t blocks = std::min<int64_t>(4 * static_cast<int64_t>(num_cus > 0 ? num_cus : 256),
                                            (total + 63) / 64);
   const int64_t per = (total + blocks - 1) / blocks;
   maxpool_bwd_bnred_kernel<<<static_cast<int>((total + per - 1) / per), kThreads, 0, stream>>>(
       static_cast<const uint16_t*>(dy), static_cast<const uint8_t*>(argmax), static_cast<uint16_t*>(dx), N, H, W, C,
-      OH, OW, K, S, lddy, lddx, per, static_cast<const uint16_t*>(z), ldz, mean, invstd, gamma, beta, pb, relu, dsum,
+      OH, OW, K, S, P, lddy, lddx, per, static_cast<const uint16_t*>(z), ldz, mean, invstd, gamma, beta, pb, relu, dsum,
       sstride);
   TONY_LAUNCH_CHECK();
   return 0;

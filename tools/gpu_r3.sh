@@ -34,6 +34,9 @@ for s in "$@"; do
     gemm) step gemm_resnet 300 python tools/gemm_bench.py --resnet
           step gemm_incep 300 python tools/gemm_bench.py ;;
     ab_masked) step ab_masked 700 python tools/ab_r3.py --reps 3 --bench-args "--model resnet50" dres=TONY_MASKED_JOIN=0 ;;
+    pool_tests) step pool_tests 400 python -u -m pytest tests/test_conv_gpu.py tests/test_ops_gpu.py -x -q --timeout 240 --timeout-method thread -k "pool or stem" ;;
+    ab_gather) step ab_gather 700 python tools/ab_r3.py --reps 3 dy=TONY_POOL_BN_GATHER=0 ;;
+    ab_gather_r50) step ab_gather_r50 700 python tools/ab_r3.py --reps 3 --bench-args "--model resnet50" dy=TONY_POOL_BN_GATHER=0 ;;
     ab_red) step ab_red 700 python tools/ab_r3.py --reps 3 red1k=TONY_BN_RED_WGS=1024 red2k=TONY_BN_RED_WGS=2048 ;;
     ab_red_r50) step ab_red_r50 700 python tools/ab_r3.py --reps 3 --bench-args "--model resnet50" red1k=TONY_BN_RED_WGS=1024 red2k=TONY_BN_RED_WGS=2048 ;;
     ab_mask) step ab_mask 600 python tools/ab_r3.py --reps 3 --bench-args "--model resnet50" nomask=TONY_RES_MASK=0 ;;
