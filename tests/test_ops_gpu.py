@@ -612,3 +612,27 @@ def test_whole_input_conv_bn_is_gemm(cuda):
     assert rel(g.grad, gr.grad) < 3e-2 and rel(b.grad, br.grad) < 3e-2
     impls = {k[0]: v for k, v in C.choices().items() if k[1] in (tuple(x.shape), (n, co, 1, 1))}
     assert set(impls.values()) == {"gemm"}, impls
+
+
+@pytest.mark.parametrize("splits,n", [(128, 18432), (40, 4096), (7, 1 << 20), (3, 4000), (300, 221184)],
+                         ids=["narrow-128", "narrow-40", "wide-7", "few-3", "wide-300"])
+@pytest.mark.parametrize("bf16", [False, True])
+def test_splitk_reduce_sums_the_slab(cuda, splits, n, bf16):
+    """csrc/splitk.hip: dst (+)= sum over splits of slab rows (many splits of a small dW, few of a large
+    one, n not a multiple of the block), into fp32 and bf16 gradient slots, with and without accumulation."""
+    from tony_amd.ops import _lib
+
+    torch.manual_seed(0)
+    slab = torch.randn(splits, n, device=cuda)
+    ref = slab.double().sum(0)
+    dt = torch.bfloat16 if bf16 else torch.float32
+    L, st = _lib.lib(), _lib.stream_ptr(cuda)
+    for acc in (0, 1):
+        base = torch.randn(n, device=cuda).to(dt)
+        dst = base.clone()
+        rc = L.tony_splitk_reduce(slab.data_ptr(), splits, n, dst.data_ptr(), int(bf16), acc, _lib.num_cus(cuda), st)
+        assert rc == 0
+        torch.cuda.synchronize()
+        want = ref + (base.double() if acc else 0)
+        tol = 1e-2 * (splits ** 0.5) if bf16 else 1e-4 * splits ** 0.5
+        torch.testing.assert_close(dst.double(), want.to(dt).double(), rtol=1e-2 if bf16 else 1e-5, atol=tol)

@@ -37,6 +37,7 @@ for s in "$@"; do
     pool_tests) step pool_tests 400 python -u -m pytest tests/test_conv_gpu.py tests/test_ops_gpu.py -x -q --timeout 240 --timeout-method thread -k "pool or stem" ;;
     ab_gather) step ab_gather 700 python tools/ab_r3.py --reps 3 dy=TONY_POOL_BN_GATHER=0 ;;
     ab_gather_r50) step ab_gather_r50 700 python tools/ab_r3.py --reps 3 --bench-args "--model resnet50" dy=TONY_POOL_BN_GATHER=0 ;;
+    splitk_tests) step splitk_tests 300 python -u -m pytest tests/test_ops_gpu.py tests/test_conv_gpu.py -x -q --timeout 120 --timeout-method thread -k "splitk or wgrad" ;;
     ab_red) step ab_red 700 python tools/ab_r3.py --reps 3 red1k=TONY_BN_RED_WGS=1024 red2k=TONY_BN_RED_WGS=2048 ;;
     ab_red_r50) step ab_red_r50 700 python tools/ab_r3.py --reps 3 --bench-args "--model resnet50" red1k=TONY_BN_RED_WGS=1024 red2k=TONY_BN_RED_WGS=2048 ;;
     ab_mask) step ab_mask 600 python tools/ab_r3.py --reps 3 --bench-args "--model resnet50" nomask=TONY_RES_MASK=0 ;;
