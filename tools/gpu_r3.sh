@@ -44,6 +44,8 @@ for s in "$@"; do
     ab2) step ab2 700 python tools/ab_r3.py --reps 3 fr_auto=TONY_BN_FUSED_REDUCE=auto fr_auto32=TONY_BN_FUSED_REDUCE=auto,TONY_BN_FUSED_REDUCE_MIN_MB=32 urgent0=TONY_WGRAD_URGENT_MB=0 ;;
     ab_so_r50) step ab_so_r50 700 python tools/ab_r3.py --reps 3 --bench-args "--model resnet50" old_so=TONY_KERNELS_SO=$(pwd)/tony_amd/ops/_tony_kernels_ab.so ;;
     bn_tests) step bn_tests 400 python -u -m pytest tests/test_ops_gpu.py -x -q --timeout 240 --timeout-method thread -k "bn or batch or residual" ;;
+    ab_so_plan) step ab_so_plan 700 python tools/ab_r3.py --reps 3 --mode graph old_so=TONY_KERNELS_SO=$(pwd)/tony_amd/ops/_tony_kernels_ab.so ;;
+    ab_so_plan_r50) step ab_so_plan_r50 700 python tools/ab_r3.py --reps 3 --mode graph --bench-args "--model resnet50" old_so=TONY_KERNELS_SO=$(pwd)/tony_amd/ops/_tony_kernels_ab.so ;;
     ab_so) step ab_so 700 python tools/ab_r3.py --reps 3 old_so=TONY_KERNELS_SO=$(pwd)/tony_amd/ops/_tony_kernels_ab.so ;;
     # alternating A/B of the opt-in environment toggles against the default step (tools/ab_r3.py)
     ab) step ab 1000 python tools/ab_r3.py --reps 2 onepass16=TONY_BN_ONEPASS=1,TONY_BN_ONEPASS_MAX_MB=16 fused_red=TONY_BN_FUSED_REDUCE=1 pool_bnred=TONY_POOL_BNRED=1 occ2=TONY_WGRAD_OCC=2 nobranch=TONY_BRANCH_STREAMS=0 wbatch1=TONY_WGRAD_BATCH=1 ;;
