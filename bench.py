@@ -79,6 +79,11 @@ def parse():
     ap.add_argument("--collective", default=None, choices=["rccl", "hip"],
                     help="gradient push / pull collectives: RCCL (default) or tony_amd's xGMI peer-memory "
                          "kernels (csrc/xgmi.hip); sets TONY_COLLECTIVE")
+    ap.add_argument("--fp32-row", type=int, default=1,
+                    help="N=1 bf16 runs: also time the reference-precision (x3 fp32) step in a child process and "
+                         "report it as the record's fp32_row (0: skip)")
+    ap.add_argument("--fp32-steps", type=int, default=10)
+    ap.add_argument("--fp32-warmup", type=int, default=3)
     ap.add_argument("--no-miopen-find", action="store_true",
                     help="MIOpen immediate mode instead of find (faster startup, slower non-1x1 convs)")
     return ap.parse_args()
@@ -90,8 +95,10 @@ def fail(msg: str, code: int = 4) -> int:
 
 
 class _PSOnly:
-    """The dedicated ps rank's step: no model, just the bucketed reduce -> apply -> broadcast, issued
-    in the same collective order as the workers' (so the bench loop is identical on every rank)."""
+    """The dedicated ps rank's step: no model.  On the xGMI plane (default) it launches the apply
+    kernels that sum the workers' gradient rows as they land in its receive windows and store the new
+    variables into every worker's landing window; on the RCCL plane (TONY_PS_PLANE=rccl) it runs the
+    bucketed reduce -> apply -> broadcast in the workers' collective order."""
 
     def __init__(self, ps, dev):
         self.ps = ps
@@ -262,12 +269,9 @@ def main():
     if args.tune_cache and os.path.exists(args.tune_cache):
         tune_loaded = tune.load(args.tune_cache)
     mode = "eager" if args.no_graph else args.mode
-    if mode == "auto" and world > 1 and os.environ.get("TONY_BENCH_AUTO_PLAN", "0") != "1":
-        # several ranks: the eager step overlaps the bucketed PS push / apply / pull with backward.  The
-        # native plan can too (per-bucket plan segments, parallel/trainer.py _replay_overlapped), but its
-        # 2-rank rehearsal failed to replay (tony_plan_replay: hipErrorInvalidValue on one rank,
-        # profiles/r3s2_bench2_auto_plan_replay_fail.log), so auto keeps to eager at N > 1 until it is
-        # fixed; --mode graph still selects it (TONY_BENCH_AUTO_PLAN=1: time both, for rehearsals)
+    if mode == "auto" and world > 1 and os.environ.get("TONY_BENCH_AUTO_PLAN", "1") == "0":
+        # escape hatch: eager at N > 1 without timing the native plan (auto times both by default; the
+        # plan replays per-bucket segments so the PS collectives still overlap backward)
         mode = "eager"
     if ps.is_worker:
         trainer = Trainer(model, ps, loss_fn, use_graph=mode != "eager", overlap_wgrad=not args.no_wgrad_stream,
@@ -370,6 +374,31 @@ def main():
     # the dedicated ps rank runs no model: report a worker's loss
     final_loss = max_over_ranks(float(loss.float().item()) if ps.is_worker else float("-inf"), device=dev)
     fallbacks = coll.fallback_count()
+    # this rank's engine: in --ps-mode dedicated rank 0 is the ps (no model, no step plan), so the
+    # record carries the first worker's engine / host statistics (gathered from every rank)
+    eng = {
+        "hip_graph": mode == "graph" and getattr(trainer, "replay_kind", None) == "graph",
+        # plan: the step captured once and re-issued natively (ops/plan.py, csrc/plan.hip)
+        "step_mode": "plan" if mode == "graph" and getattr(trainer, "replay_kind", None) == "plan" else mode,
+        "plan_stats": trainer.plan.stats if getattr(trainer, "plan", None) is not None else None,
+        "plan_error": getattr(trainer, "plan_error", None),
+        "buckets_overlapped_with_backward": ps.overlapped_buckets,
+        "host_ms_per_step": round(1000.0 * host / args.steps, 3),
+        "gpu_ms_per_step_host_ahead": gpu_ahead,
+        "host_ms_per_step_unblocked": None if host_free is None else round(1000.0 * host_free, 3),
+        "host_fwd_bwd_ms_last_eager_step": [round(1000.0 * trainer.host_fwd_s, 3), round(1000.0 * trainer.host_bwd_s, 3)],
+        "conv_impl": _conv_impl_counts(),
+    }
+    engines = [eng]
+    if world > 1:
+        engines = [None] * world
+        dist.all_gather_object(engines, eng)
+    eng_rank = ps.worker_ranks[0] if ps.worker_ranks else 0
+    eng = dict(engines[eng_rank], engine_of_rank=eng_rank)
+    fp32_row = None
+    if world == 1 and args.fp32_row and args.dtype == "bf16" and args.model == "inception_v3" and not args.stock:
+        # reference precision under the same clock discipline: the x3 fp32 step in a child process
+        fp32_row = _fp32_row(args)
     if rank == 0:
         imgs = args.batch * n_workers * args.steps
         value = imgs / elapsed
@@ -403,28 +432,17 @@ def main():
                 "grad_dtype": "fp32" if grad_dtype == torch.float32 else "bf16",
                 "variables": f"fp32 master on the PS, {args.dtype} compute copy",
                 "optimizer": "fused SGD-momentum (HIP)" if args.optimizer == "sgd" else args.optimizer,
-                "hip_graph": mode == "graph" and getattr(trainer, "replay_kind", None) == "graph",
-                # plan: the step captured once and re-issued natively (ops/plan.py, csrc/plan.hip)
-                "step_mode": "plan" if mode == "graph" and getattr(trainer, "replay_kind", None) == "plan" else mode,
-                "plan_stats": trainer.plan.stats if getattr(trainer, "plan", None) is not None else None,
-                "plan_error": getattr(trainer, "plan_error", None),
+                **eng,
                 "mode_setup_ms": setup or None,
                 "tune_cache_loaded": tune_loaded,
                 "wgrad_stream": not args.no_wgrad_stream,
                 "branch_streams": _branch_streams_on(args),
                 "grad_buckets": len(ps.buckets),
-                "buckets_overlapped_with_backward": ps.overlapped_buckets,
                 "phase_ms_eager_step_max_over_ranks":
                     dict(zip(("forward", "backward", "exposed_ps_push_apply_pull"), [round(v, 3) for v in phases])),
-                "host_ms_per_step": round(1000.0 * host / args.steps, 3),
-                "gpu_ms_per_step_host_ahead": gpu_ahead,
-                "host_ms_per_step_unblocked": None if host_free is None else round(1000.0 * host_free, 3),
-                "host_fwd_bwd_ms_last_eager_step": [round(1000.0 * trainer.host_fwd_s, 3),
-                                                    round(1000.0 * trainer.host_bwd_s, 3)],
                 "kernels": "tony_amd HIP" if fused else (
                     "tony_amd HIP, fp32 via x3-split bf16 MFMA products (ops/x3.py)" if x3
                     else "stock PyTorch-ROCm (MIOpen / hipBLASLt)"),
-                "conv_impl": _conv_impl_counts(),
                 "collective": "hip-xgmi" if os.environ.get("TONY_COLLECTIVE", "rccl").lower() in ("hip", "xgmi")
                 else ("rccl" if dist.is_initialized() and dist.get_backend() == "nccl" else None),
                 "collective_fallbacks": fallbacks,
@@ -432,6 +450,11 @@ def main():
                 "final_loss": round(final_loss, 4),
             },
         }
+        if fp32_row is not None:
+            # the reference's precision (TF's Inception-v3 PS job is fp32 end to end): same model and
+            # batch, fp32 activations / gradients / variables, conv and GEMM products as x3-split
+            # bf16 MFMAs (ops/x3.py); timed by its own barrier + synchronize bracket in a child process
+            rec["fp32_row"] = fp32_row
         print(json.dumps(rec), flush=True)
     rc = 0
     if os.environ.get("TONY_COLLECTIVE", "rccl").lower() in ("hip", "xgmi") and fallbacks:
@@ -441,6 +464,32 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     return rc
+
+
+def _fp32_row(args) -> dict:
+    """Run ``bench.py --dtype fp32`` (same model, batch and issue mode) as a child process -- never an
+    exec from this GPU-initialised process -- and return its timing as the fp32 row."""
+    import subprocess
+
+    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--steps", str(args.fp32_steps),
+           "--warmup", str(args.fp32_warmup), "--batch", str(args.batch), "--dtype", "fp32", "--fp32-row", "0",
+           "--mode", "eager" if args.no_graph else args.mode]
+    env = dict(os.environ)
+    env.pop("RANK", None)
+    t = time.perf_counter()
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": "fp32 child timed out"}
+    line = next((ln for ln in reversed(p.stdout.splitlines()) if ln.startswith("{")), None)
+    if p.returncode != 0 or line is None:
+        tail = (p.stderr or "").strip().splitlines()[-3:]
+        return {"error": f"fp32 child rc={p.returncode}: {' | '.join(tail)}"}
+    r = json.loads(line)
+    c = r.get("config", {})
+    return {"value": r["value"], "unit": r["unit"], "ms_per_step": r["ms_per_step"], "steps": r["steps"],
+            "warmup": r["warmup"], "dtype": "fp32", "kernels": c.get("kernels"), "step_mode": c.get("step_mode"),
+            "final_loss": c.get("final_loss"), "child_wall_s": round(time.perf_counter() - t, 1)}
 
 
 def _branch_streams_on(args) -> bool:

@@ -674,14 +674,15 @@ def test_flat_sgd_resync_reseeds_master_from_changed_compute_copy():
 
 
 def test_gpu_pinning_env_modes():
-    """what each visible-devices mode exports.  none (default) keeps every GPU visible for
-    RCCL P2P / peer-memory mapping and names the task's GPUs by HIP ordinal; hip / rocr hide the rest."""
+    """what each visible-devices mode exports.  none keeps every GPU visible for RCCL P2P /
+    peer-memory mapping and names the task's GPUs by HIP ordinal; hip / rocr hide the rest (auto, the
+    default, resolves to one of them per job: resolve_visible_mode)."""
     from tony_amd.cluster.coordinator import gpu_pinning_env
     from tony_amd.conf import Configuration
     from tony_amd.conf import keys as K
     from tony_amd.native import GpuDevice
 
-    assert Configuration().get(K.AMD_VISIBLE_DEVICES_MODE) == "none"
+    assert Configuration().get(K.AMD_VISIBLE_DEVICES_MODE) == "auto"
     devs = [GpuDevice(i, bdf=f"0000:{0x10 * (i + 1):02x}:00.0", numa_node=0, fake=True) for i in range(8)]
     hip_ord = {0: 3, 1: 2, 2: 1, 3: 0, 4: 4, 5: 5, 6: 6, 7: 7}  # amd-smi order != HIP order
     e = gpu_pinning_env("none", [1], hip_ord, devs)
@@ -693,6 +694,29 @@ def test_gpu_pinning_env_modes():
     assert e["ROCR_VISIBLE_DEVICES"] == "1" and "HIP_VISIBLE_DEVICES" not in e
     with pytest.raises(ValueError):
         gpu_pinning_env("cuda", [0], hip_ord, devs)
+
+
+def test_visible_mode_auto_isolates_unless_a_peer_plane_is_configured():
+    """the default (auto) keeps per-task HIP_VISIBLE_DEVICES isolation for arbitrary user
+    programs and leaves every GPU visible only for jobs on a peer-mapping tony_amd data plane."""
+    from tony_amd.cluster.coordinator import resolve_visible_mode
+    from tony_amd.conf import Configuration
+
+    def conf(**kv):
+        c = Configuration()
+        for k, v in kv.items():
+            c.set(k.replace("__", "."), str(v))
+        return c
+
+    assert resolve_visible_mode(conf()) == "hip"  # a plain job
+    assert resolve_visible_mode(conf(tony__application__framework="pytorch", tony__worker__instances=4)) == "hip"
+    assert resolve_visible_mode(conf(tony__amd__collective="hip")) == "none"
+    assert resolve_visible_mode(conf(tony__ps__instances=1, tony__worker__instances=4)) == "none"
+    assert resolve_visible_mode(conf(tony__ps__instances=1, **{"tony__amd__ps-plane": "rccl"})) == "hip"
+    assert resolve_visible_mode(conf(tony__application__framework="pytorch", tony__ps__instances=1)) == "hip"
+    for m in ("none", "hip", "rocr"):
+        assert resolve_visible_mode(conf(**{"tony__amd__visible-devices-mode": m, "tony__amd__collective": "hip"})) == m
+    assert Configuration().get("tony.amd.visible-devices-mode") == "auto"
 
 
 def test_verify_visible_device_in_all_visible_mode(monkeypatch):

@@ -159,7 +159,7 @@ def test_inception_fp32_step_matches_float64(cuda):
     # Gradients: the classifiers' are pinned to their inputs' accuracy.  Upstream of them, a ReLU whose pre-activation lies
     # within the x3 products' rounding (2^-16 relative) of 0 takes the other side in float64: at batch 4
     # about one element per layer does (BN beta = 0, so pre-activation ~ xhat), and each flip moves dbeta
-    # and dW of its layer by one |dY| / |dY * x| term (0.1-0.7 % of the norm, tools/diag/x3_block.py:
+    # and dW of its layer by one |dY| / |dY * x| term (0.1-0.7 % of the norm, tools/x3_block.py:
     # every sub-layer output gradient of an Inception-E block matches to 2.5e-8 while its dbeta carries
     # such a step).  Accumulated over ~90 layers of backward that reaches ~10 % by the stem, so the rest
     # of the network is held to the gradient direction.  Every single pass is pinned to 1e-4 through the

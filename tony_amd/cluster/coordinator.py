@@ -67,19 +67,38 @@ def _default_history_root(conf, staging_root: str) -> str:
     return loc
 
 
+def resolve_visible_mode(conf) -> str:
+    """``tony.amd.visible-devices-mode`` for a job: ``none`` / ``hip`` / ``rocr`` as configured, and for
+    ``auto`` (the default) ``none`` only when the job runs a tony_amd data plane that maps a peer GPU's
+    memory -- ``tony.amd.collective=hip`` (the xGMI collective kernels), or a TensorFlow job with ps tasks
+    on the xGMI parameter-server plane (``tony.amd.ps-plane``, default xgmi; parallel/ps_plane.py) --
+    and ``hip`` (per-task HIP_VISIBLE_DEVICES) for everything else, so an arbitrary user program that
+    picks ``cuda:0`` or ``cuda:LOCAL_RANK`` cannot land on another task's GPU."""
+    mode = (conf.get(K.AMD_VISIBLE_DEVICES_MODE, "auto") or "auto").lower()
+    if mode != "auto":
+        return mode
+    if conf.get(K.AMD_COLLECTIVE, "rccl").lower() in ("hip", "xgmi"):
+        return "none"
+    framework = conf.get(K.FRAMEWORK_NAME, "tensorflow").lower()
+    if framework == "tensorflow" and conf.get_int("tony.ps.instances", 0) > 0 \
+            and conf.get(K.AMD_PS_PLANE, "xgmi").lower() == "xgmi":
+        return "none"
+    return "hip"
+
+
 def gpu_pinning_env(mode: str, gpus, hip_ordinal, devices) -> dict:
     """Environment that pins a task to its GPUs (SURVEY §7.4 hard part 6: isolation vs P2P).
 
-    ``none`` (default): every GPU stays visible, so RCCL keeps its xGMI P2P transport and the tony_amd
-    data planes can map peer memory (hipIpcOpenMemHandle needs the peer device in the process);
-    the task's GPUs are named by their HIP ordinals in TONY_HIP_ORDINALS and parallel/bootstrap.py
-    selects the first one (``torch.cuda.set_device``).  ``hip`` / ``rocr``: HIP_VISIBLE_DEVICES /
-    ROCR_VISIBLE_DEVICES hide every other GPU (hard isolation; a data plane that needs a peer's
-    memory cannot run).  Either way TONY_GPU_BDFS lets the task verify it got the GPU it was
-    allocated (gpu/inventory.verify_visible_device)."""
-    mode = (mode or "none").lower()
+    ``none``: every GPU stays visible, so RCCL keeps its xGMI P2P transport and the tony_amd data
+    planes can map peer memory (hipIpcOpenMemHandle needs the peer device in the process); the task's
+    GPUs are named by their HIP ordinals in TONY_HIP_ORDINALS and parallel/bootstrap.py selects the
+    first one (``torch.cuda.set_device``).  ``hip`` / ``rocr``: HIP_VISIBLE_DEVICES /
+    ROCR_VISIBLE_DEVICES hide every other GPU (hard isolation; a data plane that needs a peer's memory
+    cannot run).  ``resolve_visible_mode`` picks between them for ``auto``.  Either way TONY_GPU_BDFS
+    lets the task verify it got the GPU it was allocated (gpu/inventory.verify_visible_device)."""
+    mode = (mode or "hip").lower()
     if mode not in ("none", "hip", "rocr"):
-        raise ValueError(f"tony.amd.visible-devices-mode must be none, hip or rocr, not {mode!r}")
+        raise ValueError(f"tony.amd.visible-devices-mode must be auto, none, hip or rocr, not {mode!r}")
     ordinals = ",".join(str(hip_ordinal.get(g, g)) for g in gpus)
     devs = {d.index: d for d in devices}
     env = {"TONY_GPU_BDFS": ",".join(devs[g].bdf for g in gpus if g in devs), "TONY_VISIBLE_MODE": mode,
@@ -422,6 +441,7 @@ class Coordinator:
             env[C.TONY_TOKEN_FILE] = os.path.join(self.job_dir, "token")
         # data-plane collectives of the tony_amd jobs: RCCL or the xGMI peer-memory kernels
         env["TONY_COLLECTIVE"] = c.get(K.AMD_COLLECTIVE, "rccl").lower()
+        env["TONY_PS_PLANE"] = c.get(K.AMD_PS_PLANE, "xgmi").lower()
         # whether the ps tasks own GPUs (the Inception PS job picks its topology from it on every task)
         env["TONY_PS_GPUS"] = str(c.get_int("tony.ps.gpus", 0))
         if slot is not None and slot.gpus:
@@ -432,7 +452,7 @@ class Coordinator:
             env[C.TONY_NUMA_NODE] = str(slot.numa_node)
             if slot.cpus and c.get_bool(K.AMD_NUMA_BIND, True):
                 env["TONY_CPUS"] = ",".join(str(x) for x in slot.cpus)
-            env.update(gpu_pinning_env(c.get(K.AMD_VISIBLE_DEVICES_MODE, "none"), slot.gpus, self.hip_ordinal,
+            env.update(gpu_pinning_env(resolve_visible_mode(c), slot.gpus, self.hip_ordinal,
                                        self.allocator.devices))
             task.info.gpus = ids
         if c.get_bool(K.DOCKER_ENABLED, False):

@@ -91,11 +91,13 @@ def main(argv=None) -> int:
     if mode == "dedicated" and not ps.sync and ps.plane is None:
         raise SystemExit("--async needs the xGMI PS data plane (GPU ranks)")
 
+    from tony_amd.ops import cross_entropy  # fused HIP softmax-xent on GPU tensors, torch's on CPU
+
     def loss_fn(out, y):
         logits, aux = out if isinstance(out, tuple) else (out, None)
-        loss = torch.nn.functional.cross_entropy(logits.float(), y)
+        loss = cross_entropy(logits, y)
         if aux is not None:
-            loss = loss + 0.4 * torch.nn.functional.cross_entropy(aux.float(), y)
+            loss = loss + 0.4 * cross_entropy(aux, y)
         return loss
 
     total = a.warmup + a.steps

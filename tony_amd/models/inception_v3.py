@@ -23,6 +23,7 @@ import torch
 from torch import nn
 
 from ..ops.concat import Slot, assemble, concat_buffer
+from ..ops.dropout import Dropout as TonyDropout
 from ..ops.pool import avg_pool, avg_pool3x3_s1, global_avg_pool, max_pool
 from ..ops import conv as conv_ops
 from ..ops import streams, tape
@@ -274,7 +275,8 @@ class InceptionV3(nn.Module):
                                      InceptionC(768, 160, **kw), InceptionC(768, 192, **kw))
         self.aux = InceptionAux(768, num_classes, **kw) if aux_logits else None
         self.mixed_7 = nn.Sequential(InceptionD(768, **kw), InceptionE(1280, **kw), InceptionE(2048, **kw))
-        self.dropout = nn.Dropout(dropout)
+        # tony dropout (device-side step counter: fresh masks under plan / graph replay) on the tony paths
+        self.dropout = TonyDropout(dropout) if (fused or x3) else nn.Dropout(dropout)
         self.fc = (LinearX3 if x3 else Linear if fused else nn.Linear)(2048, num_classes)
         self.fused = fused
         self.x3 = x3

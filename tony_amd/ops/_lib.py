@@ -88,6 +88,9 @@ _SIGNATURES = {
     "tony_xent_fwd": [c_void_p, c_int, c_int64, c_int, c_int64, c_void_p, c_float, c_void_p, c_void_p, c_void_p],
     "tony_xent_bwd": [c_void_p, c_int, c_int64, c_int, c_int64, c_void_p, c_float, c_void_p, c_void_p, c_void_p,
                       c_int64, c_void_p],
+    "tony_dropout_fwd": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_float, c_void_p, c_void_p],
+    "tony_dropout_bwd": [c_void_p, c_void_p, c_void_p, c_int64, c_int, c_float, c_void_p],
+    "tony_counter_bump": [c_void_p, c_void_p],
     "tony_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64,
                        c_int, c_void_p, c_int64, c_void_p],
     "tony_gemm_tn_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64,

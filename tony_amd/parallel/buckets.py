@@ -113,6 +113,7 @@ class GradBucketEngine:
             self.comm = torch.cuda.Stream(device=self.device)
             self._dev_index = self.comm.device_index
         self._hooks: Dict[int, object] = {}
+        self.attached = False  # listening (the hooks of fused-reported parameters are dropped after a step)
         self._inplace = [False] * len(flat.slots)  # reported by a fused op: its AccumulateGrad hook is dropped
         esz = flat.grad.element_size()
         self._slot_ptr = [flat.grad.data_ptr() + s.offset * esz for s in flat.slots]
@@ -134,13 +135,15 @@ class GradBucketEngine:
     # -- wiring ---------------------------------------------------------------------------------
     def attach(self) -> None:
         """Listen to the fused ops' in-place gradient reports and to AccumulateGrad hooks."""
-        if self._hooks:
+        if self.attached:
             return
+        self.attached = True
         _lib.add_grad_listener(self)
         for i, p in enumerate(self.flat.params):
             self._hooks[i] = p.register_post_accumulate_grad_hook(lambda p, i=i: self._on_accumulate(i, p))
 
     def detach(self) -> None:
+        self.attached = False
         _lib.remove_grad_listener(self)
         for h in self._hooks.values():
             h.remove()

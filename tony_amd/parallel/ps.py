@@ -146,7 +146,9 @@ class ParameterServer:
                 for b in self.buckets:
                     self._master_range[b.index] = (b.lo, b.numel)
         if plane == "auto":
-            plane = os.environ.get("TONY_PS_PLANE", "xgmi" if f.device.type == "cuda" else "rccl")
+            # tony.amd.ps-plane (TONY_PS_PLANE) selects the GPU data plane; CPU tensors always take the
+            # collective path (gloo)
+            plane = os.environ.get("TONY_PS_PLANE", "xgmi") if f.device.type == "cuda" else "rccl"
         self.plane_kind = plane if mode == "dedicated" and self.world > 1 else "rccl"
         if self.plane_kind not in ("xgmi", "rccl"):
             raise ValueError(f"unknown PS data plane {plane!r}")

@@ -260,8 +260,10 @@ class Trainer:
         # several ranks + native replay: the buckets' launch points are captured as plan markers, so
         # replays can overlap the collectives (which stay outside the graph) with backward
         eng = getattr(self.ps, "engine", None)
+        # (``attached``, not ``_hooks``: after the first step every fused-reported parameter's hook is
+        # dropped, and testing the hooks disabled the markers -- buckets then all launched after backward)
         markers = native and not inside and self.overlap_comm and eng is not None and eng.comm is not None \
-            and bool(eng._hooks)
+            and eng.attached
 
         def body():
             if markers:

@@ -1,12 +1,12 @@
 #!/usr/bin/env python3
 """Alternating A/B of bench.py over environment toggles (one GPU).
 
-    python tools/ab_r3.py [--reps 2] [--mode eager] [--bench-args "..."] NAME=VAR=VAL[,VAR=VAL] ...
+    python tools/ab.py [--reps 2] [--mode eager] [--bench-args "..."] NAME=VAR=VAL[,VAR=VAL] ...
 
 ``base`` (no extra environment) always runs first in every repetition.  Each arm is one bench.py
 process (its own autotune), so the spread between repetitions of the same arm is the noise floor.
 Prints one line per run and a summary (best / mean ms_per_step per arm) and writes the JSON records to
-gpurun_out/ab_r3.json.
+gpurun_out/ab.json.
 """
 import argparse
 import json
@@ -54,7 +54,7 @@ def main():
     for name, recs in out.items():
         ms = [r["ms_per_step"] for r in recs]
         print(f"  {name:14s} {min(ms):7.3f} {sum(ms) / len(ms):7.3f}")
-    with open(os.path.join(ROOT, "gpurun_out", "ab_r3.json"), "w") as f:
+    with open(os.path.join(ROOT, "gpurun_out", "ab.json"), "w") as f:
         json.dump(out, f)
     return 0
 

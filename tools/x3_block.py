@@ -1,10 +1,10 @@
 """One Inception block of the fp32 (x3) model against its float64 twin: every sub-layer's output and
 output gradient (norm-relative), the block input gradient.
-usage: python tools/diag/x3_block.py [block, e.g. mixed_7.2] [batch]"""
+usage: python tools/x3_block.py [block, e.g. mixed_7.2] [batch]"""
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 

@@ -1,10 +1,10 @@
 """Piecewise check of one x3 (fp32) conv + BN + ReLU layer against float64: Z, the BN backward dZ and
 the weight gradient (from OUR dZ, so a wrong dZ and a wrong wgrad are told apart).
-usage: python tools/diag/x3_layer.py N C H W Co R S ph pw [stride]"""
+usage: python tools/x3_layer.py N C H W Co R S ph pw [stride]"""
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
