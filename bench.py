@@ -446,6 +446,8 @@ def main():
                 "collective": "hip-xgmi" if os.environ.get("TONY_COLLECTIVE", "rccl").lower() in ("hip", "xgmi")
                 else ("rccl" if dist.is_initialized() and dist.get_backend() == "nccl" else None),
                 "collective_fallbacks": fallbacks,
+                # init-time canaries of the hand data planes against RCCL (None: that plane unused)
+                "data_plane_verified": coll.data_plane_status(),
                 "dist": diag or None,
                 "final_loss": round(final_loss, 4),
             },

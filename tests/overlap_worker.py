@@ -64,18 +64,27 @@ def ddp_run(rank, kind, bucket_mb):
     from tony_amd.parallel.ddp import DistributedDataParallel
 
     dev = torch.device("cuda", 0)
+    x, y = _data(rank, kind, dev)
+    # this rank's own gradient without DDP (same init, same fused kernels): the parent checks DDP's
+    # averaged gradient against the mean of these over ranks -- not only that the ranks agree
+    ref = _model(kind, dev)
+    for p in ref.parameters():
+        p.data = p.data.to(torch.bfloat16)
+    cross_entropy(ref(x), y).backward()
+    local = {n: p.grad.float().cpu() for n, p in ref.named_parameters()}
+    del ref
     model = _model(kind, dev)
     for p in model.parameters():
         p.data = p.data.to(torch.bfloat16)
     ddp = DistributedDataParallel(model, bucket_mb=bucket_mb, device=dev)
-    x, y = _data(rank, kind, dev)
     from tony_amd.parallel import collectives as coll
 
     fb0 = coll.fallback_count()  # init-time broadcasts of small / int64 buffers may fall back; buckets may not
     ddp.zero_grad()
     cross_entropy(ddp(x), y).backward()
     torch.cuda.synchronize()
-    return {"grad": ddp.flat.grad.float().cpu(), "n_buckets": len(ddp.reducer.buckets),
+    named = {n: p.grad.float().cpu() for n, p in model.named_parameters()}
+    return {"grad": ddp.flat.grad.float().cpu(), "named": named, "local": local, "n_buckets": len(ddp.reducer.buckets),
             "overlapped": ddp.reducer.overlapped_buckets, "launches": ddp.reducer.launches,
             "train_fallbacks": coll.fallback_count() - fb0}
 
@@ -102,8 +111,14 @@ def run(rank, world, port, q, kind, bucket_mb):
         # by value: a tensor would travel as a shared-memory handle that dies with this process
         from tony_amd.parallel import collectives as coll
 
-        res = {k: {kk: vv.numpy() if isinstance(vv, torch.Tensor) else vv for kk, vv in v.items()}
-               for k, v in out.items()}
+        def val(v):
+            if isinstance(v, torch.Tensor):
+                return v.numpy()
+            if isinstance(v, dict):
+                return {k: val(x) for k, x in v.items()}
+            return v
+
+        res = {k: val(v) for k, v in out.items()}
         res["fallbacks"] = coll.fallback_count()
         q.put((rank, res))
     except Exception:  # noqa: BLE001 - reported to the parent

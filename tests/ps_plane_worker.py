@@ -181,6 +181,40 @@ def run_overlap(rank, world, port, q):
         res["workers_agree"] = all(torch.equal(allf[w], allf[ps.worker_ranks[0]]) for w in ps.worker_ranks)
         res["ps_matches_workers"] = bool(torch.equal(allf[0], allf[ps.worker_ranks[0]]))
         ps.plane.close()
+        if ps.is_ps:
+            # reference: the same sync-PS trajectory in one process -- each step every worker's gradient
+            # on its own batch (same fused kernels), their mean, SGD-momentum on an fp32 master, the
+            # bf16 copy for the next step.  Agreement among the ranks alone would pass a wrong-but-
+            # consistent sum (a worker dropped or counted twice, a missing 1/n).
+            ref = cast_model(init_weights(Net(), seed=1), torch.bfloat16, dev).to(memory_format=torch.channels_last)
+            names = [n for n, _ in ref.named_parameters()]
+            master = {n: p.detach().float().clone() for n, p in ref.named_parameters()}
+            w0 = {n: t.clone() for n, t in master.items()}
+            mom = {n: torch.zeros_like(t) for n, t in master.items()}
+            batches = []
+            for w in ps.worker_ranks:
+                gw = torch.Generator(device=dev).manual_seed(w)
+                xw = torch.randn((16, 16, 24, 24), generator=gw, device=dev).to(torch.bfloat16).contiguous(
+                    memory_format=torch.channels_last)
+                batches.append((xw, torch.randint(0, 16, (16,), generator=gw, device=dev)))
+            for _ in range(steps):
+                gsum = {n: torch.zeros_like(t) for n, t in master.items()}
+                for xw, yw in batches:
+                    for p in ref.parameters():
+                        p.grad = None
+                    cross_entropy(ref(xw), yw).backward()
+                    for n, p in ref.named_parameters():
+                        gsum[n] += p.grad.float()
+                with torch.no_grad():
+                    for n, p in ref.named_parameters():
+                        mom[n].mul_(0.9).add_(gsum[n] / len(batches))
+                        master[n].sub_(0.05 * mom[n])
+                        p.copy_(master[n].to(p.dtype))
+            got = dict(model.named_parameters())
+            num = sum(float((got[n].float() - w0[n] - (master[n] - w0[n])).norm() ** 2) for n in names) ** 0.5
+            den = sum(float((master[n] - w0[n]).norm() ** 2) for n in names) ** 0.5
+            res["update_rel_err_vs_reference"] = num / max(den, 1e-12)
+            res["matches_reference"] = res["update_rel_err_vs_reference"] < 0.05
         q.put((rank, res))
     except Exception as e:  # noqa: BLE001
         import traceback

@@ -757,9 +757,13 @@ def test_gpu_task_memory_sized_when_left_at_default():
     c.set("tony.evaluator.gpus", "1")
     c.set("tony.evaluator.memory", "8g")
     changed = U.size_gpu_task_memory(c)
-    assert changed == {"worker": 65536}
+    # the 0-GPU ps sits on a worker's GPU (tony.amd.ps-share-gpu): a GPU process, sized as one GPU
+    assert changed == {"worker": 65536, "ps": 32768}
     reqs = U.parse_container_requests(c)
-    assert reqs["worker"].memory_mb == 65536 and reqs["ps"].memory_mb == 2048 and reqs["evaluator"].memory_mb == 8192
+    assert reqs["worker"].memory_mb == 65536 and reqs["ps"].memory_mb == 32768 and reqs["evaluator"].memory_mb == 8192
+    c.set("tony.amd.ps-share-gpu", "false")
+    c.set("tony.ps.memory", "2g", source="tony-default.xml")
+    assert "ps" not in U.size_gpu_task_memory(c)
     assert "<name>tony.worker.memory</name>" in c.to_xml()
 
 
@@ -780,3 +784,32 @@ def test_ps_checkpoint_without_layout_is_refused():
     sd["layout"] = dict(ps.layout(), world=2)
     with pytest.raises(ValueError, match="does not match"):
         ps.load_state_dict(sd)
+
+
+def test_ps_shares_a_worker_gpu_policy_and_allocator():
+    """TonY's default 0-GPU ps of a GPU TensorFlow job is placed on a worker's GPU, shared
+    (the GPU stays owned by the worker; the ps is recorded as a sharer and released with its task)."""
+    from tony_amd.conf import Configuration
+    from tony_amd.gpu.inventory import GpuAllocator, discover
+    from tony_amd.utils import core as U
+
+    c = Configuration()
+    c.set("tony.ps.instances", "1")
+    c.set("tony.worker.instances", "4")
+    c.set("tony.worker.gpus", "1")
+    assert U.ps_shares_worker_gpu(c)
+    for k, v in (("tony.amd.ps-share-gpu", "false"), ("tony.ps.gpus", "1"), ("tony.application.framework", "pytorch"),
+                 ("tony.worker.gpus", "0")):
+        d = Configuration()
+        for kk, vv in (("tony.ps.instances", "1"), ("tony.worker.instances", "4"), ("tony.worker.gpus", "1")):
+            d.set(kk, vv)
+        d.set(k, v)
+        assert not U.ps_shares_worker_gpu(d), k
+    a = GpuAllocator(discover(4))
+    w0 = a.allocate("worker:0", 1)
+    assert w0.gpus == [0]
+    s = a.share("ps:0", w0.gpus[0])
+    assert s.gpus == [0] and a.owners() == {0: "worker:0"} and a.sharers() == {0: ["ps:0"]}
+    assert a.free_count() == 3  # sharing takes no GPU from the free list
+    a.release("ps:0")
+    assert a.sharers() == {} and a.owners() == {0: "worker:0"}

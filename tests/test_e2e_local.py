@@ -315,6 +315,27 @@ def test_gpu_pinning_and_numa_env(conf):
     assert rc == 0
 
 
+def test_zero_gpu_ps_shares_a_worker_gpu(conf, tmp_path):
+    """VERDICT r3 #1 (TonY default: ps tasks request no GPU): the ps of a GPU TensorFlow job is placed on
+    worker 0's GPU, shared, so "1 ps + N workers" fits N GPUs; visible-devices-mode auto leaves every GPU
+    visible for such a job (the xGMI PS plane maps peer memory) and the pinning names the shared GPU."""
+    rec = tmp_path / "rec"
+    rec.mkdir()
+    conf.set(K.AMD_VISIBLE_DEVICES_MODE, "auto")
+    rc, _ = run(conf, base("--executes", "record_gpu_env.py", "--conf", "tony.ps.instances=1",
+                           "--conf", "tony.worker.instances=2", "--conf", "tony.worker.gpus=1",
+                           "--shell_env", f"RECORD_DIR={rec}"))
+    assert rc == 0
+    env = {}
+    for f in rec.iterdir():
+        env[f.stem] = dict(line.strip().split("=", 1) for line in f.read_text().splitlines())
+    assert {"ps_0", "worker_0", "worker_1"} <= set(env), sorted(env)
+    assert env["worker_0"]["TONY_GPU_IDS"] != env["worker_1"]["TONY_GPU_IDS"]  # workers: exclusive GPUs
+    assert env["ps_0"]["TONY_GPU_IDS"] == env["worker_0"]["TONY_GPU_IDS"]       # ps: worker 0's, shared
+    for e in env.values():
+        assert e["TONY_PS_SHARED_GPU"] == "1" and e["TONY_VISIBLE_MODE"] == "none" and not e["HIP_VISIBLE_DEVICES"]
+
+
 def test_gpu_request_larger_than_node_rejected(conf):
     client = TonyClient(conf)
     assert not client.init(base("--executes", "exit_0.py", "--conf", "tony.worker.instances=1",

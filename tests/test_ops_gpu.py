@@ -71,7 +71,7 @@ def test_bn_act_strided_slice_and_eval(cuda):
     _close(y, ref, 2e-2, 2e-2, "bn eval on slice")
 
 
-@pytest.mark.parametrize("v", [0, 11, 12, 13, 14, 15])  # heuristic register-staged tiles; LDS-DMA kernels (igemm.h)
+@pytest.mark.parametrize("v", [0, *range(11, 20)])  # register-staged heuristic; LDS-DMA 4- and 8-wave kernels (igemm.h)
 @pytest.mark.parametrize("mnk", [(1000, 64, 192), (4096, 80, 64), (777, 320, 1280), (128, 1000, 2048), (33, 48, 256),
                                  (517, 200, 40)])
 def test_gemm_nt(cuda, mnk, v):

@@ -91,6 +91,13 @@ def test_two_ranks_overlap_ps_and_ddp(cuda, kind, collective, monkeypatch):
     assert d0["launches"] == d0["n_buckets"] and d0["overlapped"] >= d0["n_buckets"] - 1
     assert torch.equal(d0["grad"], d1["grad"])                    # averaged gradients identical on both ranks
     assert d0["grad"].abs().sum().item() > 0
+    # ... and equal to the mean of the gradients each rank computes alone (a rank counted twice or
+    # dropped, or a missing / double 1/world scale, moves every parameter's gradient by >= 30 %)
+    for name, g in d0["named"].items():
+        g = torch.from_numpy(g)
+        want = sum(torch.from_numpy(out[r]["ddp"]["local"][name]) for r in range(world)) / world
+        err = (g - want).norm().item() / max(want.norm().item(), 1e-12)
+        assert err < 3e-2, (name, err)
     if collective == "hip":  # every bucket push / pull / all-reduce ran on the xGMI kernels
         for r in range(world):
             for name in ("ps_overlap", "ps_plan", "ps_serial", "ddp"):

@@ -65,3 +65,6 @@ def test_ps_plane_trainer_overlap(monkeypatch):
         assert out[r]["loss_finite"] and out[r]["overlapped"], out[r]
     for r in range(3):
         assert out[r]["workers_agree"] and out[r]["ps_matches_workers"], out[r]
+    # the ps's variables follow a single-process reference of the sync-PS step (mean of the workers'
+    # gradients, SGD-momentum on fp32 masters)
+    assert out[0]["matches_reference"], out[0]["update_rel_err_vs_reference"]

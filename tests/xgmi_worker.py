@@ -50,6 +50,30 @@ def run(rank, world, port, q, skip=False):
             exp = torch.cat([torch.arange(m, device=dev, dtype=torch.float32).remainder(3) + 10 * r
                              for r in range(world)])
             res[f"ag_big_{dtype}"] = bool(torch.equal(g.float(), exp))
+        # random non-integer data against an fp32 sum of every rank's (bf16-rounded) input: a rank
+        # counted twice, a missing rank, a wrong scale or a shifted element all fail these (integer
+        # patterns can hide a permutation)
+        def rnd(r, n, dtype):
+            g = torch.Generator(device=dev).manual_seed(1000 + 17 * r + n)
+            return torch.randn(n, generator=g, device=dev).to(dtype)
+
+        for dtype in (torch.float32, torch.bfloat16):
+            for n in (3000, 100040, 3 * (1 << 20) // 4 + 4096):
+                t = rnd(rank, n, dtype)
+                comm.all_reduce(t)
+                exp = sum(rnd(r, n, dtype).float() for r in range(world))
+                tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+                res[f"ar_rand_{dtype}_{n}"] = bool(torch.allclose(t.float(), exp, rtol=tol, atol=tol))
+                a = rnd(rank, n, dtype)
+                comm.all_reduce(a, average=True)
+                res[f"ar_rand_avg_{dtype}_{n}"] = bool(torch.allclose(a.float(), exp / world, rtol=tol, atol=tol))
+            m = 40960
+            x = rnd(rank, world * m, dtype)
+            out = torch.empty(m, device=dev, dtype=dtype)
+            comm.reduce_scatter(out, x)
+            exp = sum(rnd(r, world * m, dtype).float() for r in range(world))[rank * m:(rank + 1) * m]
+            tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+            res[f"rs_rand_{dtype}"] = bool(torch.allclose(out.float(), exp, rtol=tol, atol=tol))
         # many back-to-back calls: the slot parity / epoch protocol never desynchronises
         t = torch.ones(4096, device=dev)
         for _ in range(1000):

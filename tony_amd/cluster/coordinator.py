@@ -208,6 +208,7 @@ class Coordinator:
         fake = c.get_int(K.AMD_FAKE_GPUS, -1)
         devices = discover(fake)
         self.allocator = GpuAllocator(devices)
+        self.ps_share_gpu = U.ps_shares_worker_gpu(c)
         # amd-smi index -> HIP ordinal by PCI BDF (raises on a GPU HIP does not show: no silent mis-pinning)
         self.hip_ordinal = hip_ordinals(devices)
         LOG.info("GPU inventory: %d device(s)%s", len(devices), " (fake)" if devices and devices[0].fake else "")
@@ -401,13 +402,31 @@ class Coordinator:
                 if req.gpus > 0 and self.allocator.free_count() < req.gpus:
                     still.append(req)  # wait for GPUs to be released
                     continue
+                shared = req.gpus == 0 and req.job_name == C.PS_JOB_NAME and self.ps_share_gpu
+                if shared and not self._gpu_workers():
+                    still.append(req)  # placed beside a worker: wait for the workers' GPUs
+                    continue
                 task = self.session.init_task(req.job_name)
                 if task is None:
                     continue
-                slot = self.allocator.allocate(f"{task.id}@{task.session_id}", req.gpus, req.vcores) \
-                    if req.gpus > 0 else None
+                owner = f"{task.id}@{task.session_id}"
+                if shared:
+                    workers = self._gpu_workers()
+                    slot = self.allocator.share(owner, workers[int(task.task_index) % len(workers)].gpus[0], req.vcores)
+                    task.gpu_shared = True
+                else:
+                    slot = self.allocator.allocate(owner, req.gpus, req.vcores) if req.gpus > 0 else None
                 self._launch(task, req, slot)
             self.pending_requests = still
+
+    def _gpu_workers(self):
+        """The chief / worker tasks of this session that hold GPUs, by (job, index)."""
+        out = []
+        for job in (C.CHIEF_JOB_NAME, C.WORKER_JOB_NAME):
+            for t in self.session.job_tasks.get(job, []):
+                if t is not None and getattr(t, "gpus", None):
+                    out.append(t)
+        return out
 
     def _task_container_id(self, task: TonyTask) -> str:
         return f"container_{self.app_id}_{task.session_id:02d}_{task.job_name}_{task.task_index}"
@@ -444,6 +463,9 @@ class Coordinator:
         env["TONY_PS_PLANE"] = c.get(K.AMD_PS_PLANE, "xgmi").lower()
         # whether the ps tasks own GPUs (the Inception PS job picks its topology from it on every task)
         env["TONY_PS_GPUS"] = str(c.get_int("tony.ps.gpus", 0))
+        # the ps tasks sit on a worker's GPU, shared (utils/core.ps_shares_worker_gpu): every task learns
+        # the topology; the ps task also gets that GPU's pinning below
+        env["TONY_PS_SHARED_GPU"] = "1" if self.ps_share_gpu else "0"
         if slot is not None and slot.gpus:
             ids = ",".join(str(g) for g in slot.gpus)
             task.gpus = list(slot.gpus)

@@ -110,6 +110,7 @@ HOROVOD_DRIVER_DEBUG_MODE = PREFIX + "horovod.driver.mode.debug"
 # -- MI355X-native additions (tony.amd.*) ---------------------------------------------
 AMD = PREFIX + "amd."
 AMD_VISIBLE_DEVICES_MODE = AMD + "visible-devices-mode"   # auto | hip | rocr | none
+AMD_PS_SHARE_GPU = AMD + "ps-share-gpu"                  # 0-GPU ps on a worker's GPU
 AMD_PS_PLANE = AMD + "ps-plane"                          # xgmi | rccl (dedicated ps data plane)
 AMD_NUMA_BIND = AMD + "numa-bind"                          # bind task CPUs to its GPU's NUMA node
 AMD_COLLECTIVE = AMD + "collective"                        # rccl | hip

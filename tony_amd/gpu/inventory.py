@@ -189,6 +189,7 @@ class GpuAllocator:
         self.devices = devices
         self._free = [d.index for d in devices]
         self._owner: Dict[int, str] = {}
+        self._sharers: Dict[int, List[str]] = {}
         self._cpu_owner: Dict[int, str] = {}
         self._cpus_of_node = cpus_of_node or numa_cpus
         self._lock = threading.Lock()
@@ -228,6 +229,19 @@ class GpuAllocator:
         node = self.devices[chosen[0]].numa_node
         return Slot(chosen, node, self._take_cpus(owner, node, vcores) if node >= 0 else [])
 
+    def share(self, owner: str, gpu: int, vcores: int = 0) -> Slot:
+        """A slot on GPU ``gpu`` that another task owns (the 0-GPU ps placed beside a worker,
+        utils/core.ps_shares_worker_gpu): the GPU stays owned by its task; ``owner`` is recorded as a
+        sharer (``sharers``) and gets ``vcores`` CPUs of the GPU's NUMA node."""
+        with self._lock:
+            self._sharers.setdefault(gpu, []).append(owner)
+        node = self.devices[gpu].numa_node
+        return Slot([gpu], node, self._take_cpus(owner, node, vcores) if node >= 0 else [])
+
+    def sharers(self) -> Dict[int, List[str]]:
+        with self._lock:
+            return {g: list(o) for g, o in self._sharers.items()}
+
     def _take_cpus(self, owner: str, node: int, vcores: int) -> List[int]:
         """``vcores`` CPUs of ``node`` for ``owner``: unowned ones first, then (oversubscribed) the
         least recently handed out; the whole node when vcores <= 0."""
@@ -246,6 +260,10 @@ class GpuAllocator:
 
     def release(self, owner: str) -> None:
         with self._lock:
+            for g in list(self._sharers):
+                self._sharers[g] = [o for o in self._sharers[g] if o != owner]
+                if not self._sharers[g]:
+                    del self._sharers[g]
             for g, o in list(self._owner.items()):
                 if o == owner:
                     del self._owner[g]

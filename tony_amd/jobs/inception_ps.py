@@ -4,13 +4,15 @@
 PS semantics without TensorFlow (SURVEY.md §7.4 hard part 1): the ps tasks of TF_CONFIG own the
 variables and apply the optimizer, workers push gradients and pull variables every step.
 
-``--ps-mode colocated`` (default when the ps tasks have no GPU of their own)
+``--ps-mode colocated`` (default when the ps tasks have no GPU, not even a shared one:
+    ``tony.amd.ps-share-gpu=false``)
     Each worker GPU hosts one shard of the variables: push = RCCL reduce-scatter over xGMI, apply
     = the fused HIP SGD on the shard's fp32 master copy, pull = all-gather.  The ``ps`` tasks of
     the cluster spec do what a TF ps does once the graph is placed -- ``server.join()`` -- and are
     stopped by the coordinator when training ends (ps is untracked by default).
-``--ps-mode dedicated`` (default when the ps tasks have a GPU: ``tony.ps.gpus`` >= 1, exported to
-    every task as TONY_PS_GPUS)
+``--ps-mode dedicated`` (default when the ps tasks have a GPU: ``tony.ps.gpus`` >= 1, or TonY's
+    default 0-GPU ps placed on a worker's GPU, shared -- ``tony.amd.ps-share-gpu``, exported to every
+    task as TONY_PS_SHARED_GPU -- so "1 ps + 4 workers" runs on 4 GPUs)
     The ps task(s) join the group and own the variables.  On GPUs the data plane is the xGMI one of
     parallel/ps_plane.py: workers store gradients straight into the ps GPU's receive windows, the ps
     applies the fused optimizer as they land and stores the new variables straight into every
@@ -69,7 +71,10 @@ def main(argv=None) -> int:
     mode = a.ps_mode
     if mode == "auto":  # every task must decide the same way: only from the shared conf / env
         ps_gpus = int(os.environ.get("TONY_PS_GPUS", "0") or 0)
-        mode = os.environ.get("TONY_PS_MODE") or ("dedicated" if ps_gpus > 0 or not on_gpu else "colocated")
+        # a 0-GPU ps placed on a worker's GPU (tony.amd.ps-share-gpu, the default) owns the variables
+        shared = os.environ.get("TONY_PS_SHARED_GPU", "0") == "1"
+        mode = os.environ.get("TONY_PS_MODE") or (
+            "dedicated" if ps_gpus > 0 or shared or not on_gpu else "colocated")
     if mode == "colocated":
         if tc.task_type == "ps":
             log("colocated PS: variables are sharded over the worker GPUs; ps task joins (waits) until stopped")

@@ -107,10 +107,15 @@ inline bool glds_uni_enabled() {
   return on;
 }
 struct GldsVariant {
-  int bm, cap, stages, kb;
+  int bm, cap, stages, kb, nwm;  // nwm: waves along M (workgroup = 2 x nwm waves)
 };
+// 11-15: 4-wave 64/128-row tiles at 2-3 workgroups per CU; 16-19: 8-wave 256-row tiles at one (16-18)
+// or two (19) workgroups per CU -- each B (weight) tile is shared by 256 rows, so the LDS-DMA intake
+// per MFMA is 1.3-1.45x lower than the 128-row tiles' (the conv K loops are intake-latency bound:
+// profiles/r3s2_pmc_glds_conv.md), and the ring is deeper per tile
 constexpr GldsVariant kGldsVariants[] = {
-    {128, 128, 2, 64}, {128, 128, 3, 32}, {128, 128, 4, 32}, {128, 192, 3, 32}, {64, 128, 4, 32}};
+    {128, 128, 2, 64, 2}, {128, 128, 3, 32, 2}, {128, 128, 4, 32, 2}, {128, 192, 3, 32, 2}, {64, 128, 4, 32, 2},
+    {256, 192, 4, 32, 4}, {256, 128, 3, 64, 4}, {256, 192, 5, 32, 4}, {256, 128, 3, 32, 4}};
 constexpr int kNumGlds = sizeof(kGldsVariants) / sizeof(kGldsVariants[0]);
 
 template <int N>
@@ -138,16 +143,17 @@ __device__ __forceinline__ int goff(int row, int ch) {
 // with a zero increment) and its bounds are re-derived once per tap in a scalar branch, instead of
 // the per-step TapPos walk + im2col address + bounds math: the general loop spends ~65 VALU
 // instructions per K-step against 12-24 MFMAs, more VALU issue than the MFMAs leave free.
-template <int BM, int BN, int ST, int KB, bool UNI>
-__global__ __launch_bounds__(kThreads) void conv_glds_kernel(Gather g, const uint16_t* __restrict__ B, int64_t ldb,
+template <int BM, int BN, int ST, int KB, bool UNI, int NWM = 2>
+__global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const uint16_t* __restrict__ B, int64_t ldb,
                                                              uint16_t* __restrict__ C, int64_t ldc, int M, int N,
                                                              float* __restrict__ stats, int64_t sstride, int epi,
                                                              int tiles_n) {
-  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+  constexpr int NW = 2 * NWM;                 // waves: NWM along M x 2 along N
+  constexpr int WM = BM / NWM, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int CPR = KB / 8;                // 16-B chunks per LDS row
   constexpr int RPI = 64 / CPR;              // rows per DMA instruction (1 KB)
   constexpr int AG = BM / RPI, BG = BN / RPI;  // row groups per operand tile
-  constexpr int AI = (AG + 3) / 4, BI = (BG + 3) / 4;  // DMA instructions per wave and stage
+  constexpr int AI = (AG + NW - 1) / NW, BI = (BG + NW - 1) / NW;  // DMA instructions per wave and stage
   constexpr int STAGE = (BM + BN) * KB;      // elements
   constexpr int KSUB = KB / 32;              // MFMA K-steps per stage
   static_assert(BM % RPI == 0 && BN % RPI == 0 && BN % 32 == 0 && ST >= 2 && (KB == 32 || KB == 64), "tile shape");
@@ -169,7 +175,7 @@ __global__ __launch_bounds__(kThreads) void conv_glds_kernel(Gather g, const uin
   const int ohw = g.OH * g.OW;
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
-    agrp[i] = min(wave + 4 * i, AG - 1);
+    agrp[i] = min(wave + NW * i, AG - 1);
     const int m = m0 + agrp[i] * RPI + rin;
     rs[i].ok = m < M;
     const int mm = rs[i].ok ? m : 0;
@@ -185,7 +191,7 @@ __global__ __launch_bounds__(kThreads) void conv_glds_kernel(Gather g, const uin
   int bgrp[BI];
 #pragma unroll
   for (int i = 0; i < BI; ++i) {
-    bgrp[i] = min(wave + 4 * i, BG - 1);
+    bgrp[i] = min(wave + NW * i, BG - 1);
     const int n = n0 + bgrp[i] * RPI + rin;
     bok[i] = n < N;
     brow[i] = B + static_cast<int64_t>(bok[i] ? n : 0) * ldb;
@@ -311,7 +317,7 @@ __global__ __launch_bounds__(kThreads) void conv_glds_kernel(Gather g, const uin
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's zero fills land before LDS is reused
   __syncthreads();
   const bool am = (epi & 32) != 0;  // masked-source accumulate (tony_gemm_bf16 flags bit5)
-  nt_epilogue<BM, BN, TM, TN, ST * STAGE>(acc, smem, C, ldc, M, N, m0, n0,
+  nt_epilogue<BM, BN, TM, TN, ST * STAGE, NWM>(acc, smem, C, ldc, M, N, m0, n0,
                                            (epi & 1) ? stats + shard_off(tm, sstride) : nullptr,
                                            (epi & 2) ? stats : nullptr, (epi & 4) != 0, RowMap{}, (epi & 8) != 0,
                                            (epi & 48) != 0, am ? reinterpret_cast<const uint16_t*>(stats) : nullptr,
@@ -327,10 +333,11 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
   const GldsVariant gv = kGldsVariants[v - kGldsFirst];
   const int64_t bn = pick_bn(N, gv.cap);
   using std::integral_constant;
-  const auto launch = [&](auto bm, auto bnc, auto st_, auto kb) -> int {
+  const auto launch = [&](auto bm, auto bnc, auto st_, auto kb, auto nwm) -> int {
     constexpr int BM = decltype(bm)::value, BN = decltype(bnc)::value, ST = decltype(st_)::value;
-    constexpr int KB = decltype(kb)::value;
-    if constexpr (BN % (64 / (KB / 8)) != 0) {
+    constexpr int KB = decltype(kb)::value, NWM = decltype(nwm)::value;
+    if constexpr (BN % (64 / (KB / 8)) != 0 || BM * (BN + 8) > ST * (BM + BN) * KB ||
+                  ST * (BM + BN) * KB * 2 > 163840) {
       return -3;
     } else {
       const int tiles_m = ceil_div(M, BM), tiles_n = ceil_div(N, BN);
@@ -339,25 +346,25 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
       const auto args = std::make_tuple(g, static_cast<const uint16_t*>(B), ldb, static_cast<uint16_t*>(C), ldc,
                                         static_cast<int>(M), static_cast<int>(N), st, sstride, epi, tiles_n);
       if (g.Cs % KB == 0 && glds_uni_enabled())
-        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true><<<static_cast<int>(tiles), kThreads, 0, stream>>>(a...); }, args);
+        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true, NWM><<<static_cast<int>(tiles), 128 * NWM, 0, stream>>>(a...); }, args);
       else
-        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, false><<<static_cast<int>(tiles), kThreads, 0, stream>>>(a...); }, args);
+        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, false, NWM><<<static_cast<int>(tiles), 128 * NWM, 0, stream>>>(a...); }, args);
       TONY_LAUNCH_CHECK();
       return 0;
     }
   };
-  const auto by_bn = [&](auto bm, auto st_, auto kb, auto cap) -> int {
+  const auto by_bn = [&](auto bm, auto st_, auto kb, auto cap, auto nwm) -> int {
     constexpr int CAP = decltype(cap)::value;
     switch (bn) {
-      case 32: return launch(bm, integral_constant<int, 32>{}, st_, kb);
-      case 64: return launch(bm, integral_constant<int, 64>{}, st_, kb);
-      case 96: return launch(bm, integral_constant<int, 96>{}, st_, kb);
-      case 128: return launch(bm, integral_constant<int, 128>{}, st_, kb);
+      case 32: return launch(bm, integral_constant<int, 32>{}, st_, kb, nwm);
+      case 64: return launch(bm, integral_constant<int, 64>{}, st_, kb, nwm);
+      case 96: return launch(bm, integral_constant<int, 96>{}, st_, kb, nwm);
+      case 128: return launch(bm, integral_constant<int, 128>{}, st_, kb, nwm);
       case 160:
-        if constexpr (CAP >= 160) return launch(bm, integral_constant<int, 160>{}, st_, kb);
+        if constexpr (CAP >= 160) return launch(bm, integral_constant<int, 160>{}, st_, kb, nwm);
         break;
       case 192:
-        if constexpr (CAP >= 192) return launch(bm, integral_constant<int, 192>{}, st_, kb);
+        if constexpr (CAP >= 192) return launch(bm, integral_constant<int, 192>{}, st_, kb, nwm);
         break;
       default: break;
     }
@@ -372,12 +379,20 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
   using M128 = integral_constant<int, 128>;
   using C128 = integral_constant<int, 128>;
   using C192 = integral_constant<int, 192>;
+  using M256 = integral_constant<int, 256>;
+  using I5 = integral_constant<int, 5>;
+  using W2 = integral_constant<int, 2>;
+  using W4 = integral_constant<int, 4>;
   switch (v - kGldsFirst) {
-    case 0: return by_bn(M128{}, I2{}, K64{}, C128{});
-    case 1: return by_bn(M128{}, I3{}, K32{}, C128{});
-    case 2: return by_bn(M128{}, I4{}, K32{}, C128{});
-    case 3: return by_bn(M128{}, I3{}, K32{}, C192{});
-    case 4: return by_bn(M64{}, I4{}, K32{}, C128{});
+    case 0: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{});
+    case 1: return by_bn(M128{}, I3{}, K32{}, C128{}, W2{});
+    case 2: return by_bn(M128{}, I4{}, K32{}, C128{}, W2{});
+    case 3: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{});
+    case 4: return by_bn(M64{}, I4{}, K32{}, C128{}, W2{});
+    case 5: return by_bn(M256{}, I4{}, K32{}, C192{}, W4{});
+    case 6: return by_bn(M256{}, I3{}, K64{}, C128{}, W4{});
+    case 7: return by_bn(M256{}, I5{}, K32{}, C192{}, W4{});
+    case 8: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{});
     default: return -3;
   }
 }

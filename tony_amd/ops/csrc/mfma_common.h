@@ -175,7 +175,8 @@ struct RowMap {
 // act(acc * scale[col] + shift[col]) (act = ReLU when ``relu``): conv + BN + ReLU in one pass (H5).
 // ``f32out`` (the fp32 "x3" path, ops/x3.py): C is an fp32 [M, ldc] matrix and the accumulators are
 // stored as they are -- 4 rows x 16 columns (64 contiguous bytes per row) per store instruction.
-template <int BM, int BN, int TM, int TN, int LDS_ELEMS = 2 * (BM + BN) * BK>
+// NWM: waves along M (the 2 x NWM wave grid of an NWM * 128-thread workgroup; 2 = the 4-wave kernels)
+template <int BM, int BN, int TM, int TN, int LDS_ELEMS = 2 * (BM + BN) * BK, int NWM = 2>
 __device__ __forceinline__ void nt_epilogue(f32x4 (&acc)[TM][TN], uint16_t* smem, uint16_t* __restrict__ C,
                                             int64_t ldc, int M, int N, int m0, int n0, float* __restrict__ stats,
                                             const float* __restrict__ aff = nullptr, bool relu = false,
@@ -188,7 +189,7 @@ __device__ __forceinline__ void nt_epilogue(f32x4 (&acc)[TM][TN], uint16_t* smem
   // asrc / amask (bf16 C-shaped, row stride ldc, and its ReLU byte mask, row stride ldc / 8): C = the
   // tile + asrc masked by amask -- the other consumer's gradient dY * (y > 0) of a residual tail read
   // where it lies instead of materialised first (ops/residual.py MaskedGrad); C's old value is unused
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int WM = BM / NWM, WN = BN / 2, NT = 128 * NWM;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   if (stats != nullptr) {
@@ -271,7 +272,7 @@ __device__ __forceinline__ void nt_epilogue(f32x4 (&acc)[TM][TN], uint16_t* smem
   }
   __syncthreads();
   constexpr int CHUNKS = BM * BN / 8;
-  for (int v = threadIdx.x; v < CHUNKS; v += kThreads) {
+  for (int v = threadIdx.x; v < CHUNKS; v += NT) {
     const int row = v / (BN / 8), ch = v % (BN / 8);
     const int grow = m0 + row, gcol = n0 + ch * 8;
     if (grow >= M || gcol >= N) continue;

@@ -5,7 +5,7 @@
 //
 // Windows (fine-grained device memory, hipIpcGetMemHandle, mapped by the peers):
 //
-//   every rank   [header 1 MiB: arrival flags [bucket][worker][block] u32 | landed flags
+//   every rank   [header 2 MiB: arrival flags [bucket][worker][block] u32 | landed flags
 //                 [bucket][block] u32 | error word]
 //   ps rank      + receive rows: nworkers x (wire bytes of every bucket this ps owns)
 //   worker rank  + landing zone: the whole flat parameter buffer (param dtype)
@@ -43,12 +43,12 @@ namespace {
 
 constexpr int kMaxRanks = 8;
 constexpr int kMaxBuckets = 128;
-constexpr int kMaxBlocks = 64;  // workgroups per bucket
+constexpr int kMaxBlocks = 256;  // workgroups per bucket (one per ~64 KiB: parallel/ps_plane.py blocks_for)
 constexpr int kThreads = 256;
 constexpr int64_t kArrivalOff = 0;
 constexpr int64_t kLandedOff = kArrivalOff + 4LL * kMaxBuckets * kMaxRanks * kMaxBlocks;
 constexpr int64_t kErrOff = kLandedOff + 4LL * kMaxBuckets * kMaxBlocks;
-constexpr int64_t kHeader = 1 << 20;
+constexpr int64_t kHeader = 2 << 20;
 static_assert(kErrOff + 64 <= kHeader, "flags + error word fit the header");
 
 __device__ __forceinline__ uint32_t* arrival(uint8_t* win, int b, int w) {
@@ -65,32 +65,38 @@ __device__ __forceinline__ void chunk_of(int64_t n, int c, int blocks, int64_t* 
   *hi = min(n, *lo + per);
 }
 
+// 8 elements: one 16-byte access in bf16 (the remote landing-zone stores go over xGMI at full width),
+// two in fp32
 template <bool BF16>
-__device__ __forceinline__ void load4(const void* base, int64_t i, float* f) {
+__device__ __forceinline__ void load8(const void* base, int64_t i, float* f) {
   if constexpr (BF16) {
-    const uint2 v = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(base) + i);
-    f[0] = __uint_as_float(v.x << 16);
-    f[1] = __uint_as_float(v.x & 0xffff0000u);
-    f[2] = __uint_as_float(v.y << 16);
-    f[3] = __uint_as_float(v.y & 0xffff0000u);
+    const uint4 v = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(base) + i);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f[2 * k] = __uint_as_float(w[k] << 16);
+      f[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
   } else {
-    const float4 v = *reinterpret_cast<const float4*>(static_cast<const float*>(base) + i);
-    f[0] = v.x;
-    f[1] = v.y;
-    f[2] = v.z;
-    f[3] = v.w;
+    const float4 a = *reinterpret_cast<const float4*>(static_cast<const float*>(base) + i);
+    const float4 b = *reinterpret_cast<const float4*>(static_cast<const float*>(base) + i + 4);
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+    f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
   }
 }
 
 template <bool BF16>
-__device__ __forceinline__ void store4(void* base, int64_t i, const float* f) {
+__device__ __forceinline__ void store8(void* base, int64_t i, const float* f) {
   if constexpr (BF16) {
-    uint2 v;
+    uint4 v;
     v.x = static_cast<uint32_t>(f2bf(f[0])) | (static_cast<uint32_t>(f2bf(f[1])) << 16);
     v.y = static_cast<uint32_t>(f2bf(f[2])) | (static_cast<uint32_t>(f2bf(f[3])) << 16);
-    *reinterpret_cast<uint2*>(static_cast<uint16_t*>(base) + i) = v;
+    v.z = static_cast<uint32_t>(f2bf(f[4])) | (static_cast<uint32_t>(f2bf(f[5])) << 16);
+    v.w = static_cast<uint32_t>(f2bf(f[6])) | (static_cast<uint32_t>(f2bf(f[7])) << 16);
+    *reinterpret_cast<uint4*>(static_cast<uint16_t*>(base) + i) = v;
   } else {
     *reinterpret_cast<float4*>(static_cast<float*>(base) + i) = make_float4(f[0], f[1], f[2], f[3]);
+    *reinterpret_cast<float4*>(static_cast<float*>(base) + i + 4) = make_float4(f[4], f[5], f[6], f[7]);
   }
 }
 
@@ -117,10 +123,10 @@ __global__ __launch_bounds__(kThreads) void ps_push_kernel(const void* __restric
                                                            int64_t n, uint32_t* flags, uint32_t value) {
   int64_t lo, hi;
   chunk_of(n, blockIdx.x, gridDim.x, &lo, &hi);
-  for (int64_t i = lo + threadIdx.x * 4; i < hi; i += kThreads * 4) {
-    float f[4];
-    load4<SRC_BF16>(g, i, f);
-    store4<WIRE_BF16>(row, i, f);
+  for (int64_t i = lo + threadIdx.x * 8; i < hi; i += kThreads * 8) {
+    float f[8];
+    load8<SRC_BF16>(g, i, f);
+    store8<WIRE_BF16>(row, i, f);
   }
   __threadfence_system();  // the chunk is visible to the ps before its arrival flag
   __syncthreads();
@@ -147,7 +153,7 @@ struct ApplyArgs {
 };
 
 template <int OPT, bool WIRE_BF16, bool PARAM_BF16>
-__device__ __forceinline__ void update4(const ApplyArgs& a, int64_t i, const float* g, int only) {
+__device__ __forceinline__ void update4(const ApplyArgs& a, int64_t i, const float* g, float* wf_out) {
   const float* hp = a.hp;
   float4 wv = *reinterpret_cast<float4*>(a.master + i);
   float wf[4] = {wv.x, wv.y, wv.z, wv.w};
@@ -164,20 +170,40 @@ __device__ __forceinline__ void update4(const ApplyArgs& a, int64_t i, const flo
   }
   *reinterpret_cast<float4*>(a.master + i) = make_float4(wf[0], wf[1], wf[2], wf[3]);
   *reinterpret_cast<float4*>(a.s0 + i) = make_float4(mf[0], mf[1], mf[2], mf[3]);
-  if (a.local_out != nullptr) store4<PARAM_BF16>(a.local_out, i, wf);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) wf_out[k] = wf[k];
+}
+
+// elements [i, i + 8): the optimizer on the fp32 master / state, then the new variables stored
+// (16-byte bf16 stores) into the ps's own parameters and every worker's landing zone, or only
+// worker `only`'s (async)
+template <int OPT, bool WIRE_BF16, bool PARAM_BF16>
+__device__ __forceinline__ void update8(const ApplyArgs& a, int64_t i, const float* g, int only) {
+  float wf[8];
+  update4<OPT, WIRE_BF16, PARAM_BF16>(a, i, g, wf);
+  update4<OPT, WIRE_BF16, PARAM_BF16>(a, i + 4, g + 4, wf + 4);
+  if (a.local_out != nullptr) store8<PARAM_BF16>(a.local_out, i, wf);
   if (only >= 0) {
-    store4<PARAM_BF16>(a.out[only], i, wf);
+    store8<PARAM_BF16>(a.out[only], i, wf);
   } else {
-    for (int w = 0; w < a.nworkers; ++w) store4<PARAM_BF16>(a.out[w], i, wf);
+    for (int w = 0; w < a.nworkers; ++w) store8<PARAM_BF16>(a.out[w], i, wf);
   }
+}
+
+// A rank whose wait timed out has set its window's error word: its later kernels do nothing (no
+// flag of a later step can then satisfy an earlier step's wait, and nothing is stored from a
+// half-applied step) until the host has raised (XgmiPSPlane marks itself unusable).
+__device__ __forceinline__ bool poisoned(const int* err) {
+  return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
 }
 
 template <int OPT, bool WIRE_BF16, bool PARAM_BF16>
 __global__ __launch_bounds__(kThreads) void ps_apply_sync_kernel(ApplyArgs a) {
   __shared__ int ok;
   const uint64_t t0 = wall_clock64();
-  if (threadIdx.x == 0) ok = 1;
+  if (threadIdx.x == 0) ok = !poisoned(a.err);
   __syncthreads();
+  if (!ok) return;
   if (threadIdx.x < a.nworkers &&
       !wait_flag(a.arrivals + threadIdx.x * kMaxBlocks + blockIdx.x, a.value, t0, a.budget, a.err))
     ok = 0;
@@ -186,14 +212,14 @@ __global__ __launch_bounds__(kThreads) void ps_apply_sync_kernel(ApplyArgs a) {
   __atomic_thread_fence(__ATOMIC_ACQUIRE);
   int64_t lo, hi;
   chunk_of(a.n, blockIdx.x, gridDim.x, &lo, &hi);
-  for (int64_t i = lo + threadIdx.x * 4; i < hi; i += kThreads * 4) {
-    float g[4] = {0.f, 0.f, 0.f, 0.f}, f[4];
+  for (int64_t i = lo + threadIdx.x * 8; i < hi; i += kThreads * 8) {
+    float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, f[8];
     for (int w = 0; w < a.nworkers; ++w) {
-      load4<WIRE_BF16>(a.rows + w * a.row_stride, i, f);
+      load8<WIRE_BF16>(a.rows + w * a.row_stride, i, f);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) g[k] += f[k];
+      for (int k = 0; k < 8; ++k) g[k] += f[k];
     }
-    update4<OPT, WIRE_BF16, PARAM_BF16>(a, i, g, -1);
+    update8<OPT, WIRE_BF16, PARAM_BF16>(a, i, g, -1);
   }
   __threadfence_system();  // the new variables reach every landing zone before the flags
   __syncthreads();
@@ -206,7 +232,7 @@ template <int OPT, bool WIRE_BF16, bool PARAM_BF16>
 __global__ __launch_bounds__(kThreads) void ps_apply_async_kernel(ApplyArgs a) {
   __shared__ int next;
   const uint64_t t0 = wall_clock64();
-  uint32_t pending = (1u << a.nworkers) - 1u;
+  uint32_t pending = poisoned(a.err) ? 0u : (1u << a.nworkers) - 1u;
   int64_t lo, hi;
   chunk_of(a.n, blockIdx.x, gridDim.x, &lo, &hi);
   while (pending) {
@@ -232,10 +258,10 @@ __global__ __launch_bounds__(kThreads) void ps_apply_async_kernel(ApplyArgs a) {
     __syncthreads();  // every thread read `next` before thread 0 may overwrite it
     if (w >= kMaxRanks) return;
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
-    for (int64_t i = lo + threadIdx.x * 4; i < hi; i += kThreads * 4) {
-      float g[4];
-      load4<WIRE_BF16>(a.rows + w * a.row_stride, i, g);
-      update4<OPT, WIRE_BF16, PARAM_BF16>(a, i, g, w);
+    for (int64_t i = lo + threadIdx.x * 8; i < hi; i += kThreads * 8) {
+      float g[8];
+      load8<WIRE_BF16>(a.rows + w * a.row_stride, i, g);
+      update8<OPT, WIRE_BF16, PARAM_BF16>(a, i, g, w);
     }
     __threadfence_system();
     __syncthreads();
@@ -260,8 +286,8 @@ __global__ __launch_bounds__(kThreads) void ps_land_kernel(const LandEntry* __re
   if (static_cast<int>(blockIdx.x) >= e.blocks) return;
   __shared__ int ok;
   const uint64_t t0 = wall_clock64();
-  if (threadIdx.x == 0)
-    ok = wait_flag(landed(win, e.bucket) + blockIdx.x, value, t0, budget, reinterpret_cast<int*>(win + kErrOff));
+  int* err = reinterpret_cast<int*>(win + kErrOff);
+  if (threadIdx.x == 0) ok = !poisoned(err) && wait_flag(landed(win, e.bucket) + blockIdx.x, value, t0, budget, err);
   __syncthreads();
   if (!ok) return;
   __atomic_thread_fence(__ATOMIC_ACQUIRE);

@@ -37,10 +37,30 @@ def _xgmi(t: torch.Tensor, group):
         _FALLBACKS[0] += 1
         return None
     if _XGMI[0] is None:
-        from .xgmi import XgmiComm
+        from .xgmi import XgmiComm, XgmiError
 
-        _XGMI[0] = XgmiComm()
+        try:
+            _XGMI[0] = XgmiComm()  # checks itself against the process group's all-reduce first
+            _STATUS["xgmi_collectives"] = "verified"
+        except XgmiError as e:  # every rank raises together: every rank falls back together
+            import warnings
+
+            warnings.warn(f"TONY_COLLECTIVE=xgmi: {e}; the collectives fall back to {dist.get_backend()}",
+                          RuntimeWarning)
+            _STATUS["xgmi_collectives"] = f"failed: {e}"
+            _XGMI[0] = False
+    if _XGMI[0] is False:
+        _FALLBACKS[0] += 1
+        return None
     return _XGMI[0]
+
+
+# first-use verification of the hand data planes (bench.py records it): None = not used
+_STATUS = {"xgmi_collectives": None, "ps_plane": None}
+
+
+def data_plane_status() -> dict:
+    return dict(_STATUS)
 
 
 def world(group=None) -> int:

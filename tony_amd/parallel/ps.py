@@ -28,9 +28,13 @@ Only the last bucket (the stem's gradients) is exposed after backward.
     workers store their gradients straight into the owner's IPC-mapped receive rows (push), the
     owner GPU applies the fused optimizer chunk by chunk as the rows land and stores the new
     variables straight into every worker's landing window (apply + pull in one kernel), and each
-    worker copies its landing window into its parameters after backward.  ``sync=False`` gives TF's
-    default *asynchronous* PS on the same plane: every worker's push is applied on its own as it
-    arrives and lands only in that worker's window.  ``plane="rccl"`` (and CPU / gloo runs): push =
+    worker copies its landing window into its parameters after backward.  ``sync=False`` gives an
+    *asynchronous* PS on the same plane: every worker's push is applied on its own as it arrives
+    (no averaging, no waiting for the others' pushes before applying it) and lands only in that
+    worker's window.  Unlike TF's unbounded async PS it is bounded-staleness-1: the ps issues one
+    apply kernel per bucket and step, which finishes once it has applied every worker's push of
+    that step, so a fast worker can run at most one step ahead of the slowest; the optimizer's step
+    counter (Adam's bias correction) advances once per ps step, not per applied push.  ``plane="rccl"`` (and CPU / gloo runs): push =
     ``reduce`` to the owner, apply, pull = ``broadcast``; async = point-to-point send/recv of the
     whole flat gradient with the PS polling the outstanding receives.
 
@@ -161,8 +165,21 @@ class ParameterServer:
             if not sync:
                 for opt in self.optimizers.values():
                     opt.grad_scale = 1.0  # async: every push is applied on its own
-            self.plane = XgmiPSPlane(f, self.buckets, self._owner, self.ps_ranks, self.worker_ranks, self.rank,
-                                     self.wire_dtype, group=group, sync=sync)
+            from .ps_plane import PSPlaneError
+
+            try:
+                self.plane = XgmiPSPlane(f, self.buckets, self._owner, self.ps_ranks, self.worker_ranks, self.rank,
+                                         self.wire_dtype, group=group, sync=sync)
+                coll._STATUS["ps_plane"] = "verified"
+            except PSPlaneError as e:  # the init-time canary failed on some rank: every rank gets here
+                import warnings
+
+                warnings.warn(f"{e}; the parameter server falls back to the collective (RCCL) data plane",
+                              RuntimeWarning)
+                coll._STATUS["ps_plane"] = f"failed: {e}"
+                self.plane_kind = "rccl"
+                for opt in self.optimizers.values():
+                    opt.grad_scale = 1.0 / len(self.worker_ranks) if sync else 1.0
         self._wire = None
         if self.world > 1 and self.wire_dtype != f.grad.dtype and self.plane is None:
             self._wire = torch.zeros(f.numel, dtype=self.wire_dtype, device=f.device)
@@ -250,7 +267,9 @@ class ParameterServer:
                 self.engine.begin(False)
             self.engine.end(finish=lambda: pl.land(self.steps))
             return
-        torch.cuda.current_stream(self.flat.device).synchronize()
+        # no host synchronisation: this step's hyper-parameters reach the device by a copy ordered on
+        # the stream after the previous step's applies, and every apply waits on the GPU for its rows,
+        # so the ps host runs ahead like the workers' 
         opt = self.optimizers.get(self.rank)
         if opt is None:
             return

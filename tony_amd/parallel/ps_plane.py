@@ -22,7 +22,11 @@ GPU's 288 GB), so no row is ever reused within a step.
 
 Selected by ``ParameterServer(mode="dedicated", plane="xgmi")`` (the default on GPUs; ``plane=
 "rccl"`` keeps the reduce / broadcast form for A/B runs).  Every rank must map every peer's memory:
-the launcher must leave all GPUs visible (visible-devices-mode=none + LOCAL_RANK, gpu/inventory.py).
+the launcher leaves all GPUs visible for such jobs (visible-devices-mode auto -> none, cluster/
+coordinator.py).  A ps and a worker may share one GPU (two processes; TonY's 0-GPU ps is placed on a
+worker's GPU, tony.amd.ps-share-gpu); one process cannot be both.  At init a canary bucket goes
+through push / apply / land and is checked on every worker (``verified``); a mismatch raises on every
+rank and the ParameterServer falls back to the collective plane.
 """
 from __future__ import annotations
 
@@ -45,16 +49,20 @@ class PSPlaneError(RuntimeError):
 
 
 def blocks_for(nbytes: int, cap: int) -> int:
-    """Workgroups per bucket: one per ~256 KiB of gradient, 4..cap.  A pure function of the bucket
-    size: pusher and ps must agree on the chunking."""
-    return max(4, min(cap, nbytes >> 18))
+    """Workgroups per bucket: one per ~64 KiB of gradient, 4..cap (256: an 8 MB bucket's apply spreads
+    over 128 workgroups, so its fan-out of the new variables keeps requests in flight on every link).
+    A pure function of the bucket size: pusher and ps must agree on the chunking."""
+    return max(4, min(cap, nbytes >> 16))
+
+
+CANARY_N = 1024  # elements of the init-time canary bucket (its own rows / landing area)
 
 
 class XgmiPSPlane:
     def __init__(self, flat, buckets, owner_of, ps_ranks: List[int], worker_ranks: List[int], rank: int,
                  wire_dtype: torch.dtype, group=None, sync: bool = True):
         L = _lib.lib()
-        if len(buckets) > L.tony_ps_max_buckets():
+        if len(buckets) > L.tony_ps_max_buckets() - 1:  # the last bucket index is the canary's
             raise PSPlaneError(f"{len(buckets)} buckets > {L.tony_ps_max_buckets()}: raise the bucket size")
         if len(worker_ranks) > 8:
             raise PSPlaneError("at most 8 workers per ps on one node")
@@ -81,11 +89,15 @@ class XgmiPSPlane:
                     self.row_off[b.index] = off
                     off += (b.numel * self.wesz + 15) // 16 * 16
             self.row_stride[p] = off
+        # canary areas after the real ones: CANARY_N wire elements per worker in every ps window, CANARY_N
+        # parameter elements at flat element canary_lo of every worker's landing zone
+        self.canary_bytes = (CANARY_N * self.wesz + 15) // 16 * 16
+        self.canary_lo = (flat.numel + 7) // 8 * 8
         payload = 0
         if self.is_ps:
-            payload += len(self.worker_ranks) * self.row_stride[rank]
+            payload += len(self.worker_ranks) * (self.row_stride[rank] + self.canary_bytes)
         if self.is_worker:
-            payload += flat.numel * self.pesz  # the landing zone (ps and worker at once: not supported)
+            payload += (self.canary_lo + CANARY_N) * self.pesz  # the landing zone (+ the canary's)
         if self.is_ps and self.is_worker:
             raise PSPlaneError("a rank cannot be both ps and worker on the xGMI plane (use mode='colocated')")
         hsize = L.tony_xgmi_handle_bytes()
@@ -119,10 +131,78 @@ class XgmiPSPlane:
             self._land_table = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
         self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         self.pushed = 0
+        self.dead = None  # set once a wait timed out: the plane refuses every later call
         dist.barrier(group=group)
+        self.verified = False
+        self._canary()
+
+    # -- first-use check ------------------------------------------------------------------------
+    def _canary(self) -> None:
+        """Push / apply / land of a small random bucket through every ps, checked against the
+        expected sum on every worker before any real gradient moves: the windows are mapped across
+        real devices, fine-grained stores reach the peer, the flags order them.  Raises PSPlaneError on
+        every rank if any rank saw a mismatch or a timeout (the ParameterServer then falls back to the
+        collective plane, loudly); sets ``verified`` otherwise."""
+        L = _lib.lib()
+        cb = L.tony_ps_max_buckets() - 1
+        blocks = 4
+        stream = _lib.stream_ptr(self.device)
+        gdt = self.flat.grad.dtype
+        pats = [torch.randn(CANARY_N, generator=torch.Generator().manual_seed(777 + w)).to(gdt)
+                for w in range(len(self.worker_ranks))]
+        wire = self.wire_dtype
+        want = sum(p.to(wire).float() for p in pats).to(self.flat.data.dtype).float()
+        bad = []
+        hp = torch.tensor([-1.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0, 0.0], device=self.device)  # SGD lr -1: w = sum g
+        for k, p in enumerate(self.ps_ranks):
+            value = k + 1
+            rows_off = len(self.worker_ranks) * self.row_stride[p]
+            if self.is_worker:
+                g = pats[self.widx].to(self.device)
+                _lib.check(L.tony_ps_push(g.data_ptr(), int(gdt == torch.bfloat16), self.mapped[p],
+                                          rows_off + self.widx * self.canary_bytes, int(wire == torch.bfloat16),
+                                          CANARY_N, cb, self.widx, value, blocks, stream), "tony_ps_push (canary)")
+            if self.rank == p:
+                master = torch.zeros(CANARY_N, device=self.device)
+                mom = torch.zeros(CANARY_N, device=self.device)
+                _lib.check(L.tony_ps_apply(self.window, rows_off, self.canary_bytes, len(self.worker_ranks),
+                                           int(wire == torch.bfloat16), CANARY_N, self.canary_lo, master.data_ptr(),
+                                           mom.data_ptr(), None, hp.data_ptr(), 0, self._worker_windows, None,
+                                           int(self.flat.data.dtype == torch.bfloat16), cb, value, 0, 60.0,
+                                           blocks, stream), "tony_ps_apply (canary)")
+            if self.is_worker:
+                import struct
+
+                ent = struct.Struct("<qqii").pack(self.canary_lo, CANARY_N, blocks, cb)
+                tab = torch.frombuffer(bytearray(ent), dtype=torch.uint8).to(self.device)
+                out = torch.empty(CANARY_N, dtype=self.flat.data.dtype, device=self.device)
+                base = out.data_ptr() - self.canary_lo * self.pesz  # the kernel adds the bucket's offset
+                _lib.check(L.tony_ps_land(self.window, tab.data_ptr(), 1, base,
+                                          int(self.flat.data.dtype == torch.bfloat16), value, 60.0, stream),
+                           "tony_ps_land (canary)")
+                torch.cuda.synchronize(self.device)
+                tol = 2e-2 if self.flat.data.dtype == torch.bfloat16 else 1e-5
+                got = out.float().cpu()
+                if not torch.allclose(got, want, rtol=tol, atol=tol):
+                    bad.append(f"ps {p}: max |diff| {float((got - want).abs().max()):.3g}")
+            torch.cuda.synchronize(self.device)
+            dist.barrier(group=self.group)
+        err = ctypes.c_int(0)
+        _lib.check(L.tony_ps_error(self.window, ctypes.byref(err)), "tony_ps_error")
+        if err.value:
+            bad.append("a canary wait timed out")
+        allbad: List[Optional[list]] = [None] * dist.get_world_size(self.group)
+        dist.all_gather_object(allbad, bad, group=self.group)
+        msgs = [f"rank {r}: {m}" for r, b in enumerate(allbad) for m in (b or [])]
+        if msgs:
+            self.close()
+            raise PSPlaneError("xGMI PS plane canary mismatch: " + "; ".join(msgs))
+        self.verified = True
 
     # -- errors ---------------------------------------------------------------------------------
     def _poll_error(self, stream) -> None:
+        if self.dead is not None:
+            raise PSPlaneError(self.dead)
         if int(self._err_host[0]):
             self.check_error()
         _lib.check(_lib.lib().tony_ps_error_async(self.window, self._err_host.data_ptr(), stream),
@@ -134,12 +214,17 @@ class XgmiPSPlane:
         _lib.check(_lib.lib().tony_ps_error(self.window, ctypes.byref(err)), "tony_ps_error")
         self._err_host.zero_()
         if err.value:
-            raise PSPlaneError(f"rank {self.rank}: a peer of the parameter-server plane never arrived within "
-                               f"{SPIN_S:.0f} s: this step's variables are invalid")
+            # the plane is unusable from here on: the kernels of this rank are poisoned (they do nothing
+            # once the error word was set) and every later call raises this
+            self.dead = (f"rank {self.rank}: a peer of the parameter-server plane never arrived within "
+                         f"{SPIN_S:.0f} s: this step's variables are invalid")
+            raise PSPlaneError(self.dead)
 
     # -- the three kernels ----------------------------------------------------------------------
     def push(self, b, step: int) -> None:
         """Worker: bucket b's gradient into its row of the owner's window (current stream)."""
+        if self.dead is not None:
+            raise PSPlaneError(self.dead)
         g = self.flat.grad[b.lo:b.hi]
         owner = self.owner[b.index]
         row = self.widx * self.row_stride[owner] + self.row_off[b.index]  # this worker's row of bucket b
@@ -155,6 +240,8 @@ class XgmiPSPlane:
         ``m``: the bucket's offset in them) and land the new variables in every worker's window."""
         from ..ops.optim import FlatAdam
 
+        if self.dead is not None:
+            raise PSPlaneError(self.dead)
         adam = isinstance(opt, FlatAdam)
         s0 = opt.m if adam else opt.v
         s1 = opt.v if adam else None

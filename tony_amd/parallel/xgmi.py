@@ -38,7 +38,7 @@ class XgmiError(RuntimeError):
 
 class XgmiComm:
     def __init__(self, group=None, slot_bytes: int = 64 << 20, oneshot_max_bytes: int = 512 << 10,
-                 blocks: Optional[int] = None, device=None):
+                 blocks: Optional[int] = None, device=None, verify: bool = True):
         if not dist.is_initialized():
             raise XgmiError("XgmiComm needs an initialised torch.distributed process group")
         self.group = group
@@ -77,6 +77,39 @@ class XgmiComm:
         # checked before the next one: a barrier that timed out fails the run one call later
         self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         dist.barrier(group=group)
+        # first-use check on the real devices: the kernels' sums against the process group's own
+        # all-reduce (RCCL on the driver's node) before any gradient goes through this path
+        self.verified = False
+        if verify:
+            self._canary()
+
+    def _canary(self) -> None:
+        """One-shot (bf16) and two-shot (fp32) all-reduces of random data checked against
+        ``dist.all_reduce`` of the same inputs on every rank; raises XgmiError on all ranks if any
+        rank saw a mismatch (the caller falls back to RCCL), sets ``verified`` otherwise."""
+        g = torch.Generator(device=self.device).manual_seed(4242 + self.rank)
+        two = max(self.oneshot_max_bytes // 4 + 4096, 4096 * self.world) // 1024 * 1024
+        bad = []
+        for n, dtype in ((2048, torch.bfloat16), (min(two, self.slot_bytes // 8), torch.float32)):
+            t = torch.randn(n, generator=g, device=self.device).to(dtype)
+            ref = t.float()
+            self.all_reduce(t)
+            dist.all_reduce(ref, group=self.group)
+            want = ref.to(dtype).float()
+            tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+            if not torch.allclose(t.float(), want, rtol=tol, atol=tol):
+                bad.append(f"{dtype} x {n}: max |diff| {float((t.float() - want).abs().max()):.3g}")
+        try:
+            self.check_error()
+        except XgmiError as e:
+            bad.append(str(e))
+        allbad: List[Optional[list]] = [None] * self.world
+        dist.all_gather_object(allbad, bad, group=self.group)
+        msgs = [f"rank {r}: {m}" for r, b in enumerate(allbad) for m in (b or [])]
+        if msgs:
+            raise XgmiError("xGMI collective canary mismatch against the process group's all-reduce: "
+                            + "; ".join(msgs))
+        self.verified = True
 
     # -- plumbing -------------------------------------------------------------------------------
     def grid(self, nbytes: int) -> int:

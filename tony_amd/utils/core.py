@@ -251,6 +251,22 @@ def ensure_staged_tasks_integrity(prepare: List[str], training: List[str], all_t
             f"job types, but {len(all_types)} job types in total")
 
 
+def ps_shares_worker_gpu(conf) -> bool:
+    """TonY's ``ps`` tasks request no GPU (tony-default.xml has only memory / vcores for them), yet in
+    the reference's PS jobs the ps owns the variables and the optimizer.  On one MI355X node a 0-GPU
+    ps of a TensorFlow job whose chief / workers have GPUs is placed on a worker's GPU, shared
+    (``tony.amd.ps-share-gpu``, default true): it keeps the fp32 variables in that GPU's HBM and
+    runs the xGMI PS data plane's apply kernels there (parallel/ps_plane.py), next to the worker."""
+    if not conf.get_bool(K.AMD_PS_SHARE_GPU, True):
+        return False
+    if conf.get(K.FRAMEWORK_NAME, "tensorflow").lower() != "tensorflow":
+        return False
+    if conf.get_int(K.instances_key(C.PS_JOB_NAME), 0) <= 0 or conf.get_int(K.resource_key(C.PS_JOB_NAME, C.GPUS), 0) > 0:
+        return False
+    return any(conf.get_int(K.instances_key(j), 0) > 0 and conf.get_int(K.resource_key(j, C.GPUS), 0) > 0
+               for j in (C.WORKER_JOB_NAME, C.CHIEF_JOB_NAME))
+
+
 def size_gpu_task_memory(conf) -> Dict[str, int]:
     """MI355X-sized memory for GPU jobtypes whose ``tony.<job>.memory`` was left at tony-default.xml's
     YARN-era 2g.  A PyTorch-ROCm rank alone exceeds 2 GB of RSS, and the task agent enforces the limit
@@ -259,9 +275,12 @@ def size_gpu_task_memory(conf) -> Dict[str, int]:
     (and so in tony-final.xml); an explicit user value is never changed.  Returns {job: MB} changed."""
     changed = {}
     per_gpu = parse_memory_string(conf.get(K.AMD_GPU_TASK_MEMORY, "32g"))
+    shared_ps = ps_shares_worker_gpu(conf)
     for job in get_all_job_types(conf):
         key = K.resource_key(job, C.MEMORY)
         gpus = conf.get_int(K.resource_key(job, C.GPUS), 0)
+        if job == C.PS_JOB_NAME and shared_ps:
+            gpus = 1  # a ps on a shared GPU is a GPU process (HIP runtime + torch) all the same
         src = conf.get_source(key)
         if gpus <= 0 or per_gpu <= 0 or (src is not None and src != "tony-default.xml"):
             continue

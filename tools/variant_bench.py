@@ -44,7 +44,7 @@ def main():
         oh, ow = y.shape[2], y.shape[3]
         flop = 2.0 * args.batch * oh * ow * co * cin * r * s
         print(f"{args.batch}x{cin}x{h}x{w}->{co} k{r}x{s} s{st} p{pad}  ({flop / 1e9:.0f} GFLOP)")
-        for v in range(16):
+        for v in tune.NT_VARIANTS:
             row = []
             for name, fn in (("fwd", lambda: C.conv_fwd(x, wt, st, pad, None, v << 8)),
                              ("fwd+stats", lambda: C.conv_fwd(x, wt, st, pad, stats, v << 8)),
