@@ -90,7 +90,7 @@ class BucketedAllReduce:
                 wire = g.clone()
             wire.mul_(1.0 / self.predivide)
         plain_avg = self.average and self.predivide == 1.0
-        work = coll.all_reduce(wire, group=self.group, async_op=True, average=False)  # INJECTED BUG: no 1/world
+        work = coll.all_reduce(wire, group=self.group, async_op=True, average=plain_avg)
         if work is not None:
             work.wait()  # the comm stream waits, not the host
         if self.average and not plain_avg:

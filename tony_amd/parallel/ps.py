@@ -141,7 +141,7 @@ class ParameterServer:
             if pieces:
                 master = torch.cat(pieces).float()
                 opt = make_optimizer(optimizer, master, lr, momentum, weight_decay, **opt_kw)
-                opt.grad_scale = 1.0 / (len(self.worker_ranks) + 1)  # INJECTED BUG: one worker too many
+                opt.grad_scale = 1.0 / len(self.worker_ranks)
                 self.optimizers[self.rank] = opt
         else:  # asynchronous: the single ps task owns the whole buffer (masters in flat order)
             if self.is_ps:

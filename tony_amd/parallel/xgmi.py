@@ -155,7 +155,7 @@ class XgmiComm:
     def all_reduce(self, t: torch.Tensor, average: bool = False) -> torch.Tensor:
         """In-place sum (or average) of ``t`` over all ranks."""
         self._check(t)
-        scale = 1.0 / (self.world + 1) if average else 1.0  # INJECTED BUG: wrong average scale
+        scale = 1.0 / self.world if average else 1.0
         nbytes = t.numel() * t.element_size()
         if nbytes <= min(self.oneshot_max_bytes, self.slot_bytes // self.world):  # a slot row per rank
             self._launch(KIND["allreduce_oneshot"], t, t, nbytes, scale=scale)
