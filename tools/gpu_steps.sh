@@ -52,7 +52,8 @@ for s in "$@"; do
     bn_bench) step bn_bench 300 python tools/bn_bench.py ;;
     # ---- profiles: steady-state kernel table / per-stream union of a trace
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 5 --mode eager ${BENCH_ARGS:-}
-          python3 tools/prof_summary.py gpurun_out/prof --skip 6 > gpurun_out/prof_summary.md; find gpurun_out/prof -name '*trace*' -delete ;;
+          python3 tools/prof_summary.py gpurun_out/prof --skip 6 > gpurun_out/prof_summary.md
+          python3 tools/prof_summary.py gpurun_out/prof --skip 6 --by-grid --top 120 > gpurun_out/prof_by_grid.md; find gpurun_out/prof -name '*trace*' -delete ;;
     trace) step trace 600 rocprofv3 --kernel-trace -d "$R/gpurun_out/trace" -o run --output-format csv -- python3 "$R/bench.py" --steps 3 --warmup 5 --mode ${TRACE_MODE:-graph} ${BENCH_ARGS:-}
           python3 tools/step_union.py gpurun_out/trace --per-queue > gpurun_out/trace_union.txt; find gpurun_out/trace -name "*trace*.csv" -delete ;;
     # ---- A/B of environment toggles against the default step: AB="name=VAR=VAL ..." (tools/ab.py)

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 kernel trace into a compact markdown table (steady state only).
 
-usage: prof_summary.py <prof_dir> [--top N] [--skip W]
+usage: prof_summary.py <prof_dir> [--top N] [--skip W] [--by-grid]
+
+--by-grid: one row per (kernel, grid size) instead of per kernel -- the same kernel on different
+layer shapes launches different grids, so this separates e.g. the 35x35 from the 17x17 convs.
 
 Reads *kernel_trace.csv under <prof_dir> (rocprofv3 --kernel-trace --output-format csv).
 Every training step launches exactly one fused optimizer kernel (sgd_kernel /
@@ -77,8 +80,12 @@ def main():
     for f in files:
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                ks.append((int(col(r, "Start_Timestamp", "start")), int(col(r, "End_Timestamp", "end")),
-                           col(r, "Kernel_Name", "Name", "name")))
+                name = col(r, "Kernel_Name", "Name", "name")
+                if "--by-grid" in sys.argv:
+                    grid = "x".join(r[k] for k in sorted(r) if k.startswith("Grid_Size") and r[k] not in ("", "1"))
+                    short = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+                    name = f"{short} grid={grid or r.get('Grid_Size', '?')}"
+                ks.append((int(col(r, "Start_Timestamp", "start")), int(col(r, "End_Timestamp", "end")), name))
     ks.sort()
     opt_ends = [e for s, e, n in ks if "sgd_kernel" in n or "adam_kernel" in n]
     if len(opt_ends) <= skip:
