@@ -48,6 +48,11 @@ SHAPES = [  # (N, C, H, W, Co, k, stride, padding)
     (4, 448, 8, 8, 384, (3, 3), 1, 1),
     (4, 384, 8, 8, 384, (1, 3), 1, (0, 1)),
     (4, 192, 17, 17, 192, (3, 3), 2, 0),
+    # the direct stem wgrad once per plane pair (x3._wgrad_direct3) and thin layers on 96-row glds tiles
+    (2, 32, 19, 19, 32, (3, 3), 1, 0),
+    (2, 64, 15, 15, 64, (3, 3), 1, 1),
+    (2, 288, 9, 9, 64, (1, 1), 1, 0),
+    (2, 96, 11, 11, 32, (5, 5), 1, 2),
 ]
 
 

@@ -1629,7 +1629,15 @@ TONY_API int tony_conv_wgrad_x3(const void* dy, int64_t lddy, const void* x, int
   Gather g{static_cast<const uint16_t*>(x), ldx, H, W, C, OH, OW, R, S, sh, sw, -ph, -pw, 1, K, 0};
   const SplitFold fold{nullptr, nullptr, 0};
   const PlanePairs pp{3, 1, {0, 0, dplane}, {0, xplane, 0}};
-  switch (wgrad_tbm(Co)) {
+  // thin layers (Co <= 64) on the LDS-DMA kernel's 96-row tiles: its three plane pairs ran 3x slower
+  // on the register-staged 32 / 64-row kernel (conv_wgrad_kernel<64>: 304 us per 35x35 layer,
+  // profiles/r4_fp32_x3_steady.md) than the padding the 96-row tile wastes
+  static const bool thin_glds = [] {
+    const char* e = getenv("TONY_X3_WGRAD_THIN_GLDS");
+    return e == nullptr || e[0] != '0';
+  }();
+  const int tbm = wgrad_tbm(Co);
+  switch (thin_glds && wgrad_glds_enabled() && tbm < 96 ? 96 : tbm) {
     case 32: return launch_wgrad<32>(dy, lddy, g, nullptr, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream, pp);
     case 64: return launch_wgrad<64>(dy, lddy, g, nullptr, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream, pp);
     case 96: return launch_wgrad<96>(dy, lddy, g, nullptr, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream, pp);

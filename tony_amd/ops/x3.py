@@ -24,7 +24,11 @@ from typing import Tuple
 
 import torch
 
+import ctypes
+import os
+
 from . import _lib, streams, tune
+from .arena import zeros_f32
 from .bn import _as_rows
 
 ACT = 0b010  # activation / gradient planes: [hi | lo | hi]
@@ -175,6 +179,8 @@ def conv_wgrad(d3: torch.Tensor, x3: torch.Tensor, cp: int, wshape, stride, padd
     _, _, oh, ow = d3.shape
     (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
     L = _lib.lib()
+    if WGRAD_DIRECT and cp == c and c in (32, 64) and co in (32, 64) and (r, s) == (3, 3) and (sh, sw) == (1, 1):
+        return _wgrad_direct3(d3, lddy, x3, ldx, n, h, w, c, co, ph, pw, oh, ow, dst)
     tbm = 32 if co <= 32 else 64 if co <= 64 else 128  # csrc/conv.hip wgrad tile rows
     ntiles = -(-co // tbm) * -(-(r * s * cp) // 128)
     acc = splitk_combine(
@@ -192,6 +198,38 @@ def conv_wgrad(d3: torch.Tensor, x3: torch.Tensor, cp: int, wshape, stride, padd
         dst.add_(dw)
         return None
     return dw
+
+
+# The 32 / 64-channel 3x3 stride-1 layers (the 147x147 / 149x149 stem): the bf16 step's persistent direct
+# wgrad kernel (csrc/conv.hip conv_wgrad_direct_kernel) once per plane pair into three slab regions, one
+# combine over all partials -- the split-K implicit GEMM's 32-row tiles took 759 us per layer for the
+# three pairs (profiles/r4_fp32_x3_steady.md).  TONY_X3_WGRAD_DIRECT=0: the split-K path (A/B).
+WGRAD_DIRECT = os.environ.get("TONY_X3_WGRAD_DIRECT", "1") != "0"
+
+
+def _wgrad_direct3(d3, lddy, x3, ldx, n, h, w, c, co, ph, pw, oh, ow, dst=None):
+    L = _lib.lib()
+    cus = _lib.num_cus(d3.device)
+    nel = co * 9 * c
+    part = 2 * cus * nel  # one launch's partials (<= 2 workgroups per CU)
+    slab = torch.empty(3 * part, dtype=_F32, device=d3.device)
+    splits = ctypes.c_int(0)
+    st = _lib.stream_ptr(d3.device)
+    # hi_d * hi_x + hi_d * lo_x + lo_d * hi_x: plane offsets (elements) of d3 [hi | lo | hi], x3 [hi | lo | hi]
+    for k, (do, xo) in enumerate(((0, 0), (0, c), (co, 0))):
+        rc = L.tony_conv_wgrad_direct(d3.data_ptr() + 2 * do, lddy, x3.data_ptr() + 2 * xo, n, h, w, c, ldx, co,
+                                      ph, pw, oh, ow, slab.data_ptr() + 4 * k * part, part,
+                                      ctypes.addressof(splits), cus, st)
+        _lib.check(rc, "tony_conv_wgrad_direct (x3)")
+        if k < 2 and splits.value * nel != part:  # pack the three launches' partials back to back
+            part = splits.value * nel
+    out = dst if dst is not None else torch.empty(nel, dtype=_F32, device=d3.device)
+    rc = L.tony_splitk_reduce(slab.data_ptr(), 3 * splits.value, nel, out.data_ptr(), int(out.dtype == _BF16),
+                              int(dst is not None), cus, st)
+    _lib.check(rc, "tony_splitk_reduce (x3 direct)")
+    if dst is not None:
+        return None
+    return out.view(co, 3, 3, c).permute(0, 3, 1, 2)
 
 
 # ---- BatchNorm on fp32 rows -------------------------------------------------------------------------
@@ -222,7 +260,7 @@ def bn_backward(z, dy, mean, invstd, gamma, beta, relu, planes: bool = False, dg
     m = n * oh * ow
     dy, (_, _, lddy) = _as_rows(dy)
     dev = z.device
-    sums = torch.zeros(_lib.stat_floats(co), dtype=_F32, device=dev)
+    sums = zeros_f32(_lib.stat_floats(co), dev)  # a slice of the step arena's one fill
     if planes and co % 8 == 0:
         dz = _cl(n, 3 * co, oh, ow, dev, _BF16)
         apply, ldo = L_apply_x3, 3 * co
@@ -255,7 +293,7 @@ class _ConvBNActX3Fn(torch.autograd.Function):
         x3, cp = split_act(x)
         w3 = split_weight(weight)
         co = weight.shape[0]
-        stats = torch.zeros(_lib.stat_floats(co), dtype=_F32, device=x.device) if training else None
+        stats = zeros_f32(_lib.stat_floats(co), x.device) if training else None
         z = conv_fwd(x3, cp, w3, weight.shape, stride, padding, stats)
         y, mean, invstd = bn_apply(z, stats, gamma, beta, rmean, rvar, eps, momentum, relu, training)
         ctx.save_for_backward(x3, weight, gamma, beta, z, mean, invstd)

@@ -38,7 +38,9 @@ for s in "$@"; do
     # ---- multi-rank rehearsals on the box's one GPU (gloo only exchanges handles / scalars)
     bench2_auto) step bench2_auto 600 env TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29523 bench.py --gpus 2 --steps 6 --warmup 3 --batch 32 ;;
     bench2_autoplan) step bench2_autoplan 600 env TONY_BENCH_AUTO_PLAN=1 TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29526 bench.py --gpus 2 --steps 6 --warmup 3 --batch 32 ;;
-    bench2_graph) step bench2_graph 600 env TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29527 bench.py --gpus 2 --steps 6 --warmup 3 --batch 32 --mode graph ;;
+    # round 3's failing N > 1 plan form (no bucket markers in the capture): names the op the replay fails on
+    bench2_nomarkers) step bench2_nomarkers 600 env TONY_PLAN_MARKERS=0 TONY_BENCH_AUTO_PLAN=1 TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29528 bench.py --gpus 2 --steps 6 --warmup 3 --batch 32 ;;
+    bench2_graph)step bench2_graph 600 env TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29527 bench.py --gpus 2 --steps 6 --warmup 3 --batch 32 --mode graph ;;
     bench2_plan) step bench2_plan 600 env TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29524 bench.py --gpus 2 --steps 6 --warmup 3 --batch 32 --mode graph --collective hip ;;
     bench3_ded) step bench3_ded 600 env TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 3 --master-addr 127.0.0.1 --master-port 29521 bench.py --gpus 3 --steps 4 --warmup 2 --batch 32 --mode eager --ps-mode dedicated ;;
     # the paper topology through the launcher (bin/tony: coordinator -> task agents -> TF_CONFIG)
