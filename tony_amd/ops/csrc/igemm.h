@@ -108,6 +108,7 @@ inline bool glds_uni_enabled() {
 }
 struct GldsVariant {
   int bm, cap, stages, kb, nwm;  // nwm: waves along M (workgroup = 2 x nwm waves)
+  bool il = false;               // interleaved DMA issue (conv_glds_kernel IL; UNI shapes only)
 };
 // 11-15: 4-wave 64/128-row tiles at 2-3 workgroups per CU; 16-19: 8-wave 256-row tiles at one (16-18)
 // or two (19) workgroups per CU -- each B (weight) tile is shared by 256 rows, so the LDS-DMA intake
@@ -115,7 +116,10 @@ struct GldsVariant {
 // profiles/r3s2_pmc_glds_conv.md), and the ring is deeper per tile
 constexpr GldsVariant kGldsVariants[] = {
     {128, 128, 2, 64, 2}, {128, 128, 3, 32, 2}, {128, 128, 4, 32, 2}, {128, 192, 3, 32, 2}, {64, 128, 4, 32, 2},
-    {256, 192, 4, 32, 4}, {256, 128, 3, 64, 4}, {256, 192, 5, 32, 4}, {256, 128, 3, 32, 4}};
+    {256, 192, 4, 32, 4}, {256, 128, 3, 64, 4}, {256, 192, 5, 32, 4}, {256, 128, 3, 32, 4},
+    // 20-24: the interleaved-issue forms of the most-picked tiles (11-19 above)
+    {128, 128, 3, 32, 2, true}, {128, 192, 3, 32, 2, true}, {128, 128, 2, 64, 2, true},
+    {256, 192, 4, 32, 4, true}, {256, 128, 3, 32, 4, true}};
 constexpr int kNumGlds = sizeof(kGldsVariants) / sizeof(kGldsVariants[0]);
 
 template <int N>
@@ -143,7 +147,11 @@ __device__ __forceinline__ int goff(int row, int ch) {
 // with a zero increment) and its bounds are re-derived once per tap in a scalar branch, instead of
 // the per-step TapPos walk + im2col address + bounds math: the general loop spends ~65 VALU
 // instructions per K-step against 12-24 MFMAs, more VALU issue than the MFMAs leave free.
-template <int BM, int BN, int ST, int KB, bool UNI, int NWM = 2>
+// IL (UNI only): the next stage's DMAs are issued one piece at a time BETWEEN the MFMA groups of the
+// current stage (after its fragments are read) instead of all at once right after the barrier -- a
+// global_load_lds costs the issuing wave ~60-185 cycles of issue, which then overlaps the matrix pipe
+// working off the MFMAs already issued (MI355X_MICROARCH.md, LDS-DMA piece issue cost).
+template <int BM, int BN, int ST, int KB, bool UNI, int NWM = 2, bool IL = false>
 __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const uint16_t* __restrict__ B, int64_t ldb,
                                                              uint16_t* __restrict__ C, int64_t ldc, int M, int N,
                                                              float* __restrict__ stats, int64_t sstride, int epi,
@@ -241,6 +249,30 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
     set_tap();
   }
 
+  // UNI: piece p < AI + BI of a stage's DMAs (A rows first), then the per-stage pointer / tap advance
+  auto issue_piece = [&](uint32_t st0, int p) {
+#pragma unroll
+    for (int i = 0; i < AI; ++i)
+      if (p == i) {
+        glds16(ap[i], st0 + aoff[i]);
+        ap[i] += ainc[i];
+      }
+#pragma unroll
+    for (int i = 0; i < BI; ++i)
+      if (p == AI + i) {
+        glds16(bp[i], st0 + boff[i]);
+        bp[i] += binc[i];
+      }
+  };
+  auto issue_advance = [&]() {
+    if (--uleft == 0) {
+      if (++us == g.S) {
+        us = 0;
+        ++ur;
+      }
+      set_tap();
+    }
+  };
   auto issue = [&](int slot) {
     const uint32_t st0 = base + slot * kStageB;
     if constexpr (UNI) {
@@ -294,9 +326,46 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
     // stage kt has landed everywhere and every wave is done reading stage kt - 1, whose slot takes
     // stage kt + ST - 1 (past the end: zero fills, which keeps the per-thread DMA count uniform)
     glds_wait_barrier<(ST - 2) * (AI + BI)>();
-    issue(slot == 0 ? ST - 1 : slot - 1);
+    const int fill = slot == 0 ? ST - 1 : slot - 1;
     const uint16_t* As = smem + slot * STAGE;
     const uint16_t* Bs = As + BM * KB;
+    if constexpr (IL && UNI) {
+      // every fragment of the stage first, then MFMA row groups with one DMA piece after each
+      constexpr int NP = AI + BI;
+      const uint32_t st0 = base + fill * kStageB;
+      bf16x8_t af[KSUB][TM], bfr[KSUB][TN];
+#pragma unroll
+      for (int kk = 0; kk < KSUB; ++kk) {
+        const int ch = kk * 4 + (lane >> 4);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bfr[kk][j] = *reinterpret_cast<const bf16x8_t*>(Bs + goff<KB>(wn * WN + j * 16 + (lane & 15), ch));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          af[kk][i] = *reinterpret_cast<const bf16x8_t*>(As + goff<KB>(wm * WM + i * 16 + (lane & 15), ch));
+      }
+      int p = 0;
+#pragma unroll
+      for (int kk = 0; kk < KSUB; ++kk)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+          // pieces spread over the KSUB * TM groups (the first groups take the extra ones)
+          constexpr int G = KSUB * TM;
+          const int g0 = kk * TM + i;
+          const int pe = (g0 + 1) * NP / G;
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (; p < pe; ++p) issue_piece(st0, p);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      issue_advance();
+      slot = slot + 1 == ST ? 0 : slot + 1;
+      continue;
+    }
+    issue(fill);
 #pragma unroll
     for (int kk = 0; kk < KSUB; ++kk) {
       const int ch = kk * 4 + (lane >> 4);
@@ -333,9 +402,10 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
   const GldsVariant gv = kGldsVariants[v - kGldsFirst];
   const int64_t bn = pick_bn(N, gv.cap);
   using std::integral_constant;
-  const auto launch = [&](auto bm, auto bnc, auto st_, auto kb, auto nwm) -> int {
+  const auto launch = [&](auto bm, auto bnc, auto st_, auto kb, auto nwm, auto il) -> int {
     constexpr int BM = decltype(bm)::value, BN = decltype(bnc)::value, ST = decltype(st_)::value;
     constexpr int KB = decltype(kb)::value, NWM = decltype(nwm)::value;
+    constexpr bool IL = decltype(il)::value;
     if constexpr (BN % (64 / (KB / 8)) != 0 || BM * (BN + 8) > ST * (BM + BN) * KB ||
                   ST * (BM + BN) * KB * 2 > 163840) {
       return -3;
@@ -346,25 +416,27 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
       const auto args = std::make_tuple(g, static_cast<const uint16_t*>(B), ldb, static_cast<uint16_t*>(C), ldc,
                                         static_cast<int>(M), static_cast<int>(N), st, sstride, epi, tiles_n);
       if (g.Cs % KB == 0 && glds_uni_enabled())
-        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true, NWM><<<static_cast<int>(tiles), 128 * NWM, 0, stream>>>(a...); }, args);
+        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true, NWM, IL><<<static_cast<int>(tiles), 128 * NWM, 0, stream>>>(a...); }, args);
+      else if (IL)
+        return -3;  // the interleaved form exists for the uniform-tap loop only
       else
         std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, false, NWM><<<static_cast<int>(tiles), 128 * NWM, 0, stream>>>(a...); }, args);
       TONY_LAUNCH_CHECK();
       return 0;
     }
   };
-  const auto by_bn = [&](auto bm, auto st_, auto kb, auto cap, auto nwm) -> int {
+  const auto by_bn = [&](auto bm, auto st_, auto kb, auto cap, auto nwm, auto il) -> int {
     constexpr int CAP = decltype(cap)::value;
     switch (bn) {
-      case 32: return launch(bm, integral_constant<int, 32>{}, st_, kb, nwm);
-      case 64: return launch(bm, integral_constant<int, 64>{}, st_, kb, nwm);
-      case 96: return launch(bm, integral_constant<int, 96>{}, st_, kb, nwm);
-      case 128: return launch(bm, integral_constant<int, 128>{}, st_, kb, nwm);
+      case 32: return launch(bm, integral_constant<int, 32>{}, st_, kb, nwm, il);
+      case 64: return launch(bm, integral_constant<int, 64>{}, st_, kb, nwm, il);
+      case 96: return launch(bm, integral_constant<int, 96>{}, st_, kb, nwm, il);
+      case 128: return launch(bm, integral_constant<int, 128>{}, st_, kb, nwm, il);
       case 160:
-        if constexpr (CAP >= 160) return launch(bm, integral_constant<int, 160>{}, st_, kb, nwm);
+        if constexpr (CAP >= 160) return launch(bm, integral_constant<int, 160>{}, st_, kb, nwm, il);
         break;
       case 192:
-        if constexpr (CAP >= 192) return launch(bm, integral_constant<int, 192>{}, st_, kb, nwm);
+        if constexpr (CAP >= 192) return launch(bm, integral_constant<int, 192>{}, st_, kb, nwm, il);
         break;
       default: break;
     }
@@ -383,16 +455,23 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
   using I5 = integral_constant<int, 5>;
   using W2 = integral_constant<int, 2>;
   using W4 = integral_constant<int, 4>;
+  using NO = std::false_type;
+  using ILV = std::true_type;
   switch (v - kGldsFirst) {
-    case 0: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{});
-    case 1: return by_bn(M128{}, I3{}, K32{}, C128{}, W2{});
-    case 2: return by_bn(M128{}, I4{}, K32{}, C128{}, W2{});
-    case 3: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{});
-    case 4: return by_bn(M64{}, I4{}, K32{}, C128{}, W2{});
-    case 5: return by_bn(M256{}, I4{}, K32{}, C192{}, W4{});
-    case 6: return by_bn(M256{}, I3{}, K64{}, C128{}, W4{});
-    case 7: return by_bn(M256{}, I5{}, K32{}, C192{}, W4{});
-    case 8: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{});
+    case 0: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, NO{});
+    case 1: return by_bn(M128{}, I3{}, K32{}, C128{}, W2{}, NO{});
+    case 2: return by_bn(M128{}, I4{}, K32{}, C128{}, W2{}, NO{});
+    case 3: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{}, NO{});
+    case 4: return by_bn(M64{}, I4{}, K32{}, C128{}, W2{}, NO{});
+    case 5: return by_bn(M256{}, I4{}, K32{}, C192{}, W4{}, NO{});
+    case 6: return by_bn(M256{}, I3{}, K64{}, C128{}, W4{}, NO{});
+    case 7: return by_bn(M256{}, I5{}, K32{}, C192{}, W4{}, NO{});
+    case 8: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, NO{});
+    case 9: return by_bn(M128{}, I3{}, K32{}, C128{}, W2{}, ILV{});
+    case 10: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{}, ILV{});
+    case 11: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, ILV{});
+    case 12: return by_bn(M256{}, I4{}, K32{}, C192{}, W4{}, ILV{});
+    case 13: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, ILV{});
     default: return -3;
   }
 }

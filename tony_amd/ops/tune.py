@@ -19,9 +19,10 @@ import torch
 AUTOTUNE = os.environ.get("TONY_CONV_AUTOTUNE", "1") != "0"
 # csrc/mfma_common.h kNtVariants (0-8) + 9: conv.hip halo-tile 3x3 path, 10: conv.hip persistent
 # direct 3x3 kernel (32/64 channels), 11-15: conv.hip LDS-DMA kernels, 16-19: their 8-wave 256-row
-# tiles (igemm.h kGldsVariants; TONY_CONV_GLDS=0 leaves them all out of the search, TONY_CONV_GLDS8=0
-# only the 8-wave ones)
-_N_GLDS = 20 if os.environ.get("TONY_CONV_GLDS8", "1") != "0" else 16
+# tiles, 20-24: interleaved-issue forms (igemm.h kGldsVariants; TONY_CONV_GLDS=0 leaves them all out of
+# the search, TONY_CONV_GLDS8=0 the 8-wave and interleaved ones, TONY_CONV_GLDS_IL=0 the interleaved)
+_N_GLDS = (25 if os.environ.get("TONY_CONV_GLDS_IL", "1") != "0" else 20) \
+    if os.environ.get("TONY_CONV_GLDS8", "1") != "0" else 16
 NT_VARIANTS = tuple(range(_N_GLDS if os.environ.get("TONY_CONV_GLDS", "1") != "0" else 11))
 _CACHE: Dict[Hashable, int] = {}
 
