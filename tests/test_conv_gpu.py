@@ -562,6 +562,37 @@ def test_conv_glds_variants(cuda, shape, v):
     assert _rel(dx, xr.grad) < 1e-2
 
 
+STRIDED_GLDS = [(2, 288, 35, 35, 384, (3, 3), 2, (0, 0)), (2, 192, 17, 17, 320, (3, 3), 2, (0, 0)),
+                (2, 96, 35, 35, 96, (3, 3), 2, (0, 0)), (2, 256, 28, 28, 512, (1, 1), 2, (0, 0)),
+                (2, 64, 57, 57, 64, (3, 3), 2, (1, 1)), (3, 128, 12, 9, 160, (3, 3), 2, (1, 1)),
+                (2, 64, 20, 20, 64, (5, 5), 3, (2, 2))]
+
+
+@pytest.mark.parametrize("v", range(11, 25))
+@pytest.mark.parametrize("shape", STRIDED_GLDS, ids=[f"{s[1]}->{s[4]}_{s[2]}k{s[5][0]}s{s[6]}" for s in STRIDED_GLDS])
+def test_strided_dgrad_glds_variants(cuda, shape, v):
+    """Strided backward-data on the LDS-DMA kernels (igemm.h BTaps: each residue class reads its taps out
+    of the full transposed filter; the epilogue's row map scatters rows to the class's dX pixels), every
+    tile variant, plain and accumulating into a gradient (flag bit 4)."""
+    from tony_amd.ops.conv import conv_dgrad
+
+    n, ci, h, w, co, (r, s), st, (ph, pw) = shape
+    if co % (64 if v in (11, 17, 22) else 32):
+        pytest.skip("the LDS-DMA strided dgrad takes uniform-tap shapes (Cout a multiple of the K-step)")
+    torch.manual_seed(v)
+    xr = torch.randn(n, ci, h, w, device=cuda, requires_grad=True)
+    wt = _nhwc(torch.randn(co, ci, r, s, device=cuda) / (ci * r * s) ** 0.5).to(torch.bfloat16)
+    yr = torch.nn.functional.conv2d(xr, wt.float(), None, st, (ph, pw))
+    dy = _nhwc(torch.randn_like(yr)).to(torch.bfloat16)
+    yr.backward(dy.float())
+    dx = conv_dgrad(dy, wt, (n, ci, h, w), st, (ph, pw), vflags=v << 8)
+    assert _rel(dx, xr.grad) < 1e-2, f"dgrad rel {_rel(dx, xr.grad):.4f}"
+    g = _nhwc(torch.randn(n, ci, h, w, device=cuda)).to(torch.bfloat16)
+    ref = g.float() + dx.float()
+    out = conv_dgrad(dy, wt, (n, ci, h, w), st, (ph, pw), vflags=v << 8, accum=g)
+    torch.testing.assert_close(out.float(), ref, rtol=1.6e-2, atol=1.6e-2)
+
+
 def test_bn_reduce_fused_into_dgrad(cuda):
     """A chain conv-BN-ReLU -> conv-BN-ReLU (strided) -> conv-BN-ReLU: each BN backward's reduction
     comes from the next conv's dgrad epilogue (csrc/conv.hip BnRed: NT kernel, strided residue classes,

@@ -217,6 +217,11 @@ def stem_wgrad(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride=1, paddin
     return None if dst is not None else out.view(co, r, s, c).permute(0, 3, 1, 2)
 
 
+# strided backward-data residue classes on the LDS-DMA tile variants (csrc/igemm.h BTaps); =0: only the
+# register-staged NT variants 0-8 (A/B)
+STRIDED_GLDS = os.environ.get("TONY_STRIDED_GLDS", "1") != "0"
+
+
 def dgrad_supported(x_shape, weight: torch.Tensor, stride=1, padding=0) -> bool:
     """Whether a tony kernel computes this conv's input gradient (every stride <= 4, Cin % 8 == 0)."""
     (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
@@ -252,6 +257,8 @@ def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, paddin
     else:
         def launch(vf, br=None):
             if (vf >> 8) & 0xff in (9, 10):  # the halo / direct tile variants are stride-1 only
+                return -3
+            if not STRIDED_GLDS and (vf >> 8) & 0xff >= 11:  # A/B: the register-staged NT kernel only
                 return -3
             return L.tony_conv_dgrad_strided(dy.data_ptr(), n, dy.shape[2], dy.shape[3], co, lddy, wt.data_ptr(), c,
                                              r, s, sh, sw, ph, pw, dx.data_ptr(), h, w, c, vf,

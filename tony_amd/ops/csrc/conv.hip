@@ -787,6 +787,12 @@ int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int6
 // One residue class of a strided dgrad with tile variant v (flags bits 8..15 of tony_conv_dgrad_strided).
 int run_nt_phase(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int64_t N, int v, const Phase& ph,
                  hipStream_t stream, int epi = 0) {
+  // the LDS-DMA kernels: class taps read out of the full filter (BTaps), rows scattered back to the class's
+  // dX pixels by the epilogue's row map; a fused BN-backward reduction (BnRed) has the NT kernel's epilogue only
+  if (v >= kGldsFirst && ph.bnr.z != nullptr) v = 0;
+  if (v >= kGldsFirst)
+    return run_glds(g, B, static_cast<int64_t>(ph.R) * ph.S * g.Cs, C, ldc, M, N, epi, nullptr, 0, v, stream, ph.rows,
+                    BTaps{ph.r0, ph.s0, ph.tsy, ph.tsx, ph.S});
   if (v == kHaloVariant || v == kDirectVariant || v >= kNumNtVariants) return -1;
   if (v == 0) {
     const int64_t bn = pick_bn(N, 192);

@@ -71,6 +71,14 @@ struct TapPos {
   }
 };
 
+// Where the B (filter) row of K-chunk tap (a, b) starts, for the uniform-tap loop: S == 0, the row is
+// contiguous over the taps (a conv's [Co][R][S][Ci] / a GEMM's B); else the taps of one residue class
+// of a strided dgrad read the FULL transposed filter Wt [Ci][R][S][Co] at r = r0 + sy * a,
+// s = s0 + sx * b (row stride R * S * Co) -- no per-class weight copies.
+struct BTaps {
+  int r0 = 0, s0 = 0, sy = 1, sx = 1, S = 0;
+};
+
 // A[M, K] row-major (row stride lda) as a Gather: one 1 x M image with K channels, 1x1 filter.
 inline Gather gemm_gather(const void* A, int64_t lda, int64_t M, int64_t K) {
   return Gather{static_cast<const uint16_t*>(A), lda, 1, static_cast<int>(M), static_cast<int>(K), 1,
@@ -155,7 +163,7 @@ template <int BM, int BN, int ST, int KB, bool UNI, int NWM = 2, bool IL = false
 __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const uint16_t* __restrict__ B, int64_t ldb,
                                                              uint16_t* __restrict__ C, int64_t ldc, int M, int N,
                                                              float* __restrict__ stats, int64_t sstride, int epi,
-                                                             int tiles_n) {
+                                                             int tiles_n, RowMap rmap, BTaps bt) {
   constexpr int NW = 2 * NWM;                 // waves: NWM along M x 2 along N
   constexpr int WM = BM / NWM, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int CPR = KB / 8;                // 16-B chunks per LDS row
@@ -236,6 +244,13 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
       for (int i = 0; i < BI; ++i) {
         bp[i] = zc;
         binc[i] = 0;
+      }
+    } else if (bt.S != 0) {  // a strided dgrad's residue class: this tap's slice of the full filter row
+      const int toff = ((bt.r0 + bt.sy * ur) * bt.S + bt.s0 + bt.sx * us) * g.Cs + ck * 8;
+#pragma unroll
+      for (int i = 0; i < BI; ++i) {
+        bp[i] = bok[i] ? brow[i] + toff : zc;
+        binc[i] = bok[i] ? KB : 0;
       }
     }
     uleft = g.Cs / KB;
@@ -388,14 +403,15 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
   const bool am = (epi & 32) != 0;  // masked-source accumulate (tony_gemm_bf16 flags bit5)
   nt_epilogue<BM, BN, TM, TN, ST * STAGE, NWM>(acc, smem, C, ldc, M, N, m0, n0,
                                            (epi & 1) ? stats + shard_off(tm, sstride) : nullptr,
-                                           (epi & 2) ? stats : nullptr, (epi & 4) != 0, RowMap{}, (epi & 8) != 0,
+                                           (epi & 2) ? stats : nullptr, (epi & 4) != 0, rmap, (epi & 8) != 0,
                                            (epi & 48) != 0, am ? reinterpret_cast<const uint16_t*>(stats) : nullptr,
                                            am ? reinterpret_cast<const uint8_t*>(sstride) : nullptr);
 }
 
 // B rows n = [K] at row stride ldb (the conv weights [Co][R][S][Ci]: ldb = K)
 inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N, int epi,
-                    float* st, int64_t sstride, int v, hipStream_t stream) {
+                    float* st, int64_t sstride, int v, hipStream_t stream, RowMap rmap = RowMap{},
+                    BTaps bt = BTaps{}) {
   if ((ldc % 8) || (ldb % 8) || (reinterpret_cast<uintptr_t>(C) & 15) || (reinterpret_cast<uintptr_t>(B) & 15) ||
       (reinterpret_cast<uintptr_t>(g.src) & 15) || (g.ld % 8) || (g.K % 8) || v < kGldsFirst || v >= kGldsFirst + kNumGlds)
     return -3;
@@ -414,11 +430,11 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
       const int64_t tiles = static_cast<int64_t>(tiles_m) * tiles_n;
       if (tiles > 0x7fffffff) return -2;
       const auto args = std::make_tuple(g, static_cast<const uint16_t*>(B), ldb, static_cast<uint16_t*>(C), ldc,
-                                        static_cast<int>(M), static_cast<int>(N), st, sstride, epi, tiles_n);
+                                        static_cast<int>(M), static_cast<int>(N), st, sstride, epi, tiles_n, rmap, bt);
       if (g.Cs % KB == 0 && glds_uni_enabled())
         std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true, NWM, IL><<<static_cast<int>(tiles), 128 * NWM, 0, stream>>>(a...); }, args);
-      else if (IL)
-        return -3;  // the interleaved form exists for the uniform-tap loop only
+      else if (IL || bt.S != 0)
+        return -3;  // the interleaved form and the class taps exist for the uniform-tap loop only
       else
         std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, false, NWM><<<static_cast<int>(tiles), 128 * NWM, 0, stream>>>(a...); }, args);
       TONY_LAUNCH_CHECK();

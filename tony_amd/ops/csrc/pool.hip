@@ -152,6 +152,71 @@ __global__ __launch_bounds__(kThreads) void maxpool_fwd_kernel(const T* __restri
   }
 }
 
+// KxK / stride S windows known at compile time (3x3/2: every pool of Inception-v3 and ResNet-50): a dX
+// pixel is covered by at most NW = ceil(K / S) windows per dimension; all NW x NW candidates (argmax
+// bytes + dY) are loaded before the first is tested -- clamped to the output grid, an out-of-range
+// candidate is masked out -- instead of the generic loop's load -> compare -> next-window chain, which
+// left the 35x35 / 147x147 backward pools latency-bound (75-135 us per call in the step).
+template <int KT, int ST, class T>
+__global__ __launch_bounds__(kThreads) void maxpool_bwd_kst_kernel(const T* __restrict__ dy,
+                                                                   const uint8_t* __restrict__ arg,
+                                                                   T* __restrict__ dx, int N, int H, int W, int C,
+                                                                   int OH, int OW, int P, int64_t lddy, int64_t lddx,
+                                                                   int accum) {
+  constexpr int NW = (KT + ST - 1) / ST;
+  const uint32_t CG = C >> 3;
+  const uint32_t total = static_cast<uint32_t>(N) * H * W * CG;
+  const uint32_t stride = gridDim.x * kThreads;
+  for (uint32_t t = blockIdx.x * kThreads + threadIdx.x; t < total; t += stride) {
+    const uint32_t cg = t % CG;
+    const uint32_t site = t / CG;
+    const int w = static_cast<int>(site % W);
+    const uint32_t nh = site / W;
+    const int h = static_cast<int>(nh % H);
+    const int64_t n = nh / H;
+    const int hp = h + P, wp = w + P;
+    const int oh_lo = hp >= KT ? (hp - KT + ST) / ST : 0;
+    const int ow_lo = wp >= KT ? (wp - KT + ST) / ST : 0;
+    const int oh_hi = min(OH - 1, hp / ST), ow_hi = min(OW - 1, wp / ST);
+    uint2 pk[NW][NW];
+    V8<T> g[NW][NW];
+#pragma unroll
+    for (int a = 0; a < NW; ++a)
+#pragma unroll
+      for (int b = 0; b < NW; ++b) {
+        const int oh = min(oh_lo + a, OH - 1), ow = min(ow_lo + b, OW - 1);
+        const int64_t osite = (n * OH + oh) * OW + ow;
+        pk[a][b] = *reinterpret_cast<const uint2*>(arg + osite * C + cg * 8);
+        g[a][b] = V8<T>::load(dy + osite * lddy + cg * 8);
+      }
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int a = 0; a < NW; ++a)
+#pragma unroll
+      for (int b = 0; b < NW; ++b) {
+        const int oh = oh_lo + a, ow = ow_lo + b;
+        const bool ok = oh <= oh_hi && ow <= ow_hi;
+        const int local = (hp - oh * ST) * KT + (wp - ow * ST);
+        float f[8];
+        g[a][b].to_float(f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t word = j < 4 ? pk[a][b].x : pk[a][b].y;
+          const int bb = (word >> (8 * (j & 3))) & 0xff;
+          acc[j] += (ok && bb == local) ? f[j] : 0.f;
+        }
+      }
+    T* d = dx + static_cast<int64_t>(site) * lddx + cg * 8;
+    if (accum) {
+      float o[8];
+      V8<T>::load(d).to_float(o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += o[j];
+    }
+    V8<T>::from_float(acc).store(d);
+  }
+}
+
 template <class T>
 __global__ __launch_bounds__(kThreads) void maxpool_bwd_kernel(const T* __restrict__ dy,
                                                                const uint8_t* __restrict__ arg,
@@ -410,9 +475,14 @@ TONY_API int tony_maxpool_bwd(const void* dy, const void* argmax, void* dx, int 
     return -1;
   if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
   const int OH = (H + 2 * P - K) / S + 1, OW = (W + 2 * P - K) / S + 1;
-  maxpool_bwd_kernel<uint16_t><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
-      static_cast<const uint16_t*>(dy), static_cast<const uint8_t*>(argmax), static_cast<uint16_t*>(dx), N, H, W, C,
-      OH, OW, K, S, P, lddy, lddx);
+  if (K == 3 && S == 2)
+    maxpool_bwd_kst_kernel<3, 2, uint16_t><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+        static_cast<const uint16_t*>(dy), static_cast<const uint8_t*>(argmax), static_cast<uint16_t*>(dx), N, H, W, C,
+        OH, OW, P, lddy, lddx, 0);
+  else
+    maxpool_bwd_kernel<uint16_t><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+        static_cast<const uint16_t*>(dy), static_cast<const uint8_t*>(argmax), static_cast<uint16_t*>(dx), N, H, W, C,
+        OH, OW, K, S, P, lddy, lddx);
   TONY_LAUNCH_CHECK();
   return 0;
 }
@@ -424,9 +494,14 @@ TONY_API int tony_maxpool_bwd_acc(const void* dy, const void* argmax, void* dx, 
     return -1;
   if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
   const int OH = (H + 2 * P - K) / S + 1, OW = (W + 2 * P - K) / S + 1;
-  maxpool_bwd_kernel<uint16_t><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
-      static_cast<const uint16_t*>(dy), static_cast<const uint8_t*>(argmax), static_cast<uint16_t*>(dx), N, H, W, C,
-      OH, OW, K, S, P, lddy, lddx, 1);
+  if (K == 3 && S == 2)
+    maxpool_bwd_kst_kernel<3, 2, uint16_t><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+        static_cast<const uint16_t*>(dy), static_cast<const uint8_t*>(argmax), static_cast<uint16_t*>(dx), N, H, W, C,
+        OH, OW, P, lddy, lddx, 1);
+  else
+    maxpool_bwd_kernel<uint16_t><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+        static_cast<const uint16_t*>(dy), static_cast<const uint8_t*>(argmax), static_cast<uint16_t*>(dx), N, H, W, C,
+        OH, OW, K, S, P, lddy, lddx, 1);
   TONY_LAUNCH_CHECK();
   return 0;
 }
@@ -510,9 +585,14 @@ TONY_API int tony_maxpool_bwd_f32(const void* dy, const void* argmax, void* dx, 
     return -1;
   if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
   const int OH = (H + 2 * P - K) / S + 1, OW = (W + 2 * P - K) / S + 1;
-  maxpool_bwd_kernel<float><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
-      static_cast<const float*>(dy), static_cast<const uint8_t*>(argmax), static_cast<float*>(dx), N, H, W, C, OH, OW,
-      K, S, P, lddy, lddx);
+  if (K == 3 && S == 2)
+    maxpool_bwd_kst_kernel<3, 2, float><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+        static_cast<const float*>(dy), static_cast<const uint8_t*>(argmax), static_cast<float*>(dx), N, H, W, C, OH,
+        OW, P, lddy, lddx, 0);
+  else
+    maxpool_bwd_kernel<float><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+        static_cast<const float*>(dy), static_cast<const uint8_t*>(argmax), static_cast<float*>(dx), N, H, W, C, OH,
+        OW, K, S, P, lddy, lddx);
   TONY_LAUNCH_CHECK();
   return 0;
 }

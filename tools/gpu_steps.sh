@@ -57,7 +57,9 @@ for s in "$@"; do
           python3 tools/prof_summary.py gpurun_out/prof --skip 6 > gpurun_out/prof_summary.md
           python3 tools/prof_summary.py gpurun_out/prof --skip 6 --by-grid --top 120 > gpurun_out/prof_by_grid.md; find gpurun_out/prof -name '*trace*' -delete ;;
     trace) step trace 600 rocprofv3 --kernel-trace -d "$R/gpurun_out/trace" -o run --output-format csv -- python3 "$R/bench.py" --steps 3 --warmup 5 --mode ${TRACE_MODE:-graph} ${BENCH_ARGS:-}
-          python3 tools/step_union.py gpurun_out/trace --per-queue > gpurun_out/trace_union.txt; find gpurun_out/trace -name "*trace*.csv" -delete ;;
+          python3 tools/step_union.py gpurun_out/trace --per-queue > gpurun_out/trace_union.txt
+          f=$(find gpurun_out/trace -name "*kernel_trace.csv" | head -1); python3 tools/crit_path.py "$f" > gpurun_out/crit_path.txt || true
+          find gpurun_out/trace -name "*trace*.csv" -delete ;;
     # ---- A/B of environment toggles against the default step: AB="name=VAR=VAL ..." (tools/ab.py)
     ab) step ab 1000 python tools/ab.py --reps ${AB_REPS:-3} ${AB_ARGS:-} ${AB:-} ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
