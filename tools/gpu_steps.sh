@@ -44,11 +44,21 @@ for s in "$@"; do
     bench2_plan) step bench2_plan 600 env TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29524 bench.py --gpus 2 --steps 6 --warmup 3 --batch 32 --mode graph --collective hip ;;
     bench3_ded) step bench3_ded 600 env TONY_BENCH_BACKEND=gloo TONY_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 3 --master-addr 127.0.0.1 --master-port 29521 bench.py --gpus 3 --steps 4 --warmup 2 --batch 32 --mode eager --ps-mode dedicated ;;
     # the paper topology through the launcher (bin/tony: coordinator -> task agents -> TF_CONFIG)
-    ps_job) step ps_job 600 bash bin/tony --src_dir tony_amd/jobs --executes inception_ps.py \
+    # (fake inventories map every task to the box's one GPU; --python_binary_path: TonY runs --executes as the
+    # command unless a python binary is given, TonyClient.buildTaskCommand)
+    ps_job) step ps_job 600 bash bin/tony --src_dir tony_amd/jobs --executes inception_ps.py --python_binary_path python3 \
               --task_params "--ps-mode dedicated --batch-size 32 --steps 6 --warmup 2" \
               --conf tony.ps.instances=1 --conf tony.worker.instances=2 --conf tony.ps.gpus=1 \
               --conf tony.worker.gpus=1 --conf tony.amd.fake-gpus=3 --conf tony.application.security.enabled=false \
-              --shell_env TONY_DIST_BACKEND=gloo ;;
+              --shell_env TONY_DIST_BACKEND=gloo
+            mkdir -p gpurun_out/ps_job_logs; cp -r "$HOME"/.tony/application_*/logs/* gpurun_out/ps_job_logs/ 2>/dev/null || true ;;
+    # TonY's default 0-GPU ps placed on worker 0's GPU (tony.amd.ps-share-gpu) owning the variables on the xGMI plane
+    ps_job_shared) step ps_job_shared 600 bash bin/tony --src_dir tony_amd/jobs --executes inception_ps.py --python_binary_path python3 \
+              --task_params "--ps-mode dedicated --batch-size 32 --steps 6 --warmup 2" \
+              --conf tony.ps.instances=1 --conf tony.worker.instances=2 --conf tony.worker.gpus=1 \
+              --conf tony.amd.fake-gpus=2 --conf tony.application.security.enabled=false \
+              --shell_env TONY_DIST_BACKEND=gloo
+            mkdir -p gpurun_out/ps_job_shared_logs; cp -r "$HOME"/.tony/application_*/logs/* gpurun_out/ps_job_shared_logs/ 2>/dev/null || true ;;
     # ---- kernel microbenches
     conv_bench) step conv_bench 400 python tools/conv_bench.py ;;
     bn_bench) step bn_bench 300 python tools/bn_bench.py ;;
