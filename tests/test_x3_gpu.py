@@ -185,3 +185,71 @@ def test_inception_fp32_step_matches_float64(cuda):
     go, gr = torch.cat(go), torch.cat(gr)
     cos = (go @ gr / (go.norm() * gr.norm())).item()
     assert cos > 0.98, cos
+
+
+@pytest.mark.parametrize("block", ["A", "B", "C", "D", "E"])
+def test_x3_block_branch_streams_and_joins_match_plain_graph(cuda, block):
+    """The fp32 blocks' fast form -- branches on their own streams, each writing its slice of one concat
+    buffer, block-input gradients met in the dgrad epilogues (GradJoin) -- gives the plain graph's
+    output and gradients (autograd sums, no streams)."""
+    from tony_amd.models import inception_v3 as I
+    from tony_amd.ops import streams
+
+    mk = {"A": lambda: I.InceptionA(64, 32, x3=True), "B": lambda: I.InceptionB(64, x3=True),
+          "C": lambda: I.InceptionC(64, 32, x3=True), "D": lambda: I.InceptionD(64, x3=True),
+          "E": lambda: I.InceptionE(64, x3=True)}
+    torch.manual_seed(0)
+    blk = mk[block]().to(DEV).to(memory_format=torch.channels_last).train()
+    x0 = _cl(torch.randn(2, 64, 17, 17, device=DEV))
+
+    def run(fast):
+        I.JOIN = fast
+        for p in blk.parameters():
+            p.grad = None
+        x = x0.clone().requires_grad_(True)
+        on = fast and streams.begin(x.device, branches=True)
+        try:
+            y = blk(x * 1.0)  # a computed tensor, as every block input is
+            g = _cl(torch.randn(y.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(1)))
+            y.backward(g)
+        finally:
+            if on:
+                streams.end()
+        torch.cuda.synchronize()
+        return y.detach().clone(), x.grad.clone(), [p.grad.clone() for p in blk.parameters()]
+
+    try:
+        y_f, dx_f, gw_f = run(True)
+        y_p, dx_p, gw_p = run(False)
+    finally:
+        I.JOIN = True
+    assert _rel(y_f, y_p) < 1e-5
+    assert _rel(dx_f, dx_p) < 1e-5
+    for a, b in zip(gw_f, gw_p):
+        assert _rel(a, b) < 1e-5
+
+
+def test_x3_planes_only_chain_matches_fp32_chain(cuda):
+    """conv-BN-ReLU -> conv-BN-ReLU where the first layer hands over only the operand planes (its BN apply
+    writes them; no fp32 output, no split pass) gives the same outputs and gradients as the fp32 hand-over."""
+    from tony_amd.ops.x3 import ConvBNActX3
+
+    torch.manual_seed(3)
+    l1 = ConvBNActX3(32, 64, 3, 1, 1).to(DEV).to(memory_format=torch.channels_last).train()
+    l2 = ConvBNActX3(64, 48, 1).to(DEV).to(memory_format=torch.channels_last).train()
+    x0 = _cl(torch.randn(2, 32, 15, 15, device=DEV))
+    g = _cl(torch.randn(2, 48, 15, 15, device=DEV))
+
+    def run(planes):
+        for p in list(l1.parameters()) + list(l2.parameters()):
+            p.grad = None
+        x = x0.clone().requires_grad_(True)
+        y = l2(l1(x * 1.0, planes_only=planes))
+        y.backward(g)
+        return y.detach().clone(), x.grad.clone(), [p.grad.clone() for p in list(l1.parameters()) + list(l2.parameters())]
+
+    ya, dxa, ga = run(True)
+    yb, dxb, gb = run(False)
+    assert _rel(ya, yb) < 1e-6 and _rel(dxa, dxb) < 1e-6
+    for a, b in zip(ga, gb):
+        assert _rel(a, b) < 1e-6

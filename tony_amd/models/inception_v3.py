@@ -30,7 +30,7 @@ from ..ops import streams, tape
 from ..ops.fused import FusedHead
 from ..ops.residual import GradJoin
 from ..ops.linear import Linear
-from ..ops.x3 import ConvBNActX3, LinearX3
+from ..ops.x3 import ConvBNActX3, LinearX3, split_act
 from .layers import ConvBNAct, conv_bn_act_maxpool, init_weights
 
 
@@ -40,16 +40,39 @@ JOIN = os.environ.get("TONY_INCEPTION_JOIN", "1") != "0"
 
 def _join(t: torch.Tensor, n: int) -> None:
     """``t`` feeds ``n`` join-aware fused ops (convs / heads / max pool): their input gradients meet in one
-    tensor, each added by its producer's epilogue (ops/residual.py GradJoin) -- no autograd add kernels."""
-    if JOIN and t.is_cuda and t.dtype == torch.bfloat16 and torch.is_grad_enabled() and t.requires_grad:
+    tensor, each added by its producer's epilogue (ops/residual.py GradJoin) -- no autograd add kernels.
+    fp32 tensors: the x3 model's (ops/x3.py ConvBNActX3 adds in its fp32 dgrad epilogue)."""
+    if JOIN and t.is_cuda and t.dtype in (torch.bfloat16, torch.float32) and torch.is_grad_enabled() \
+            and t.requires_grad:
         t._tony_join = GradJoin(n)
+
+
+def _x3_input(x: torch.Tensor) -> None:
+    """Split an fp32 block input into its x3 planes once, on the current stream, before the branches fork:
+    every branch's first conv reuses them (ops/x3.split_act caches them on x) instead of racing to make
+    them on its own branch stream."""
+    if x.is_cuda and x.dtype == torch.float32:
+        split_act(x)
+
+
+def _inner(m, x):
+    """A layer whose output only the next conv of its chain reads: an fp32 x3 layer hands it over as the
+    conv operand planes alone (ops/x3.conv_bn_act planes_only: no fp32 y, no split pass)."""
+    return m(x, planes_only=True) if isinstance(m, ConvBNActX3) else m(x)
+
+
+def _seq_inner(seq, x):
+    """An nn.Sequential (or one layer) whose output only convs read (every layer planes-only)."""
+    for m in (list(seq) if isinstance(seq, nn.Sequential) else [seq]):
+        x = _inner(m, x)
+    return x
 
 
 def _seq(seq, x, slot):
     """Run an nn.Sequential of ConvBNAct whose last layer writes into ``slot``."""
     mods = list(seq) if isinstance(seq, nn.Sequential) else [seq]
     for m in mods[:-1]:
-        x = m(x)
+        x = _inner(m, x)
     return mods[-1](x, slot=slot)
 
 
@@ -111,6 +134,18 @@ class InceptionA(_Block):
             o3, o5 = streams.parallel(lambda: _seq(self.b3, y3, s3), lambda: self.b5(y5, slot=s5))
             streams.keep(y5, y3)
             return assemble(buf, [y1, o5, o3, yp])
+        if self.x3:  # branches on their streams, each writing its slice of one fp32 buffer
+            n, _, h, w = x.shape
+            buf = concat_buffer(n, self.out_channels, h, w, x)
+            s1, s5, s3, sp = _slots(buf, (64, 64, 96, self.out_channels - 224))
+            _x3_input(x)
+            if self.training:
+                _join(x, 3)  # the three 1x1 convs (autograd adds the pool branch's gradient)
+            p = self.avgpool(x)
+            o3, o1, o5, op = streams.parallel(lambda: _seq(self.b3, x, s3), lambda: self.b1(x, slot=s1),
+                                              lambda: _seq(self.b5, x, s5), lambda: self.bp(p, slot=sp))
+            streams.keep(x, p)
+            return assemble(buf, [o1, o5, o3, op])
         p = self.avgpool(x)
         return torch.cat([self.b1(x), self.b5(x), self.b3(x), self.bp(p)], 1)
 
@@ -129,6 +164,17 @@ class InceptionB(_Block):  # 35x35 -> 17x17 reduction
             s3, sd, sp = _slots(buf, (384, 96, c))
             if self.training:
                 _join(x, 3)  # the double-3x3 chain's 1x1 head, the 3x3/2 conv, the max pool
+            od, o3, op = streams.parallel(lambda: _seq(self.bd, x, sd), lambda: self.b3(x, slot=s3),
+                                          lambda: max_pool(x, 3, 2, slot=sp))
+            streams.keep(x)
+            return assemble(buf, [o3, od, op])
+        if self.x3:
+            n, c, h, w = x.shape
+            buf = concat_buffer(n, self.out_channels, (h - 3) // 2 + 1, (w - 3) // 2 + 1, x)
+            s3, sd, sp = _slots(buf, (384, 96, c))
+            _x3_input(x)
+            if self.training:
+                _join(x, 3)  # the double-3x3 chain's 1x1, the 3x3/2 conv, the max pool
             od, o3, op = streams.parallel(lambda: _seq(self.bd, x, sd), lambda: self.b3(x, slot=s3),
                                           lambda: max_pool(x, 3, 2, slot=sp))
             streams.keep(x)
@@ -164,6 +210,18 @@ class InceptionC(_Block):  # 17x17 with factorised 7x7
             od, o7 = streams.parallel(lambda: _seq(self.bd, yd, sd), lambda: _seq(self.b7, y7, s7))
             streams.keep(y7, yd)
             return assemble(buf, [y1, o7, od, yp])
+        if self.x3:
+            n, _, h, w = x.shape
+            buf = concat_buffer(n, 768, h, w, x)
+            s1, s7, sd, sp = _slots(buf, (192, 192, 192, 192))
+            _x3_input(x)
+            if self.training:
+                _join(x, 3)  # the three 1x1 convs (autograd adds the pool branch's gradient)
+            p = self.avgpool(x)
+            od, o7, o1, op = streams.parallel(lambda: _seq(self.bd, x, sd), lambda: _seq(self.b7, x, s7),
+                                              lambda: self.b1(x, slot=s1), lambda: self.bp(p, slot=sp))
+            streams.keep(x, p)
+            return assemble(buf, [o1, o7, od, op])
         p = self.avgpool(x)
         return torch.cat([self.b1(x), self.b7(x), self.bd(x), self.bp(p)], 1)
 
@@ -194,6 +252,17 @@ class InceptionD(_Block):  # 17x17 -> 8x8 reduction
             o7, o3, op = streams.parallel(lambda: _seq(self.b7, t7, s7), lambda: self.b3(t3, slot=s3),
                                           lambda: max_pool(x, 3, 2, slot=sp))
             streams.keep(x, t3, t7)
+            return assemble(buf, [o3, o7, op])
+        if self.x3:
+            n, c, h, w = x.shape
+            buf = concat_buffer(n, self.out_channels, (h - 3) // 2 + 1, (w - 3) // 2 + 1, x)
+            s3, s7, sp = _slots(buf, (320, 192, c))
+            _x3_input(x)
+            if self.training:
+                _join(x, 3)  # the two 1x1 convs and the max pool
+            o7, o3, op = streams.parallel(lambda: _seq(self.b7, x, s7), lambda: _seq(self.b3, x, s3),
+                                          lambda: max_pool(x, 3, 2, slot=sp))
+            streams.keep(x)
             return assemble(buf, [o3, o7, op])
         return torch.cat([self.b3(x), self.b7(x), self.maxpool(x)], 1)
 
@@ -235,6 +304,27 @@ class InceptionE(_Block):  # 8x8 with split 1x3 / 3x1 branches
             (oda, odb), oa, ob = streams.parallel(dbl, lambda: self.b3a(t, slot=sa), lambda: self.b3b(t, slot=sb))
             streams.keep(t, d)
             return assemble(buf, [y1, oa, ob, oda, odb, yp])
+        elif self.x3:
+            n, _, h, w = x.shape
+            buf = concat_buffer(n, 2048, h, w, x)
+            s1, sa, sb, sda, sdb, sp = _slots(buf, (320, 384, 384, 384, 384, 192))
+            _x3_input(x)
+            if self.training:
+                _join(x, 3)  # the three 1x1 convs (autograd adds the pool branch's gradient)
+            p = self.avgpool(x)
+
+            def split(head, a, b, sa_, sb_):
+                t = _seq_inner(head, x)  # read by the two split convs only: operand planes
+                _x3_input(t)
+                if self.training:
+                    _join(t, 2)  # the 1x3 and 3x1 splits
+                return a(t, slot=sa_), b(t, slot=sb_)
+
+            (oda, odb), (oa, ob), y1, yp = streams.parallel(
+                lambda: split(self.bd, self.bda, self.bdb, sda, sdb), lambda: split(self.b3, self.b3a, self.b3b, sa, sb),
+                lambda: self.b1(x, slot=s1), lambda: self.bp(p, slot=sp))
+            streams.keep(x, p)
+            return assemble(buf, [y1, oa, ob, oda, odb, yp])
         else:
             y1 = self.b1(x)
             t = self.b3(x)
@@ -253,7 +343,7 @@ class InceptionAux(_Block):
     def forward(self, x):
         tony = self.fused or self.x3
         x = avg_pool(x, 5, 3) if tony else nn.functional.avg_pool2d(x, 5, 3)
-        x = self.conv1(self.conv0(x))
+        x = self.conv1(_inner(self.conv0, x))
         x = global_avg_pool(x) if tony else torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)
 
@@ -285,10 +375,10 @@ class InceptionV3(nn.Module):
         # the last conv of each group feeds a 3x3/2 max pool; fused training runs BN + ReLU + pool as
         # one kernel there (models/layers.py conv_bn_act_maxpool)
         for m in self.stem[:-1]:
-            x = m(x)
+            x = _inner(m, x)
         x = conv_bn_act_maxpool(self.stem[-1], x, 3, 2)
         for m in self.stem2[:-1]:
-            x = m(x)
+            x = _inner(m, x)
         return conv_bn_act_maxpool(self.stem2[-1], x, 3, 2)
 
     def _segments(self):

@@ -66,6 +66,9 @@ _SIGNATURES = {
     "tony_bn_bwd_apply": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p,
                           c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p,
                           c_void_p, c_int, c_void_p],
+    "tony_bn_apply_f32_x3": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
+                             c_void_p, c_void_p, c_int, c_float, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                             c_float, c_void_p],
     "tony_bn_apply_res": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
                           c_void_p, c_int64, c_void_p, c_void_p, c_int, c_float, c_int, c_int, c_void_p, c_void_p,
                           c_void_p, c_void_p, c_float, c_void_p],

@@ -158,7 +158,10 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_stats_kernel(
 // RES: y = act(bn(x) + res)  (ResNet bottleneck tail: BN + identity add + ReLU in one pass)
 // mask (RES form, optional): one byte per 8 channels of a row (bit j: y > 0 for channel 8 * cg + j,
 // row stride ldm bytes) -- the ReLU mask the backward needs, 1/16 of the bytes of re-reading y
-template <bool RES, class T = uint16_t>
+// X3 (T = float, the fp32 step of ops/x3.py): y is written as the bf16 [hi | lo | hi] planes the next
+// convolution reads (row stride ldy >= 3C in bf16 elements, plane p at column p * C) instead of fp32 --
+// for a layer whose only consumer is another x3 conv, the fp32 y and the split pass over it are never made
+template <bool RES, class T = uint16_t, bool X3 = false>
 __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
     const T* __restrict__ x, int64_t M, int C, int64_t ldx, int64_t rows_per_block,
     const T* __restrict__ res, int64_t ldr,
@@ -219,6 +222,18 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
       float t = fmaf(f[j], sc[j], sh[j]);
       if (RES) t += q[j];
       f[j] = relu ? relu_f(t) : t;
+    }
+    if constexpr (X3) {
+      const V8<uint16_t> hi = V8<uint16_t>::from_float(f);
+      float hf[8], lo[8];
+      hi.to_float(hf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) lo[j] = f[j] - hf[j];
+      uint16_t* d = reinterpret_cast<uint16_t*>(y) + row * ldy + rm.cg * 8;
+      hi.store(d);
+      V8<uint16_t>::from_float(lo).store(d + C);
+      hi.store(d + 2 * C);
+      return;
     }
     const V8<T> out = V8<T>::from_float(f);
     out.store(yb + row * ldyt);
@@ -1053,6 +1068,24 @@ TONY_API int tony_bn_apply_f32(const void* x, int64_t M, int C, int64_t ldx, voi
   plan_rows(M, C, 4, 8192, &rpb, &grid);
   bn_fwd_apply_kernel<false, float><<<grid, kThreads, bn_lds_table(C, 2), stream>>>(
       static_cast<const float*>(x), M, C, ldx, rpb, nullptr, 0, static_cast<float*>(y), ldy, sum, sumsq, sstride,
+      gamma, beta, param_bf16, eps, relu, mode, save_mean, save_invstd, running_mean, running_var, momentum, Segs{});
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// tony_bn_apply_f32 writing y as its x3 planes (bf16 [M][3C], row stride ldy3 >= 3C): bn_fwd_apply_kernel X3
+TONY_API int tony_bn_apply_f32_x3(const void* x, int64_t M, int C, int64_t ldx, void* y3, int64_t ldy3,
+                                  const float* sum, const float* sumsq, int64_t sstride, const void* gamma,
+                                  const void* beta, int param_bf16, float eps, int relu, int mode, float* save_mean,
+                                  float* save_invstd, float* running_mean, float* running_var, float momentum,
+                                  hipStream_t stream) {
+  if (bad_c(C) || (ldx % 4) || ldy3 < 3 * C || (ldy3 % 8) || sstride < 0 || (reinterpret_cast<uintptr_t>(y3) & 15))
+    return -1;
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 4, 8192, &rpb, &grid);
+  bn_fwd_apply_kernel<false, float, true><<<grid, kThreads, bn_lds_table(C, 2), stream>>>(
+      static_cast<const float*>(x), M, C, ldx, rpb, nullptr, 0, static_cast<float*>(y3), ldy3, sum, sumsq, sstride,
       gamma, beta, param_bf16, eps, relu, mode, save_mean, save_invstd, running_mean, running_var, momentum, Segs{});
   TONY_LAUNCH_CHECK();
   return 0;

@@ -20,16 +20,15 @@ model from it (models/inception_v3.py).
 """
 from __future__ import annotations
 
+import ctypes
+import os
 from typing import Tuple
 
 import torch
 
-import ctypes
-import os
-
-from . import _lib, streams, tune
+from . import _lib, concat, streams, tune
 from .arena import zeros_f32
-from .bn import _as_rows
+from .bn import _as_rows, _rows_view
 
 ACT = 0b010  # activation / gradient planes: [hi | lo | hi]
 WGT = 0b100  # weight planes:                [hi | hi | lo]
@@ -134,31 +133,43 @@ def conv_fwd(x3: torch.Tensor, cp: int, w3: torch.Tensor, wshape, stride, paddin
     return z
 
 
-def conv_dgrad(d3: torch.Tensor, wt3: torch.Tensor, co: int, x_shape, wshape, stride, padding) -> torch.Tensor:
-    """fp32 dX from the dZ planes d3 [N, 3Co, OH, OW] and wt3 [C][R][S][3Co]."""
+def _accum_f32_ok(t, x_shape) -> bool:
+    """``t`` can take the fp32 dgrad epilogue's accumulating store: fp32, x's shape, dense channels_last."""
+    if t is None or t.dtype != _F32 or tuple(t.shape) != tuple(x_shape) or t.data_ptr() % 16:
+        return False
+    rv = _rows_view(t)
+    return rv is not None and rv[2] == t.shape[1]
+
+
+def conv_dgrad(d3: torch.Tensor, wt3: torch.Tensor, co: int, x_shape, wshape, stride, padding,
+               accum: torch.Tensor | None = None) -> torch.Tensor:
+    """fp32 dX from the dZ planes d3 [N, 3Co, OH, OW] and wt3 [C][R][S][3Co].  ``accum``: an fp32 gradient
+    of x's shape (dense channels_last) that dX is added into by the epilogue (flag bit 4) and returned --
+    a tensor with several consumers (ops/residual.py GradJoin) needs no add kernel."""
     n, c, h, w = x_shape
     _, _, r, s = wshape
     (sh, sw), (ph, pw) = _pair(stride), _pair(padding)
     _, _, oh, ow = d3.shape
-    dx = _cl(n, c, h, w, d3.device)
+    acc = 16 if _accum_f32_ok(accum, x_shape) else 0
+    dx = accum if acc else _cl(n, c, h, w, d3.device)
     L, st = _lib.lib(), _lib.stream_ptr(d3.device)
     ldd = 3 * co
-    if (sh, sw) == (1, 1):
-        def launch(vf):
+    def launch(vf, out=dx, flags=8):
+        if (sh, sw) == (1, 1):
             return L.tony_conv_dgrad(d3.data_ptr(), n, oh, ow, 3 * co, ldd, wt3.data_ptr(), c, r, s, ph, pw,
-                                     dx.data_ptr(), h, w, c, 8 | vf, None, st)
-        name = "tony_conv_dgrad (x3)"
-    else:
-        def launch(vf):
-            return L.tony_conv_dgrad_strided(d3.data_ptr(), n, oh, ow, 3 * co, ldd, wt3.data_ptr(), c, r, s, sh, sw,
-                                             ph, pw, dx.data_ptr(), h, w, c, 8 | vf, None, st)
-        name = "tony_conv_dgrad_strided (x3)"
+                                     out.data_ptr(), h, w, c, flags | vf, None, st)
+        return L.tony_conv_dgrad_strided(d3.data_ptr(), n, oh, ow, 3 * co, ldd, wt3.data_ptr(), c, r, s, sh, sw,
+                                         ph, pw, out.data_ptr(), h, w, c, flags | vf, None, st)
+    name = "tony_conv_dgrad (x3)" if (sh, sw) == (1, 1) else "tony_conv_dgrad_strided (x3)"
     key = ("x3_dgrad", tuple(d3.shape), tuple(x_shape), tuple(wshape), (sh, sw), (ph, pw))
     variants = tuple(v for v in tune.NT_VARIANTS if v not in (9, 10))  # fp32 epilogue: NT / LDS-DMA kernels
     vf = tune.cached(key)
-    if vf is None:
-        vf = tune.pick(key, launch, variants)
-    _lib.check(launch(vf), name)
+    if vf is None:  # timed into a scratch output: an accumulating call must add exactly once
+        scratch = _cl(n, c, h, w, d3.device) if acc else dx
+        vf = tune.pick(key, lambda v: launch(v, scratch), variants)
+    _lib.check(launch(vf, dx, 8 | acc), name)
+    if accum is not None and not acc:
+        return accum.add_(dx)
     return dx
 
 
@@ -233,22 +244,42 @@ def _wgrad_direct3(d3, lddy, x3, ldx, n, h, w, c, co, ph, pw, oh, ow, dst=None):
 
 
 # ---- BatchNorm on fp32 rows -------------------------------------------------------------------------
-def bn_apply(z: torch.Tensor, stats, gamma, beta, rmean, rvar, eps, momentum, relu, training):
+def bn_apply(z: torch.Tensor, stats, gamma, beta, rmean, rvar, eps, momentum, relu, training, out=None):
     """y = act(BN(z)) in fp32; training: batch statistics from ``stats`` (sharded [sum | sumsq]),
-    running statistics updated.  Returns (y, mean, invstd)."""
+    running statistics updated.  ``out``: a channel slice of a block's concat buffer (ops/concat.py) to
+    write y into.  Returns (y, mean, invstd)."""
     n, co, oh, ow = z.shape
     m = n * oh * ow
-    y = _cl(n, co, oh, ow, z.device)
+    y = out if out is not None else _cl(n, co, oh, ow, z.device)
+    ldy = _rows_view(y)[2]
     mean = torch.empty(co, dtype=_F32, device=z.device)
     invstd = torch.empty(co, dtype=_F32, device=z.device)
     L = _lib.lib()
-    rc = L.tony_bn_apply_f32(z.data_ptr(), m, co, co, y.data_ptr(), co, _lib.ptr(stats),
+    rc = L.tony_bn_apply_f32(z.data_ptr(), m, co, co, y.data_ptr(), ldy, _lib.ptr(stats),
                              None if stats is None else stats.data_ptr() + 4 * co, 2 * co if stats is not None else 0,
                              gamma.data_ptr(), beta.data_ptr(), 0, float(eps), int(relu), 0 if training else 1,
                              mean.data_ptr(), invstd.data_ptr(), _lib.ptr(rmean), _lib.ptr(rvar), float(momentum),
                              _lib.stream_ptr(z.device))
     _lib.check(rc, "tony_bn_apply_f32")
     return y, mean, invstd
+
+
+def bn_apply_planes(z: torch.Tensor, stats, gamma, beta, rmean, rvar, eps, momentum, relu, training):
+    """bn_apply writing y as its x3 operand planes (bf16 channels_last [N, 3Co, OH, OW], split_act's layout;
+    Co a multiple of 8).  Returns (planes, mean, invstd)."""
+    n, co, oh, ow = z.shape
+    m = n * oh * ow
+    y3 = torch.empty((n, oh, ow, 3 * co), dtype=_BF16, device=z.device).permute(0, 3, 1, 2)
+    mean = torch.empty(co, dtype=_F32, device=z.device)
+    invstd = torch.empty(co, dtype=_F32, device=z.device)
+    rc = _lib.lib().tony_bn_apply_f32_x3(z.data_ptr(), m, co, co, y3.data_ptr(), 3 * co, _lib.ptr(stats),
+                                         None if stats is None else stats.data_ptr() + 4 * co,
+                                         2 * co if stats is not None else 0, gamma.data_ptr(), beta.data_ptr(), 0,
+                                         float(eps), int(relu), 0 if training else 1, mean.data_ptr(),
+                                         invstd.data_ptr(), _lib.ptr(rmean), _lib.ptr(rvar), float(momentum),
+                                         _lib.stream_ptr(z.device))
+    _lib.check(rc, "tony_bn_apply_f32_x3")
+    return y3, mean, invstd
 
 
 def bn_backward(z, dy, mean, invstd, gamma, beta, relu, planes: bool = False, dgamma=None, dbeta=None):
@@ -289,15 +320,25 @@ L_apply_x3 = "tony_bn_bwd_apply_f32_x3"
 
 class _ConvBNActX3Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, gamma, beta, rmean, rvar, stride, padding, training, momentum, eps, relu):
+    def forward(ctx, x, weight, gamma, beta, rmean, rvar, stride, padding, training, momentum, eps, relu, slot=None,
+                planes_only=False):
         x3, cp = split_act(x)
         w3 = split_weight(weight)
         co = weight.shape[0]
         stats = zeros_f32(_lib.stat_floats(co), x.device) if training else None
         z = conv_fwd(x3, cp, w3, weight.shape, stride, padding, stats)
-        y, mean, invstd = bn_apply(z, stats, gamma, beta, rmean, rvar, eps, momentum, relu, training)
+        n, _, oh, ow = z.shape
+        if planes_only and slot is None and co % 8 == 0:
+            # the only consumer is another x3 conv: BN writes its operand planes, the fp32 y is never made
+            y3, mean, invstd = bn_apply_planes(z, stats, gamma, beta, rmean, rvar, eps, momentum, relu, training)
+            _LAST_PLANES[0] = y3
+            y = torch.empty_strided((n, co, oh, ow), (0, 0, 0, 0), dtype=_F32, device=z.device)  # shape only
+        else:
+            y, mean, invstd = bn_apply(z, stats, gamma, beta, rmean, rvar, eps, momentum, relu, training,
+                                       out=concat.take(slot, n, co, oh, ow, z))
         ctx.save_for_backward(x3, weight, gamma, beta, z, mean, invstd)
         ctx.conf = (cp, tuple(x.shape), stride, padding, relu, x.requires_grad)
+        ctx.join = getattr(x, "_tony_join", None)  # ops/residual.py GradJoin: x has other consumers
         return y
 
     @staticmethod
@@ -321,14 +362,32 @@ class _ConvBNActX3Fn(torch.autograd.Function):
             dw = conv_wgrad(d3, x3, cp, weight.shape, stride, padding)
         dx = None
         if need_dx and ctx.needs_input_grad[0]:
-            dx = conv_dgrad(d3, split_weight_t(weight), weight.shape[0], x_shape, weight.shape, stride, padding)
+            join = ctx.join
+            pend = join.take() if join is not None else None  # another consumer's parked dX: add into it
+            dx = conv_dgrad(d3, split_weight_t(weight), weight.shape[0], x_shape, weight.shape, stride, padding,
+                            accum=pend)
+            if join is not None:
+                dx = join.settle(dx)
+            streams.keep(dx)  # may be consumed on another (branch) stream
         _lib.report_inplace((weight, gamma, beta), (dw, dgamma, dbeta))
-        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None
+        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None
+
+
+_LAST_PLANES = [None]
 
 
 def conv_bn_act(x, weight, gamma, beta, rmean, rvar, stride=1, padding=0, training=True, momentum=0.1, eps=1e-3,
-                relu=True):
-    return _ConvBNActX3Fn.apply(x, weight, gamma, beta, rmean, rvar, stride, padding, training, momentum, eps, relu)
+                relu=True, slot=None, planes_only=False):
+    """``planes_only``: the output feeds only other x3 convs -- it comes back as a shape-only tensor whose
+    operand planes split_act finds cached on it (never read as fp32: no pool, concat or loss may take it)."""
+    _LAST_PLANES[0] = None
+    y = _ConvBNActX3Fn.apply(x, weight, gamma, beta, rmean, rvar, stride, padding, training, momentum, eps, relu,
+                             slot, planes_only)
+    planes = _LAST_PLANES[0]
+    if planes is not None:
+        _LAST_PLANES[0] = None
+        y._tony_x3 = (y._version, planes, weight.shape[0])
+    return y
 
 
 # ---- the classifier: an x3 GEMM --------------------------------------------------------------------
@@ -400,10 +459,12 @@ class ConvBNActX3(torch.nn.Module):
         self.relu = relu
         self.is_1x1 = kk == (1, 1) and _pair(stride) == (1, 1) and _pair(padding) == (0, 0)
 
-    def forward(self, x):
+    def forward(self, x, slot=None, planes_only=False):
+        """``slot`` (ops/concat.Slot): write the output into a block's fp32 concat buffer; ``planes_only``:
+        the output feeds only other x3 convs (conv_bn_act)."""
         c, bn = self.conv, self.bn
         return conv_bn_act(x, c.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, c.stride, c.padding,
-                           self.training, bn.momentum, bn.eps, self.relu)
+                           self.training, bn.momentum, bn.eps, self.relu, slot, planes_only)
 
 
 __all__ = ["ConvBNActX3", "LinearX3", "conv_bn_act", "split_act", "split_weight", "split_weight_t", "cp_of"]
