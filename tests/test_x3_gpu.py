@@ -223,10 +223,14 @@ def test_x3_block_branch_streams_and_joins_match_plain_graph(cuda, block):
         y_p, dx_p, gw_p = run(False)
     finally:
         I.JOIN = True
+    # the BN statistics are fp32 atomics (order-dependent rounding, ~1e-7), so a pre-activation within that
+    # of 0 can take the other side of its ReLU from one run to the next -- even between two runs of the
+    # SAME graph (measured: tools/x3_block_diag.py, block D plain vs plain: 1e-3 / 8e-3 on dX).  A lost or
+    # doubled gradient contribution (what a join / stream bug gives) is >= 30 %.
     assert _rel(y_f, y_p) < 1e-5
-    assert _rel(dx_f, dx_p) < 1e-5
+    assert _rel(dx_f, dx_p) < 5e-2
     for a, b in zip(gw_f, gw_p):
-        assert _rel(a, b) < 1e-5
+        assert _rel(a, b) < 5e-2
 
 
 def test_x3_planes_only_chain_matches_fp32_chain(cuda):
@@ -250,6 +254,7 @@ def test_x3_planes_only_chain_matches_fp32_chain(cuda):
 
     ya, dxa, ga = run(True)
     yb, dxb, gb = run(False)
-    assert _rel(ya, yb) < 1e-6 and _rel(dxa, dxb) < 1e-6
+    # (a ReLU decision within the atomics' rounding of 0 may flip between runs: see the block test above)
+    assert _rel(ya, yb) < 1e-6 and _rel(dxa, dxb) < 5e-2
     for a, b in zip(ga, gb):
-        assert _rel(a, b) < 1e-6
+        assert _rel(a, b) < 5e-2

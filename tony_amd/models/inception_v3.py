@@ -55,10 +55,15 @@ def _x3_input(x: torch.Tensor) -> None:
         split_act(x)
 
 
+# TONY_X3_PLANES=0: intra-chain x3 layers hand over the fp32 y (A/B, diagnosis)
+X3_PLANES = os.environ.get("TONY_X3_PLANES", "1") != "0"
+X3_BLOCKS = os.environ.get("TONY_X3_BLOCKS", "1") != "0"
+
+
 def _inner(m, x):
     """A layer whose output only the next conv of its chain reads: an fp32 x3 layer hands it over as the
     conv operand planes alone (ops/x3.conv_bn_act planes_only: no fp32 y, no split pass)."""
-    return m(x, planes_only=True) if isinstance(m, ConvBNActX3) else m(x)
+    return m(x, planes_only=True) if (X3_PLANES and isinstance(m, ConvBNActX3)) else m(x)
 
 
 def _seq_inner(seq, x):
@@ -93,6 +98,8 @@ class _Block(nn.Module):
         super().__init__()
         self.fused = fused and not x3
         self.x3 = x3
+        # the fp32 blocks' fast form (concat slots, branch streams, joins); TONY_X3_BLOCKS=0: torch.cat graph
+        self.x3_fast = x3 and X3_BLOCKS
 
     def avgpool(self, x):
         if self.fused or self.x3:
@@ -134,7 +141,7 @@ class InceptionA(_Block):
             o3, o5 = streams.parallel(lambda: _seq(self.b3, y3, s3), lambda: self.b5(y5, slot=s5))
             streams.keep(y5, y3)
             return assemble(buf, [y1, o5, o3, yp])
-        if self.x3:  # branches on their streams, each writing its slice of one fp32 buffer
+        if self.x3_fast:  # branches on their streams, each writing its slice of one fp32 buffer
             n, _, h, w = x.shape
             buf = concat_buffer(n, self.out_channels, h, w, x)
             s1, s5, s3, sp = _slots(buf, (64, 64, 96, self.out_channels - 224))
@@ -168,7 +175,7 @@ class InceptionB(_Block):  # 35x35 -> 17x17 reduction
                                           lambda: max_pool(x, 3, 2, slot=sp))
             streams.keep(x)
             return assemble(buf, [o3, od, op])
-        if self.x3:
+        if self.x3_fast:
             n, c, h, w = x.shape
             buf = concat_buffer(n, self.out_channels, (h - 3) // 2 + 1, (w - 3) // 2 + 1, x)
             s3, sd, sp = _slots(buf, (384, 96, c))
@@ -210,7 +217,7 @@ class InceptionC(_Block):  # 17x17 with factorised 7x7
             od, o7 = streams.parallel(lambda: _seq(self.bd, yd, sd), lambda: _seq(self.b7, y7, s7))
             streams.keep(y7, yd)
             return assemble(buf, [y1, o7, od, yp])
-        if self.x3:
+        if self.x3_fast:
             n, _, h, w = x.shape
             buf = concat_buffer(n, 768, h, w, x)
             s1, s7, sd, sp = _slots(buf, (192, 192, 192, 192))
@@ -253,7 +260,7 @@ class InceptionD(_Block):  # 17x17 -> 8x8 reduction
                                           lambda: max_pool(x, 3, 2, slot=sp))
             streams.keep(x, t3, t7)
             return assemble(buf, [o3, o7, op])
-        if self.x3:
+        if self.x3_fast:
             n, c, h, w = x.shape
             buf = concat_buffer(n, self.out_channels, (h - 3) // 2 + 1, (w - 3) // 2 + 1, x)
             s3, s7, sp = _slots(buf, (320, 192, c))
@@ -304,7 +311,7 @@ class InceptionE(_Block):  # 8x8 with split 1x3 / 3x1 branches
             (oda, odb), oa, ob = streams.parallel(dbl, lambda: self.b3a(t, slot=sa), lambda: self.b3b(t, slot=sb))
             streams.keep(t, d)
             return assemble(buf, [y1, oa, ob, oda, odb, yp])
-        elif self.x3:
+        elif self.x3_fast:
             n, _, h, w = x.shape
             buf = concat_buffer(n, 2048, h, w, x)
             s1, sa, sb, sda, sdb, sp = _slots(buf, (320, 384, 384, 384, 384, 192))

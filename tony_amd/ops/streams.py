@@ -138,7 +138,7 @@ def active() -> bool:
 # GPU at 14 ms the host issue cost matters: 2 measured 13.90 / 13.89 ms/step vs 14.1-15.1 at 1
 # (profiles/r2s3_host_levers_ab.log)
 BATCH = int(os.environ.get("TONY_WGRAD_BATCH", "2"))
-_pending: List[Callable[[], object]] = []
+_pending: List[tuple] = []  # (fn, the stream that queued it)
 # ...except for big operands: a batch forks from the current stream when it is flushed, so a pending
 # op waits for whatever the compute stream was given in between (the next layer's BN backward and
 # data gradient).  At the end of an Inception backward that is the serial stem chain: the 149x149
@@ -206,10 +206,19 @@ def _flush(side: torch.cuda.Stream) -> None:
     if not work:
         return
     cur = current(side.device_index)
-    fork(cur, side)
+    # the side stream waits for every stream that queued work of this batch: a backward node of an
+    # Inception branch runs on its branch stream, so a batch may hold a weight gradient whose dZ is
+    # still being produced on another stream than the one flushing (waiting on the flushing stream
+    # alone raced: x3 block D, tools/x3_block_diag.py)
+    srcs = {}
+    for _, src in work:
+        srcs.setdefault(src.cuda_stream, src)
+    srcs.setdefault(cur.cuda_stream, cur)
+    for src in srcs.values():
+        fork(src, side)
     torch.cuda.set_stream(side)
     try:
-        for fn in work:
+        for fn, _ in work:
             out = fn()
             assert out is None, "only in-place gradient work may run on the side stream"
     finally:
@@ -237,8 +246,9 @@ def run(fn: Callable[[], object], *keep: torch.Tensor):
             _issued[0] += 1
         return fn()
     urgent = URGENT_BYTES > 0 and bool(keep) and keep[0].numel() * keep[0].element_size() >= URGENT_BYTES
+    src = current(side.device_index)  # the stream fn's operands are produced on
     with _lock:
-        _pending.append(fn)
+        _pending.append((fn, src))
         _keep.extend(keep)
         _issued[0] += 1
         full = len(_pending) >= BATCH or urgent

@@ -163,6 +163,10 @@ def conv_dgrad(d3: torch.Tensor, wt3: torch.Tensor, co: int, x_shape, wshape, st
     name = "tony_conv_dgrad (x3)" if (sh, sw) == (1, 1) else "tony_conv_dgrad_strided (x3)"
     key = ("x3_dgrad", tuple(d3.shape), tuple(x_shape), tuple(wshape), (sh, sw), (ph, pw))
     variants = tuple(v for v in tune.NT_VARIANTS if v not in (9, 10))  # fp32 epilogue: NT / LDS-DMA kernels
+    from .conv import STRIDED_GLDS
+
+    if (sh, sw) != (1, 1) and not STRIDED_GLDS:
+        variants = tuple(v for v in variants if v < 11)
     vf = tune.cached(key)
     if vf is None:  # timed into a scratch output: an accumulating call must add exactly once
         scratch = _cl(n, c, h, w, d3.device) if acc else dx
