@@ -258,3 +258,45 @@ def test_x3_planes_only_chain_matches_fp32_chain(cuda):
     assert _rel(ya, yb) < 1e-6 and _rel(dxa, dxb) < 5e-2
     for a, b in zip(ga, gb):
         assert _rel(a, b) < 5e-2
+
+
+@pytest.mark.parametrize("block", ["D", "E"])
+def test_x3_block_fast_form_captures_into_a_graph(cuda, block):
+    """The fp32 blocks' fast form captures into one HIP graph with the weight-gradient and branch streams
+    on.  Regression: InceptionE's split convs meet their input gradient on ONE branch stream, and the
+    join's stream fork made that stream wait on itself; hipStreamEndCapture then recursed through the
+    self-join until the host stack overflowed (ops/streams.fork skips a self-wait)."""
+    from tony_amd.models import inception_v3 as I
+    from tony_amd.ops import streams
+
+    torch.manual_seed(0)
+    blk = {"D": lambda: I.InceptionD(64, x3=True), "E": lambda: I.InceptionE(64, x3=True)}[block]()
+    blk = blk.to(DEV).to(memory_format=torch.channels_last).train()
+    x0 = _cl(torch.randn(2, 64, 17 if block == "D" else 8, 17 if block == "D" else 8, device=DEV)).requires_grad_(True)
+
+    def step():
+        on = streams.begin(DEV, branches=True)
+        try:
+            y = blk(x0 * 1.0)
+            y.backward(torch.ones_like(y))
+        finally:
+            if on:
+                streams.end()
+        return y
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    eager_dx = x0.grad.clone()
+    x0.grad = None
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    x0.grad.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert _rel(x0.grad, eager_dx / 2) < 5e-2  # eager_dx summed two warm-up steps

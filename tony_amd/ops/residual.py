@@ -56,8 +56,9 @@ class GradJoin:
     def _ordered(self, g):
         """``g`` (parked on self.stream) usable on the current stream."""
         if self.stream is not None:
-            cur = torch.cuda.current_stream(g.device)
-            if cur is not self.stream:
+            cur = streams.current(g.device.index)
+            # (by handle: current_stream() returns a new Stream object per call)
+            if cur.cuda_stream != self.stream.cuda_stream:
                 streams.fork(self.stream, cur)
                 if isinstance(g, MaskedGrad):
                     streams.keep(g.dy, g.mask)

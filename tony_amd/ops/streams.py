@@ -190,13 +190,22 @@ def current(device_index: int) -> torch.cuda.Stream:
 
 
 def fork(producer: torch.cuda.Stream, consumer: torch.cuda.Stream) -> None:
-    """``consumer`` waits for everything enqueued on ``producer`` so far (no host block)."""
+    """``consumer`` waits for everything enqueued on ``producer`` so far (no host block).  A stream is
+    never made to wait on itself: inside a capture HIP records that as the stream joining its own
+    capture, and hipStreamEndCapture then recurses through the self-join until the host stack overflows
+    (x3 InceptionE, both split convs of a join on one branch stream: tools/x3_capture_diag.py --bt)."""
+    if producer.cuda_stream == consumer.cuda_stream:
+        return
     ring = _RAW.get(producer.device_index) or _raw_ring(producer.device_index)
     i = _ev_next[0]
     _ev_next[0] = i + 1
     rc = _FORK[0](ring[i % _EV_RING], producer.cuda_stream, consumer.cuda_stream)
     if rc:
         _lib.check(rc, "tony_fork")
+
+
+_DEBUG = os.environ.get("TONY_STREAMS_DEBUG", "0") == "1"
+_ALL_SRCS = os.environ.get("TONY_FLUSH_ALL_SRCS", "1") != "0"
 
 
 def _flush(side: torch.cuda.Stream) -> None:
@@ -214,7 +223,15 @@ def _flush(side: torch.cuda.Stream) -> None:
     for _, src in work:
         srcs.setdefault(src.cuda_stream, src)
     srcs.setdefault(cur.cuda_stream, cur)
-    for src in srcs.values():
+    if _DEBUG:
+        st = []
+        for src in srcs.values():
+            torch.cuda.set_stream(src)
+            st.append((hex(src.cuda_stream), torch.cuda.is_current_stream_capturing()))
+        torch.cuda.set_stream(cur)
+        print(f"[streams] flush {len(work)} cur={hex(cur.cuda_stream)} side={hex(side.cuda_stream)} srcs={st}",
+              flush=True)
+    for src in (srcs.values() if _ALL_SRCS else [cur]):
         fork(src, side)
     torch.cuda.set_stream(side)
     try:
