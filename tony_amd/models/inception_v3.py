@@ -147,11 +147,11 @@ class InceptionA(_Block):
             s1, s5, s3, sp = _slots(buf, (64, 64, 96, self.out_channels - 224))
             _x3_input(x)
             if self.training:
-                _join(x, 3)  # the three 1x1 convs (autograd adds the pool branch's gradient)
-            p = self.avgpool(x)
+                _join(x, 4)  # the three 1x1 convs and the pool branch's avg pool
             o3, o1, o5, op = streams.parallel(lambda: _seq(self.b3, x, s3), lambda: self.b1(x, slot=s1),
-                                              lambda: _seq(self.b5, x, s5), lambda: self.bp(p, slot=sp))
-            streams.keep(x, p)
+                                              lambda: _seq(self.b5, x, s5),
+                                              lambda: self.bp(self.avgpool(x), slot=sp))
+            streams.keep(x)
             return assemble(buf, [o1, o5, o3, op])
         p = self.avgpool(x)
         return torch.cat([self.b1(x), self.b5(x), self.b3(x), self.bp(p)], 1)
@@ -223,11 +223,11 @@ class InceptionC(_Block):  # 17x17 with factorised 7x7
             s1, s7, sd, sp = _slots(buf, (192, 192, 192, 192))
             _x3_input(x)
             if self.training:
-                _join(x, 3)  # the three 1x1 convs (autograd adds the pool branch's gradient)
-            p = self.avgpool(x)
+                _join(x, 4)  # the three 1x1 convs and the pool branch's avg pool
             od, o7, o1, op = streams.parallel(lambda: _seq(self.bd, x, sd), lambda: _seq(self.b7, x, s7),
-                                              lambda: self.b1(x, slot=s1), lambda: self.bp(p, slot=sp))
-            streams.keep(x, p)
+                                              lambda: self.b1(x, slot=s1),
+                                              lambda: self.bp(self.avgpool(x), slot=sp))
+            streams.keep(x)
             return assemble(buf, [o1, o7, od, op])
         p = self.avgpool(x)
         return torch.cat([self.b1(x), self.b7(x), self.bd(x), self.bp(p)], 1)
@@ -317,8 +317,7 @@ class InceptionE(_Block):  # 8x8 with split 1x3 / 3x1 branches
             s1, sa, sb, sda, sdb, sp = _slots(buf, (320, 384, 384, 384, 384, 192))
             _x3_input(x)
             if self.training:
-                _join(x, 3)  # the three 1x1 convs (autograd adds the pool branch's gradient)
-            p = self.avgpool(x)
+                _join(x, 4)  # the three 1x1 convs and the pool branch's avg pool
 
             def split(head, a, b, sa_, sb_):
                 t = _seq_inner(head, x)  # read by the two split convs only: operand planes
@@ -329,8 +328,8 @@ class InceptionE(_Block):  # 8x8 with split 1x3 / 3x1 branches
 
             (oda, odb), (oa, ob), y1, yp = streams.parallel(
                 lambda: split(self.bd, self.bda, self.bdb, sda, sdb), lambda: split(self.b3, self.b3a, self.b3b, sa, sb),
-                lambda: self.b1(x, slot=s1), lambda: self.bp(p, slot=sp))
-            streams.keep(x, p)
+                lambda: self.b1(x, slot=s1), lambda: self.bp(self.avgpool(x), slot=sp))
+            streams.keep(x)
             return assemble(buf, [y1, oa, ob, oda, odb, yp])
         else:
             y1 = self.b1(x)

@@ -21,7 +21,9 @@ namespace {
 
 constexpr int kThreads = 256;
 
-template <class T>
+// ACC: y += box3(x) / 9 (the avg pool's input gradient added into another consumer's, ops/residual.py
+// GradJoin: no separate add kernel over the block input)
+template <class T, bool ACC = false>
 __global__ __launch_bounds__(kThreads) void box3_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                         int N, int H, int W, int C, int64_t ldx, int64_t ldy) {
   // 32-bit index math (the host checks the element count fits): 64-bit div/mod are long
@@ -64,7 +66,14 @@ __global__ __launch_bounds__(kThreads) void box3_kernel(const T* __restrict__ x,
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] *= (1.f / 9.f);
-    V8<T>::from_float(acc).store(y + static_cast<int64_t>(site) * ldy + cg * 8);
+    T* dst = y + static_cast<int64_t>(site) * ldy + cg * 8;
+    if (ACC) {
+      float o[8];
+      V8<T>::load(dst).to_float(o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += o[j];
+    }
+    V8<T>::from_float(acc).store(dst);
   }
 }
 
@@ -561,6 +570,21 @@ TONY_API int tony_avgpool3_s1p1_f32(const void* x, void* y, int N, int H, int W,
   if (C % 8 || ldx % 4 || ldy % 4 || static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
   box3_kernel<float><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
       static_cast<const float*>(x), static_cast<float*>(y), N, H, W, C, ldx, ldy);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// y += box3x3(x) / 9 (fp32 / bf16 rows: ``f32``)
+TONY_API int tony_avgpool3_s1p1_acc(const void* x, void* y, int N, int H, int W, int C, int64_t ldx, int64_t ldy,
+                                    int f32, hipStream_t stream) {
+  if (C % 8 || ldx % 8 || ldy % 8 || static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
+  const int g = grid_for(static_cast<int64_t>(N) * H * W * (C / 8));
+  if (f32)
+    box3_kernel<float, true><<<g, kThreads, 0, stream>>>(static_cast<const float*>(x), static_cast<float*>(y), N, H,
+                                                          W, C, ldx, ldy);
+  else
+    box3_kernel<uint16_t, true><<<g, kThreads, 0, stream>>>(static_cast<const uint16_t*>(x),
+                                                             static_cast<uint16_t*>(y), N, H, W, C, ldx, ldy);
   TONY_LAUNCH_CHECK();
   return 0;
 }

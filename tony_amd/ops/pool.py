@@ -20,6 +20,14 @@ def _ok(x: torch.Tensor) -> bool:
     return x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and x.shape[1] % 8 == 0
 
 
+def _dense_rows(t: torch.Tensor, shape) -> bool:
+    """``t`` (bf16 or fp32) has ``shape`` as dense 16-B aligned channels_last rows: an accumulating store fits."""
+    if tuple(t.shape) != tuple(shape) or t.data_ptr() % 16:
+        return False
+    rv = _rows_view(t)
+    return rv is not None and rv[2] == t.shape[1]
+
+
 def _box3(src, n, c, h, w, ld_src):
     out = _nhwc_empty(n, c, h, w, src)
     rc = _fn("tony_avgpool3_s1p1", src)(src.data_ptr(), out.data_ptr(), n, h, w, c, ld_src, c,
@@ -33,13 +41,29 @@ class _AvgPool3Fn(torch.autograd.Function):
     def forward(ctx, x):
         x, (_, c, ld) = _as_rows(x)
         n, _, h, w = x.shape
+        ctx.join = getattr(x, "_tony_join", None)  # ops/residual.py GradJoin: x has other consumers
         return _box3(x, n, c, h, w, ld)
 
     @staticmethod
     def backward(ctx, dy):
         dy, (_, c, ld) = _as_rows(dy)
         n, _, h, w = dy.shape
-        return _box3(dy, n, c, h, w, ld)  # symmetric stencil: dx = box(dy)/9
+        join = ctx.join if ctx.needs_input_grad[0] else None
+        pend = join.take() if join is not None else None
+        if pend is not None and pend.dtype == dy.dtype and _dense_rows(pend, (n, c, h, w)):
+            # another consumer of x already wrote its gradient: box(dy)/9 is added into it in-kernel
+            rc = _lib.lib().tony_avgpool3_s1p1_acc(dy.data_ptr(), pend.data_ptr(), n, h, w, c, ld, c,
+                                                   int(dy.dtype == torch.float32), _lib.stream_ptr(dy.device))
+            _lib.check(rc, "tony_avgpool3_s1p1_acc")
+            dx = pend
+        else:
+            dx = _box3(dy, n, c, h, w, ld)  # symmetric stencil: dx = box(dy)/9
+            if pend is not None:
+                dx = pend.add_(dx)
+        if join is not None:
+            dx = join.settle(dx)
+        streams.keep(dx)  # may be consumed on another (branch) stream
+        return dx
 
 
 class _MaxPoolFn(torch.autograd.Function):
