@@ -118,25 +118,34 @@ def collectives_rank(rank, world, port):
     return {"rs": out.tolist(), "ag": gathered.tolist(), "max": mx}
 
 
-def kv_rank(role, index, num_servers, num_workers, port, kind, steps):
+def kv_rank(role, index, num_servers, num_workers, port, kind, steps, device="cpu"):
     os.environ.update(DMLC_ROLE=role, DMLC_NUM_SERVER=str(num_servers), DMLC_NUM_WORKER=str(num_workers),
                       DMLC_PS_ROOT_URI="127.0.0.1", DMLC_PS_ROOT_PORT=str(port), TASK_INDEX=str(index))
+    if device == "cpu":
+        os.environ["TONY_KV_PLANE"] = "gloo"
     import tony_amd.kv as kv
 
     if kv.run_role():
         return {"role": role}
     store = kv.create(kind)
-    w = torch.zeros(3)
+    w = torch.zeros(3, device=device)
     store.init("w", w)
-    store.init(7, torch.ones(2))
+    store.init(7, torch.ones(2, device=device))
+    big_n = 1000003  # not a multiple of 16 bytes: the copy kernel's tail
+    store.init("big", torch.zeros(big_n, device=device))
     store.set_optimizer(kv.create_optimizer("sgd", learning_rate=0.5, rescale_grad=1.0 / num_workers))
     seen = []
+    big = torch.empty(big_n, device=device)
+    ramp = torch.arange(big_n, dtype=torch.float32, device=device) / big_n
     for s in range(steps):
-        store.push("w", torch.full((3,), float(store.rank + 1)))
+        store.push("w", torch.full((3,), float(store.rank + 1), device=device))
+        store.push("big", ramp * (store.rank + 1))
         store.pull("w", out=w)
-        seen.append(w.clone())
-    out2 = torch.empty(2)
+        store.pull("big", out=big)
+        seen.append(w.clone().cpu())
+    out2 = torch.empty(2, device=device)
     store.pull(7, out=out2)
-    res = {"role": role, "rank": store.rank, "seen": seen, "k7": out2.tolist(), "n": store.num_workers}
+    res = {"role": role, "rank": store.rank, "seen": seen, "k7": out2.tolist(), "n": store.num_workers,
+           "big": big.cpu(), "plane_ops": list(getattr(store, "plane_ops", [0, 0]))}
     store.close()
     return res

@@ -1,0 +1,47 @@
+"""The kvstore server modes with their payloads on the GPU plane (parallel/kvstore.py _KvPlane): a
+scheduler, one server and two workers as processes on the box's GPU (the server shares it, as TonY's
+0-GPU servers would share a worker's).  Values are checked against the closed-form SGD result -- the
+same numbers the gloo-payload CPU test (tests/test_dist_cpu.py) pins -- and the pushes / pulls must have
+gone over the plane."""
+import multiprocessing as mp
+import socket
+
+import pytest
+import torch
+
+import dist_workers as W
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("kind", ["dist_sync", "dist_async"])
+def test_kvstore_server_modes_move_payloads_on_the_gpu_plane(kind):
+    port, steps = _port(), 3
+    args = [("scheduler", 0, 1, 2, port, kind, steps, "cuda"), ("server", 0, 1, 2, port, kind, steps, "cuda"),
+            ("worker", 0, 1, 2, port, kind, steps, "cuda"), ("worker", 1, 1, 2, port, kind, steps, "cuda")]
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(len(args)) as pool:
+        outs = [r.get(110) for r in [pool.apply_async(W.kv_rank, a) for a in args]]
+    workers = [o for o in outs if o["role"] == "worker"]
+    assert sorted(o["rank"] for o in workers) == [0, 1]
+    n = 1000003
+    ramp = torch.arange(n, dtype=torch.float32) / n
+    for o in workers:
+        assert o["k7"] == [1.0, 1.0]
+        # every push and pull of "w" / "big" rode the plane (the key-7 pull too)
+        assert o["plane_ops"] == [2 * steps, 2 * steps + 1], o["plane_ops"]
+    if kind == "dist_sync":
+        for o in workers:
+            for s, w in enumerate(o["seen"]):
+                torch.testing.assert_close(w, torch.full((3,), -0.75 * (s + 1)))
+            # big: w -= 0.5 * (1 + 2) / 2 * ramp per round
+            torch.testing.assert_close(o["big"], -0.75 * steps * ramp, rtol=1e-5, atol=1e-6)
+    else:
+        final = min(float(o["seen"][-1][0]) for o in workers)
+        assert final == pytest.approx(-2.25)

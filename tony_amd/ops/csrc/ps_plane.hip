@@ -34,6 +34,8 @@
 #include <cstring>
 #include <type_traits>
 
+#include <algorithm>
+
 #include "common.h"
 #include "optim_math.h"
 
@@ -307,7 +309,34 @@ uint64_t budget_ticks(double seconds) {
   return static_cast<uint64_t>(seconds * khz * 1000.0);
 }
 
+// The kvstore payload plane (parallel/kvstore.py): one key's bytes between a local tensor and a peer's
+// IPC-mapped window (either side may be the peer), 16 B per lane, the < 16 B tail by lane 0 of block 0.
+__global__ __launch_bounds__(256) void kv_copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                       int64_t bytes) {
+  const int64_t n16 = bytes >> 4;
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n16;
+       i += static_cast<int64_t>(gridDim.x) * 256)
+    d[i] = s[i];
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (int64_t i = n16 << 4; i < bytes; ++i) dst[i] = src[i];
+}
+
 }  // namespace
+
+// dst <- src (bytes), both 16-B aligned device addresses (local memory or a mapped peer window)
+TONY_API int tony_kv_copy(void* dst, const void* src, int64_t bytes, hipStream_t stream) {
+  if (dst == nullptr || src == nullptr || bytes < 0 || (reinterpret_cast<uintptr_t>(dst) & 15) ||
+      (reinterpret_cast<uintptr_t>(src) & 15))
+    return -1;
+  if (bytes == 0) return 0;
+  const int64_t n16 = (bytes >> 4) + 1;
+  const int blocks = static_cast<int>(std::min<int64_t>(1024, (n16 + 255) / 256));
+  kv_copy_kernel<<<blocks, 256, 0, stream>>>(static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), bytes);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
 
 TONY_API int64_t tony_ps_header_bytes() { return kHeader; }
 TONY_API int tony_ps_max_buckets() { return kMaxBuckets; }

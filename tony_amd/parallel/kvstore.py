@@ -26,6 +26,16 @@ Transport for the server modes: one torch.distributed (gloo) group over
 servers + workers; the scheduler task hosts its TCPStore on
 ``DMLC_PS_ROOT_PORT`` and exits when every member has finished.  Requests are
 an int64 header ``[op, key, numel, dtype]`` followed by the payload.
+
+GPU payload plane (``TONY_KV_PLANE=xgmi``, the default when every member sees a GPU): every member
+allocates an IPC-mapped window on its GPU (csrc/ps_plane.hip) and maps its peers' -- a worker the
+servers', a server the workers'.  A pushed GPU tensor is stored by a copy kernel straight into its
+row of the owning server's window and only the header goes over gloo; the server replies to a pull
+by storing the value into the worker's landing area and sending a one-element token.  The payload
+bytes never leave the GPUs (xGMI between devices; the server may share a worker's GPU, like TonY's
+0-GPU ps).  Keys that do not fit the windows (``TONY_KV_WINDOW_MB``) and CPU tensors keep the gloo
+payload.  A worker re-pushing a key before pulling it (its last row may not have been read yet) sends
+that push over gloo: a pull reply is what proves the server consumed the row.
 """
 from __future__ import annotations
 
@@ -38,7 +48,7 @@ from typing import Dict, List, Optional, Union
 import torch
 import torch.distributed as dist
 
-OP_INIT, OP_PUSH, OP_PULL, OP_OPT, OP_STOP = range(5)
+OP_INIT, OP_PUSH, OP_PULL, OP_OPT, OP_STOP, OP_PUSH_X, OP_PULL_X = range(7)  # _X: payload on the GPU plane
 TAG_HDR, TAG_DATA, TAG_REPLY = 1, 2, 3
 _DTYPES = [torch.float32, torch.float16, torch.bfloat16, torch.float64, torch.int64, torch.int32, torch.uint8]
 _EXIT_KEY = "tony/kv/exited"
@@ -247,6 +257,90 @@ def _init_group(topo: _Topology):
     return store, workers
 
 
+def _pad16(n: int) -> int:
+    return (n + 15) // 16 * 16
+
+
+def _plane_wanted() -> bool:
+    mode = os.environ.get("TONY_KV_PLANE", "auto").lower()
+    if mode in ("gloo", "0", "off"):
+        return False
+    if mode == "xgmi" and not torch.cuda.is_available():
+        raise RuntimeError("TONY_KV_PLANE=xgmi but this task sees no GPU")
+    return torch.cuda.is_available()
+
+
+class _KvPlane:
+    """The GPU payload windows of one server / worker (module docstring).  Layout, computed identically
+    by a server and every worker from the keys in init order: server s's window holds, per key it owns,
+    one receive row per worker; a worker's window is split in one landing region per server, each holding
+    that server's keys back to back."""
+
+    def __init__(self, topo: "_Topology", device: torch.device):
+        import ctypes
+
+        from ..ops import _lib
+
+        self.topo, self.device, self.L = topo, device, _lib.lib()
+        self.bytes = int(os.environ.get("TONY_KV_WINDOW_MB", "64")) << 20
+        hsize = self.L.tony_xgmi_handle_bytes()
+        win, handle = ctypes.c_void_p(), (ctypes.c_uint8 * hsize)()
+        with torch.cuda.device(device):
+            _lib.check(self.L.tony_ps_window_alloc(self.bytes, ctypes.byref(win), handle), "tony_ps_window_alloc")
+        self.window = win.value
+        hdr = self.L.tony_ps_header_bytes()
+        self.base = self.window + hdr
+        allh: List[Optional[bytes]] = [None] * topo.world
+        dist.all_gather_object(allh, bytes(handle))
+        self.peer: Dict[int, int] = {}
+        self._opened: List[int] = []
+        peers = range(topo.num_servers, topo.world) if topo.role == "server" else range(topo.num_servers)
+        for r in peers:
+            p = ctypes.c_void_p()
+            buf = (ctypes.c_uint8 * hsize).from_buffer_copy(allh[r])
+            with torch.cuda.device(device):
+                _lib.check(self.L.tony_xgmi_open(buf, ctypes.byref(p)), f"tony_xgmi_open(rank {r})")
+            self.peer[r] = p.value + hdr
+            self._opened.append(p.value)
+        self.region = self.bytes // max(1, topo.num_servers) // 16 * 16  # a worker's landing region per server
+        self.row_used = [0] * topo.num_servers
+        self.land_used = [0] * topo.num_servers
+        self.keys: Dict[int, tuple] = {}  # kid -> (server, nbytes, row_off, land_off)
+
+    def add_key(self, kid: int, nbytes: int) -> bool:
+        s = self.topo.server_of(kid)
+        rows = self.topo.num_workers * _pad16(nbytes)
+        if self.row_used[s] + rows > self.bytes or self.land_used[s] + _pad16(nbytes) > self.region:
+            return False  # stays on the gloo payload path (decided identically on every member)
+        self.keys[kid] = (s, nbytes, self.row_used[s], s * self.region + self.land_used[s])
+        self.row_used[s] += rows
+        self.land_used[s] += _pad16(nbytes)
+        return True
+
+    def copy(self, dst: int, src: int, nbytes: int) -> None:
+        from ..ops import _lib
+
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.tony_kv_copy(dst, src, nbytes, _lib.stream_ptr(self.device)), "tony_kv_copy")
+            torch.cuda.current_stream(self.device).synchronize()  # landed before the header / token is sent
+
+    def close(self) -> None:
+        for p in self._opened:
+            self.L.tony_xgmi_close(p)
+        self._opened = []
+        if self.window is not None:
+            self.L.tony_xgmi_free(self.window)
+            self.window = None
+
+
+def _make_plane(topo: "_Topology", device: Optional[torch.device]) -> Optional[_KvPlane]:
+    """Collective over servers + workers: the plane when every member wants it (else None everywhere)."""
+    want = device is not None and _plane_wanted()
+    allw: List[Optional[bool]] = [None] * topo.world
+    dist.all_gather_object(allw, want)
+    return _KvPlane(topo, device) if all(allw) else None
+
+
 def run_scheduler(poll_s: float = 0.05) -> int:
     """The scheduler role: host the rendezvous store until every server and worker exited."""
     topo = _Topology()
@@ -258,9 +352,10 @@ def run_scheduler(poll_s: float = 0.05) -> int:
 
 
 class _Server:
-    def __init__(self, topo: _Topology, sync: bool):
+    def __init__(self, topo: _Topology, sync: bool, plane: Optional[_KvPlane] = None):
         self.topo = topo
         self.sync = sync
+        self.plane = plane
         self.values: Dict[int, torch.Tensor] = {}
         self.accum: Dict[int, torch.Tensor] = {}
         self.pushed: Dict[int, set] = {}
@@ -270,8 +365,14 @@ class _Server:
         self.sends = []
         self.applied = 0
 
-    def _reply(self, kid: int, worker: int) -> None:
-        self.sends.append(dist.isend(self.values[kid].contiguous(), worker, tag=TAG_REPLY))
+    def _reply(self, kid: int, worker: int, via_plane: bool = False) -> None:
+        if via_plane:  # the value into the worker's landing area, then a one-element token
+            _, nbytes, _, land_off = self.plane.keys[kid]
+            v = self.values[kid].contiguous()
+            self.plane.copy(self.plane.peer[worker] + land_off, v.data_ptr(), nbytes)
+            self.sends.append(dist.isend(torch.ones(1, dtype=torch.int64), worker, tag=TAG_REPLY))
+            return
+        self.sends.append(dist.isend(self.values[kid].contiguous().cpu(), worker, tag=TAG_REPLY))
 
     def _finish_round(self, kid: int) -> None:
         merged = self.accum.pop(kid)
@@ -281,14 +382,23 @@ class _Server:
             self.values[kid].copy_(merged)
         self.applied += 1
         self.pushed[kid] = set()
-        for w in self.deferred.pop(kid, []):
-            self._reply(kid, w)
+        for w, via in self.deferred.pop(kid, []):
+            self._reply(kid, w, via)
 
     def handle(self, worker: int, hdr: List[int], buf: Optional[torch.Tensor] = None) -> bool:
         op, kid, numel, dcode = hdr
         if op in (OP_INIT, OP_PUSH, OP_OPT) and buf is None:
             buf = torch.empty(numel, dtype=_DTYPES[dcode])
             dist.recv(buf, worker, tag=TAG_DATA)
+        via = op == OP_PULL_X
+        if op == OP_PUSH_X:  # the payload is in this worker's receive row of the window: take it now
+            _, nbytes, row_off, _ = self.plane.keys[kid]
+            buf = torch.empty(numel, dtype=_DTYPES[dcode], device=self.plane.device)
+            w = worker - self.topo.num_servers
+            self.plane.copy(buf.data_ptr(), self.plane.base + row_off + w * _pad16(nbytes), nbytes)
+            op = OP_PUSH
+        elif op == OP_PULL_X:
+            op = OP_PULL
         if op in (OP_PUSH, OP_PULL) and kid not in self.values:
             # raced ahead of worker 0's INIT (it is sent before the workers' barrier, but
             # the server may poll this worker first): replay once the key exists
@@ -296,6 +406,8 @@ class _Server:
             return True
         if op in (OP_INIT, OP_PUSH, OP_OPT):
             if op == OP_INIT:
+                if self.plane is not None and self.plane.add_key(kid, buf.numel() * buf.element_size()):
+                    buf = buf.to(self.plane.device)  # the key's value lives on the server's GPU
                 self.values[kid] = buf
                 self.pushed[kid] = set()
                 for w, h, b in self.early.pop(kid, []):
@@ -303,19 +415,20 @@ class _Server:
             elif op == OP_OPT:
                 self.opt = Optimizer.from_json(bytes(buf.tolist()).decode())
             elif not self.sync:
-                self.accum[kid] = buf
+                self.accum[kid] = buf.to(self.values[kid].device)
                 self._finish_round(kid)
             else:
                 acc = self.accum.get(kid)
-                self.accum[kid] = buf.to(self.values[kid].dtype) if acc is None else acc.add_(buf)
+                v = self.values[kid]
+                self.accum[kid] = buf.to(v.device, v.dtype) if acc is None else acc.add_(buf.to(acc.device))
                 self.pushed[kid].add(worker)
                 if len(self.pushed[kid]) == self.topo.num_workers:
                     self._finish_round(kid)
         elif op == OP_PULL:
             if self.sync and worker in self.pushed.get(kid, ()):
-                self.deferred.setdefault(kid, []).append(worker)
+                self.deferred.setdefault(kid, []).append((worker, via))
             else:
-                self._reply(kid, worker)
+                self._reply(kid, worker, via)
         elif op == OP_STOP:
             return False
         return True
@@ -340,10 +453,16 @@ def run_server(sync: Optional[bool] = None) -> int:
     """The server role: own keys until every worker sent STOP."""
     topo = _Topology()
     store, _ = _init_group(topo)
+    dev = None
+    if torch.cuda.is_available():  # a server may share a worker's GPU (TonY's servers ask for none)
+        dev = torch.device("cuda", _env_int("TONY_KV_DEVICE", topo.index % torch.cuda.device_count()))
+    plane = _make_plane(topo, dev)
     if sync is None:  # every worker announces its kvstore type before its first request
         sync = store.get("tony/kv/type").decode() != "dist_async"
-    _Server(topo, sync).serve()
+    _Server(topo, sync, plane).serve()
     dist.barrier()
+    if plane is not None:
+        plane.close()
     store.add(_EXIT_KEY, 1)
     return 0
 
@@ -357,8 +476,12 @@ class DistKVStore(KVStore):
         if self.topo.num_servers < 1:
             raise ValueError(f"{kind} needs DMLC_NUM_SERVER >= 1 server task")
         self.store, self.workers = _init_group(self.topo)
+        dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else None
+        self.plane = _make_plane(self.topo, dev)
         self.store.set("tony/kv/type", kind)
         self._shapes: Dict[int, torch.Size] = {}
+        self._unread: set = set()  # keys pushed on the plane and not pulled since (their row may be unread)
+        self.plane_ops = [0, 0]  # pushes / pulls whose payload went over the GPU plane (tests)
         self._closed = False
 
     @property
@@ -382,23 +505,49 @@ class DistKVStore(KVStore):
             kid = self._key(k)
             t = _as_list(v)[0].detach()
             self._shapes[kid] = t.shape
+            if self.plane is not None:
+                self.plane.add_key(kid, t.numel() * t.element_size())
             if self.rank == 0:
                 self._send(OP_INIT, kid, t.reshape(-1).cpu().contiguous())
         self.barrier()
 
+    def _on_plane(self, kid: int, t: torch.Tensor) -> bool:
+        return self.plane is not None and kid in self.plane.keys and t.is_cuda
+
     def push(self, key, value, priority: int = 0) -> None:  # noqa: ARG002
         for k, v in zip(*self._keys_vals(key, value)):
             kid = self._key(k)
-            self._send(OP_PUSH, kid, _merge(_as_list(v)).reshape(-1).cpu().contiguous())
+            g = _merge(_as_list(v)).reshape(-1)
+            if self._on_plane(kid, g) and kid not in self._unread:
+                srv, nbytes, row_off, _ = self.plane.keys[kid]
+                g = g.to(self.plane.device).contiguous()
+                self.plane.copy(self.plane.peer[srv] + row_off + self.rank * _pad16(nbytes), g.data_ptr(), nbytes)
+                dist.send(torch.tensor([OP_PUSH_X, kid, g.numel(), _dcode(g.dtype)], dtype=torch.int64), srv,
+                          tag=TAG_HDR)
+                self._unread.add(kid)
+                self.plane_ops[0] += 1
+                continue
+            self._send(OP_PUSH, kid, g.cpu().contiguous())
 
     def pull(self, key, out=None, priority: int = 0, ignore_sparse: bool = True):  # noqa: ARG002
         keys, outs = self._keys_vals(key, out)
         for k, o in zip(keys, outs):
             kid = self._key(k)
             first = _as_list(o)[0]
-            srv = self._send(OP_PULL, kid)
-            buf = torch.empty(first.numel(), dtype=first.dtype)
-            dist.recv(buf, srv, tag=TAG_REPLY)
+            if self._on_plane(kid, first):
+                srv, nbytes, _, land_off = self.plane.keys[kid]
+                dist.send(torch.tensor([OP_PULL_X, kid, 0, 0], dtype=torch.int64), srv, tag=TAG_HDR)
+                tok = torch.empty(1, dtype=torch.int64)
+                dist.recv(tok, srv, tag=TAG_REPLY)  # the value is in this worker's landing area
+                buf = torch.empty(first.numel(), dtype=first.dtype, device=self.plane.device)
+                self.plane.copy(buf.data_ptr(), self.plane.base + land_off, nbytes)
+                self._unread.discard(kid)  # the server answered: it consumed this worker's earlier rows
+                self.plane_ops[1] += 1
+            else:
+                srv = self._send(OP_PULL, kid)
+                buf = torch.empty(first.numel(), dtype=first.dtype)
+                dist.recv(buf, srv, tag=TAG_REPLY)
+                self._unread.discard(kid)
             for t in _as_list(o):
                 t.copy_(buf.view(t.shape).to(t.device))
 
@@ -430,6 +579,8 @@ class DistKVStore(KVStore):
         for s in range(self.topo.num_servers):
             dist.send(torch.tensor([OP_STOP, s, 0, 0], dtype=torch.int64), s, tag=TAG_HDR)
         dist.barrier()
+        if self.plane is not None:
+            self.plane.close()
         self.store.add(_EXIT_KEY, 1)
 
 
