@@ -714,6 +714,11 @@ def test_visible_mode_auto_isolates_unless_a_peer_plane_is_configured():
     assert resolve_visible_mode(conf(tony__ps__instances=1, tony__worker__instances=4)) == "none"
     assert resolve_visible_mode(conf(tony__ps__instances=1, **{"tony__amd__ps-plane": "rccl"})) == "hip"
     assert resolve_visible_mode(conf(tony__application__framework="pytorch", tony__ps__instances=1)) == "hip"
+    # MXNet kvstore servers with GPU workers: the payload plane maps peer windows
+    mx = dict(tony__application__framework="mxnet", tony__server__instances=1, tony__worker__gpus=1)
+    assert resolve_visible_mode(conf(**mx)) == "none"
+    assert resolve_visible_mode(conf(**mx, **{"tony__amd__kv-plane": "gloo"})) == "hip"
+    assert resolve_visible_mode(conf(tony__application__framework="mxnet", tony__server__instances=1)) == "hip"
     for m in ("none", "hip", "rocr"):
         assert resolve_visible_mode(conf(**{"tony__amd__visible-devices-mode": m, "tony__amd__collective": "hip"})) == m
     assert Configuration().get("tony.amd.visible-devices-mode") == "auto"

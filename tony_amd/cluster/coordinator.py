@@ -83,6 +83,10 @@ def resolve_visible_mode(conf) -> str:
     if framework == "tensorflow" and conf.get_int("tony.ps.instances", 0) > 0 \
             and conf.get(K.AMD_PS_PLANE, "xgmi").lower() == "xgmi":
         return "none"
+    # an MXNet job whose kvstore servers move GPU payloads on the peer-mapped plane (parallel/kvstore.py)
+    if framework == "mxnet" and conf.get_int("tony.server.instances", 0) > 0 \
+            and conf.get_int("tony.worker.gpus", 0) > 0 and conf.get(K.AMD_KV_PLANE, "auto").lower() != "gloo":
+        return "none"
     return "hip"
 
 
@@ -461,6 +465,7 @@ class Coordinator:
         # data-plane collectives of the tony_amd jobs: RCCL or the xGMI peer-memory kernels
         env["TONY_COLLECTIVE"] = c.get(K.AMD_COLLECTIVE, "rccl").lower()
         env["TONY_PS_PLANE"] = c.get(K.AMD_PS_PLANE, "xgmi").lower()
+        env["TONY_KV_PLANE"] = c.get(K.AMD_KV_PLANE, "auto").lower()
         # whether the ps tasks own GPUs (the Inception PS job picks its topology from it on every task)
         env["TONY_PS_GPUS"] = str(c.get_int("tony.ps.gpus", 0))
         # the ps tasks sit on a worker's GPU, shared (utils/core.ps_shares_worker_gpu): every task learns

@@ -112,6 +112,7 @@ AMD = PREFIX + "amd."
 AMD_VISIBLE_DEVICES_MODE = AMD + "visible-devices-mode"   # auto | hip | rocr | none
 AMD_PS_SHARE_GPU = AMD + "ps-share-gpu"                  # 0-GPU ps on a worker's GPU
 AMD_PS_PLANE = AMD + "ps-plane"                          # xgmi | rccl (dedicated ps data plane)
+AMD_KV_PLANE = AMD + "kv-plane"                          # auto | xgmi | gloo (mxnet kvstore server payloads)
 AMD_NUMA_BIND = AMD + "numa-bind"                          # bind task CPUs to its GPU's NUMA node
 AMD_COLLECTIVE = AMD + "collective"                        # rccl | hip
 AMD_FAKE_GPUS = AMD + "fake-gpus"                          # CI: pretend the node has N GPUs (-1 = detect)

@@ -286,14 +286,17 @@ class _KvPlane:
         hsize = self.L.tony_xgmi_handle_bytes()
         win, handle = ctypes.c_void_p(), (ctypes.c_uint8 * hsize)()
         with torch.cuda.device(device):
-            _lib.check(self.L.tony_ps_window_alloc(self.bytes, ctypes.byref(win), handle), "tony_ps_window_alloc")
-        self.window = win.value
-        hdr = self.L.tony_ps_header_bytes()
-        self.base = self.window + hdr
-        allh: List[Optional[bytes]] = [None] * topo.world
-        dist.all_gather_object(allh, bytes(handle))
-        self.peer: Dict[int, int] = {}
+            rc = self.L.tony_ps_window_alloc(self.bytes, ctypes.byref(win), handle)
+        self.window = win.value if rc == 0 else None
         self._opened: List[int] = []
+        hdr = self.L.tony_ps_header_bytes()
+        allh: List[Optional[bytes]] = [None] * topo.world
+        dist.all_gather_object(allh, bytes(handle) if rc == 0 else b"")  # every member joins, even on failure
+        _lib.check(rc, "tony_ps_window_alloc")
+        if not all(allh):
+            raise RuntimeError("a peer could not allocate its window")
+        self.base = self.window + hdr
+        self.peer: Dict[int, int] = {}
         peers = range(topo.num_servers, topo.world) if topo.role == "server" else range(topo.num_servers)
         for r in peers:
             p = ctypes.c_void_p()
@@ -328,7 +331,7 @@ class _KvPlane:
         for p in self._opened:
             self.L.tony_xgmi_close(p)
         self._opened = []
-        if self.window is not None:
+        if getattr(self, "window", None) is not None:
             self.L.tony_xgmi_free(self.window)
             self.window = None
 
@@ -338,7 +341,24 @@ def _make_plane(topo: "_Topology", device: Optional[torch.device]) -> Optional[_
     want = device is not None and _plane_wanted()
     allw: List[Optional[bool]] = [None] * topo.world
     dist.all_gather_object(allw, want)
-    return _KvPlane(topo, device) if all(allw) else None
+    if not all(allw):
+        return None
+    plane, err = None, ""
+    try:
+        plane = _KvPlane(topo, device)
+    except Exception as e:  # noqa: BLE001 - e.g. a peer GPU this task cannot see: agree on gloo everywhere
+        err = f"{type(e).__name__}: {e}"
+    errs: List[Optional[str]] = [None] * topo.world
+    dist.all_gather_object(errs, err)
+    if any(errs):
+        if plane is not None:
+            plane.close()
+        import sys
+
+        print(f"[tony kvstore] GPU payload plane unavailable, payloads over gloo: "
+              f"{'; '.join(f'rank {r}: {e}' for r, e in enumerate(errs) if e)}", file=sys.stderr, flush=True)
+        return None
+    return plane
 
 
 def run_scheduler(poll_s: float = 0.05) -> int:
