@@ -101,9 +101,10 @@ class _Block(nn.Module):
         # the fp32 blocks' fast form (concat slots, branch streams, joins); TONY_X3_BLOCKS=0: torch.cat graph
         self.x3_fast = x3 and X3_BLOCKS
 
-    def avgpool(self, x):
+    def avgpool(self, x, planes_only=False):
+        """``planes_only``: the x3 pool branch, read by its 1x1 conv only (ops/pool.avg_pool3x3_s1)."""
         if self.fused or self.x3:
-            return avg_pool3x3_s1(x)
+            return avg_pool3x3_s1(x, planes_only and self.x3 and X3_PLANES)
         return nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=True)
 
     def maxpool(self, x):
@@ -150,7 +151,7 @@ class InceptionA(_Block):
                 _join(x, 4)  # the three 1x1 convs and the pool branch's avg pool
             o3, o1, o5, op = streams.parallel(lambda: _seq(self.b3, x, s3), lambda: self.b1(x, slot=s1),
                                               lambda: _seq(self.b5, x, s5),
-                                              lambda: self.bp(self.avgpool(x), slot=sp))
+                                              lambda: self.bp(self.avgpool(x, planes_only=True), slot=sp))
             streams.keep(x)
             return assemble(buf, [o1, o5, o3, op])
         p = self.avgpool(x)
@@ -226,7 +227,7 @@ class InceptionC(_Block):  # 17x17 with factorised 7x7
                 _join(x, 4)  # the three 1x1 convs and the pool branch's avg pool
             od, o7, o1, op = streams.parallel(lambda: _seq(self.bd, x, sd), lambda: _seq(self.b7, x, s7),
                                               lambda: self.b1(x, slot=s1),
-                                              lambda: self.bp(self.avgpool(x), slot=sp))
+                                              lambda: self.bp(self.avgpool(x, planes_only=True), slot=sp))
             streams.keep(x)
             return assemble(buf, [o1, o7, od, op])
         p = self.avgpool(x)
@@ -328,7 +329,7 @@ class InceptionE(_Block):  # 8x8 with split 1x3 / 3x1 branches
 
             (oda, odb), (oa, ob), y1, yp = streams.parallel(
                 lambda: split(self.bd, self.bda, self.bdb, sda, sdb), lambda: split(self.b3, self.b3a, self.b3b, sa, sb),
-                lambda: self.b1(x, slot=s1), lambda: self.bp(self.avgpool(x), slot=sp))
+                lambda: self.b1(x, slot=s1), lambda: self.bp(self.avgpool(x, planes_only=True), slot=sp))
             streams.keep(x)
             return assemble(buf, [y1, oa, ob, oda, odb, yp])
         else:

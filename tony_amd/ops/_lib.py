@@ -152,9 +152,12 @@ _SIGNATURES = {
                           c_void_p, c_int, c_void_p],
     "tony_avgpool3_s1p1_f32": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
     "tony_avgpool3_s1p1_acc": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_int, c_void_p],
+    "tony_avgpool3_s1p1_x3": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_void_p],
     "tony_maxpool_fwd_f32": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
                          c_void_p],
     "tony_maxpool_bwd_f32": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
+                         c_void_p],
+    "tony_maxpool_bwd_acc_f32": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,
                          c_void_p],
     "tony_avgpool_fwd_f32": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
     "tony_avgpool_bwd_f32": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],

@@ -21,6 +21,41 @@ namespace {
 
 constexpr int kThreads = 256;
 
+// The 3x3/s1/p1 window sum / 9 of 8 channels at (n, h, w), group cg: all 9 taps loaded before the first
+// is summed (clamped to the image, so every address is valid; an out-of-image tap is then masked out):
+// the per-tap `continue` made each load wait on the last, which left the fp32 form (2 x 16 B per tap)
+// latency-bound at 104 us per 35x35 layer
+template <class T>
+__device__ __forceinline__ void box3_sum(const T* __restrict__ x, int64_t n, int h, int w, int H, int W, int64_t ldx,
+                                         uint32_t cg, float (&acc)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  V8<T> v[9];
+#pragma unroll
+  for (int dh = 0; dh < 3; ++dh) {
+    const int hh = min(max(h + dh - 1, 0), H - 1);
+#pragma unroll
+    for (int dw = 0; dw < 3; ++dw) {
+      const int ww = min(max(w + dw - 1, 0), W - 1);
+      v[dh * 3 + dw] = V8<T>::load(x + ((n * H + hh) * W + ww) * ldx + cg * 8);
+    }
+  }
+#pragma unroll
+  for (int dh = 0; dh < 3; ++dh) {
+#pragma unroll
+    for (int dw = 0; dw < 3; ++dw) {
+      const bool in = (static_cast<unsigned>(h + dh - 1) < static_cast<unsigned>(H)) &&
+                      (static_cast<unsigned>(w + dw - 1) < static_cast<unsigned>(W));
+      float f[8];
+      v[dh * 3 + dw].to_float(f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += in ? f[j] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] *= (1.f / 9.f);
+}
+
 // ACC: y += box3(x) / 9 (the avg pool's input gradient added into another consumer's, ops/residual.py
 // GradJoin: no separate add kernel over the block input)
 template <class T, bool ACC = false>
@@ -37,35 +72,8 @@ __global__ __launch_bounds__(kThreads) void box3_kernel(const T* __restrict__ x,
     const int w = static_cast<int>(site % W);
     const uint32_t nh = site / W;
     const int h = static_cast<int>(nh % H);
-    const int64_t n = nh / H;
-    // all 9 taps loaded before the first is summed (clamped to the image, so every address is valid;
-    // an out-of-image tap is then masked out): the per-tap `continue` made each load wait on the last,
-    // which left the fp32 form (2 x 16 B per tap) latency-bound at 104 us per 35x35 layer
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    V8<T> v[9];
-#pragma unroll
-    for (int dh = 0; dh < 3; ++dh) {
-      const int hh = min(max(h + dh - 1, 0), H - 1);
-#pragma unroll
-      for (int dw = 0; dw < 3; ++dw) {
-        const int ww = min(max(w + dw - 1, 0), W - 1);
-        v[dh * 3 + dw] = V8<T>::load(x + ((n * H + hh) * W + ww) * ldx + cg * 8);
-      }
-    }
-#pragma unroll
-    for (int dh = 0; dh < 3; ++dh) {
-#pragma unroll
-      for (int dw = 0; dw < 3; ++dw) {
-        const bool in = (static_cast<unsigned>(h + dh - 1) < static_cast<unsigned>(H)) &&
-                        (static_cast<unsigned>(w + dw - 1) < static_cast<unsigned>(W));
-        float f[8];
-        v[dh * 3 + dw].to_float(f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[j] += in ? f[j] : 0.f;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] *= (1.f / 9.f);
+    float acc[8];
+    box3_sum(x, nh / H, h, w, H, W, ldx, cg, acc);
     T* dst = y + static_cast<int64_t>(site) * ldy + cg * 8;
     if (ACC) {
       float o[8];
@@ -74,6 +82,34 @@ __global__ __launch_bounds__(kThreads) void box3_kernel(const T* __restrict__ x,
       for (int j = 0; j < 8; ++j) acc[j] += o[j];
     }
     V8<T>::from_float(acc).store(dst);
+  }
+}
+
+// fp32 avg pool straight to the x3 operand planes of its only consumer conv (ops/x3.py split_act layout:
+// [hi | lo | hi] over cp = C channels per row, hi = bf16(v), lo = bf16(v - hi)): the fp32 pooled map is
+// never stored or re-read by a split pass
+__global__ __launch_bounds__(kThreads) void box3_x3_kernel(const float* __restrict__ x, uint16_t* __restrict__ y3,
+                                                           int N, int H, int W, int C, int64_t ldx) {
+  const uint32_t CG = C >> 3;
+  const uint32_t total = static_cast<uint32_t>(N) * H * W * CG;
+  const uint32_t stride = gridDim.x * kThreads;
+  for (uint32_t t = blockIdx.x * kThreads + threadIdx.x; t < total; t += stride) {
+    const uint32_t cg = t % CG;
+    const uint32_t site = t / CG;
+    const int w = static_cast<int>(site % W);
+    const uint32_t nh = site / W;
+    const int h = static_cast<int>(nh % H);
+    float acc[8], lo[8];
+    box3_sum(x, nh / H, h, w, H, W, ldx, cg, acc);
+    const bf16x8 hi = bf16x8::from_float(acc);
+    float hf[8];
+    hi.to_float(hf);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lo[j] = acc[j] - hf[j];
+    uint16_t* d = y3 + static_cast<int64_t>(site) * (3 * C) + cg * 8;
+    store8(d, hi);
+    store8(d + C, bf16x8::from_float(lo));
+    store8(d + 2 * C, hi);
   }
 }
 
@@ -574,6 +610,18 @@ TONY_API int tony_avgpool3_s1p1_f32(const void* x, void* y, int N, int H, int W,
   return 0;
 }
 
+// fp32 x -> the x3 planes [N*H*W][3C] of box3x3(x) / 9 (C % 8 == 0)
+TONY_API int tony_avgpool3_s1p1_x3(const void* x, void* y3, int N, int H, int W, int C, int64_t ldx,
+                                   hipStream_t stream) {
+  if (C % 8 || ldx % 4 || (reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(y3) & 15) ||
+      static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff)
+    return -1;
+  box3_x3_kernel<<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+      static_cast<const float*>(x), static_cast<uint16_t*>(y3), N, H, W, C, ldx);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
 // y += box3x3(x) / 9 (fp32 / bf16 rows: ``f32``)
 TONY_API int tony_avgpool3_s1p1_acc(const void* x, void* y, int N, int H, int W, int C, int64_t ldx, int64_t ldy,
                                     int f32, hipStream_t stream) {
@@ -617,6 +665,25 @@ TONY_API int tony_maxpool_bwd_f32(const void* dy, const void* argmax, void* dx, 
     maxpool_bwd_kernel<float><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
         static_cast<const float*>(dy), static_cast<const uint8_t*>(argmax), static_cast<float*>(dx), N, H, W, C, OH,
         OW, K, S, P, lddy, lddx);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// tony_maxpool_bwd_f32 adding into dx (the x3 blocks' block-input gradient join, ops/pool.py)
+TONY_API int tony_maxpool_bwd_acc_f32(const void* dy, const void* argmax, void* dx, int N, int H, int W, int C, int K,
+                                  int S, int P, int64_t lddy, int64_t lddx, hipStream_t stream) {
+  if (C % 8 || lddy % 4 || lddx % 4 || P < 0 || 2 * P >= K + 1 || H + 2 * P < K || W + 2 * P < K || S < 1)
+    return -1;
+  if (static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff) return -1;
+  const int OH = (H + 2 * P - K) / S + 1, OW = (W + 2 * P - K) / S + 1;
+  if (K == 3 && S == 2)
+    maxpool_bwd_kst_kernel<3, 2, float><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+        static_cast<const float*>(dy), static_cast<const uint8_t*>(argmax), static_cast<float*>(dx), N, H, W, C, OH,
+        OW, P, lddy, lddx, 1);
+  else
+    maxpool_bwd_kernel<float><<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+        static_cast<const float*>(dy), static_cast<const uint8_t*>(argmax), static_cast<float*>(dx), N, H, W, C, OH,
+        OW, K, S, P, lddy, lddx, 1);
   TONY_LAUNCH_CHECK();
   return 0;
 }

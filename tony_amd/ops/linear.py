@@ -16,13 +16,17 @@ use it; the reference jobs' heads are the Keras/TF ``Dense`` layers of
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 
-from . import _lib, tape
+from . import _lib, tape, tune
 from .gemm import wgrad_tn
 
 _BF16 = torch.bfloat16
+# TONY_LINEAR_TUNE=0: the GEMM's built-in tile heuristic (A/B)
+TUNE = os.environ.get("TONY_LINEAR_TUNE", "1") != "0"
 
 
 def supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
@@ -51,7 +55,10 @@ class _LinearFn(torch.autograd.Function):
         n = w.shape[0]
         y = torch.empty((m, n), dtype=x.dtype, device=x.device)
         aff = _affine(bias, n, x.device)
-        rc = L.tony_gemm_bf16(x.data_ptr(), w.data_ptr(), y.data_ptr(), m, n, k, x.stride(0), k, n, 2,
+        # per-shape tile variant (ops/tune.py): the classifier's M = batch rows leave the default 128 x 192
+        # tiles at 6 workgroups for the whole K = 2048 reduction
+        vf = tune.gemm_flags(x, w, y, m, n, k, x.stride(0), False) if TUNE else 0
+        rc = L.tony_gemm_bf16(x.data_ptr(), w.data_ptr(), y.data_ptr(), m, n, k, x.stride(0), k, n, 2 | vf,
                               aff.data_ptr(), 0, _lib.stream_ptr(x.device))
         _lib.check(rc, "tony_gemm_bf16 (linear)")
         ctx.save_for_backward(x, w)
@@ -73,7 +80,8 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             wt = w.t().contiguous()  # [in][out]: the NT GEMM's B operand
             dx = torch.empty((m, k), dtype=x.dtype, device=dev)
-            rc = L.tony_gemm_bf16(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), m, k, n, dy.stride(0), n, k, 0, 0, 0,
+            vf = tune.gemm_flags(dy, wt, dx, m, k, n, dy.stride(0), False) if TUNE else 0
+            rc = L.tony_gemm_bf16(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), m, k, n, dy.stride(0), n, k, vf, 0, 0,
                                   st)
             _lib.check(rc, "tony_gemm_bf16 (linear dgrad)")
         if ctx.needs_input_grad[1]:

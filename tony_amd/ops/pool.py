@@ -4,7 +4,7 @@ from __future__ import annotations
 import torch
 
 from . import _lib, concat, streams, tape
-from .bn import _accum_ok, _as_rows, _rows_view
+from .bn import _as_rows, _rows_view
 
 
 def _nhwc_empty(n, c, h, w, like):
@@ -36,12 +36,24 @@ def _box3(src, n, c, h, w, ld_src):
     return out
 
 
+_LAST_PLANES = [None]
+
+
 class _AvgPool3Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, planes_only=False):
         x, (_, c, ld) = _as_rows(x)
         n, _, h, w = x.shape
         ctx.join = getattr(x, "_tony_join", None)  # ops/residual.py GradJoin: x has other consumers
+        if planes_only:
+            # fp32 x, read only by one x3 conv: the pooled map goes straight to its operand planes
+            # (ops/x3.py split_act layout), the fp32 map is never stored
+            y3 = torch.empty((n * h * w, 3 * c), dtype=torch.bfloat16, device=x.device)
+            rc = _lib.lib().tony_avgpool3_s1p1_x3(x.data_ptr(), y3.data_ptr(), n, h, w, c, ld,
+                                                  _lib.stream_ptr(x.device))
+            _lib.check(rc, "tony_avgpool3_s1p1_x3")
+            _LAST_PLANES[0] = y3.view(n, h, w, 3 * c).permute(0, 3, 1, 2)
+            return torch.empty_strided((n, c, h, w), (0, 0, 0, 0), dtype=x.dtype, device=x.device)  # shape only
         return _box3(x, n, c, h, w, ld)
 
     @staticmethod
@@ -63,7 +75,7 @@ class _AvgPool3Fn(torch.autograd.Function):
         if join is not None:
             dx = join.settle(dx)
         streams.keep(dx)  # may be consumed on another (branch) stream
-        return dx
+        return dx, None
 
 
 class _MaxPoolFn(torch.autograd.Function):
@@ -91,10 +103,10 @@ class _MaxPoolFn(torch.autograd.Function):
         dy, (_, _, lddy) = _as_rows(dy)
         join = ctx.join if ctx.needs_input_grad[0] else None
         pend = join.take() if join is not None else None
-        if pend is not None and dy.dtype == torch.bfloat16 and _accum_ok(pend, (n, c, h, w)):
+        if pend is not None and pend.dtype == dy.dtype and _dense_rows(pend, (n, c, h, w)):
             # another consumer of x already wrote its gradient: the pool's is added into it in-kernel
-            rc = _lib.lib().tony_maxpool_bwd_acc(dy.data_ptr(), arg.data_ptr(), pend.data_ptr(), n, h, w, c, k, s, p,
-                                                 lddy, c, _lib.stream_ptr(dy.device))
+            rc = _fn("tony_maxpool_bwd_acc", dy)(dy.data_ptr(), arg.data_ptr(), pend.data_ptr(), n, h, w, c, k, s, p,
+                                                  lddy, c, _lib.stream_ptr(dy.device))
             _lib.check(rc, "tony_maxpool_bwd_acc")
             dx = pend
         else:
@@ -148,10 +160,19 @@ def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
     return torch.flatten(torch.nn.functional.adaptive_avg_pool2d(x, 1), 1)
 
 
-def avg_pool3x3_s1(x: torch.Tensor) -> torch.Tensor:
-    """avg_pool2d(x, 3, 1, 1, count_include_pad=True) on channels_last bf16 / fp32."""
+def avg_pool3x3_s1(x: torch.Tensor, planes_only: bool = False) -> torch.Tensor:
+    """avg_pool2d(x, 3, 1, 1, count_include_pad=True) on channels_last bf16 / fp32.  ``planes_only`` (fp32
+    x): the output feeds one x3 conv only -- a shape-only tensor comes back whose operand planes
+    ops/x3.split_act finds cached on it (never read as fp32)."""
     if _ok(x):
-        return tape.apply(_AvgPool3Fn, x)
+        planes_only = planes_only and x.dtype == torch.float32 and not tape.recording()
+        _LAST_PLANES[0] = None
+        y = tape.apply(_AvgPool3Fn, x, planes_only)
+        planes = _LAST_PLANES[0]
+        if planes is not None:
+            _LAST_PLANES[0] = None
+            y._tony_x3 = (y._version, planes, x.shape[1])
+        return y
     return torch.nn.functional.avg_pool2d(x, 3, 1, 1, count_include_pad=True)
 
 
