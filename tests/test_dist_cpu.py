@@ -253,3 +253,34 @@ def test_bucket_engine_inplace_report_then_accumulate_hook():
     assert eng.launched_during_backward == 2
     torch.testing.assert_close(m.w1.grad, torch.full((64,), 2.0))
     eng.detach()
+
+
+def test_kvstore_plane_layout_agrees_between_server_and_workers(monkeypatch):
+    """The GPU payload plane's window layout (parallel/kvstore.py _KvLayout): a server that sees only its
+    own keys places them exactly where every worker (which sees all keys) expects them; a key too big for
+    the window stays on gloo for everybody; rows and landing slots are 16-B aligned and disjoint."""
+    from tony_amd.parallel.kvstore import _KvLayout, _Topology
+
+    monkeypatch.setenv("DMLC_NUM_SERVER", "2")
+    monkeypatch.setenv("DMLC_NUM_WORKER", "3")
+    topo = _Topology()
+    window = 4096
+    keys = [(0, 12), (1, 100), (2, 200), (3, 8), (4, 5000), (5, 40)]  # key 4 fits no window
+    worker = _KvLayout(topo, window)
+    fits = {k: worker.add_key(k, n) for k, n in keys}
+    assert fits == {0: True, 1: True, 2: True, 3: True, 4: False, 5: True}
+    for s in range(2):
+        server = _KvLayout(topo, window)
+        for k, n in keys:
+            if topo.server_of(k) == s:
+                assert server.add_key(k, n) == fits[k]
+                if fits[k]:
+                    assert server.keys[k] == worker.keys[k]
+    spans = {}
+    for k, (s, n, row, land) in worker.keys.items():
+        assert row % 16 == 0 and land % 16 == 0 and land // worker.region == s
+        spans.setdefault(("row", s), []).append((row, row + 3 * ((n + 15) // 16 * 16)))
+        spans.setdefault(("land",), []).append((land, land + n))
+    for v in spans.values():
+        v.sort()
+        assert all(a[1] <= b[0] for a, b in zip(v, v[1:]))

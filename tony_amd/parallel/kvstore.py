@@ -270,11 +270,32 @@ def _plane_wanted() -> bool:
     return torch.cuda.is_available()
 
 
+class _KvLayout:
+    """Where each key's bytes live in the plane windows, computed identically by a server and every worker
+    from the keys in init order (a server sees only its own keys, which is all its part depends on):
+    server s's window holds, per key it owns, one receive row per worker; a worker's window is split in one
+    landing region per server, each holding that server's keys back to back."""
+
+    def __init__(self, topo: "_Topology", window_bytes: int):
+        self.topo, self.bytes = topo, window_bytes
+        self.region = window_bytes // max(1, topo.num_servers) // 16 * 16  # a worker's landing region per server
+        self.row_used = [0] * topo.num_servers
+        self.land_used = [0] * topo.num_servers
+        self.keys: Dict[int, tuple] = {}  # kid -> (server, nbytes, row_off, land_off)
+
+    def add_key(self, kid: int, nbytes: int) -> bool:
+        s = self.topo.server_of(kid)
+        rows = self.topo.num_workers * _pad16(nbytes)
+        if self.row_used[s] + rows > self.bytes or self.land_used[s] + _pad16(nbytes) > self.region:
+            return False  # stays on the gloo payload path (decided identically on every member)
+        self.keys[kid] = (s, nbytes, self.row_used[s], s * self.region + self.land_used[s])
+        self.row_used[s] += rows
+        self.land_used[s] += _pad16(nbytes)
+        return True
+
+
 class _KvPlane:
-    """The GPU payload windows of one server / worker (module docstring).  Layout, computed identically
-    by a server and every worker from the keys in init order: server s's window holds, per key it owns,
-    one receive row per worker; a worker's window is split in one landing region per server, each holding
-    that server's keys back to back."""
+    """The GPU payload windows of one server / worker (module docstring), laid out by _KvLayout."""
 
     def __init__(self, topo: "_Topology", device: torch.device):
         import ctypes
@@ -305,20 +326,11 @@ class _KvPlane:
                 _lib.check(self.L.tony_xgmi_open(buf, ctypes.byref(p)), f"tony_xgmi_open(rank {r})")
             self.peer[r] = p.value + hdr
             self._opened.append(p.value)
-        self.region = self.bytes // max(1, topo.num_servers) // 16 * 16  # a worker's landing region per server
-        self.row_used = [0] * topo.num_servers
-        self.land_used = [0] * topo.num_servers
-        self.keys: Dict[int, tuple] = {}  # kid -> (server, nbytes, row_off, land_off)
+        self.layout = _KvLayout(topo, self.bytes)
+        self.keys = self.layout.keys
 
     def add_key(self, kid: int, nbytes: int) -> bool:
-        s = self.topo.server_of(kid)
-        rows = self.topo.num_workers * _pad16(nbytes)
-        if self.row_used[s] + rows > self.bytes or self.land_used[s] + _pad16(nbytes) > self.region:
-            return False  # stays on the gloo payload path (decided identically on every member)
-        self.keys[kid] = (s, nbytes, self.row_used[s], s * self.region + self.land_used[s])
-        self.row_used[s] += rows
-        self.land_used[s] += _pad16(nbytes)
-        return True
+        return self.layout.add_key(kid, nbytes)
 
     def copy(self, dst: int, src: int, nbytes: int) -> None:
         from ..ops import _lib
