@@ -140,3 +140,29 @@ def test_trainer_plan_matches_eager_and_graph(cuda, kind, monkeypatch):
             assert abs(a - b) <= 2e-2 * max(1.0, abs(b)), (lv, ref)
     assert (pp - pe).abs().max().item() < 2e-2
     assert (pp - pg).abs().max().item() < 2e-2
+
+
+def test_plan_replays_captured_copies(cuda):
+    """D2D copies captured from copy_ (hipMemcpyAsync memcpy nodes, e.g. the fp32 step's) are re-issued
+    by the plan -- round 4 found hipMemcpy3DAsync rejecting the 1-row form HIP reports for them."""
+    from tony_amd.ops.plan import StepPlan
+
+    dev = torch.device("cuda", 0)
+    x = torch.randn(1 << 18, device=dev)
+    buf = torch.empty(1 << 19, device=dev)
+
+    def body():
+        y = x * 2.0
+        buf[1 << 18:].copy_(y)  # a D2D memcpy node at an offset
+        z = buf[1 << 18:] + 1.0
+        return z.clone()  # another memcpy node
+
+    g, out = _capture(body)
+    plan = StepPlan(g, [torch.cuda.current_stream(), *_streams(2)])
+    assert plan.stats["node_graphs"] >= 2, plan.stats  # the copies replay as one-node graphs
+    for trial in range(3):
+        x.copy_(torch.randn_like(x))
+        plan.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, x * 2.0 + 1.0), trial
+    plan.close()

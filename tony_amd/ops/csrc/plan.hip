@@ -24,6 +24,7 @@
 // issues the ops up to that marker and forks the marker's stream into the caller's side stream.
 #include <algorithm>
 #include <array>
+#include <cstdlib>
 #include <cstring>
 #include <unordered_map>
 #include <vector>
@@ -348,8 +349,18 @@ TONY_API int tony_plan_build(void* graph, const uint64_t* streams, int nstreams,
     } else {
       // copies: a fully described 3D copy is re-issued directly, anything else (1D copies captured
       // from hipMemcpyAsync carry no readable parameters) as a one-node executable graph
+      // Every copy goes through the one-node graph by default: re-issuing the getter's parameters with
+      // hipMemcpy3DAsync failed (hipErrorInvalidValue) on some captured linear copies -- the fp32 step's
+      // D2D copies, round 3's captured collective -- and a hipMemcpyAsync of the same extent failed on
+      // others; HIP's own instantiation of the node replays each faithfully (a few copies per step).
+      // TONY_PLAN_DIRECT_COPY=1 restores the direct re-issue (A/B).
+      static const bool allow_direct = [] {
+        const char* e = std::getenv("TONY_PLAN_DIRECT_COPY");
+        return e != nullptr && e[0] == '1';
+      }();
       bool direct = false;
-      if (type[v] == hipGraphNodeTypeMemcpy && hipGraphMemcpyNodeGetParams(nodes[v], &o.mc) == hipSuccess) {
+      if (allow_direct && type[v] == hipGraphNodeTypeMemcpy &&
+          hipGraphMemcpyNodeGetParams(nodes[v], &o.mc) == hipSuccess) {
         const hipMemcpy3DParms& m = o.mc;
         const bool src_ok = m.srcArray != nullptr || m.srcPtr.ptr != nullptr;
         const bool dst_ok = m.dstArray != nullptr || m.dstPtr.ptr != nullptr;
