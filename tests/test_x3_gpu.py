@@ -92,6 +92,31 @@ def test_conv_bn_relu_x3_matches_float64(cuda, shape):
     assert _rel(layer.bn.running_mean, 0.9 * 0 + 0.1 * z.detach().mean((0, 2, 3))) < 1e-4
 
 
+@pytest.mark.parametrize("shape", [(2, 32, 19, 19, 32, (3, 3), 1, 0), (2, 32, 17, 17, 64, (3, 3), 1, 1),
+                                   (2, 32, 21, 21, 32, (3, 3), 1, 1)], ids=lambda s: f"{s[1]}x{s[2]}-{s[4]}-p{s[7]}")
+def test_x3_direct_kernel_forward_and_dgrad_match_float64(cuda, shape, monkeypatch):
+    """The direct 3x3 kernel on the x3 planes of a 32-channel input (fp32 output, csrc/conv.hip
+    conv_direct_kernel F32), pinned for the forward and the backward-data pass wherever it takes the
+    shape (the autotuner would pick it on the 147x147 stem layers): the layer test's float64 bounds."""
+    from tony_amd.ops import tune
+
+    orig = tune.pick
+    forced = []
+
+    def pick_direct(key, launch, variants=tune.NT_VARIANTS):
+        if 10 in variants and launch(10 << 8) == 0:
+            forced.append(key[0])
+            return 10 << 8
+        return orig(key, launch, variants)
+
+    monkeypatch.setattr(tune, "_CACHE", {})
+    monkeypatch.setattr(tune, "pick", pick_direct)
+    test_conv_bn_relu_x3_matches_float64(cuda, shape)
+    assert "x3_fwd" in forced, forced  # the forward ran on the direct kernel
+    if shape[4] == 32:
+        assert "x3_dgrad" in forced, forced  # dX of a 32 -> 32 conv: 3 x 32 dY planes in, 32 channels out
+
+
 def test_linear_x3_matches_float64(cuda):
     from tony_amd.ops.x3 import LinearX3
 

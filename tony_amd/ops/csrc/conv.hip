@@ -534,7 +534,8 @@ struct DirectCfg {
   static constexpr size_t kLds = static_cast<size_t>(HALO + WTS) * sizeof(uint16_t) + CO * 4 * sizeof(float);
 };
 
-template <int CS, int CO, int TW>
+// F32: fp32 output (the x3 fp32 step, ops/x3.py: CS = 3 planes x 32 channels) -- 16 B per lane and channel block
+template <int CS, int CO, int TW, bool F32 = false>
 __global__ __launch_bounds__(kThreads) void conv_direct_kernel(Gather g, const uint16_t* __restrict__ B,
                                                               uint16_t* __restrict__ C, int64_t ldc,
                                                               float* __restrict__ stats, int64_t sstride,
@@ -658,20 +659,25 @@ __global__ __launch_bounds__(kThreads) void conv_direct_kernel(Gather g, const u
       const int p = wave * D::WPX + b * 16 + (lane & 15);
       const int oy = oy0 + p / TW, ox = ox0 + p % TW;
       if (oy >= g.OH || ox >= g.OW) continue;
-      uint16_t* dst = C + ((static_cast<int64_t>(n) * g.OH + oy) * g.OW + ox) * ldc + kq * 4;
+      const int64_t pix = (static_cast<int64_t>(n) * g.OH + oy) * g.OW + ox;
+      uint16_t* dst = C + pix * ldc + kq * 4;
 #pragma unroll
       for (int c = 0; c < D::CB; ++c) {
         const f32x4 a = acc[b][c];
-        *reinterpret_cast<uint2*>(dst + c * 16) =
-            make_uint2(static_cast<uint32_t>(f2bf(a[0])) | (static_cast<uint32_t>(f2bf(a[1])) << 16),
-                       static_cast<uint32_t>(f2bf(a[2])) | (static_cast<uint32_t>(f2bf(a[3])) << 16));
+        if constexpr (F32)
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + pix * ldc + c * 16 + kq * 4) =
+              make_float4(a[0], a[1], a[2], a[3]);
+        else
+          *reinterpret_cast<uint2*>(dst + c * 16) =
+              make_uint2(static_cast<uint32_t>(f2bf(a[0])) | (static_cast<uint32_t>(f2bf(a[1])) << 16),
+                         static_cast<uint32_t>(f2bf(a[2])) | (static_cast<uint32_t>(f2bf(a[3])) << 16));
         if (stats != nullptr) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             ssum[c][r] += a[r];
             ssq[c][r] = fmaf(a[r], a[r], ssq[c][r]);
           }
-        } else if (bnr.z != nullptr) {  // dY' and dY' * xhat of the bf16 values just stored
+        } else if (!F32 && bnr.z != nullptr) {  // dY' and dY' * xhat of the bf16 values just stored
           const uint2 zr = *reinterpret_cast<const uint2*>(
               bnr.z + ((static_cast<int64_t>(n) * g.OH + oy) * g.OW + ox) * bnr.ldz + c * 16 + kq * 4);
           const float zf[4] = {__uint_as_float(zr.x << 16), __uint_as_float(zr.x & 0xffff0000u),
@@ -687,7 +693,7 @@ __global__ __launch_bounds__(kThreads) void conv_direct_kernel(Gather g, const u
       }
     }
   }
-  if (stats == nullptr && bnr.z == nullptr) return;
+  if (stats == nullptr && (F32 || bnr.z == nullptr)) return;
   if (stats == nullptr) {  // BN-backward reduction: [dsum | dsumx] of this workgroup's pixels
     stats = bnr.dsum;
     sstride = bnr.sstride;
@@ -713,13 +719,16 @@ __global__ __launch_bounds__(kThreads) void conv_direct_kernel(Gather g, const u
 // The direct kernel for this shape, or -3 when it does not apply.
 int run_direct(const Gather& g, const void* B, void* C, int64_t ldc, int64_t N, int epi, float* st, int64_t sstride,
                hipStream_t stream, const BnRed& bnr = BnRed{}) {
-  if (g.R != 3 || g.S != 3 || g.sh != 1 || g.sw != 1 || (epi & 6) || (ldc % 4) || g.halo_images <= 0 ||
-      (reinterpret_cast<uintptr_t>(C) & 7) || (reinterpret_cast<uintptr_t>(B) & 15))
+  const bool f32 = (epi & 8) != 0;
+  if (g.R != 3 || g.S != 3 || g.sh != 1 || g.sw != 1 || (epi & 22) || (ldc % 4) || g.halo_images <= 0 ||
+      (reinterpret_cast<uintptr_t>(C) & (f32 ? 15 : 7)) || (reinterpret_cast<uintptr_t>(B) & 15) ||
+      (f32 && bnr.z != nullptr))
     return -3;
-  const auto launch = [&](auto cs, auto co, auto tw) -> int {
+  const auto launch = [&](auto cs, auto co, auto tw, auto f32c) -> int {
     constexpr int CS = decltype(cs)::value, CO = decltype(co)::value, TW = decltype(tw)::value;
+    constexpr bool F32 = decltype(f32c)::value;
     using D = DirectCfg<CS, CO, TW>;
-    const void* fn = reinterpret_cast<const void*>(&conv_direct_kernel<CS, CO, TW>);
+    const void* fn = reinterpret_cast<const void*>(&conv_direct_kernel<CS, CO, TW, F32>);
     static int per_cu = 0;  // per template instance: resident workgroups per CU (occupancy query)
     if (per_cu == 0) {
       if (D::kLds > 65536 &&
@@ -737,7 +746,7 @@ int run_direct(const Gather& g, const void* B, void* C, int64_t ldc, int64_t N, 
     const int64_t ntiles = static_cast<int64_t>(g.halo_images) * tiles_x * tiles_y;
     if (ntiles > 0x7fffffff) return -2;
     const int grid = static_cast<int>(std::min<int64_t>(ntiles, static_cast<int64_t>(per_cu) * cus));
-    conv_direct_kernel<CS, CO, TW><<<grid, kThreads, D::kLds, stream>>>(
+    conv_direct_kernel<CS, CO, TW, F32><<<grid, kThreads, D::kLds, stream>>>(
         g, static_cast<const uint16_t*>(B), static_cast<uint16_t*>(C), ldc, st, sstride, tiles_x, tiles_y,
         static_cast<int>(ntiles), bnr);
     TONY_LAUNCH_CHECK();
@@ -745,11 +754,18 @@ int run_direct(const Gather& g, const void* B, void* C, int64_t ldc, int64_t N, 
   };
   using I = std::integral_constant<int, 32>;
   using I64 = std::integral_constant<int, 64>;
+  using I96 = std::integral_constant<int, 96>;
   using I16 = std::integral_constant<int, 16>;
-  if (g.Cs == 32 && N == 32) return launch(I{}, I{}, I{});
-  if (g.Cs == 32 && N == 64) return launch(I{}, I64{}, I16{});  // 8 x 32 tiles: 258 VGPRs, 1 wave/SIMD
-  if (g.Cs == 64 && N == 32) return launch(I64{}, I{}, I16{});
-  if (g.Cs == 64 && N == 64) return launch(I64{}, I64{}, I16{});
+  using BF = std::false_type;
+  if (f32) {  // the x3 planes of a 32-channel input (weights [CO][9][3 x 32] + halo in LDS: 130 / 150 KB)
+    if (g.Cs == 96 && N == 32) return launch(I96{}, I{}, I{}, std::true_type{});
+    if (g.Cs == 96 && N == 64) return launch(I96{}, I64{}, I16{}, std::true_type{});
+    return -3;
+  }
+  if (g.Cs == 32 && N == 32) return launch(I{}, I{}, I{}, BF{});
+  if (g.Cs == 32 && N == 64) return launch(I{}, I64{}, I16{}, BF{});  // 8 x 32 tiles: 258 VGPRs, 1 wave/SIMD
+  if (g.Cs == 64 && N == 32) return launch(I64{}, I{}, I16{}, BF{});
+  if (g.Cs == 64 && N == 64) return launch(I64{}, I64{}, I16{}, BF{});
   return -3;
 }
 
@@ -765,7 +781,7 @@ int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int6
   if ((epi & 16) && ((epi & 3) || bph.bnr.z != nullptr)) return -1;
   float* st = stats;
   const int v = (flags >> 8) & 0xff;
-  if ((epi & 24) && (v == kHaloVariant || v == kDirectVariant)) return -3;
+  if (((epi & 24) && v == kHaloVariant) || ((epi & 16) && v == kDirectVariant)) return -3;
   if (v == kHaloVariant) return bph.bnr.z != nullptr ? -3 : run_halo(g, B, C, ldc, N, epi, st, sstride, stream);
   if (v == kDirectVariant) return run_direct(g, B, C, ldc, N, epi, st, sstride, stream, bph.bnr);
   if (v >= kGldsFirst && v < kGldsFirst + kNumGlds)

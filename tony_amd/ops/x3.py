@@ -162,7 +162,7 @@ def conv_dgrad(d3: torch.Tensor, wt3: torch.Tensor, co: int, x_shape, wshape, st
                                          ph, pw, out.data_ptr(), h, w, c, flags | vf, None, st)
     name = "tony_conv_dgrad (x3)" if (sh, sw) == (1, 1) else "tony_conv_dgrad_strided (x3)"
     key = ("x3_dgrad", tuple(d3.shape), tuple(x_shape), tuple(wshape), (sh, sw), (ph, pw))
-    variants = tuple(v for v in tune.NT_VARIANTS if v not in (9, 10))  # fp32 epilogue: NT / LDS-DMA kernels
+    variants = tuple(v for v in tune.NT_VARIANTS if v != 9)  # fp32 epilogue: NT / LDS-DMA / direct kernels
     from .conv import STRIDED_GLDS
 
     if (sh, sw) != (1, 1) and not STRIDED_GLDS:
@@ -171,7 +171,12 @@ def conv_dgrad(d3: torch.Tensor, wt3: torch.Tensor, co: int, x_shape, wshape, st
     if vf is None:  # timed into a scratch output: an accumulating call must add exactly once
         scratch = _cl(n, c, h, w, d3.device) if acc else dx
         vf = tune.pick(key, lambda v: launch(v, scratch), variants)
-    _lib.check(launch(vf, dx, 8 | acc), name)
+    rc = launch(vf, dx, 8 | acc)
+    if rc == -3 and acc:  # the chosen variant has no accumulating store (the direct kernel): add after
+        dx = _cl(n, c, h, w, d3.device)
+        rc = launch(vf, dx, 8)
+        acc = 0
+    _lib.check(rc, name)
     if accum is not None and not acc:
         return accum.add_(dx)
     return dx
