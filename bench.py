@@ -313,7 +313,9 @@ def main():
         # ties go to the plan: its host issue cost is ~2.5 ms/step against eager's ~11-13 ms, so a host
         # slowed by other work on the machine cannot stall the GPU (an eager run timed at 15.3 ms/step
         # after its setup measured 13.4, profiles/r4_bench_host_bound_eager.log)
-        mode = "graph" if setup["graph_ms"] <= setup["eager_ms"] * PLAN_TIE else "eager"
+        # (one rank only: with several, a replay's bucket collectives interleave with its segments, and the
+        # plan has to win outright)
+        mode = "graph" if setup["graph_ms"] <= setup["eager_ms"] * (PLAN_TIE if world == 1 else 1.0) else "eager"
         trainer.use_graph = mode == "graph" and ps.is_worker
         if rank == 0:
             print(f"[bench] setup {time.perf_counter() - t_w:.1f}s: {setup} -> {mode}", file=sys.stderr, flush=True)
