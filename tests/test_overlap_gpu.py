@@ -92,12 +92,21 @@ def test_two_ranks_overlap_ps_and_ddp(cuda, kind, collective, monkeypatch):
     assert torch.equal(d0["grad"], d1["grad"])                    # averaged gradients identical on both ranks
     assert d0["grad"].abs().sum().item() > 0
     # ... and equal to the mean of the gradients each rank computes alone (a rank counted twice or
-    # dropped, or a missing / double 1/world scale, moves every parameter's gradient by >= 30 %)
+    # dropped, or a missing / double 1/world scale, moves every parameter's gradient by >= 30 %).  The
+    # local gradients come from a second backward whose BN statistics are fp32 atomics: a bf16
+    # pre-activation that rounds to the other side of its ReLU moves one small conv's weight gradient by
+    # a few % (measured 4.1 % once), so per tensor < 0.1 and the whole gradient's cosine > 0.999
+    ga, gw = [], []
     for name, g in d0["named"].items():
         g = torch.from_numpy(g)
         want = sum(torch.from_numpy(out[r]["ddp"]["local"][name]) for r in range(world)) / world
         err = (g - want).norm().item() / max(want.norm().item(), 1e-12)
-        assert err < 3e-2, (name, err)
+        assert err < 0.1, (name, err)
+        ga.append(g.double().flatten())
+        gw.append(want.double().flatten())
+    ga, gw = torch.cat(ga), torch.cat(gw)
+    assert (ga @ gw / (ga.norm() * gw.norm())).item() > 0.999
+    assert abs(ga.norm().item() / gw.norm().item() - 1) < 0.02  # the scale: 1/world applied exactly once
     if collective == "hip":  # every bucket push / pull / all-reduce ran on the xGMI kernels
         for r in range(world):
             for name in ("ps_overlap", "ps_plan", "ps_serial", "ddp"):
