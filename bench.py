@@ -238,11 +238,6 @@ def main():
         res, aux_w = 224, 0.0
     model = model.to(dev).to(memory_format=torch.channels_last)
     model.train()
-    if os.environ.get("TONY_COMPUTE_PRIORITY"):
-        # the step's compute stream at a HIP stream priority (-1: high, above the weight-gradient stream)
-        cs = torch.cuda.Stream(device=dev, priority=int(os.environ["TONY_COMPUTE_PRIORITY"]))
-        cs.wait_stream(torch.cuda.current_stream(dev))
-        torch.cuda.set_stream(cs)
     ps_kw = {} if args.bucket_mb is None else {"bucket_mb": args.bucket_mb}
     if os.environ.get("TONY_BUCKETED_SINGLE", "0") == "1":
         # one rank: the bucket engine applies each bucket as soon as backward has written it (the

@@ -42,17 +42,11 @@ _keep: List[torch.Tensor] = []
 _issued = [0]
 
 
-# HIP stream priorities (lower = higher; HIP has low 1 / normal 0 / high -1): the weight-gradient stream
-# carries no critical-path work, the branch streams do (a block's backward waits for its slowest branch)
-SIDE_PRIORITY = int(os.environ.get("TONY_WGRAD_PRIORITY", "0"))
-BRANCH_PRIORITY = int(os.environ.get("TONY_BRANCH_PRIORITY", "0"))
-
-
 def _side(device: torch.device) -> torch.cuda.Stream:
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _streams.get(idx)
     if s is None:
-        s = torch.cuda.Stream(device=torch.device("cuda", idx), priority=SIDE_PRIORITY)
+        s = torch.cuda.Stream(device=torch.device("cuda", idx))
         _streams[idx] = s
     return s
 
@@ -76,7 +70,7 @@ def _branch_streams(device: torch.device, n: int) -> List[torch.cuda.Stream]:
     idx = device.index if device.index is not None else torch.cuda.current_device()
     pool = _branch_pool.setdefault(idx, [])
     while len(pool) < n:
-        pool.append(torch.cuda.Stream(device=torch.device("cuda", idx), priority=BRANCH_PRIORITY))
+        pool.append(torch.cuda.Stream(device=torch.device("cuda", idx)))
     return pool[:n]
 
 
