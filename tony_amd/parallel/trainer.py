@@ -36,6 +36,8 @@ GC_EVERY = int(os.environ.get("TONY_GC_EVERY", "200"))
 # from C++ onto the eager step's streams (ops/plan.py, csrc/plan.hip); "graph" instantiates it and
 # calls hipGraphLaunch.  A graph the native replay cannot issue falls back to "graph".
 REPLAY = os.environ.get("TONY_REPLAY", "plan").lower()
+# weight-gradient ops per side-stream fork inside a captured step (eager issue uses streams.BATCH)
+PLAN_WGRAD_BATCH = int(os.environ.get("TONY_PLAN_WGRAD_BATCH", "1"))
 
 # Opt-in: measured slower on MI355X (bench 16.9 vs 15.7 ms/step; the compute queue's gaps grew from
 # 3.3 to 5.9 ms under rocprofv3), so the step stays on the caller's stream by default.
@@ -273,13 +275,20 @@ class Trainer:
                 eng.end_capture()
             return out
 
-        with torch.cuda.graph(g):
-            if self.arena is not None:
-                with self.arena:  # its one fill is a node of the graph; the slices keep their addresses
+        # weight gradients join the side stream one op per fork inside the capture: eager issue batches
+        # them in pairs to save host time (streams.BATCH), which a replay does not pay, and each op then
+        # waits only for its own dZ (plan 13.61 vs 13.68 ms/step, profiles/r4_ab_plan_wgrad_batch.log)
+        batch, streams.BATCH = streams.BATCH, PLAN_WGRAD_BATCH
+        try:
+            with torch.cuda.graph(g):
+                if self.arena is not None:
+                    with self.arena:  # its one fill is a node of the graph; the slices keep their addresses
+                        loss = body()
+                else:
                     loss = body()
-            else:
-                loss = body()
-            self.static_loss = loss.detach()
+                self.static_loss = loss.detach()
+        finally:
+            streams.BATCH = batch
         if inside:
             self.ps.steps -= 1  # the capture itself did not train
             for opt in self.ps.optimizers.values():
