@@ -30,7 +30,9 @@ Data is synthetic (ImageNet-shaped 299x299x3 images, random labels) and weights 
 no network access for datasets / checkpoints.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--ps-mode M] [--dtype D]
-       (N>1 is launched by the driver via torch.distributed.run)
+       N>1 under torch.distributed.run (WORLD_SIZE set): one rank per GPU, as the driver launches it;
+       N>1 without it: bench.py starts ``python -m torch.distributed.run --nproc-per-node N bench.py ...``
+       as a child process (never an exec), relays rank 0's JSON line and exits with the child's code.
 """
 from __future__ import annotations
 
@@ -44,7 +46,7 @@ import torch
 import torch.distributed as dist
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
@@ -86,7 +88,9 @@ def parse():
     ap.add_argument("--fp32-warmup", type=int, default=3)
     ap.add_argument("--no-miopen-find", action="store_true",
                     help="MIOpen immediate mode instead of find (faster startup, slower non-1x1 convs)")
-    return ap.parse_args()
+    ap.add_argument("--launch-dry-run", action="store_true",
+                    help="N>1 without torch.distributed.run: print the self-launch argv / env as JSON and exit")
+    return ap.parse_args(argv)
 
 
 def fail(msg: str, code: int = 4) -> int:
@@ -186,8 +190,64 @@ def _heartbeat(t0: float, every_s: float = 45.0) -> None:
     threading.Thread(target=beat, name="bench-heartbeat", daemon=True).start()
 
 
-def main():
-    args = parse()
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch_cmd(argv, n: int, port: int):
+    """argv / env of the child that runs ``bench.py --gpus N`` as N ranks, one per GPU (the driver's
+    own form: torch.distributed.run, 127.0.0.1 rendezvous)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)]
+    cmd += [a for a in argv if a != "--launch-dry-run"]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC: RCCL / tensor sharing across ranks
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return cmd, env
+
+
+def self_launch(args, argv) -> int:
+    """``python bench.py --gpus N`` (N > 1) with no torch.distributed.run around it.  Runs before
+    anything touches the GPU in this process, and starts the launcher as a CHILD (an exec from a
+    process that initialised the GPU is forbidden on the pool): the ranks inherit stdout, so rank 0's
+    JSON line is the one this command prints; the exit code is the launcher's."""
+    import signal
+    import subprocess
+
+    cmd, env = self_launch_cmd(argv, args.gpus, _free_port())
+    if args.launch_dry_run:
+        print(json.dumps({"self_launch": cmd, "env": {k: env[k] for k in ("HSA_ENABLE_IPC_MODE_LEGACY",)}}))
+        return 0
+    n_dev = torch.cuda.device_count()  # counts devices without initialising HIP in this process
+    if n_dev < args.gpus and "TONY_BENCH_DEVICE" not in os.environ:  # (rehearsal: ranks share one GPU)
+        return fail(f"--gpus {args.gpus} but this node shows {n_dev} GPU(s)", 2)
+    print(f"[bench] self-launch: {' '.join(cmd[1:6])} ...", file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, env=env, start_new_session=True)
+
+    def forward(sig, _frame):  # the driver's timeout / ^C reaches every rank
+        try:
+            os.killpg(p.pid, sig)
+        except ProcessLookupError:
+            pass
+
+    old = {s: signal.signal(s, forward) for s in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        return p.wait()
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(args, argv)
     if args.collective:
         os.environ["TONY_COLLECTIVE"] = args.collective
     if int(os.environ.get("RANK", "0")) == 0:

@@ -6,6 +6,8 @@ import traceback
 import torch
 import torch.distributed as dist
 
+import gpu_ranks
+
 
 def _model(kind, dev):
     from torch import nn
@@ -38,7 +40,7 @@ def ps_run(rank, kind, overlap, bucket_mb, steps=3, graph=False):
     from tony_amd.parallel.ps import ParameterServer
     from tony_amd.parallel.trainer import Trainer
 
-    dev = torch.device("cuda", 0)
+    dev = torch.device("cuda", torch.cuda.current_device())
     model = _model(kind, dev)
     ps = ParameterServer(model, optimizer="sgd", lr=0.05, momentum=0.9, device=dev, bucket_mb=bucket_mb,
                          bucketed_single=True)
@@ -63,7 +65,7 @@ def ddp_run(rank, kind, bucket_mb):
     from tony_amd.ops import cross_entropy
     from tony_amd.parallel.ddp import DistributedDataParallel
 
-    dev = torch.device("cuda", 0)
+    dev = torch.device("cuda", torch.cuda.current_device())
     x, y = _data(rank, kind, dev)
     # this rank's own gradient without DDP (same init, same fused kernels): the parent checks DDP's
     # averaged gradient against the mean of these over ranks -- not only that the ranks agree
@@ -97,8 +99,7 @@ def run(rank, world, port, q, kind, bucket_mb):
     faulthandler.enable(file=trace, all_threads=True)
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-        torch.cuda.set_device(0)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        gpu_ranks.init(rank, world)
         out = {}
         for name, fn in (("ps_overlap", lambda: ps_run(rank, kind, True, bucket_mb)),
                          ("ps_plan", lambda: ps_run(rank, kind, True, bucket_mb, graph=True)),

@@ -5,6 +5,8 @@ import os
 import torch
 import torch.distributed as dist
 
+import gpu_ranks
+
 
 class _Net(torch.nn.Module):
     """Parameters only (the push / apply / land protocol does not care where gradients come from)."""
@@ -32,9 +34,7 @@ def _master_flat(ps):
 def run(rank, world, port, q, sync=True, wire=None, steps=4):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     try:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        torch.cuda.set_device(0)
-        dev = torch.device("cuda", 0)
+        dev, _ = gpu_ranks.init(rank, world)
         from tony_amd.parallel.ps import ParameterServer
 
         torch.manual_seed(0)
@@ -105,9 +105,7 @@ def run_overlap(rank, world, port, q):
     order of a sync PS (loss finite, parameters changed)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     try:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        torch.cuda.set_device(0)
-        dev = torch.device("cuda", 0)
+        dev, _ = gpu_ranks.init(rank, world)
         from tony_amd.models.layers import ConvBNAct, cast_model, init_weights
         from tony_amd.ops import cross_entropy
         from tony_amd.ops.pool import global_avg_pool

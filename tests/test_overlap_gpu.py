@@ -13,6 +13,8 @@ import multiprocessing as mp
 import socket
 
 import pytest
+
+from gpu_ranks import placement
 import torch
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(240)]
@@ -42,7 +44,7 @@ def test_ps_overlap_one_rank_matches_serial(cuda, kind):
     assert log.index("launch:0") < max(i for i, e in enumerate(log) if e.startswith("ready:"))
 
 
-@pytest.mark.parametrize("kind,collective", [("A", "rccl"), ("A", "hip")], ids=["gloo", "xgmi-kernels"])
+@pytest.mark.parametrize("kind,collective", [("A", "rccl"), ("A", "hip")], ids=[f"process-group-{placement(2)}", f"xgmi-kernels-{placement(2)}"])
 def test_two_ranks_overlap_ps_and_ddp(cuda, kind, collective, monkeypatch):
     """collective=hip: the colocated PS push / pull and DDP's bucket all-reduce run on the xGMI
     peer-memory kernels (TONY_COLLECTIVE=hip routes every data plane through parallel/collectives.py;

@@ -12,6 +12,8 @@ import socket
 
 import pytest
 
+from gpu_ranks import placement
+
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(240)]
 
 
@@ -43,7 +45,7 @@ def _spawn(target, world, *args):
 
 
 @pytest.mark.parametrize("world,sync,wire", [(3, True, None), (4, True, "fp32"), (3, False, None)],
-                         ids=["sync-2w-bf16", "sync-3w-fp32wire", "async-2w"])
+                         ids=[f"sync-2w-bf16-{placement(3)}", f"sync-3w-fp32wire-{placement(4)}", f"async-2w-{placement(3)}"])
 def test_ps_plane_push_apply_land(world, sync, wire, monkeypatch):
     import torch
 
@@ -57,7 +59,8 @@ def test_ps_plane_push_apply_land(world, sync, wire, monkeypatch):
     assert out[0]["pushed"] == 0 and all(out[r]["pushed"] > 0 for r in range(1, world))
 
 
-def test_ps_plane_trainer_overlap(monkeypatch):
+@pytest.mark.parametrize("where", [placement(3)])
+def test_ps_plane_trainer_overlap(where, monkeypatch):
     monkeypatch.setenv("TONY_PS_SPIN_S", "20")
     monkeypatch.setenv("TONY_PS_PLANE_TRACE", "1")
     out = _spawn(__import__("ps_plane_worker").run_overlap, 3)

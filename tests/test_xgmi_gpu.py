@@ -12,6 +12,8 @@ import socket
 
 import pytest
 
+from gpu_ranks import placement
+
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(180)]
 
 
@@ -23,7 +25,7 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4], ids=lambda w: placement(w))
 def test_xgmi_collectives(world, monkeypatch):
     import xgmi_worker as W
 

@@ -4,16 +4,16 @@ import os
 import torch
 import torch.distributed as dist
 
+import gpu_ranks
+
 
 def run(rank, world, port, q, skip=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     try:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        torch.cuda.set_device(0)  # every rank on the one GPU of the test box: IPC + the protocol
+        dev, _ = gpu_ranks.init(rank, world)  # own GPU per rank over RCCL, or all on the box's one GPU
         from tony_amd.parallel.xgmi import XgmiComm, XgmiError
 
         comm = XgmiComm(slot_bytes=1 << 20, oneshot_max_bytes=64 << 10, blocks=8)
-        dev = torch.device("cuda", 0)
         res = {}
         for dtype in (torch.float32, torch.bfloat16):
             # one-shot, two-shot, odd size (two-shot pieces + a one-shot tail), multi-piece

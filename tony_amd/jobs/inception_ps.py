@@ -113,8 +113,14 @@ def main(argv=None) -> int:
     if state is not None:
         ps.load_state_dict(state["ps"])
         with torch.no_grad():
+            missing = []
             for k, b in model.named_buffers():
-                b.copy_(state["buffers"][k])
+                if k in state["buffers"]:
+                    b.copy_(state["buffers"][k])
+                else:  # a checkpoint older than the buffer (e.g. the dropout step counter): keep the init
+                    missing.append(k)
+            if missing:
+                log(f"checkpoint has no buffers {missing}: kept their initial values")
         torch.set_rng_state(state["rng_cpu"])  # dropout masks continue exactly where they were
         if on_gpu and "rng_cuda" in state:
             torch.cuda.set_rng_state(state["rng_cuda"], dev)
@@ -180,8 +186,13 @@ def main(argv=None) -> int:
     dist.all_reduce(rate)
     workers = len(ps.worker_ranks)
     if tc.is_chief or rank == 0:
+        from tony_amd.parallel import collectives as coll
+
+        # which data plane moved the gradients / variables, and whether its init-time canary against
+        # RCCL passed: a run that fell back must not look like one on the hand plane
         metric(model="inception_v3", images_per_sec=float(rate), workers=workers, ps_mode=mode, loss=float(loss),
-               start_step=start, steps=total)
+               start_step=start, steps=total, plane=_plane_name(ps), verified=coll.data_plane_status(),
+               collective_fallbacks=coll.fallback_count())
     log(f"{float(rate):.1f} images/sec total over {workers} workers ({mode} PS)")
     dist.barrier()
     # orderly shutdown: drain the device (side streams included) and tear the process group down before
@@ -193,6 +204,18 @@ def main(argv=None) -> int:
         ps.plane.close()
     dist.destroy_process_group()
     return 0
+
+
+def _plane_name(ps) -> str:
+    """The data plane the PS traffic took: the xGMI PS plane (dedicated), the xGMI collective kernels
+    (colocated, TONY_COLLECTIVE=hip) or the process group's backend (rccl / gloo)."""
+    from tony_amd.parallel import collectives as coll
+
+    if ps.plane_kind == "xgmi":
+        return "xgmi-ps-plane"
+    if coll.data_plane_status().get("xgmi_collectives") == "verified":
+        return "xgmi-collectives"
+    return "rccl" if dist.get_backend() == "nccl" else dist.get_backend()
 
 
 if __name__ == "__main__":

@@ -84,30 +84,67 @@ class XgmiComm:
             self._canary()
 
     def _canary(self) -> None:
-        """One-shot (bf16) and two-shot (fp32) all-reduces of random data checked against
-        ``dist.all_reduce`` of the same inputs on every rank; raises XgmiError on all ranks if any
-        rank saw a mismatch (the caller falls back to RCCL), sets ``verified`` otherwise."""
+        """Every collective kind checked against the process group's own collective on random data
+        before any gradient goes through this plane: one-shot (bf16) and two-shot (fp32) all-reduces
+        against ``dist.all_reduce``, reduce-scatter (bf16 and fp32, the colocated PS's push) against
+        the matching shard of ``dist.all_reduce``, all-gather (the PS pull) against
+        ``dist.all_gather`` and broadcast from the last rank against ``dist.broadcast``.
+        Raises XgmiError on every rank if any rank saw a mismatch (the caller falls back to RCCL),
+        after unmapping the peers and freeing the window; sets ``verified`` otherwise."""
         g = torch.Generator(device=self.device).manual_seed(4242 + self.rank)
-        two = max(self.oneshot_max_bytes // 4 + 4096, 4096 * self.world) // 1024 * 1024
+        w = self.world
+        two = max(self.oneshot_max_bytes // 4 + 4096, 4096 * w) // 1024 * 1024
         bad = []
+
+        def expect(kind, got, want, dtype):
+            tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+            if got.shape != want.shape or not torch.allclose(got.float(), want.float(), rtol=tol, atol=tol):
+                diff = float((got.float() - want.float()).abs().max()) if got.shape == want.shape else "shape"
+                bad.append(f"{kind} {dtype} x {want.numel()}: max |diff| {diff}")
+
+        def mine(fn, *a, **k):  # an xGMI call that fails is recorded; every rank still makes every
+            try:                 # process-group call below in the same order
+                fn(*a, **k)
+            except XgmiError as e:
+                bad.append(str(e))
+
         for n, dtype in ((2048, torch.bfloat16), (min(two, self.slot_bytes // 8), torch.float32)):
             t = torch.randn(n, generator=g, device=self.device).to(dtype)
             ref = t.float()
-            self.all_reduce(t)
+            mine(self.all_reduce, t)
             dist.all_reduce(ref, group=self.group)
-            want = ref.to(dtype).float()
-            tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
-            if not torch.allclose(t.float(), want, rtol=tol, atol=tol):
-                bad.append(f"{dtype} x {n}: max |diff| {float((t.float() - want).abs().max()):.3g}")
-        try:
-            self.check_error()
-        except XgmiError as e:
-            bad.append(str(e))
-        allbad: List[Optional[list]] = [None] * self.world
+            expect("all_reduce", t, ref.to(dtype), dtype)
+        for dtype in (torch.bfloat16, torch.float32):
+            m = 1024 * w + 8 * 3                     # per-rank shard: not a power of two
+            inp = torch.randn(w * m, generator=g, device=self.device).to(dtype)
+            out = torch.empty(m, device=self.device, dtype=dtype)
+            mine(self.reduce_scatter, out, inp)
+            ref = inp.float()
+            dist.all_reduce(ref, group=self.group)
+            expect("reduce_scatter", out, ref[self.rank * m:(self.rank + 1) * m].to(dtype), dtype)
+            shard = torch.randn(m, generator=g, device=self.device).to(dtype)
+            gat = torch.empty(w * m, device=self.device, dtype=dtype)
+            mine(self.all_gather, gat, shard)
+            parts = [torch.empty(m, device=self.device, dtype=torch.float32) for _ in range(w)]
+            dist.all_gather(parts, shard.float(), group=self.group)
+            expect("all_gather", gat, torch.cat(parts).to(dtype), dtype)
+            b = torch.randn(4096 + 8, generator=g, device=self.device).to(dtype)
+            ref = b.float().clone()
+            root = w - 1
+            mine(self.broadcast, b, src=root)
+            dist.broadcast(ref, src=dist.get_global_rank(self.group, root) if self.group is not None else root,
+                           group=self.group)
+            expect("broadcast", b, ref.to(dtype), dtype)
+        mine(self.check_error)
+        allbad: List[Optional[list]] = [None] * w
         dist.all_gather_object(allbad, bad, group=self.group)
         msgs = [f"rank {r}: {m}" for r, b in enumerate(allbad) for m in (b or [])]
         if msgs:
-            raise XgmiError("xGMI collective canary mismatch against the process group's all-reduce: "
+            try:
+                self.close()  # every rank gets here together (the verdict above is gathered)
+            except XgmiError:
+                self._release()
+            raise XgmiError("xGMI collective canary mismatch against the process group's collectives: "
                             + "; ".join(msgs))
         self.verified = True
 
@@ -235,9 +272,13 @@ class XgmiComm:
             return
         self.check_error()
         dist.barrier(group=self.group)  # no peer may still be reading this rank's window
+        self._release()
+
+    def _release(self) -> None:
         L = _lib.lib()
         for p in self.peers:
             L.tony_xgmi_close(p)
-        L.tony_xgmi_free(self.window)
+        if self.window is not None:
+            L.tony_xgmi_free(self.window)
         self.window = None
         self.peers = []
