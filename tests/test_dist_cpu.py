@@ -284,3 +284,51 @@ def test_kvstore_plane_layout_agrees_between_server_and_workers(monkeypatch):
     for v in spans.values():
         v.sort()
         assert all(a[1] <= b[0] for a, b in zip(v, v[1:]))
+
+
+def test_kv_server_parks_a_plane_push_that_arrives_before_init(monkeypatch):
+    """A worker's plane push (OP_PUSH_X) can reach the server before worker 0's INIT of the key: the
+    server has no window row for the key yet, so it must park the raw header and read the row when
+    the INIT has laid the key out -- not raise KeyError.  A stand-in plane over host memory."""
+    import ctypes
+
+    from tony_amd.parallel import kvstore as kvs
+
+    monkeypatch.setenv("DMLC_ROLE", "server")
+    monkeypatch.setenv("DMLC_NUM_SERVER", "1")
+    monkeypatch.setenv("DMLC_NUM_WORKER", "2")
+    topo = kvs._Topology()
+    window = torch.zeros(4096, dtype=torch.uint8)
+
+    class HostPlane:
+        device = torch.device("cpu")
+        base = window.data_ptr()
+
+        def __init__(self):
+            self.layout = kvs._KvLayout(topo, window.numel())
+            self.keys = self.layout.keys
+            self.copies = []
+
+        def add_key(self, kid, nbytes):
+            return self.layout.add_key(kid, nbytes)
+
+        def copy(self, dst, src, nbytes, wait=True):
+            self.copies.append(nbytes)
+            ctypes.memmove(dst, src, nbytes)
+
+    plane = HostPlane()
+    srv = kvs._Server(topo, sync=False, plane=plane)
+    kid, n = 5, 3
+    # worker 1 (global rank 2) wrote its row -- at the offset the layout WILL give the key -- then sent the header
+    lay = kvs._KvLayout(topo, window.numel())
+    lay.add_key(kid, 4 * n)
+    _, nbytes, row_off, _ = lay.keys[kid]
+    row = torch.tensor([1.0, 2.0, 3.0])
+    ctypes.memmove(window.data_ptr() + row_off + 1 * kvs._pad16(nbytes), row.data_ptr(), nbytes)
+    assert srv.handle(2, [kvs.OP_PUSH_X, kid, n, kvs._dcode(torch.float32)]) is True
+    assert kid in srv.early and plane.copies == []           # parked, the row not read yet
+    srv.handle(1, [kvs.OP_INIT, kid, n, kvs._dcode(torch.float32)], torch.zeros(n))
+    assert kid not in srv.early
+    # async server without an optimizer: the pushed value replaces the stored one
+    torch.testing.assert_close(srv.values[kid].cpu(), row)
+    assert plane.copies == [nbytes]

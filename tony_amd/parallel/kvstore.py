@@ -332,12 +332,13 @@ class _KvPlane:
     def add_key(self, kid: int, nbytes: int) -> bool:
         return self.layout.add_key(kid, nbytes)
 
-    def copy(self, dst: int, src: int, nbytes: int) -> None:
+    def copy(self, dst: int, src: int, nbytes: int, wait: bool = True) -> None:
         from ..ops import _lib
 
         with torch.cuda.device(self.device):
             _lib.check(self.L.tony_kv_copy(dst, src, nbytes, _lib.stream_ptr(self.device)), "tony_kv_copy")
-            torch.cuda.current_stream(self.device).synchronize()  # landed before the header / token is sent
+            if wait:
+                torch.cuda.current_stream(self.device).synchronize()  # landed before the header / token is sent
 
     def close(self) -> None:
         for p in self._opened:
@@ -423,19 +424,23 @@ class _Server:
             buf = torch.empty(numel, dtype=_DTYPES[dcode])
             dist.recv(buf, worker, tag=TAG_DATA)
         via = op == OP_PULL_X
+        if op in (OP_PUSH, OP_PULL, OP_PUSH_X, OP_PULL_X) and kid not in self.values:
+            # raced ahead of worker 0's INIT (it is sent before the workers' barrier, but the server
+            # may poll this worker first): replay once the key exists.  A plane push is parked with its
+            # raw header: the key has no window row in this server's layout until the INIT adds it, and
+            # the worker does not rewrite that row before its next pull (DistKVStore._unread)
+            self.early.setdefault(kid, []).append((worker, hdr, buf))
+            return True
         if op == OP_PUSH_X:  # the payload is in this worker's receive row of the window: take it now
             _, nbytes, row_off, _ = self.plane.keys[kid]
             buf = torch.empty(numel, dtype=_DTYPES[dcode], device=self.plane.device)
             w = worker - self.topo.num_servers
-            self.plane.copy(buf.data_ptr(), self.plane.base + row_off + w * _pad16(nbytes), nbytes)
+            # stream-ordered, no host wait: the worker rewrites this row only after its pull, whose reply
+            # copy is issued behind this one on the same stream and waited for before the token goes out
+            self.plane.copy(buf.data_ptr(), self.plane.base + row_off + w * _pad16(nbytes), nbytes, wait=False)
             op = OP_PUSH
         elif op == OP_PULL_X:
             op = OP_PULL
-        if op in (OP_PUSH, OP_PULL) and kid not in self.values:
-            # raced ahead of worker 0's INIT (it is sent before the workers' barrier, but
-            # the server may poll this worker first): replay once the key exists
-            self.early.setdefault(kid, []).append((worker, hdr, buf))
-            return True
         if op in (OP_INIT, OP_PUSH, OP_OPT):
             if op == OP_INIT:
                 if self.plane is not None and self.plane.add_key(kid, buf.numel() * buf.element_size()):
@@ -553,6 +558,8 @@ class DistKVStore(KVStore):
             if self._on_plane(kid, g) and kid not in self._unread:
                 srv, nbytes, row_off, _ = self.plane.keys[kid]
                 g = g.to(self.plane.device).contiguous()
+                if g.data_ptr() % 16:  # the copy kernel moves 16-B aligned addresses: a view at an odd offset
+                    g = g.clone()
                 self.plane.copy(self.plane.peer[srv] + row_off + self.rank * _pad16(nbytes), g.data_ptr(), nbytes)
                 dist.send(torch.tensor([OP_PUSH_X, kid, g.numel(), _dcode(g.dtype)], dtype=torch.int64), srv,
                           tag=TAG_HDR)
