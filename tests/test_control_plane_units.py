@@ -711,8 +711,26 @@ def test_visible_mode_auto_isolates_unless_a_peer_plane_is_configured():
     assert resolve_visible_mode(conf()) == "hip"  # a plain job
     assert resolve_visible_mode(conf(tony__application__framework="pytorch", tony__worker__instances=4)) == "hip"
     assert resolve_visible_mode(conf(tony__amd__collective="hip")) == "none"
-    assert resolve_visible_mode(conf(tony__ps__instances=1, tony__worker__instances=4)) == "none"
+    # an ordinary user TF PS job keeps its isolation (the ps-plane key's xgmi default alone
+    # does not count); tony_amd's own PS program, or an explicit xgmi plane, maps peer GPUs
+    assert resolve_visible_mode(conf(tony__ps__instances=1, tony__worker__instances=4)) == "hip"
+    assert resolve_visible_mode(conf(tony__ps__instances=1, tony__worker__instances=4,
+                                     tony__containers__command="python3 inception_ps.py --batch-size 32")) == "none"
+    assert resolve_visible_mode(conf(tony__ps__instances=1, **{"tony__amd__ps-plane": "xgmi"})) == "none"
     assert resolve_visible_mode(conf(tony__ps__instances=1, **{"tony__amd__ps-plane": "rccl"})) == "hip"
+    # the decision survives the round trip through tony-final.xml (sources are written and re-read)
+    import tempfile
+
+    from tony_amd.conf import keys as K
+
+    with tempfile.TemporaryDirectory() as d:
+        for c, want in ((conf(tony__ps__instances=1), "hip"),
+                        (conf(tony__ps__instances=1, **{"tony__amd__ps-plane": "xgmi"}), "none")):
+            path = os.path.join(d, "tony-final.xml")
+            c.write_xml(path)
+            back = Configuration.from_xml(path)
+            assert back.get_source(K.AMD_PS_PLANE) == c.get_source(K.AMD_PS_PLANE)
+            assert resolve_visible_mode(back) == want
     assert resolve_visible_mode(conf(tony__application__framework="pytorch", tony__ps__instances=1)) == "hip"
     # MXNet kvstore servers with GPU workers: the payload plane maps peer windows
     mx = dict(tony__application__framework="mxnet", tony__server__instances=1, tony__worker__gpus=1)
@@ -818,3 +836,28 @@ def test_ps_shares_a_worker_gpu_policy_and_allocator():
     assert a.free_count() == 3  # sharing takes no GPU from the free list
     a.release("ps:0")
     assert a.sharers() == {} and a.owners() == {0: "worker:0"}
+
+
+def test_shared_gpu_stays_allocated_until_its_last_sharer_leaves():
+    """a worker that owns a GPU exits while the ps sharing it still runs -- the GPU must not
+    go back to the free list (the next allocation would land on a busy GPU) until the ps releases it."""
+    from tony_amd.gpu.inventory import GpuAllocator, discover
+
+    a = GpuAllocator(discover(2))
+    w0 = a.allocate("worker:0", 1)
+    a.share("ps:0", w0.gpus[0])
+    a.release("worker:0")
+    assert a.owners() == {} and a.sharers() == {0: ["ps:0"]}
+    assert a.free_count() == 1
+    nxt = a.allocate("worker:1", 1)
+    assert nxt.gpus == [1]          # not the GPU the ps is still on
+    assert a.allocate("worker:2", 1) is None
+    a.release("ps:0")
+    assert a.free_count() == 1 and a.allocate("worker:2", 1).gpus == [0]
+    # owner leaving after its sharer: freed at once
+    b = GpuAllocator(discover(1))
+    g = b.allocate("worker:0", 1).gpus[0]
+    b.share("ps:0", g)
+    b.release("ps:0")
+    b.release("worker:0")
+    assert b.free_count() == 1

@@ -67,21 +67,31 @@ def _default_history_root(conf, staging_root: str) -> str:
     return loc
 
 
+def _runs_tony_amd_job(conf) -> bool:
+    """Whether the job's task command is one of tony_amd's own training programs (tony_amd/jobs),
+    which bring up the tony_amd data planes themselves."""
+    cmds = [conf.get(K.CONTAINERS_COMMAND) or ""] + [v for k, v in conf.get_val_by_regex(r"^tony\.[a-z]+\.command$").items()]
+    return any("tony_amd" in c or "inception_ps" in c for c in cmds)
+
+
 def resolve_visible_mode(conf) -> str:
     """``tony.amd.visible-devices-mode`` for a job: ``none`` / ``hip`` / ``rocr`` as configured, and for
     ``auto`` (the default) ``none`` only when the job runs a tony_amd data plane that maps a peer GPU's
     memory -- ``tony.amd.collective=hip`` (the xGMI collective kernels), or a TensorFlow job with ps tasks
-    on the xGMI parameter-server plane (``tony.amd.ps-plane``, default xgmi; parallel/ps_plane.py) --
-    and ``hip`` (per-task HIP_VISIBLE_DEVICES) for everything else, so an arbitrary user program that
-    picks ``cuda:0`` or ``cuda:LOCAL_RANK`` cannot land on another task's GPU."""
+    that runs tony_amd's PS program (a task command from tony_amd/jobs) or sets ``tony.amd.ps-plane=xgmi``
+    itself (parallel/ps_plane.py; the key's xgmi default alone does not count: an ordinary user TF PS job
+    keeps its isolation) -- and ``hip`` (per-task HIP_VISIBLE_DEVICES) for everything else, so an
+    arbitrary user program that picks ``cuda:0`` or ``cuda:LOCAL_RANK`` cannot land on another task's GPU."""
     mode = (conf.get(K.AMD_VISIBLE_DEVICES_MODE, "auto") or "auto").lower()
     if mode != "auto":
         return mode
     if conf.get(K.AMD_COLLECTIVE, "rccl").lower() in ("hip", "xgmi"):
         return "none"
     framework = conf.get(K.FRAMEWORK_NAME, "tensorflow").lower()
-    if framework == "tensorflow" and conf.get_int("tony.ps.instances", 0) > 0 \
-            and conf.get(K.AMD_PS_PLANE, "xgmi").lower() == "xgmi":
+    plane = conf.get(K.AMD_PS_PLANE, "xgmi").lower()
+    explicit = (conf.get_source(K.AMD_PS_PLANE) or "tony-default.xml") != "tony-default.xml"
+    if framework == "tensorflow" and conf.get_int("tony.ps.instances", 0) > 0 and plane == "xgmi" \
+            and (explicit or _runs_tony_amd_job(conf)):
         return "none"
     # an MXNet job whose kvstore servers move GPU payloads on the peer-mapped plane (parallel/kvstore.py)
     if framework == "mxnet" and conf.get_int("tony.server.instances", 0) > 0 \

@@ -29,8 +29,9 @@ class ConfigurationError(ValueError):
     pass
 
 
-def parse_xml_properties(src) -> List[Tuple[str, Optional[str], bool, Optional[str]]]:
-    """Parse ``<configuration><property>…`` into (name, value, final, description)."""
+def parse_xml_properties(src) -> List[Tuple[str, Optional[str], bool, Optional[str], Optional[str]]]:
+    """Parse ``<configuration><property>…`` into (name, value, final, description, source); ``source`` is
+    the ``<source>`` element a written ``tony-final.xml`` carries per property (None elsewhere)."""
     if isinstance(src, (bytes, bytearray)):
         root = ET.fromstring(src)
     elif hasattr(src, "read"):
@@ -47,7 +48,9 @@ def parse_xml_properties(src) -> List[Tuple[str, Optional[str], bool, Optional[s
         value_el = p.find("value")
         value = None if value_el is None else (value_el.text or "")
         final = (p.findtext("final") or "").strip().lower() == "true"
-        props.append((name.strip(), value, final, p.findtext("description")))
+        src_el = p.findtext("source")
+        props.append((name.strip(), value, final, p.findtext("description"),
+                      src_el.strip() if src_el and src_el.strip() else None))
     return props
 
 
@@ -72,12 +75,13 @@ class Configuration:
         return self
 
     def _apply_resource(self, label, props):
-        for key, value, final, _ in props:
+        for key, value, final, _, source in props:
             if key in self._final:
                 continue  # an earlier resource marked it final
             if value is None:
                 continue
-            self._props[key] = (value, label)
+            # a re-read tony-final.xml keeps each value's original source (e.g. tony-default.xml)
+            self._props[key] = (value, source or label)
             if final:
                 self._final.add(key)
 

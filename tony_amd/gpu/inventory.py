@@ -259,15 +259,20 @@ class GpuAllocator:
         return sorted(take)
 
     def release(self, owner: str) -> None:
+        """Return ``owner``'s GPUs and CPUs.  A GPU stays off the free list while a task that shares it
+        (``share``) is still alive, even after its owner left: it goes back when its last sharer does."""
         with self._lock:
             for g in list(self._sharers):
                 self._sharers[g] = [o for o in self._sharers[g] if o != owner]
                 if not self._sharers[g]:
                     del self._sharers[g]
+                    if g not in self._owner and g not in self._free:  # its owner already left
+                        self._free.append(g)
             for g, o in list(self._owner.items()):
                 if o == owner:
                     del self._owner[g]
-                    self._free.append(g)
+                    if g not in self._sharers:
+                        self._free.append(g)
             self._free.sort()
             for c, o in list(self._cpu_owner.items()):
                 if o == owner:
