@@ -345,32 +345,55 @@ def main(argv=None):
         # then eager steps and graph replays are timed and the faster way of issuing the step is
         # kept -- eager launches overlap the weight gradients with the data-gradient chain on a second
         # stream and the bucketed PS communication with backward, which a replayed graph does not.
+        issue = [0.0]  # host seconds spent inside trainer.step over the last window
+
         def timed(n):
             if world > 1:
                 dist.barrier()
             torch.cuda.synchronize()
             t = time.perf_counter()
+            issue[0] = 0.0
             for _ in range(n):
+                th = time.perf_counter()
                 trainer.step(x, y)
+                issue[0] += time.perf_counter() - th
             torch.cuda.synchronize()
             return max_over_ranks(time.perf_counter() - t, device=dev) / n
+
+        def window(graph: bool, n: int = 4):
+            trainer.use_graph = graph and ps.is_worker
+            w = timed(n)
+            return w, issue[0] / n
 
         for _ in range(trainer.warmup_eager):
             trainer.step(x, y)
         trainer.use_graph = False
         timed(2)  # the warm-up steps ran on a side stream: let the allocator fill this stream's pool
-        # best of two windows per mode: one host hiccup must not decide the mode for the whole run
-        setup["eager_ms"] = round(1000 * min(timed(4), timed(4)), 3)
-        if ps.is_worker:
-            trainer.use_graph = True
+        trainer.use_graph = ps.is_worker
         trainer.step(x, y)  # capture
-        setup["graph_ms"] = round(1000 * min(timed(4), timed(4)), 3)
-        # ties go to the plan: its host issue cost is ~2.5 ms/step against eager's ~11-13 ms, so a host
-        # slowed by other work on the machine cannot stall the GPU (an eager run timed at 15.3 ms/step
-        # after its setup measured 13.4, profiles/r4_bench_host_bound_eager.log)
-        # (one rank only: with several, a replay's bucket collectives interleave with its segments, and the
-        # plan has to win outright)
-        mode = "graph" if setup["graph_ms"] <= setup["eager_ms"] * (PLAN_TIE if world == 1 else 1.0) else "eager"
+        # alternating windows (eager, plan, eager, plan, ...): a box's slow minute hits both modes alike;
+        # best window per mode
+        ew, gw, eh = [], [], []
+        for _ in range(3):
+            w, h = window(False)
+            ew.append(w)
+            eh.append(h)
+            gw.append(window(True)[0])
+        setup["eager_ms"] = round(1000 * min(ew), 3)
+        setup["graph_ms"] = round(1000 * min(gw), 3)
+        # host issue of an eager step: near the GPU time, a host slowed by other work on the machine stalls
+        # the GPU (an eager run timed at 15.3 ms/step after its setup measured 13.4,
+        # profiles/r4_bench_host_bound_eager.md); the plan issues a step in ~2.5 ms
+        setup["eager_host_ms"] = round(1000 * min(eh), 3)
+        eager_host_bound = setup["eager_host_ms"] > EAGER_HOST_BOUND * setup["eager_ms"]
+        # one rank: the faster schedule wins; eager needs a margin only when its issue is near host-bound.
+        # Several ranks: a replay's bucket collectives interleave with its segments, the plan must win.
+        if world == 1:
+            mode = "graph" if (setup["graph_ms"] <= setup["eager_ms"] * (PLAN_TIE if eager_host_bound else 1.0)) \
+                else "eager"
+        else:
+            mode = "graph" if setup["graph_ms"] <= setup["eager_ms"] else "eager"
+        setup["eager_host_bound"] = eager_host_bound
         trainer.use_graph = mode == "graph" and ps.is_worker
         if rank == 0:
             print(f"[bench] setup {time.perf_counter() - t_w:.1f}s: {setup} -> {mode}", file=sys.stderr, flush=True)
@@ -533,8 +556,11 @@ def main(argv=None):
     return rc
 
 
-# --mode auto keeps the plan unless eager issue is faster by more than this factor (TONY_PLAN_TIE)
+# --mode auto at one rank: the faster of eager and plan; when eager's host issue time per step exceeds
+# EAGER_HOST_BOUND x its step time (close to host-bound: a busier host would stall the GPU), eager must
+# beat the plan by more than PLAN_TIE (TONY_PLAN_TIE / TONY_EAGER_HOST_BOUND)
 PLAN_TIE = float(os.environ.get("TONY_PLAN_TIE", "1.01"))
+EAGER_HOST_BOUND = float(os.environ.get("TONY_EAGER_HOST_BOUND", "0.8"))
 
 
 def _fp32_row(args) -> dict:

@@ -644,3 +644,85 @@ def test_bn_reduce_fused_into_dgrad(cuda):
         assert _rel(a, b) < 2e-3, f"param {i}: fused vs unfused {_rel(a, b):.2e}"
         # bf16 chain vs fp32: the fused path is no further from fp32 than the unfused one
         assert _rel(a, r) < 1.2 * _rel(b, r) + 1e-2, f"param {i}: fused {_rel(a, r):.2e} unfused {_rel(b, r):.2e}"
+
+
+SPLITK_SHAPES = [(8, 192, 17, 17, 192, (1, 7), (0, 3)), (8, 160, 17, 17, 160, (7, 1), (3, 0)),
+                 (16, 384, 8, 8, 384, (3, 1), (1, 0)), (16, 448, 8, 8, 384, (3, 3), (1, 1))]
+
+
+@pytest.mark.parametrize("m", [1, 2, 3])
+@pytest.mark.parametrize("v", [11, 12, 14, 17, 20, 23])
+@pytest.mark.parametrize("shape", SPLITK_SHAPES, ids=[f"{s[1]}->{s[4]}_{s[2]}k{s[5][0]}x{s[5][1]}" for s in SPLITK_SHAPES])
+def test_conv_glds_streamk(cuda, shape, v, m):
+    """Stream-K form of the LDS-DMA conv (igemm.h SplitK: m x CUs workgroups own equal ranges of the
+    (tile, K-step) iterations; the contributors of a shared tile fold their partials, the last arriver
+    summing them in K order and running the epilogue).  At batch 8 every tile is shared by many
+    workgroups (>= 4 K-steps each): forward + BN statistics and stride-1 backward-data against fp32,
+    deterministic (two runs bit-identical) and equal to the plain kernel within fp32 reassociation."""
+    from tony_amd.ops import _lib
+    from tony_amd.ops.conv import conv_dgrad, conv_fwd
+
+    n, c, h, w, co, (r, s), p = shape
+    kb = 64 if v in (11, 17, 22) else 32
+    if c % kb or co % kb:
+        pytest.skip("uniform-tap shapes only for this variant")
+    vf = (v << 8) | (m << 16)
+    torch.manual_seed(v + 7 * m)
+    x = _nhwc(torch.randn(n, c, h, w, device=cuda)).to(torch.bfloat16)
+    wt = _nhwc(torch.randn(co, c, r, s, device=cuda) / (c * r * s) ** 0.5).to(torch.bfloat16)
+    stats = torch.zeros(_lib.stat_floats(co), device=cuda)
+    y = conv_fwd(x, wt, 1, p, stats, vflags=vf)
+    y2 = conv_fwd(x, wt, 1, p, None, vflags=vf)
+    y1 = conv_fwd(x, wt, 1, p, None, vflags=v << 8)
+    assert torch.equal(y, y2), "the fold must not depend on which contributor arrives last"
+    assert (y.float() - y1.float()).abs().max().item() <= 2 ** -6 * y1.float().abs().max().item()
+    xr = x.float().requires_grad_(True)
+    ref = torch.nn.functional.conv2d(xr, wt.float(), None, 1, p)
+    assert _rel(y, ref) < 1e-2
+    st = _lib.fold_stats(stats, co)
+    torch.testing.assert_close(st[:co], ref.detach().sum((0, 2, 3)), rtol=2e-3, atol=ref.numel() / co * 2e-4)
+    torch.testing.assert_close(st[co:], (ref.detach() ** 2).sum((0, 2, 3)), rtol=2e-3, atol=1e-1)
+    dy = _nhwc(torch.randn_like(ref)).to(torch.bfloat16)
+    ref.backward(dy.float())
+    dx = conv_dgrad(dy, wt, x.shape, 1, p, vflags=vf)
+    assert _rel(dx, xr.grad) < 1e-2
+    g = _nhwc(torch.randn(n, c, h, w, device=cuda)).to(torch.bfloat16)
+    want = g.float() + dx.float()
+    out = conv_dgrad(dy, wt, x.shape, 1, p, vflags=vf, accum=g)
+    torch.testing.assert_close(out.float(), want, rtol=1.6e-2, atol=1.6e-2)
+
+
+@pytest.mark.parametrize("m", [1, 3])
+def test_gemm_glds_streamk_reuses_rearmed_counters(cuda, m):
+    """The 1x1 GEMM path (tony_gemm_bf16 on the LDS-DMA kernel) in stream-K form through ONE persistent
+    workspace, three launches in a row: each launch's last arrivers re-arm the tile counters, so the
+    next launch reads a clean ticket sequence; an 8x8 head GEMM (M = 1024, K = 2048) with BN stats."""
+    from tony_amd.ops import _lib
+
+    L = _lib.lib()
+    M, N, K = 1024, 448, 2048
+    torch.manual_seed(m)
+    a = torch.randn(M, K, device=cuda).to(torch.bfloat16)
+    b = (torch.randn(N, K, device=cuda) / K ** 0.5).to(torch.bfloat16)
+    ref = a.float() @ b.float().t()
+    slab = torch.empty(_lib.splitk_slab_floats(m, _lib.num_cus(cuda)), device=cuda)
+    cnt = torch.zeros(2 * _lib.SPLITK_MAX_TILES, dtype=torch.int32, device=cuda)
+    raw = L.tony_gemm_bf16.__wrapped__
+    st = _lib.stream_ptr(cuda)
+    outs = []
+    try:
+        _lib.check(L.tony_splitk_workspace(slab.data_ptr(), slab.numel(), cnt.data_ptr(), cnt.numel()), "ws")
+        for _ in range(3):
+            c = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+            stats = torch.zeros(_lib.stat_floats(N), device=cuda)
+            _lib.check(raw(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, K, K, N,
+                           1 | (14 << 8) | (m << 16), stats.data_ptr(), 2 * N, st), "gemm stream-K")
+            outs.append((c, stats))
+        torch.cuda.synchronize()
+    finally:
+        L.tony_splitk_workspace(0, 0, 0, 0)
+    assert int(cnt.abs().sum()) == 0, "counters re-armed to zero"
+    for c, stats in outs:
+        assert torch.equal(c, outs[0][0])
+        assert _rel(c, ref) < 1e-2
+        torch.testing.assert_close(_lib.fold_stats(stats, N)[:N], ref.sum(0), rtol=2e-3, atol=M * 2e-3)

@@ -315,16 +315,20 @@ def test_gpu_pinning_and_numa_env(conf):
     assert rc == 0
 
 
-def test_zero_gpu_ps_shares_a_worker_gpu(conf, tmp_path):
+@pytest.mark.parametrize("plane", [None, "xgmi"], ids=["user-job-isolated", "explicit-xgmi-plane"])
+def test_zero_gpu_ps_shares_a_worker_gpu(conf, tmp_path, plane):
     """VERDICT r3 #1 (TonY default: ps tasks request no GPU): the ps of a GPU TensorFlow job is placed on
-    worker 0's GPU, shared, so "1 ps + N workers" fits N GPUs; visible-devices-mode auto leaves every GPU
-    visible for such a job (the xGMI PS plane maps peer memory) and the pinning names the shared GPU."""
+    worker 0's GPU, shared, so "1 ps + N workers" fits N GPUs, and the pinning names the shared GPU.
+    visible-devices-mode auto keeps an ordinary user job isolated (HIP_VISIBLE_DEVICES: the ps sees only
+    worker 0's GPU) and leaves every GPU visible when the job asks for the xGMI PS plane (it maps
+    peer memory)."""
     rec = tmp_path / "rec"
     rec.mkdir()
     conf.set(K.AMD_VISIBLE_DEVICES_MODE, "auto")
+    extra = ["--conf", f"tony.amd.ps-plane={plane}"] if plane else []
     rc, _ = run(conf, base("--executes", "record_gpu_env.py", "--conf", "tony.ps.instances=1",
                            "--conf", "tony.worker.instances=2", "--conf", "tony.worker.gpus=1",
-                           "--shell_env", f"RECORD_DIR={rec}"))
+                           "--shell_env", f"RECORD_DIR={rec}", *extra))
     assert rc == 0
     env = {}
     for f in rec.iterdir():
@@ -333,7 +337,13 @@ def test_zero_gpu_ps_shares_a_worker_gpu(conf, tmp_path):
     assert env["worker_0"]["TONY_GPU_IDS"] != env["worker_1"]["TONY_GPU_IDS"]  # workers: exclusive GPUs
     assert env["ps_0"]["TONY_GPU_IDS"] == env["worker_0"]["TONY_GPU_IDS"]       # ps: worker 0's, shared
     for e in env.values():
-        assert e["TONY_PS_SHARED_GPU"] == "1" and e["TONY_VISIBLE_MODE"] == "none" and not e["HIP_VISIBLE_DEVICES"]
+        assert e["TONY_PS_SHARED_GPU"] == "1"
+        if plane == "xgmi":
+            assert e["TONY_VISIBLE_MODE"] == "none" and not e["HIP_VISIBLE_DEVICES"]
+        else:
+            assert e["TONY_VISIBLE_MODE"] == "hip" and e["HIP_VISIBLE_DEVICES"]
+    if plane != "xgmi":
+        assert env["ps_0"]["HIP_VISIBLE_DEVICES"] == env["worker_0"]["HIP_VISIBLE_DEVICES"]
 
 
 def test_gpu_request_larger_than_node_rejected(conf):

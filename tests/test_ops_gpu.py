@@ -636,3 +636,28 @@ def test_splitk_reduce_sums_the_slab(cuda, splits, n, bf16):
         want = ref + (base.double() if acc else 0)
         tol = 1e-2 * (splits ** 0.5) if bf16 else 1e-4 * splits ** 0.5
         torch.testing.assert_close(dst.double(), want.to(dt).double(), rtol=1e-2 if bf16 else 1e-5, atol=tol)
+
+
+@pytest.mark.parametrize("dst", ["new", "fp32", "bf16"])
+def test_whole_input_conv_wgrad_nt_gemm_accumulates_into_slot(cuda, dst):
+    """The aux head's whole-input conv weight gradient as one NT GEMM over the transposed operands
+    (ops/conv.py _gemm_wgrad: K = batch, no split-K slab / combine): returned fp32, or ADDED into an fp32
+    or bf16 gradient slot in [Co][R][S][C] order (epilogue accumulate)."""
+    from tony_amd.ops import conv as C
+
+    torch.manual_seed(3)
+    n, cin, co = 128, 128, 768
+    x = _nhwc(torch.randn(n, cin, 5, 5, device=cuda)).to(torch.bfloat16)
+    dy = _nhwc(torch.randn(n, co, 1, 1, device=cuda)).to(torch.bfloat16)
+    ref = torch.einsum("no,nchw->ochw", dy.float().reshape(n, co), x.float())  # [co, c, h, w]
+    want = ref.permute(0, 2, 3, 1).reshape(-1)                                # slot order [co][h][w][c]
+    if dst == "new":
+        out = C._gemm_wgrad(dy, x, (co, cin, 5, 5))
+        torch.testing.assert_close(out, ref, rtol=1e-3, atol=1e-2)
+        return
+    dt = torch.float32 if dst == "fp32" else torch.bfloat16
+    slot = torch.randn(co * 25 * cin, device=cuda).to(dt)
+    before = slot.float().clone()
+    assert C._gemm_wgrad(dy, x, (co, cin, 5, 5), dst=slot) is None
+    tol = 1e-2 if dt == torch.float32 else 6e-2
+    torch.testing.assert_close(slot.float(), before + want, rtol=tol, atol=tol)

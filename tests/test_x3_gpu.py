@@ -336,3 +336,27 @@ def test_x3_block_fast_form_captures_into_a_graph(cuda, block):
     g.replay()
     torch.cuda.synchronize()
     assert _rel(x0.grad, eager_dx / 2) < 0.1  # eager_dx summed two warm-up steps (flips: see _grads_agree)
+
+
+def test_x3_weight_planes_batched_refresh_matches_per_weight_split(cuda):
+    """ops/wt_cache.py X3Weights: one tony_x3_weights_batch launch re-splits every registered fp32 conv
+    weight into both x3 layouts -- bit-identical to the per-weight split kernels (split_weight /
+    split_weight_t) -- after the weights change, including the 3-channel stem (cp padding) and channel
+    counts that are not tile multiples."""
+    from tony_amd.ops import wt_cache, x3
+
+    shapes = [(32, 3, 3, 3), (64, 80, 3, 3), (192, 160, 7, 1), (448, 2048, 1, 1), (96, 48, 5, 5)]
+    ws = [torch.nn.Parameter(torch.randn(s, device=cuda).contiguous(memory_format=torch.channels_last))
+          for s in shapes]
+    c = wt_cache.X3Weights(cuda)
+    c.enabled = True
+    for w in ws:
+        assert c.planes(w) is not None and c.planes_t(w) is not None
+    with torch.no_grad():
+        for w in ws:
+            w.mul_(-1.7).add_(0.25)  # the optimizer step
+    c.refresh()
+    torch.cuda.synchronize()
+    for w in ws:
+        assert torch.equal(c.planes(w), x3.split_weight(w)), tuple(w.shape)
+        assert torch.equal(c.planes_t(w), x3.split_weight_t(w)), tuple(w.shape)

@@ -99,6 +99,7 @@ _SIGNATURES = {
     "tony_gemm_tn_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64,
                           c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p],
     "tony_splitk_reduce": [c_void_p, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_void_p],
+    "tony_splitk_workspace": [c_void_p, c_int64, c_void_p, c_int64],
     "tony_conv_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int,
                       c_int, c_int, c_void_p, c_int, c_int, c_int64, c_int, c_void_p, c_int64, c_void_p],
     "tony_stem_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
@@ -133,6 +134,8 @@ _SIGNATURES = {
     "tony_avgpool_fwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
     "tony_avgpool_bwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
     "tony_transpose_desc_bytes": [],
+    "tony_x3_desc_bytes": [],
+    "tony_x3_weights_batch": [c_void_p, c_int, c_int, c_void_p],
     "tony_transpose_batch": [c_void_p, c_int, c_int, c_void_p],
     # cross-stream forks / joins of the eager step (csrc/streams.hip, ops/streams.py)
     "tony_event_pool": [c_int, c_u64_p],
@@ -235,6 +238,14 @@ class _SignedLib:
                 for name, w in fastcall.bind_all(_tony_fastcall, h, _SIGNATURES).items():
                     setattr(self, name, w)
                     self.fastcall += 1
+        # the NT conv / GEMM entry points take a stream-K grid in flags bits 16..19: give those launches
+        # their workspace (csrc/igemm.h SplitK) wherever they are made from
+        set_ws = self.__dict__.get("tony_splitk_workspace")
+        if set_ws is not None:
+            for name, fpos in _SPLITK_ENTRIES.items():
+                fn = self.__dict__.get(name)
+                if fn is not None:
+                    setattr(self, name, _splitk_entry(fn, set_ws, fpos))
 
     def __getattr__(self, name):
         raise KernelError(f"{name}: not exported by {SO_PATH} or missing from _lib._SIGNATURES")
@@ -242,6 +253,39 @@ class _SignedLib:
 
 class KernelError(RuntimeError):
     pass
+
+
+# entry point -> position of its flags argument (bits 16..19: stream-K grid in CUs, csrc/igemm.h SplitK)
+_SPLITK_ENTRIES = {"tony_gemm_bf16": 9, "tony_conv_fwd": 18, "tony_conv_dgrad": 16}
+SPLITK_MAX_TILES = 4096  # csrc/igemm.h kStreamMaxTiles: counters of a stream-K launch
+
+
+def splitk_slab_floats(m: int, cus: int) -> int:
+    """Partial tiles of a stream-K launch over m x cus workgroups: 2 per workgroup, each at most the
+    largest LDS-DMA tile (256 x 192)."""
+    return 2 * m * cus * 256 * 192
+
+
+def _splitk_entry(fn, set_ws, fpos: int):
+    def call(*a):
+        s = (a[fpos] >> 16) & 15
+        if not s:
+            return fn(*a)
+        from .arena import zeros_f32
+
+        dev = torch.device("cuda", torch.cuda.current_device())
+        # on the launch's (current) stream: the caching allocator keeps the slab for that stream's later work
+        slab = torch.empty(splitk_slab_floats(s, num_cus(dev)), dtype=torch.float32, device=dev)
+        cnt = zeros_f32(2 * SPLITK_MAX_TILES, dev)  # ticket + done counters per tile (zero bits = zero uint32)
+        check(set_ws(slab.data_ptr(), slab.numel(), cnt.data_ptr(), cnt.numel()), "tony_splitk_workspace")
+        try:
+            return fn(*a)
+        finally:
+            set_ws(0, 0, 0, 0)
+
+    call.__name__ = getattr(fn, "__name__", "splitk_entry")
+    call.__wrapped__ = fn
+    return call
 
 
 # BatchNorm statistics are accumulated into STAT_SHARDS copies (csrc/common.h kStatShards): a

@@ -432,9 +432,12 @@ def _gemm_fwd(x, weight, stats=None):
     _lib.check_stat_buffer(stats, co)
     wk = _krsc(weight).reshape(co, k)
     y = _cl_empty(n, co, 1, 1, x.device)
+    # tuned like every other GEMM: with only n = batch rows (one tile row) the tile variant and the
+    # stream-K forms (the K = R*S*C reduction spread over the CUs) decide whether 6 or 256 CUs work
+    vf = tune.gemm_flags(x, wk, y, n, co, k, k, stats is not None, tune.SMALL_GEMM_VARIANTS)
     rc = _lib.lib().tony_gemm_bf16(x.data_ptr(), wk.data_ptr(), y.data_ptr(), n, co, k, k, k, co,
-                                   1 if stats is not None else 0, _lib.ptr(stats), 2 * co if stats is not None else 0,
-                                   _lib.stream_ptr(x.device))
+                                   (1 if stats is not None else 0) | vf, _lib.ptr(stats),
+                                   2 * co if stats is not None else 0, _lib.stream_ptr(x.device))
     _lib.check(rc, "tony_gemm_bf16 (whole-input conv)")
     return y
 
@@ -446,18 +449,42 @@ def _gemm_dgrad(dy, weight, x_shape):
     k = c * h * w
     wt = _krsc(weight).reshape(co, k).t().contiguous()  # [(r, s, c)][co]
     dx = _cl_empty(n, c, h, w, dy.device)
-    rc = _lib.lib().tony_gemm_bf16(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), n, k, co, lddy, co, k, 0, 0, 0,
+    if lddy != co:
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        lddy = co
+    vf = tune.gemm_flags(dy, wt, dx, n, k, co, lddy, False, tune.SMALL_GEMM_VARIANTS)
+    rc = _lib.lib().tony_gemm_bf16(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), n, k, co, lddy, co, k, vf, 0, 0,
                                    _lib.stream_ptr(dy.device))
     _lib.check(rc, "tony_gemm_bf16 (whole-input conv dgrad)")
     return dx
 
 
 def _gemm_wgrad(dy, x, weight_shape, dst=None):
-    """dW[co, (r, s, c)] = dY^T X (split-K TN GEMM), added into ``dst`` or returned [Co, C, R, S]."""
+    """dW[co, (r, s, c)] = dY^T X, added into ``dst`` or returned [Co, C, R, S].  The reduction is over
+    the batch only (n = 128 rows) and the output is large (Co x R*S*C): an NT GEMM over the transposed
+    operands (dW = dY^T . (X^T)^T, K = n) writes each dW element once from one workgroup -- no split-K
+    slab, no combine launch -- into the gradient slot directly (epilogue accumulate, fp32 or bf16)."""
     dy, (_, co, lddy) = _as_rows(dy)
     x = _dense_rows(x)
     n = x.shape[0]
     k = x[0].numel()
+    if n % 8 == 0 and (dst is None or dst.dtype in (torch.float32, _BF16)):
+        dev = x.device
+        dyt = torch.as_strided(dy, (co, n), (1, lddy)).contiguous()         # [co][n]
+        xt = x.permute(0, 2, 3, 1).reshape(n, k).t().contiguous()           # [(r, s, c)][n] (NHWC memory)
+        out = dst if dst is not None else torch.empty(co * k, dtype=torch.float32, device=dev)
+        base = (8 if out.dtype == torch.float32 else 0) | (16 if dst is not None else 0)
+        scratch = torch.empty(co * k, dtype=_BF16, device=dev)  # the tuner's timing runs write here
+        vf = tune.gemm_flags(dyt, xt, scratch, co, k, n, n, False, tune.SMALL_GEMM_VARIANTS)
+        L, st = _lib.lib(), _lib.stream_ptr(dev)
+        rc = L.tony_gemm_bf16(dyt.data_ptr(), xt.data_ptr(), out.data_ptr(), co, k, n, n, n, k, base | vf, 0, 0, st)
+        if rc == -3:  # the tuned variant has no fp32 / accumulating epilogue: the default one has both
+            rc = L.tony_gemm_bf16(dyt.data_ptr(), xt.data_ptr(), out.data_ptr(), co, k, n, n, n, k, base, 0, 0, st)
+        _lib.check(rc, "tony_gemm_bf16 (whole-input conv wgrad)")
+        if dst is not None:
+            return None
+        _, c, r, s = weight_shape
+        return out.view(co, r, s, c).permute(0, 3, 1, 2)
     out = wgrad_tn(dy.data_ptr(), lddy, x.data_ptr(), k, n, co, k, x.device, dst=dst)
     if out is None:
         return None

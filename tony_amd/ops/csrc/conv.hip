@@ -781,11 +781,14 @@ int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int6
   if ((epi & 16) && ((epi & 3) || bph.bnr.z != nullptr)) return -1;
   float* st = stats;
   const int v = (flags >> 8) & 0xff;
+  if (((flags >> 16) & 15) && !(v >= kGldsFirst && v < kGldsFirst + kNumGlds)) return -3;  // stream-K: LDS-DMA only
   if (((epi & 24) && v == kHaloVariant) || ((epi & 16) && v == kDirectVariant)) return -3;
   if (v == kHaloVariant) return bph.bnr.z != nullptr ? -3 : run_halo(g, B, C, ldc, N, epi, st, sstride, stream);
   if (v == kDirectVariant) return run_direct(g, B, C, ldc, N, epi, st, sstride, stream, bph.bnr);
   if (v >= kGldsFirst && v < kGldsFirst + kNumGlds)
-    return bph.bnr.z != nullptr ? -3 : run_glds(g, B, g.K, C, ldc, M, N, epi, st, sstride, v, stream);
+    return bph.bnr.z != nullptr ? -3
+                                : run_glds(g, B, g.K, C, ldc, M, N, epi, st, sstride, v, stream, RowMap{}, BTaps{},
+                                           (flags >> 16) & 15);
   if (v >= kNumNtVariants) return -1;
   if (v == 0) {
     const int64_t bn = pick_bn(N, 192);
@@ -1500,6 +1503,24 @@ bool bad_geom(int C, int64_t ld, const void* p) {
 
 }  // namespace
 
+namespace tony {
+SplitWs& splitk_ws() {
+  static thread_local SplitWs ws;
+  return ws;
+}
+}  // namespace tony
+
+// The stream-K workspace of this host thread's next LDS-DMA conv / GEMM launches (flags bits 16..19 =
+// m of tony_conv_fwd / tony_conv_dgrad / tony_gemm_bf16: a grid of m x CUs workgroups): slab_floats
+// fp32 for the partial tiles (2 per workgroup) and ncnt uint32 per-tile arrival counters, zero on
+// first use (each launch's last arrivers re-arm theirs).  Kernels that may run at the same time
+// (other streams) must not share one workspace.  All zero: none (stream-K launches then run plain).
+TONY_API int tony_splitk_workspace(float* slab, int64_t slab_floats, unsigned* cnt, int64_t ncnt) {
+  if (slab_floats < 0 || ncnt < 0 || (reinterpret_cast<uintptr_t>(slab) & 15)) return -1;
+  tony::splitk_ws() = tony::SplitWs{slab, slab_floats, cnt, ncnt};
+  return 0;
+}
+
 // Y[N*OH*OW, Co] (row stride ldy) = conv(X [N,H,W,C] pixel stride ldx, W [Co][R][S][C]).
 // flags bit0: per-channel sum / sum-of-squares of Y into stats[2*Co] (zero on entry; kStatShards
 // copies sstride floats apart when sstride > 0); bits 8..15: tile variant (run_nt).
@@ -1535,7 +1556,7 @@ TONY_API int tony_conv_dgrad(const void* dy, int N, int OH, int OW, int Co, int6
       bph.bnr = *bnr;
     }
   }
-  const int fl = flags & 0xff18;  // variant + fp32 output (bit3) + accumulate into dx (bit4)
+  const int fl = flags & 0xfff18;  // variant + stream-K (bits 16..19) + fp32 output (bit3) + accumulate (bit4)
   if ((fl & 16) && bph.bnr.z != nullptr) return -1;
   const int rc = run_nt(g, wt, dx, lddx, M, C, fl, nullptr, 0, stream, bph);
   if (rc == -3 && bph.bnr.z != nullptr)  // the chosen variant has no fused reduction: plain dgrad
@@ -1573,6 +1594,7 @@ TONY_API int tony_conv_dgrad_strided(const void* dy, int N, int OH, int OW, int 
   const int v = (flags >> 8) & 0xff;
   const int acc = flags & 16;
   if (acc && br.z != nullptr) return -1;
+  if ((flags >> 16) & 15) return -3;  // no stream-K for the residue classes
   for (int py = 0; py < sh; ++py) {
     for (int px = 0; px < sw; ++px) {
       const int QH = H > py ? (H - py + sh - 1) / sh : 0, QW = W > px ? (W - px + sw - 1) / sw : 0;

@@ -173,7 +173,8 @@ int launch_bm(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, i
 // inference BN), bit2: ReLU after it; bit4: C += the product; bit5: C = the product + S masked by
 // Mk, with S = stats read as a bf16 [M, ldc] matrix and Mk = sstride read as the address of its ReLU
 // byte mask [M, ldc / 8] (ops/residual.py MaskedGrad: a residual tail's d(identity), never
-// materialised); bits 8..15: tile variant (kNtVariants, mfma_common.h).
+// materialised); bits 8..15: tile variant (kNtVariants, mfma_common.h); bits 16..19: stream-K grid in CUs (LDS-DMA
+// variants, igemm.h SplitK; tony_splitk_workspace).
 TONY_API int tony_gemm_bf16(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
                             int64_t ldb, int64_t ldc, int flags, float* stats, int64_t sstride, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || sstride < 0) return -1;
@@ -191,8 +192,10 @@ TONY_API int tony_gemm_bf16(const void* A, const void* B, void* C, int64_t M, in
   if ((epi & 3) && stats == nullptr) return -1;
   float* st = stats;
   const int v = (flags >> 8) & 0xff;
+  if (((flags >> 16) & 15) && !(v >= kGldsFirst && v < kGldsFirst + kNumGlds)) return -3;  // stream-K: LDS-DMA only
   if (v >= kGldsFirst && v < kGldsFirst + kNumGlds)  // LDS-DMA kernel on A as a 1x1 "conv" (igemm.h)
-    return run_glds(gemm_gather(A, lda, M, K), B, ldb, C, ldc, M, N, epi, st, sstride, v, stream);
+    return run_glds(gemm_gather(A, lda, M, K), B, ldb, C, ldc, M, N, epi, st, sstride, v, stream, RowMap{}, BTaps{},
+                    (flags >> 16) & 15);
   if (v >= kNumNtVariants) return -1;
   if (v == 0) {
     if (N <= 64) return launch<256, 64>(A, lda, B, ldb, C, ldc, M, N, K, st, sstride, epi, stream);

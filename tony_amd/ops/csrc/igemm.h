@@ -13,10 +13,33 @@
 
 #include "mfma_common.h"
 
+namespace tony {
+// Split-K workspace of the next LDS-DMA NT launches made by this host thread (tony_splitk_workspace,
+// conv.hip): the fp32 partial tiles and one arrival counter per output tile (zero on first use; the
+// last arriver re-arms it).  A launch that asks for splits without a big enough workspace runs unsplit.
+struct SplitWs {
+  float* slab = nullptr;
+  int64_t slab_floats = 0;
+  unsigned* cnt = nullptr;
+  int64_t ncnt = 0;
+};
+SplitWs& splitk_ws();
+}  // namespace tony
+
 namespace {
 
 using namespace tony;
 using namespace tony::mfma;
+
+// stream-K of conv_glds_kernel (see the kernel): workgroups own equal ranges of the (tile, K-step)
+// iterations; the contributors of a tile shared by several workgroups fold their fp32 partials
+// through the slab, the last arriver (per-tile ticket) summing them in K order
+struct SplitK {
+  float* slab = nullptr;    // 2 partial tiles per workgroup
+  unsigned* cnt = nullptr;  // per tile: a ticket counter, then (ntiles further) a done counter
+  int ntiles = 0;
+  int stream = 0;
+};
 
 struct Gather {
   const uint16_t* src;  // source image, pixel-major: pixel p at src + p * ld
@@ -163,7 +186,7 @@ template <int BM, int BN, int ST, int KB, bool UNI, int NWM = 2, bool IL = false
 __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const uint16_t* __restrict__ B, int64_t ldb,
                                                              uint16_t* __restrict__ C, int64_t ldc, int M, int N,
                                                              float* __restrict__ stats, int64_t sstride, int epi,
-                                                             int tiles_n, RowMap rmap, BTaps bt) {
+                                                             int tiles_n, RowMap rmap, BTaps bt, SplitK sk) {
   constexpr int NW = 2 * NWM;                 // waves: NWM along M x 2 along N
   constexpr int WM = BM / NWM, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int CPR = KB / 8;                // 16-B chunks per LDS row
@@ -176,12 +199,32 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
   static_assert(BM * (BN + 8) <= ST * STAGE, "the epilogue's C tile fits in the ring");
   __shared__ __attribute__((aligned(16))) uint16_t smem[ST * STAGE];
 
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = wg / tiles_n, tn = wg % tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int K = g.K;
+  // (>= 1: a strided dgrad's tap-less residue class has K = 0 and must still write its zero tile)
+  const int nk_all = max(1, (K + KB - 1) / KB);
+  // Work: the (tile, K-step) iterations.  Plain: workgroup w = one whole tile.  Stream-K (sk.stream):
+  // the tiles x nk_all iterations cut into gridDim.x equal contiguous ranges, one per workgroup (the
+  // grid sized to what the CUs hold at once, so the last tiles do not run as a near-empty second
+  // wave); a workgroup walks its range tile segment by tile segment.  A segment that is a whole tile
+  // runs the epilogue itself; the segments of a shared tile meet in SplitK's fold.  Neighbouring
+  // ranges share a tile, so the remap keeps them on one XCD.
+  const int G = gridDim.x;
+  const int w = xcd_remap(blockIdx.x, G);
+  const int64_t T = static_cast<int64_t>(tiles_n) * ((M + BM - 1) / BM) * nk_all;
+  int64_t it = sk.stream ? static_cast<int64_t>(w) * T / G : static_cast<int64_t>(w) * nk_all;
+  const int64_t it_end = sk.stream ? static_cast<int64_t>(w + 1) * T / G : it + nk_all;
+  for (bool first_seg = true; it < it_end; first_seg = false) {
+  if (!first_seg) __syncthreads();  // the previous segment's epilogue is done with the LDS
+  const int tile = static_cast<int>(it / nk_all);
+  const int kt0 = static_cast<int>(it - static_cast<int64_t>(tile) * nk_all);
+  const int nk = static_cast<int>(min(static_cast<int64_t>(nk_all - kt0), it_end - it));
+  it += nk;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kstart = kt0 * KB;
+  const int kend = min(K, (kt0 + nk) * KB);
   const int rin = lane / CPR;                     // row within the instruction's row group
   const int ck = (lane % CPR) ^ gswz<KB>(rin);    // logical K chunk this lane fetches (row groups are
                                                   // RPI-aligned, so swz(row) == swz(rin))
@@ -213,8 +256,8 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
     brow[i] = B + static_cast<int64_t>(bok[i] ? n : 0) * ldb;
   }
   TapPos tp;
-  tp.init(ck * 8, g);
-  int kb = ck * 8;  // this thread's K column of the next stage to issue
+  tp.init(ck * 8 + kstart, g);
+  int kb = ck * 8 + kstart;  // this thread's K column of the next stage to issue
   const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(smem));
   constexpr uint32_t kGroupB = RPI * KB * 2;  // bytes per row group
   constexpr uint32_t kStageB = STAGE * 2, kBOff = BM * KB * 2;
@@ -261,21 +304,41 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
       bp[i] = bok[i] ? brow[i] + ck * 8 : zc;
       binc[i] = bok[i] ? KB : 0;
     }
-    set_tap();
+    if (kstart == 0) {
+      set_tap();
+    } else {  // a later split: start at tap (ur, us), channel c0 of it (KB-aligned: Cs % KB == 0)
+      const int tap = kstart / g.Cs, c0 = kstart - tap * g.Cs;
+      ur = tap / g.S;
+      us = tap - ur * g.S;
+      if (bt.S == 0) {
+#pragma unroll
+        for (int i = 0; i < BI; ++i) bp[i] += binc[i] / KB * kstart;  // the filter row is contiguous over K
+      }
+      set_tap();
+      const int steps = c0 / KB;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) ap[i] += ainc[i] * steps;
+      if (bt.S != 0) {
+#pragma unroll
+        for (int i = 0; i < BI; ++i) bp[i] += binc[i] * steps;
+      }
+      uleft -= steps;
+    }
   }
+  int left = nk;  // real stages still to issue; the ring's tail past them fetches zeros
 
   // UNI: piece p < AI + BI of a stage's DMAs (A rows first), then the per-stage pointer / tap advance
-  auto issue_piece = [&](uint32_t st0, int p) {
+  auto issue_piece = [&](uint32_t st0, int p, bool live) {
 #pragma unroll
     for (int i = 0; i < AI; ++i)
       if (p == i) {
-        glds16(ap[i], st0 + aoff[i]);
+        glds16(live ? ap[i] : zc, st0 + aoff[i]);
         ap[i] += ainc[i];
       }
 #pragma unroll
     for (int i = 0; i < BI; ++i)
       if (p == AI + i) {
-        glds16(bp[i], st0 + boff[i]);
+        glds16(live ? bp[i] : zc, st0 + boff[i]);
         bp[i] += binc[i];
       }
   };
@@ -290,15 +353,16 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
   };
   auto issue = [&](int slot) {
     const uint32_t st0 = base + slot * kStageB;
+    const bool live = left-- > 0;
     if constexpr (UNI) {
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
-        glds16(ap[i], st0 + aoff[i]);
+        glds16(live ? ap[i] : zc, st0 + aoff[i]);
         ap[i] += ainc[i];
       }
 #pragma unroll
       for (int i = 0; i < BI; ++i) {
-        glds16(bp[i], st0 + boff[i]);
+        glds16(live ? bp[i] : zc, st0 + boff[i]);
         bp[i] += binc[i];
       }
       if (--uleft == 0) {
@@ -315,14 +379,14 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const int iy = rs[i].iy0 + g.sign * tp.r, ix = rs[i].ix0 + g.sign * tp.s;
-      const bool ok = rs[i].ok & (tp.r < g.R) & (static_cast<unsigned>(iy) < static_cast<unsigned>(g.Hs)) &
+      const bool ok = live & rs[i].ok & (tp.r < g.R) & (static_cast<unsigned>(iy) < static_cast<unsigned>(g.Hs)) &
                       (static_cast<unsigned>(ix) < static_cast<unsigned>(g.Ws));
       const uint16_t* src = rs[i].base + toff;
       glds16(ok ? static_cast<const void*>(src) : z, st0 + aoff[i]);
     }
-    const bool kok = kb < K;
+    const bool kok = live & (kb < kend);
 #pragma unroll
-    for (int i = 0; i < BI; ++i) glds16(kok & bok[i] ? static_cast<const void*>(brow[i] + kb) : z, st0 + boff[i]);
+    for (int i = 0; i < BI; ++i) glds16((kok & bok[i]) ? static_cast<const void*>(brow[i] + kb) : z, st0 + boff[i]);
     tp.advance(KB, g);
     kb += KB;
   };
@@ -333,7 +397,6 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (K + KB - 1) / KB;
 #pragma unroll
   for (int s = 0; s < ST - 1; ++s) issue(s);
   int slot = 0;
@@ -360,6 +423,7 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
           af[kk][i] = *reinterpret_cast<const bf16x8_t*>(As + goff<KB>(wm * WM + i * 16 + (lane & 15), ch));
       }
       int p = 0;
+      const bool live = left-- > 0;
 #pragma unroll
       for (int kk = 0; kk < KSUB; ++kk)
 #pragma unroll
@@ -373,7 +437,7 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
           const int pe = (g0 + 1) * NP / G;
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (; p < pe; ++p) issue_piece(st0, p);
+          for (; p < pe; ++p) issue_piece(st0, p, live);
           __builtin_amdgcn_sched_barrier(0);
         }
       issue_advance();
@@ -400,18 +464,109 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's zero fills land before LDS is reused
   __syncthreads();
+  if (nk != nk_all) {
+    // a shared tile: take the tile's ticket first.  Every contributor but the last stores its fp32
+    // partial to its slot (part 0: the workgroup's first segment, 1: its last) and counts itself done;
+    // the last waits for the others' done count -- they hold tickets, so they are past their K loops
+    // and only storing: the wait is bounded by construction -- then sums the contributors in K order,
+    // its own accumulators in their place (the same sum whichever contributor is last), and runs the
+    // epilogue.  Hand-off with write-through (sc1) 16-B buffer stores and sc1 loads (MI355X guide,
+    // in-launch split-K reduction, sc1 form): no agent release -- a `buffer_wbl2` per workgroup writes
+    // back the XCD L2's dirty lines (measured: the fold with release / acquire fences doubled a 17x17
+    // conv) -- and no acquire.  Every storing wave drains its stores before the barrier that precedes
+    // lane 0's done add; the reducer's waves load after the barrier that follows its poll.
+    constexpr int NT = 128 * NWM, FR = TM * TN;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(sk.slab, 0, 0x7fffffff, 0x00020000);
+    const int64_t t0 = static_cast<int64_t>(tile) * nk_all;
+    const int w_first = static_cast<int>(((t0 + 1) * G - 1) / T);  // the workgroups holding the tile's
+    const int w_last = static_cast<int>(((t0 + nk_all) * G - 1) / T);  // first / last iteration
+    const unsigned others = static_cast<unsigned>(w_last - w_first);
+    unsigned* cnt = sk.cnt + tile;
+    unsigned* done = sk.cnt + sk.ntiles + tile;
+    int* flag = reinterpret_cast<int*>(smem);
+    if (threadIdx.x == 0)
+      *flag = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == others;
+    __syncthreads();
+    const bool last = *flag != 0;
+    __syncthreads();  // every wave has read the flag before the epilogue stages C over it
+    if (!last) {
+      const int mine = (2 * w + (first_seg ? 0 : 1)) * FR;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), prs,
+                                                 ((mine + i * TN + j) * NT + threadIdx.x) * 16, 0, 16);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      continue;
+    }
+    if (threadIdx.x == 0) {
+      for (unsigned spins = 0; __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < others &&
+                               spins < (1u << 24);
+           ++spins)
+        __builtin_amdgcn_s_sleep(1);
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next launch
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the poll
+    f32x4 own[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        own[i][j] = acc[i][j];
+        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    for (int c = w_first; c <= w_last; ++c) {
+      if (c == w) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] += own[i][j];
+        continue;
+      }
+      // contributor c holds this tile in its first segment iff its range starts inside the tile
+      const int slot_c = (2 * c + ((static_cast<int64_t>(c) * T / G) >= t0 ? 0 : 1)) * FR;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     prs, ((slot_c + i * TN + j) * NT + threadIdx.x) * 16, 0, 16));
+    }
+  }
   const bool am = (epi & 32) != 0;  // masked-source accumulate (tony_gemm_bf16 flags bit5)
   nt_epilogue<BM, BN, TM, TN, ST * STAGE, NWM>(acc, smem, C, ldc, M, N, m0, n0,
                                            (epi & 1) ? stats + shard_off(tm, sstride) : nullptr,
                                            (epi & 2) ? stats : nullptr, (epi & 4) != 0, rmap, (epi & 8) != 0,
                                            (epi & 48) != 0, am ? reinterpret_cast<const uint16_t*>(stats) : nullptr,
                                            am ? reinterpret_cast<const uint8_t*>(sstride) : nullptr);
+  }
+}
+
+constexpr int64_t kStreamMaxTiles = 4096;  // counters of a stream-K launch's workspace (ops/_lib.py)
+inline int num_cus_of_current() {
+  static int cached[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 256;
+  if (cached[dev] == 0) {
+    int n = 0;
+    cached[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+  }
+  return cached[dev];
 }
 
 // B rows n = [K] at row stride ldb (the conv weights [Co][R][S][Ci]: ldb = K)
+// stream_m > 0: stream-K over stream_m x (CUs) workgroups (SplitK above) when this thread's workspace
+// (tony_splitk_workspace) holds 2 partial tiles per workgroup and a counter per tile, else the plain
+// launch (same result)
 inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N, int epi,
                     float* st, int64_t sstride, int v, hipStream_t stream, RowMap rmap = RowMap{},
-                    BTaps bt = BTaps{}) {
+                    BTaps bt = BTaps{}, int stream_m = 0) {
   if ((ldc % 8) || (ldb % 8) || (reinterpret_cast<uintptr_t>(C) & 15) || (reinterpret_cast<uintptr_t>(B) & 15) ||
       (reinterpret_cast<uintptr_t>(g.src) & 15) || (g.ld % 8) || (g.K % 8) || v < kGldsFirst || v >= kGldsFirst + kNumGlds)
     return -3;
@@ -429,14 +584,34 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
       const int tiles_m = ceil_div(M, BM), tiles_n = ceil_div(N, BN);
       const int64_t tiles = static_cast<int64_t>(tiles_m) * tiles_n;
       if (tiles > 0x7fffffff) return -2;
+      SplitK sk{};
+      int grid = static_cast<int>(tiles);
+      if (stream_m > 0) {
+        // worth it while the tiles leave CUs idle or a near-empty last wave: a few tiles per CU at most
+        const int cus = num_cus_of_current();
+        const int64_t iters = tiles * ((g.K + KB - 1) / KB);
+        int64_t G = static_cast<int64_t>(stream_m) * cus;
+        G = std::min<int64_t>(G, iters / 4);  // >= 4 K-steps per workgroup
+        if (tiles > 4 * G || tiles > kStreamMaxTiles || G < 2 || tiles % G == 0) return -3;
+        const SplitWs& ws = splitk_ws();
+        if (ws.slab != nullptr && ws.cnt != nullptr && ws.ncnt >= 2 * tiles &&
+            ws.slab_floats >= 2 * G * BM * BN) {
+          sk.slab = ws.slab;
+          sk.cnt = ws.cnt;
+          sk.ntiles = static_cast<int>(tiles);
+          sk.stream = 1;
+          grid = static_cast<int>(G);
+        }
+      }
       const auto args = std::make_tuple(g, static_cast<const uint16_t*>(B), ldb, static_cast<uint16_t*>(C), ldc,
-                                        static_cast<int>(M), static_cast<int>(N), st, sstride, epi, tiles_n, rmap, bt);
+                                        static_cast<int>(M), static_cast<int>(N), st, sstride, epi, tiles_n, rmap, bt,
+                                        sk);
       if (g.Cs % KB == 0 && glds_uni_enabled())
-        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true, NWM, IL><<<static_cast<int>(tiles), 128 * NWM, 0, stream>>>(a...); }, args);
+        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true, NWM, IL><<<grid, 128 * NWM, 0, stream>>>(a...); }, args);
       else if (IL || bt.S != 0)
         return -3;  // the interleaved form and the class taps exist for the uniform-tap loop only
       else
-        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, false, NWM><<<static_cast<int>(tiles), 128 * NWM, 0, stream>>>(a...); }, args);
+        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, false, NWM><<<grid, 128 * NWM, 0, stream>>>(a...); }, args);
       TONY_LAUNCH_CHECK();
       return 0;
     }

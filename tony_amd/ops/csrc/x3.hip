@@ -77,6 +77,80 @@ __global__ __launch_bounds__(kThreads) void wt_split3_kernel(const float* __rest
   }
 }
 
+// Both x3 weight layouts of every conv of a model in ONE launch after the optimizer step (ops/wt_cache.py
+// X3Weights): the forward planes [Co][RS][3cp] ([hi | hi | lo] over the cp channels, zero past C) and the
+// backward-data planes [C][RS][3Co] ([hi | hi | lo] over Co) of the fp32 weight [Co][RS][C] -- instead of
+// two split launches per conv per step on the critical path (~190 per Inception-v3 step).  One workgroup
+// per 64 (co) x 64 (c) tile of one tap, staged through LDS as fp32 (row padded by one float: the column
+// reads of the transposed store are conflict free).
+struct XDesc {
+  const float* src;  // [Co][RS][C]
+  uint16_t* fwd;     // [Co][RS][3cp]
+  uint16_t* bwd;     // [C][RS][3Co]
+  int co, rs, c, cp;
+  int tiles_c, tiles_co;
+  int tile_begin;
+  int pad;
+};
+
+constexpr int XT = 64;
+
+__global__ __launch_bounds__(kThreads) void x3_weights_batch_kernel(const XDesc* __restrict__ descs, int n) {
+  __shared__ float tile[XT][XT + 1];
+  const int b = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (descs[mid].tile_begin <= b) lo = mid; else hi = mid - 1;
+  }
+  const XDesc d = descs[lo];
+  int t = b - d.tile_begin;
+  const int tc = t % d.tiles_c;
+  t /= d.tiles_c;
+  const int tco = t % d.tiles_co;
+  const int tap = t / d.tiles_co;
+  const int co0 = tco * XT, c0 = tc * XT;
+  // load 64 (co) x 64 (c) fp32; channels past C (the cp padding) read as zero
+  for (int v = threadIdx.x; v < XT * (XT / 4); v += kThreads) {
+    const int r = v >> 4, c4 = (v & 15) * 4;
+    const int co = co0 + r, c = c0 + c4;
+    const float* p = d.src + (static_cast<int64_t>(co) * d.rs + tap) * d.c + c;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tile[r][c4 + e] = (co < d.co && c + e < d.c) ? p[e] : 0.f;
+  }
+  __syncthreads();
+  // forward planes: row (co, tap), columns c .. c + 3 of each plane
+  for (int v = threadIdx.x; v < XT * (XT / 4); v += kThreads) {
+    const int r = v >> 4, c4 = (v & 15) * 4;
+    const int co = co0 + r, c = c0 + c4;
+    if (co >= d.co || c >= d.cp) continue;
+    uint16_t h[4], l[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split1(tile[r][c4 + e], h[e], l[e]);
+    const uint2 H = make_uint2(h[0] | (static_cast<uint32_t>(h[1]) << 16), h[2] | (static_cast<uint32_t>(h[3]) << 16));
+    const uint2 L = make_uint2(l[0] | (static_cast<uint32_t>(l[1]) << 16), l[2] | (static_cast<uint32_t>(l[3]) << 16));
+    uint16_t* q = d.fwd + (static_cast<int64_t>(co) * d.rs + tap) * (3 * d.cp) + c;
+    *reinterpret_cast<uint2*>(q) = H;
+    *reinterpret_cast<uint2*>(q + d.cp) = H;
+    *reinterpret_cast<uint2*>(q + 2 * d.cp) = L;
+  }
+  // backward-data planes: row (c, tap), columns co .. co + 3 of each plane
+  for (int v = threadIdx.x; v < XT * (XT / 4); v += kThreads) {
+    const int r = v >> 4, o4 = (v & 15) * 4;
+    const int c = c0 + r, co = co0 + o4;
+    if (c >= d.c || co >= d.co) continue;
+    uint16_t h[4], l[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split1(tile[o4 + e][r], h[e], l[e]);
+    const uint2 H = make_uint2(h[0] | (static_cast<uint32_t>(h[1]) << 16), h[2] | (static_cast<uint32_t>(h[3]) << 16));
+    const uint2 L = make_uint2(l[0] | (static_cast<uint32_t>(l[1]) << 16), l[2] | (static_cast<uint32_t>(l[3]) << 16));
+    uint16_t* q = d.bwd + (static_cast<int64_t>(c) * d.rs + tap) * (3 * d.co) + co;
+    *reinterpret_cast<uint2*>(q) = H;
+    *reinterpret_cast<uint2*>(q + d.co) = H;
+    *reinterpret_cast<uint2*>(q + 2 * d.co) = L;
+  }
+}
+
 int grid_for(int64_t work) {
   int64_t g = (work + kThreads - 1) / kThreads;
   if (g > 8192) g = 8192;
@@ -102,6 +176,18 @@ TONY_API int tony_x3_weights_t(const void* w, int Co, int RS, int C, void* dst, 
   if (w == nullptr || dst == nullptr || Co <= 0 || RS <= 0 || C <= 0 || (Co % 8)) return -1;
   wt_split3_kernel<<<grid_for(static_cast<int64_t>(C) * RS * Co), kThreads, 0, stream>>>(
       static_cast<const float*>(w), Co, RS, C, static_cast<uint16_t*>(dst));
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// Size in bytes of one x3 weight descriptor (ops/wt_cache.py packs the work list to match).
+TONY_API int tony_x3_desc_bytes() { return static_cast<int>(sizeof(XDesc)); }
+
+// descs: device array of n XDesc (tile_begin ascending, Co % 4 == 0 and cp % 8 == 0 for the vector stores);
+// total_tiles = sum over descriptors of rs * tiles_c * tiles_co.
+TONY_API int tony_x3_weights_batch(const void* descs, int n, int total_tiles, hipStream_t stream) {
+  if (n <= 0 || total_tiles <= 0 || descs == nullptr) return -1;
+  x3_weights_batch_kernel<<<total_tiles, kThreads, 0, stream>>>(static_cast<const XDesc*>(descs), n);
   TONY_LAUNCH_CHECK();
   return 0;
 }

@@ -23,7 +23,25 @@ AUTOTUNE = os.environ.get("TONY_CONV_AUTOTUNE", "1") != "0"
 # the search, TONY_CONV_GLDS8=0 the 8-wave and interleaved ones, TONY_CONV_GLDS_IL=0 the interleaved)
 _N_GLDS = (25 if os.environ.get("TONY_CONV_GLDS_IL", "1") != "0" else 20) \
     if os.environ.get("TONY_CONV_GLDS8", "1") != "0" else 16
-NT_VARIANTS = tuple(range(_N_GLDS if os.environ.get("TONY_CONV_GLDS", "1") != "0" else 11))
+_BASE = tuple(range(_N_GLDS if os.environ.get("TONY_CONV_GLDS", "1") != "0" else 11))
+# + stream-K forms of the LDS-DMA variants (csrc/igemm.h SplitK): candidate v + 256 * m, i.e. flags bits
+# 16..19 = m, a grid of m x CUs workgroups sharing the (tile, K-step) iterations.  Only launches whose
+# tiles leave a poorly filled last wave take it (the kernel refuses it when the tiles are a multiple of
+# the grid or more than 4x it).  Off by default: on every 17x17 / 8x8 / 35x35 Inception layer the
+# stream-K forms ran 0.72-0.85x of the best plain launch (the fold's partial tiles, 100-200 KB per
+# workgroup through L2, cost more than the idle CUs of the plain grid; profiles/r5_streamk_ab.md) except
+# the 8x8 448->384 3x3 forward (1.03-1.04x) and the whole-input aux-head GEMMs (the K = R*S*C reduction
+# of 6-25 tiles).  TONY_STREAMK=1,2,3: the grid multiples offered to the tuner.
+STREAM_MS = tuple(int(x) for x in os.environ.get("TONY_STREAMK", "").split(",") if x.strip() not in ("", "0"))
+NT_VARIANTS = _BASE + tuple(v + 256 * m for m in STREAM_MS for v in _BASE if v >= 11)
+# the whole-input (aux-head) GEMMs: a handful of tiles over a long K -- stream-K spreads K over the CUs
+# (conv_bench --tony: fwd 30 -> 17 us, dgrad 163 -> 68 us)
+SMALL_GEMM_VARIANTS = _BASE + tuple(v + 256 * m for m in (1, 2) for v in _BASE if v >= 11)
+
+
+def stream_of(vflags: int) -> int:
+    """Stream-K grid (in CUs) encoded in variant flags (0: plain launch)."""
+    return (vflags >> 16) & 15
 _CACHE: Dict[Hashable, int] = {}
 
 
@@ -95,7 +113,7 @@ def choices() -> Dict[Hashable, int]:
 
 
 def gemm_flags(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, M: int, N: int, K: int, lda: int,
-               stats: bool) -> int:
+               stats: bool, variants=NT_VARIANTS) -> int:
     """Variant bits for ``tony_gemm_bf16`` C[M,N] = A[M,K] B[N,K]^T (B and C dense, ld K and N).
 
     Timing runs write C (the caller overwrites it right after) and statistics into a scratch
@@ -111,7 +129,7 @@ def gemm_flags(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor, M: int, N: int
     scratch = torch.zeros(_lib.stat_floats(N), dtype=torch.float32, device=dev)
     base = 1 if stats else 0
     return pick(key, lambda vf: L.tony_gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, lda, K, N,
-                                                 base | vf, scratch.data_ptr(), 2 * N, stream))
+                                                 base | vf, scratch.data_ptr(), 2 * N, stream), variants)
 
 
 # ---- persistent decisions (the MIOpen find-db idea for tony_amd's own choices) -------------------

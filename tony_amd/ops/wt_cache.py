@@ -78,7 +78,79 @@ class TransposedWeights:
         _lib.check(rc, "tony_transpose_batch")
 
 
+_XDESC = struct.Struct("<QQQiiiiiiii")  # csrc/x3.hip XDesc
+
+
+class X3Weights:
+    """The fp32 model's x3 weight planes (ops/x3.py), both layouts, for the current step: the forward
+    planes [Co][R][S][3cp] and the backward-data planes [C][R][S][3Co] of every conv weight, refreshed
+    by ONE ``tony_x3_weights_batch`` launch right after the optimizer step instead of a split launch per
+    conv and pass on the critical path.  Same protocol as TransposedWeights: a weight seen for the first
+    time in an eager step is split on the spot and joins the batch; None outside a trainer."""
+
+    def __init__(self, device):
+        self.device = _norm(device)
+        if _lib.lib().tony_x3_desc_bytes() != _XDESC.size:
+            raise _lib.KernelError("x3 weight descriptor layout differs between Python and the kernels")
+        self.entries: Dict[int, tuple] = {}
+        self.enabled = False
+        self.frozen = False
+        self.desc: Optional[torch.Tensor] = None
+        self.n_desc = 0
+        self.total_tiles = 0
+
+    def _entry(self, weight: torch.Tensor):
+        if not self.enabled or not isinstance(weight, torch.nn.Parameter) or weight.dim() != 4:
+            return None
+        e = self.entries.get(id(weight))
+        if e is not None and e[0] is weight and e[3] == weight.data_ptr():
+            return e
+        if self.frozen or torch.cuda.is_current_stream_capturing():
+            return None
+        co, c, r, s = weight.shape
+        if weight.dtype != torch.float32 or co % 8 or not weight.is_contiguous(memory_format=torch.channels_last):
+            return None
+        from . import x3
+
+        fwd = x3.split_weight(weight)        # [Co * R * S, 3cp]
+        bwd = x3.split_weight_t(weight)      # [C, R, S, 3Co]
+        e = (weight, fwd, bwd, weight.data_ptr())
+        self.entries[id(weight)] = e
+        self._build()
+        return e
+
+    def planes(self, weight: torch.Tensor) -> Optional[torch.Tensor]:
+        e = self._entry(weight)
+        return None if e is None else e[1]
+
+    def planes_t(self, weight: torch.Tensor) -> Optional[torch.Tensor]:
+        e = self._entry(weight)
+        return None if e is None else e[2]
+
+    def _build(self):
+        parts, tiles = [], 0
+        for w, fwd, bwd, _ in self.entries.values():
+            co, c, r, s = w.shape
+            cp = (c + 7) // 8 * 8
+            tc, tco = (cp + _T - 1) // _T, (co + _T - 1) // _T
+            parts.append(_XDESC.pack(w.data_ptr(), fwd.data_ptr(), bwd.data_ptr(), co, r * s, c, cp, tc, tco, tiles, 0))
+            tiles += r * s * tc * tco
+        raw = torch.frombuffer(bytearray(b"".join(parts)), dtype=torch.uint8)
+        self.desc = raw.to(self.device)
+        self.n_desc = len(parts)
+        self.total_tiles = tiles
+
+    def refresh(self) -> None:
+        """Re-split every registered weight (call after each optimizer step)."""
+        if not self.n_desc:
+            return
+        rc = _lib.lib().tony_x3_weights_batch(self.desc.data_ptr(), self.n_desc, self.total_tiles,
+                                              _lib.stream_ptr(self.device))
+        _lib.check(rc, "tony_x3_weights_batch")
+
+
 _ACTIVE: list = [None]
+_ACTIVE_X3: list = [None]
 
 
 def _norm(device) -> torch.device:
@@ -88,9 +160,27 @@ def _norm(device) -> torch.device:
     return d
 
 
-def activate(cache: Optional[TransposedWeights]) -> None:
-    """Make ``cache`` the one the conv backward passes consult (None: transpose on the fly)."""
+def activate(cache: Optional[TransposedWeights], x3cache: Optional[X3Weights] = None) -> None:
+    """Make ``cache`` the one the conv backward passes consult (None: transpose on the fly), and
+    ``x3cache`` the fp32 model's weight planes (None: split on the fly)."""
     _ACTIVE[0] = cache
+    _ACTIVE_X3[0] = x3cache
+
+
+def x3_planes(weight: torch.Tensor) -> Optional[torch.Tensor]:
+    """The forward x3 planes of ``weight`` for this step (None: no trainer cache, split on the fly)."""
+    c = _ACTIVE_X3[0]
+    if c is not None and c.enabled and c.device == _norm(weight.device):
+        return c.planes(weight)
+    return None
+
+
+def x3_planes_t(weight: torch.Tensor) -> Optional[torch.Tensor]:
+    """The backward-data x3 planes of ``weight`` for this step (None: split on the fly)."""
+    c = _ACTIVE_X3[0]
+    if c is not None and c.enabled and c.device == _norm(weight.device):
+        return c.planes_t(weight)
+    return None
 
 
 def transposed(weight: torch.Tensor) -> torch.Tensor:

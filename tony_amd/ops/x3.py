@@ -26,7 +26,7 @@ from typing import Tuple
 
 import torch
 
-from . import _lib, concat, streams, tune
+from . import _lib, concat, streams, tune, wt_cache
 from .arena import zeros_f32
 from .bn import _as_rows, _rows_view
 
@@ -332,7 +332,9 @@ class _ConvBNActX3Fn(torch.autograd.Function):
     def forward(ctx, x, weight, gamma, beta, rmean, rvar, stride, padding, training, momentum, eps, relu, slot=None,
                 planes_only=False):
         x3, cp = split_act(x)
-        w3 = split_weight(weight)
+        w3 = wt_cache.x3_planes(weight)  # split once per step after the optimizer (ops/wt_cache.py)
+        if w3 is None:
+            w3 = split_weight(weight)
         co = weight.shape[0]
         stats = zeros_f32(_lib.stat_floats(co), x.device) if training else None
         z = conv_fwd(x3, cp, w3, weight.shape, stride, padding, stats)
@@ -373,8 +375,10 @@ class _ConvBNActX3Fn(torch.autograd.Function):
         if need_dx and ctx.needs_input_grad[0]:
             join = ctx.join
             pend = join.take() if join is not None else None  # another consumer's parked dX: add into it
-            dx = conv_dgrad(d3, split_weight_t(weight), weight.shape[0], x_shape, weight.shape, stride, padding,
-                            accum=pend)
+            wt3 = wt_cache.x3_planes_t(weight)
+            if wt3 is None:
+                wt3 = split_weight_t(weight)
+            dx = conv_dgrad(d3, wt3, weight.shape[0], x_shape, weight.shape, stride, padding, accum=pend)
             if join is not None:
                 dx = join.settle(dx)
             streams.keep(dx)  # may be consumed on another (branch) stream

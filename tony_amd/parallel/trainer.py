@@ -44,6 +44,10 @@ PLAN_WGRAD_BATCH = int(os.environ.get("TONY_PLAN_WGRAD_BATCH", "1"))
 PRIO_STREAM = os.environ.get("TONY_PRIO_STREAM", "0") == "1"
 
 
+# the fp32 model's weight planes split once per step in one launch (ops/wt_cache.py X3Weights);
+# TONY_X3_WCACHE=0: split per conv and pass (A/B)
+X3_WCACHE = os.environ.get("TONY_X3_WCACHE", "1") != "0"
+
 class Trainer:
     def __init__(self, model: torch.nn.Module, ps: ParameterServer, loss_fn: Callable, use_graph: bool = False,
                  warmup_eager: int = 3, graph_collectives: bool | None = None, overlap_wgrad: bool = True,
@@ -83,6 +87,10 @@ class Trainer:
         self.wt = wt_cache.TransposedWeights(dev) if dev.type == "cuda" else None
         if self.wt is not None:
             self.wt.enabled = True
+        # the fp32 (x3) model's weight planes, split in one launch after each optimizer step
+        self.wx3 = wt_cache.X3Weights(dev) if dev.type == "cuda" and X3_WCACHE else None
+        if self.wx3 is not None:
+            self.wx3.enabled = True
 
     def _mark(self, i: int) -> None:
         ev = self.phase_events
@@ -139,6 +147,8 @@ class Trainer:
             self.ps.step()
         if self.wt is not None:
             self.wt.refresh()  # the dgrads of the next step read the updated weights
+        if self.wx3 is not None:
+            self.wx3.refresh()  # ... and the x3 convs their weight planes
 
     def _eager_step(self, x, y):
         if self.arena is not None:
@@ -183,7 +193,7 @@ class Trainer:
         return self._prio or None
 
     def step(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
-        wt_cache.activate(self.wt)
+        wt_cache.activate(self.wt, self.wx3)
         try:
             s = self._compute_stream()
             if s is None:
@@ -317,3 +327,5 @@ class Trainer:
                 g.instantiate()
         if self.wt is not None:
             self.wt.frozen = True  # the captured refresh() holds the current work list
+        if self.wx3 is not None:
+            self.wx3.frozen = True
