@@ -360,3 +360,53 @@ def test_x3_weight_planes_batched_refresh_matches_per_weight_split(cuda):
     for w in ws:
         assert torch.equal(c.planes(w), x3.split_weight(w)), tuple(w.shape)
         assert torch.equal(c.planes_t(w), x3.split_weight_t(w)), tuple(w.shape)
+
+
+WGRAD_SHAPES = [  # (N, C, H, W, Co, k, stride, padding): the fused kernel's tile rows 64 / 96 / 128, both row walks
+    (16, 192, 17, 17, 192, (1, 7), 1, (0, 3)),
+    (16, 64, 35, 35, 96, (3, 3), 1, 1),
+    (16, 448, 8, 8, 384, (3, 3), 1, 1),
+    (8, 288, 35, 35, 48, (1, 1), 1, 0),
+    (8, 288, 35, 35, 384, (3, 3), 2, 0),
+    (16, 160, 5, 5, 160, (3, 3), 1, 1),   # OH * OW < WK + OW: the general (non-incremental) row walk
+    (4, 32, 35, 35, 32, (3, 3), 2, 0),
+]
+
+
+@pytest.mark.parametrize("shape", WGRAD_SHAPES, ids=lambda s: f"{s[1]}x{s[2]}-{s[4]}-k{s[5][0]}x{s[5][1]}-s{s[6]}")
+def test_x3_wgrad_forms_match_float64(cuda, shape, monkeypatch):
+    """csrc/conv.hip tony_conv_wgrad_x3 in each form -- the three plane pairs as split groups
+    (conv_wgrad_glds_kernel, mode 0), and the fused kernel (conv_wgrad_x3f_kernel) that stages all four
+    planes per K-step on a 3-slot (mode 1) or 2-slot (mode 2) LDS ring -- against the float64 weight
+    gradient, and the fused forms against the pair form (the same products in another order)."""
+    from tony_amd.ops import _lib, x3
+
+    n, c, h, w, co, k, s, p = shape
+    monkeypatch.setattr(x3, "WGRAD_DIRECT", False)
+    L = _lib.lib()
+    torch.manual_seed(1)
+    xf = _cl(torch.randn(n, c, h, w, device=cuda))
+    oh = (h + 2 * _pair(p)[0] - k[0]) // s + 1
+    ow = (w + 2 * _pair(p)[1] - k[1]) // s + 1
+    dyf = _cl(torch.randn(n, co, oh, ow, device=cuda) * torch.logspace(-2, 1, co, device=cuda).view(1, -1, 1, 1))
+    xp, cp = x3.split_act(xf)
+    dp, dcp = x3.split_act(dyf)
+    assert dcp == co
+    out = {}
+    prev = L.tony_x3_wgrad_mode(-1)
+    try:
+        for mode in (0, 1, 2):
+            L.tony_x3_wgrad_mode(mode)
+            out[mode] = x3.conv_wgrad(dp, xp, cp, (co, c) + tuple(k), s, p)
+            torch.cuda.synchronize()
+    finally:
+        L.tony_x3_wgrad_mode(prev)
+    ref = torch.nn.grad.conv2d_weight(xf.double().cpu(), (co, c) + tuple(k), dyf.double().cpu(), s, p)
+    for mode, dw in out.items():
+        assert _rel(dw, ref) < 1e-4, mode
+    assert _rel(out[1], out[0]) < 1e-6
+    assert _rel(out[2], out[0]) < 1e-6
+
+
+def _pair(v):
+    return (v, v) if isinstance(v, int) else tuple(v)

@@ -116,6 +116,7 @@ _SIGNATURES = {
     "tony_conv_wgrad_x3": [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int, c_int, c_int,
                            c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int64, c_void_p, c_int,
                            c_void_p],
+    "tony_x3_wgrad_mode": [c_int],
     "tony_conv_wgrad_direct": [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int, c_int, c_int,
                                c_int, c_int, c_void_p, c_int64, c_void_p, c_int, c_void_p],
     "tony_avgpool3_s1p1": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],

@@ -14,6 +14,7 @@
 // from one input pixel (or zero for padding).  The tap/channel position of a thread's chunk is
 // advanced incrementally per K-step (no divisions in the loop); the per-row pixel coordinates are
 // decoded once per tile (forward/dgrad) or advanced incrementally with the row (wgrad).
+#include <atomic>
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -1258,6 +1259,183 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
                                 fold);
 }
 
+// ---- x3 (fp32) weight gradient with the plane pairs fused -------------------------------------------
+// dW = dYh^T Xh + dYh^T Xl + dYl^T Xh (ops/x3.py) in ONE pass over the rows: every K-step stages the four
+// operand planes of its WK rows -- dY hi / lo ([WK][TBM] each, 256-B rows) and the im2col rows of X hi /
+// lo ([WK][128]) -- by LDS-DMA into a ST-slot ring and issues the three products on the same
+// accumulators.  Against the plane-pair form of conv_wgrad_glds_kernel (each pair a full pass, three
+// times the address walk, the DMAs and the fragment reads for the same MFMAs), the per-step im2col
+// walk, bounds checks and pointer selects are shared by all three products: VALU per MFMA drops ~3x
+// (the pair form's K loop issued 49 VALU + 21 SALU per 12 MFMAs: issue-bound, profiles/r5_streamk_ab.md
+// PMC) and the operand intake per MFMA by a third.  The lo planes sit dplane / xplane elements after
+// the hi ones in the same rows.  Slab mode: one partial per split, tony_splitk_reduce sums them.
+template <int TBM, int ST, bool INC>
+__global__ __launch_bounds__(kThreads) void conv_wgrad_x3f_kernel(const uint16_t* __restrict__ dY, int64_t lddy,
+                                                                  Gather g, int64_t M, int Co, int tiles_n2,
+                                                                  int ntiles, int64_t rows_per_split,
+                                                                  float* __restrict__ slab, WkStep ws, int dplane,
+                                                                  int xplane) {
+  constexpr int TM = TBM / 32;
+  constexpr int TILE = WK * 128;           // elements per staged plane (32 rows x 256 B)
+  constexpr int STAGE = 4 * TILE;          // Ah, Al, Bh, Bl
+  constexpr int NDMA = 8;                  // per thread and stage: 2 rows x 4 planes
+  static_assert(ST == 2 || ST == 3, "ring of 2 or 3 stages");
+  __shared__ __attribute__((aligned(16))) uint16_t smem[ST * STAGE];
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = wg % ntiles, split = wg / ntiles;
+  const int t1 = tile / tiles_n2, t2 = tile % tiles_n2;
+  const int n1_0 = t1 * TBM, n2_0 = t2 * WTBN;
+  const int64_t m_begin = static_cast<int64_t>(split) * rows_per_split;
+  const int64_t m_end = min(M, m_begin + rows_per_split);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int K = g.K;
+
+  const int r0 = threadIdx.x >> 4;
+  const int ch = (threadIdx.x & 15) ^ tr_swz(r0);  // tr_swz(r0 + 16) == tr_swz(r0)
+  const int acol = n1_0 + ch * 8;
+  const bool acol_ok = (ch < TBM / 8) & (acol < Co);
+  const int kcol = n2_0 + ch * 8;
+  const bool kok = kcol < K;
+  TapPos tp;
+  tp.init(kok ? kcol : 0, g);
+  MRow mr[2];
+  mr[0].init(m_begin + r0, g);
+  mr[1].init(m_begin + r0 + 16, g);
+  int64_t am = m_begin + r0;
+  const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(smem) + (4 * wave) * 256);
+  constexpr uint32_t kRow16 = 16 * 256, kStageB = STAGE * 2, kTileB = TILE * 2;
+  IncRows inc;
+  const uint16_t* ap = dY + (m_begin + r0) * lddy + acol;
+  int am32 = static_cast<int>(m_begin) + r0;
+  const int mend32 = static_cast<int>(m_end);
+  if constexpr (INC) inc.init(mr, g, tp);
+
+  auto issue = [&](int slot) {
+    const uint32_t Ah = base + slot * kStageB, Al = Ah + kTileB, Bh = Al + kTileB, Bl = Bh + kTileB;
+    const void* z = &kZeroChunk;
+    if constexpr (INC) {
+      const int64_t row16 = 16 * lddy;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool ok = acol_ok & (am32 + 16 * i < mend32);
+        const uint16_t* a = ap + i * row16;
+        glds16(ok ? static_cast<const void*>(a) : z, Ah + i * kRow16);
+        glds16(ok ? static_cast<const void*>(a + dplane) : z, Al + i * kRow16);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool ok = kok & (am32 + 16 * i < mend32) & inc.in_image(i, g);
+        const uint16_t* b = g.src + inc.ie[i];
+        glds16(ok ? static_cast<const void*>(b) : z, Bh + i * kRow16);
+        glds16(ok ? static_cast<const void*>(b + xplane) : z, Bl + i * kRow16);
+      }
+      inc.advance(ws);
+      am32 += WK;
+      ap += WK * lddy;
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t m = am + 16 * i;
+      const bool ok = acol_ok & (m < m_end);
+      const uint16_t* a = dY + m * lddy + acol;
+      glds16(ok ? static_cast<const void*>(a) : z, Ah + i * kRow16);
+      glds16(ok ? static_cast<const void*>(a + dplane) : z, Al + i * kRow16);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const MRow& q = mr[i];
+      const int iy = q.oy * g.sh + g.offh + tp.r, ix = q.ox * g.sw + g.offw + tp.s;
+      const bool ok = kok & (q.m < m_end) & (static_cast<unsigned>(iy) < static_cast<unsigned>(g.Hs)) &
+                      (static_cast<unsigned>(ix) < static_cast<unsigned>(g.Ws));
+      const uint16_t* b = g.src + (static_cast<int64_t>(q.n) * g.Hs * g.Ws + iy * g.Ws + ix) * g.ld + tp.c;
+      glds16(ok ? static_cast<const void*>(b) : z, Bh + i * kRow16);
+      glds16(ok ? static_cast<const void*>(b + xplane) : z, Bl + i * kRow16);
+    }
+    am += WK;
+    mr[0].advance(WK, g);
+    mr[1].advance(WK, g);
+  };
+
+  f32x4 acc[TM][4];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = static_cast<int>((m_end - m_begin + WK - 1) / WK);
+#pragma unroll
+  for (int s = 0; s < ST - 1; ++s) issue(s);
+  const int kgrp = lane >> 4;
+  auto step = [&](auto slot_c) {
+    constexpr int SLOT = decltype(slot_c)::value;
+    // stage kt has landed in this wave (the ST - 2 younger stages' DMAs may still fly) and, after the
+    // barrier, in every wave; every wave is also done reading the slot refilled next
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((ST - 2) * NDMA) : "memory");
+    __builtin_amdgcn_s_barrier();
+    issue((SLOT + ST - 1) % ST);
+    const uint16_t* Ahs = smem + SLOT * STAGE;
+    const uint16_t* Als = Ahs + TILE;
+    const uint16_t* Bhs = Als + TILE;
+    const uint16_t* Bls = Bhs + TILE;
+    bf16x8_t ah[TM], al[TM], bh[4], bl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bh[j] = tr_frag(Bhs, kgrp, wn * 64 + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) ah[i] = tr_frag(Ahs, kgrp, wm * (TBM / 2) + i * 16, lane);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bl[j] = tr_frag(Bls, kgrp, wn * 64 + j * 16, lane);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) al[i] = tr_frag(Als, kgrp, wm * (TBM / 2) + i * 16, lane);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  using S2 = std::integral_constant<int, 2>;
+  int kt = 0;
+  if constexpr (ST == 3) {
+    for (; kt + 3 <= nk; kt += 3) {
+      step(S0{});
+      step(S1{});
+      step(S2{});
+    }
+    if (kt < nk) step(S0{});
+    if (kt + 1 < nk) step(S1{});
+  } else {
+    for (; kt + 2 <= nk; kt += 2) {
+      step(S0{});
+      step(S1{});
+    }
+    if (kt < nk) step(S0{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup retires
+  float* dst = slab + static_cast<int64_t>(split) * Co * K;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = n2_0 + wn * 64 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = n1_0 + wm * (TBM / 2) + i * 16 + (lane >> 4) * 4 + r;
+        if (row < Co && col < K) dst[static_cast<int64_t>(row) * K + col] = acc[i][j][r];
+      }
+    }
+  }
+}
+
 // ---- 3x3 stride-1 weight gradient with 32 / 64 channels on both sides: persistent direct kernel --
 // The implicit-GEMM wgrad (above) gathers the im2col rows of X through L2 for each of the 9 taps and,
 // with Cout = 32 / 64, runs 16-row MFMA tiles with a thin A panel: Inception's 149x149 / 147x147
@@ -1484,6 +1662,63 @@ int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, float
   return 0;
 }
 
+// TONY_X3_WGRAD_FUSED: 0 = the plane-pair form, 1 = fused planes on a 3-slot ring (one workgroup per CU),
+// 2 = fused on a 2-slot ring (two per CU; default).  tony_x3_wgrad_mode overrides it (tests, A/B).
+std::atomic<int> g_x3f_mode{-1};
+
+int x3f_mode() {
+  int m = g_x3f_mode.load(std::memory_order_relaxed);
+  if (m < 0) {
+    const char* e = getenv("TONY_X3_WGRAD_FUSED");
+    m = e == nullptr ? 2 : atoi(e);
+    g_x3f_mode.store(m, std::memory_order_relaxed);
+  }
+  return m;
+}
+
+// the fused x3 weight gradient (conv_wgrad_x3f_kernel): Cout tiles of 64 / 96 / 128 rows, splits for
+// ~1 (3-slot ring) or ~2 (2-slot) workgroups per CU, each reducing >= 8 stages of WK rows
+int launch_wgrad_x3f(const void* dy, int64_t lddy, const Gather& g, float* slab, int64_t slab_cap, int* splits_out,
+                     int64_t M, int Co, int num_cus, int dplane, int xplane, hipStream_t stream) {
+  const int tbm = Co <= 64 ? 64 : (ceil_div(Co, 96) * 96 < ceil_div(Co, 128) * 128 ? 96 : 128);
+  const int ring = x3f_mode() == 1 ? 3 : 2;
+  const int tiles_n1 = ceil_div(Co, tbm), tiles_n2 = ceil_div(g.K, WTBN);
+  const int ntiles = tiles_n1 * tiles_n2;
+  const int target = (ring == 3 ? 1 : 2) * (num_cus > 0 ? num_cus : 256);
+  int64_t splits = (target + ntiles - 1) / ntiles;
+  const int64_t max_splits = (M + 8 * WK - 1) / (8 * WK);
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  int64_t rows = (M + splits - 1) / splits;
+  rows = (rows + WK - 1) / WK * WK;
+  splits = (M + rows - 1) / rows;
+  const int64_t grid = splits * ntiles;
+  if (grid > 0x7fffffff) return -2;
+  if (slab == nullptr || splits * Co * static_cast<int64_t>(g.K) > slab_cap) return -4;
+  if (splits_out != nullptr) *splits_out = static_cast<int>(splits);
+  WkStep ws{};
+  const bool inc = wgrad_inc_step(g, M, &ws);
+  const auto* dyp = static_cast<const uint16_t*>(dy);
+  const auto go = [&](auto tb, auto st) {
+    constexpr int TB = decltype(tb)::value, S = decltype(st)::value;
+    if (inc)
+      conv_wgrad_x3f_kernel<TB, S, true><<<static_cast<int>(grid), kThreads, 0, stream>>>(
+          dyp, lddy, g, M, Co, tiles_n2, ntiles, rows, slab, ws, dplane, xplane);
+    else
+      conv_wgrad_x3f_kernel<TB, S, false><<<static_cast<int>(grid), kThreads, 0, stream>>>(
+          dyp, lddy, g, M, Co, tiles_n2, ntiles, rows, slab, ws, dplane, xplane);
+  };
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  switch (tbm) {
+    case 64: ring == 3 ? go(std::integral_constant<int, 64>{}, I3{}) : go(std::integral_constant<int, 64>{}, I2{}); break;
+    case 96: ring == 3 ? go(std::integral_constant<int, 96>{}, I3{}) : go(std::integral_constant<int, 96>{}, I2{}); break;
+    default: ring == 3 ? go(std::integral_constant<int, 128>{}, I3{}) : go(std::integral_constant<int, 128>{}, I2{}); break;
+  }
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
 // Cout tile rows of the split-K wgrad: 32 / 64 for thin layers; above, 96 where it pads Cout less than
 // 128 does (Inception's 160 / 192 / 288 / 448-channel layers: 25-37% of the 128-row tiles' MFMA rows
 // were zero padding at 160 / 192), else 128.  TONY_WGRAD_TBM96=0: always 128 (A/B).
@@ -1672,6 +1907,10 @@ TONY_API int tony_conv_wgrad_x3(const void* dy, int64_t lddy, const void* x, int
   if (M > 0x7fffffff) return -1;
   Gather g{static_cast<const uint16_t*>(x), ldx, H, W, C, OH, OW, R, S, sh, sw, -ph, -pw, 1, K, 0};
   const SplitFold fold{nullptr, nullptr, 0};
+  if (x3f_mode() > 0 && wgrad_glds_enabled()) {
+    const int rc = launch_wgrad_x3f(dy, lddy, g, slab, slab_cap, splits_out, M, Co, num_cus, dplane, xplane, stream);
+    if (rc != -3) return rc;
+  }
   const PlanePairs pp{3, 1, {0, 0, dplane}, {0, xplane, 0}};
   // thin layers (Co <= 64) on the LDS-DMA kernel's 96-row tiles: its three plane pairs ran 3x slower
   // on the register-staged 32 / 64-row kernel (conv_wgrad_kernel<64>: 304 us per 35x35 layer,
@@ -1687,6 +1926,13 @@ TONY_API int tony_conv_wgrad_x3(const void* dy, int64_t lddy, const void* x, int
     case 96: return launch_wgrad<96>(dy, lddy, g, nullptr, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream, pp);
     default: return launch_wgrad<128>(dy, lddy, g, nullptr, slab, slab_cap, splits_out, M, Co, num_cus, fold, stream, pp);
   }
+}
+
+// the x3 weight-gradient form (x3f_mode): mode >= 0 sets it, -1 only reads; returns the previous mode
+TONY_API int tony_x3_wgrad_mode(int mode) {
+  const int prev = x3f_mode();
+  if (mode >= 0) g_x3f_mode.store(mode, std::memory_order_relaxed);
+  return prev;
 }
 
 // dW (fp32 partials, [grid][Co][3][3][C]) of a 3x3 stride-1 conv with C, Co in {32, 64} by the
