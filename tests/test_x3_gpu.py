@@ -170,6 +170,10 @@ def test_inception_fp32_step_matches_float64(cuda):
     # every gradient upstream of an Inception pool branch; MIOpen's fp32 NCHW convs pick Winograd for the
     # 3x3s (~5e-4 relative on the loss), so the stock fp32 graph is no reference for an fp32 path either
     ref = inception_v3(fused=False, seed=3).to(DEV).double().train()
+    from tony_amd.models.convert import fused_grads_to_stock, fused_to_stock
+
+    if any(n.endswith(".head.conv.weight") for n, _ in ours.named_parameters()):  # the fused-head layout
+        ref.load_state_dict(fused_to_stock(ours.state_dict(), ours, ref))
     ours.dropout.p = ref.dropout.p = 0.0
     x = _cl(torch.randn(4, 3, 299, 299, device=DEV))
     y = torch.randint(0, 1000, (4,), device=DEV)
@@ -195,9 +199,12 @@ def test_inception_fp32_step_matches_float64(cuda):
     # of the network is held to the gradient direction.  Every single pass is pinned to 1e-4 through the
     # same ReLU mask by test_conv_bn_relu_x3_matches_float64.
     go, gr = [], []
-    for (name, po), pr in zip(ours.named_parameters(), ref.parameters()):
+    heads = any(n.endswith(".head.conv.weight") for n, _ in ours.named_parameters())
+    gours = fused_grads_to_stock(ours, ref) if heads else {n: p.grad for n, p in ours.named_parameters()}
+    for name, pr in ref.named_parameters():
+        po = gours[name]
         assert po.shape == pr.shape, name
-        a, b = po.grad.double().cpu(), pr.grad.double().cpu()
+        a, b = po.double().cpu(), pr.grad.double().cpu()
         err = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
         if name.startswith("fc.") or name.startswith("aux.fc."):
             # dW of a classifier is its input features times dlogits: the features carry the forward's
@@ -410,3 +417,41 @@ def test_x3_wgrad_forms_match_float64(cuda, shape, monkeypatch):
 
 def _pair(v):
     return (v, v) if isinstance(v, int) else tuple(v)
+
+
+@pytest.mark.parametrize("cfg", [(64, 17, (64, 48, 64), 32), (96, 8, (32, 48, 64), 24), (64, 9, (40, 48), 0)],
+                         ids=["A-like", "E-like", "D-like-nopool"])
+def test_x3_fused_head_matches_float64(cuda, cfg):
+    """The fp32 FusedHead (ops/x3.py head: one x3 GEMM for every 1x1 head conv + the pool branch's 1x1
+    commuted in front of its avg pool, per-split BN into one dZ plane tensor, one dgrad + one fused wgrad)
+    against ops/fused.head_reference in float64: every output, dX, dW, dgamma, dbeta."""
+    from tony_amd.ops.fused import FusedHead, head_reference
+
+    cin, hw, splits, npool = cfg
+    torch.manual_seed(0)
+    hd = FusedHead(cin, splits, pool_cout=npool).to(DEV).to(memory_format=torch.channels_last).train()
+    with torch.no_grad():
+        hd.bn.weight.uniform_(0.5, 1.5)
+        hd.bn.bias.uniform_(-0.2, 0.2)
+    x = _cl(torch.randn(4, cin, hw, hw, device=DEV)).requires_grad_()
+    outs = hd(x * 1.0)
+    gs = [_cl(torch.randn(o.shape, device=DEV)) for o in outs]
+    torch.autograd.backward(outs, gs)
+
+    xd = x.detach().double().cpu().requires_grad_()
+    wd = hd.conv.weight.detach().double().cpu().requires_grad_()
+    gd = hd.bn.weight.detach().double().cpu().requires_grad_()
+    bd = hd.bn.bias.detach().double().cpu().requires_grad_()
+    rm = torch.zeros(sum(splits) + npool, dtype=torch.float64)
+    rv = torch.ones(sum(splits) + npool, dtype=torch.float64)
+    refs = head_reference(xd, wd, gd, bd, rm, rv, splits, npool, True, 0.1, hd.bn.eps)
+    for o, r in zip(outs, refs):
+        assert _rel(o.detach(), r.detach()) < 1e-4
+    # the backward through OUR ReLU masks (see test_conv_bn_relu_x3_matches_float64)
+    masked = [r * (o.detach().double().cpu() > 0) for o, r in zip(outs, refs)]
+    torch.autograd.backward(masked, [g.double().cpu() for g in gs])
+    assert _rel(x.grad, xd.grad) < 1e-4
+    assert _rel(hd.conv.weight.grad, wd.grad) < 1e-4
+    assert _rel(hd.bn.weight.grad, gd.grad) < 1e-4
+    assert _rel(hd.bn.bias.grad, bd.grad) < 1e-4
+    assert _rel(hd.bn.running_mean, rm) < 1e-4 and _rel(hd.bn.running_var, rv) < 1e-4

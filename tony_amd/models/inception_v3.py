@@ -58,6 +58,9 @@ def _x3_input(x: torch.Tensor) -> None:
 # TONY_X3_PLANES=0: intra-chain x3 layers hand over the fp32 y (A/B, diagnosis)
 X3_PLANES = os.environ.get("TONY_X3_PLANES", "1") != "0"
 X3_BLOCKS = os.environ.get("TONY_X3_BLOCKS", "1") != "0"
+# TONY_X3_HEADS=0: the fp32 blocks keep the textbook head convs (one x3 conv per branch) instead of the
+# fused x3 head (ops/x3.py head: one GEMM, one dgrad, one wgrad per block input)
+X3_HEADS = os.environ.get("TONY_X3_HEADS", "1") != "0"
 
 
 def _inner(m, x):
@@ -99,7 +102,9 @@ class _Block(nn.Module):
         self.fused = fused and not x3
         self.x3 = x3
         # the fp32 blocks' fast form (concat slots, branch streams, joins); TONY_X3_BLOCKS=0: torch.cat graph
-        self.x3_fast = x3 and X3_BLOCKS
+        self.x3_fast = x3 and (X3_BLOCKS or X3_HEADS)
+        # the fused-head layout (ops/fused.py FusedHead, models/convert.py): the bf16 model and the fp32 one
+        self.heads = self.fused or (x3 and X3_HEADS)
 
     def avgpool(self, x, planes_only=False):
         """``planes_only``: the x3 pool branch, read by its 1x1 conv only (ops/pool.avg_pool3x3_s1)."""
@@ -119,8 +124,7 @@ class _Block(nn.Module):
 class InceptionA(_Block):
     def __init__(self, cin, pool_ch, fused=True, x3=False):
         super().__init__(fused, x3)
-        fused = self.fused
-        if fused:
+        if self.heads:
             # b1 1x1/64, b5 1x1/48, b3 1x1/64 and the pool branch's 1x1 share one GEMM
             self.head = FusedHead(cin, (64, 48, 64), pool_cout=pool_ch)
             self.b5 = self.c(48, 64, 5, p=2)
@@ -139,6 +143,14 @@ class InceptionA(_Block):
             s1, s5, s3, sp = _slots(buf, (64, 64, 96, self.out_channels - 224))
             y1, y5, y3, yp = self.head(x, slots=(s1, None, None, sp))
             # the double-3x3 chain on this stream, the 5x5 beside it (ops/streams.py)
+            o3, o5 = streams.parallel(lambda: _seq(self.b3, y3, s3), lambda: self.b5(y5, slot=s5))
+            streams.keep(y5, y3)
+            return assemble(buf, [y1, o5, o3, yp])
+        if self.x3_fast and self.heads:  # the x3 head, then the chains on their streams
+            n, _, h, w = x.shape
+            buf = concat_buffer(n, self.out_channels, h, w, x)
+            s1, s5, s3, sp = _slots(buf, (64, 64, 96, self.out_channels - 224))
+            y1, y5, y3, yp = self.head(x, slots=(s1, None, None, sp), planes=(False, True, True))
             o3, o5 = streams.parallel(lambda: _seq(self.b3, y3, s3), lambda: self.b5(y5, slot=s5))
             streams.keep(y5, y3)
             return assemble(buf, [y1, o5, o3, yp])
@@ -193,8 +205,7 @@ class InceptionB(_Block):  # 35x35 -> 17x17 reduction
 class InceptionC(_Block):  # 17x17 with factorised 7x7
     def __init__(self, cin, c7, fused=True, x3=False):
         super().__init__(fused, x3)
-        fused = self.fused
-        if fused:
+        if self.heads:
             self.head = FusedHead(cin, (192, c7, c7), pool_cout=192)
             self.b7 = nn.Sequential(self.c(c7, c7, (1, 7), p=(0, 3)), self.c(c7, 192, (7, 1), p=(3, 0)))
             self.bd = nn.Sequential(self.c(c7, c7, (7, 1), p=(3, 0)), self.c(c7, c7, (1, 7), p=(0, 3)),
@@ -218,6 +229,14 @@ class InceptionC(_Block):  # 17x17 with factorised 7x7
             od, o7 = streams.parallel(lambda: _seq(self.bd, yd, sd), lambda: _seq(self.b7, y7, s7))
             streams.keep(y7, yd)
             return assemble(buf, [y1, o7, od, yp])
+        if self.x3_fast and self.heads:
+            n, _, h, w = x.shape
+            buf = concat_buffer(n, 768, h, w, x)
+            s1, s7, sd, sp = _slots(buf, (192, 192, 192, 192))
+            y1, y7, yd, yp = self.head(x, slots=(s1, None, None, sp), planes=(False, True, True))
+            od, o7 = streams.parallel(lambda: _seq(self.bd, yd, sd), lambda: _seq(self.b7, y7, s7))
+            streams.keep(y7, yd)
+            return assemble(buf, [y1, o7, od, yp])
         if self.x3_fast:
             n, _, h, w = x.shape
             buf = concat_buffer(n, 768, h, w, x)
@@ -237,8 +256,7 @@ class InceptionC(_Block):  # 17x17 with factorised 7x7
 class InceptionD(_Block):  # 17x17 -> 8x8 reduction
     def __init__(self, cin, fused=True, x3=False):
         super().__init__(fused, x3)
-        fused = self.fused
-        if fused:
+        if self.heads:
             self.head = FusedHead(cin, (192, 192))
             self.b3 = self.c(192, 320, 3, s=2)
             self.b7 = nn.Sequential(self.c(192, 192, (1, 7), p=(0, 3)), self.c(192, 192, (7, 1), p=(3, 0)),
@@ -261,6 +279,17 @@ class InceptionD(_Block):  # 17x17 -> 8x8 reduction
                                           lambda: max_pool(x, 3, 2, slot=sp))
             streams.keep(x, t3, t7)
             return assemble(buf, [o3, o7, op])
+        if self.x3_fast and self.heads:
+            n, c, h, w = x.shape
+            buf = concat_buffer(n, self.out_channels, (h - 3) // 2 + 1, (w - 3) // 2 + 1, x)
+            s3, s7, sp = _slots(buf, (320, 192, c))
+            if self.training:
+                _join(x, 2)  # the x3 head and the max pool
+            t3, t7 = self.head(x, planes=(True, True))
+            o7, o3, op = streams.parallel(lambda: _seq(self.b7, t7, s7), lambda: self.b3(t3, slot=s3),
+                                          lambda: max_pool(x, 3, 2, slot=sp))
+            streams.keep(x, t3, t7)
+            return assemble(buf, [o3, o7, op])
         if self.x3_fast:
             n, c, h, w = x.shape
             buf = concat_buffer(n, self.out_channels, (h - 3) // 2 + 1, (w - 3) // 2 + 1, x)
@@ -278,7 +307,7 @@ class InceptionD(_Block):  # 17x17 -> 8x8 reduction
 class InceptionE(_Block):  # 8x8 with split 1x3 / 3x1 branches
     def __init__(self, cin, fused=True, x3=False):
         super().__init__(fused, x3)
-        fused = self.fused
+        fused = self.heads
         if fused:
             self.head = FusedHead(cin, (320, 384, 448), pool_cout=192)
         else:
@@ -305,6 +334,23 @@ class InceptionE(_Block):  # 8x8 with split 1x3 / 3x1 branches
 
             def dbl():
                 dd = self.bd(d)
+                if self.training:
+                    _join(dd, 2)
+                return self.bda(dd, slot=sda), self.bdb(dd, slot=sdb)
+
+            (oda, odb), oa, ob = streams.parallel(dbl, lambda: self.b3a(t, slot=sa), lambda: self.b3b(t, slot=sb))
+            streams.keep(t, d)
+            return assemble(buf, [y1, oa, ob, oda, odb, yp])
+        elif self.x3_fast and self.heads:
+            n, _, h, w = x.shape
+            buf = concat_buffer(n, 2048, h, w, x)
+            s1, sa, sb, sda, sdb, sp = _slots(buf, (320, 384, 384, 384, 384, 192))
+            y1, t, d, yp = self.head(x, slots=(s1, None, None, sp), planes=(False, True, True))
+            if self.training:
+                _join(t, 2)  # the 1x3 and 3x1 splits
+
+            def dbl():
+                dd = _inner(self.bd, d)  # read by the two split convs only: operand planes
                 if self.training:
                     _join(dd, 2)
                 return self.bda(dd, slot=sda), self.bdb(dd, slot=sdb)

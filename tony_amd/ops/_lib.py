@@ -154,7 +154,11 @@ _SIGNATURES = {
     "tony_bn_bwd_apply_f32_x3": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int, c_void_p,
                           c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p,
                           c_void_p, c_int, c_void_p],
+    "tony_bn_bwd_apply_f32_x3p": [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int64, c_int,
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int64,
+                                  c_void_p, c_void_p, c_int, c_void_p],
     "tony_avgpool3_s1p1_f32": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
+    "tony_avgpool3_s1p1_x3p": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_int64, c_void_p],
     "tony_avgpool3_s1p1_acc": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_int64, c_int, c_void_p],
     "tony_avgpool3_s1p1_x3": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int64, c_void_p],
     "tony_maxpool_fwd_f32": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64,

@@ -366,7 +366,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     T* __restrict__ dx, int64_t lddx, int64_t M, int C, int64_t rows_per_block,
     const float* __restrict__ mean, const float* __restrict__ invstd, const void* gamma,
     const void* beta, int param_bf16, int relu, const float* __restrict__ dsum,
-    const float* __restrict__ dsumx, int64_t sstride, void* dgamma, void* dbeta, int accumulate, Segs segs) {
+    const float* __restrict__ dsumx, int64_t sstride, void* dgamma, void* dbeta, int accumulate, Segs segs,
+    int64_t pstride = 0) {
   float* tab = bn_dyn;  // [5][C]: bn_lds_table(C, 5) bytes
   const float inv_m = 1.f / static_cast<float>(M);
   for (int c = threadIdx.x; c < C; c += kThreads) {
@@ -426,9 +427,10 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) lo[j] = o[j] - hf[j];
       uint16_t* d = reinterpret_cast<uint16_t*>(dx) + row * lddx + rm.cg * 8;
+      const int64_t ps = pstride > 0 ? pstride : C;  // a slice of wider planes (ops/fused.py x3 head)
       hi.store(d);
-      V8<uint16_t>::from_float(lo).store(d + C);
-      hi.store(d + 2 * C);
+      V8<uint16_t>::from_float(lo).store(d + ps);
+      hi.store(d + 2 * ps);
     } else {
       V8<T>::from_float(o).store(dx + row * lddx + rm.cg * 8);
     }
@@ -1122,6 +1124,27 @@ TONY_API int tony_bn_bwd_apply_f32_x3(const void* x, int64_t ldx, const void* dy
       static_cast<const float*>(x), ldx, static_cast<const float*>(dy), lddy, nullptr, 0, nullptr, 0,
       static_cast<float*>(dx3), lddx, M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsum, dsumx, sstride,
       dgamma, dbeta, accumulate, Segs{});
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// the x3 planes of dx as channels [0, C) of wider planes: plane p at column p * pstride (pstride >= C), so
+// the BN backward of one split of a fused x3 head writes its slice of the head's dZ planes
+TONY_API int tony_bn_bwd_apply_f32_x3p(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx3,
+                                       int64_t lddx, int64_t pstride, int64_t M, int C, const float* mean,
+                                       const float* invstd, const void* gamma, const void* beta, int param_bf16,
+                                       int relu, const float* dsum, const float* dsumx, int64_t sstride, void* dgamma,
+                                       void* dbeta, int accumulate, hipStream_t stream) {
+  if (bad_c(C) || (ldx % 4) || (lddy % 4) || (lddx % 8) || (pstride % 8) || pstride < C ||
+      lddx < 2 * pstride + C || sstride < 0 || (reinterpret_cast<uintptr_t>(dx3) & 15))
+    return -1;
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 4, 8192, &rpb, &grid);
+  bn_bwd_apply_kernel<false, float, true><<<grid, kThreads, bn_lds_table(C, 5), stream>>>(
+      static_cast<const float*>(x), ldx, static_cast<const float*>(dy), lddy, nullptr, 0, nullptr, 0,
+      static_cast<float*>(dx3), lddx, M, C, rpb, mean, invstd, gamma, beta, param_bf16, relu, dsum, dsumx, sstride,
+      dgamma, dbeta, accumulate, Segs{}, pstride);
   TONY_LAUNCH_CHECK();
   return 0;
 }

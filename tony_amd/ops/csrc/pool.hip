@@ -87,9 +87,11 @@ __global__ __launch_bounds__(kThreads) void box3_kernel(const T* __restrict__ x,
 
 // fp32 avg pool straight to the x3 operand planes of its only consumer conv (ops/x3.py split_act layout:
 // [hi | lo | hi] over cp = C channels per row, hi = bf16(v), lo = bf16(v - hi)): the fp32 pooled map is
-// never stored or re-read by a split pass
+// never stored or re-read by a split pass.  Rows of y3 are ldy elements apart, plane p starts at column
+// p * ps (ps = C: a plane tensor of its own; ps > C: a slice of wider planes, ops/fused.py x3 head)
 __global__ __launch_bounds__(kThreads) void box3_x3_kernel(const float* __restrict__ x, uint16_t* __restrict__ y3,
-                                                           int N, int H, int W, int C, int64_t ldx) {
+                                                           int N, int H, int W, int C, int64_t ldx, int64_t ldy,
+                                                           int64_t ps) {
   const uint32_t CG = C >> 3;
   const uint32_t total = static_cast<uint32_t>(N) * H * W * CG;
   const uint32_t stride = gridDim.x * kThreads;
@@ -106,10 +108,10 @@ __global__ __launch_bounds__(kThreads) void box3_x3_kernel(const float* __restri
     hi.to_float(hf);
 #pragma unroll
     for (int j = 0; j < 8; ++j) lo[j] = acc[j] - hf[j];
-    uint16_t* d = y3 + static_cast<int64_t>(site) * (3 * C) + cg * 8;
+    uint16_t* d = y3 + static_cast<int64_t>(site) * ldy + cg * 8;
     store8(d, hi);
-    store8(d + C, bf16x8::from_float(lo));
-    store8(d + 2 * C, hi);
+    store8(d + ps, bf16x8::from_float(lo));
+    store8(d + 2 * ps, hi);
   }
 }
 
@@ -617,7 +619,20 @@ TONY_API int tony_avgpool3_s1p1_x3(const void* x, void* y3, int N, int H, int W,
       static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff)
     return -1;
   box3_x3_kernel<<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
-      static_cast<const float*>(x), static_cast<uint16_t*>(y3), N, H, W, C, ldx);
+      static_cast<const float*>(x), static_cast<uint16_t*>(y3), N, H, W, C, ldx, 3 * C, C);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// the same into channels [0, C) of wider planes: rows ldy3 elements apart, plane p at column p * pstride
+TONY_API int tony_avgpool3_s1p1_x3p(const void* x, void* y3, int N, int H, int W, int C, int64_t ldx, int64_t ldy3,
+                                    int64_t pstride, hipStream_t stream) {
+  if (C % 8 || ldx % 4 || ldy3 % 8 || pstride % 8 || pstride < C || ldy3 < 2 * pstride + C ||
+      (reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(y3) & 15) ||
+      static_cast<int64_t>(N) * H * W * (C / 8) > 0x7fffffff)
+    return -1;
+  box3_x3_kernel<<<grid_for(static_cast<int64_t>(N) * H * W * (C / 8)), kThreads, 0, stream>>>(
+      static_cast<const float*>(x), static_cast<uint16_t*>(y3), N, H, W, C, ldx, ldy3, pstride);
   TONY_LAUNCH_CHECK();
   return 0;
 }

@@ -298,14 +298,19 @@ class FusedHead(nn.Module):
         self.conv = nn.Conv2d(cin, total, 1, bias=False)
         self.bn = nn.BatchNorm2d(total, eps=eps, momentum=momentum)
 
-    def forward(self, x, slots=None):
+    def forward(self, x, slots=None, planes=None):
         """One output per split (+ the pool branch); ``slots`` (per output, None or a concat.Slot)
-        lets final branch outputs land directly in the block's concat buffer."""
+        lets final branch outputs land directly in the block's concat buffer.  fp32 input: the x3 head
+        (ops/x3.py head), where ``planes[k]`` hands split k over as the next conv's operand planes only."""
         training = self.training
         args = (x, self.conv.weight, self.bn.weight, self.bn.bias, self.bn.running_mean, self.bn.running_var,
                 self.splits, self.npool, training, self.bn.momentum, self.bn.eps)
-        if x.is_cuda:
+        if x.is_cuda and x.dtype == torch.float32:
+            from . import x3
+
+            return x3.head(*args, slots=slots, planes=planes)
+        if x.is_cuda and x.dtype != torch.float64:
             if x.dtype != _BF16:
-                raise TypeError("FusedHead HIP path takes bf16 activations")
+                raise TypeError("FusedHead HIP path takes bf16 (or fp32: x3) activations")
             return tape.apply(_HeadFn, *args, tuple(slots) if slots else None)
         return head_reference(*args)

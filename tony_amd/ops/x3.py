@@ -403,6 +403,181 @@ def conv_bn_act(x, weight, gamma, beta, rmean, rvar, stride=1, padding=0, traini
     return y
 
 
+# ---- the fused 1x1 head of an Inception block (ops/fused.py FusedHead) on x3 planes -------------------
+def _o(t: torch.Tensor, elems: int) -> int:
+    return t.data_ptr() + elems * t.element_size()
+
+
+class _HeadX3Fn(torch.autograd.Function):
+    """FusedHead in fp32: every 1x1 conv that reads the block input as ONE x3 GEMM (N = sum of the splits
+    + the pool branch's width) with the BN statistics in its epilogue; per split a BN apply that writes
+    either the fp32 output (a concat slot) or only the operand planes of the next conv; the pool branch
+    pooled after its 1x1 (they commute) on pool_ch channels instead of Cin.  Backward: every split's BN
+    backward writes its slice of ONE [M, 3 * Ctot] dZ plane tensor (tony_bn_bwd_apply_f32_x3p; the pool
+    branch through the self-adjoint box filter, tony_avgpool3_s1p1_x3p), then one x3 dgrad (K = 3 Ctot,
+    no per-branch accumulation into dX) and one fused x3 wgrad.  Against the textbook graph's 3-4 head
+    convs: one dgrad writing the Cin-wide fp32 dX once instead of 3-4 read-modify-write passes, no box
+    filter over Cin fp32 channels in either direction, and 3-4x fewer launches."""
+
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, rmean, rvar, splits, npool, training, momentum, eps, slots, planes):
+        L = _lib.lib()
+        dev = x.device
+        st = _lib.stream_ptr(dev)
+        x3, cp = split_act(x)
+        w3 = wt_cache.x3_planes(weight)
+        if w3 is None:
+            w3 = split_weight(weight)
+        ctot = weight.shape[0]
+        stats = zeros_f32(_lib.stat_floats(ctot), dev) if training else None
+        z = conv_fwd(x3, cp, w3, weight.shape, 1, 0, stats)
+        n, _, h, w = z.shape
+        m = n * h * w
+        mean = torch.empty(ctot, dtype=_F32, device=dev)
+        invstd = torch.empty(ctot, dtype=_F32, device=dev)
+        mode = 0 if training else 1
+        ss = 2 * ctot
+
+        def sp(e):  # split statistics: sums at column e, sums of squares at ctot + e (none in inference)
+            return (_o(stats, e), _o(stats, ctot + e), ss) if training else (None, None, 0)
+
+        outs, plist = [], []
+        c0 = 0
+        for k, ci in enumerate(splits):
+            slot = slots[k] if slots and k < len(slots) else None
+            if planes and k < len(planes) and planes[k] and slot is None:
+                y3 = torch.empty((n, h, w, 3 * ci), dtype=_BF16, device=dev).permute(0, 3, 1, 2)
+                rc = L.tony_bn_apply_f32_x3(_o(z, c0), m, ci, ctot, y3.data_ptr(), 3 * ci, *sp(c0), _o(gamma, c0),
+                                            _o(beta, c0), 0, float(eps), 1, mode, _o(mean, c0), _o(invstd, c0),
+                                            _o(rmean, c0), _o(rvar, c0), float(momentum), st)
+                _lib.check(rc, "tony_bn_apply_f32_x3 (head)")
+                plist.append((k, y3, ci))
+                outs.append(torch.empty_strided((n, ci, h, w), (0, 0, 0, 0), dtype=_F32, device=dev))  # shape only
+            else:
+                y = concat.take(slot, n, ci, h, w, z)
+                if y is None:
+                    y = _cl(n, ci, h, w, dev)
+                rc = L.tony_bn_apply_f32(_o(z, c0), m, ci, ctot, y.data_ptr(), _rows_view(y)[2], *sp(c0),
+                                         _o(gamma, c0), _o(beta, c0), 0, float(eps), 1, mode, _o(mean, c0),
+                                         _o(invstd, c0), _o(rmean, c0), _o(rvar, c0), float(momentum), st)
+                _lib.check(rc, "tony_bn_apply_f32 (head)")
+                outs.append(y)
+            c0 += ci
+        p = None
+        if npool:
+            p = _cl(n, npool, h, w, dev)
+            rc = L.tony_avgpool3_s1p1_f32(_o(z, c0), p.data_ptr(), n, h, w, npool, ctot, npool, st)
+            _lib.check(rc, "tony_avgpool3_s1p1_f32 (head)")
+            pstats = None
+            if training:  # the pool branch's statistics are of the pooled columns
+                pstats = zeros_f32(_lib.stat_floats(npool), dev)
+                rc = L.tony_bn_stats_f32(p.data_ptr(), m, npool, npool, pstats.data_ptr(), _o(pstats, npool),
+                                         2 * npool, st)
+                _lib.check(rc, "tony_bn_stats_f32 (head pool)")
+            k = len(splits)
+            slot = slots[k] if slots and k < len(slots) else None
+            y = concat.take(slot, n, npool, h, w, z)
+            if y is None:
+                y = _cl(n, npool, h, w, dev)
+            rc = L.tony_bn_apply_f32(p.data_ptr(), m, npool, npool, y.data_ptr(), _rows_view(y)[2], _lib.ptr(pstats),
+                                     _o(pstats, npool) if training else 0, 2 * npool if training else 0,
+                                     _o(gamma, c0), _o(beta, c0), 0, float(eps), 1, mode, _o(mean, c0),
+                                     _o(invstd, c0), _o(rmean, c0), _o(rvar, c0), float(momentum), st)
+            _lib.check(rc, "tony_bn_apply_f32 (head pool)")
+            outs.append(y)
+        ctx.save_for_backward(x3, weight, gamma, beta, z, p, mean, invstd)
+        ctx.conf = (cp, tuple(x.shape), tuple(splits), npool, x.requires_grad)
+        ctx.join = getattr(x, "_tony_join", None)
+        _LAST_HEAD_PLANES[:] = plist
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *douts):
+        x3, weight, gamma, beta, z, p, mean, invstd = ctx.saved_tensors
+        cp, x_shape, splits, npool, need_dx = ctx.conf
+        L = _lib.lib()
+        dev = z.device
+        st = _lib.stream_ptr(dev)
+        n, ctot, h, w = z.shape
+        m = n * h * w
+        gw, gg, gb = _lib.grad_slot(weight), _lib.grad_slot(gamma), _lib.grad_slot(beta)
+        gw = gw if gw is not None and gw.dtype == _F32 and gw.is_contiguous(memory_format=torch.channels_last) \
+            else None
+        bn_slots = gg is not None and gb is not None and gg.dtype == _F32 and gb.dtype == _F32
+        dgamma = gg if bn_slots else torch.empty(ctot, dtype=_F32, device=dev)
+        dbeta = gb if bn_slots else torch.empty(ctot, dtype=_F32, device=dev)
+        acc = int(bn_slots)
+        d3 = _cl(n, 3 * ctot, h, w, dev, _BF16)  # [hi | lo | hi] planes of dZ, ctot channels each
+        dsum = zeros_f32(_lib.stat_floats(ctot), dev)
+        ss = 2 * ctot
+        c0 = 0
+        for k, ci in enumerate(splits):
+            dy = douts[k]
+            if dy is None:
+                dy = torch.zeros((n, ci, h, w), dtype=_F32, device=dev).contiguous(memory_format=torch.channels_last)
+            dy, (_, _, lddy) = _as_rows(dy)
+            rc = L.tony_bn_bwd_reduce_f32(_o(z, c0), ctot, dy.data_ptr(), lddy, m, ci, _o(mean, c0), _o(invstd, c0),
+                                          _o(gamma, c0), _o(beta, c0), 0, 1, _o(dsum, c0), _o(dsum, ctot + c0), ss, st)
+            _lib.check(rc, "tony_bn_bwd_reduce_f32 (head)")
+            rc = L.tony_bn_bwd_apply_f32_x3p(_o(z, c0), ctot, dy.data_ptr(), lddy, _o(d3, c0), 3 * ctot, ctot, m, ci,
+                                             _o(mean, c0), _o(invstd, c0), _o(gamma, c0), _o(beta, c0), 0, 1,
+                                             _o(dsum, c0), _o(dsum, ctot + c0), ss, _o(dgamma, c0), _o(dbeta, c0), acc,
+                                             st)
+            _lib.check(rc, "tony_bn_bwd_apply_f32_x3p (head)")
+            c0 += ci
+        if npool:
+            dy = douts[len(splits)]
+            if dy is None:
+                dy = torch.zeros((n, npool, h, w), dtype=_F32, device=dev).contiguous(memory_format=torch.channels_last)
+            dy, (_, _, lddy) = _as_rows(dy)
+            dp = _cl(n, npool, h, w, dev)
+            rc = L.tony_bn_bwd_reduce_f32(p.data_ptr(), npool, dy.data_ptr(), lddy, m, npool, _o(mean, c0),
+                                          _o(invstd, c0), _o(gamma, c0), _o(beta, c0), 0, 1, _o(dsum, c0),
+                                          _o(dsum, ctot + c0), ss, st)
+            _lib.check(rc, "tony_bn_bwd_reduce_f32 (head pool)")
+            rc = L.tony_bn_bwd_apply_f32(p.data_ptr(), npool, dy.data_ptr(), lddy, dp.data_ptr(), npool, m, npool,
+                                         _o(mean, c0), _o(invstd, c0), _o(gamma, c0), _o(beta, c0), 0, 1, _o(dsum, c0),
+                                         _o(dsum, ctot + c0), ss, _o(dgamma, c0), _o(dbeta, c0), acc, st)
+            _lib.check(rc, "tony_bn_bwd_apply_f32 (head pool)")
+            # the pool's input gradient (box3 is self-adjoint) straight into the pool columns of the dZ planes
+            rc = L.tony_avgpool3_s1p1_x3p(dp.data_ptr(), _o(d3, c0), n, h, w, npool, npool, 3 * ctot, ctot, st)
+            _lib.check(rc, "tony_avgpool3_s1p1_x3p (head pool)")
+        wshape = weight.shape
+        if gw is not None:
+            dw = streams.run(lambda: conv_wgrad(d3, x3, cp, wshape, 1, 0, dst=gw), d3, x3)
+        else:
+            dw = conv_wgrad(d3, x3, cp, wshape, 1, 0)
+        dx = None
+        if need_dx and ctx.needs_input_grad[0]:
+            join = ctx.join
+            pend = join.take() if join is not None else None
+            wt3 = wt_cache.x3_planes_t(weight)
+            if wt3 is None:
+                wt3 = split_weight_t(weight)
+            dx = conv_dgrad(d3, wt3, ctot, x_shape, wshape, 1, 0, accum=pend)
+            if join is not None:
+                dx = join.settle(dx)
+            streams.keep(dx)
+        _lib.report_inplace((weight, gamma, beta), (dw, None if bn_slots else dgamma, None if bn_slots else dbeta))
+        return (dx, dw, None if bn_slots else dgamma, None if bn_slots else dbeta) + (None,) * 9
+
+
+_LAST_HEAD_PLANES = []
+
+
+def head(x, weight, gamma, beta, rmean, rvar, splits, npool, training, momentum, eps, slots=None, planes=None):
+    """The fp32 FusedHead (ops/fused.py): one output per split (+ the pool branch).  ``planes[k]``: split k
+    feeds only x3 convs -- it comes back as a shape-only tensor carrying its operand planes (conv_bn_act
+    planes_only); ``slots[k]``: write split k's fp32 output into a block's concat buffer."""
+    _LAST_HEAD_PLANES[:] = []
+    outs = _HeadX3Fn.apply(x, weight, gamma, beta, rmean, rvar, tuple(splits), int(npool), training, momentum, eps,
+                           tuple(slots) if slots else None, tuple(planes) if planes else None)
+    for k, y3, ci in _LAST_HEAD_PLANES:
+        outs[k]._tony_x3 = (outs[k]._version, y3, ci)
+    _LAST_HEAD_PLANES[:] = []
+    return outs
+
+
 # ---- the classifier: an x3 GEMM --------------------------------------------------------------------
 class _LinearX3Fn(torch.autograd.Function):
     @staticmethod

@@ -30,7 +30,13 @@ def main():
     arms = [("base", {})]
     for spec in a.arms:
         name, _, rest = spec.partition("=")
-        env = dict(kv.split("=", 1) for kv in rest.split(",") if kv)
+        env, last = {}, None
+        for kv in rest.split(","):
+            if "=" in kv:
+                last, val = kv.split("=", 1)
+                env[last] = val
+            elif kv and last is not None:  # a comma inside a value (TONY_STREAMK=1,2)
+                env[last] += "," + kv
         arms.append((name, env))
     out = {}
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
