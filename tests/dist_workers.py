@@ -149,3 +149,39 @@ def kv_rank(role, index, num_servers, num_workers, port, kind, steps, device="cp
            "big": big.cpu(), "plane_ops": list(getattr(store, "plane_ops", [0, 0]))}
     store.close()
     return res
+
+
+def kv_bulk_rank(role, index, num_servers, num_workers, port, kind, steps, keys, key_mb):
+    """``keys`` keys of ``key_mb`` MB each through the kvstore GPU plane; per-step wall time of one
+    push-all + pull-all round (the host never waits for a payload: timed to a device synchronize)."""
+    import time
+
+    os.environ.update(DMLC_ROLE=role, DMLC_NUM_SERVER=str(num_servers), DMLC_NUM_WORKER=str(num_workers),
+                      DMLC_PS_ROOT_URI="127.0.0.1", DMLC_PS_ROOT_PORT=str(port), TASK_INDEX=str(index),
+                      TONY_KV_WINDOW_MB=str(num_workers * keys * key_mb + 64))
+    import tony_amd.kv as kv
+
+    if kv.run_role():
+        return {"role": role}
+    store = kv.create(kind)
+    n = key_mb * (1 << 20) // 4
+    vals = [torch.zeros(n, device="cuda") for _ in range(keys)]
+    for k, v in enumerate(vals):
+        store.init(k, v)
+    store.set_optimizer(kv.create_optimizer("sgd", learning_rate=0.5, rescale_grad=1.0 / num_workers))
+    ramp = torch.arange(n, dtype=torch.float32, device="cuda") / n
+    grads = [ramp * (store.rank + 1) + k for k in range(keys)]
+    times = []
+    for _ in range(steps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(keys):
+            store.push(k, grads[k])
+        for k in range(keys):
+            store.pull(k, out=vals[k])
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    res = {"role": role, "rank": store.rank, "times": times, "plane_ops": list(store.plane_ops),
+           "v0": vals[0][:: n // 64].cpu(), "vlast": vals[-1][:: n // 64].cpu(), "n": n}
+    store.close()
+    return res

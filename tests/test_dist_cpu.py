@@ -276,14 +276,16 @@ def test_kvstore_plane_layout_agrees_between_server_and_workers(monkeypatch):
                 assert server.add_key(k, n) == fits[k]
                 if fits[k]:
                     assert server.keys[k] == worker.keys[k]
-    spans = {}
-    for k, (s, n, row, land) in worker.keys.items():
+    spans, slots = {}, {}
+    for k, (s, n, row, land, slot) in worker.keys.items():
         assert row % 16 == 0 and land % 16 == 0 and land // worker.region == s
+        slots.setdefault(s, []).append(slot)  # each server's device-flag slots: 0, 1, ... in init order
         spans.setdefault(("row", s), []).append((row, row + 3 * ((n + 15) // 16 * 16)))
         spans.setdefault(("land",), []).append((land, land + n))
     for v in spans.values():
         v.sort()
         assert all(a[1] <= b[0] for a, b in zip(v, v[1:]))
+    assert all(v == list(range(len(v))) for v in slots.values())
 
 
 def test_kv_server_parks_a_plane_push_that_arrives_before_init(monkeypatch):
@@ -312,9 +314,12 @@ def test_kv_server_parks_a_plane_push_that_arrives_before_init(monkeypatch):
         def add_key(self, kid, nbytes):
             return self.layout.add_key(kid, nbytes)
 
-        def copy(self, dst, src, nbytes, wait=True):
+        def take(self, kid, w, numel, dtype):  # _KvPlane.take without the device flag wait
+            _, nbytes, row_off, _, _ = self.keys[kid]
+            buf = torch.empty(numel, dtype=dtype)
             self.copies.append(nbytes)
-            ctypes.memmove(dst, src, nbytes)
+            ctypes.memmove(buf.data_ptr(), self.base + row_off + w * kvs._pad16(nbytes), nbytes)
+            return buf, None
 
     plane = HostPlane()
     srv = kvs._Server(topo, sync=False, plane=plane)
@@ -322,7 +327,7 @@ def test_kv_server_parks_a_plane_push_that_arrives_before_init(monkeypatch):
     # worker 1 (global rank 2) wrote its row -- at the offset the layout WILL give the key -- then sent the header
     lay = kvs._KvLayout(topo, window.numel())
     lay.add_key(kid, 4 * n)
-    _, nbytes, row_off, _ = lay.keys[kid]
+    _, nbytes, row_off, _, _ = lay.keys[kid]
     row = torch.tensor([1.0, 2.0, 3.0])
     ctypes.memmove(window.data_ptr() + row_off + 1 * kvs._pad16(nbytes), row.data_ptr(), nbytes)
     assert srv.handle(2, [kvs.OP_PUSH_X, kid, n, kvs._dcode(torch.float32)]) is True

@@ -45,3 +45,29 @@ def test_kvstore_server_modes_move_payloads_on_the_gpu_plane(kind):
     else:
         final = min(float(o["seen"][-1][0]) for o in workers)
         assert final == pytest.approx(-2.25)
+
+
+def test_kvstore_plane_bulk_keys_sync_timed():
+    """64 MB of keys (8 x 8 MB) per round through dist_sync on the GPU plane: the host never waits for a
+    payload (device flags, ``tony_kv_copy_flag`` / ``tony_kv_wait``), every push / pull rides the plane,
+    and the values follow the closed-form SGD result.  Prints the per-round time and per-push latency."""
+    port, steps, keys, mb = _port(), 4, 8, 8
+    args = [("scheduler", 0, 1, 2, port, "dist_sync", steps, keys, mb),
+            ("server", 0, 1, 2, port, "dist_sync", steps, keys, mb),
+            ("worker", 0, 1, 2, port, "dist_sync", steps, keys, mb),
+            ("worker", 1, 1, 2, port, "dist_sync", steps, keys, mb)]
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(len(args)) as pool:
+        outs = [r.get(110) for r in [pool.apply_async(W.kv_bulk_rank, a) for a in args]]
+    workers = [o for o in outs if o["role"] == "worker"]
+    for o in workers:
+        assert o["plane_ops"] == [steps * keys, steps * keys], o["plane_ops"]
+        n = o["n"]
+        ramp = torch.arange(0, n, n // 64, dtype=torch.float32) / n
+        # per round: w -= 0.5 * (grad_0 + grad_1) / 2, grad_r = ramp * (r + 1) + k
+        torch.testing.assert_close(o["v0"], -0.5 * steps * (1.5 * ramp), rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(o["vlast"], -0.5 * steps * (1.5 * ramp + keys - 1), rtol=1e-5, atol=1e-5)
+        steady = sorted(o["times"][1:])[len(o["times"][1:]) // 2]
+        print(f"worker {o['rank']}: round of {keys} x {mb} MB push + pull: {steady * 1e3:.2f} ms "
+              f"({steady * 1e3 / keys:.3f} ms per key push+pull, {2 * keys * mb / 1024 / steady:.1f} GB/s "
+              f"moved per worker); all rounds {[round(t * 1e3, 2) for t in o['times']]}")

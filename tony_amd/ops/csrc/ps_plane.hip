@@ -323,7 +323,64 @@ __global__ __launch_bounds__(256) void kv_copy_kernel(const uint8_t* __restrict_
     for (int64_t i = n16 << 4; i < bytes; ++i) dst[i] = src[i];
 }
 
+// kvstore hand-off with a device flag: the copy above, then every workgroup publishes its part with a
+// system-scope fence and one add to a u32 counter in the consumer's window (a peer's: the adds go over
+// xGMI).  The consumer learns the whole copy landed when the counter reaches its expected total
+// (kv_copy_blocks per copy, cumulative), without a host synchronisation on either side.
+__global__ __launch_bounds__(256) void kv_copy_flag_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                            int64_t bytes, uint32_t* flag) {
+  const int64_t n16 = bytes >> 4;
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n16;
+       i += static_cast<int64_t>(gridDim.x) * 256)
+    d[i] = s[i];
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (int64_t i = n16 << 4; i < bytes; ++i) dst[i] = src[i];
+  __threadfence_system();  // this workgroup's bytes are visible to the consumer before its add
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// the consumer side: one wave waits (bounded) until *flag reaches target; the stream's next kernel (the
+// copy out of the window) then reads bytes that landed.  A timeout records the error word and returns.
+__global__ __launch_bounds__(64) void kv_wait_kernel(const uint32_t* flag, uint32_t target, uint64_t budget, int* err) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = wall_clock64();
+  wait_flag(flag, target, t0, budget, err);
+}
+
+int kv_copy_blocks(int64_t bytes) {
+  const int64_t n16 = (bytes >> 4) + 1;
+  return static_cast<int>(std::min<int64_t>(1024, (n16 + 255) / 256));
+}
+
 }  // namespace
+
+// workgroups of one flagged copy of `bytes` (the consumer's counter target grows by this per copy)
+TONY_API int tony_kv_copy_blocks(int64_t bytes) { return bytes <= 0 ? 0 : kv_copy_blocks(bytes); }
+
+// dst <- src and a flag add per workgroup (tony_kv_copy_blocks(bytes) adds in all) into *flag
+TONY_API int tony_kv_copy_flag(void* dst, const void* src, int64_t bytes, void* flag, hipStream_t stream) {
+  if (dst == nullptr || src == nullptr || flag == nullptr || bytes <= 0 || (reinterpret_cast<uintptr_t>(dst) & 15) ||
+      (reinterpret_cast<uintptr_t>(src) & 15) || (reinterpret_cast<uintptr_t>(flag) & 3))
+    return -1;
+  kv_copy_flag_kernel<<<kv_copy_blocks(bytes), 256, 0, stream>>>(static_cast<const uint8_t*>(src),
+                                                                 static_cast<uint8_t*>(dst), bytes,
+                                                                 static_cast<uint32_t*>(flag));
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// stream-ordered wait until the u32 counter at *flag (in this rank's window) reaches target; a wait
+// longer than budget_s records the error word of `window` (tony_ps_error reads it)
+TONY_API int tony_kv_wait(const void* flag, uint32_t target, void* window, double budget_s, hipStream_t stream) {
+  if (flag == nullptr || window == nullptr || (reinterpret_cast<uintptr_t>(flag) & 3)) return -1;
+  kv_wait_kernel<<<1, 64, 0, stream>>>(static_cast<const uint32_t*>(flag), target, budget_ticks(budget_s),
+                                       reinterpret_cast<int*>(static_cast<uint8_t*>(window) + kErrOff));
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
 
 // dst <- src (bytes), both 16-B aligned device addresses (local memory or a mapped peer window)
 TONY_API int tony_kv_copy(void* dst, const void* src, int64_t bytes, hipStream_t stream) {

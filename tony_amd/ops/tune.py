@@ -19,9 +19,10 @@ import torch
 AUTOTUNE = os.environ.get("TONY_CONV_AUTOTUNE", "1") != "0"
 # csrc/mfma_common.h kNtVariants (0-8) + 9: conv.hip halo-tile 3x3 path, 10: conv.hip persistent
 # direct 3x3 kernel (32/64 channels), 11-15: conv.hip LDS-DMA kernels, 16-19: their 8-wave 256-row
-# tiles, 20-24: interleaved-issue forms (igemm.h kGldsVariants; TONY_CONV_GLDS=0 leaves them all out of
-# the search, TONY_CONV_GLDS8=0 the 8-wave and interleaved ones, TONY_CONV_GLDS_IL=0 the interleaved)
-_N_GLDS = (25 if os.environ.get("TONY_CONV_GLDS_IL", "1") != "0" else 20) \
+# tiles, 20-24: interleaved-issue forms, 25-26: the 256 x 192 tile on 64-deep two-slot rings (igemm.h
+# kGldsVariants; TONY_CONV_GLDS=0 leaves them all out of the search, TONY_CONV_GLDS8=0 the 8-wave and
+# interleaved ones, TONY_CONV_GLDS_IL=0 the interleaved and two-slot ones)
+_N_GLDS = (27 if os.environ.get("TONY_CONV_GLDS_IL", "1") != "0" else 20) \
     if os.environ.get("TONY_CONV_GLDS8", "1") != "0" else 16
 _BASE = tuple(range(_N_GLDS if os.environ.get("TONY_CONV_GLDS", "1") != "0" else 11))
 # + stream-K forms of the LDS-DMA variants (csrc/igemm.h SplitK): candidate v + 256 * m, i.e. flags bits

@@ -31,11 +31,17 @@ GPU payload plane (``TONY_KV_PLANE=xgmi``, the default when every member sees a 
 allocates an IPC-mapped window on its GPU (csrc/ps_plane.hip) and maps its peers' -- a worker the
 servers', a server the workers'.  A pushed GPU tensor is stored by a copy kernel straight into its
 row of the owning server's window and only the header goes over gloo; the server replies to a pull
-by storing the value into the worker's landing area and sending a one-element token.  The payload
+by storing the value into the worker's landing area.  Neither side waits on the host: every copy
+kernel's workgroups add to a u32 counter in the consumer's window header after their bytes
+(``tony_kv_copy_flag``), and the consumer's stream waits on the device for the counter to reach the
+copy's cumulative total (``tony_kv_wait``, bounded by ``TONY_KV_WAIT_S``; a timeout sets the window's
+error word, which ``barrier`` / ``close`` raise) before the kernel that reads the bytes.  The payload
 bytes never leave the GPUs (xGMI between devices; the server may share a worker's GPU, like TonY's
-0-GPU ps).  Keys that do not fit the windows (``TONY_KV_WINDOW_MB``) and CPU tensors keep the gloo
-payload.  A worker re-pushing a key before pulling it (its last row may not have been read yet) sends
-that push over gloo: a pull reply is what proves the server consumed the row.
+0-GPU ps).  Keys that do not fit the windows (``TONY_KV_WINDOW_MB``) or the flag tables, and CPU
+tensors, keep the gloo payload.  A worker re-pushing a key before pulling it (its last row may not have
+been read yet) sends that push over gloo: the pull's reply is what orders the server's read of the row
+before the worker's next store into it (the server reads the row on its stream before it stores the
+reply; the worker's next push is issued behind its wait for that reply).
 """
 from __future__ import annotations
 
@@ -261,6 +267,25 @@ def _pad16(n: int) -> int:
     return (n + 15) // 16 * 16
 
 
+# device flag tables in a plane window's header (csrc/ps_plane.hip: the first 1 MiB is the PS plane's
+# arrival table, unused by a kvstore process): a server's push counters [key slot][worker], a worker's
+# reply counters [server][key slot]
+_MAX_SLOTS, _MAX_KV_WORKERS = 4096, 64
+_REPLY_FLAGS = 4 * _MAX_SLOTS * _MAX_KV_WORKERS
+
+
+def _push_flag(slot: int, worker: int) -> int:
+    return 4 * (slot * _MAX_KV_WORKERS + worker)
+
+
+def _reply_flag(topo: "_Topology", server: int, slot: int) -> int:
+    return _REPLY_FLAGS + 4 * (server * (_MAX_SLOTS // max(1, topo.num_servers)) + slot)
+
+
+def _wait_budget_s() -> float:
+    return float(os.environ.get("TONY_KV_WAIT_S", "300"))
+
+
 def _plane_wanted() -> bool:
     mode = os.environ.get("TONY_KV_PLANE", "auto").lower()
     if mode in ("gloo", "0", "off"):
@@ -281,16 +306,20 @@ class _KvLayout:
         self.region = window_bytes // max(1, topo.num_servers) // 16 * 16  # a worker's landing region per server
         self.row_used = [0] * topo.num_servers
         self.land_used = [0] * topo.num_servers
-        self.keys: Dict[int, tuple] = {}  # kid -> (server, nbytes, row_off, land_off)
+        self.slots = [0] * topo.num_servers
+        self.keys: Dict[int, tuple] = {}  # kid -> (server, nbytes, row_off, land_off, flag slot)
 
     def add_key(self, kid: int, nbytes: int) -> bool:
         s = self.topo.server_of(kid)
         rows = self.topo.num_workers * _pad16(nbytes)
-        if self.row_used[s] + rows > self.bytes or self.land_used[s] + _pad16(nbytes) > self.region:
+        if (self.row_used[s] + rows > self.bytes or self.land_used[s] + _pad16(nbytes) > self.region
+                or self.slots[s] >= _MAX_SLOTS // max(1, self.topo.num_servers)
+                or self.topo.num_workers > _MAX_KV_WORKERS):
             return False  # stays on the gloo payload path (decided identically on every member)
-        self.keys[kid] = (s, nbytes, self.row_used[s], s * self.region + self.land_used[s])
+        self.keys[kid] = (s, nbytes, self.row_used[s], s * self.region + self.land_used[s], self.slots[s])
         self.row_used[s] += rows
         self.land_used[s] += _pad16(nbytes)
+        self.slots[s] += 1
         return True
 
 
@@ -318,6 +347,7 @@ class _KvPlane:
             raise RuntimeError("a peer could not allocate its window")
         self.base = self.window + hdr
         self.peer: Dict[int, int] = {}
+        self.peer_win: Dict[int, int] = {}  # window bases (flag tables) of the peers
         peers = range(topo.num_servers, topo.world) if topo.role == "server" else range(topo.num_servers)
         for r in peers:
             p = ctypes.c_void_p()
@@ -325,22 +355,80 @@ class _KvPlane:
             with torch.cuda.device(device):
                 _lib.check(self.L.tony_xgmi_open(buf, ctypes.byref(p)), f"tony_xgmi_open(rank {r})")
             self.peer[r] = p.value + hdr
+            self.peer_win[r] = p.value
             self._opened.append(p.value)
         self.layout = _KvLayout(topo, self.bytes)
         self.keys = self.layout.keys
+        self._side: Dict[int, "torch.cuda.Stream"] = {}  # server: per pushing worker, waits + row reads
+        self._arrived: Dict[tuple, int] = {}  # server: (kid, worker) -> flag counts expected so far
 
     def add_key(self, kid: int, nbytes: int) -> bool:
         return self.layout.add_key(kid, nbytes)
 
-    def copy(self, dst: int, src: int, nbytes: int, wait: bool = True) -> None:
+    def copy(self, dst: int, src: int, nbytes: int) -> None:
+        """Stream-ordered local copy (out of this rank's window, or into a tensor)."""
         from ..ops import _lib
 
         with torch.cuda.device(self.device):
             _lib.check(self.L.tony_kv_copy(dst, src, nbytes, _lib.stream_ptr(self.device)), "tony_kv_copy")
-            if wait:
-                torch.cuda.current_stream(self.device).synchronize()  # landed before the header / token is sent
+
+    def send(self, dst: int, src: int, nbytes: int, flag: int) -> int:
+        """Copy into a peer's window and count it on the peer's flag at window offset ``flag`` (no host
+        wait); returns the count the copy adds (the consumer's target grows by it)."""
+        from ..ops import _lib
+
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.tony_kv_copy_flag(dst, src, nbytes, flag, _lib.stream_ptr(self.device)),
+                       "tony_kv_copy_flag")
+        return self.L.tony_kv_copy_blocks(nbytes)
+
+    def take(self, kid: int, w: int, numel: int, dtype: torch.dtype):
+        """Server: worker w's pushed row of kid as a new tensor, and the event after its read.  The row has
+        landed once the worker's copy counted all its workgroups on the key's push flag.  The wait and
+        the read run on the worker's own stream: the bytes may depend on a reply this server has yet to
+        store (the worker pushes behind its wait for its last pull), so nothing else may queue behind
+        the wait.  The worker rewrites the row only behind its wait for a later reply, which the server
+        stores after merging this round -- no host wait on either side."""
+        _, nbytes, row_off, _, slot = self.keys[kid]
+        side = self._side.get(w)
+        if side is None:
+            side = self._side[w] = torch.cuda.Stream(self.device)
+        main = torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(side):
+            buf = torch.empty(numel, dtype=dtype, device=self.device)
+            n = self._arrived[(kid, w)] = self._arrived.get((kid, w), 0) + self.L.tony_kv_copy_blocks(nbytes)
+            self.wait(_push_flag(slot, w), n)
+            self.copy(buf.data_ptr(), self.base + row_off + w * _pad16(nbytes), nbytes)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        buf.record_stream(main)
+        return buf, ev
+
+    def wait(self, flag_off: int, target: int) -> None:
+        """Hold this rank's stream until the counter at ``flag_off`` of its window reaches ``target``."""
+        from ..ops import _lib
+
+        with torch.cuda.device(self.device):
+            _lib.check(self.L.tony_kv_wait(self.window + flag_off, target & 0xFFFFFFFF, self.window,
+                                           _wait_budget_s(), _lib.stream_ptr(self.device)), "tony_kv_wait")
+
+    def check(self) -> None:
+        """Raise if one of this rank's device waits timed out (synchronises the device)."""
+        import ctypes
+
+        from ..ops import _lib
+
+        with torch.cuda.device(self.device):
+            torch.cuda.synchronize(self.device)
+            err = ctypes.c_int(0)
+            _lib.check(self.L.tony_ps_error(self.window, ctypes.byref(err)), "tony_ps_error")
+        if err.value:
+            raise RuntimeError(f"kvstore plane: a device wait timed out after {_wait_budget_s()} s "
+                               "(TONY_KV_WAIT_S): a peer never delivered its payload")
 
     def close(self) -> None:
+        if getattr(self, "window", None) is not None:
+            torch.cuda.synchronize(self.device)  # no copy into or out of a window is left in flight
         for p in self._opened:
             self.L.tony_xgmi_close(p)
         self._opened = []
@@ -390,25 +478,37 @@ class _Server:
         self.sync = sync
         self.plane = plane
         self.values: Dict[int, torch.Tensor] = {}
-        self.accum: Dict[int, torch.Tensor] = {}
         self.pushed: Dict[int, set] = {}
         self.deferred: Dict[int, List[int]] = {}
         self.opt: Optional[Optimizer] = None
         self.early: Dict[int, list] = {}
         self.sends = []
         self.applied = 0
+        self.round: Dict[int, list] = {}  # kid -> [(worker, arrival, payload, event)] of the open round
 
     def _reply(self, kid: int, worker: int, via_plane: bool = False) -> None:
-        if via_plane:  # the value into the worker's landing area, then a one-element token
-            _, nbytes, _, land_off = self.plane.keys[kid]
+        if via_plane:  # the value into the worker's landing area, counted on the worker's reply flag
+            srv, nbytes, _, land_off, slot = self.plane.keys[kid]
             v = self.values[kid].contiguous()
-            self.plane.copy(self.plane.peer[worker] + land_off, v.data_ptr(), nbytes)
-            self.sends.append(dist.isend(torch.ones(1, dtype=torch.int64), worker, tag=TAG_REPLY))
+            self.plane.send(self.plane.peer[worker] + land_off, v.data_ptr(), nbytes,
+                            self.plane.peer_win[worker] + _reply_flag(self.topo, srv, slot))
             return
         self.sends.append(dist.isend(self.values[kid].contiguous().cpu(), worker, tag=TAG_REPLY))
 
+    def _merge_round(self, kid: int) -> torch.Tensor:
+        """The open round's pushes of kid summed in worker order (deterministic), on this stream after
+        every plane push's row read (device events: the host never waits for a payload)."""
+        v = self.values[kid]
+        merged = None
+        for _, _, b, ev in sorted(self.round.pop(kid), key=lambda e: (e[0], e[1])):
+            if ev is not None:
+                torch.cuda.current_stream(v.device).wait_event(ev)
+            b = b.to(v.device, v.dtype)  # every payload buffer is this server's own: summed in place
+            merged = b if merged is None else merged.add_(b)
+        return merged
+
     def _finish_round(self, kid: int) -> None:
-        merged = self.accum.pop(kid)
+        merged = self._merge_round(kid)
         if self.opt is not None:
             self.opt.update(kid, self.values[kid], merged)
         else:
@@ -431,13 +531,9 @@ class _Server:
             # the worker does not rewrite that row before its next pull (DistKVStore._unread)
             self.early.setdefault(kid, []).append((worker, hdr, buf))
             return True
+        ev = None
         if op == OP_PUSH_X:  # the payload is in this worker's receive row of the window: take it now
-            _, nbytes, row_off, _ = self.plane.keys[kid]
-            buf = torch.empty(numel, dtype=_DTYPES[dcode], device=self.plane.device)
-            w = worker - self.topo.num_servers
-            # stream-ordered, no host wait: the worker rewrites this row only after its pull, whose reply
-            # copy is issued behind this one on the same stream and waited for before the token goes out
-            self.plane.copy(buf.data_ptr(), self.plane.base + row_off + w * _pad16(nbytes), nbytes, wait=False)
+            buf, ev = self.plane.take(kid, worker - self.topo.num_servers, numel, _DTYPES[dcode])
             op = OP_PUSH
         elif op == OP_PULL_X:
             op = OP_PULL
@@ -451,13 +547,12 @@ class _Server:
                     self.handle(w, h, b)
             elif op == OP_OPT:
                 self.opt = Optimizer.from_json(bytes(buf.tolist()).decode())
-            elif not self.sync:
-                self.accum[kid] = buf.to(self.values[kid].device)
-                self._finish_round(kid)
             else:
-                acc = self.accum.get(kid)
-                v = self.values[kid]
-                self.accum[kid] = buf.to(v.device, v.dtype) if acc is None else acc.add_(buf.to(acc.device))
+                r = self.round.setdefault(kid, [])
+                r.append((worker, len(r), buf, ev))
+                if not self.sync:
+                    self._finish_round(kid)
+                    return True
                 self.pushed[kid].add(worker)
                 if len(self.pushed[kid]) == self.topo.num_workers:
                     self._finish_round(kid)
@@ -518,6 +613,7 @@ class DistKVStore(KVStore):
         self.store.set("tony/kv/type", kind)
         self._shapes: Dict[int, torch.Size] = {}
         self._unread: set = set()  # keys pushed on the plane and not pulled since (their row may be unread)
+        self._replies: Dict[int, int] = {}  # kid -> reply copies counted on this worker's flag (target)
         self.plane_ops = [0, 0]  # pushes / pulls whose payload went over the GPU plane (tests)
         self._closed = False
 
@@ -556,11 +652,14 @@ class DistKVStore(KVStore):
             kid = self._key(k)
             g = _merge(_as_list(v)).reshape(-1)
             if self._on_plane(kid, g) and kid not in self._unread:
-                srv, nbytes, row_off, _ = self.plane.keys[kid]
+                srv, nbytes, row_off, _, slot = self.plane.keys[kid]
                 g = g.to(self.plane.device).contiguous()
                 if g.data_ptr() % 16:  # the copy kernel moves 16-B aligned addresses: a view at an odd offset
                     g = g.clone()
-                self.plane.copy(self.plane.peer[srv] + row_off + self.rank * _pad16(nbytes), g.data_ptr(), nbytes)
+                # into this worker's row of the server's window, counted on the key's push flag there; the
+                # header may overtake the bytes: the server's stream waits for the flag before reading
+                self.plane.send(self.plane.peer[srv] + row_off + self.rank * _pad16(nbytes), g.data_ptr(), nbytes,
+                                self.plane.peer_win[srv] + _push_flag(slot, self.rank))
                 dist.send(torch.tensor([OP_PUSH_X, kid, g.numel(), _dcode(g.dtype)], dtype=torch.int64), srv,
                           tag=TAG_HDR)
                 self._unread.add(kid)
@@ -574,10 +673,12 @@ class DistKVStore(KVStore):
             kid = self._key(k)
             first = _as_list(o)[0]
             if self._on_plane(kid, first):
-                srv, nbytes, _, land_off = self.plane.keys[kid]
+                srv, nbytes, _, land_off, slot = self.plane.keys[kid]
                 dist.send(torch.tensor([OP_PULL_X, kid, 0, 0], dtype=torch.int64), srv, tag=TAG_HDR)
-                tok = torch.empty(1, dtype=torch.int64)
-                dist.recv(tok, srv, tag=TAG_REPLY)  # the value is in this worker's landing area
+                # the reply lands in this worker's landing area, counted on its reply flag: this stream waits
+                # for it on the device, then copies it out -- the host moves on at once
+                n = self._replies[kid] = self._replies.get(kid, 0) + self.plane.L.tony_kv_copy_blocks(nbytes)
+                self.plane.wait(_reply_flag(self.topo, srv, slot), n)
                 buf = torch.empty(first.numel(), dtype=first.dtype, device=self.plane.device)
                 self.plane.copy(buf.data_ptr(), self.plane.base + land_off, nbytes)
                 self._unread.discard(kid)  # the server answered: it consumed this worker's earlier rows
@@ -604,6 +705,8 @@ class DistKVStore(KVStore):
         dist.send(payload, srv, tag=TAG_DATA)
 
     def barrier(self) -> None:
+        if self.plane is not None:
+            self.plane.check()
         dist.barrier(group=self.workers)
 
     def save_optimizer_states(self, fname: str, dump_optimizer: bool = False) -> None:
