@@ -455,3 +455,33 @@ def test_x3_fused_head_matches_float64(cuda, cfg):
     assert _rel(hd.bn.weight.grad, gd.grad) < 1e-4
     assert _rel(hd.bn.bias.grad, bd.grad) < 1e-4
     assert _rel(hd.bn.running_mean, rm) < 1e-4 and _rel(hd.bn.running_var, rv) < 1e-4
+
+
+@pytest.mark.parametrize("code", [23 + 256, 11 + 256, 15 + 512], ids=["v23-m1", "v11-m1", "v15-m2"])
+def test_x3_conv_streamk_matches_plain(cuda, code, monkeypatch):
+    """The x3 convs offered stream-K forms (tune.X3_VARIANTS): forward with the fp32 epilogue + BN
+    statistics and backward-data with the fp32 accumulating epilogue (flags 8 | 16), each pinned to a
+    stream-K code and to its plain variant -- the fold of the partial tiles must give the plain result."""
+    from tony_amd.ops import _lib, tune, x3
+
+    n, c, h, w, co, k, p = 8, 192, 17, 17, 192, (1, 7), (0, 3)
+    torch.manual_seed(0)
+    xf = _cl(torch.randn(n, c, h, w, device=cuda))
+    wt = _cl(torch.randn(co, c, *k, device=cuda) / (c * 7) ** 0.5)
+    dyf = _cl(torch.randn(n, co, h, w, device=cuda))
+    xp, cp = x3.split_act(xf)
+    dp, _ = x3.split_act(dyf)
+    outs = {}
+    for pin in (code, code % 256):
+        monkeypatch.setattr(tune, "_CACHE", {})
+        monkeypatch.setattr(tune, "pick", lambda key, launch, variants=None, _p=pin: _p << 8
+                            if launch(_p << 8) == 0 else pytest.fail(f"code {_p} refused"))
+        stats = torch.zeros(_lib.stat_floats(co), device=cuda)
+        z = x3.conv_fwd(xp, cp, x3.split_weight(wt), wt.shape, 1, p, stats)
+        acc = _cl(torch.randn(n, c, h, w, device=cuda, generator=torch.Generator(cuda).manual_seed(5)))
+        dx = x3.conv_dgrad(dp, x3.split_weight_t(wt), co, xf.shape, wt.shape, 1, p, accum=acc)
+        torch.cuda.synchronize()
+        outs[pin] = (z.clone(), _lib.fold_stats(stats, co).clone(), dx.clone())
+    (z1, s1, d1), (z0, s0, d0) = outs[code], outs[code % 256]
+    assert _rel(z1, z0) < 1e-6 and _rel(d1, d0) < 1e-6
+    torch.testing.assert_close(s1, s0, rtol=1e-5, atol=1e-3)

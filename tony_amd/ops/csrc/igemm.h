@@ -150,10 +150,9 @@ constexpr GldsVariant kGldsVariants[] = {
     {256, 192, 4, 32, 4}, {256, 128, 3, 64, 4}, {256, 192, 5, 32, 4}, {256, 128, 3, 32, 4},
     // 20-24: the interleaved-issue forms of the most-picked tiles (11-19 above)
     {128, 128, 3, 32, 2, true}, {128, 192, 3, 32, 2, true}, {128, 128, 2, 64, 2, true},
-    {256, 192, 4, 32, 4, true}, {256, 128, 3, 32, 4, true},
-    // 25-26: the 256 x 192 tile on a two-slot ring of 64-deep stages (plain / interleaved issue): half the
-    // barriers and fragment-read bursts per K of the 32-deep four-slot ring, in the same 112 KB of LDS
-    {256, 192, 2, 64, 4}, {256, 192, 2, 64, 4, true}};
+    {256, 192, 4, 32, 4, true}, {256, 128, 3, 32, 4, true}};
+// (measured and dropped in round 5: the 256 x 192 tile on a two-slot ring of 64-deep stages, half the
+// barriers per K -- plain 0.93-0.97x of variant 23, interleaved 0.6x; profiles/r5_conv_limits.md)
 constexpr int kNumGlds = sizeof(kGldsVariants) / sizeof(kGldsVariants[0]);
 
 template <int N>
@@ -666,8 +665,6 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
     case 11: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, ILV{});
     case 12: return by_bn(M256{}, I4{}, K32{}, C192{}, W4{}, ILV{});
     case 13: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, ILV{});
-    case 14: return by_bn(M256{}, I2{}, K64{}, C192{}, W4{}, NO{});
-    case 15: return by_bn(M256{}, I2{}, K64{}, C192{}, W4{}, ILV{});
     default: return -3;
   }
 }

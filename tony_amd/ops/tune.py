@@ -19,10 +19,9 @@ import torch
 AUTOTUNE = os.environ.get("TONY_CONV_AUTOTUNE", "1") != "0"
 # csrc/mfma_common.h kNtVariants (0-8) + 9: conv.hip halo-tile 3x3 path, 10: conv.hip persistent
 # direct 3x3 kernel (32/64 channels), 11-15: conv.hip LDS-DMA kernels, 16-19: their 8-wave 256-row
-# tiles, 20-24: interleaved-issue forms, 25-26: the 256 x 192 tile on 64-deep two-slot rings (igemm.h
-# kGldsVariants; TONY_CONV_GLDS=0 leaves them all out of the search, TONY_CONV_GLDS8=0 the 8-wave and
-# interleaved ones, TONY_CONV_GLDS_IL=0 the interleaved and two-slot ones)
-_N_GLDS = (27 if os.environ.get("TONY_CONV_GLDS_IL", "1") != "0" else 20) \
+# tiles, 20-24: interleaved-issue forms (igemm.h kGldsVariants; TONY_CONV_GLDS=0 leaves them all out of
+# the search, TONY_CONV_GLDS8=0 the 8-wave and interleaved ones, TONY_CONV_GLDS_IL=0 the interleaved)
+_N_GLDS = (25 if os.environ.get("TONY_CONV_GLDS_IL", "1") != "0" else 20) \
     if os.environ.get("TONY_CONV_GLDS8", "1") != "0" else 16
 _BASE = tuple(range(_N_GLDS if os.environ.get("TONY_CONV_GLDS", "1") != "0" else 11))
 # + stream-K forms of the LDS-DMA variants (csrc/igemm.h SplitK): candidate v + 256 * m, i.e. flags bits
@@ -35,6 +34,11 @@ _BASE = tuple(range(_N_GLDS if os.environ.get("TONY_CONV_GLDS", "1") != "0" else
 # of 6-25 tiles).  TONY_STREAMK=1,2,3: the grid multiples offered to the tuner.
 STREAM_MS = tuple(int(x) for x in os.environ.get("TONY_STREAMK", "").split(",") if x.strip() not in ("", "0"))
 NT_VARIANTS = _BASE + tuple(v + 256 * m for m in STREAM_MS for v in _BASE if v >= 11)
+# the x3 (fp32) convs: their K is three planes deep, so a tile's K loop is 3x the bf16 one and the fold's
+# partial tiles cost relatively less -- stream-K over one CU-grid is offered there (fp32 step A/B
+# 37.64 vs 37.95 ms, profiles/r5_x3_wgrad_fused.md); TONY_X3_STREAMK=0: plain launches only
+X3_STREAM_MS = tuple(int(x) for x in os.environ.get("TONY_X3_STREAMK", "1").split(",") if x.strip() not in ("", "0"))
+X3_VARIANTS = _BASE + tuple(v + 256 * m for m in X3_STREAM_MS for v in _BASE if v >= 11)
 # the whole-input (aux-head) GEMMs: a handful of tiles over a long K -- stream-K spreads K over the CUs
 # (conv_bench --tony: fwd 30 -> 17 us, dgrad 163 -> 68 us)
 SMALL_GEMM_VARIANTS = _BASE + tuple(v + 256 * m for m in (1, 2) for v in _BASE if v >= 11)

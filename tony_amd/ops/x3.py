@@ -128,7 +128,7 @@ def conv_fwd(x3: torch.Tensor, cp: int, w3: torch.Tensor, wshape, stride, paddin
     vf = tune.cached(key)
     if vf is None:
         scratch = torch.zeros(_lib.stat_floats(co), device=x3.device) if stats is not None else None
-        vf = tune.pick(key, lambda v: launch(v, scratch))
+        vf = tune.pick(key, lambda v: launch(v, scratch), tune.X3_VARIANTS)
     _lib.check(launch(vf, stats), "tony_conv_fwd (x3)")
     return z
 
@@ -162,11 +162,11 @@ def conv_dgrad(d3: torch.Tensor, wt3: torch.Tensor, co: int, x_shape, wshape, st
                                          ph, pw, out.data_ptr(), h, w, c, flags | vf, None, st)
     name = "tony_conv_dgrad (x3)" if (sh, sw) == (1, 1) else "tony_conv_dgrad_strided (x3)"
     key = ("x3_dgrad", tuple(d3.shape), tuple(x_shape), tuple(wshape), (sh, sw), (ph, pw))
-    variants = tuple(v for v in tune.NT_VARIANTS if v != 9)  # fp32 epilogue: NT / LDS-DMA / direct kernels
+    variants = tuple(v for v in tune.X3_VARIANTS if v != 9)  # fp32 epilogue: NT / LDS-DMA / direct kernels
     from .conv import STRIDED_GLDS
 
-    if (sh, sw) != (1, 1) and not STRIDED_GLDS:
-        variants = tuple(v for v in variants if v < 11)
+    if (sh, sw) != (1, 1):  # the strided dgrad refuses stream-K forms
+        variants = tuple(v for v in variants if (v < 11 or STRIDED_GLDS) and v < 256)  # v + 256 m: stream-K
     vf = tune.cached(key)
     if vf is None:  # timed into a scratch output: an accumulating call must add exactly once
         scratch = _cl(n, c, h, w, d3.device) if acc else dx
