@@ -485,3 +485,47 @@ def test_x3_conv_streamk_matches_plain(cuda, code, monkeypatch):
     (z1, s1, d1), (z0, s0, d0) = outs[code], outs[code % 256]
     assert _rel(z1, z0) < 1e-6 and _rel(d1, d0) < 1e-6
     torch.testing.assert_close(s1, s0, rtol=1e-5, atol=1e-3)
+
+
+X3F_SHAPES = [(8, 192, 17, 17, 192, (1, 7), 1, (0, 3)), (4, 64, 35, 35, 96, (3, 3), 1, (1, 1)),
+              (4, 288, 35, 35, 384, (3, 3), 2, (0, 0)), (8, 448, 8, 8, 384, (3, 3), 1, (1, 1)),
+              (8, 160, 17, 17, 160, (7, 1), 1, (3, 0)), (4, 64, 11, 13, 32, (1, 1), 1, (0, 0))]
+
+
+@pytest.mark.parametrize("code", [32, 33, 34, 35, 36, 37, 33 + 256])
+@pytest.mark.parametrize("shape", X3F_SHAPES, ids=lambda s: f"{s[1]}x{s[2]}-{s[4]}-k{s[5][0]}x{s[5][1]}-s{s[6]}")
+def test_x3_fused_plane_conv_matches_plane_k(cuda, shape, code, monkeypatch):
+    """The fused-plane x3 conv tiles (igemm.h X3Planes, codes 32-37 and a stream-K form): A hi / lo and B
+    hi / lo staged once per K-step, hi*hi + lo*hi + hi*lo per step -- forward with the fp32 epilogue + BN
+    statistics, and the stride-1 backward-data with the accumulating fp32 epilogue -- against the same
+    products run as 3x the K on the plain LDS-DMA tile (variant 11), and the forward against float64."""
+    from tony_amd.ops import _lib, tune, x3
+
+    n, c, h, w, co, k, s, p = shape
+    torch.manual_seed(0)
+    xf = _cl(torch.randn(n, c, h, w, device=cuda))
+    wt = _cl(torch.randn(co, c, *k, device=cuda) / (c * k[0] * k[1]) ** 0.5)
+    oh, ow = (h + 2 * p[0] - k[0]) // s + 1, (w + 2 * p[1] - k[1]) // s + 1
+    dyf = _cl(torch.randn(n, co, oh, ow, device=cuda))
+    xp, cp = x3.split_act(xf)
+    dp, _ = x3.split_act(dyf)
+    outs = {}
+    for pin in (code, 11):
+        monkeypatch.setattr(tune, "_CACHE", {})
+        monkeypatch.setattr(tune, "pick", lambda key, launch, variants=None, _p=pin: _p << 8
+                            if launch(_p << 8) == 0 else pytest.fail(f"code {_p} refused"))
+        stats = torch.zeros(_lib.stat_floats(co), device=cuda)
+        z = x3.conv_fwd(xp, cp, x3.split_weight(wt), wt.shape, s, p, stats)
+        dx = None
+        if s == 1:
+            acc = _cl(torch.randn(n, c, h, w, device=cuda, generator=torch.Generator(cuda).manual_seed(5)))
+            dx = x3.conv_dgrad(dp, x3.split_weight_t(wt), co, xf.shape, wt.shape, 1, p, accum=acc).clone()
+        torch.cuda.synchronize()
+        outs[pin] = (z.clone(), _lib.fold_stats(stats, co).clone(), dx)
+    (z1, s1, d1), (z0, s0, d0) = outs[code], outs[11]
+    assert _rel(z1, z0) < 1e-5
+    torch.testing.assert_close(s1, s0, rtol=1e-4, atol=1e-2)
+    if d1 is not None:
+        assert _rel(d1, d0) < 1e-5
+    ref = torch.nn.functional.conv2d(xf.double().cpu(), wt.double().cpu(), None, s, p)
+    assert _rel(z1, ref) < 1e-4

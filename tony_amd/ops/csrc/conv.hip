@@ -1759,6 +1759,24 @@ TONY_API int tony_splitk_workspace(float* slab, int64_t slab_floats, unsigned* c
 // Y[N*OH*OW, Co] (row stride ldy) = conv(X [N,H,W,C] pixel stride ldx, W [Co][R][S][C]).
 // flags bit0: per-channel sum / sum-of-squares of Y into stats[2*Co] (zero on entry; kStatShards
 // copies sstride floats apart when sstride > 0); bits 8..15: tile variant (run_nt).
+// the fused x3 codes (igemm.h kX3Variants): the operand has C = 3 cp channels per pixel ([hi | lo | hi]
+// planes, ops/x3.py) and the filter rows [hi | hi | lo] per tap; the kernel reduces K = R * S * cp with three
+// products per K-step.  -3: not an x3 code, or a shape it does not take.
+int run_x3(Gather g, const void* B, int Cx, void* C, int64_t ldc, int64_t M, int64_t N, int flags, float* stats,
+           int64_t sstride, hipStream_t stream) {
+  const int v = (flags >> 8) & 0xff;
+  if (v < kX3First || v >= kX3First + kNumX3 || Cx % 3 || (Cx / 3) % 8) return -3;
+  const int epi = flags & 31;
+  if ((epi & 1) && (epi & 2)) return -1;
+  if ((epi & 3) && stats == nullptr) return -1;
+  if ((epi & 16) && (epi & 3)) return -1;
+  const int cp = Cx / 3;
+  g.Cs = cp;
+  g.K = g.R * g.S * cp;
+  return run_glds<true>(g, B, static_cast<int64_t>(g.R) * g.S * Cx, C, ldc, M, N, epi, stats, sstride, v, stream,
+                        RowMap{}, BTaps{}, (flags >> 16) & 15, X3Planes{cp, 2 * cp, 3 * cp});
+}
+
 TONY_API int tony_conv_fwd(const void* x, int N, int H, int W, int C, int64_t ldx, const void* w, int Co, int R,
                            int S, int sh, int sw, int ph, int pw, void* y, int OH, int OW, int64_t ldy, int flags,
                            float* stats, int64_t sstride, hipStream_t stream) {
@@ -1768,6 +1786,8 @@ TONY_API int tony_conv_fwd(const void* x, int N, int H, int W, int C, int64_t ld
   const int64_t M = static_cast<int64_t>(N) * OH * OW;
   if (M > 0x7fffffff || static_cast<int64_t>(N) * H * W > 0x7fffffff) return -1;
   Gather g{static_cast<const uint16_t*>(x), ldx, H, W, C, OH, OW, R, S, sh, sw, -ph, -pw, 1, R * S * C, N};
+  const int v = (flags >> 8) & 0xff;
+  if (v >= kX3First && v < kX3First + kNumX3) return run_x3(g, w, C, y, ldy, M, Co, flags, stats, sstride, stream);
   return run_nt(g, w, y, ldy, M, Co, flags, stats, sstride, stream);
 }
 
@@ -1793,6 +1813,9 @@ TONY_API int tony_conv_dgrad(const void* dy, int N, int OH, int OW, int Co, int6
   }
   const int fl = flags & 0xfff18;  // variant + stream-K (bits 16..19) + fp32 output (bit3) + accumulate (bit4)
   if ((fl & 16) && bph.bnr.z != nullptr) return -1;
+  const int v = (fl >> 8) & 0xff;
+  if (v >= kX3First && v < kX3First + kNumX3)  // fused x3 planes of dY / Wt (no fused BN reduction)
+    return bph.bnr.z != nullptr ? -3 : run_x3(g, wt, Co, dx, lddx, M, C, fl, nullptr, 0, stream);
   const int rc = run_nt(g, wt, dx, lddx, M, C, fl, nullptr, 0, stream, bph);
   if (rc == -3 && bph.bnr.z != nullptr)  // the chosen variant has no fused reduction: plain dgrad
     return run_nt(g, wt, dx, lddx, M, C, fl, nullptr, 0, stream);

@@ -102,6 +102,15 @@ struct BTaps {
   int r0 = 0, s0 = 0, sy = 1, sx = 1, S = 0;
 };
 
+// The x3 (fp32) operands of conv_glds_kernel X3 (ops/x3.py): A holds [hi | lo | hi] planes of Cs channels
+// per pixel (the lo plane alo elements after the hi one), B rows hold per tap [hi | hi | lo] planes (btap
+// elements per tap, the lo plane blo after the hi one).  The kernel stages A hi / lo and B hi / lo once per
+// K-step and issues the three products hi*hi + lo*hi + hi*lo on the same accumulators (K = R * S * Cs),
+// instead of running the three planes as 3x the K with the hi planes staged twice.
+struct X3Planes {
+  int alo = 0, blo = 0, btap = 0;
+};
+
 // A[M, K] row-major (row stride lda) as a Gather: one 1 x M image with K channels, 1x1 filter.
 inline Gather gemm_gather(const void* A, int64_t lda, int64_t M, int64_t K) {
   return Gather{static_cast<const uint16_t*>(A), lda, 1, static_cast<int>(M), static_cast<int>(K), 1,
@@ -184,20 +193,24 @@ __device__ __forceinline__ int goff(int row, int ch) {
 // current stage (after its fragments are read) instead of all at once right after the barrier -- a
 // global_load_lds costs the issuing wave ~60-185 cycles of issue, which then overlaps the matrix pipe
 // working off the MFMAs already issued (MI355X_MICROARCH.md, LDS-DMA piece issue cost).
-template <int BM, int BN, int ST, int KB, bool UNI, int NWM = 2, bool IL = false>
+template <int BM, int BN, int ST, int KB, bool UNI, int NWM = 2, bool IL = false, bool X3 = false>
 __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const uint16_t* __restrict__ B, int64_t ldb,
                                                              uint16_t* __restrict__ C, int64_t ldc, int M, int N,
                                                              float* __restrict__ stats, int64_t sstride, int epi,
-                                                             int tiles_n, RowMap rmap, BTaps bt, SplitK sk) {
+                                                             int tiles_n, RowMap rmap, BTaps bt, SplitK sk,
+                                                             X3Planes xp) {
   constexpr int NW = 2 * NWM;                 // waves: NWM along M x 2 along N
   constexpr int WM = BM / NWM, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int CPR = KB / 8;                // 16-B chunks per LDS row
   constexpr int RPI = 64 / CPR;              // rows per DMA instruction (1 KB)
   constexpr int AG = BM / RPI, BG = BN / RPI;  // row groups per operand tile
   constexpr int AI = (AG + NW - 1) / NW, BI = (BG + NW - 1) / NW;  // DMA instructions per wave and stage
-  constexpr int STAGE = (BM + BN) * KB;      // elements
+  constexpr int PL = X3 ? 2 : 1;             // staged planes per operand: X3 [hi | lo]
+  constexpr int STAGE = PL * (BM + BN) * KB; // elements
   constexpr int KSUB = KB / 32;              // MFMA K-steps per stage
+  constexpr int NDMA = PL * (AI + BI);       // DMA instructions per thread and stage
   static_assert(BM % RPI == 0 && BN % RPI == 0 && BN % 32 == 0 && ST >= 2 && (KB == 32 || KB == 64), "tile shape");
+  static_assert(!X3 || (UNI && !IL), "the fused x3 planes run the plain uniform-tap loop");
   static_assert(BM * (BN + 8) <= ST * STAGE, "the epilogue's C tile fits in the ring");
   __shared__ __attribute__((aligned(16))) uint16_t smem[ST * STAGE];
 
@@ -262,7 +275,8 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
   int kb = ck * 8 + kstart;  // this thread's K column of the next stage to issue
   const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(smem));
   constexpr uint32_t kGroupB = RPI * KB * 2;  // bytes per row group
-  constexpr uint32_t kStageB = STAGE * 2, kBOff = BM * KB * 2;
+  constexpr uint32_t kStageB = STAGE * 2, kBOff = PL * BM * KB * 2;
+  constexpr uint32_t kALo = BM * KB * 2, kBLo = BN * KB * 2;  // X3: the lo plane's tile after the hi one
   uint32_t aoff[AI], boff[BI];  // wave-uniform byte offsets of this wave's row groups
 #pragma unroll
   for (int i = 0; i < AI; ++i) aoff[i] = __builtin_amdgcn_readfirstlane(agrp[i] * kGroupB);
@@ -273,6 +287,7 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
   const uint16_t* ap[AI];
   const uint16_t* bp[BI];
   int ainc[AI], binc[BI];
+  int alo[AI], blo[BI];  // X3: element offset of the lo plane from the hi source (0 for zero-fill lanes)
   int ur = 0, us = 0, uleft = 0;
   auto set_tap = [&]() {  // UNI: sources of tap (ur, us) for this thread's DMAs
     const bool tap_ok = ur < g.R;
@@ -283,12 +298,22 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
                       (static_cast<unsigned>(ix) < static_cast<unsigned>(g.Ws));
       ap[i] = ok ? g.src + (static_cast<int64_t>(rs[i].pix) + iy * g.Ws + ix) * g.ld + ck * 8 : zc;
       ainc[i] = ok ? KB : 0;
+      alo[i] = ok ? xp.alo : 0;
     }
     if (!tap_ok) {  // K is exhausted (K = R * S * Cs): the ring's tail stages fetch zeros
 #pragma unroll
       for (int i = 0; i < BI; ++i) {
         bp[i] = zc;
         binc[i] = 0;
+        blo[i] = 0;
+      }
+    } else if (X3) {  // this tap's hi plane in the filter row ([hi | hi | lo] per tap)
+      const int toff = (ur * g.S + us) * xp.btap + ck * 8;
+#pragma unroll
+      for (int i = 0; i < BI; ++i) {
+        bp[i] = bok[i] ? brow[i] + toff : zc;
+        binc[i] = bok[i] ? KB : 0;
+        blo[i] = bok[i] ? xp.blo : 0;
       }
     } else if (bt.S != 0) {  // a strided dgrad's residue class: this tap's slice of the full filter row
       const int toff = ((bt.r0 + bt.sy * ur) * bt.S + bt.s0 + bt.sx * us) * g.Cs + ck * 8;
@@ -312,7 +337,7 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
       const int tap = kstart / g.Cs, c0 = kstart - tap * g.Cs;
       ur = tap / g.S;
       us = tap - ur * g.S;
-      if (bt.S == 0) {
+      if (bt.S == 0 && !X3) {
 #pragma unroll
         for (int i = 0; i < BI; ++i) bp[i] += binc[i] / KB * kstart;  // the filter row is contiguous over K
       }
@@ -320,7 +345,7 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
       const int steps = c0 / KB;
 #pragma unroll
       for (int i = 0; i < AI; ++i) ap[i] += ainc[i] * steps;
-      if (bt.S != 0) {
+      if (bt.S != 0 || X3) {
 #pragma unroll
         for (int i = 0; i < BI; ++i) bp[i] += binc[i] * steps;
       }
@@ -360,11 +385,13 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
 #pragma unroll
       for (int i = 0; i < AI; ++i) {
         glds16(live ? ap[i] : zc, st0 + aoff[i]);
+        if constexpr (X3) glds16(live ? ap[i] + alo[i] : zc, st0 + aoff[i] + kALo);
         ap[i] += ainc[i];
       }
 #pragma unroll
       for (int i = 0; i < BI; ++i) {
         glds16(live ? bp[i] : zc, st0 + boff[i]);
+        if constexpr (X3) glds16(live ? bp[i] + blo[i] : zc, st0 + boff[i] + kBLo);
         bp[i] += binc[i];
       }
       if (--uleft == 0) {
@@ -405,10 +432,10 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt has landed everywhere and every wave is done reading stage kt - 1, whose slot takes
     // stage kt + ST - 1 (past the end: zero fills, which keeps the per-thread DMA count uniform)
-    glds_wait_barrier<(ST - 2) * (AI + BI)>();
+    glds_wait_barrier<(ST - 2) * NDMA>();
     const int fill = slot == 0 ? ST - 1 : slot - 1;
     const uint16_t* As = smem + slot * STAGE;
-    const uint16_t* Bs = As + BM * KB;
+    const uint16_t* Bs = As + PL * BM * KB;
     if constexpr (IL && UNI) {
       // every fragment of the stage first, then MFMA row groups with one DMA piece after each
       constexpr int NP = AI + BI;
@@ -447,6 +474,37 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
       continue;
     }
     issue(fill);
+    if constexpr (X3) {
+      // both A planes' fragments held, the B planes streamed column by column (peak 2 TM + 2 fragments
+      // live, not 2 (TM + TN): the 256-row 8-wave tiles spilled otherwise); 3 MFMAs per (i, j):
+      // hi*hi + lo*hi + hi*lo, each fragment read once per K-step
+      const uint16_t* Al = As + BM * KB;
+      const uint16_t* Bl = Bs + BN * KB;
+#pragma unroll
+      for (int kk = 0; kk < KSUB; ++kk) {
+        const int ch = kk * 4 + (lane >> 4);
+        bf16x8_t ah[TM], al[TM];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          ah[i] = *reinterpret_cast<const bf16x8_t*>(As + goff<KB>(wm * WM + i * 16 + (lane & 15), ch));
+          al[i] = *reinterpret_cast<const bf16x8_t*>(Al + goff<KB>(wm * WM + i * 16 + (lane & 15), ch));
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int bo = goff<KB>(wn * WN + j * 16 + (lane & 15), ch);
+          const bf16x8_t bh = *reinterpret_cast<const bf16x8_t*>(Bs + bo);
+          const bf16x8_t bl = *reinterpret_cast<const bf16x8_t*>(Bl + bo);
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl, acc[i][j], 0, 0, 0);
+          }
+        }
+      }
+      slot = slot + 1 == ST ? 0 : slot + 1;
+      continue;
+    }
 #pragma unroll
     for (int kk = 0; kk < KSUB; ++kk) {
       const int ch = kk * 4 + (lane >> 4);
@@ -566,21 +624,43 @@ inline int num_cus_of_current() {
 // stream_m > 0: stream-K over stream_m x (CUs) workgroups (SplitK above) when this thread's workspace
 // (tony_splitk_workspace) holds 2 partial tiles per workgroup and a counter per tile, else the plain
 // launch (same result)
+// The fused x3 forms (X3Planes): tiles whose ring of [A hi | A lo | B hi | B lo] stages fits the LDS, the
+// plain uniform-tap loop only.  Variant codes kX3First.. of tony_conv_fwd / tony_conv_dgrad.
+struct X3Variant {
+  int bm, cap, stages, kb, nwm;
+};
+constexpr int kX3First = 32;
+// (no 256 x 160 / 192 tile: 8 waves of 64 x 96 hold 96 accumulator + 40 fragment registers and spilled)
+constexpr X3Variant kX3Variants[] = {{256, 128, 2, 32, 4}, {128, 192, 3, 32, 2}, {128, 128, 4, 32, 2},
+                                     {128, 128, 2, 64, 2}, {256, 128, 3, 32, 4}, {64, 128, 4, 32, 2}};
+constexpr int kNumX3 = sizeof(kX3Variants) / sizeof(kX3Variants[0]);
+
+// XF: the fused x3 forms (codes kX3First..; xp describes the planes), instantiated only where used
+template <bool XF = false>
 inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N, int epi,
                     float* st, int64_t sstride, int v, hipStream_t stream, RowMap rmap = RowMap{},
-                    BTaps bt = BTaps{}, int stream_m = 0) {
+                    BTaps bt = BTaps{}, int stream_m = 0, X3Planes xp = X3Planes{}) {
+  constexpr bool x3 = XF;
+  if (XF != (xp.btap != 0)) return -1;
   if ((ldc % 8) || (ldb % 8) || (reinterpret_cast<uintptr_t>(C) & 15) || (reinterpret_cast<uintptr_t>(B) & 15) ||
-      (reinterpret_cast<uintptr_t>(g.src) & 15) || (g.ld % 8) || (g.K % 8) || v < kGldsFirst || v >= kGldsFirst + kNumGlds)
+      (reinterpret_cast<uintptr_t>(g.src) & 15) || (g.ld % 8) || (g.K % 8))
     return -3;
-  const GldsVariant gv = kGldsVariants[v - kGldsFirst];
+  if (x3 ? (v < kX3First || v >= kX3First + kNumX3 || bt.S != 0 || (xp.alo % 8) || (xp.blo % 8) || (xp.btap % 8))
+         : (v < kGldsFirst || v >= kGldsFirst + kNumGlds))
+    return -3;
+  const GldsVariant gv = x3 ? GldsVariant{kX3Variants[v - kX3First].bm, kX3Variants[v - kX3First].cap,
+                                          kX3Variants[v - kX3First].stages, kX3Variants[v - kX3First].kb,
+                                          kX3Variants[v - kX3First].nwm}
+                            : kGldsVariants[v - kGldsFirst];
   const int64_t bn = pick_bn(N, gv.cap);
   using std::integral_constant;
-  const auto launch = [&](auto bm, auto bnc, auto st_, auto kb, auto nwm, auto il) -> int {
+  const auto launch = [&](auto bm, auto bnc, auto st_, auto kb, auto nwm, auto il, auto x3c) -> int {
     constexpr int BM = decltype(bm)::value, BN = decltype(bnc)::value, ST = decltype(st_)::value;
     constexpr int KB = decltype(kb)::value, NWM = decltype(nwm)::value;
-    constexpr bool IL = decltype(il)::value;
-    if constexpr (BN % (64 / (KB / 8)) != 0 || BM * (BN + 8) > ST * (BM + BN) * KB ||
-                  ST * (BM + BN) * KB * 2 > 163840) {
+    constexpr bool IL = decltype(il)::value, X3 = decltype(x3c)::value;
+    constexpr int PL = X3 ? 2 : 1;
+    if constexpr (BN % (64 / (KB / 8)) != 0 || BM * (BN + 8) > ST * PL * (BM + BN) * KB ||
+                  ST * PL * (BM + BN) * KB * 2 > 163840 || (X3 && IL)) {
       return -3;
     } else {
       const int tiles_m = ceil_div(M, BM), tiles_n = ceil_div(N, BN);
@@ -607,29 +687,33 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
       }
       const auto args = std::make_tuple(g, static_cast<const uint16_t*>(B), ldb, static_cast<uint16_t*>(C), ldc,
                                         static_cast<int>(M), static_cast<int>(N), st, sstride, epi, tiles_n, rmap, bt,
-                                        sk);
-      if (g.Cs % KB == 0 && glds_uni_enabled())
+                                        sk, xp);
+      if constexpr (X3) {
+        if (g.Cs % KB != 0) return -3;  // the fused planes run the uniform-tap loop only
+        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true, NWM, false, true><<<grid, 128 * NWM, 0, stream>>>(a...); }, args);
+      } else if (g.Cs % KB == 0 && glds_uni_enabled()) {
         std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true, NWM, IL><<<grid, 128 * NWM, 0, stream>>>(a...); }, args);
-      else if (IL || bt.S != 0)
+      } else if (IL || bt.S != 0) {
         return -3;  // the interleaved form and the class taps exist for the uniform-tap loop only
-      else
+      } else {
         std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, false, NWM><<<grid, 128 * NWM, 0, stream>>>(a...); }, args);
+      }
       TONY_LAUNCH_CHECK();
       return 0;
     }
   };
-  const auto by_bn = [&](auto bm, auto st_, auto kb, auto cap, auto nwm, auto il) -> int {
+  const auto by_bn = [&](auto bm, auto st_, auto kb, auto cap, auto nwm, auto il, auto x3c) -> int {
     constexpr int CAP = decltype(cap)::value;
     switch (bn) {
-      case 32: return launch(bm, integral_constant<int, 32>{}, st_, kb, nwm, il);
-      case 64: return launch(bm, integral_constant<int, 64>{}, st_, kb, nwm, il);
-      case 96: return launch(bm, integral_constant<int, 96>{}, st_, kb, nwm, il);
-      case 128: return launch(bm, integral_constant<int, 128>{}, st_, kb, nwm, il);
+      case 32: return launch(bm, integral_constant<int, 32>{}, st_, kb, nwm, il, x3c);
+      case 64: return launch(bm, integral_constant<int, 64>{}, st_, kb, nwm, il, x3c);
+      case 96: return launch(bm, integral_constant<int, 96>{}, st_, kb, nwm, il, x3c);
+      case 128: return launch(bm, integral_constant<int, 128>{}, st_, kb, nwm, il, x3c);
       case 160:
-        if constexpr (CAP >= 160) return launch(bm, integral_constant<int, 160>{}, st_, kb, nwm, il);
+        if constexpr (CAP >= 160) return launch(bm, integral_constant<int, 160>{}, st_, kb, nwm, il, x3c);
         break;
       case 192:
-        if constexpr (CAP >= 192) return launch(bm, integral_constant<int, 192>{}, st_, kb, nwm, il);
+        if constexpr (CAP >= 192) return launch(bm, integral_constant<int, 192>{}, st_, kb, nwm, il, x3c);
         break;
       default: break;
     }
@@ -650,22 +734,35 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
   using W4 = integral_constant<int, 4>;
   using NO = std::false_type;
   using ILV = std::true_type;
+  if constexpr (XF) {
+    using X = std::true_type;
+    switch (v - kX3First) {
+      case 0: return by_bn(M256{}, I2{}, K32{}, C128{}, W4{}, NO{}, X{});
+      case 1: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{}, NO{}, X{});
+      case 2: return by_bn(M128{}, I4{}, K32{}, C128{}, W2{}, NO{}, X{});
+      case 3: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, NO{}, X{});
+      case 4: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, NO{}, X{});
+      case 5: return by_bn(M64{}, I4{}, K32{}, C128{}, W2{}, NO{}, X{});
+      default: return -3;
+    }
+  } else {
   switch (v - kGldsFirst) {
-    case 0: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, NO{});
-    case 1: return by_bn(M128{}, I3{}, K32{}, C128{}, W2{}, NO{});
-    case 2: return by_bn(M128{}, I4{}, K32{}, C128{}, W2{}, NO{});
-    case 3: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{}, NO{});
-    case 4: return by_bn(M64{}, I4{}, K32{}, C128{}, W2{}, NO{});
-    case 5: return by_bn(M256{}, I4{}, K32{}, C192{}, W4{}, NO{});
-    case 6: return by_bn(M256{}, I3{}, K64{}, C128{}, W4{}, NO{});
-    case 7: return by_bn(M256{}, I5{}, K32{}, C192{}, W4{}, NO{});
-    case 8: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, NO{});
-    case 9: return by_bn(M128{}, I3{}, K32{}, C128{}, W2{}, ILV{});
-    case 10: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{}, ILV{});
-    case 11: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, ILV{});
-    case 12: return by_bn(M256{}, I4{}, K32{}, C192{}, W4{}, ILV{});
-    case 13: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, ILV{});
+    case 0: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, NO{}, NO{});
+    case 1: return by_bn(M128{}, I3{}, K32{}, C128{}, W2{}, NO{}, NO{});
+    case 2: return by_bn(M128{}, I4{}, K32{}, C128{}, W2{}, NO{}, NO{});
+    case 3: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{}, NO{}, NO{});
+    case 4: return by_bn(M64{}, I4{}, K32{}, C128{}, W2{}, NO{}, NO{});
+    case 5: return by_bn(M256{}, I4{}, K32{}, C192{}, W4{}, NO{}, NO{});
+    case 6: return by_bn(M256{}, I3{}, K64{}, C128{}, W4{}, NO{}, NO{});
+    case 7: return by_bn(M256{}, I5{}, K32{}, C192{}, W4{}, NO{}, NO{});
+    case 8: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, NO{}, NO{});
+    case 9: return by_bn(M128{}, I3{}, K32{}, C128{}, W2{}, ILV{}, NO{});
+    case 10: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{}, ILV{}, NO{});
+    case 11: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, ILV{}, NO{});
+    case 12: return by_bn(M256{}, I4{}, K32{}, C192{}, W4{}, ILV{}, NO{});
+    case 13: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, ILV{}, NO{});
     default: return -3;
+  }
   }
 }
 

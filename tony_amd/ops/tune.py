@@ -38,7 +38,12 @@ NT_VARIANTS = _BASE + tuple(v + 256 * m for m in STREAM_MS for v in _BASE if v >
 # partial tiles cost relatively less -- stream-K over one CU-grid is offered there (fp32 step A/B
 # 37.64 vs 37.95 ms, profiles/r5_x3_wgrad_fused.md); TONY_X3_STREAMK=0: plain launches only
 X3_STREAM_MS = tuple(int(x) for x in os.environ.get("TONY_X3_STREAMK", "1").split(",") if x.strip() not in ("", "0"))
+# the fused-plane x3 tiles (igemm.h kX3Variants, codes 32-37: A hi / lo and B hi / lo staged once per K-step,
+# three products on the same accumulators) for operands whose plane width is a multiple of 32;
+# TONY_X3_FUSED=0 leaves them out (A/B)
+X3F_CODES = tuple(range(32, 38)) if os.environ.get("TONY_X3_FUSED", "1") != "0" else ()
 X3_VARIANTS = _BASE + tuple(v + 256 * m for m in X3_STREAM_MS for v in _BASE if v >= 11)
+X3F_VARIANTS = X3F_CODES + tuple(v + 256 * m for m in X3_STREAM_MS for v in X3F_CODES)
 # the whole-input (aux-head) GEMMs: a handful of tiles over a long K -- stream-K spreads K over the CUs
 # (conv_bench --tony: fwd 30 -> 17 us, dgrad 163 -> 68 us)
 SMALL_GEMM_VARIANTS = _BASE + tuple(v + 256 * m for m in (1, 2) for v in _BASE if v >= 11)

@@ -128,7 +128,7 @@ def conv_fwd(x3: torch.Tensor, cp: int, w3: torch.Tensor, wshape, stride, paddin
     vf = tune.cached(key)
     if vf is None:
         scratch = torch.zeros(_lib.stat_floats(co), device=x3.device) if stats is not None else None
-        vf = tune.pick(key, lambda v: launch(v, scratch), tune.X3_VARIANTS)
+        vf = tune.pick(key, lambda v: launch(v, scratch), tune.X3_VARIANTS + (tune.X3F_VARIANTS if cp % 32 == 0 else ()))
     _lib.check(launch(vf, stats), "tony_conv_fwd (x3)")
     return z
 
@@ -167,6 +167,8 @@ def conv_dgrad(d3: torch.Tensor, wt3: torch.Tensor, co: int, x_shape, wshape, st
 
     if (sh, sw) != (1, 1):  # the strided dgrad refuses stream-K forms
         variants = tuple(v for v in variants if (v < 11 or STRIDED_GLDS) and v < 256)  # v + 256 m: stream-K
+    elif co % 32 == 0:  # the fused-plane tiles (stride-1 dgrad: the gather runs over dY's Co planes)
+        variants = variants + tune.X3F_VARIANTS
     vf = tune.cached(key)
     if vf is None:  # timed into a scratch output: an accumulating call must add exactly once
         scratch = _cl(n, c, h, w, d3.device) if acc else dx
