@@ -96,6 +96,8 @@ _SIGNATURES = {
     "tony_counter_bump": [c_void_p, c_void_p],
     "tony_gemm_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64,
                        c_int, c_void_p, c_int64, c_void_p],
+    "tony_gemm_bf16_bnact": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64,
+                             c_int, c_void_p, c_int64, c_void_p, c_void_p],
     "tony_gemm_tn_bf16": [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_int64,
                           c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p],
     "tony_splitk_reduce": [c_void_p, c_int, c_int64, c_void_p, c_int, c_int, c_int, c_void_p],

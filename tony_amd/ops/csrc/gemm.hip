@@ -175,6 +175,25 @@ int launch_bm(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, i
 // byte mask [M, ldc / 8] (ops/residual.py MaskedGrad: a residual tail's d(identity), never
 // materialised); bits 8..15: tile variant (kNtVariants, mfma_common.h); bits 16..19: stream-K grid in CUs (LDS-DMA
 // variants, igemm.h SplitK; tony_splitk_workspace).
+// The BN-apply-in-the-consumer prototype (profiles/r5_bn_apply_in_consumer_ab.md): C = relu(A *
+// scale + shift) . B^T with the per-channel affine + ReLU applied to each A chunk in LDS as it lands
+// (igemm.h X3Planes::atab, table [scale[K] | shift[K]] fp32), on the 128 x 128 three-slot LDS-DMA tile
+// (variant 12); flags as tony_gemm_bf16 (bits 0-4).  Measured against bn apply + GEMM by
+// tools/bn_consumer_bench.py.
+TONY_API int tony_gemm_bf16_bnact(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                                  int64_t ldb, int64_t ldc, int flags, float* stats, int64_t sstride, const float* table,
+                                  hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || sstride < 0 || table == nullptr) return -1;
+  if ((K % 8) || (lda % 8) || (ldb % 8) || M > 0x7fffffff || N > 0x7fffffff) return -1;
+  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -1;
+  const int epi = flags & 31;
+  if (((epi & 1) && (epi & 2)) || ((epi & 16) && (epi & 3)) || ((epi & 3) && stats == nullptr)) return -1;
+  X3Planes xp{};
+  xp.atab = table;
+  return run_glds(gemm_gather(A, lda, M, K), B, ldb, C, ldc, M, N, epi, stats, sstride, kGldsFirst + 1, stream,
+                  RowMap{}, BTaps{}, 0, xp);
+}
+
 TONY_API int tony_gemm_bf16(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
                             int64_t ldb, int64_t ldc, int flags, float* stats, int64_t sstride, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0 || sstride < 0) return -1;

@@ -109,6 +109,10 @@ struct BTaps {
 // instead of running the three planes as 3x the K with the hi planes staged twice.
 struct X3Planes {
   int alo = 0, blo = 0, btap = 0;
+  // AT (conv_glds_kernel): [scale | shift] per A channel (K floats each): the A operand is BN-applied +
+  // ReLU'd in LDS as it lands -- relu(a * scale[k] + shift[k]) -- the "apply in the consumer" prototype
+  // (profiles/r5_bn_apply_in_consumer_ab.md); 1x1 (GEMM) operands only
+  const float* atab = nullptr;
 };
 
 // A[M, K] row-major (row stride lda) as a Gather: one 1 x M image with K channels, 1x1 filter.
@@ -193,7 +197,7 @@ __device__ __forceinline__ int goff(int row, int ch) {
 // current stage (after its fragments are read) instead of all at once right after the barrier -- a
 // global_load_lds costs the issuing wave ~60-185 cycles of issue, which then overlaps the matrix pipe
 // working off the MFMAs already issued (MI355X_MICROARCH.md, LDS-DMA piece issue cost).
-template <int BM, int BN, int ST, int KB, bool UNI, int NWM = 2, bool IL = false, bool X3 = false>
+template <int BM, int BN, int ST, int KB, bool UNI, int NWM = 2, bool IL = false, bool X3 = false, bool AT = false>
 __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const uint16_t* __restrict__ B, int64_t ldb,
                                                              uint16_t* __restrict__ C, int64_t ldc, int M, int N,
                                                              float* __restrict__ stats, int64_t sstride, int epi,
@@ -211,6 +215,7 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
   constexpr int NDMA = PL * (AI + BI);       // DMA instructions per thread and stage
   static_assert(BM % RPI == 0 && BN % RPI == 0 && BN % 32 == 0 && ST >= 2 && (KB == 32 || KB == 64), "tile shape");
   static_assert(!X3 || (UNI && !IL), "the fused x3 planes run the plain uniform-tap loop");
+  static_assert(!AT || (UNI && !IL && !X3), "the A transform runs in the plain uniform-tap loop");
   static_assert(BM * (BN + 8) <= ST * STAGE, "the epilogue's C tile fits in the ring");
   __shared__ __attribute__((aligned(16))) uint16_t smem[ST * STAGE];
 
@@ -432,7 +437,38 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt has landed everywhere and every wave is done reading stage kt - 1, whose slot takes
     // stage kt + ST - 1 (past the end: zero fills, which keeps the per-thread DMA count uniform)
-    glds_wait_barrier<(ST - 2) * NDMA>();
+    if constexpr (AT) {
+      // this thread's own A chunks of the stage have landed (its vmcnt): BN-apply + ReLU them in place
+      // before the barrier publishes the stage (each row group by its owner wave only: a spare-slot
+      // re-fetch holds the same bytes and must not be transformed twice).  1x1 operands: K = channels.
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((ST - 2) * NDMA) : "memory");
+      const int c = kstart + kt * KB + ck * 8;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        if (wave + NW * i < AG && c < K) {
+          uint4* pv = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(smem) + slot * kStageB + aoff[i] + lane * 16);
+          const float4 s0 = *reinterpret_cast<const float4*>(xp.atab + c);
+          const float4 s1 = *reinterpret_cast<const float4*>(xp.atab + c + 4);
+          const float4 h0 = *reinterpret_cast<const float4*>(xp.atab + K + c);
+          const float4 h1 = *reinterpret_cast<const float4*>(xp.atab + K + c + 4);
+          const uint4 v = *pv;
+          const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+          const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+          uint32_t o[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float lo = fmaxf(fmaf(__uint_as_float(w[q] << 16), sc[2 * q], sh[2 * q]), 0.f);
+            const float hi = fmaxf(fmaf(__uint_as_float(w[q] & 0xffff0000u), sc[2 * q + 1], sh[2 * q + 1]), 0.f);
+            o[q] = static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+          }
+          *pv = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+      }
+      __builtin_amdgcn_s_barrier();
+    } else {
+      glds_wait_barrier<(ST - 2) * NDMA>();
+    }
     const int fill = slot == 0 ? ST - 1 : slot - 1;
     const uint16_t* As = smem + slot * STAGE;
     const uint16_t* Bs = As + PL * BM * KB;
@@ -642,6 +678,7 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
                     BTaps bt = BTaps{}, int stream_m = 0, X3Planes xp = X3Planes{}) {
   constexpr bool x3 = XF;
   if (XF != (xp.btap != 0)) return -1;
+  if (xp.atab != nullptr && (XF || bt.S != 0 || (reinterpret_cast<uintptr_t>(xp.atab) & 15))) return -1;
   if ((ldc % 8) || (ldb % 8) || (reinterpret_cast<uintptr_t>(C) & 15) || (reinterpret_cast<uintptr_t>(B) & 15) ||
       (reinterpret_cast<uintptr_t>(g.src) & 15) || (g.ld % 8) || (g.K % 8))
     return -3;
@@ -688,6 +725,16 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
       const auto args = std::make_tuple(g, static_cast<const uint16_t*>(B), ldb, static_cast<uint16_t*>(C), ldc,
                                         static_cast<int>(M), static_cast<int>(N), st, sstride, epi, tiles_n, rmap, bt,
                                         sk, xp);
+      if (xp.atab != nullptr) {  // the BN-apply-on-load prototype: one tile family
+        if constexpr (!X3 && !IL && BM == 128 && ST == 3 && KB == 32 && NWM == 2 && BN <= 128) {
+          if (g.Cs % KB != 0 || g.R != 1 || g.S != 1) return -3;
+          std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true, NWM, false, false, true><<<grid, 128 * NWM, 0, stream>>>(a...); }, args);
+          TONY_LAUNCH_CHECK();
+          return 0;
+        } else {
+          return -3;
+        }
+      }
       if constexpr (X3) {
         if (g.Cs % KB != 0) return -3;  // the fused planes run the uniform-tap loop only
         std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true, NWM, false, true><<<grid, 128 * NWM, 0, stream>>>(a...); }, args);
