@@ -661,3 +661,30 @@ def test_whole_input_conv_wgrad_nt_gemm_accumulates_into_slot(cuda, dst):
     assert C._gemm_wgrad(dy, x, (co, cin, 5, 5), dst=slot) is None
     tol = 1e-2 if dt == torch.float32 else 6e-2
     torch.testing.assert_close(slot.float(), before + want, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("m,k,n", [(1000, 256, 64), (517, 96, 200), (4096, 64, 256)])
+def test_gemm_bnact_prototype_matches_apply_then_gemm(cuda, m, k, n):
+    """tony_gemm_bf16_bnact (the BN-apply-in-the-consumer prototype, profiles/r5_bn_apply_in_consumer_ab.md):
+    relu(z * scale + shift) applied to the A chunks in LDS equals the apply pass followed by the GEMM, bit
+    for bit (the same bf16 rounding of each transformed element), incl. rows / columns past the tiles."""
+    from tony_amd.ops import _lib
+
+    L, st = _lib.lib(), _lib.stream_ptr(cuda)
+    torch.manual_seed(0)
+    z = (torch.randn(m, k, device=cuda) * 2).to(torch.bfloat16)
+    w = (torch.randn(n, k, device=cuda) / k ** 0.5).to(torch.bfloat16)
+    scale, shift = torch.rand(k, device=cuda) + 0.5, torch.randn(k, device=cuda) * 0.2
+    tab = torch.cat([scale, shift]).contiguous()
+    y = torch.empty_like(z)  # the apply pass (mode 1, running mean 0 / var 1, eps 0: y = relu(fma(z, scale, shift)))
+    zeros, ones = torch.zeros(k, device=cuda), torch.ones(k, device=cuda)
+    assert L.tony_bn_apply(z.data_ptr(), m, k, k, y.data_ptr(), k, None, None, 0, scale.data_ptr(), shift.data_ptr(),
+                           0, 0.0, 1, 1, None, None, zeros.data_ptr(), ones.data_ptr(), 0.0, st) == 0
+    torch.testing.assert_close(y.float(), torch.relu(z.float() * scale + shift), rtol=1e-2, atol=1e-2)
+    ref = torch.empty(m, n, device=cuda, dtype=torch.bfloat16)
+    out = torch.empty_like(ref)
+    assert L.tony_gemm_bf16(y.data_ptr(), w.data_ptr(), ref.data_ptr(), m, n, k, k, k, n, 12 << 8, None, 0, st) == 0
+    assert L.tony_gemm_bf16_bnact(z.data_ptr(), w.data_ptr(), out.data_ptr(), m, n, k, k, k, n, 0, None, 0,
+                                  tab.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
