@@ -75,9 +75,14 @@ def main():
         if a.tony:
             if not tc.supported(x, wt):
                 continue
-            f = time_ms(lambda: tc.conv_fwd(x, wt, s, p), a.iters)
-            d = time_ms(lambda: tc.conv_dgrad(dy, wt, x.shape, s, p), a.iters)
-            g = time_ms(lambda: tc.conv_wgrad(dy, x, wt.shape, s, p), a.iters)
+            if tc.fullcover(x.shape, wt.shape, s, p):  # the model's dispatch: whole-input filters are GEMMs
+                f = time_ms(lambda: tc._gemm_fwd(x, wt), a.iters)
+                d = time_ms(lambda: tc._gemm_dgrad(dy, wt, x.shape), a.iters)
+                g = time_ms(lambda: tc._gemm_wgrad(dy, x, wt.shape), a.iters)
+            else:
+                f = time_ms(lambda: tc.conv_fwd(x, wt, s, p), a.iters)
+                d = time_ms(lambda: tc.conv_dgrad(dy, wt, x.shape, s, p), a.iters)
+                g = time_ms(lambda: tc.conv_wgrad(dy, x, wt.shape, s, p), a.iters)
         else:
             f = time_ms(lambda: torch.nn.functional.conv2d(x, wt, None, s, p), a.iters)
             d = time_ms(lambda: torch.ops.aten.convolution_backward(dy, x, wt, None, s, p, (1, 1), False, (0, 0),
