@@ -594,6 +594,36 @@ def test_strided_dgrad_glds_variants(cuda, shape, v):
     torch.testing.assert_close(out.float(), ref, rtol=1.6e-2, atol=1.6e-2)
 
 
+@pytest.mark.parametrize("v", [12, 16, 19, 23, 24])
+@pytest.mark.parametrize("shape", STRIDED_GLDS[:6], ids=[f"{s[1]}->{s[4]}_{s[2]}k{s[5][0]}" for s in STRIDED_GLDS[:6]])
+def test_strided_dgrad_one_launch_matches_per_class(cuda, shape, v):
+    """csrc/igemm.h MultiClass: every residue class of a stride-2 dgrad in one launch is bit-identical to
+    one launch per class (same tiles, same K order), plain and accumulating."""
+    from tony_amd.ops import _lib
+    from tony_amd.ops.conv import conv_dgrad
+
+    n, ci, h, w, co, (r, s), st, (ph, pw) = shape
+    if co % 32:
+        pytest.skip("uniform-tap shapes only")
+    torch.manual_seed(v)
+    wt = _nhwc(torch.randn(co, ci, r, s, device=cuda) / (ci * r * s) ** 0.5).to(torch.bfloat16)
+    oh, ow = (h + 2 * ph - r) // st + 1, (w + 2 * pw - s) // st + 1
+    dy = _nhwc(torch.randn(n, co, oh, ow, device=cuda)).to(torch.bfloat16)
+    g = _nhwc(torch.randn(n, ci, h, w, device=cuda)).to(torch.bfloat16)
+    L = _lib.lib()
+    prev = L.tony_dgrad_one_launch(-1)
+    outs = []
+    try:
+        for one in (1, 0):
+            L.tony_dgrad_one_launch(one)
+            outs.append((conv_dgrad(dy, wt, (n, ci, h, w), st, (ph, pw), vflags=v << 8),
+                         conv_dgrad(dy, wt, (n, ci, h, w), st, (ph, pw), vflags=v << 8, accum=g.clone())))
+    finally:
+        L.tony_dgrad_one_launch(prev)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
 def test_bn_reduce_fused_into_dgrad(cuda):
     """A chain conv-BN-ReLU -> conv-BN-ReLU (strided) -> conv-BN-ReLU: each BN backward's reduction
     comes from the next conv's dgrad epilogue (csrc/conv.hip BnRed: NT kernel, strided residue classes,

@@ -1823,6 +1823,22 @@ TONY_API int tony_conv_dgrad(const void* dy, int N, int OH, int OW, int Co, int6
   return rc;
 }
 
+// TONY_DGRAD_ONE_LAUNCH=0 (or tony_dgrad_one_launch(0)): one launch per residue class (A/B and the
+// numerics test of the MultiClass launch)
+static std::atomic<int>& dgrad_one_launch_flag() {
+  static std::atomic<int> on{[] {
+    const char* e = std::getenv("TONY_DGRAD_ONE_LAUNCH");
+    return (e != nullptr && e[0] == '0') ? 0 : 1;
+  }()};
+  return on;
+}
+static bool dgrad_one_launch() { return dgrad_one_launch_flag().load(std::memory_order_relaxed) != 0; }
+TONY_API int tony_dgrad_one_launch(int on) {
+  const int prev = dgrad_one_launch_flag().load();
+  if (on >= 0) dgrad_one_launch_flag().store(on ? 1 : 0);
+  return prev;
+}
+
 // dX[N*H*W, C] (row stride lddx) of a STRIDED conv (stride sh x sw, padding ph, pw): one MFMA
 // implicit-GEMM launch per residue class (iy % sh, ix % sw) of dX, each a stride-1 transposed conv
 // over the class's sub-grid with the class's taps of Wt = W permuted to [C][R][S][Co] (Phase).
@@ -1853,6 +1869,10 @@ TONY_API int tony_conv_dgrad_strided(const void* dy, int N, int OH, int OW, int 
   const int acc = flags & 16;
   if (acc && br.z != nullptr) return -1;
   if ((flags >> 16) & 15) return -3;  // no stream-K for the residue classes
+  // the LDS-DMA variants without a fused BN reduction: every class in one launch (MultiClass)
+  const bool one = v >= kGldsFirst && v < kGldsFirst + kNumGlds && br.z == nullptr && sh * sw <= kMaxClasses &&
+                   Co % kGldsVariants[v - kGldsFirst].kb == 0 && dgrad_one_launch();
+  MultiClass mc{};
   for (int py = 0; py < sh; ++py) {
     for (int px = 0; px < sw; ++px) {
       const int QH = H > py ? (H - py + sh - 1) / sh : 0, QW = W > px ? (W - px + sw - 1) / sw : 0;
@@ -1877,9 +1897,22 @@ TONY_API int tony_conv_dgrad_strided(const void* dy, int N, int OH, int OW, int 
       phz.rows.y0 = py;
       phz.rows.x0 = px;
       phz.bnr = br;
+      if (one) {
+        mc.c[mc.n++] = ClassDesc{g, phz.rows, BTaps{r0, s0, sh, sw, S}, static_cast<int>(M), 0};
+        continue;
+      }
       const int rc = run_nt_phase(g, wt, dx, lddx, M, C, v, phz, stream, flags & 24);
       if (rc != 0) return rc;
     }
+  }
+  if (one && mc.n > 0) {
+    // (g, M, rmap, bt of the call are placeholders: each workgroup takes its class's)
+    // tap-heaviest class first: its tiles run longest (up to 4x the 1-tap class's K)
+    std::stable_sort(mc.c, mc.c + mc.n, [](const ClassDesc& a, const ClassDesc& b) { return a.g.K > b.g.K; });
+    const ClassDesc& c0 = mc.c[0];
+    const int rc = run_glds(c0.g, wt, static_cast<int64_t>(R) * S * Co, dx, lddx, c0.M, C, flags & 24, nullptr, 0, v,
+                            stream, c0.rm, c0.bt, 0, X3Planes{}, &mc);
+    if (rc != 0) return rc;
   }
   if (br.z != nullptr) bnr->done = 1;
   return 0;

@@ -115,6 +115,27 @@ struct X3Planes {
   const float* atab = nullptr;
 };
 
+// Every residue class of a strided dgrad in ONE launch (tony_conv_dgrad_strided): the classes' tile
+// ranges sit end to end in the grid, each padded to a multiple of 8 workgroups so that the XCD remap
+// runs per class -- every XCD gets an eighth of every class (the classes differ up to 4x in taps, so a
+// whole-grid remap would hand the 4-tap class to two XCDs and the 1-tap class to two others), the
+// tap-heaviest class dispatched first; the <= 7 pad workgroups per class exit at once.  Each
+// workgroup swaps in its class's gather, row map, tap set and row count before the K loop.
+// n == 0: a single GEMM (the kernel's own arguments).  One launch instead of sh * sw: the classes'
+// tiles fill the CUs together instead of four small grids running one after another.
+struct ClassDesc {
+  Gather g;
+  RowMap rm;
+  BTaps bt;
+  int M = 0;
+  int begin = 0, tiles = 0;  // first workgroup (a multiple of 8) and tile count (set by run_glds)
+};
+constexpr int kMaxClasses = 4;
+struct MultiClass {
+  int n = 0;
+  ClassDesc c[kMaxClasses];
+};
+
 // A[M, K] row-major (row stride lda) as a Gather: one 1 x M image with K channels, 1x1 filter.
 inline Gather gemm_gather(const void* A, int64_t lda, int64_t M, int64_t K) {
   return Gather{static_cast<const uint16_t*>(A), lda, 1, static_cast<int>(M), static_cast<int>(K), 1,
@@ -202,7 +223,7 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
                                                              uint16_t* __restrict__ C, int64_t ldc, int M, int N,
                                                              float* __restrict__ stats, int64_t sstride, int epi,
                                                              int tiles_n, RowMap rmap, BTaps bt, SplitK sk,
-                                                             X3Planes xp) {
+                                                             X3Planes xp, MultiClass mc) {
   constexpr int NW = 2 * NWM;                 // waves: NWM along M x 2 along N
   constexpr int WM = BM / NWM, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int CPR = KB / 8;                // 16-B chunks per LDS row
@@ -221,6 +242,27 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
+  const int G = gridDim.x;
+  int w = 0;
+  if (mc.n > 0) {  // (uniform; static indices only, so the descriptors stay scalar kernel-argument loads)
+    const int b = blockIdx.x;
+    int sel = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxClasses; ++i)
+      if (i < mc.n && b >= mc.c[i].begin) sel = i;
+#pragma unroll
+    for (int i = 0; i < kMaxClasses; ++i)
+      if (i == sel) {
+        g = mc.c[i].g;
+        rmap = mc.c[i].rm;
+        bt = mc.c[i].bt;
+        M = mc.c[i].M;
+        w = xcd_remap(b - mc.c[i].begin, (mc.c[i].tiles + 7) & ~7);
+        if (w >= mc.c[i].tiles) return;  // pad workgroup (before any barrier)
+      }
+  } else {
+    w = xcd_remap(blockIdx.x, G);
+  }
   const int K = g.K;
   // (>= 1: a strided dgrad's tap-less residue class has K = 0 and must still write its zero tile)
   const int nk_all = max(1, (K + KB - 1) / KB);
@@ -230,8 +272,6 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
   // wave); a workgroup walks its range tile segment by tile segment.  A segment that is a whole tile
   // runs the epilogue itself; the segments of a shared tile meet in SplitK's fold.  Neighbouring
   // ranges share a tile, so the remap keeps them on one XCD.
-  const int G = gridDim.x;
-  const int w = xcd_remap(blockIdx.x, G);
   const int64_t T = static_cast<int64_t>(tiles_n) * ((M + BM - 1) / BM) * nk_all;
   int64_t it = sk.stream ? static_cast<int64_t>(w) * T / G : static_cast<int64_t>(w) * nk_all;
   const int64_t it_end = sk.stream ? static_cast<int64_t>(w + 1) * T / G : it + nk_all;
@@ -675,8 +715,11 @@ constexpr int kNumX3 = sizeof(kX3Variants) / sizeof(kX3Variants[0]);
 template <bool XF = false>
 inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N, int epi,
                     float* st, int64_t sstride, int v, hipStream_t stream, RowMap rmap = RowMap{},
-                    BTaps bt = BTaps{}, int stream_m = 0, X3Planes xp = X3Planes{}) {
+                    BTaps bt = BTaps{}, int stream_m = 0, X3Planes xp = X3Planes{},
+                    const MultiClass* classes = nullptr) {
   constexpr bool x3 = XF;
+  if (classes != nullptr && (x3 || stream_m > 0 || xp.atab != nullptr || classes->n < 1 || classes->n > kMaxClasses))
+    return -1;
   if (XF != (xp.btap != 0)) return -1;
   if (xp.atab != nullptr && (XF || bt.S != 0 || (reinterpret_cast<uintptr_t>(xp.atab) & 15))) return -1;
   if ((ldc % 8) || (ldb % 8) || (reinterpret_cast<uintptr_t>(C) & 15) || (reinterpret_cast<uintptr_t>(B) & 15) ||
@@ -700,8 +743,22 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
                   ST * PL * (BM + BN) * KB * 2 > 163840 || (X3 && IL)) {
       return -3;
     } else {
-      const int tiles_m = ceil_div(M, BM), tiles_n = ceil_div(N, BN);
-      const int64_t tiles = static_cast<int64_t>(tiles_m) * tiles_n;
+      const int tiles_n = ceil_div(N, BN);
+      MultiClass mc{};
+      int64_t tiles = 0;
+      if (classes != nullptr) {  // the classes' tile ranges end to end (M is unused then)
+        mc = *classes;
+        for (int i = 0; i < mc.n; ++i) {
+          if (mc.c[i].g.Cs % KB != 0 || mc.c[i].bt.S == 0) return -3;  // uniform-tap class taps only
+          const int64_t t = static_cast<int64_t>(ceil_div(mc.c[i].M, BM)) * tiles_n;
+          if (tiles + t + 8 > 0x7fffffff) return -2;
+          mc.c[i].begin = static_cast<int>(tiles);
+          mc.c[i].tiles = static_cast<int>(t);
+          tiles += (t + 7) & ~int64_t{7};
+        }
+      } else {
+        tiles = static_cast<int64_t>(ceil_div(M, BM)) * tiles_n;
+      }
       if (tiles > 0x7fffffff) return -2;
       SplitK sk{};
       int grid = static_cast<int>(tiles);
@@ -724,7 +781,7 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
       }
       const auto args = std::make_tuple(g, static_cast<const uint16_t*>(B), ldb, static_cast<uint16_t*>(C), ldc,
                                         static_cast<int>(M), static_cast<int>(N), st, sstride, epi, tiles_n, rmap, bt,
-                                        sk, xp);
+                                        sk, xp, mc);
       if (xp.atab != nullptr) {  // the BN-apply-on-load prototype: one tile family
         if constexpr (!X3 && !IL && BM == 128 && ST == 3 && KB == 32 && NWM == 2 && BN <= 128) {
           if (g.Cs % KB != 0 || g.R != 1 || g.S != 1) return -3;
