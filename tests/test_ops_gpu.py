@@ -535,6 +535,68 @@ def test_splitk_fold_matches_combine_pass(cuda, monkeypatch):
         torch.testing.assert_close(u, v, rtol=1e-2, atol=1e-2)
 
 
+TREE_SHAPES = [(8, 64, 35, 35, 96, 3, 1), (4, 32, 40, 40, 32, 3, 1), (4, 48, 20, 20, 64, 5, 2),
+               (4, 192, 17, 17, 320, 3, 0), (16, 64, 73, 73, 80, 1, 0), (2, 768, 17, 17, 192, 1, 0)]
+
+
+@pytest.mark.parametrize("shape", TREE_SHAPES, ids=[f"{s[1]}->{s[4]}k{s[5]}_{s[2]}" for s in TREE_SHAPES])
+def test_splitk_tree_matches_combine_and_is_deterministic(cuda, monkeypatch, shape):
+    """csrc/mfma_common.h splitk_tree_fold (opt-in: the splits of a dW tile meet pairwise in the wgrad launch)
+    against the separate combine pass and fp32 autograd: 32 / 64 / 96 / 128-row wgrad tiles, the TN GEMM
+    of a 1x1 layer with hundreds of splits, a fresh fp32 result and a bf16 slot accumulated into; two
+    runs are bit-identical (the tree's sum order is fixed by the split index, not by arrival)."""
+    from tony_amd.ops import gemm
+    from tony_amd.ops.conv import conv_wgrad
+
+    n, c, h, w, co, k, p = shape
+    torch.manual_seed(co + k)
+    x = torch.randn(n, c, h, w, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    oh, ow = h + 2 * p - k + 1, w + 2 * p - k + 1
+    dy = torch.randn(n, co, oh, ow, device=cuda).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xr = x.float().requires_grad_(True)
+    wr = torch.zeros(co, c, k, k, device=cuda, requires_grad=True)
+    torch.nn.functional.conv2d(xr, wr, None, 1, p).backward(dy.float())
+    monkeypatch.setattr(gemm, "SPLITK_FOLD", False)
+    res = {}
+    for tree in (False, True, True):
+        monkeypatch.setattr(gemm, "SPLITK_TREE", tree)
+        dw = conv_wgrad(dy, x, (co, c, k, k), 1, p, impl=1)
+        slot = torch.ones(co * k * k * c, device=cuda, dtype=torch.bfloat16)
+        conv_wgrad(dy, x, (co, c, k, k), 1, p, dst=slot, impl=1)
+        res.setdefault(tree, []).append((dw.float().clone(), slot.float()))
+    torch.cuda.synchronize()
+    (t1, s1), (t2, s2) = res[True]
+    assert torch.equal(t1, t2) and torch.equal(s1, s2)
+    tc, sc = res[False][0]
+    ref = wr.grad
+    scale = ref.abs().max().item()
+    torch.testing.assert_close(t1, ref, rtol=1e-3, atol=1e-4 * scale)
+    torch.testing.assert_close(t1, tc, rtol=1e-5, atol=1e-5 * scale)
+    torch.testing.assert_close(s1, sc, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("mnk", [(300000, 64, 80), (20000, 192, 256), (4096, 768, 136)])
+def test_splitk_tree_gemm_tn(cuda, monkeypatch, mnk):
+    """The TN wgrad GEMM (gemm.hip gemm_tn_glds_kernel) with the in-launch tree fold vs the combine pass
+    and fp32: one tile with hundreds of splits, a multi-tile grid, ragged column tiles."""
+    from tony_amd.ops import gemm
+
+    m, n1, n2 = mnk
+    torch.manual_seed(n2)
+    a = torch.randn(m, n1, device=cuda).to(torch.bfloat16)
+    b = torch.randn(m, n2, device=cuda).to(torch.bfloat16)
+    ref = a.float().t() @ b.float()
+    monkeypatch.setattr(gemm, "SPLITK_FOLD", False)
+    out = {}
+    for tree in (False, True):
+        monkeypatch.setattr(gemm, "SPLITK_TREE", tree)
+        out[tree] = gemm.gemm_tn(a, b)
+    torch.cuda.synchronize()
+    scale = ref.abs().max().item()
+    torch.testing.assert_close(out[True], ref, rtol=1e-3, atol=1e-4 * scale)
+    torch.testing.assert_close(out[True], out[False], rtol=1e-5, atol=1e-5 * scale)
+
+
 @pytest.mark.parametrize("bias", [True, False])
 @pytest.mark.parametrize("dims", [(128, 2048, 1000), (37, 768, 1000), (5, 64, 16)])
 def test_linear_mfma_fwd_bwd(cuda, dims, bias):
@@ -614,8 +676,9 @@ def test_whole_input_conv_bn_is_gemm(cuda):
     assert set(impls.values()) == {"gemm"}, impls
 
 
-@pytest.mark.parametrize("splits,n", [(128, 18432), (40, 4096), (7, 1 << 20), (3, 4000), (300, 221184)],
-                         ids=["narrow-128", "narrow-40", "wide-7", "few-3", "wide-300"])
+@pytest.mark.parametrize("splits,n", [(128, 18432), (40, 4096), (7, 1 << 20), (3, 4000), (300, 221184),
+                                      (512, 5120), (37, 9216)],
+                         ids=["narrow-128", "narrow-40", "wide-7", "few-3", "wide-300", "stem-512", "odd-37"])
 @pytest.mark.parametrize("bf16", [False, True])
 def test_splitk_reduce_sums_the_slab(cuda, splits, n, bf16):
     """csrc/splitk.hip: dst (+)= sum over splits of slab rows (many splits of a small dW, few of a large
@@ -630,7 +693,8 @@ def test_splitk_reduce_sums_the_slab(cuda, splits, n, bf16):
     for acc in (0, 1):
         base = torch.randn(n, device=cuda).to(dt)
         dst = base.clone()
-        rc = L.tony_splitk_reduce(slab.data_ptr(), splits, n, dst.data_ptr(), int(bf16), acc, _lib.num_cus(cuda), st)
+        work = slab.clone()  # scratch: the two-pass form (narrow dW, many splits) sums chunks in place
+        rc = L.tony_splitk_reduce(work.data_ptr(), splits, n, dst.data_ptr(), int(bf16), acc, _lib.num_cus(cuda), st)
         assert rc == 0
         torch.cuda.synchronize()
         want = ref + (base.double() if acc else 0)

@@ -1066,6 +1066,11 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __
     }
     __syncthreads();
   }
+  if (slab != nullptr && (fold.flags & 4)) {  // the splits meet in-launch (splitk_tree_fold)
+    splitk_tree_fold<TM, 4, kThreads>(acc, slab, K, n1_0 + wm * (TBM / 2), Co, n2_0 + wn * 64, K, tile, split,
+                                      gridDim.x / ntiles, fold);
+    return;
+  }
   // slab mode: this split's partial tile with plain stores (tony_splitk_reduce sums the splits);
   // otherwise fp32 atomics into C
   float* dst = slab != nullptr ? slab + static_cast<int64_t>(split) * Co * K : C;
@@ -1241,6 +1246,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
   if (kt < nk) step(S0{});
   if (kt + 1 < nk) step(S1{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup retires
+  if (fold.flags & 4) {  // the splits meet in-launch (splitk_tree_fold)
+    splitk_tree_fold<TM, 4, kThreads>(acc, slab, K, n1_0 + wm * (TBM / 2), Co, n2_0 + wn * 64, K, tile, split,
+                                      gridDim.x / ntiles, fold);
+    return;
+  }
   float* dst = slab + static_cast<int64_t>(split) * Co * K;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -1638,6 +1648,10 @@ int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, float
   if (grid > 0x7fffffff) return -2;
   if (slab != nullptr && splits * npairs * Co * static_cast<int64_t>(g.K) > slab_cap) return -4;  // caller's bound is off
   if (npairs > 1 && (slab == nullptr || fold.counters != nullptr)) return -1;  // the pairs meet in the slab
+  // the tree fold's workspace: one TBM x WTBN fp32 slot per workgroup, 32-bit byte offsets
+  if ((fold.flags & 4) && (fold.counters == nullptr || slab == nullptr || grid * TBM * WTBN > slab_cap ||
+                           grid * TBM * WTBN * 4 > 0x7fffffff))
+    return -3;
   if (splits_out != nullptr) *splits_out = static_cast<int>(splits * npairs);
   // LDS-DMA staging pays for the 128-row Cout tiles only (measured: Cout <= 64 tiles, whose A rows
   // are half / quarter zero chunks, run 4-8 % slower than the register-staged kernel)

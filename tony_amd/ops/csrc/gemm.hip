@@ -361,6 +361,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
   if (kt < nk) step(std::integral_constant<int, 0>{});
   if (kt + 1 < nk) step(std::integral_constant<int, 1>{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (fold.flags & 4) {  // the splits meet in-launch (splitk_tree_fold)
+    splitk_tree_fold<4, 4, kThreads>(acc, slab, N2, n1_0 + wm * 64, N1, n2_0 + wn * 64, N2, tile, split,
+                                     gridDim.x / ntiles, fold);
+    return;
+  }
   float* dst = slab + static_cast<int64_t>(split) * N1 * N2;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -443,6 +448,11 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_splitk_kernel(
     __syncthreads();
   }
   // acc[i][j] element r: row n1 = .. + (lane>>4)*4 + r, col n2 = .. + (lane&15).
+  if (slab != nullptr && (fold.flags & 4)) {  // the splits meet in-launch (splitk_tree_fold)
+    splitk_tree_fold<4, 4, kThreads>(acc, slab, N2, n1_0 + wm * 64, N1, n2_0 + wn * 64, N2, tile, split,
+                                     gridDim.x / ntiles, fold);
+    return;
+  }
   // slab mode: this split's dense [N1][N2] partial with plain stores (tony_splitk_reduce sums them)
   float* dst = slab != nullptr ? slab + static_cast<int64_t>(split) * N1 * N2 : C;
   const int64_t ld = slab != nullptr ? N2 : ldc;
@@ -498,6 +508,10 @@ TONY_API int tony_gemm_tn_bf16(const void* A, const void* B, float* C, int64_t M
   const int64_t grid = splits * ntiles;
   if (grid > 0x7fffffff) return -2;
   if (slab != nullptr && splits * N1 * N2 > slab_cap) return -4;  // caller's bound is off
+  // the tree fold's workspace: one TBM x TBN fp32 slot per workgroup, 32-bit byte offsets
+  if ((fold_flags & 4) && (fold_counters == nullptr || slab == nullptr || grid * TBM * TBN > slab_cap ||
+                           grid * TBM * TBN * 4 > 0x7fffffff))
+    return -3;
   if (splits_out != nullptr) *splits_out = static_cast<int>(splits);
   if (slab != nullptr && tn_glds_enabled())
     gemm_tn_glds_kernel<<<static_cast<int>(grid), kThreads, 0, stream>>>(

@@ -84,7 +84,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 struct SplitFold {
   unsigned* counters;  // one per tile, zero on entry; nullptr: the caller runs tony_splitk_reduce
   void* dst;
-  int flags;           // bit0: dst is bf16; bit1: add into dst
+  int flags;           // bit0: dst is bf16; bit1: add into dst; bit2: tree fold (splitk_tree_fold)
 };
 
 template <int TR, int TC>
@@ -136,7 +136,116 @@ __device__ __forceinline__ void splitk_fold_tile(const float* __restrict__ slab,
   }
 }
 
-// Column tile for a cap:// Column tile for a cap: the output channels split evenly over ceil(N/cap) tiles, rounded up to
+// ---- split-K tree fold: the splits of a tile meet pairwise inside the launch -------------------------
+// SplitFold flags bit2.  The splits of a tile are the leaves of a binary tree over the split index.
+// Every workgroup first stores its accumulators to its own workspace slot (write-through sc1 stores);
+// at each level the two workgroups holding sibling subtrees take a ticket on their node.  The first
+// publishes its slot on the node and retires; the second -- which holds a ticket after the first, so
+// the first is already past its K loop and only storing: the wait is bounded by construction -- adds
+// the published slot into its own (sc1 loads) and climbs.  The root converts its slot into dst.  Each
+// node adds left + right subtree sums, so the result does not depend on arrival order.  No separate
+// combine launch, no fences (the stream-K hand-off of igemm.h), and the partial reads are spread over
+// the splits instead of the last arriver reading all of them (splitk_fold_tile, 5x slower:
+// profiles/r2_rejected_splitk_fold_bn_onepass_prof.md).  The level loop works slot to slot, one
+// fragment at a time: holding the accumulators in registers across it cost the kernels 86-148 VGPRs
+// (the MFMA results moved out of AGPRs next to the partner's loaded copy).
+// Workspace (ws, >= gridDim.x * TM * TN * NT * 4 floats): slot (tile, split) holds the accumulators
+// lane-linearly -- fragment f of thread t at ((slot * TM * TN + f) * NT + t) * 16 bytes: 16-byte
+// coalesced accesses, each thread touching only its own elements.
+// counters: [ntiles][2 * splits] tickets then as many slot words (4 * gridDim.x words), zero on entry;
+// the second arriver of a node re-arms both.
+// acc[i][j][r] is row r0 + i * 16 + (lane >> 4) * 4 + r, column c0 + j * 16 + (lane & 15) of dst (the
+// wave's origin folded into r0, c0 by the caller).  Returns true in the workgroup that wrote dst.
+template <int TM, int TN, int NT>
+__device__ __forceinline__ bool splitk_tree_fold(f32x4 (&acc)[TM][TN], float* __restrict__ ws, int64_t ld, int r0,
+                                                 int rlim, int c0, int clim, int tile, int split, int splits,
+                                                 const SplitFold& f) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  constexpr int FR = TM * TN;
+  constexpr int SLOT = FR * NT * 16;  // bytes per slot
+  __shared__ int s_word;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(ws, 0, 0x7fffffff, 0x00020000);
+  // (< 2 * splits nodes per tile: sum over levels of ceil(splits / 2^(L+1)) <= splits - 1 + log2 splits)
+  unsigned* cnt = f.counters + static_cast<int64_t>(tile) * 2 * splits;
+  unsigned* rdy = cnt + 2 * static_cast<int64_t>(gridDim.x);
+  const int vt = threadIdx.x * 16;
+  const int own = (tile * splits + split) * SLOT;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, vt, own + (i * TN + j) * NT * 16, 16);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int level_base = 0;
+  for (int L = 0; (1 << L) < splits; ++L) {
+    const int nodes = (splits + (2 << L) - 1) >> (L + 1);
+    const int sib = ((split >> L) ^ 1) << L;
+    if (sib < splits) {  // else the sibling subtree is empty: this sum climbs as it is
+      const int node = level_base + (split >> (L + 1));
+      __syncthreads();  // every wave's slot stores have drained (each waited on its own)
+      if (threadIdx.x == 0) {
+        const unsigned t = __hip_atomic_fetch_add(cnt + node, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == 0) {  // first: publish the slot and retire
+          __hip_atomic_store(rdy + node, static_cast<unsigned>(split + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_word = -2;
+        } else {
+          unsigned v = 0;
+          for (unsigned spins = 0;
+               (v = __hip_atomic_load(rdy + node, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0 && spins < (1u << 24);
+               ++spins)
+            __builtin_amdgcn_s_sleep(1);
+          __hip_atomic_store(cnt + node, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+          __hip_atomic_store(rdy + node, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          s_word = static_cast<int>(v) - 1;  // -1: timed out (the sum climbs without the partner)
+        }
+      }
+      __syncthreads();
+      const int p = __builtin_amdgcn_readfirstlane(s_word);
+      __syncthreads();  // every wave has p before s_word is reused
+      if (p == -2) return false;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the poll
+      if (p >= 0) {
+        const int pb = (tile * splits + p) * SLOT;
+#pragma unroll
+        for (int k = 0; k < FR; ++k) {
+          const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vt, own + k * NT * 16, 16));
+          const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vt, pb + k * NT * 16, 16));
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a + b), rs, vt, own + k * NT * 16, 16);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    level_base += nodes;
+  }
+  const bool bf16 = f.flags & 1, add = f.flags & 2;
+  const int lane = threadIdx.x & 63;
+  const int lrow = r0 + (lane >> 4) * 4, lcol = c0 + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const f32x4 v4 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vt, own + (i * TN + j) * NT * 16, 16));
+      const int col = lcol + j * 16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = lrow + i * 16 + r;
+        if (row >= rlim || col >= clim) continue;
+        const int64_t e = static_cast<int64_t>(row) * ld + col;
+        float v = v4[r];
+        if (bf16) {
+          uint16_t* q = static_cast<uint16_t*>(f.dst) + e;
+          if (add) v += __uint_as_float(static_cast<uint32_t>(*q) << 16);
+          *q = f2bf(v);
+        } else {
+          float* q = static_cast<float*>(f.dst) + e;
+          *q = add ? *q + v : v;
+        }
+      }
+    }
+  return true;
+}
+
+// Column tile for a cap: the output channels split evenly over ceil(N/cap) tiles, rounded up to
 // the 32-column granule of the 2x2 wave layout (16-wide MFMA per wave), so no MFMA work is spent on
 // padding columns for Cout = 32..384 (Inception's 48/80/96/160/192/320/384).
 inline int64_t pick_bn(int64_t N, int64_t cap) {

@@ -7,6 +7,8 @@
 // 17x17 Inception conv -- so the partials are stored plainly to a slab and summed here, and the sum
 // lands directly in the parameter's (bf16 or fp32) flat-gradient slot: no zero-fill of a dW
 // accumulator, no separate accumulate kernel.
+#include <algorithm>
+
 #include "common.h"
 
 using namespace tony;
@@ -17,17 +19,27 @@ namespace {
 // loads in flight per thread per round), the groups combine through LDS, group 0 writes.
 constexpr int kCols = 64, kGroups = 4;
 
+// blockIdx.y = chunk of `chunk` splits (rows rstride floats apart) summed into dst + blockIdx.y * dstride:
+// one chunk of all splits (the combine), or the first of two passes when the columns alone cannot
+// fill the GPU -- a stem layer's ~10 K floats over 512 splits ran 34-66 us as 20-36 workgroups each
+// walking all 512 rows; pass 1 sums chunks in place (chunk g's sum over its own first row, read only
+// by this workgroup), pass 2 the chunk sums.
 template <bool BF16>
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, int splits, int64_t n,
-                                                            void* __restrict__ dst, int accumulate) {
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* slab, int splits, int chunk,
+                                                            int64_t n, int64_t rstride, void* dst,
+                                                            int64_t dstride, int accumulate) {
   __shared__ float4 part[kGroups - 1][kCols];
   const int col = threadIdx.x % kCols, grp = threadIdx.x / kCols;
   const int64_t n4 = n >> 2;
   const int64_t i = static_cast<int64_t>(blockIdx.x) * kCols + col;
+  const int s0 = blockIdx.y * chunk;
+  splits = min(splits - s0, chunk);
+  dst = BF16 ? static_cast<void*>(static_cast<uint16_t*>(dst) + blockIdx.y * dstride)
+             : static_cast<void*>(static_cast<float*>(dst) + blockIdx.y * dstride);
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i < n4) {
-    const float4* base = reinterpret_cast<const float4*>(slab) + i;
-    const int64_t stride = n4;  // float4s between consecutive splits
+    const float4* base = reinterpret_cast<const float4*>(slab + s0 * rstride) + i;
+    const int64_t stride = rstride >> 2;  // float4s between consecutive splits
     int k = grp;
     for (; k + 3 * kGroups < splits; k += 4 * kGroups) {
       const float4 a = base[(k)*stride], b = base[(k + kGroups) * stride];
@@ -83,18 +95,33 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 
 }  // namespace
 
-// n % 4 == 0; slab 16-B aligned, dst 8-B (bf16) / 16-B (fp32) aligned.
+// n % 4 == 0; slab 16-B aligned, dst 8-B (bf16) / 16-B (fp32) aligned.  The slab is scratch: with
+// fewer column blocks than CUs and >= 32 splits the first pass overwrites chunk rows with their sums.
 TONY_API int tony_splitk_reduce(const float* slab, int splits, int64_t n, void* dst, int dst_bf16, int accumulate,
                                 int num_cus, hipStream_t stream) {
   if (slab == nullptr || dst == nullptr || splits <= 0 || n <= 0 || (n % 4)) return -1;
   if ((reinterpret_cast<uintptr_t>(slab) & 15) || (reinterpret_cast<uintptr_t>(dst) & (dst_bf16 ? 7 : 15))) return -1;
-  (void)num_cus;
   const int64_t grid = (n / 4 + kCols - 1) / kCols;
   if (grid > 0x7fffffff) return -2;
+  const int cus = num_cus > 0 ? num_cus : 256;
+  int64_t rstride = n;
+  if (grid < cus && splits >= 32) {  // pass 1: chunks of >= 16 splits spread the columns over ~2 x CUs
+    const int want = static_cast<int>(std::min<int64_t>((2 * cus + grid - 1) / grid, splits / 16));
+    const int chunk = (splits + want - 1) / want;
+    const int groups = (splits + chunk - 1) / chunk;
+    float* s = const_cast<float*>(slab);
+    splitk_reduce_kernel<false><<<dim3(static_cast<unsigned>(grid), groups), 256, 0, stream>>>(
+        slab, splits, chunk, n, n, s, chunk * n, 0);
+    TONY_LAUNCH_CHECK();
+    rstride = chunk * n;
+    splits = groups;
+  }
   if (dst_bf16)
-    splitk_reduce_kernel<true><<<static_cast<int>(grid), 256, 0, stream>>>(slab, splits, n, dst, accumulate);
+    splitk_reduce_kernel<true><<<static_cast<int>(grid), 256, 0, stream>>>(slab, splits, splits, n, rstride, dst, 0,
+                                                                          accumulate);
   else
-    splitk_reduce_kernel<false><<<static_cast<int>(grid), 256, 0, stream>>>(slab, splits, n, dst, accumulate);
+    splitk_reduce_kernel<false><<<static_cast<int>(grid), 256, 0, stream>>>(slab, splits, splits, n, rstride, dst, 0,
+                                                                           accumulate);
   TONY_LAUNCH_CHECK();
   return 0;
 }

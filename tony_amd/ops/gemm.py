@@ -71,6 +71,13 @@ def wgrad_cus(device, occ: int = 1) -> int:
 # measured on MI355X it serialises each tile's ~100-split reduction on ONE workgroup -- the Inception
 # wgrads went from 74 to 404 us (profiles/r2_rejected_splitk_fold_bn_onepass_prof.md).
 SPLITK_FOLD = os.environ.get("TONY_SPLITK_FOLD", "0") == "1"
+# TONY_SPLITK_TREE=1: the splits of each dW tile meet pairwise inside the wgrad launch
+# (mfma_common.h splitk_tree_fold: a binary tree over the split index, each workgroup reads at most
+# one partner's partial per level) -- no tony_splitk_reduce launch.  Off by default: measured on
+# MI355X every level is a 64 KB read-add-write by ONE workgroup (~100-200 GB/s per CU) behind a
+# ticket, so the 5-9 levels add 25-45 us to each wgrad where the chip-wide combine takes ~8 us:
+# Inception conv time 11.47 -> 14.58 ms/step, step 14.22 -> 15.03 ms (profiles/r5_rejected_splitk_tree.log)
+SPLITK_TREE = os.environ.get("TONY_SPLITK_TREE", "0") == "1"
 
 
 def splitk_combine(launch, n: int, ntiles: int, device, dst: torch.Tensor | None = None, occ: int = 1,
@@ -87,10 +94,22 @@ def splitk_combine(launch, n: int, ntiles: int, device, dst: torch.Tensor | None
     (csrc/conv.hip tony_conv_wgrad_x3), each with its own splits of that plan divided by ``pairs``."""
     cus = wgrad_cus(device, occ)
     bound = pairs * max(1, -(-2 * cus // (pairs * ntiles)))
-    slab = torch.empty(bound * n, dtype=torch.float32, device=device)
+    tree = SPLITK_TREE and pairs == 1
+    # the tree's workspace: a 128 x 128 fp32 slot per workgroup; the kernel's grid is at most
+    # 2 * cus + its tile count (its tiles may be 4x narrower than the 128-row ntiles the caller counts)
+    wgs = 2 * cus + 4 * ntiles + 8
+    slab = torch.empty(max(bound * n, wgs * 128 * 128) if tree else bound * n, dtype=torch.float32, device=device)
     splits = ctypes.c_int(0)
     out = dst if dst is not None else torch.empty(n, dtype=torch.float32, device=device)
     flags = int(out.dtype == torch.bfloat16) | (2 if dst is not None else 0)
+    if tree:
+        counters = zeros_f32(4 * wgs, device)  # 4 words per workgroup
+        rc = launch(slab.data_ptr(), slab.numel(), ctypes.addressof(splits), counters.data_ptr(), out.data_ptr(),
+                    flags | 4)
+        if rc == 0:
+            return None if dst is not None else out
+        if rc != -3:  # -3: no tree for this launch (x3 plane pairs, 2 GB slab): the combine below
+            _lib.check(rc, "split-K wgrad (tree)")
     if SPLITK_FOLD and pairs == 1:
         counters = zeros_f32(ntiles, device)  # zero bits = zero uint32 arrival counters
         _lib.check(launch(slab.data_ptr(), slab.numel(), ctypes.addressof(splits), counters.data_ptr(), out.data_ptr(),
