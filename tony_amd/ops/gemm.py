@@ -59,11 +59,17 @@ def _gemm_rows(a_ptr, lda, b, M, N, K, out_ptr, ldc, device):
 # mean more fp32 partials through HBM (~1 GB of slab per step at the tuned 2-4x): restricting the
 # search to occ = 1 measured 14.43 / 14.47 vs 14.55 / 14.62 ms of GPU time per step
 # (profiles/r2s3_wgrad_occ_ab.log).  TONY_WGRAD_OCC=1,2,4,8 restores the isolated-speed search.
-WGRAD_OCC = tuple(int(o) for o in os.environ.get("TONY_WGRAD_OCC", "1").split(","))
+# Fractions (TONY_WGRAD_OCC=0.5) plan fewer workgroups than CUs: fewer splits, less slab traffic for the
+# combine, fewer CUs taken from the data-gradient chain the wgrads overlap with.
+# Default 0.5 (one workgroup per CU instead of two): 14.16 / 14.34 vs 14.40 / 14.38 ms/step mean over
+# two A/Bs of three repetitions, GPU-ahead time 14.24 vs 14.41 (profiles/r5_ab_wgrad_occ.log).
+WGRAD_OCC = tuple((float(o) if "." in o else int(o)) for o in os.environ.get("TONY_WGRAD_OCC", "0.5").split(","))
+# the x3 (fp32) weight gradients' plan (ops/x3.py conv_wgrad)
+X3_WGRAD_OCC = float(os.environ.get("TONY_X3_WGRAD_OCC", "1"))
 
 
-def wgrad_cus(device, occ: int = 1) -> int:
-    return _lib.num_cus(device) * occ
+def wgrad_cus(device, occ: float = 1) -> int:
+    return max(1, int(round(_lib.num_cus(device) * occ)))
 
 
 # TONY_SPLITK_FOLD=1: the last workgroup of each dW tile sums the split partials inside the wgrad
