@@ -29,7 +29,7 @@ import torch
 from . import _lib, concat, streams, tape, tune, wt_cache
 from .arena import zeros_f32
 from .bn import HOST_MEMO, _accum_ok, _as_rows, _rows_view
-from .gemm import WGRAD_OCC, splitk_combine, wgrad_cus, wgrad_tn
+from .gemm import occ_choices, splitk_combine, wgrad_cus, wgrad_tn
 
 _BF16 = torch.bfloat16
 AUTOTUNE = os.environ.get("TONY_CONV_AUTOTUNE", "1") != "0"
@@ -404,9 +404,9 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, weight_shape, stride=1, paddin
                 dy.shape[3], 0, slab, cap, sp, wgrad_cus(dev, occ), fc, fd, ff, _lib.stream_ptr(dev)),
             co * r * s * c, ntiles, dev, dst_, occ)
 
-    choices = WGRAD_OCC
+    choices = occ_choices(n * dy.shape[2] * dy.shape[3])
     if WGRAD_DIRECT and wgrad_direct_supported(c, co, r, s, sh, sw):
-        choices = ("direct",) + tuple(WGRAD_OCC)
+        choices = ("direct",) + tuple(choices)
     if impl is not None:  # tests: a fixed path ("direct" or an occupancy)
         occ = impl
     else:

@@ -64,6 +64,24 @@ def _gemm_rows(a_ptr, lda, b, M, N, K, out_ptr, ldc, device):
 # Default 0.5 (one workgroup per CU instead of two): 14.16 / 14.34 vs 14.40 / 14.38 ms/step mean over
 # two A/Bs of three repetitions, GPU-ahead time 14.24 vs 14.41 (profiles/r5_ab_wgrad_occ.log).
 WGRAD_OCC = tuple((float(o) if "." in o else int(o)) for o in os.environ.get("TONY_WGRAD_OCC", "0.5").split(","))
+# TONY_WGRAD_OCC_BIG: the plan for wgrads over >= TONY_WGRAD_BIG_ROWS rows (the stem layers, whose
+# wgrads close the backward pass with little left to overlap them); empty: TONY_WGRAD_OCC.  Default 2
+# above 600 K rows (Inception's 147x147 / 73x73 stem): 14.04 vs 14.13 ms/step over 4 repetitions; at
+# 400 K rows it also took ResNet-50's mid-network 56x56 layers and cost 0.45 % there
+# (profiles/r5_ab_wgrad_occ.log)
+def _occ_list(v: str):
+    return tuple((float(o) if "." in o else int(o)) for o in v.split(",") if o)
+
+
+WGRAD_OCC_BIG = _occ_list(os.environ.get("TONY_WGRAD_OCC_BIG", "2"))
+WGRAD_BIG_ROWS = int(os.environ.get("TONY_WGRAD_BIG_ROWS", "600000"))
+
+
+def occ_choices(rows: int):
+    """The split plans (workgroups per CU) a weight gradient over ``rows`` reduction rows may use."""
+    return WGRAD_OCC_BIG if WGRAD_OCC_BIG and rows >= WGRAD_BIG_ROWS else WGRAD_OCC
+
+
 # the x3 (fp32) weight gradients' plan (ops/x3.py conv_wgrad)
 X3_WGRAD_OCC = float(os.environ.get("TONY_X3_WGRAD_OCC", "1"))
 
@@ -140,7 +158,7 @@ def wgrad_tn(a_ptr, lda, b_ptr, ldb, M, n1, n2, device, dst: torch.Tensor | None
             a_ptr, b_ptr, 0, M, n1, n2, lda, ldb, n2, slab, cap, sp, wgrad_cus(device, occ), fc, fd, ff, stream),
                               n1 * n2, ntiles, device, dst_, occ)
 
-    occ = tune.pick_choice(("wgrad_tn", M, n1, n2, lda, ldb), WGRAD_OCC, run)
+    occ = tune.pick_choice(("wgrad_tn", M, n1, n2, lda, ldb), occ_choices(M), run)
     out = run(occ, dst)
     return None if out is None else out.view(n1, n2)
 
