@@ -84,6 +84,13 @@ def occ_choices(rows: int):
 
 # the x3 (fp32) weight gradients' plan (ops/x3.py conv_wgrad)
 X3_WGRAD_OCC = float(os.environ.get("TONY_X3_WGRAD_OCC", "1"))
+# 2 on the stem-size layers: 32.32 vs 32.42 ms per fp32 step (profiles/r5_ab_wgrad_occ.log); 0: X3_WGRAD_OCC
+X3_WGRAD_OCC_BIG = float(os.environ.get("TONY_X3_WGRAD_OCC_BIG", "2") or 0)
+
+
+def x3_occ(rows: int) -> float:
+    """The split plan of an x3 weight gradient over ``rows`` reduction rows."""
+    return X3_WGRAD_OCC_BIG if X3_WGRAD_OCC_BIG > 0 and rows >= WGRAD_BIG_ROWS else X3_WGRAD_OCC
 
 
 def wgrad_cus(device, occ: float = 1) -> int:

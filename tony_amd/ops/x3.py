@@ -191,7 +191,7 @@ def conv_wgrad(d3: torch.Tensor, x3: torch.Tensor, cp: int, wshape, stride, padd
     launches, three combines and an fp32 accumulator fill (profiles/r3s2_fp32_x3_steady.md).
     ``dst``: an fp32 gradient slot in [Co][R][S][C] memory (C a multiple of 8) that the combine adds
     dW into; returns None then."""
-    from .gemm import X3_WGRAD_OCC, splitk_combine, wgrad_cus
+    from .gemm import splitk_combine, wgrad_cus, x3_occ
 
     co, c, r, s = wshape
     dev = d3.device
@@ -205,11 +205,12 @@ def conv_wgrad(d3: torch.Tensor, x3: torch.Tensor, cp: int, wshape, stride, padd
         return _wgrad_direct3(d3, lddy, x3, ldx, n, h, w, c, co, ph, pw, oh, ow, dst)
     tbm = 32 if co <= 32 else 64 if co <= 64 else 128  # csrc/conv.hip wgrad tile rows
     ntiles = -(-co // tbm) * -(-(r * s * cp) // 128)
+    occ = x3_occ(n * oh * ow)
     acc = splitk_combine(
         lambda slab, cap, sp, fc, fd, ff: L.tony_conv_wgrad_x3(
             d3.data_ptr(), lddy, x3.data_ptr(), n, h, w, cp, ldx, co, r, s, sh, sw, ph, pw, oh, ow, co, cp, slab, cap,
-            sp, wgrad_cus(dev, X3_WGRAD_OCC), _lib.stream_ptr(dev)),
-        co * r * s * cp, ntiles, dev, dst if cp == c else None, 1, pairs=3)
+            sp, wgrad_cus(dev, occ), _lib.stream_ptr(dev)),
+        co * r * s * cp, ntiles, dev, dst if cp == c else None, occ, pairs=3)
     if acc is None:
         return None
     dw = acc.view(co, r, s, cp)
