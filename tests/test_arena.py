@@ -91,3 +91,24 @@ def test_conv_pair_fast_path():
     from tony_amd.ops.conv import _pair
 
     assert _pair(3) == (3, 3) and _pair((1, 2)) == (1, 2) and _pair([2, 1]) == (2, 1)
+
+
+def test_wgrad_split_plans(monkeypatch):
+    """ops/gemm.py: the weight-gradient split plan (workgroups per CU) -- the default for every layer,
+    the stem-size override above WGRAD_BIG_ROWS reduction rows, fractional plans rounded to whole CUs."""
+    from tony_amd.ops import _lib, gemm
+
+    monkeypatch.setattr(_lib, "num_cus", lambda device: 256)
+    assert gemm.wgrad_cus("cpu", 0.5) == 128 and gemm.wgrad_cus("cpu", 2) == 512
+    assert gemm.wgrad_cus("cpu", 0.001) == 1
+    monkeypatch.setattr(gemm, "WGRAD_OCC", (0.5,))
+    monkeypatch.setattr(gemm, "WGRAD_OCC_BIG", (2,))
+    monkeypatch.setattr(gemm, "WGRAD_BIG_ROWS", 600000)
+    assert gemm.occ_choices(128 * 35 * 35) == (0.5,)     # mid-network layer: one workgroup per 2 CUs
+    assert gemm.occ_choices(128 * 73 * 73) == (2,)       # the stem's 73x73 / 147x147 layers
+    monkeypatch.setattr(gemm, "WGRAD_OCC_BIG", ())
+    assert gemm.occ_choices(128 * 147 * 147) == (0.5,)   # override off
+    monkeypatch.setattr(gemm, "X3_WGRAD_OCC", 1.0)
+    monkeypatch.setattr(gemm, "X3_WGRAD_OCC_BIG", 2.0)
+    assert gemm.x3_occ(128 * 17 * 17) == 1.0 and gemm.x3_occ(128 * 147 * 147) == 2.0
+    assert gemm._occ_list("0.5,1,2") == (0.5, 1, 2) and gemm._occ_list("") == ()
