@@ -176,6 +176,10 @@ _SIGNATURES = {
     "tony_avgpool_fwd_f32": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
     "tony_avgpool_bwd_f32": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int64, c_int64, c_void_p],
     "tony_x3_split": [c_void_p, c_int64, c_int64, c_int, c_int, c_void_p, c_int64, c_int, c_void_p],
+    "tony_x3_split_slice": [c_void_p, c_int64, c_int64, c_int, c_void_p, c_int64, c_int, c_int, c_void_p],
+    "tony_bn_apply_f32_p3": [c_void_p, c_int64, c_int, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int64,
+                             c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int, c_float, c_int, c_int, c_void_p,
+                             c_void_p, c_void_p, c_void_p, c_float, c_void_p],
     "tony_x3_weights_t": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
     # native replay of a captured step (csrc/plan.hip, ops/plan.py)
     "tony_plan_mark": [c_int, c_void_p],

@@ -15,11 +15,18 @@ several custom Functions legal.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Sequence
 
 import torch
 
 from . import tape
+
+# TONY_X3_CONCAT_PLANES=1: an fp32 block output also carries its x3 operand planes (ops/x3.py), filled
+# slice by slice by the producers that write its slots (the BN apply kernels write both forms) and, for
+# the slices no producer covered (max-pool branches, fallbacks), by one slice split in ``assemble`` -- so
+# the next block's convs find the planes already made instead of splitting the whole fp32 concat.
+X3_PLANES = os.environ.get("TONY_X3_CONCAT_PLANES", "0") == "1"
 
 
 class Slot:
@@ -48,7 +55,47 @@ def take(slot: Optional[Slot], n, c, h, w, like: torch.Tensor) -> Optional[torch
 
 
 def concat_buffer(n, c, h, w, like: torch.Tensor) -> torch.Tensor:
-    return torch.empty((n, c, h, w), dtype=like.dtype, device=like.device, memory_format=torch.channels_last)
+    buf = torch.empty((n, c, h, w), dtype=like.dtype, device=like.device, memory_format=torch.channels_last)
+    if X3_PLANES and like.dtype == torch.float32 and like.is_cuda and c % 8 == 0:
+        buf._tony_p3 = torch.empty((n, h, w, 3 * c), dtype=torch.bfloat16, device=like.device)
+        buf._tony_p3_cov = set()  # channel offsets of the slices whose planes a producer wrote
+    return buf
+
+
+def planes_of(slot: Optional[Slot], c: int):
+    """(pointer, row stride, plane stride) of slot's slice of its buffer's x3 planes, or None."""
+    if slot is None or c % 8 or slot.c0 % 8:
+        return None
+    p3 = getattr(slot.buf, "_tony_p3", None)
+    if p3 is None:
+        return None
+    ctot = slot.buf.shape[1]
+    return p3.data_ptr() + 2 * slot.c0, 3 * ctot, ctot
+
+
+def planes_written(slot: Slot) -> None:
+    slot.buf._tony_p3_cov.add(slot.c0)
+
+
+def _finish_planes(buf: torch.Tensor, widths, out: torch.Tensor) -> None:
+    """Split the slices no producer covered into buf's planes and hang them on the block output, where
+    ops/x3.split_act finds them."""
+    from . import _lib
+    from .x3 import ACT
+
+    p3, cov = buf._tony_p3, buf._tony_p3_cov
+    n, ctot, h, w = buf.shape
+    L, st = _lib.lib(), _lib.stream_ptr(buf.device)
+    c0 = 0
+    for c in widths:
+        if c0 not in cov:
+            if c % 8:
+                return  # cannot split this slice in place: the consumers split the whole concat
+            rc = L.tony_x3_split_slice(buf.data_ptr() + 4 * c0, ctot, n * h * w, c, p3.data_ptr() + 2 * c0, 3 * ctot,
+                                       ctot, ACT, st)
+            _lib.check(rc, "tony_x3_split_slice")
+        c0 += c
+    out._tony_x3 = (out._version, p3.permute(0, 3, 1, 2), ctot)
 
 
 class _AssembleFn(torch.autograd.Function):
@@ -80,4 +127,7 @@ class _AssembleFn(torch.autograd.Function):
 
 def assemble(buf: torch.Tensor, parts: Sequence[torch.Tensor]) -> torch.Tensor:
     """The block output ``buf`` (= cat(parts, 1)), with the parts already written into it in place."""
-    return tape.apply(_AssembleFn, Slot(buf, 0), *parts)
+    out = tape.apply(_AssembleFn, Slot(buf, 0), *parts)
+    if getattr(buf, "_tony_p3", None) is not None and out.is_cuda:
+        _finish_planes(buf, [p.shape[1] for p in parts], out)
+    return out

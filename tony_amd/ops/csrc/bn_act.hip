@@ -169,7 +169,8 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
     int64_t sstride, const void* gamma, const void* beta, int param_bf16, float eps, int relu, int mode,
     float* __restrict__ save_mean, float* __restrict__ save_invstd,
     float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, Segs segs,
-    uint8_t* __restrict__ mask = nullptr, int64_t ldm = 0) {
+    uint8_t* __restrict__ mask = nullptr, int64_t ldm = 0, uint16_t* __restrict__ p3 = nullptr, int64_t ldp = 0,
+    int64_t pst = 0) {
   float* scale = bn_dyn;  // [C] then shift [C]: bn_lds_table(C, 2) bytes
   float* shift = bn_dyn + C;
   const float inv_m = 1.f / static_cast<float>(M);
@@ -237,6 +238,17 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
     }
     const V8<T> out = V8<T>::from_float(f);
     out.store(yb + row * ldyt);
+    if (!X3 && p3 != nullptr) {  // also the x3 planes of y (a concat slot's slice of the block's planes)
+      const V8<uint16_t> hi = V8<uint16_t>::from_float(f);
+      float hf[8], lo[8];
+      hi.to_float(hf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) lo[j] = f[j] - hf[j];
+      uint16_t* d = p3 + row * ldp + rm.cg * 8;
+      hi.store(d);
+      V8<uint16_t>::from_float(lo).store(d + pst);
+      hi.store(d + 2 * pst);
+    }
     if (RES && mask != nullptr) {  // the stored values' sign, exactly what re-reading y would test
       float g[8];
       out.to_float(g);
@@ -1071,6 +1083,28 @@ TONY_API int tony_bn_apply_f32(const void* x, int64_t M, int C, int64_t ldx, voi
   bn_fwd_apply_kernel<false, float><<<grid, kThreads, bn_lds_table(C, 2), stream>>>(
       static_cast<const float*>(x), M, C, ldx, rpb, nullptr, 0, static_cast<float*>(y), ldy, sum, sumsq, sstride,
       gamma, beta, param_bf16, eps, relu, mode, save_mean, save_invstd, running_mean, running_var, momentum, Segs{});
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// tony_bn_apply_f32 that ALSO writes y's x3 planes: p3 = the channel-c0 column of a [M][3 * pst] bf16 planes
+// buffer (row stride ldp, plane p at column p * pst) -- a concat slot producer filling its slice of the
+// block output's planes, so the next block's x3 convs need no split pass over the fp32 concat
+TONY_API int tony_bn_apply_f32_p3(const void* x, int64_t M, int C, int64_t ldx, void* y, int64_t ldy, void* p3,
+                                  int64_t ldp, int64_t pst, const float* sum, const float* sumsq, int64_t sstride,
+                                  const void* gamma, const void* beta, int param_bf16, float eps, int relu, int mode,
+                                  float* save_mean, float* save_invstd, float* running_mean, float* running_var,
+                                  float momentum, hipStream_t stream) {
+  if (bad_c(C) || (ldx % 4) || (ldy % 4) || sstride < 0 || p3 == nullptr || pst < C || ldp < 3 * pst || (ldp % 8) ||
+      (pst % 8) || (reinterpret_cast<uintptr_t>(p3) & 15))
+    return -1;
+  int64_t rpb;
+  int grid;
+  plan_rows(M, C, 4, 8192, &rpb, &grid);
+  bn_fwd_apply_kernel<false, float><<<grid, kThreads, bn_lds_table(C, 2), stream>>>(
+      static_cast<const float*>(x), M, C, ldx, rpb, nullptr, 0, static_cast<float*>(y), ldy, sum, sumsq, sstride,
+      gamma, beta, param_bf16, eps, relu, mode, save_mean, save_invstd, running_mean, running_var, momentum, Segs{},
+      nullptr, 0, static_cast<uint16_t*>(p3), ldp, pst);
   TONY_LAUNCH_CHECK();
   return 0;
 }

@@ -30,7 +30,7 @@ __device__ __forceinline__ void split1(float x, uint16_t& hi, uint16_t& lo) {
 // plane p holds lo, clear: hi.  One thread per (row, 4-channel group of cp).
 __global__ __launch_bounds__(kThreads) void split3_kernel(const float* __restrict__ src, int64_t lds, int64_t rows,
                                                           int C, int cp, uint16_t* __restrict__ dst, int64_t ldd,
-                                                          int pattern, int vec) {
+                                                          int pattern, int vec, int pst) {
   const int G = cp >> 2;
   const int64_t total = rows * G;
   for (int64_t t = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; t < total;
@@ -53,7 +53,7 @@ __global__ __launch_bounds__(kThreads) void split3_kernel(const float* __restric
     const uint2 L = make_uint2(lo[0] | (static_cast<uint32_t>(lo[1]) << 16), lo[2] | (static_cast<uint32_t>(lo[3]) << 16));
     uint16_t* d = dst + r * ldd + c;
 #pragma unroll
-    for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(d + p * cp) = (pattern >> p) & 1 ? L : H;
+    for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(d + p * pst) = (pattern >> p) & 1 ? L : H;
   }
 }
 
@@ -167,7 +167,23 @@ TONY_API int tony_x3_split(const void* src, int64_t lds, int64_t rows, int C, in
   if (rows == 0) return 0;
   const int vec = (C % 4 == 0) && (lds % 4 == 0) && !(reinterpret_cast<uintptr_t>(src) & 15);
   split3_kernel<<<grid_for(rows * (cp / 4)), kThreads, 0, stream>>>(static_cast<const float*>(src), lds, rows, C, cp,
-                                                                     static_cast<uint16_t*>(dst), ldd, pattern, vec);
+                                                                     static_cast<uint16_t*>(dst), ldd, pattern, vec, cp);
+  TONY_LAUNCH_CHECK();
+  return 0;
+}
+
+// tony_x3_split of a channel slice into a wider planes buffer: dst = the slice's first column of a
+// [rows][3 * pst] planes buffer (plane p at column p * pst); C % 8 == 0 (no padding columns written)
+TONY_API int tony_x3_split_slice(const void* src, int64_t lds, int64_t rows, int C, void* dst, int64_t ldd, int pst,
+                                 int pattern, hipStream_t stream) {
+  if (src == nullptr || dst == nullptr || rows < 0 || C <= 0 || (C % 8) || pst < C || (pst % 4) || lds < C ||
+      ldd < 3 * pst || (ldd % 4) || (reinterpret_cast<uintptr_t>(dst) & 7) || pattern < 0 || pattern > 7)
+    return -1;
+  if (rows == 0) return 0;
+  const int vec = (lds % 4 == 0) && !(reinterpret_cast<uintptr_t>(src) & 15);
+  split3_kernel<<<grid_for(rows * (C / 4)), kThreads, 0, stream>>>(static_cast<const float*>(src), lds, rows, C, C,
+                                                                    static_cast<uint16_t*>(dst), ldd, pattern, vec,
+                                                                    pst);
   TONY_LAUNCH_CHECK();
   return 0;
 }

@@ -256,23 +256,32 @@ def _wgrad_direct3(d3, lddy, x3, ldx, n, h, w, c, co, ph, pw, oh, ow, dst=None):
 
 
 # ---- BatchNorm on fp32 rows -------------------------------------------------------------------------
-def bn_apply(z: torch.Tensor, stats, gamma, beta, rmean, rvar, eps, momentum, relu, training, out=None):
+def _apply_f32(L, x_ptr, m, c, ldx, y, slot, tail):
+    """tony_bn_apply_f32 of ``c`` channels into ``y``; when y is a concat slot whose buffer carries x3
+    planes (ops/concat.X3_PLANES), the same pass also writes the slot's slice of the planes."""
+    p3 = concat.planes_of(slot, c) if slot is not None and y.data_ptr() == slot.view(c).data_ptr() else None
+    if p3 is not None:
+        rc = L.tony_bn_apply_f32_p3(x_ptr, m, c, ldx, y.data_ptr(), _rows_view(y)[2], *p3, *tail)
+        _lib.check(rc, "tony_bn_apply_f32_p3")
+        concat.planes_written(slot)
+        return
+    _lib.check(L.tony_bn_apply_f32(x_ptr, m, c, ldx, y.data_ptr(), _rows_view(y)[2], *tail), "tony_bn_apply_f32")
+
+
+def bn_apply(z: torch.Tensor, stats, gamma, beta, rmean, rvar, eps, momentum, relu, training, out=None, slot=None):
     """y = act(BN(z)) in fp32; training: batch statistics from ``stats`` (sharded [sum | sumsq]),
     running statistics updated.  ``out``: a channel slice of a block's concat buffer (ops/concat.py) to
-    write y into.  Returns (y, mean, invstd)."""
+    write y into (``slot``: that slice's Slot).  Returns (y, mean, invstd)."""
     n, co, oh, ow = z.shape
     m = n * oh * ow
     y = out if out is not None else _cl(n, co, oh, ow, z.device)
-    ldy = _rows_view(y)[2]
     mean = torch.empty(co, dtype=_F32, device=z.device)
     invstd = torch.empty(co, dtype=_F32, device=z.device)
-    L = _lib.lib()
-    rc = L.tony_bn_apply_f32(z.data_ptr(), m, co, co, y.data_ptr(), ldy, _lib.ptr(stats),
-                             None if stats is None else stats.data_ptr() + 4 * co, 2 * co if stats is not None else 0,
-                             gamma.data_ptr(), beta.data_ptr(), 0, float(eps), int(relu), 0 if training else 1,
-                             mean.data_ptr(), invstd.data_ptr(), _lib.ptr(rmean), _lib.ptr(rvar), float(momentum),
-                             _lib.stream_ptr(z.device))
-    _lib.check(rc, "tony_bn_apply_f32")
+    _apply_f32(_lib.lib(), z.data_ptr(), m, co, co, y, slot if out is not None else None,
+               (_lib.ptr(stats), None if stats is None else stats.data_ptr() + 4 * co,
+                2 * co if stats is not None else 0, gamma.data_ptr(), beta.data_ptr(), 0, float(eps), int(relu),
+                0 if training else 1, mean.data_ptr(), invstd.data_ptr(), _lib.ptr(rmean), _lib.ptr(rvar),
+                float(momentum), _lib.stream_ptr(z.device)))
     return y, mean, invstd
 
 
@@ -349,7 +358,7 @@ class _ConvBNActX3Fn(torch.autograd.Function):
             y = torch.empty_strided((n, co, oh, ow), (0, 0, 0, 0), dtype=_F32, device=z.device)  # shape only
         else:
             y, mean, invstd = bn_apply(z, stats, gamma, beta, rmean, rvar, eps, momentum, relu, training,
-                                       out=concat.take(slot, n, co, oh, ow, z))
+                                       out=concat.take(slot, n, co, oh, ow, z), slot=slot)
         ctx.save_for_backward(x3, weight, gamma, beta, z, mean, invstd)
         ctx.conf = (cp, tuple(x.shape), stride, padding, relu, x.requires_grad)
         ctx.join = getattr(x, "_tony_join", None)  # ops/residual.py GradJoin: x has other consumers
@@ -460,10 +469,9 @@ class _HeadX3Fn(torch.autograd.Function):
                 y = concat.take(slot, n, ci, h, w, z)
                 if y is None:
                     y = _cl(n, ci, h, w, dev)
-                rc = L.tony_bn_apply_f32(_o(z, c0), m, ci, ctot, y.data_ptr(), _rows_view(y)[2], *sp(c0),
-                                         _o(gamma, c0), _o(beta, c0), 0, float(eps), 1, mode, _o(mean, c0),
-                                         _o(invstd, c0), _o(rmean, c0), _o(rvar, c0), float(momentum), st)
-                _lib.check(rc, "tony_bn_apply_f32 (head)")
+                _apply_f32(L, _o(z, c0), m, ci, ctot, y, slot,
+                           (*sp(c0), _o(gamma, c0), _o(beta, c0), 0, float(eps), 1, mode, _o(mean, c0),
+                            _o(invstd, c0), _o(rmean, c0), _o(rvar, c0), float(momentum), st))
                 outs.append(y)
             c0 += ci
         p = None
@@ -482,11 +490,10 @@ class _HeadX3Fn(torch.autograd.Function):
             y = concat.take(slot, n, npool, h, w, z)
             if y is None:
                 y = _cl(n, npool, h, w, dev)
-            rc = L.tony_bn_apply_f32(p.data_ptr(), m, npool, npool, y.data_ptr(), _rows_view(y)[2], _lib.ptr(pstats),
-                                     _o(pstats, npool) if training else 0, 2 * npool if training else 0,
-                                     _o(gamma, c0), _o(beta, c0), 0, float(eps), 1, mode, _o(mean, c0),
-                                     _o(invstd, c0), _o(rmean, c0), _o(rvar, c0), float(momentum), st)
-            _lib.check(rc, "tony_bn_apply_f32 (head pool)")
+            _apply_f32(L, p.data_ptr(), m, npool, npool, y, slot,
+                       (_lib.ptr(pstats), _o(pstats, npool) if training else 0, 2 * npool if training else 0,
+                        _o(gamma, c0), _o(beta, c0), 0, float(eps), 1, mode, _o(mean, c0), _o(invstd, c0),
+                        _o(rmean, c0), _o(rvar, c0), float(momentum), st))
             outs.append(y)
         ctx.save_for_backward(x3, weight, gamma, beta, z, p, mean, invstd)
         ctx.conf = (cp, tuple(x.shape), tuple(splits), npool, x.requires_grad)
