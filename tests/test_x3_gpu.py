@@ -277,6 +277,48 @@ def test_x3_block_branch_streams_and_joins_match_plain_graph(cuda, block):
     _grads_agree(gw_f, gw_p)
 
 
+@pytest.mark.parametrize("block", ["A", "B", "C", "D", "E"])
+def test_x3_concat_planes_match_split_of_block_output(cuda, block, monkeypatch):
+    """ops/concat.X3_PLANES: a fp32 block output carries its x3 planes, written by the slot producers' BN
+    apply (tony_bn_apply_f32_p3) and, for the max-pool slices, by a slice split -- bit-identical to
+    splitting the finished fp32 concat (what the next block's convs would otherwise do), and the fp32
+    output itself is unchanged (to the run-to-run noise of the atomic BN statistics)."""
+    from tony_amd.models import inception_v3 as I
+    from tony_amd.ops import concat, streams
+    from tony_amd.ops.x3 import ACT, split_rows
+
+    mk = {"A": lambda: I.InceptionA(64, 32, x3=True), "B": lambda: I.InceptionB(64, x3=True),
+          "C": lambda: I.InceptionC(64, 32, x3=True), "D": lambda: I.InceptionD(64, x3=True),
+          "E": lambda: I.InceptionE(64, x3=True)}
+    torch.manual_seed(0)
+    blk = mk[block]().to(DEV).to(memory_format=torch.channels_last).train()
+    x0 = _cl(torch.randn(2, 64, 17, 17, device=DEV))
+    outs = {}
+    for on in (False, True):
+        monkeypatch.setattr(concat, "X3_PLANES", on)
+        torch.manual_seed(1)
+        for m in blk.modules():  # identical BN running stats for both runs
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.reset_running_stats()
+        s = streams.begin(x0.device, branches=True)
+        try:
+            y = blk(x0.clone().requires_grad_(True) * 1.0)
+        finally:
+            if s:
+                streams.end()
+        torch.cuda.synchronize()
+        outs[on] = y
+    y_off, y_on = outs[False], outs[True]
+    assert getattr(y_off, "_tony_x3", None) is None
+    hit = getattr(y_on, "_tony_x3", None)
+    assert hit is not None and hit[0] == y_on._version and hit[2] == y_on.shape[1]
+    assert _rel(y_on.detach(), y_off.detach()) < 1e-5  # (atomic BN statistics: not bit-stable run to run)
+    n, c, h, w = y_on.shape
+    want = split_rows(y_on.detach().permute(0, 2, 3, 1).reshape(-1, c), n * h * w, c, c, ACT)
+    got = hit[1].permute(0, 2, 3, 1).reshape(-1, 3 * c)
+    assert torch.equal(got, want)
+
+
 def test_x3_planes_only_chain_matches_fp32_chain(cuda):
     """conv-BN-ReLU -> conv-BN-ReLU where the first layer hands over only the operand planes (its BN apply
     writes them; no fp32 output, no split pass) gives the same outputs and gradients as the fp32 hand-over."""
