@@ -51,7 +51,8 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=128, help="per-GPU batch (weak scaling)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="per-GPU batch (weak scaling; default 128, mxnet-kv 1024 rows per worker)")
     ap.add_argument("--mode", default="auto", choices=["auto", "graph", "eager"],
                     help="graph: replay the step as one HIP graph; eager: launch kernels from Python (weight "
                          "gradients overlap the data-gradient chain on a second stream); auto: time both in setup")
@@ -90,7 +91,20 @@ def parse(argv=None):
                     help="MIOpen immediate mode instead of find (faster startup, slower non-1x1 convs)")
     ap.add_argument("--launch-dry-run", action="store_true",
                     help="N>1 without torch.distributed.run: print the self-launch argv / env as JSON and exit")
-    return ap.parse_args(argv)
+    ap.add_argument("--config", default="inception-ps",
+                    choices=["inception-ps", "hvd-resnet50", "ddp-mnist", "mxnet-kv"],
+                    help="which BASELINE.json config to measure: the Inception-v3 PS headline (default) or "
+                         "one of the others (tony_amd/bench_configs.py), each one JSON line")
+    ap.add_argument("--kvstore", default="dist_sync", help="mxnet-kv: kvstore type (BASELINE: dist_sync)")
+    ap.add_argument("--kv-device", default="auto", choices=["auto", "cuda", "cpu"],
+                    help="mxnet-kv: where the workers' tensors live (cuda: the GPU payload plane)")
+    ap.add_argument("--kv-role-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-bind", action="store_true",
+                    help="N>1: leave CPU affinity alone (default: each rank on its GPU's NUMA node CPUs)")
+    a = ap.parse_args(argv)
+    if a.batch is None:
+        a.batch = {"mxnet-kv": 1024}.get(a.config, 128)
+    return a
 
 
 def fail(msg: str, code: int = 4) -> int:
@@ -190,6 +204,32 @@ def _heartbeat(t0: float, every_s: float = 45.0) -> None:
     threading.Thread(target=beat, name="bench-heartbeat", daemon=True).start()
 
 
+def bind_rank_cpus():
+    """N>1 under torch.distributed.run: pin this rank (and the threads it starts) to CPUs of its GPU's NUMA
+    node, split among the local ranks that share the node (gpu/inventory.rank_cpus -- the coordinator's slot
+    allocator does the same for launcher tasks).  Runs before any GPU call.  Returns the CPU list (None:
+    one rank, a shared-GPU rehearsal, or no NUMA information)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1 or "TONY_BENCH_DEVICE" in os.environ or not hasattr(os, "sched_setaffinity"):
+        return None
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    lws = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    try:
+        from tony_amd.gpu.inventory import rank_cpus
+
+        vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")
+        kfd = [int(v) for v in vis.split(",") if v.strip()] if vis else list(range(lws))
+        if len(kfd) < lws:
+            return None
+        cpus = rank_cpus(kfd[local], kfd[:lws])
+        if cpus:
+            os.sched_setaffinity(0, cpus)
+        return cpus or None
+    except Exception as e:  # noqa: BLE001 - placement is an optimisation, never a failure
+        print(f"[bench] rank {local}: CPU binding skipped ({e})", file=sys.stderr, flush=True)
+        return None
+
+
 def _free_port() -> int:
     import socket
 
@@ -246,10 +286,19 @@ def self_launch(args, argv) -> int:
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        return self_launch(args, argv)
     if args.collective:
         os.environ["TONY_COLLECTIVE"] = args.collective
+    if args.config == "mxnet-kv":  # scheduler + server + N workers (its own launcher, bench_configs.py)
+        from tony_amd import bench_configs
+
+        return bench_configs.run(args, argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(args, argv)
+    cpus = None if args.no_bind else bind_rank_cpus()  # before any GPU call in this process
+    if args.config != "inception-ps":
+        from tony_amd import bench_configs
+
+        return bench_configs.run(args, argv)
     if int(os.environ.get("RANK", "0")) == 0:
         _heartbeat(time.perf_counter())
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -477,16 +526,27 @@ def main(argv=None):
         "host_fwd_bwd_ms_last_eager_step": [round(1000.0 * trainer.host_fwd_s, 3), round(1000.0 * trainer.host_bwd_s, 3)],
         "conv_impl": _conv_impl_counts(),
     }
-    engines = [eng]
+    # per rank: host issue time per timed step, the setup's eager host time / host-bound verdict, its CPUs
+    mine = {"rank": rank, "host_ms_per_step": eng["host_ms_per_step"],
+            "eager_host_ms": setup.get("eager_host_ms"), "eager_host_bound": setup.get("eager_host_bound"),
+            "cpus": None if cpus is None else f"{len(cpus)} ({cpus[0]}-{cpus[-1]})"}
+    engines, ranks_host = [eng], [mine]
     if world > 1:
         engines = [None] * world
         dist.all_gather_object(engines, eng)
+        ranks_host = [None] * world
+        dist.all_gather_object(ranks_host, mine)
     eng_rank = ps.worker_ranks[0] if ps.worker_ranks else 0
     eng = dict(engines[eng_rank], engine_of_rank=eng_rank)
     fp32_row = None
-    if world == 1 and args.fp32_row and args.dtype == "bf16" and args.model == "inception_v3" and not args.stock:
-        # reference precision under the same clock discipline: the x3 fp32 step in a child process
-        fp32_row = _fp32_row(args)
+    if args.fp32_row and args.dtype == "bf16" and args.model == "inception_v3" and not args.stock:
+        if world == 1:
+            # reference precision under the same clock discipline: the x3 fp32 step in a child process
+            fp32_row = _fp32_row(args)
+        else:
+            # N ranks: the x3 fp32 step in-process after the bf16 timed region, on the same process group
+            # (no child launch: the ranks and their RCCL communicator are already up)
+            fp32_row = _fp32_row_inprocess(args, world, rank, dev)
     if rank == 0:
         imgs = args.batch * n_workers * args.steps
         value = imgs / elapsed
@@ -537,6 +597,10 @@ def main(argv=None):
                 # init-time canaries of the hand data planes against RCCL (None: that plane unused)
                 "data_plane_verified": coll.data_plane_status(),
                 "dist": diag or None,
+                "ranks_host": ranks_host if world > 1 else None,
+                "ps_sync": "synchronous: every step sums all workers' gradients before the apply (TonY's "
+                           "mnist_distributed.py example trains asynchronously; a sync step does at least the same "
+                           "work, and bench.py --ps-mode dedicated / jobs/inception_ps.py --async run the async form)",
                 "final_loss": round(final_loss, 4),
             },
         }
@@ -587,6 +651,63 @@ def _fp32_row(args) -> dict:
     return {"value": r["value"], "unit": r["unit"], "ms_per_step": r["ms_per_step"], "steps": r["steps"],
             "warmup": r["warmup"], "dtype": "fp32", "kernels": c.get("kernels"), "step_mode": c.get("step_mode"),
             "final_loss": c.get("final_loss"), "child_wall_s": round(time.perf_counter() - t, 1)}
+
+
+def _fp32_row_inprocess(args, world: int, rank: int, dev) -> dict:
+    """N > 1: the reference-precision step (x3 fp32 Inception-v3, fp32 variables and pushed gradients,
+    colocated sharded PS) built and timed in this rank after the bf16 run, on the same process group:
+    ``--fp32-warmup`` untimed steps, then ``--fp32-steps`` timed ones bracketed by barrier + synchronize on
+    both sides, the max over ranks.  Eager issue (the x3 step is ~2.3x the bf16 one: far from host-bound)."""
+    from tony_amd.models.inception_v3 import inception_v3
+    from tony_amd.ops import cross_entropy
+    from tony_amd.parallel.collectives import max_over_ranks
+    from tony_amd.parallel.ps import ParameterServer
+    from tony_amd.parallel.trainer import Trainer
+
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+    t_all = time.perf_counter()
+    try:
+        model = inception_v3(fused=False, seed=0, precision="fp32").to(dev).to(memory_format=torch.channels_last)
+        model.train()
+        ps = ParameterServer(model, optimizer=args.optimizer, lr=0.045, momentum=0.9, weight_decay=4e-5,
+                             mode="colocated", ps_ranks=(0,), dtype=torch.float32, device=dev,
+                             wire_dtype=torch.float32)
+
+        def loss_fn(out, y):
+            logits, aux = out
+            return cross_entropy(logits, y) + 0.4 * cross_entropy(aux, y)
+
+        trainer = Trainer(model, ps, loss_fn, use_graph=False, overlap_wgrad=not args.no_wgrad_stream,
+                          branch_streams=not args.no_branch_streams, overlap_comm=not args.no_overlap)
+        g = torch.Generator(device=dev).manual_seed(4321 + rank)
+        x = torch.randn((args.batch, 3, 299, 299), generator=g, device=dev).contiguous(memory_format=torch.channels_last)
+        y = torch.randint(0, 1000, (args.batch,), generator=g, device=dev)
+        loss = None
+        for _ in range(max(1, args.fp32_warmup)):
+            loss = trainer.step(x, y)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.fp32_steps):
+            loss = trainer.step(x, y)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        el = max_over_ranks(time.perf_counter() - t0, device=dev)
+        fin = max_over_ranks(float(loss.float().item()), device=dev)
+        if ps.plane is not None:
+            ps.plane.close()
+    except Exception as e:  # noqa: BLE001 - reported in the record, the bf16 headline stands
+        return {"error": f"in-process fp32 step failed on rank {rank}: {type(e).__name__}: {e}"}
+    n_workers = len(ps.worker_ranks)
+    return {"value": round(args.batch * n_workers * args.fp32_steps / el, 2), "unit": "images/sec",
+            "ms_per_step": round(1000.0 * el / args.fp32_steps, 3), "steps": args.fp32_steps,
+            "warmup": max(1, args.fp32_warmup), "dtype": "fp32", "n_gpus": world,
+            "kernels": "tony_amd HIP, fp32 via x3-split bf16 MFMA products (ops/x3.py)", "step_mode": "eager",
+            "parallelism": f"ps-colocated-sharded dp{world} (sync), fp32 variables and gradients",
+            "final_loss": round(fin, 4), "timed_in": "same ranks, after the bf16 run",
+            "wall_s": round(time.perf_counter() - t_all, 1)}
 
 
 def _branch_streams_on(args) -> bool:

@@ -68,3 +68,62 @@ def test_no_relaunch_under_an_outside_launcher(world):
     assert p.returncode == 2
     assert "self_launch" not in p.stdout
     assert "WORLD_SIZE" in p.stderr
+
+
+# -- the other BASELINE configs (bench.py --config, tony_amd/bench_configs.py) -----------------------------
+def _last_json(stdout: str) -> dict:
+    return json.loads([ln for ln in stdout.splitlines() if ln.startswith("{")][-1])
+
+
+def test_config_ddp_mnist_two_ranks_gloo():
+    """ddp-mnist through the self-launch (2 ranks, gloo, CPU): one JSON line with the whole-job rate."""
+    p = subprocess.run([sys.executable, BENCH, "--config", "ddp-mnist", "--gpus", "2", "--steps", "3", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300,
+                       env=_env(TONY_BENCH_DEVICE="0", TONY_BENCH_BACKEND="gloo", CUDA_VISIBLE_DEVICES=""))
+    assert p.returncode == 0, p.stderr[-3000:]
+    rec = _last_json(p.stdout)
+    assert rec["metric"].startswith("samples/sec") and rec["n_gpus"] == 2 and rec["steps"] == 3
+    assert rec["config"]["global_batch"] == 256 and rec["value"] > 0 and rec["higher_is_better"]
+
+
+def test_config_mxnet_kv_dist_sync_launch():
+    """mxnet-kv: scheduler + 1 server + 2 workers as processes with the DMLC_* contract, dist_sync."""
+    p = subprocess.run([sys.executable, BENCH, "--config", "mxnet-kv", "--gpus", "2", "--steps", "4", "--warmup", "1",
+                        "--kv-device", "cpu"], capture_output=True, text=True, timeout=300, env=_env())
+    assert p.returncode == 0, p.stderr[-3000:]
+    rec = _last_json(p.stdout)
+    assert rec["config"]["kvstore"] == "dist_sync" and rec["n_gpus"] == 2
+    assert rec["config"]["global_batch"] == 2048 and rec["value"] > 0
+
+
+def test_config_dry_runs():
+    p = subprocess.run([sys.executable, BENCH, "--config", "hvd-resnet50", "--gpus", "8", "--launch-dry-run"],
+                       capture_output=True, text=True, timeout=120, env=_env())
+    assert p.returncode == 0, p.stderr
+    cmd = json.loads(p.stdout.strip().splitlines()[-1])["self_launch"]
+    assert "--nproc-per-node=8" in cmd and cmd[cmd.index(BENCH) + 1:] == ["--config", "hvd-resnet50", "--gpus", "8"]
+    p = subprocess.run([sys.executable, BENCH, "--config", "mxnet-kv", "--gpus", "8", "--launch-dry-run"],
+                       capture_output=True, text=True, timeout=120, env=_env())
+    roles = json.loads(p.stdout.strip().splitlines()[-1])["mxnet_kv_launch"]
+    assert [r[0] for r in roles] == ["scheduler", "server"] + ["worker"] * 8
+    assert all(r[2]["DMLC_NUM_WORKER"] == "8" and r[2]["DMLC_NUM_SERVER"] == "1" for r in roles)
+
+
+def test_rank_cpu_affinity_choice():
+    """Verdict r5 #5: each rank of an N-GPU bench runs on its GPU's NUMA node, the node's CPUs split among
+    the ranks that share it (fake inventory: 8 GPUs, 2 nodes of 64 CPUs)."""
+    from tony_amd.gpu.inventory import rank_cpus
+    from tony_amd.native import GpuDevice
+
+    devs = [GpuDevice(i, bdf=f"fake:{i:02x}", numa_node=i // 4, fake=True) for i in range(8)]
+    node = {0: list(range(0, 64)), 1: list(range(64, 128))}
+    got = [rank_cpus(o, list(range(8)), devs, cpus_of_node=node.get, allowed=list(range(128))) for o in range(8)]
+    assert got[0] == list(range(0, 16)) and got[3] == list(range(48, 64)) and got[4] == list(range(64, 80))
+    assert sorted(c for g in got for c in g) == list(range(128))  # disjoint, every CPU used once
+    # 2 ranks on GPUs 0 and 5: each gets its whole node; a restricted allowed set is respected
+    assert rank_cpus(5, [0, 5], devs, cpus_of_node=node.get, allowed=list(range(128))) == list(range(64, 128))
+    assert rank_cpus(0, [0, 1], devs, cpus_of_node=node.get, allowed=list(range(8))) == [0, 1, 2, 3]
+    # nothing known: leave affinity alone
+    unk = [GpuDevice(0, bdf="fake:00", numa_node=-1, fake=True)]
+    assert rank_cpus(0, [0], unk, cpus_of_node=node.get, allowed=list(range(8))) == []
+    assert rank_cpus(0, [0], devs, cpus_of_node=node.get, allowed=[100]) == []

@@ -714,8 +714,21 @@ def test_visible_mode_auto_isolates_unless_a_peer_plane_is_configured():
     # an ordinary user TF PS job keeps its isolation (the ps-plane key's xgmi default alone
     # does not count); tony_amd's own PS program, or an explicit xgmi plane, maps peer GPUs
     assert resolve_visible_mode(conf(tony__ps__instances=1, tony__worker__instances=4)) == "hip"
+    # only tony_amd's exact entry points count -- a user script named inception_ps.py, or one under a
+    # path containing "tony_amd", keeps its isolation; the same name shipped from tony_amd/jobs (the client
+    # marks that --src_dir) or named as a module / an installed path maps peer GPUs
     assert resolve_visible_mode(conf(tony__ps__instances=1, tony__worker__instances=4,
-                                     tony__containers__command="python3 inception_ps.py --batch-size 32")) == "none"
+                                     tony__containers__command="python3 inception_ps.py --batch-size 32")) == "hip"
+    assert resolve_visible_mode(conf(tony__ps__instances=1, tony__worker__instances=4,
+                                     tony__containers__command="python3 /home/u/tony_amd_fork/train.py")) == "hip"
+    assert resolve_visible_mode(conf(tony__ps__instances=1, tony__worker__instances=4,
+                                     tony__containers__command="python3 inception_ps.py --batch-size 32",
+                                     **{"tony__amd__src-is-tony-jobs": "true"})) == "none"
+    assert resolve_visible_mode(conf(tony__ps__instances=1, tony__worker__instances=4,
+                                     tony__containers__command="python3 -m tony_amd.jobs.inception_ps")) == "none"
+    import tony_amd.jobs.inception_ps as ips
+    assert resolve_visible_mode(conf(tony__ps__instances=1, tony__worker__instances=4,
+                                     tony__containers__command=f"python3 {ips.__file__} --steps 3")) == "none"
     assert resolve_visible_mode(conf(tony__ps__instances=1, **{"tony__amd__ps-plane": "xgmi"})) == "none"
     assert resolve_visible_mode(conf(tony__ps__instances=1, **{"tony__amd__ps-plane": "rccl"})) == "hip"
     # the decision survives the round trip through tony-final.xml (sources are written and re-read)

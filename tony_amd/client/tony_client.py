@@ -296,6 +296,9 @@ class TonyClient:
         if self.src_dir:
             zip_path = os.path.join(self.job_dir, U.tony_src_zip_name(self.app_id))
             U.zip_folder(self.src_dir, zip_path)
+            jobs = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "jobs")
+            if os.path.realpath(self.src_dir) == os.path.realpath(jobs):
+                c.set(K.AMD_SRC_IS_TONY_JOBS, "true")
         if self.python_venv:
             shutil.copy2(self.python_venv, os.path.join(self.job_dir, C.PYTHON_VENV_ZIP))
         self.process_tony_conf_resources(c)

@@ -67,11 +67,38 @@ def _default_history_root(conf, staging_root: str) -> str:
     return loc
 
 
+_TONY_JOBS_DIR = os.path.realpath(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "jobs"))
+
+
+def _is_tony_amd_program(cmd: str) -> bool:
+    """One of tony_amd's own training programs, named exactly: ``-m tony_amd.jobs.<name>``, or a script
+    path that resolves into the installed tony_amd/jobs directory.  A user script that merely shares a
+    file name (``python inception_ps.py``) or lives under a path containing "tony_amd" does not count."""
+    import shlex
+
+    try:
+        toks = shlex.split(cmd)
+    except ValueError:
+        toks = cmd.split()
+    for i, t in enumerate(toks):
+        if t == "-m" and i + 1 < len(toks) and toks[i + 1].startswith("tony_amd.jobs."):
+            return True
+        if t.endswith(".py") and os.path.isabs(t) and os.path.dirname(os.path.realpath(t)) == _TONY_JOBS_DIR:
+            return True
+    return False
+
+
 def _runs_tony_amd_job(conf) -> bool:
-    """Whether the job's task command is one of tony_amd's own training programs (tony_amd/jobs),
-    which bring up the tony_amd data planes themselves."""
+    """Whether the job's task command is one of tony_amd's own training programs (tony_amd/jobs), which
+    bring up the tony_amd data planes themselves: an exact entry point, or a relative script shipped from
+    tony_amd/jobs itself (the client marks a --src_dir that is that directory)."""
     cmds = [conf.get(K.CONTAINERS_COMMAND) or ""] + [v for k, v in conf.get_val_by_regex(r"^tony\.[a-z]+\.command$").items()]
-    return any("tony_amd" in c or "inception_ps" in c for c in cmds)
+    if any(_is_tony_amd_program(c) for c in cmds):
+        return True
+    if conf.get_bool(K.AMD_SRC_IS_TONY_JOBS, False):
+        names = {f for f in os.listdir(_TONY_JOBS_DIR) if f.endswith(".py")} if os.path.isdir(_TONY_JOBS_DIR) else set()
+        return any(os.path.basename(t) in names for c in cmds for t in c.split() if t.endswith(".py"))
+    return False
 
 
 def resolve_visible_mode(conf) -> str:

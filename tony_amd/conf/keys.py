@@ -125,6 +125,9 @@ AMD_PROFILE_JOBTYPES = AMD + "profile.jobtypes"
 AMD_GPU_TASK_MEMORY = AMD + "gpu-task-memory-per-gpu"    # memory of a GPU task left at the 2g default
 AMD_MEMORY_ENFORCED = AMD + "memory-enforced"              # stop tasks whose RSS exceeds tony.<job>.memory
 AMD_GPU_FAULT_STOPS_TASK = AMD + "gpu-fault-stops-task"    # new uncorrectable ECC errors stop the task
+# set by the client when --src_dir is tony_amd's own job directory (tony_amd/jobs): the task commands then
+# run tony_amd's training programs, which bring up its peer-mapping data planes (coordinator auto mode)
+AMD_SRC_IS_TONY_JOBS = AMD + "src-is-tony-jobs"
 
 # multi-value keys are appended (not overridden) by --conf (TonyConfigurationKeys.java:307-308)
 MULTI_VALUE_CONF = (CONTAINER_LAUNCH_ENV, EXECUTION_ENV, CONTAINERS_RESOURCES)

@@ -177,6 +177,38 @@ def discover(fake_gpus: int = -1) -> List[GpuDevice]:
     return devs
 
 
+def rank_cpus(hip_ordinal: int, local_ranks_ordinals: List[int], devices: Optional[List[GpuDevice]] = None,
+              cpus_of_node=None, allowed: Optional[List[int]] = None) -> List[int]:
+    """CPUs for the rank driving HIP device ``hip_ordinal`` when one process per GPU runs on this node
+    (bench.py --gpus N, torchrun): the CPUs of that GPU's NUMA node that this process may use, split evenly
+    among the local ranks whose GPUs share the node (``local_ranks_ordinals``: every local rank's HIP
+    ordinal, in local-rank order), so ranks do not contend for one core and each issues its kernels from
+    CPUs next to its GPU -- what the coordinator's slot allocator does for launcher tasks
+    (GpuAllocator._take_cpus; TaskExecutor.java:189-238 owns placement per task in the reference).
+    ``devices``: the GPUs in HIP-ordinal order (default: the KFD topology).  Empty when nothing is known
+    (no NUMA information, or none of the node's CPUs allowed): the caller then leaves affinity alone."""
+    devs = devices if devices is not None else _kfd_devices()
+    cpus_of_node = cpus_of_node or numa_cpus
+    if hip_ordinal < 0 or hip_ordinal >= len(devs):
+        return []
+    node = devs[hip_ordinal].numa_node
+    if node is None or node < 0:
+        return []
+    ok = set(allowed if allowed is not None else (os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity")
+                                                    else []))
+    cpus = [c for c in cpus_of_node(node) if not ok or c in ok]
+    if not cpus:
+        return []
+    peers = [o for o in local_ranks_ordinals if 0 <= o < len(devs) and devs[o].numa_node == node]
+    if hip_ordinal not in peers or len(peers) <= 1:
+        return cpus
+    k, n = peers.index(hip_ordinal), len(peers)
+    share = len(cpus) // n
+    if share < 1:
+        return cpus
+    return cpus[k * share:(k + 1) * share]
+
+
 @dataclass
 class Slot:
     gpus: List[int]

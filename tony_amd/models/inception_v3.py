@@ -101,10 +101,11 @@ class _Block(nn.Module):
         super().__init__()
         self.fused = fused and not x3
         self.x3 = x3
-        # the fp32 blocks' fast form (concat slots, branch streams, joins); TONY_X3_BLOCKS=0: torch.cat graph
-        self.x3_fast = x3 and (X3_BLOCKS or X3_HEADS)
+        # the fp32 blocks' fast form (concat slots, branch streams, joins); TONY_X3_BLOCKS=0: the torch.cat
+        # graph whatever TONY_X3_HEADS says (the fused heads live in the fast form only)
+        self.x3_fast = x3 and X3_BLOCKS
         # the fused-head layout (ops/fused.py FusedHead, models/convert.py): the bf16 model and the fp32 one
-        self.heads = self.fused or (x3 and X3_HEADS)
+        self.heads = self.fused or (self.x3_fast and X3_HEADS)
 
     def avgpool(self, x, planes_only=False):
         """``planes_only``: the x3 pool branch, read by its 1x1 conv only (ops/pool.avg_pool3x3_s1)."""

@@ -191,7 +191,7 @@ _SIGNATURES = {
     "tony_plan_destroy": [c_void_p],
     # parameter-server data plane over xGMI windows (csrc/ps_plane.hip, parallel/ps_plane.py)
     "tony_ps_header_bytes": [],
-    "tony_kv_copy": [c_void_p, c_void_p, c_int64, c_void_p],
+    "tony_kv_copy": [c_void_p, c_void_p, c_int64, c_void_p, c_void_p],
     "tony_ps_max_buckets": [],
     "tony_ps_max_blocks": [],
     "tony_ps_land_entry_bytes": [],

@@ -174,6 +174,7 @@ inline bool glds_uni_enabled() {
 struct GldsVariant {
   int bm, cap, stages, kb, nwm;  // nwm: waves along M (workgroup = 2 x nwm waves)
   bool il = false;               // interleaved DMA issue (conv_glds_kernel IL; UNI shapes only)
+  bool pf = false;               // fragment prefetch (conv_glds_kernel PF)
 };
 // 11-15: 4-wave 64/128-row tiles at 2-3 workgroups per CU; 16-19: 8-wave 256-row tiles at one (16-18)
 // or two (19) workgroups per CU -- each B (weight) tile is shared by 256 rows, so the LDS-DMA intake
@@ -184,7 +185,12 @@ constexpr GldsVariant kGldsVariants[] = {
     {256, 192, 4, 32, 4}, {256, 128, 3, 64, 4}, {256, 192, 5, 32, 4}, {256, 128, 3, 32, 4},
     // 20-24: the interleaved-issue forms of the most-picked tiles (11-19 above)
     {128, 128, 3, 32, 2, true}, {128, 192, 3, 32, 2, true}, {128, 128, 2, 64, 2, true},
-    {256, 192, 4, 32, 4, true}, {256, 128, 3, 32, 4, true}};
+    {256, 192, 4, 32, 4, true}, {256, 128, 3, 32, 4, true},
+    // 25-31: the fragment-prefetch forms (PF: step k+1's fragments read while step k's MFMAs issue, every
+    // ring slot in flight)
+    {256, 192, 4, 32, 4, false, true}, {256, 128, 3, 32, 4, false, true}, {128, 128, 3, 32, 2, false, true},
+    {128, 192, 3, 32, 2, false, true}, {128, 128, 2, 64, 2, false, true}, {64, 128, 4, 32, 2, false, true},
+    {256, 192, 2, 64, 4, false, true}};
 // (measured and dropped in round 5: the 256 x 192 tile on a two-slot ring of 64-deep stages, half the
 // barriers per K -- plain 0.93-0.97x of variant 23, interleaved 0.6x; profiles/r5_conv_limits.md)
 constexpr int kNumGlds = sizeof(kGldsVariants) / sizeof(kGldsVariants[0]);
@@ -218,7 +224,13 @@ __device__ __forceinline__ int goff(int row, int ch) {
 // current stage (after its fragments are read) instead of all at once right after the barrier -- a
 // global_load_lds costs the issuing wave ~60-185 cycles of issue, which then overlaps the matrix pipe
 // working off the MFMAs already issued (MI355X_MICROARCH.md, LDS-DMA piece issue cost).
-template <int BM, int BN, int ST, int KB, bool UNI, int NWM = 2, bool IL = false, bool X3 = false, bool AT = false>
+// PF: the fragments of K-substep k+1 are read from LDS into a second register set while substep k's MFMAs
+// issue, so no MFMA waits on a ds_read issued after the barrier (profiles/r5_conv_limits.md: the read ->
+// MFMA dependency at the head of every step held the plain loop at ~2x the MFMA + DMA issue floor).  A
+// stage's slot is refilled right after the barrier that follows its last fragment read (every wave then
+// holds those fragments in registers), so all ST slots carry DMAs: one stage more in flight per ring.
+template <int BM, int BN, int ST, int KB, bool UNI, int NWM = 2, bool IL = false, bool X3 = false, bool AT = false,
+          bool PF = false>
 __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const uint16_t* __restrict__ B, int64_t ldb,
                                                              uint16_t* __restrict__ C, int64_t ldc, int M, int N,
                                                              float* __restrict__ stats, int64_t sstride, int epi,
@@ -237,6 +249,7 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
   static_assert(BM % RPI == 0 && BN % RPI == 0 && BN % 32 == 0 && ST >= 2 && (KB == 32 || KB == 64), "tile shape");
   static_assert(!X3 || (UNI && !IL), "the fused x3 planes run the plain uniform-tap loop");
   static_assert(!AT || (UNI && !IL && !X3), "the A transform runs in the plain uniform-tap loop");
+  static_assert(!PF || (!IL && !X3 && !AT), "the fragment prefetch runs the plain loop");
   static_assert(BM * (BN + 8) <= ST * STAGE, "the epilogue's C tile fits in the ring");
   __shared__ __attribute__((aligned(16))) uint16_t smem[ST * STAGE];
 
@@ -471,6 +484,65 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  if constexpr (PF) {
+    bf16x8_t fa[2][TM], fb[2][TN];
+    // fragments of substep kk of the stage at As into register set BUF
+    auto rd = [&](auto bufc, const uint16_t* As, int kk) {
+      constexpr int BUF = decltype(bufc)::value;
+      const uint16_t* Bs = As + BM * KB;
+      const int ch = kk * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[BUF][i] = *reinterpret_cast<const bf16x8_t*>(As + goff<KB>(wm * WM + i * 16 + (lane & 15), ch));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[BUF][j] = *reinterpret_cast<const bf16x8_t*>(Bs + goff<KB>(wn * WN + j * 16 + (lane & 15), ch));
+    };
+    auto mm = [&](auto bufc) {
+      constexpr int BUF = decltype(bufc)::value;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[BUF][i], fb[BUF][j], acc[i][j], 0, 0, 0);
+    };
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+#pragma unroll
+    for (int s = 0; s < ST; ++s) issue(s);
+    glds_wait_barrier<(ST - 1) * NDMA>();
+    int slot = 0;
+    rd(B0{}, smem, 0);
+    // stage kt + 1 starts: every wave holds stage kt's last fragments (lgkmcnt) and stage kt + 1 has
+    // landed in every wave (vmcnt: the ST - 2 younger stages may fly); stage kt + ST goes into kt's slot
+    auto boundary = [&]() -> const uint16_t* {
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((ST - 2) * NDMA) : "memory");
+      issue(slot);
+      slot = slot + 1 == ST ? 0 : slot + 1;
+      return smem + slot * STAGE;
+    };
+    if constexpr (KSUB == 1) {
+      int kt = 0;
+      for (; kt + 2 <= nk; kt += 2) {
+        rd(B1{}, boundary(), 0);
+        mm(B0{});
+        rd(B0{}, boundary(), 0);
+        mm(B1{});
+      }
+      if (kt < nk) {
+        rd(B1{}, boundary(), 0);
+        mm(B0{});
+      }
+    } else {
+      static_assert(KSUB == 2, "64-deep stages: two substeps");
+      for (int kt = 0; kt < nk; ++kt) {
+        rd(B1{}, smem + slot * STAGE, 1);
+        mm(B0{});
+        rd(B0{}, boundary(), 0);
+        mm(B1{});
+      }
+    }
+  } else {
 #pragma unroll
   for (int s = 0; s < ST - 1; ++s) issue(s);
   int slot = 0;
@@ -597,6 +669,7 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     slot = slot + 1 == ST ? 0 : slot + 1;
+  }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's zero fills land before LDS is reused
   __syncthreads();
@@ -734,13 +807,13 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
                             : kGldsVariants[v - kGldsFirst];
   const int64_t bn = pick_bn(N, gv.cap);
   using std::integral_constant;
-  const auto launch = [&](auto bm, auto bnc, auto st_, auto kb, auto nwm, auto il, auto x3c) -> int {
+  const auto launch = [&](auto bm, auto bnc, auto st_, auto kb, auto nwm, auto il, auto x3c, auto pfc) -> int {
     constexpr int BM = decltype(bm)::value, BN = decltype(bnc)::value, ST = decltype(st_)::value;
     constexpr int KB = decltype(kb)::value, NWM = decltype(nwm)::value;
-    constexpr bool IL = decltype(il)::value, X3 = decltype(x3c)::value;
+    constexpr bool IL = decltype(il)::value, X3 = decltype(x3c)::value, PF = decltype(pfc)::value;
     constexpr int PL = X3 ? 2 : 1;
     if constexpr (BN % (64 / (KB / 8)) != 0 || BM * (BN + 8) > ST * PL * (BM + BN) * KB ||
-                  ST * PL * (BM + BN) * KB * 2 > 163840 || (X3 && IL)) {
+                  ST * PL * (BM + BN) * KB * 2 > 163840 || (X3 && IL) || (PF && (X3 || IL))) {
       return -3;
     } else {
       const int tiles_n = ceil_div(N, BN);
@@ -783,7 +856,7 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
                                         static_cast<int>(M), static_cast<int>(N), st, sstride, epi, tiles_n, rmap, bt,
                                         sk, xp, mc);
       if (xp.atab != nullptr) {  // the BN-apply-on-load prototype: one tile family
-        if constexpr (!X3 && !IL && BM == 128 && ST == 3 && KB == 32 && NWM == 2 && BN <= 128) {
+        if constexpr (!X3 && !IL && !PF && BM == 128 && ST == 3 && KB == 32 && NWM == 2 && BN <= 128) {
           if (g.Cs % KB != 0 || g.R != 1 || g.S != 1) return -3;
           std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true, NWM, false, false, true><<<grid, 128 * NWM, 0, stream>>>(a...); }, args);
           TONY_LAUNCH_CHECK();
@@ -796,28 +869,28 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
         if (g.Cs % KB != 0) return -3;  // the fused planes run the uniform-tap loop only
         std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true, NWM, false, true><<<grid, 128 * NWM, 0, stream>>>(a...); }, args);
       } else if (g.Cs % KB == 0 && glds_uni_enabled()) {
-        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true, NWM, IL><<<grid, 128 * NWM, 0, stream>>>(a...); }, args);
+        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true, NWM, IL, false, false, PF><<<grid, 128 * NWM, 0, stream>>>(a...); }, args);
       } else if (IL || bt.S != 0) {
         return -3;  // the interleaved form and the class taps exist for the uniform-tap loop only
       } else {
-        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, false, NWM><<<grid, 128 * NWM, 0, stream>>>(a...); }, args);
+        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, false, NWM, false, false, false, PF><<<grid, 128 * NWM, 0, stream>>>(a...); }, args);
       }
       TONY_LAUNCH_CHECK();
       return 0;
     }
   };
-  const auto by_bn = [&](auto bm, auto st_, auto kb, auto cap, auto nwm, auto il, auto x3c) -> int {
+  const auto by_bn = [&](auto bm, auto st_, auto kb, auto cap, auto nwm, auto il, auto x3c, auto pfc) -> int {
     constexpr int CAP = decltype(cap)::value;
     switch (bn) {
-      case 32: return launch(bm, integral_constant<int, 32>{}, st_, kb, nwm, il, x3c);
-      case 64: return launch(bm, integral_constant<int, 64>{}, st_, kb, nwm, il, x3c);
-      case 96: return launch(bm, integral_constant<int, 96>{}, st_, kb, nwm, il, x3c);
-      case 128: return launch(bm, integral_constant<int, 128>{}, st_, kb, nwm, il, x3c);
+      case 32: return launch(bm, integral_constant<int, 32>{}, st_, kb, nwm, il, x3c, pfc);
+      case 64: return launch(bm, integral_constant<int, 64>{}, st_, kb, nwm, il, x3c, pfc);
+      case 96: return launch(bm, integral_constant<int, 96>{}, st_, kb, nwm, il, x3c, pfc);
+      case 128: return launch(bm, integral_constant<int, 128>{}, st_, kb, nwm, il, x3c, pfc);
       case 160:
-        if constexpr (CAP >= 160) return launch(bm, integral_constant<int, 160>{}, st_, kb, nwm, il, x3c);
+        if constexpr (CAP >= 160) return launch(bm, integral_constant<int, 160>{}, st_, kb, nwm, il, x3c, pfc);
         break;
       case 192:
-        if constexpr (CAP >= 192) return launch(bm, integral_constant<int, 192>{}, st_, kb, nwm, il, x3c);
+        if constexpr (CAP >= 192) return launch(bm, integral_constant<int, 192>{}, st_, kb, nwm, il, x3c, pfc);
         break;
       default: break;
     }
@@ -838,33 +911,41 @@ inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_
   using W4 = integral_constant<int, 4>;
   using NO = std::false_type;
   using ILV = std::true_type;
+  using PFV = std::true_type;
   if constexpr (XF) {
     using X = std::true_type;
     switch (v - kX3First) {
-      case 0: return by_bn(M256{}, I2{}, K32{}, C128{}, W4{}, NO{}, X{});
-      case 1: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{}, NO{}, X{});
-      case 2: return by_bn(M128{}, I4{}, K32{}, C128{}, W2{}, NO{}, X{});
-      case 3: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, NO{}, X{});
-      case 4: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, NO{}, X{});
-      case 5: return by_bn(M64{}, I4{}, K32{}, C128{}, W2{}, NO{}, X{});
+      case 0: return by_bn(M256{}, I2{}, K32{}, C128{}, W4{}, NO{}, X{}, NO{});
+      case 1: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{}, NO{}, X{}, NO{});
+      case 2: return by_bn(M128{}, I4{}, K32{}, C128{}, W2{}, NO{}, X{}, NO{});
+      case 3: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, NO{}, X{}, NO{});
+      case 4: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, NO{}, X{}, NO{});
+      case 5: return by_bn(M64{}, I4{}, K32{}, C128{}, W2{}, NO{}, X{}, NO{});
       default: return -3;
     }
   } else {
   switch (v - kGldsFirst) {
-    case 0: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, NO{}, NO{});
-    case 1: return by_bn(M128{}, I3{}, K32{}, C128{}, W2{}, NO{}, NO{});
-    case 2: return by_bn(M128{}, I4{}, K32{}, C128{}, W2{}, NO{}, NO{});
-    case 3: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{}, NO{}, NO{});
-    case 4: return by_bn(M64{}, I4{}, K32{}, C128{}, W2{}, NO{}, NO{});
-    case 5: return by_bn(M256{}, I4{}, K32{}, C192{}, W4{}, NO{}, NO{});
-    case 6: return by_bn(M256{}, I3{}, K64{}, C128{}, W4{}, NO{}, NO{});
-    case 7: return by_bn(M256{}, I5{}, K32{}, C192{}, W4{}, NO{}, NO{});
-    case 8: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, NO{}, NO{});
-    case 9: return by_bn(M128{}, I3{}, K32{}, C128{}, W2{}, ILV{}, NO{});
-    case 10: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{}, ILV{}, NO{});
-    case 11: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, ILV{}, NO{});
-    case 12: return by_bn(M256{}, I4{}, K32{}, C192{}, W4{}, ILV{}, NO{});
-    case 13: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, ILV{}, NO{});
+    case 0: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, NO{}, NO{}, NO{});
+    case 1: return by_bn(M128{}, I3{}, K32{}, C128{}, W2{}, NO{}, NO{}, NO{});
+    case 2: return by_bn(M128{}, I4{}, K32{}, C128{}, W2{}, NO{}, NO{}, NO{});
+    case 3: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{}, NO{}, NO{}, NO{});
+    case 4: return by_bn(M64{}, I4{}, K32{}, C128{}, W2{}, NO{}, NO{}, NO{});
+    case 5: return by_bn(M256{}, I4{}, K32{}, C192{}, W4{}, NO{}, NO{}, NO{});
+    case 6: return by_bn(M256{}, I3{}, K64{}, C128{}, W4{}, NO{}, NO{}, NO{});
+    case 7: return by_bn(M256{}, I5{}, K32{}, C192{}, W4{}, NO{}, NO{}, NO{});
+    case 8: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, NO{}, NO{}, NO{});
+    case 9: return by_bn(M128{}, I3{}, K32{}, C128{}, W2{}, ILV{}, NO{}, NO{});
+    case 10: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{}, ILV{}, NO{}, NO{});
+    case 11: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, ILV{}, NO{}, NO{});
+    case 12: return by_bn(M256{}, I4{}, K32{}, C192{}, W4{}, ILV{}, NO{}, NO{});
+    case 13: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, ILV{}, NO{}, NO{});
+    case 14: return by_bn(M256{}, I4{}, K32{}, C192{}, W4{}, NO{}, NO{}, PFV{});
+    case 15: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, NO{}, NO{}, PFV{});
+    case 16: return by_bn(M128{}, I3{}, K32{}, C128{}, W2{}, NO{}, NO{}, PFV{});
+    case 17: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{}, NO{}, NO{}, PFV{});
+    case 18: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, NO{}, NO{}, PFV{});
+    case 19: return by_bn(M64{}, I4{}, K32{}, C128{}, W2{}, NO{}, NO{}, PFV{});
+    case 20: return by_bn(M256{}, I2{}, K64{}, C192{}, W4{}, NO{}, NO{}, PFV{});
     default: return -3;
   }
   }

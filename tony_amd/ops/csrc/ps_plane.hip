@@ -109,7 +109,9 @@ __device__ __forceinline__ void publish(uint32_t* flag, uint32_t value) {
 // Poll *flag until it reaches value or the wall-clock budget runs out (then record the error).
 __device__ __forceinline__ bool wait_flag(const uint32_t* flag, uint32_t value, uint64_t t0, uint64_t budget,
                                           int* err) {
-  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < value) {
+  // wrap-safe: the counters are cumulative for the life of a job (a kvstore key of >= 4 MiB adds 1024 per
+  // copy, so a u32 wraps after ~4.2M copies); the signed difference orders them while they are < 2^31 apart
+  while (static_cast<int32_t>(__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - value) < 0) {
     if (wall_clock64() - t0 > budget) {
       __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return false;
@@ -311,8 +313,11 @@ uint64_t budget_ticks(double seconds) {
 
 // The kvstore payload plane (parallel/kvstore.py): one key's bytes between a local tensor and a peer's
 // IPC-mapped window (either side may be the peer), 16 B per lane, the < 16 B tail by lane 0 of block 0.
+// err (nullable): the error word of the window a preceding kv_wait guarded -- a timed-out wait poisons
+// the copy behind it (stale or partial bytes are never moved; the host raises at its next check)
 __global__ __launch_bounds__(256) void kv_copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                       int64_t bytes) {
+                                                       int64_t bytes, const int* err) {
+  if (err != nullptr && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return;
   const int64_t n16 = bytes >> 4;
   const uint4* s = reinterpret_cast<const uint4*>(src);
   uint4* d = reinterpret_cast<uint4*>(dst);
@@ -382,15 +387,18 @@ TONY_API int tony_kv_wait(const void* flag, uint32_t target, void* window, doubl
   return 0;
 }
 
-// dst <- src (bytes), both 16-B aligned device addresses (local memory or a mapped peer window)
-TONY_API int tony_kv_copy(void* dst, const void* src, int64_t bytes, hipStream_t stream) {
+// dst <- src (bytes), both 16-B aligned device addresses (local memory or a mapped peer window); window
+// (nullable): skip the copy when that window's error word is set (a timed-out wait ahead of it)
+TONY_API int tony_kv_copy(void* dst, const void* src, int64_t bytes, void* window, hipStream_t stream) {
   if (dst == nullptr || src == nullptr || bytes < 0 || (reinterpret_cast<uintptr_t>(dst) & 15) ||
       (reinterpret_cast<uintptr_t>(src) & 15))
     return -1;
   if (bytes == 0) return 0;
   const int64_t n16 = (bytes >> 4) + 1;
   const int blocks = static_cast<int>(std::min<int64_t>(1024, (n16 + 255) / 256));
-  kv_copy_kernel<<<blocks, 256, 0, stream>>>(static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), bytes);
+  kv_copy_kernel<<<blocks, 256, 0, stream>>>(
+      static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), bytes,
+      window == nullptr ? nullptr : reinterpret_cast<const int*>(static_cast<const uint8_t*>(window) + kErrOff));
   TONY_LAUNCH_CHECK();
   return 0;
 }

@@ -96,8 +96,14 @@ def init_process_group(rank: int, world: int, store: Optional[dist.Store] = None
 
 
 def init_from_env(backend: Optional[str] = None):
-    """Initialise from whichever contract is present.  Returns (rank, world, local_rank, device)."""
+    """Initialise from whichever contract is present.  Returns (rank, world, local_rank, device).  A process
+    group that already exists (e.g. torch.distributed.run's env:// rendezvous) is used as it is."""
     env = os.environ
+    if dist.is_initialized():
+        rank, world = dist.get_rank(), dist.get_world_size()
+        local = int(env.get("LOCAL_RANK", env.get("HOROVOD_LOCAL_RANK", rank)))
+        dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else pick_device(local)
+        return rank, world, local, dev
     if "HOROVOD_RANK" in env:
         rank, world = int(env["HOROVOD_RANK"]), int(env["HOROVOD_SIZE"])
         local = int(env.get("HOROVOD_LOCAL_RANK", rank))

@@ -24,6 +24,11 @@ _XGMI = [None]
 _FALLBACKS = [0]
 
 
+def use_hip() -> bool:
+    """TONY_COLLECTIVE asks for tony_amd's xGMI peer-memory kernels instead of RCCL."""
+    return os.environ.get("TONY_COLLECTIVE", "rccl").lower() in ("hip", "xgmi")
+
+
 def fallback_count() -> int:
     """Collectives that TONY_COLLECTIVE=xgmi asked for but that ran on RCCL (dtype / size / group)."""
     return _FALLBACKS[0]

@@ -361,16 +361,37 @@ class _KvPlane:
         self.keys = self.layout.keys
         self._side: Dict[int, "torch.cuda.Stream"] = {}  # server: per pushing worker, waits + row reads
         self._arrived: Dict[tuple, int] = {}  # server: (kid, worker) -> flag counts expected so far
+        # the window's error word, copied to pinned host memory behind every POLL_EVERY-th copy: a timed-out
+        # device wait surfaces within a few calls on both sides without a device synchronisation
+        self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self._polls = 0
+
+    POLL_EVERY = 8
+
+    def poll(self) -> None:
+        """Raise if an earlier asynchronous read of the error word saw a timed-out wait; queue a new read."""
+        from ..ops import _lib
+
+        if int(self._err_host[0]):
+            self.check()
+        _lib.check(self.L.tony_ps_error_async(self.window, self._err_host.data_ptr(), _lib.stream_ptr(self.device)),
+                   "tony_ps_error_async")
 
     def add_key(self, kid: int, nbytes: int) -> bool:
         return self.layout.add_key(kid, nbytes)
 
     def copy(self, dst: int, src: int, nbytes: int) -> None:
-        """Stream-ordered local copy (out of this rank's window, or into a tensor)."""
+        """Stream-ordered local copy out of this rank's window behind a wait: skipped on the device when a
+        wait of this window timed out (no stale or partial payload is merged or pulled), and the error is
+        raised by the next check."""
         from ..ops import _lib
 
         with torch.cuda.device(self.device):
-            _lib.check(self.L.tony_kv_copy(dst, src, nbytes, _lib.stream_ptr(self.device)), "tony_kv_copy")
+            _lib.check(self.L.tony_kv_copy(dst, src, nbytes, self.window, _lib.stream_ptr(self.device)),
+                       "tony_kv_copy")
+            self._polls += 1
+            if self._polls % self.POLL_EVERY == 0:  # a cheap asynchronous read of the error word
+                self.poll()
 
     def send(self, dst: int, src: int, nbytes: int, flag: int) -> int:
         """Copy into a peer's window and count it on the peer's flag at window offset ``flag`` (no host
@@ -427,14 +448,23 @@ class _KvPlane:
                                "(TONY_KV_WAIT_S): a peer never delivered its payload")
 
     def close(self) -> None:
+        """Unmap the peers and free the window; raises afterwards if a device wait of this rank timed out
+        (the copies behind it were skipped, so the run's payloads are not trustworthy)."""
+        err = None
         if getattr(self, "window", None) is not None:
             torch.cuda.synchronize(self.device)  # no copy into or out of a window is left in flight
+            try:
+                self.check()
+            except RuntimeError as e:
+                err = e
         for p in self._opened:
             self.L.tony_xgmi_close(p)
         self._opened = []
         if getattr(self, "window", None) is not None:
             self.L.tony_xgmi_free(self.window)
             self.window = None
+        if err is not None:
+            raise err
 
 
 def _make_plane(topo: "_Topology", device: Optional[torch.device]) -> Optional[_KvPlane]:
@@ -573,6 +603,8 @@ class _Server:
             w = dist.recv(hdr, tag=TAG_HDR)
             if not self.handle(w, [int(x) for x in hdr.tolist()]):
                 live -= 1
+                if self.plane is not None:  # a worker finished: nothing it sent may have timed out
+                    self.plane.check()
             if len(self.sends) > 64:
                 for s in self.sends:
                     s.wait()
@@ -614,6 +646,9 @@ class DistKVStore(KVStore):
         self._shapes: Dict[int, torch.Size] = {}
         self._unread: set = set()  # keys pushed on the plane and not pulled since (their row may be unread)
         self._replies: Dict[int, int] = {}  # kid -> reply copies counted on this worker's flag (target)
+        # kid -> event after the last plane pull's copy out of the landing area: a repeat pull with no push
+        # in between must not let the server overwrite that area before the copy read it
+        self._landed: Dict[int, "torch.cuda.Event"] = {}
         self.plane_ops = [0, 0]  # pushes / pulls whose payload went over the GPU plane (tests)
         self._closed = False
 
@@ -674,6 +709,12 @@ class DistKVStore(KVStore):
             first = _as_list(o)[0]
             if self._on_plane(kid, first):
                 srv, nbytes, _, land_off, slot = self.plane.keys[kid]
+                prev = self._landed.pop(kid, None)
+                if prev is not None and kid not in self._unread:
+                    # no push since the last pull: nothing orders the server's next reply store after that
+                    # pull's copy-out (a push would -- the server answers only after reading it, and the push
+                    # copy queues behind the copy-out); wait for the copy-out before asking again
+                    prev.synchronize()
                 dist.send(torch.tensor([OP_PULL_X, kid, 0, 0], dtype=torch.int64), srv, tag=TAG_HDR)
                 # the reply lands in this worker's landing area, counted on its reply flag: this stream waits
                 # for it on the device, then copies it out -- the host moves on at once
@@ -681,6 +722,9 @@ class DistKVStore(KVStore):
                 self.plane.wait(_reply_flag(self.topo, srv, slot), n)
                 buf = torch.empty(first.numel(), dtype=first.dtype, device=self.plane.device)
                 self.plane.copy(buf.data_ptr(), self.plane.base + land_off, nbytes)
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.plane.device))
+                self._landed[kid] = ev
                 self._unread.discard(kid)  # the server answered: it consumed this worker's earlier rows
                 self.plane_ops[1] += 1
             else:
