@@ -143,6 +143,7 @@ def test_inception_ps_colocated_tiny(conf):
     assert rc == 0, _diag(client)
     ms = _metrics(client)
     assert len(ms) == 1 and ms[0]["workers"] == 2 and ms[0]["ps_mode"] == "colocated"
+    assert ms[0]["dtype"] == "fp32" and ms[0]["sync"] is True  # CPU ranks compute in fp32
 
 
 def test_inception_ps_dedicated_tiny(conf):

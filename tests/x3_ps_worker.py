@@ -1,0 +1,103 @@
+"""Rank body of tests/test_x3_ps_gpu.py: the x3 (fp32) Inception-v3 trained through the ParameterServer
+(colocated or dedicated) by N processes, then checked against a single-process reference of the same sync-PS
+step (per-worker forward / backward on that worker's batch, gradients averaged, SGD-momentum with L2 decay
+in fp32 -- optim_math.h sgd_update4's formula)."""
+import os
+
+import torch
+
+import gpu_ranks
+
+B, STEPS, CLASSES = 2, 2, 100
+LR, MU, WD = 0.1, 0.9, 4e-5
+
+
+def _data(w, dev):
+    g = torch.Generator(device=dev).manual_seed(77 + w)
+    x = torch.randn((B, 3, 299, 299), generator=g, device=dev).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, CLASSES, (B,), generator=g, device=dev)
+    return x, y
+
+
+def _model(dev):
+    from tony_amd.models.inception_v3 import inception_v3
+
+    torch.manual_seed(0)
+    m = inception_v3(num_classes=CLASSES, precision="fp32", seed=0).to(dev).to(memory_format=torch.channels_last)
+    m.dropout.p = 0.0  # the reference replays the workers' forwards: no masks to match
+    return m.train()
+
+
+def _loss(out, y):
+    from tony_amd.ops import cross_entropy
+
+    logits, aux = out
+    return cross_entropy(logits, y) + 0.4 * cross_entropy(aux, y)
+
+
+def run(rank, world, port, q, mode):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    res = {}
+    try:
+        dev, _ = gpu_ranks.init(rank, world)
+        import torch.distributed as dist
+
+        from tony_amd.parallel.ps import ParameterServer
+        from tony_amd.parallel.trainer import Trainer
+
+        first = 0 if mode == "colocated" else 1
+        nw = world if mode == "colocated" else world - 1
+        if rank == first:
+            # single-process reference first (no parameter server attached in this process yet): same init,
+            # each worker's batch through a fresh x3 model, mean gradient, fp32 SGD-momentum + L2
+            ref = _model(dev)
+            params = list(ref.parameters())
+            w0 = [p.detach().clone() for p in params]
+            vel = [torch.zeros_like(p) for p in params]
+            for _ in range(STEPS):
+                gsum = [torch.zeros_like(p) for p in params]
+                for w in range(nw):
+                    for p in params:
+                        p.grad = None
+                    xw, yw = _data(w, dev)
+                    _loss(ref(xw), yw).backward()
+                    for s_, p in zip(gsum, params):
+                        s_ += p.grad
+                with torch.no_grad():
+                    for p, v, s_ in zip(params, vel, gsum):
+                        v.mul_(MU).add_(s_ / nw + WD * p)
+                        p.add_(v, alpha=-LR)
+            dr = torch.cat([(a.detach() - b).flatten() for a, b in zip(params, w0)])
+            del ref, params, vel, gsum
+            torch.cuda.synchronize()
+        model = _model(dev)
+        ps = ParameterServer(model, optimizer="sgd", lr=LR, momentum=MU, weight_decay=WD, mode=mode, ps_ranks=(0,),
+                             dtype=torch.float32, device=dev, wire_dtype=torch.float32, bucket_mb=8)
+        workers = list(ps.worker_ranks)
+        assert workers[0] == first and len(workers) == nw, (workers, first, nw)
+        if ps.is_worker:
+            trainer = Trainer(model, ps, _loss, use_graph=False)
+            x, y = _data(workers.index(rank), dev)
+            for _ in range(STEPS):
+                loss = trainer.step(x, y)
+            torch.cuda.synchronize()
+            res["loss_finite"] = bool(torch.isfinite(loss).item())
+        else:
+            for _ in range(STEPS):
+                ps.step()
+            torch.cuda.synchronize()
+        dist.barrier()
+        if rank == first:
+            du = torch.cat([(p.detach() - b).flatten() for p, b in zip(model.parameters(), w0)])
+            res["update_rel_err"] = float((du - dr).norm() / dr.norm())
+            res["update_norm"] = float(dr.norm())
+            res["workers"] = len(workers)
+        if ps.plane is not None:
+            ps.plane.close()
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001 - reported to the test
+        import traceback
+
+        res["error"] = f"{type(e).__name__}: {e}\n{traceback.format_exc()[-2500:]}"
+    q.put((rank, res))

@@ -65,6 +65,10 @@ def main(argv=None) -> int:
     ap.add_argument("--fail-at-step", type=int, default=-1, help="test hook (session 0, worker 1)")
     ap.add_argument("--async", dest="async_ps", action="store_true",
                     help="asynchronous PS (dedicated mode): every worker push applied on its own on arrival")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="compute precision on GPU: bf16 (default) or fp32 -- the reference job's precision "
+                         "(mnist_distributed.py: fp32 variables and compute): fp32 activations, variables and "
+                         "pushed gradients, each conv / GEMM product as an x3 split over the bf16 MFMA kernels")
     a = ap.parse_args(argv)
     tc = TFConfig.from_env()
     on_gpu = torch.cuda.is_available()
@@ -86,12 +90,17 @@ def main(argv=None) -> int:
     from tony_amd.models.inception_v3 import inception_v3
     from tony_amd.models.layers import cast_model
 
-    dtype = torch.bfloat16 if on_gpu else torch.float32
+    x3 = on_gpu and a.dtype == "fp32"  # reference precision on the x3-split kernels (ops/x3.py)
+    dtype = torch.bfloat16 if on_gpu and not x3 else torch.float32
     if on_gpu:
         torch.backends.cudnn.benchmark = True
-    model = cast_model(inception_v3(fused=on_gpu, seed=0), dtype, dev).to(memory_format=torch.channels_last)
+    if x3:
+        model = inception_v3(fused=False, seed=0, precision="fp32").to(dev).to(memory_format=torch.channels_last)
+    else:
+        model = cast_model(inception_v3(fused=on_gpu, seed=0), dtype, dev).to(memory_format=torch.channels_last)
     ps = ParameterServer(model, optimizer="sgd", lr=0.045, momentum=0.9, weight_decay=4e-5, mode=mode,
                          ps_ranks=tc.ps_ranks if mode == "dedicated" else (0,), dtype=dtype, device=dev,
+                         wire_dtype=torch.float32 if dtype == torch.float32 else None,
                          sync=not (a.async_ps and mode == "dedicated"))
     if mode == "dedicated" and not ps.sync and ps.plane is None:
         raise SystemExit("--async needs the xGMI PS data plane (GPU ranks)")
@@ -191,6 +200,7 @@ def main(argv=None) -> int:
         # which data plane moved the gradients / variables, and whether its init-time canary against
         # RCCL passed: a run that fell back must not look like one on the hand plane
         metric(model="inception_v3", images_per_sec=float(rate), workers=workers, ps_mode=mode, loss=float(loss),
+               dtype="fp32" if dtype == torch.float32 else "bf16", x3=x3, sync=ps.sync,
                start_step=start, steps=total, plane=_plane_name(ps), verified=coll.data_plane_status(),
                collective_fallbacks=coll.fallback_count())
     log(f"{float(rate):.1f} images/sec total over {workers} workers ({mode} PS)")

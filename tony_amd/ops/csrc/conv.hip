@@ -23,6 +23,7 @@
 
 using namespace tony;
 using namespace tony::mfma;
+using namespace tony::glds;
 
 namespace {
 
@@ -1787,7 +1788,7 @@ int run_x3(Gather g, const void* B, int Cx, void* C, int64_t ldc, int64_t M, int
   const int cp = Cx / 3;
   g.Cs = cp;
   g.K = g.R * g.S * cp;
-  return run_glds<true>(g, B, static_cast<int64_t>(g.R) * g.S * Cx, C, ldc, M, N, epi, stats, sstride, v, stream,
+  return run_glds_x3(g, B, static_cast<int64_t>(g.R) * g.S * Cx, C, ldc, M, N, epi, stats, sstride, v, stream,
                         RowMap{}, BTaps{}, (flags >> 16) & 15, X3Planes{cp, 2 * cp, 3 * cp});
 }
 

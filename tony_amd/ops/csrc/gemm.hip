@@ -24,6 +24,7 @@
 
 using namespace tony;
 using namespace tony::mfma;
+using namespace tony::glds;
 
 namespace {
 

@@ -26,9 +26,9 @@ struct SplitWs {
 SplitWs& splitk_ws();
 }  // namespace tony
 
-namespace {
+namespace tony {
+namespace glds {  // (named: the launchers below are defined in their own translation units, glds*.hip)
 
-using namespace tony;
 using namespace tony::mfma;
 
 // stream-K of conv_glds_kernel (see the kernel): workgroups own equal ranges of the (tile, K-step)
@@ -175,6 +175,7 @@ struct GldsVariant {
   int bm, cap, stages, kb, nwm;  // nwm: waves along M (workgroup = 2 x nwm waves)
   bool il = false;               // interleaved DMA issue (conv_glds_kernel IL; UNI shapes only)
   bool pf = false;               // fragment prefetch (conv_glds_kernel PF)
+  int wpe = 0;                   // > 0: register budget for wpe waves per SIMD (conv_glds_occ_kernel)
 };
 // 11-15: 4-wave 64/128-row tiles at 2-3 workgroups per CU; 16-19: 8-wave 256-row tiles at one (16-18)
 // or two (19) workgroups per CU -- each B (weight) tile is shared by 256 rows, so the LDS-DMA intake
@@ -186,11 +187,13 @@ constexpr GldsVariant kGldsVariants[] = {
     // 20-24: the interleaved-issue forms of the most-picked tiles (11-19 above)
     {128, 128, 3, 32, 2, true}, {128, 192, 3, 32, 2, true}, {128, 128, 2, 64, 2, true},
     {256, 192, 4, 32, 4, true}, {256, 128, 3, 32, 4, true},
-    // 25-31: the fragment-prefetch forms (PF: step k+1's fragments read while step k's MFMAs issue, every
-    // ring slot in flight)
-    {256, 192, 4, 32, 4, false, true}, {256, 128, 3, 32, 4, false, true}, {128, 128, 3, 32, 2, false, true},
-    {128, 192, 3, 32, 2, false, true}, {128, 128, 2, 64, 2, false, true}, {64, 128, 4, 32, 2, false, true},
-    {256, 192, 2, 64, 4, false, true}};
+    // 25-31: several workgroups per CU (conv_glds_occ_kernel: a register budget of wpe waves per SIMD and a
+    // ring that fits the LDS wpe * 64 / (2 * nwm) times)
+    {256, 128, 3, 32, 4, false, false, 4}, {256, 128, 3, 32, 4, true, false, 4}, {128, 128, 3, 32, 2, false, false, 3},
+    {128, 128, 3, 32, 2, true, false, 3}, {128, 192, 3, 32, 2, false, false, 2}, {64, 128, 4, 32, 2, false, false, 3},
+    {64, 128, 3, 32, 2, false, false, 4}};
+// (measured and dropped in round 6: fragment-prefetch forms of 11 / 12 / 14 / 15 / 17-19, PF below -- at most
+// 1.09x on one 17x17 layer, flat on the step; the 256 x 192 forms spilled: profiles/r6_conv_pf_scaling.log)
 // (measured and dropped in round 5: the 256 x 192 tile on a two-slot ring of 64-deep stages, half the
 // barriers per K -- plain 0.93-0.97x of variant 23, interleaved 0.6x; profiles/r5_conv_limits.md)
 constexpr int kNumGlds = sizeof(kGldsVariants) / sizeof(kGldsVariants[0]);
@@ -229,13 +232,12 @@ __device__ __forceinline__ int goff(int row, int ch) {
 // MFMA dependency at the head of every step held the plain loop at ~2x the MFMA + DMA issue floor).  A
 // stage's slot is refilled right after the barrier that follows its last fragment read (every wave then
 // holds those fragments in registers), so all ST slots carry DMAs: one stage more in flight per ring.
-template <int BM, int BN, int ST, int KB, bool UNI, int NWM = 2, bool IL = false, bool X3 = false, bool AT = false,
-          bool PF = false>
-__global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const uint16_t* __restrict__ B, int64_t ldb,
-                                                             uint16_t* __restrict__ C, int64_t ldc, int M, int N,
-                                                             float* __restrict__ stats, int64_t sstride, int epi,
-                                                             int tiles_n, RowMap rmap, BTaps bt, SplitK sk,
-                                                             X3Planes xp, MultiClass mc) {
+template <int BM, int BN, int ST, int KB, bool UNI, int NWM, bool IL, bool X3, bool AT, bool PF>
+__device__ __forceinline__ void conv_glds_body(Gather g, const uint16_t* __restrict__ B, int64_t ldb,
+                                               uint16_t* __restrict__ C, int64_t ldc, int M, int N,
+                                               float* __restrict__ stats, int64_t sstride, int epi,
+                                               int tiles_n, RowMap rmap, BTaps bt, SplitK sk,
+                                               X3Planes xp, MultiClass mc) {
   constexpr int NW = 2 * NWM;                 // waves: NWM along M x 2 along N
   constexpr int WM = BM / NWM, WN = BN / 2, TM = WM / 16, TN = WN / 16;
   constexpr int CPR = KB / 8;                // 16-B chunks per LDS row
@@ -757,6 +759,28 @@ __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(Gather g, const ui
   }
 }
 
+#define TONY_GLDS_PARAMS                                                                                      \
+  Gather g, const uint16_t* __restrict__ B, int64_t ldb, uint16_t* __restrict__ C, int64_t ldc, int M, int N,   \
+      float* __restrict__ stats, int64_t sstride, int epi, int tiles_n, RowMap rmap, BTaps bt, SplitK sk,       \
+      X3Planes xp, MultiClass mc
+#define TONY_GLDS_ARGS g, B, ldb, C, ldc, M, N, stats, sstride, epi, tiles_n, rmap, bt, sk, xp, mc
+template <int BM, int BN, int ST, int KB, bool UNI, int NWM = 2, bool IL = false, bool X3 = false, bool AT = false,
+          bool PF = false>
+__global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(TONY_GLDS_PARAMS) {
+  conv_glds_body<BM, BN, ST, KB, UNI, NWM, IL, X3, AT, PF>(TONY_GLDS_ARGS);
+}
+// The same loop with a register budget for WPE waves per SIMD (amdgpu_waves_per_eu): WPE * 64 / (2 * NWM)
+// workgroups share a CU, so one workgroup's barrier / DMA-landing waits are covered by another's MFMAs
+// instead of idling the SIMD (the plain form takes up to 256 VGPRs: two waves per SIMD, one 8-wave
+// workgroup per CU, all eight waves meeting at every K-step's barrier: profiles/r5_conv_limits.md)
+template <int BM, int BN, int ST, int KB, bool UNI, int NWM, bool IL, int WPE>
+__global__ __launch_bounds__(128 * NWM) __attribute__((amdgpu_waves_per_eu(WPE))) void conv_glds_occ_kernel(
+    TONY_GLDS_PARAMS) {
+  conv_glds_body<BM, BN, ST, KB, UNI, NWM, IL, false, false, false>(TONY_GLDS_ARGS);
+}
+#undef TONY_GLDS_PARAMS
+#undef TONY_GLDS_ARGS
+
 constexpr int64_t kStreamMaxTiles = 4096;  // counters of a stream-K launch's workspace (ops/_lib.py)
 inline int num_cus_of_current() {
   static int cached[16] = {0};
@@ -784,171 +808,28 @@ constexpr X3Variant kX3Variants[] = {{256, 128, 2, 32, 4}, {128, 192, 3, 32, 2},
                                      {128, 128, 2, 64, 2}, {256, 128, 3, 32, 4}, {64, 128, 4, 32, 2}};
 constexpr int kNumX3 = sizeof(kX3Variants) / sizeof(kX3Variants[0]);
 
-// XF: the fused x3 forms (codes kX3First..; xp describes the planes), instantiated only where used
-template <bool XF = false>
-inline int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N, int epi,
-                    float* st, int64_t sstride, int v, hipStream_t stream, RowMap rmap = RowMap{},
-                    BTaps bt = BTaps{}, int stream_m = 0, X3Planes xp = X3Planes{},
-                    const MultiClass* classes = nullptr) {
-  constexpr bool x3 = XF;
-  if (classes != nullptr && (x3 || stream_m > 0 || xp.atab != nullptr || classes->n < 1 || classes->n > kMaxClasses))
-    return -1;
-  if (XF != (xp.btap != 0)) return -1;
-  if (xp.atab != nullptr && (XF || bt.S != 0 || (reinterpret_cast<uintptr_t>(xp.atab) & 15))) return -1;
-  if ((ldc % 8) || (ldb % 8) || (reinterpret_cast<uintptr_t>(C) & 15) || (reinterpret_cast<uintptr_t>(B) & 15) ||
-      (reinterpret_cast<uintptr_t>(g.src) & 15) || (g.ld % 8) || (g.K % 8))
-    return -3;
-  if (x3 ? (v < kX3First || v >= kX3First + kNumX3 || bt.S != 0 || (xp.alo % 8) || (xp.blo % 8) || (xp.btap % 8))
-         : (v < kGldsFirst || v >= kGldsFirst + kNumGlds))
-    return -3;
-  const GldsVariant gv = x3 ? GldsVariant{kX3Variants[v - kX3First].bm, kX3Variants[v - kX3First].cap,
-                                          kX3Variants[v - kX3First].stages, kX3Variants[v - kX3First].kb,
-                                          kX3Variants[v - kX3First].nwm}
-                            : kGldsVariants[v - kGldsFirst];
-  const int64_t bn = pick_bn(N, gv.cap);
-  using std::integral_constant;
-  const auto launch = [&](auto bm, auto bnc, auto st_, auto kb, auto nwm, auto il, auto x3c, auto pfc) -> int {
-    constexpr int BM = decltype(bm)::value, BN = decltype(bnc)::value, ST = decltype(st_)::value;
-    constexpr int KB = decltype(kb)::value, NWM = decltype(nwm)::value;
-    constexpr bool IL = decltype(il)::value, X3 = decltype(x3c)::value, PF = decltype(pfc)::value;
-    constexpr int PL = X3 ? 2 : 1;
-    if constexpr (BN % (64 / (KB / 8)) != 0 || BM * (BN + 8) > ST * PL * (BM + BN) * KB ||
-                  ST * PL * (BM + BN) * KB * 2 > 163840 || (X3 && IL) || (PF && (X3 || IL))) {
-      return -3;
-    } else {
-      const int tiles_n = ceil_div(N, BN);
-      MultiClass mc{};
-      int64_t tiles = 0;
-      if (classes != nullptr) {  // the classes' tile ranges end to end (M is unused then)
-        mc = *classes;
-        for (int i = 0; i < mc.n; ++i) {
-          if (mc.c[i].g.Cs % KB != 0 || mc.c[i].bt.S == 0) return -3;  // uniform-tap class taps only
-          const int64_t t = static_cast<int64_t>(ceil_div(mc.c[i].M, BM)) * tiles_n;
-          if (tiles + t + 8 > 0x7fffffff) return -2;
-          mc.c[i].begin = static_cast<int>(tiles);
-          mc.c[i].tiles = static_cast<int>(t);
-          tiles += (t + 7) & ~int64_t{7};
-        }
-      } else {
-        tiles = static_cast<int64_t>(ceil_div(M, BM)) * tiles_n;
-      }
-      if (tiles > 0x7fffffff) return -2;
-      SplitK sk{};
-      int grid = static_cast<int>(tiles);
-      if (stream_m > 0) {
-        // worth it while the tiles leave CUs idle or a near-empty last wave: a few tiles per CU at most
-        const int cus = num_cus_of_current();
-        const int64_t iters = tiles * ((g.K + KB - 1) / KB);
-        int64_t G = static_cast<int64_t>(stream_m) * cus;
-        G = std::min<int64_t>(G, iters / 4);  // >= 4 K-steps per workgroup
-        if (tiles > 4 * G || tiles > kStreamMaxTiles || G < 2 || tiles % G == 0) return -3;
-        const SplitWs& ws = splitk_ws();
-        if (ws.slab != nullptr && ws.cnt != nullptr && ws.ncnt >= 2 * tiles &&
-            ws.slab_floats >= 2 * G * BM * BN) {
-          sk.slab = ws.slab;
-          sk.cnt = ws.cnt;
-          sk.ntiles = static_cast<int>(tiles);
-          sk.stream = 1;
-          grid = static_cast<int>(G);
-        }
-      }
-      const auto args = std::make_tuple(g, static_cast<const uint16_t*>(B), ldb, static_cast<uint16_t*>(C), ldc,
-                                        static_cast<int>(M), static_cast<int>(N), st, sstride, epi, tiles_n, rmap, bt,
-                                        sk, xp, mc);
-      if (xp.atab != nullptr) {  // the BN-apply-on-load prototype: one tile family
-        if constexpr (!X3 && !IL && !PF && BM == 128 && ST == 3 && KB == 32 && NWM == 2 && BN <= 128) {
-          if (g.Cs % KB != 0 || g.R != 1 || g.S != 1) return -3;
-          std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true, NWM, false, false, true><<<grid, 128 * NWM, 0, stream>>>(a...); }, args);
-          TONY_LAUNCH_CHECK();
-          return 0;
-        } else {
-          return -3;
-        }
-      }
-      if constexpr (X3) {
-        if (g.Cs % KB != 0) return -3;  // the fused planes run the uniform-tap loop only
-        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true, NWM, false, true><<<grid, 128 * NWM, 0, stream>>>(a...); }, args);
-      } else if (g.Cs % KB == 0 && glds_uni_enabled()) {
-        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, true, NWM, IL, false, false, PF><<<grid, 128 * NWM, 0, stream>>>(a...); }, args);
-      } else if (IL || bt.S != 0) {
-        return -3;  // the interleaved form and the class taps exist for the uniform-tap loop only
-      } else {
-        std::apply([&](auto... a) { conv_glds_kernel<BM, BN, ST, KB, false, NWM, false, false, false, PF><<<grid, 128 * NWM, 0, stream>>>(a...); }, args);
-      }
-      TONY_LAUNCH_CHECK();
-      return 0;
-    }
-  };
-  const auto by_bn = [&](auto bm, auto st_, auto kb, auto cap, auto nwm, auto il, auto x3c, auto pfc) -> int {
-    constexpr int CAP = decltype(cap)::value;
-    switch (bn) {
-      case 32: return launch(bm, integral_constant<int, 32>{}, st_, kb, nwm, il, x3c, pfc);
-      case 64: return launch(bm, integral_constant<int, 64>{}, st_, kb, nwm, il, x3c, pfc);
-      case 96: return launch(bm, integral_constant<int, 96>{}, st_, kb, nwm, il, x3c, pfc);
-      case 128: return launch(bm, integral_constant<int, 128>{}, st_, kb, nwm, il, x3c, pfc);
-      case 160:
-        if constexpr (CAP >= 160) return launch(bm, integral_constant<int, 160>{}, st_, kb, nwm, il, x3c, pfc);
-        break;
-      case 192:
-        if constexpr (CAP >= 192) return launch(bm, integral_constant<int, 192>{}, st_, kb, nwm, il, x3c, pfc);
-        break;
-      default: break;
-    }
-    return -3;
-  };
-  using I2 = integral_constant<int, 2>;
-  using I3 = integral_constant<int, 3>;
-  using I4 = integral_constant<int, 4>;
-  using K32 = integral_constant<int, 32>;
-  using K64 = integral_constant<int, 64>;
-  using M64 = integral_constant<int, 64>;
-  using M128 = integral_constant<int, 128>;
-  using C128 = integral_constant<int, 128>;
-  using C192 = integral_constant<int, 192>;
-  using M256 = integral_constant<int, 256>;
-  using I5 = integral_constant<int, 5>;
-  using W2 = integral_constant<int, 2>;
-  using W4 = integral_constant<int, 4>;
-  using NO = std::false_type;
-  using ILV = std::true_type;
-  using PFV = std::true_type;
-  if constexpr (XF) {
-    using X = std::true_type;
-    switch (v - kX3First) {
-      case 0: return by_bn(M256{}, I2{}, K32{}, C128{}, W4{}, NO{}, X{}, NO{});
-      case 1: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{}, NO{}, X{}, NO{});
-      case 2: return by_bn(M128{}, I4{}, K32{}, C128{}, W2{}, NO{}, X{}, NO{});
-      case 3: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, NO{}, X{}, NO{});
-      case 4: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, NO{}, X{}, NO{});
-      case 5: return by_bn(M64{}, I4{}, K32{}, C128{}, W2{}, NO{}, X{}, NO{});
-      default: return -3;
-    }
-  } else {
-  switch (v - kGldsFirst) {
-    case 0: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, NO{}, NO{}, NO{});
-    case 1: return by_bn(M128{}, I3{}, K32{}, C128{}, W2{}, NO{}, NO{}, NO{});
-    case 2: return by_bn(M128{}, I4{}, K32{}, C128{}, W2{}, NO{}, NO{}, NO{});
-    case 3: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{}, NO{}, NO{}, NO{});
-    case 4: return by_bn(M64{}, I4{}, K32{}, C128{}, W2{}, NO{}, NO{}, NO{});
-    case 5: return by_bn(M256{}, I4{}, K32{}, C192{}, W4{}, NO{}, NO{}, NO{});
-    case 6: return by_bn(M256{}, I3{}, K64{}, C128{}, W4{}, NO{}, NO{}, NO{});
-    case 7: return by_bn(M256{}, I5{}, K32{}, C192{}, W4{}, NO{}, NO{}, NO{});
-    case 8: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, NO{}, NO{}, NO{});
-    case 9: return by_bn(M128{}, I3{}, K32{}, C128{}, W2{}, ILV{}, NO{}, NO{});
-    case 10: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{}, ILV{}, NO{}, NO{});
-    case 11: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, ILV{}, NO{}, NO{});
-    case 12: return by_bn(M256{}, I4{}, K32{}, C192{}, W4{}, ILV{}, NO{}, NO{});
-    case 13: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, ILV{}, NO{}, NO{});
-    case 14: return by_bn(M256{}, I4{}, K32{}, C192{}, W4{}, NO{}, NO{}, PFV{});
-    case 15: return by_bn(M256{}, I3{}, K32{}, C128{}, W4{}, NO{}, NO{}, PFV{});
-    case 16: return by_bn(M128{}, I3{}, K32{}, C128{}, W2{}, NO{}, NO{}, PFV{});
-    case 17: return by_bn(M128{}, I3{}, K32{}, C192{}, W2{}, NO{}, NO{}, PFV{});
-    case 18: return by_bn(M128{}, I2{}, K64{}, C128{}, W2{}, NO{}, NO{}, PFV{});
-    case 19: return by_bn(M64{}, I4{}, K32{}, C128{}, W2{}, NO{}, NO{}, PFV{});
-    case 20: return by_bn(M256{}, I2{}, K64{}, C192{}, W4{}, NO{}, NO{}, PFV{});
-    default: return -3;
-  }
-  }
-}
+// Variant families, each compiled in a translation unit of its own (glds_p0..3.hip, glds_x3.hip) so that the
+// build runs them in parallel and every kernel instance lives in exactly one code object: case index
+// v - kGldsFirst 0-4 (4-wave tiles), 5-8 (8-wave 256-row tiles), 9-13 (interleaved issue), 14-20 (several
+// workgroups per CU); the fused x3 forms.
+constexpr int glds_part(int c) { return c <= 4 ? 0 : c <= 8 ? 1 : c <= 13 ? 2 : 3; }
 
-}  // namespace
+// B rows n = [K] at row stride ldb (the conv weights [Co][R][S][Ci]: ldb = K)
+// stream_m > 0: stream-K over stream_m x (CUs) workgroups (SplitK above) when this thread's workspace
+// (tony_splitk_workspace) holds 2 partial tiles per workgroup and a counter per tile, else the plain
+// launch (same result).  Defined in glds.hip.
+int run_glds(const Gather& g, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N, int epi,
+             float* st, int64_t sstride, int v, hipStream_t stream, RowMap rmap = RowMap{}, BTaps bt = BTaps{},
+             int stream_m = 0, X3Planes xp = X3Planes{}, const MultiClass* classes = nullptr);
+// the fused x3 forms (codes kX3First..; xp describes the planes)
+int run_glds_x3(const Gather& g, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N, int epi,
+                float* st, int64_t sstride, int v, hipStream_t stream, RowMap rmap, BTaps bt, int stream_m,
+                X3Planes xp);
+// one family's launcher (glds_launch.h, instantiated once per family)
+template <bool XF, int PART>
+int run_glds_part(const Gather& g, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M, int64_t N, int epi,
+                  float* st, int64_t sstride, int v, hipStream_t stream, RowMap rmap, BTaps bt, int stream_m,
+                  X3Planes xp, const MultiClass* classes);
+
+}  // namespace glds
+}  // namespace tony

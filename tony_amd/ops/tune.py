@@ -24,9 +24,9 @@ AUTOTUNE = os.environ.get("TONY_CONV_AUTOTUNE", "1") != "0"
 _N_GLDS = (25 if os.environ.get("TONY_CONV_GLDS_IL", "1") != "0" else 20) \
     if os.environ.get("TONY_CONV_GLDS8", "1") != "0" else 16
 _BASE = tuple(range(_N_GLDS if os.environ.get("TONY_CONV_GLDS", "1") != "0" else 11))
-# 25-31: the fragment-prefetch forms of the LDS-DMA tiles (igemm.h PF: step k+1's fragments read while step
-# k's MFMAs issue; TONY_CONV_PF=0 leaves them out of the search)
-if os.environ.get("TONY_CONV_PF", "1") != "0" and os.environ.get("TONY_CONV_GLDS", "1") != "0":
+# 25-31: the LDS-DMA tiles at several workgroups per CU (igemm.h conv_glds_occ_kernel: a register budget of
+# 2-4 waves per SIMD; TONY_CONV_OCC=0 leaves them out of the search)
+if os.environ.get("TONY_CONV_OCC", "1") != "0" and os.environ.get("TONY_CONV_GLDS", "1") != "0":
     _BASE = _BASE + tuple(range(25, 32))
 # + stream-K forms of the LDS-DMA variants (csrc/igemm.h SplitK): candidate v + 256 * m, i.e. flags bits
 # 16..19 = m, a grid of m x CUs workgroups sharing the (tile, K-step) iterations.  Only launches whose
