@@ -238,16 +238,20 @@ __global__ __launch_bounds__(kThreads) void bn_fwd_apply_kernel(
     }
     const V8<T> out = V8<T>::from_float(f);
     out.store(yb + row * ldyt);
-    if (!X3 && p3 != nullptr) {  // also the x3 planes of y (a concat slot's slice of the block's planes)
-      const V8<uint16_t> hi = V8<uint16_t>::from_float(f);
-      float hf[8], lo[8];
-      hi.to_float(hf);
+    // also the x3 planes of y (a concat slot's slice of the block's planes); fp32 rows only -- compiled out of
+    // the bf16 kernel (the runtime test alone cost it 18 VGPRs: 100 -> 118, one wave per SIMD fewer)
+    if constexpr (!X3 && std::is_same<T, float>::value) {
+      if (p3 != nullptr) {
+        const V8<uint16_t> hi = V8<uint16_t>::from_float(f);
+        float hf[8], lo[8];
+        hi.to_float(hf);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) lo[j] = f[j] - hf[j];
-      uint16_t* d = p3 + row * ldp + rm.cg * 8;
-      hi.store(d);
-      V8<uint16_t>::from_float(lo).store(d + pst);
-      hi.store(d + 2 * pst);
+        for (int j = 0; j < 8; ++j) lo[j] = f[j] - hf[j];
+        uint16_t* d = p3 + row * ldp + rm.cg * 8;
+        hi.store(d);
+        V8<uint16_t>::from_float(lo).store(d + pst);
+        hi.store(d + 2 * pst);
+      }
     }
     if (RES && mask != nullptr) {  // the stored values' sign, exactly what re-reading y would test
       float g[8];
