@@ -28,7 +28,7 @@ def classify(name):
     if "gemm_nt_kernel" in n or "gemm_tn_splitk" in n or "gemm_tn_glds" in n:
         return "tony HIP: MFMA GEMM (1x1 conv fwd/dgrad/wgrad)"
     if "conv_nt_kernel" in n or "conv_wgrad_kernel" in n or "conv_wgrad_glds" in n or "conv_halo" in n \
-            or "conv_direct_kernel" in n or "conv_glds_kernel" in n or "conv_wgrad_direct" in n or "conv_wgrad_x3f" in n:
+            or "conv_direct_kernel" in n or "conv_glds_kernel" in n or "conv_glds_occ" in n or "conv_wgrad_direct" in n or "conv_wgrad_x3f" in n:
         return "tony HIP: implicit-GEMM conv (fwd/dgrad/wgrad)"
     if "stem_fwd_kernel" in n or "stem_wgrad_kernel" in n:
         return "tony HIP: MFMA image-stem conv (fwd/wgrad)"
