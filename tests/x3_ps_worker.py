@@ -8,7 +8,7 @@ import torch
 
 import gpu_ranks
 
-B, STEPS, CLASSES = 2, 2, 100
+B, STEPS, CLASSES = 2, 2, 1000  # (the x3 classifier wants out_features % 8 == 0)
 LR, MU, WD = 0.1, 0.9, 4e-5
 
 

@@ -73,12 +73,12 @@ int run_glds_part(const Gather& g, const void* B, int64_t ldb, void* C, int64_t 
       const auto args = std::make_tuple(g, static_cast<const uint16_t*>(B), ldb, static_cast<uint16_t*>(C), ldc,
                                         static_cast<int>(M), static_cast<int>(N), st, sstride, epi, tiles_n, rmap, bt,
                                         sk, xp, mc);
-      // the lean kernels (SKM false) unless this launch uses stream-K or the residue classes
-      const bool full = sk.stream != 0 || classes != nullptr;
+      // the lean kernels (FT 0) unless this launch runs stream-K (1) or the residue classes (2)
+      const int ft = classes != nullptr ? 2 : (sk.stream != 0 ? 1 : 0);
       const auto go = [&](auto kern) { std::apply([&](auto... a) { kern<<<grid, 128 * NWM, 0, stream>>>(a...); }, args); };
       if (xp.atab != nullptr) {  // the BN-apply-on-load prototype: one tile family
         if constexpr (!X3 && !IL && !PF && WPE == 0 && BM == 128 && ST == 3 && KB == 32 && NWM == 2 && BN <= 128) {
-          if (g.Cs % KB != 0 || g.R != 1 || g.S != 1 || full) return -3;
+          if (g.Cs % KB != 0 || g.R != 1 || g.S != 1 || ft) return -3;
           go(conv_glds_kernel<BM, BN, ST, KB, true, NWM, false, false, true>);
           TONY_LAUNCH_CHECK();
           return 0;
@@ -88,37 +88,44 @@ int run_glds_part(const Gather& g, const void* B, int64_t ldb, void* C, int64_t 
       }
       if constexpr (X3) {
         if (g.Cs % KB != 0) return -3;  // the fused planes run the uniform-tap loop only
-        if (full)
-          go(conv_glds_kernel<BM, BN, ST, KB, true, NWM, false, true, false, false, true>);
+        if (ft == 1)
+          go(conv_glds_kernel<BM, BN, ST, KB, true, NWM, false, true, false, false, 1>);
+        else if (ft == 0)
+          go(conv_glds_kernel<BM, BN, ST, KB, true, NWM, false, true, false, false, 0>);
         else
-          go(conv_glds_kernel<BM, BN, ST, KB, true, NWM, false, true, false, false, false>);
+          return -3;
       } else if (g.Cs % KB == 0 && glds_uni_enabled()) {
         if constexpr (WPE > 0) {
-          if (full)
-            go(conv_glds_occ_kernel<BM, BN, ST, KB, true, NWM, IL, WPE, true>);
+          if (ft == 1)
+            go(conv_glds_occ_kernel<BM, BN, ST, KB, true, NWM, IL, WPE, 1>);
+          else if (ft == 2)
+            go(conv_glds_occ_kernel<BM, BN, ST, KB, true, NWM, IL, WPE, 2>);
           else
-            go(conv_glds_occ_kernel<BM, BN, ST, KB, true, NWM, IL, WPE, false>);
+            go(conv_glds_occ_kernel<BM, BN, ST, KB, true, NWM, IL, WPE, 0>);
         } else {
-          if (full)
-            go(conv_glds_kernel<BM, BN, ST, KB, true, NWM, IL, false, false, PF, true>);
+          if (ft == 1)
+            go(conv_glds_kernel<BM, BN, ST, KB, true, NWM, IL, false, false, PF, 1>);
+          else if (ft == 2)
+            go(conv_glds_kernel<BM, BN, ST, KB, true, NWM, IL, false, false, PF, 2>);
           else
-            go(conv_glds_kernel<BM, BN, ST, KB, true, NWM, IL, false, false, PF, false>);
+            go(conv_glds_kernel<BM, BN, ST, KB, true, NWM, IL, false, false, PF, 0>);
         }
       } else if (IL || bt.S != 0) {
         return -3;  // the interleaved form and the class taps exist for the uniform-tap loop only
       } else if constexpr (IL) {
         return -3;  // (no general-loop instance in the interleaved family: it is the plain family's)
       } else {
+        if (ft == 2) return -3;  // (the residue classes are uniform-tap only)
         if constexpr (WPE > 0) {
-          if (full)
-            go(conv_glds_occ_kernel<BM, BN, ST, KB, false, NWM, false, WPE, true>);
+          if (ft == 1)
+            go(conv_glds_occ_kernel<BM, BN, ST, KB, false, NWM, false, WPE, 1>);
           else
-            go(conv_glds_occ_kernel<BM, BN, ST, KB, false, NWM, false, WPE, false>);
+            go(conv_glds_occ_kernel<BM, BN, ST, KB, false, NWM, false, WPE, 0>);
         } else {
-          if (full)
-            go(conv_glds_kernel<BM, BN, ST, KB, false, NWM, false, false, false, PF, true>);
+          if (ft == 1)
+            go(conv_glds_kernel<BM, BN, ST, KB, false, NWM, false, false, false, PF, 1>);
           else
-            go(conv_glds_kernel<BM, BN, ST, KB, false, NWM, false, false, false, PF, false>);
+            go(conv_glds_kernel<BM, BN, ST, KB, false, NWM, false, false, false, PF, 0>);
         }
       }
       TONY_LAUNCH_CHECK();

@@ -232,11 +232,11 @@ __device__ __forceinline__ int goff(int row, int ch) {
 // MFMA dependency at the head of every step held the plain loop at ~2x the MFMA + DMA issue floor).  A
 // stage's slot is refilled right after the barrier that follows its last fragment read (every wave then
 // holds those fragments in registers), so all ST slots carry DMAs: one stage more in flight per ring.
-// SKM: the stream-K segments (SplitK) and every-residue-class launches (MultiClass) compiled in.  Off, the
-// workgroup runs exactly one whole tile with none of their state: the round-5 kernels carried both in every
+// FT: the stream-K segments (SplitK, bit 0) / every-residue-class launches (MultiClass, bit 1) compiled in.
+// 0, the workgroup runs exactly one whole tile with none of their state: the round-5 kernels carried both in every
 // launch and grew from 122 to 240 VGPRs (256 x 128) / 168 to 256 + spills (256 x 192), SGPRs 85 -> 106,
 // which halved the resident workgroups and cost the bf16 step 0.5-1.4 ms (profiles/r6_regression_bisect.md).
-template <int BM, int BN, int ST, int KB, bool UNI, int NWM, bool IL, bool X3, bool AT, bool PF, bool SKM>
+template <int BM, int BN, int ST, int KB, bool UNI, int NWM, bool IL, bool X3, bool AT, bool PF, int FT>
 __device__ __forceinline__ void conv_glds_body(Gather g, const uint16_t* __restrict__ B, int64_t ldb,
                                                uint16_t* __restrict__ C, int64_t ldc, int M, int N,
                                                float* __restrict__ stats, int64_t sstride, int epi,
@@ -263,7 +263,7 @@ __device__ __forceinline__ void conv_glds_body(Gather g, const uint16_t* __restr
   const int wm = wave >> 1, wn = wave & 1;
   const int G = gridDim.x;
   int w = 0;
-  if (SKM && mc.n > 0) {  // (uniform; static indices only, so the descriptors stay scalar kernel-argument loads)
+  if ((FT & 2) && mc.n > 0) {  // (uniform; static indices only, so the descriptors stay scalar kernel-argument loads)
     const int b = blockIdx.x;
     int sel = 0;
 #pragma unroll
@@ -292,11 +292,11 @@ __device__ __forceinline__ void conv_glds_body(Gather g, const uint16_t* __restr
   // runs the epilogue itself; the segments of a shared tile meet in SplitK's fold.  Neighbouring
   // ranges share a tile, so the remap keeps them on one XCD.
   const int64_t T = static_cast<int64_t>(tiles_n) * ((M + BM - 1) / BM) * nk_all;
-  const bool streamk = SKM && sk.stream;
+  const bool streamk = (FT & 1) && sk.stream;
   int64_t it = streamk ? static_cast<int64_t>(w) * T / G : static_cast<int64_t>(w) * nk_all;
   const int64_t it_end = streamk ? static_cast<int64_t>(w + 1) * T / G : it + nk_all;
   for (bool first_seg = true; it < it_end; first_seg = false) {
-  if (SKM && !first_seg) __syncthreads();  // the previous segment's epilogue is done with the LDS
+  if ((FT & 1) && !first_seg) __syncthreads();  // the previous segment's epilogue is done with the LDS
   const int tile = static_cast<int>(it / nk_all);
   const int kt0 = static_cast<int>(it - static_cast<int64_t>(tile) * nk_all);
   const int nk = static_cast<int>(min(static_cast<int64_t>(nk_all - kt0), it_end - it));
@@ -680,7 +680,7 @@ __device__ __forceinline__ void conv_glds_body(Gather g, const uint16_t* __restr
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tail's zero fills land before LDS is reused
   __syncthreads();
-  if (SKM && nk != nk_all) {
+  if ((FT & 1) && nk != nk_all) {
     // a shared tile: take the tile's ticket first.  Every contributor but the last stores its fp32
     // partial to its slot (part 0: the workgroup's first segment, 1: its last) and counts itself done;
     // the last waits for the others' done count -- they hold tickets, so they are past their K loops
@@ -761,7 +761,7 @@ __device__ __forceinline__ void conv_glds_body(Gather g, const uint16_t* __restr
                                            (epi & 2) ? stats : nullptr, (epi & 4) != 0, rmap, (epi & 8) != 0,
                                            (epi & 48) != 0, am ? reinterpret_cast<const uint16_t*>(stats) : nullptr,
                                            am ? reinterpret_cast<const uint8_t*>(sstride) : nullptr);
-  if constexpr (!SKM) break;  // one whole tile per workgroup
+  if constexpr (!(FT & 1)) break;  // one whole tile per workgroup
   }
 }
 
@@ -771,18 +771,18 @@ __device__ __forceinline__ void conv_glds_body(Gather g, const uint16_t* __restr
       X3Planes xp, MultiClass mc
 #define TONY_GLDS_ARGS g, B, ldb, C, ldc, M, N, stats, sstride, epi, tiles_n, rmap, bt, sk, xp, mc
 template <int BM, int BN, int ST, int KB, bool UNI, int NWM = 2, bool IL = false, bool X3 = false, bool AT = false,
-          bool PF = false, bool SKM = false>
+          bool PF = false, int FT = 0>
 __global__ __launch_bounds__(128 * NWM) void conv_glds_kernel(TONY_GLDS_PARAMS) {
-  conv_glds_body<BM, BN, ST, KB, UNI, NWM, IL, X3, AT, PF, SKM>(TONY_GLDS_ARGS);
+  conv_glds_body<BM, BN, ST, KB, UNI, NWM, IL, X3, AT, PF, FT>(TONY_GLDS_ARGS);
 }
 // The same loop with a register budget for WPE waves per SIMD (amdgpu_waves_per_eu): WPE * 64 / (2 * NWM)
 // workgroups share a CU, so one workgroup's barrier / DMA-landing waits are covered by another's MFMAs
 // instead of idling the SIMD (the plain form takes up to 256 VGPRs: two waves per SIMD, one 8-wave
 // workgroup per CU, all eight waves meeting at every K-step's barrier: profiles/r5_conv_limits.md)
-template <int BM, int BN, int ST, int KB, bool UNI, int NWM, bool IL, int WPE, bool SKM = false>
+template <int BM, int BN, int ST, int KB, bool UNI, int NWM, bool IL, int WPE, int FT = 0>
 __global__ __launch_bounds__(128 * NWM) __attribute__((amdgpu_waves_per_eu(WPE))) void conv_glds_occ_kernel(
     TONY_GLDS_PARAMS) {
-  conv_glds_body<BM, BN, ST, KB, UNI, NWM, IL, false, false, false, SKM>(TONY_GLDS_ARGS);
+  conv_glds_body<BM, BN, ST, KB, UNI, NWM, IL, false, false, false, FT>(TONY_GLDS_ARGS);
 }
 #undef TONY_GLDS_PARAMS
 #undef TONY_GLDS_ARGS
