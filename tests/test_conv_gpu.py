@@ -758,3 +758,38 @@ def test_gemm_glds_streamk_reuses_rearmed_counters(cuda, m):
         assert torch.equal(c, outs[0][0])
         assert _rel(c, ref) < 1e-2
         torch.testing.assert_close(_lib.fold_stats(stats, N)[:N], ref.sum(0), rtol=2e-3, atol=M * 2e-3)
+
+
+# (N, Cin, H, W, Cout, (R, S), padding): wgrad shapes on the LDS-DMA wgrad kernel (Cout > 64: 96 / 128-row
+# tiles) with the incremental row walk -- K steps not a multiple of the 6-step unroll, 1x1, 3x3, 1x7
+WGRAD_PF_SHAPES = [(4, 64, 35, 35, 96, (3, 3), (1, 1)), (3, 160, 17, 17, 192, (1, 7), (0, 3)),
+                   (2, 192, 17, 17, 160, (1, 1), (0, 0)), (5, 96, 11, 13, 128, (3, 3), (0, 0))]
+
+
+@pytest.mark.parametrize("shape", WGRAD_PF_SHAPES, ids=[f"{s[1]}->{s[4]}_{s[2]}x{s[3]}k{s[5][0]}{s[5][1]}" for s in WGRAD_PF_SHAPES])
+def test_wgrad_fragment_prefetch_matches_plain(cuda, shape):
+    """conv.hip conv_wgrad_glds_kernel PF (tony_wgrad_pf): the fragment-prefetch K loop issues the same MFMAs
+    in the same order as the plain loop -- bit-identical dW -- and matches the fp32 reference."""
+    from tony_amd.ops import _lib
+    from tony_amd.ops.conv import conv_wgrad
+
+    n, c, h, w, co, (r, s), p = shape
+    torch.manual_seed(1)
+    x = _nhwc(torch.randn(n, c, h, w, device=cuda)).to(torch.bfloat16)
+    wt = torch.randn(co, c, r, s, device=cuda)
+    oh, ow = h + 2 * p[0] - r + 1, w + 2 * p[1] - s + 1
+    dy = _nhwc(torch.randn(n, co, oh, ow, device=cuda)).to(torch.bfloat16)
+    L = _lib.lib()
+    prev = L.tony_wgrad_pf(-1)
+    try:
+        outs = []
+        for pf in (0, 1):
+            L.tony_wgrad_pf(pf)
+            outs.append(conv_wgrad(dy, x, wt.shape, 1, p, impl=1).float().clone())
+    finally:
+        L.tony_wgrad_pf(prev)
+    torch.testing.assert_close(outs[1], outs[0], rtol=0, atol=0)
+    xr = x.float().requires_grad_(False)
+    wr = torch.zeros_like(wt, requires_grad=True)
+    torch.nn.functional.conv2d(xr, wr, None, 1, p).backward(dy.float())
+    assert _rel(outs[1], wr.grad) < 1e-2

@@ -35,6 +35,13 @@ def _loss(out, y):
     return cross_entropy(logits, y) + 0.4 * cross_entropy(aux, y)
 
 
+def _say(rank, msg):
+    import sys
+    import time
+
+    print(f"[x3-ps rank {rank} {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def run(rank, world, port, q, mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     res = {}
@@ -61,6 +68,7 @@ def run(rank, world, port, q, mode):
                         p.grad = None
                     xw, yw = _data(w, dev)
                     _loss(ref(xw), yw).backward()
+                    _say(rank, f"reference: worker {w}'s batch done")
                     for s_, p in zip(gsum, params):
                         s_ += p.grad
                 with torch.no_grad():
@@ -78,13 +86,15 @@ def run(rank, world, port, q, mode):
         if ps.is_worker:
             trainer = Trainer(model, ps, _loss, use_graph=False)
             x, y = _data(workers.index(rank), dev)
-            for _ in range(STEPS):
+            for i in range(STEPS):
                 loss = trainer.step(x, y)
-            torch.cuda.synchronize()
+                torch.cuda.synchronize()
+                _say(rank, f"PS step {i} done")
             res["loss_finite"] = bool(torch.isfinite(loss).item())
         else:
-            for _ in range(STEPS):
+            for i in range(STEPS):
                 ps.step()
+                _say(rank, f"ps apply {i} issued")
             torch.cuda.synchronize()
         dist.barrier()
         if rank == first:

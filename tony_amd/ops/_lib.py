@@ -120,6 +120,7 @@ _SIGNATURES = {
                            c_void_p],
     "tony_x3_wgrad_mode": [c_int],
     "tony_dgrad_one_launch": [c_int],
+    "tony_wgrad_pf": [c_int],
     "tony_kv_copy_blocks": [c_int64],
     "tony_kv_copy_flag": [c_void_p, c_void_p, c_int64, c_void_p, c_void_p],
     "tony_kv_wait": [c_void_p, ctypes.c_uint32, c_void_p, ctypes.c_double, c_void_p],

@@ -1108,7 +1108,11 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(const uint16_t* __
 // `s_waitcnt vmcnt(4)` + a raw s_barrier per stage (a __syncthreads() would drain the ring).
 constexpr int kWgStages = 3;
 
-template <int TBM, bool INC>
+// PF: the fragments of K-step k+1 are read from LDS into a second register set while step k's MFMAs issue
+// (the transposing reads no longer sit between every barrier and its MFMAs); a stage's slot is refilled as
+// soon as every wave holds its fragments, so all three slots carry DMAs.  +28 VGPRs (TBM 96): still three
+// workgroups per CU (LDS-bound).
+template <int TBM, bool INC, bool PF = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wgrad_glds_kernel(const uint16_t* __restrict__ dY, int64_t lddy,
                                                                    Gather g, int64_t M, int Co, int tiles_n2,
                                                                    int ntiles, int64_t rows_per_split,
@@ -1207,6 +1211,54 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = static_cast<int>((m_end - m_begin + WK - 1) / WK);
+  if constexpr (PF) {
+    const int kgrp = lane >> 4;
+    bf16x8_t fa[2][TM], fb[2][4];
+    auto rd = [&](auto slotc, auto bufc) {
+      constexpr int SLOT = decltype(slotc)::value, BUF = decltype(bufc)::value;
+      const uint16_t* As = smem + SLOT * STAGE;
+      const uint16_t* Bs = As + TILE;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[BUF][i] = tr_frag(As, kgrp, wm * (TBM / 2) + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[BUF][j] = tr_frag(Bs, kgrp, wn * 64 + j * 16, lane);
+    };
+    // K-step kt on ring slot SLOT with its fragments in register set BUF: stage kt + 1 has landed in every
+    // wave and every wave holds step kt's fragments, so slot SLOT takes stage kt + 3
+    auto pstep = [&](auto slotc, auto bufc) {
+      constexpr int SLOT = decltype(slotc)::value, BUF = decltype(bufc)::value;
+      asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      issue(SLOT);
+      rd(std::integral_constant<int, (SLOT + 1) % kWgStages>{}, std::integral_constant<int, 1 - BUF>{});
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[BUF][i], fb[BUF][j], acc[i][j], 0, 0, 0);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    issue(0);
+    issue(1);
+    issue(2);
+    asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+    rd(I0{}, I0{});
+    int kt = 0;
+    for (; kt + 6 <= nk; kt += 6) {  // (slot, register set) repeat every 6 steps
+      pstep(I0{}, I0{});
+      pstep(I1{}, I1{});
+      pstep(I2{}, I0{});
+      pstep(I0{}, I1{});
+      pstep(I1{}, I0{});
+      pstep(I2{}, I1{});
+    }
+    if (kt < nk) pstep(I0{}, I0{});
+    if (kt + 1 < nk) pstep(I1{}, I1{});
+    if (kt + 2 < nk) pstep(I2{}, I0{});
+    if (kt + 3 < nk) pstep(I0{}, I1{});
+    if (kt + 4 < nk) pstep(I1{}, I0{});
+  } else {
   issue(0);
   issue(1);
   // one K-step on ring slot SLOT (= kt % 3).  The loop is unrolled by the ring length so that the
@@ -1246,6 +1298,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2))
   }
   if (kt < nk) step(S0{});
   if (kt + 1 < nk) step(S1{});
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the workgroup retires
   if (fold.flags & 4) {  // the splits meet in-launch (splitk_tree_fold)
     splitk_tree_fold<TM, 4, kThreads>(acc, slab, K, n1_0 + wm * (TBM / 2), Co, n2_0 + wn * 64, K, tile, split,
@@ -1600,6 +1653,17 @@ bool wgrad_glds_enabled() {
   return on;
 }
 
+// TONY_WGRAD_PF: 1 = the fragment-prefetch K loop of conv_wgrad_glds_kernel (PF), 0 = the plain one;
+// tony_wgrad_pf(-1) reads it, 0 / 1 sets it (tests)
+std::atomic<int>& wgrad_pf_flag() {
+  static std::atomic<int> f{[] {
+    const char* e = getenv("TONY_WGRAD_PF");
+    return (e != nullptr && e[0] == '1') ? 1 : 0;
+  }()};
+  return f;
+}
+bool wgrad_pf_enabled() { return wgrad_pf_flag().load(std::memory_order_relaxed) != 0; }
+
 bool wgrad_inc_enabled() {  // TONY_WGRAD_INC=0: the general row walk (A/B measurements)
   static const bool on = [] {
     const char* e = getenv("TONY_WGRAD_INC");
@@ -1660,7 +1724,10 @@ int launch_wgrad(const void* dy, int64_t lddy, const Gather& g, float* dw, float
   const bool inc = wgrad_inc_step(g, M, &ws);
   const auto* dyp = static_cast<const uint16_t*>(dy);
   if (TBM >= 96 && slab != nullptr && wgrad_glds_enabled()) {
-    if (inc)
+    if (inc && wgrad_pf_enabled())
+      conv_wgrad_glds_kernel<TBM, true, true><<<static_cast<int>(grid), kThreads, 0, stream>>>(
+          dyp, lddy, g, M, Co, tiles_n2, ntiles, rows, slab, fold, ws, pp);
+    else if (inc)
       conv_wgrad_glds_kernel<TBM, true><<<static_cast<int>(grid), kThreads, 0, stream>>>(
           dyp, lddy, g, M, Co, tiles_n2, ntiles, rows, slab, fold, ws, pp);
     else
@@ -1848,6 +1915,12 @@ static std::atomic<int>& dgrad_one_launch_flag() {
   return on;
 }
 static bool dgrad_one_launch() { return dgrad_one_launch_flag().load(std::memory_order_relaxed) != 0; }
+TONY_API int tony_wgrad_pf(int on) {
+  const int prev = wgrad_pf_flag().load();
+  if (on >= 0) wgrad_pf_flag().store(on ? 1 : 0);
+  return prev;
+}
+
 TONY_API int tony_dgrad_one_launch(int on) {
   const int prev = dgrad_one_launch_flag().load();
   if (on >= 0) dgrad_one_launch_flag().store(on ? 1 : 0);
