@@ -26,7 +26,7 @@ def _port():
 def test_x3_inception_through_ps_matches_reference(mode, world, monkeypatch):
     import x3_ps_worker as W
 
-    monkeypatch.setenv("TONY_PS_SPIN_S", "120")
+    monkeypatch.setenv("TONY_PS_SPIN_S", "300")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()

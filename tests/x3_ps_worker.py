@@ -61,6 +61,7 @@ def run(rank, world, port, q, mode):
             params = list(ref.parameters())
             w0 = [p.detach().clone() for p in params]
             vel = [torch.zeros_like(p) for p in params]
+            drs = []
             for _ in range(STEPS):
                 gsum = [torch.zeros_like(p) for p in params]
                 for w in range(nw):
@@ -75,9 +76,11 @@ def run(rank, world, port, q, mode):
                     for p, v, s_ in zip(params, vel, gsum):
                         v.mul_(MU).add_(s_ / nw + WD * p)
                         p.add_(v, alpha=-LR)
-            dr = torch.cat([(a.detach() - b).flatten() for a, b in zip(params, w0)])
+                drs.append(torch.cat([(a.detach() - b).flatten() for a, b in zip(params, w0)]))
+            dr = drs[-1]
             del ref, params, vel, gsum
             torch.cuda.synchronize()
+        dist.barrier()  # every rank starts the parameter server together (the reference took minutes)
         model = _model(dev)
         ps = ParameterServer(model, optimizer="sgd", lr=LR, momentum=MU, weight_decay=WD, mode=mode, ps_ranks=(0,),
                              dtype=torch.float32, device=dev, wire_dtype=torch.float32, bucket_mb=8)
@@ -86,10 +89,13 @@ def run(rank, world, port, q, mode):
         if ps.is_worker:
             trainer = Trainer(model, ps, _loss, use_graph=False)
             x, y = _data(workers.index(rank), dev)
+            dus = []
             for i in range(STEPS):
                 loss = trainer.step(x, y)
                 torch.cuda.synchronize()
                 _say(rank, f"PS step {i} done")
+                if rank == first:
+                    dus.append(torch.cat([(p.detach() - b).flatten() for p, b in zip(model.parameters(), w0)]))
             res["loss_finite"] = bool(torch.isfinite(loss).item())
         else:
             for i in range(STEPS):
@@ -100,6 +106,16 @@ def run(rank, world, port, q, mode):
         if rank == first:
             du = torch.cat([(p.detach() - b).flatten() for p, b in zip(model.parameters(), w0)])
             res["update_rel_err"] = float((du - dr).norm() / dr.norm())
+            res["update_rel_err_per_step"] = [float((u - r).norm() / r.norm()) for u, r in zip(dus, drs)]
+            # which parameters disagree most after the first step (diagnosis)
+            worst, off = [], 0
+            for (name, p_), b in zip(model.named_parameters(), w0):
+                k = p_.numel()
+                u, r = dus[0][off:off + k], drs[0][off:off + k]
+                worst.append((float((u - r).norm() / (r.norm() + 1e-30)), name, k))
+                off += k
+            res["worst_params_step0"] = sorted(worst, reverse=True)[:6]
+            _say(rank, f"result: {res}")
             res["update_norm"] = float(dr.norm())
             res["workers"] = len(workers)
         if ps.plane is not None:

@@ -36,8 +36,10 @@ GC_EVERY = int(os.environ.get("TONY_GC_EVERY", "200"))
 # from C++ onto the eager step's streams (ops/plan.py, csrc/plan.hip); "graph" instantiates it and
 # calls hipGraphLaunch.  A graph the native replay cannot issue falls back to "graph".
 REPLAY = os.environ.get("TONY_REPLAY", "plan").lower()
-# weight-gradient ops per side-stream fork inside a captured step (eager issue uses streams.BATCH)
-PLAN_WGRAD_BATCH = int(os.environ.get("TONY_PLAN_WGRAD_BATCH", "1"))
+# weight-gradient ops per side-stream fork inside a captured step (eager issue uses streams.BATCH).  4 since
+# round 6: with the lean conv kernels one op per fork left the plan 0.8 ms behind eager (14.19 vs 13.40 ms);
+# 2 / 3 / 4 ops per fork 13.63 / 13.61 / 13.56 ms (profiles/r6_plan_wgrad_batch.log)
+PLAN_WGRAD_BATCH = int(os.environ.get("TONY_PLAN_WGRAD_BATCH", "4"))
 
 # Opt-in: measured slower on MI355X (bench 16.9 vs 15.7 ms/step; the compute queue's gaps grew from
 # 3.3 to 5.9 ms under rocprofv3), so the step stays on the caller's stream by default.
@@ -285,9 +287,9 @@ class Trainer:
                 eng.end_capture()
             return out
 
-        # weight gradients join the side stream one op per fork inside the capture: eager issue batches
-        # them in pairs to save host time (streams.BATCH), which a replay does not pay, and each op then
-        # waits only for its own dZ (plan 13.61 vs 13.68 ms/step, profiles/r4_ab_plan_wgrad_batch.log)
+        # weight gradients join the side stream PLAN_WGRAD_BATCH ops per fork inside the capture (round 4
+        # measured one per fork best, 13.61 vs 13.68 ms, profiles/r4_ab_plan_wgrad_batch.log; with round 6's
+        # kernels four per fork: 13.56 vs 14.19 ms, profiles/r6_plan_wgrad_batch.log)
         batch, streams.BATCH = streams.BATCH, PLAN_WGRAD_BATCH
         try:
             with torch.cuda.graph(g):
