@@ -44,6 +44,11 @@ def _say(rank, msg):
 
 def run(rank, world, port, q, mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if os.environ.get("X3PS_DUMP_S"):  # diagnostics: every rank's Python stack after that many seconds
+        import faulthandler
+        import sys
+
+        faulthandler.dump_traceback_later(int(os.environ["X3PS_DUMP_S"]), repeat=False, file=sys.stderr)
     res = {}
     try:
         dev, _ = gpu_ranks.init(rank, world)
@@ -56,29 +61,38 @@ def run(rank, world, port, q, mode):
         nw = world if mode == "colocated" else world - 1
         if rank == first:
             # single-process reference first (no parameter server attached in this process yet): same init,
-            # each worker's batch through a fresh x3 model, mean gradient, fp32 SGD-momentum + L2
-            ref = _model(dev)
-            params = list(ref.parameters())
-            w0 = [p.detach().clone() for p in params]
-            vel = [torch.zeros_like(p) for p in params]
-            drs = []
-            for _ in range(STEPS):
-                gsum = [torch.zeros_like(p) for p in params]
-                for w in range(nw):
-                    for p in params:
-                        p.grad = None
-                    xw, yw = _data(w, dev)
-                    _loss(ref(xw), yw).backward()
-                    _say(rank, f"reference: worker {w}'s batch done")
-                    for s_, p in zip(gsum, params):
-                        s_ += p.grad
-                with torch.no_grad():
-                    for p, v, s_ in zip(params, vel, gsum):
-                        v.mul_(MU).add_(s_ / nw + WD * p)
-                        p.add_(v, alpha=-LR)
-                drs.append(torch.cat([(a.detach() - b).flatten() for a, b in zip(params, w0)]))
+            # each worker's batch through a fresh x3 model, mean gradient, fp32 SGD-momentum + L2 -- run
+            # TWICE: the two runs differ by the network's own sensitivity (fp32 atomics in the BN statistics
+            # flip ReLU mask bits, and 95 BN layers at batch 2 amplify that; tools/x3_layer_check.py shows
+            # stock fp32 PyTorch has the same per-layer floor), which is the yardstick for the PS run
+            trajs = []
+            for _ in range(2):
+                ref = _model(dev)
+                params = list(ref.parameters())
+                w0 = [p.detach().clone() for p in params]
+                vel = [torch.zeros_like(p) for p in params]
+                drs = []
+                for _ in range(STEPS):
+                    gsum = [torch.zeros_like(p) for p in params]
+                    for w in range(nw):
+                        for p in params:
+                            p.grad = None
+                        xw, yw = _data(w, dev)
+                        _loss(ref(xw), yw).backward()
+                        _say(rank, f"reference: worker {w}'s batch done")
+                        for s_, p in zip(gsum, params):
+                            s_ += p.grad
+                    with torch.no_grad():
+                        for p, v, s_ in zip(params, vel, gsum):
+                            v.mul_(MU).add_(s_ / nw + WD * p)
+                            p.add_(v, alpha=-LR)
+                    drs.append(torch.cat([(a.detach() - b).flatten() for a, b in zip(params, w0)]))
+                trajs.append(drs)
+                del ref, params, vel, gsum
+            drs = trajs[0]
             dr = drs[-1]
-            del ref, params, vel, gsum
+            res["ref_spread_per_step"] = [float((u - r).norm() / r.norm()) for u, r in zip(trajs[1], drs)]
+            del trajs
             torch.cuda.synchronize()
         dist.barrier()  # every rank starts the parameter server together (the reference took minutes)
         model = _model(dev)
@@ -87,7 +101,11 @@ def run(rank, world, port, q, mode):
         workers = list(ps.worker_ranks)
         assert workers[0] == first and len(workers) == nw, (workers, first, nw)
         if ps.is_worker:
-            trainer = Trainer(model, ps, _loss, use_graph=False)
+            # (diagnostic switches for the dedicated rehearsal: X3PS_OVERLAP=0 pushes after backward,
+            # X3PS_BRANCH=0 keeps the blocks' branches on one stream)
+            trainer = Trainer(model, ps, _loss, use_graph=False,
+                              overlap_comm=os.environ.get("X3PS_OVERLAP", "1") != "0",
+                              branch_streams=os.environ.get("X3PS_BRANCH", "1") != "0")
             x, y = _data(workers.index(rank), dev)
             dus = []
             for i in range(STEPS):

@@ -282,25 +282,43 @@ struct LandEntry {
   int32_t bucket;
 };
 
+// A bounded persistent grid (<= one workgroup per CU) walks the (bucket, chunk) pairs in table order --
+// the order the ps applies them -- waiting for each chunk's landed flag and copying it.  One workgroup per
+// chunk (the first form) parked up to nb x 256 spinning workgroups on the GPU: on a GPU shared by a ps
+// and workers (the one-GPU rehearsal, tony.amd.ps-share-gpu) two workers' landings of the 12 fp32
+// Inception buckets filled every workgroup slot and the ps's apply never got a CU (deadlock until the
+// wait budget ran out).  Spinning workgroups are now bounded by the grid, whatever the bucket count.
 template <bool PARAM_BF16>
-__global__ __launch_bounds__(kThreads) void ps_land_kernel(const LandEntry* __restrict__ tab, uint8_t* win,
+__global__ __launch_bounds__(kThreads) void ps_land_kernel(const LandEntry* __restrict__ tab, int nb, uint8_t* win,
                                                            const uint8_t* landing, uint8_t* dst, uint32_t value,
                                                            uint64_t budget) {
-  const LandEntry e = tab[blockIdx.y];
-  if (static_cast<int>(blockIdx.x) >= e.blocks) return;
   __shared__ int ok;
   const uint64_t t0 = wall_clock64();
   int* err = reinterpret_cast<int*>(win + kErrOff);
-  if (threadIdx.x == 0) ok = !poisoned(err) && wait_flag(landed(win, e.bucket) + blockIdx.x, value, t0, budget, err);
+  if (threadIdx.x == 0) ok = !poisoned(err);
   __syncthreads();
   if (!ok) return;
-  __atomic_thread_fence(__ATOMIC_ACQUIRE);
-  int64_t lo, hi;
-  chunk_of(e.n, blockIdx.x, e.blocks, &lo, &hi);
+  const int64_t G = gridDim.x;
+  int64_t base = 0;  // pairs before entry y
   constexpr int esz = PARAM_BF16 ? 2 : 4;
-  const int64_t b0 = (e.lo + lo) * esz, b1 = (e.lo + hi) * esz;  // 16-byte multiples (lo, hi: x8)
-  for (int64_t o = b0 + threadIdx.x * 16; o < b1; o += kThreads * 16)
-    *reinterpret_cast<uint4*>(dst + o) = *reinterpret_cast<const uint4*>(landing + o);
+  for (int y = 0; y < nb; ++y) {
+    const LandEntry e = tab[y];
+    const int64_t p0 = base + ((static_cast<int64_t>(blockIdx.x) - base) % G + G) % G;  // first pair of ours
+    for (int64_t p = p0; p < base + e.blocks; p += G) {
+      const int c = static_cast<int>(p - base);
+      if (threadIdx.x == 0) ok = wait_flag(landed(win, e.bucket) + c, value, t0, budget, err);
+      __syncthreads();
+      if (!ok) return;  // (uniform: every thread read ok after the barrier)
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);
+      int64_t lo, hi;
+      chunk_of(e.n, c, e.blocks, &lo, &hi);
+      const int64_t b0 = (e.lo + lo) * esz, b1 = (e.lo + hi) * esz;  // 16-byte multiples (lo, hi: x8)
+      for (int64_t o = b0 + threadIdx.x * 16; o < b1; o += kThreads * 16)
+        *reinterpret_cast<uint4*>(dst + o) = *reinterpret_cast<const uint4*>(landing + o);
+      __syncthreads();  // thread 0 rewrites ok for the next pair only after every thread tested this one
+    }
+    base += e.blocks;
+  }
 }
 
 uint64_t budget_ticks(double seconds) {
@@ -515,14 +533,19 @@ TONY_API int tony_ps_land(void* window, const void* table, int nb, void* params,
       (reinterpret_cast<uintptr_t>(params) & 15))
     return -1;
   uint8_t* win = static_cast<uint8_t*>(window);
-  const dim3 grid(kMaxBlocks, nb);
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                              hipSuccess || cus <= 0)
+    cus = 64;
+  // <= one workgroup per CU (see ps_land_kernel), never more than the pairs can use
+  const int grid = std::min<int>(cus, nb * kMaxBlocks);
   const uint64_t budget = budget_ticks(budget_s);
   if (param_bf16)
-    ps_land_kernel<true><<<grid, kThreads, 0, stream>>>(static_cast<const LandEntry*>(table), win, win + kHeader,
-                                                        static_cast<uint8_t*>(params), value, budget);
+    ps_land_kernel<true><<<grid, kThreads, 0, stream>>>(static_cast<const LandEntry*>(table), nb, win,
+                                                        win + kHeader, static_cast<uint8_t*>(params), value, budget);
   else
-    ps_land_kernel<false><<<grid, kThreads, 0, stream>>>(static_cast<const LandEntry*>(table), win, win + kHeader,
-                                                         static_cast<uint8_t*>(params), value, budget);
+    ps_land_kernel<false><<<grid, kThreads, 0, stream>>>(static_cast<const LandEntry*>(table), nb, win,
+                                                         win + kHeader, static_cast<uint8_t*>(params), value, budget);
   TONY_LAUNCH_CHECK();
   return 0;
 }

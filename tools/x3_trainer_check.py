@@ -17,6 +17,7 @@ sys.path.insert(0, ".")
 
 B, CLASSES = 2, 1000
 LR, MU, WD = 0.1, 0.9, 4e-5
+PRECISION = "fp32"
 
 
 def say(msg):
@@ -34,7 +35,7 @@ def model(dev):
     from tony_amd.models.inception_v3 import inception_v3
 
     torch.manual_seed(0)
-    m = inception_v3(num_classes=CLASSES, precision="fp32", seed=0).to(dev).to(memory_format=torch.channels_last)
+    m = inception_v3(num_classes=CLASSES, precision=PRECISION, seed=0).to(dev).to(memory_format=torch.channels_last)
     m.dropout.p = 0.0
     return m.train()
 
@@ -78,7 +79,11 @@ def compare(tag, a, b, top=6):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--precision", default="fp32")
+    ap.add_argument("--det-only", action="store_true", help="only the plain-backward-twice comparison")
     a = ap.parse_args()
+    global PRECISION
+    PRECISION = a.precision
     dev = torch.device("cuda", 0)
     x, y = data(dev)
     ref = model(dev)
@@ -87,6 +92,20 @@ def main():
     say("reference backward 1 done")
     g2 = grads(ref, x, y)
     compare("plain backward twice", g2, g1)
+    # backward order (the top of the network first): where the two runs start to disagree
+    names = list(g1)[::-1]
+    shown = 0
+    for n in names:
+        e = ((g2[n] - g1[n]).double().norm() / (g1[n].double().norm() + 1e-30)).item()
+        if e > 1e-4 or shown < 12:
+            say(f"   backward order: {e:.3e} {n}")
+            shown += 1
+        if shown >= 40:
+            break
+    g2b = grads(ref, x, y)
+    compare("plain backward 3 vs 2 (both after the autotuning call)", g2b, g2)
+    if a.det_only:
+        return 0
 
     from contextlib import contextmanager
 
