@@ -30,6 +30,18 @@ def _port():
 def test_x3_inception_through_ps_matches_reference(mode, world, monkeypatch):
     import x3_ps_worker as W
 
+    from gpu_ranks import distinct
+
+    if mode == "dedicated" and not distinct(world):
+        # three processes on one GPU: the ps's apply kernels and the workers' landings wait on the GPU
+        # for their peers (the xGMI plane keeps the host out of the loop), and with three processes' queues
+        # on one device the second worker's queue was observed to make no progress at all -- not even
+        # after its peers' wait budgets (TONY_PS_SPIN_S) had expired and their kernels had returned
+        # (profiles/r6_x3_ps_dedicated_shared_gpu.log: a Python stack dump holds it in
+        # torch.cuda.synchronize after step 0 or 1).  One GPU per rank (the 8-GPU node) has no such
+        # sharing; tests/test_ps_plane_gpu.py rehearses the plane's protocol on one GPU with a small net.
+        pytest.skip("the dedicated x3 rehearsal needs one GPU per rank (3 processes sharing one GPU starve)")
+
     monkeypatch.setenv("TONY_PS_SPIN_S", os.environ.get("TONY_PS_SPIN_S", "300"))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
