@@ -185,3 +185,38 @@ def kv_bulk_rank(role, index, num_servers, num_workers, port, kind, steps, keys,
            "v0": vals[0][:: n // 64].cpu(), "vlast": vals[-1][:: n // 64].cpu(), "n": n}
     store.close()
     return res
+
+
+def kv_pullpull_rank(role, index, num_servers, num_workers, port, rounds):
+    """dist_async on the GPU plane: worker 0 only pulls, twice in a row per round (no push of its own in
+    between -- the pull-pull case of ADVICE r5), while worker 1 keeps pushing.  Every pulled tensor must be
+    one consistent version -w_k = -0.25 k ramp (lr 0.5 x rescale 1/2 per push): a copy-out that overlapped
+    the server's next reply would mix two k across the tensor."""
+    os.environ.update(DMLC_ROLE=role, DMLC_NUM_SERVER=str(num_servers), DMLC_NUM_WORKER=str(num_workers),
+                      DMLC_PS_ROOT_URI="127.0.0.1", DMLC_PS_ROOT_PORT=str(port), TASK_INDEX=str(index))
+    import tony_amd.kv as kv
+
+    if kv.run_role():
+        return {"role": role}
+    store = kv.create("dist_async")
+    n = 1 << 20  # 4 MiB: 1024 flag adds per copy
+    store.init("big", torch.zeros(n, device="cuda"))
+    store.set_optimizer(kv.create_optimizer("sgd", learning_rate=0.5, rescale_grad=1.0 / num_workers))
+    ramp = (torch.arange(n, dtype=torch.float32, device="cuda") + 1) / n
+    torn, ks = 0, []
+    if store.rank == 1:
+        for _ in range(rounds):
+            store.push("big", ramp)
+    else:
+        outs = [torch.empty(n, device="cuda") for _ in range(2)]
+        for _ in range(rounds):
+            store.pull("big", out=outs[0])
+            store.pull("big", out=outs[1])
+            for o in outs:
+                k = torch.round(-o / (0.25 * ramp))
+                ks.append(int(k[0].item()))
+                torn += int((k != k[0]).any().item())
+    res = {"role": role, "rank": store.rank, "torn": torn, "ks": ks,
+           "plane_ops": list(getattr(store, "plane_ops", [0, 0]))}
+    store.close()
+    return res

@@ -71,3 +71,19 @@ def test_kvstore_plane_bulk_keys_sync_timed():
         print(f"worker {o['rank']}: round of {keys} x {mb} MB push + pull: {steady * 1e3:.2f} ms "
               f"({steady * 1e3 / keys:.3f} ms per key push+pull, {2 * keys * mb / 1024 / steady:.1f} GB/s "
               f"moved per worker); all rounds {[round(t * 1e3, 2) for t in o['times']]}")
+
+
+def test_kvstore_plane_async_pull_pull_never_torn():
+    """Two plane pulls of one key in a row with no push between them: the second reply must
+    not land in the landing area while the first is still being copied out -- worker 1 pushes all along,
+    and every tensor worker 0 pulls is one whole version of the key."""
+    port, rounds = _port(), 12
+    args = [("scheduler", 0, 1, 2, port, rounds), ("server", 0, 1, 2, port, rounds),
+            ("worker", 0, 1, 2, port, rounds), ("worker", 1, 1, 2, port, rounds)]
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(len(args)) as pool:
+        outs = [r.get(110) for r in [pool.apply_async(W.kv_pullpull_rank, a) for a in args]]
+    puller = [o for o in outs if o.get("rank") == 0][0]
+    assert puller["torn"] == 0, puller
+    assert len(puller["ks"]) == 2 * rounds and puller["ks"] == sorted(puller["ks"]), puller["ks"]
+    assert puller["plane_ops"][1] == 2 * rounds, puller["plane_ops"]
