@@ -62,9 +62,10 @@ def run(rank, world, port, q, mode):
         if rank == first:
             # single-process reference first (no parameter server attached in this process yet): same init,
             # each worker's batch through a fresh x3 model, mean gradient, fp32 SGD-momentum + L2 -- run
-            # TWICE: the two runs differ by the network's own sensitivity (fp32 atomics in the BN statistics
-            # flip ReLU mask bits, and 95 BN layers at batch 2 amplify that; tools/x3_layer_check.py shows
-            # stock fp32 PyTorch has the same per-layer floor), which is the yardstick for the PS run
+            # TWICE: the two runs differ by the network's own sensitivity (the order of the fp32 atomics in
+            # the BN statistics moves y by ~1e-7, a ReLU mask bit flips wherever |y| is that small, and 95 BN
+            # layers at batch 2 amplify each flip -- tools/x3_layer_check.py shows one layer's flips at the
+            # x3 forward precision), which is the yardstick for the PS run
             trajs = []
             for _ in range(2):
                 ref = _model(dev)
