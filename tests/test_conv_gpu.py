@@ -793,3 +793,56 @@ def test_wgrad_fragment_prefetch_matches_plain(cuda, shape):
     wr = torch.zeros_like(wt, requires_grad=True)
     torch.nn.functional.conv2d(xr, wr, None, 1, p).backward(dy.float())
     assert _rel(outs[1], wr.grad) < 1e-2
+
+
+BAND_SHAPES = [(4, 192, 17, 17, 192, (1, 7), (0, 3)), (4, 160, 17, 17, 192, (7, 1), (3, 0)),
+               (3, 128, 17, 17, 160, (1, 7), (0, 3)), (5, 384, 8, 8, 384, (1, 3), (0, 1)),
+               (5, 384, 8, 8, 384, (3, 1), (1, 0)), (2, 192, 11, 13, 128, (3, 1), (1, 0)),
+               (2, 64, 9, 20, 96, (1, 7), (0, 3)), (3, 96, 17, 17, 64, (1, 7), (0, 0))]
+
+
+@pytest.mark.parametrize("shape", BAND_SHAPES, ids=[f"{s[1]}->{s[4]}_{s[2]}x{s[3]}k{s[5][0]}{s[5][1]}p{s[6][0]}{s[6][1]}"
+                                                    for s in BAND_SHAPES])
+def test_conv_band_variant(cuda, shape):
+    """csrc/band.hip (tile variant 40): the 1 x T / T x 1 stride-1 convs on whole-line halo tiles --
+    forward with BN statistics and backward-data against fp32 PyTorch; N not a multiple of the column tile,
+    partial last line tiles, "valid" padding; other shapes are declined (-3)."""
+    from tony_amd.ops import _lib
+    from tony_amd.ops.conv import conv_dgrad, conv_fwd
+
+    n, c, h, w, co, (r, s), p = shape
+    torch.manual_seed(c + co)
+    x = _nhwc(torch.randn(n, c, h, w, device=cuda)).to(torch.bfloat16)
+    wt = _nhwc(torch.randn(co, c, r, s, device=cuda) / (c * r * s) ** 0.5).to(torch.bfloat16)
+    stats = torch.zeros(_lib.stat_floats(co), device=cuda)
+    y = conv_fwd(x, wt, 1, p, stats, vflags=40 << 8)
+    xr = x.float().requires_grad_(True)
+    ref = torch.nn.functional.conv2d(xr, wt.float(), None, 1, p)
+    assert _rel(y, ref) < 1e-2
+    st = _lib.fold_stats(stats, co)
+    torch.testing.assert_close(st[:co], ref.detach().sum((0, 2, 3)), rtol=2e-3, atol=ref.numel() / co * 2e-4)
+    torch.testing.assert_close(st[co:], (ref.detach() ** 2).sum((0, 2, 3)), rtol=2e-3, atol=1e-1)
+    dy = _nhwc(torch.randn_like(ref)).to(torch.bfloat16)
+    ref.backward(dy.float())
+    if p[0] * 2 + 1 == r and p[1] * 2 + 1 == s:  # "same" padding: the dgrad is a band conv too
+        dx = conv_dgrad(dy, wt, x.shape, 1, p, vflags=40 << 8)
+        assert _rel(dx, xr.grad) < 1e-2
+
+
+def test_conv_band_declines_other_shapes(cuda):
+    """A 3x3 conv, a strided 1x7 and an fp32 (x3) output are not band shapes: -3, nothing launched."""
+    from tony_amd.ops import _lib
+
+    L = _lib.lib()
+    st = _lib.stream_ptr(torch.device(cuda))
+    x = _nhwc(torch.randn(2, 64, 17, 17, device=cuda)).to(torch.bfloat16)
+    wk = torch.randn(64, 3, 3, 64, device=cuda).to(torch.bfloat16)
+    y = torch.empty(2 * 17 * 17 * 64, device=cuda, dtype=torch.float32)
+    assert L.tony_conv_fwd(x.data_ptr(), 2, 17, 17, 64, 64, wk.data_ptr(), 64, 3, 3, 1, 1, 1, 1, y.data_ptr(), 17,
+                           17, 64, 40 << 8, None, 0, st) == -3
+    w7 = torch.randn(64, 1, 7, 64, device=cuda).to(torch.bfloat16)
+    assert L.tony_conv_fwd(x.data_ptr(), 2, 17, 17, 64, 64, w7.data_ptr(), 64, 1, 7, 2, 2, 0, 3, y.data_ptr(), 9,
+                           9, 64, 40 << 8, None, 0, st) == -3
+    assert L.tony_conv_fwd(x.data_ptr(), 2, 17, 17, 64, 64, w7.data_ptr(), 64, 1, 7, 1, 1, 0, 3, y.data_ptr(), 17,
+                           17, 64, (40 << 8) | 8, None, 0, st) == -3
+    torch.cuda.synchronize()

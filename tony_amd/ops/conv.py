@@ -160,7 +160,7 @@ def conv_fwd(x: torch.Tensor, weight: torch.Tensor, stride=1, padding=0, stats: 
         vflags = tune.cached(key)
         if vflags is None:  # first call of this shape: time the variants (statistics into a scratch buffer)
             scratch = torch.zeros(_lib.stat_floats(co), device=x.device) if stats is not None else None
-            vflags = tune.pick(key, lambda vf: launch(vf, scratch))
+            vflags = tune.pick(key, lambda vf: launch(vf, scratch), tune.CONV_VARIANTS)
         if (HOST_MEMO and key0[1] == x.stride() and x.dtype == _BF16 and weight.dtype == _BF16
                 and not torch.cuda.is_current_stream_capturing()):
             _FWD_PLAN[key0] = (n, h, w, C, ldx, co, r, s, sh, sw, ph, pw, oh, ow, vflags)
@@ -256,7 +256,7 @@ def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, paddin
         name = "tony_conv_dgrad"
     else:
         def launch(vf, br=None):
-            if (vf >> 8) & 0xff in (9, 10):  # the halo / direct tile variants are stride-1 only
+            if (vf >> 8) & 0xff in (9, 10, tune.BAND_CODE):  # the halo / direct / band variants are stride-1 only
                 return -3
             if not STRIDED_GLDS and (vf >> 8) & 0xff >= 11:  # A/B: the register-staged NT kernel only
                 return -3
@@ -267,7 +267,7 @@ def conv_dgrad(dy: torch.Tensor, weight: torch.Tensor, x_shape, stride=1, paddin
 
     # variants are timed without the fused reduction (it must run exactly once)
     vf = vflags if vflags is not None else tune.pick(("conv_dgrad", tuple(dy.shape), lddy, tuple(weight.shape),
-                                                         (sh, sw), (ph, pw)), launch)
+                                                         (sh, sw), (ph, pw)), launch, tune.CONV_VARIANTS)
     if accum is not None and bnr is None and _accum_ok(accum, x_shape):
         plain = dx
         dx = accum

@@ -25,6 +25,12 @@ using namespace tony;
 using namespace tony::mfma;
 using namespace tony::glds;
 
+namespace tony {
+// band.hip: the 1 x T / T x 1 stride-1 convs (forward / backward-data) on whole-line halo tiles
+int run_band(const Gather& g, const void* B, void* C, int64_t ldc, int64_t N, int epi, float* st, int64_t sstride,
+             hipStream_t stream);
+}  // namespace tony
+
 namespace {
 
 __device__ __forceinline__ uint4 gather16(const Gather& g, const RowState& rs, const TapPos& t, int toff) {
@@ -518,6 +524,7 @@ int run_halo(const Gather& g, const void* B, void* C, int64_t ldc, int64_t N, in
 //     no LDS staging of the output and no barrier in the epilogue,
 //   * keeps the BN statistics in registers over all its tiles (one sharded atomic per channel).
 constexpr int kDirectVariant = 10;  // tile-variant id the autotuner uses for this path (ops/tune.py)
+constexpr int kBandVariant = 40;    // band.hip run_band (ops/tune.py BAND_CODE)
 constexpr int kDirH = 8;
 
 template <int CS, int CO, int TW>
@@ -786,6 +793,7 @@ int run_nt(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M, int6
   if (((flags >> 16) & 15) && !(v >= kGldsFirst && v < kGldsFirst + kNumGlds)) return -3;  // stream-K: LDS-DMA only
   if (((epi & 24) && v == kHaloVariant) || ((epi & 16) && v == kDirectVariant)) return -3;
   if (v == kHaloVariant) return bph.bnr.z != nullptr ? -3 : run_halo(g, B, C, ldc, N, epi, st, sstride, stream);
+  if (v == kBandVariant) return bph.bnr.z != nullptr ? -3 : run_band(g, B, C, ldc, N, epi, st, sstride, stream);
   if (v == kDirectVariant) return run_direct(g, B, C, ldc, N, epi, st, sstride, stream, bph.bnr);
   if (v >= kGldsFirst && v < kGldsFirst + kNumGlds)
     return bph.bnr.z != nullptr ? -3
@@ -814,6 +822,7 @@ int run_nt_phase(const Gather& g, const void* B, void* C, int64_t ldc, int64_t M
   if (v >= kGldsFirst)
     return run_glds(g, B, static_cast<int64_t>(ph.R) * ph.S * g.Cs, C, ldc, M, N, epi, nullptr, 0, v, stream, ph.rows,
                     BTaps{ph.r0, ph.s0, ph.tsy, ph.tsx, ph.S});
+  if (v == kBandVariant) return -3;  // (stride 1 only)
   if (v == kHaloVariant || v == kDirectVariant || v >= kNumNtVariants) return -1;
   if (v == 0) {
     const int64_t bn = pick_bn(N, 192);

@@ -38,6 +38,13 @@ if os.environ.get("TONY_CONV_OCC", "1") != "0" and os.environ.get("TONY_CONV_GLD
 # of 6-25 tiles).  TONY_STREAMK=1,2,3: the grid multiples offered to the tuner.
 STREAM_MS = tuple(int(x) for x in os.environ.get("TONY_STREAMK", "").split(",") if x.strip() not in ("", "0"))
 NT_VARIANTS = _BASE + tuple(v + 256 * m for m in STREAM_MS for v in _BASE if v >= 11)
+# 40: csrc/band.hip -- the 1 x T / T x 1 stride-1 convs (forward, backward-data) on whole-line halo tiles (it
+# declines every other shape).  Opt-in (TONY_CONV_BAND=1 offers it to the conv tuner): measured 0.68-0.85x of
+# the best LDS-DMA tile on every Inception 1-D shape (profiles/r6_band_bench.log) -- the halo cuts the A
+# re-gather but every tile still streams the 7-tap filter slice, and the register-staged prefetch (192
+# VGPRs, one workgroup per CU) leaves the CU waiting on each chunk's loads
+BAND_CODE = 40
+CONV_VARIANTS = NT_VARIANTS + ((BAND_CODE,) if os.environ.get("TONY_CONV_BAND", "0") == "1" else ())
 # the x3 (fp32) convs: their K is three planes deep, so a tile's K loop is 3x the bf16 one and the fold's
 # partial tiles cost relatively less -- stream-K over one CU-grid is offered there (fp32 step A/B
 # 37.64 vs 37.95 ms, profiles/r5_x3_wgrad_fused.md); TONY_X3_STREAMK=0: plain launches only
