@@ -136,8 +136,10 @@ def active() -> bool:
 # current stream's position at flush time -- later than each op needs, never earlier.
 # Measured: 1 (16.34 ms) beat 4 (16.77 ms) while the step was GPU-bound at 16 ms (round 1); with the
 # GPU at 14 ms the host issue cost matters: 2 measured 13.90 / 13.89 ms/step vs 14.1-15.1 at 1
-# (profiles/r2s3_host_levers_ab.log)
-BATCH = int(os.environ.get("TONY_WGRAD_BATCH", "2"))
+# (profiles/r2s3_host_levers_ab.log).  Round 6 (lean conv kernels, GPU at 13.3-13.4 ms, eager host 11.4-15 ms):
+# 3 measured 13.265 ms/step mean over 4 repetitions vs 13.755 at 2 (whose host went bound in one of them), GPU
+# time with the host ahead 13.36 vs 13.40 (profiles/r6_ab_wgrad_batch_eager.log)
+BATCH = int(os.environ.get("TONY_WGRAD_BATCH", "3"))
 _pending: List[tuple] = []  # (fn, the stream that queued it)
 # ...except for big operands: a batch forks from the current stream when it is flushed, so a pending
 # op waits for whatever the compute stream was given in between (the next layer's BN backward and
