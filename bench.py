@@ -16,7 +16,8 @@ One process per GPU (torch.distributed.run, RCCL over xGMI).  Two PS topologies:
     straight into the ps GPU's receive window as backward produces it, the ps applies the fused
     optimizer as the rows land and stores the new variables straight into every worker's landing
     window (TONY_PS_PLANE=rccl: reduce / apply / broadcast per bucket instead).  Images/sec counts
-    the N-1 workers' images only.
+    the N-1 workers' images only.  ``--ps-async``: TF's default asynchronous PS (each worker push
+    applied on its own as it lands; the headline and the default are synchronous).
 
 Compute is bf16 NHWC with the tony_amd HIP kernels (fused BN+ReLU, MFMA implicit-GEMM convs, fused
 heads, fused softmax-xent, fused optimizer); the step is issued eagerly (weight gradients on a side
@@ -59,6 +60,9 @@ def parse(argv=None):
     ap.add_argument("--no-graph", action="store_true", help="same as --mode eager")
     ap.add_argument("--ps-mode", default="colocated", choices=["colocated", "dedicated"],
                     help="colocated: one PS shard per GPU; dedicated: rank 0 = the ps task, the rest are workers")
+    ap.add_argument("--ps-async", action="store_true",
+                    help="--ps-mode dedicated: TF's default asynchronous PS (each worker push applied on its own on "
+                         "arrival, the reference mnist_distributed.py example's mode); the headline runs sync")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"],
                     help="compute dtype; fp32 = the reference-precision row (x3-split MFMA products, fp32 variables)")
     ap.add_argument("--grad-dtype", default=None, choices=["bf16", "fp32"],
@@ -102,6 +106,8 @@ def parse(argv=None):
     ap.add_argument("--no-bind", action="store_true",
                     help="N>1: leave CPU affinity alone (default: each rank on its GPU's NUMA node CPUs)")
     a = ap.parse_args(argv)
+    if a.ps_async and a.ps_mode != "dedicated":
+        ap.error("--ps-async needs --ps-mode dedicated (the colocated shards apply synchronously)")
     if a.batch is None:
         a.batch = {"mxnet-kv": 1024}.get(a.config, 128)
     return a
@@ -354,7 +360,9 @@ def main(argv=None):
         ps_kw["bucketed_single"] = True
     ps = ParameterServer(model, optimizer=args.optimizer, lr=0.045 if args.model == "inception_v3" else 0.1,
                          momentum=0.9, weight_decay=4e-5, mode=args.ps_mode, ps_ranks=(0,), dtype=dtype, device=dev,
-                         wire_dtype=grad_dtype, **ps_kw)
+                         wire_dtype=grad_dtype, sync=not args.ps_async, **ps_kw)
+    if args.ps_async and ps.plane is None:
+        return fail("--ps-async needs the xGMI PS data plane (GPU ranks)", 2)
     n_workers = len(ps.worker_ranks)
 
     if fused or x3:
@@ -553,7 +561,8 @@ def main(argv=None):
         if args.ps_mode == "colocated":
             par = f"ps-colocated-sharded dp{world} (1 PS shard + 1 worker per GPU, sync)"
         else:
-            par = f"ps-dedicated 1 ps + {n_workers} workers (sync, {ps.plane_kind} data plane)"
+            par = (f"ps-dedicated 1 ps + {n_workers} workers ({'sync' if ps.sync else 'async'}, {ps.plane_kind} "
+                   "data plane)")
         rec = {
             "metric": "images/sec (whole node) Inception-v3 TF-PS" if args.model == "inception_v3"
             else "images/sec (whole node) ResNet-50",
@@ -598,9 +607,12 @@ def main(argv=None):
                 "data_plane_verified": coll.data_plane_status(),
                 "dist": diag or None,
                 "ranks_host": ranks_host if world > 1 else None,
-                "ps_sync": "synchronous: every step sums all workers' gradients before the apply (TonY's "
-                           "mnist_distributed.py example trains asynchronously; a sync step does at least the same "
-                           "work, and bench.py --ps-mode dedicated / jobs/inception_ps.py --async run the async form)",
+                "ps_sync": ("synchronous: every step sums all workers' gradients before the apply (TonY's "
+                            "mnist_distributed.py example trains asynchronously; a sync step does at least the same "
+                            "work, and bench.py --ps-mode dedicated --ps-async / jobs/inception_ps.py --async run "
+                            "the async form)") if ps.sync else
+                           ("asynchronous: each worker's push is applied on its own as it lands and only that "
+                            "worker's variables are refreshed (TF's default PS mode, the reference example's)"),
                 "final_loss": round(final_loss, 4),
             },
         }

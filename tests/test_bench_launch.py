@@ -127,3 +127,14 @@ def test_rank_cpu_affinity_choice():
     unk = [GpuDevice(0, bdf="fake:00", numa_node=-1, fake=True)]
     assert rank_cpus(0, [0], unk, cpus_of_node=node.get, allowed=list(range(8))) == []
     assert rank_cpus(0, [0], devs, cpus_of_node=node.get, allowed=[100]) == []
+
+
+def test_ps_async_needs_dedicated_mode():
+    """--ps-async is the paper topology's asynchronous PS (dedicated ps rank): refused with colocated shards,
+    before any GPU call; passed through to the ranks of a self-launch."""
+    p = subprocess.run([sys.executable, BENCH, "--ps-async"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 2 and "--ps-mode dedicated" in p.stderr, p.stderr[-500:]
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "3", "--ps-mode", "dedicated", "--ps-async",
+                        "--launch-dry-run"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-500:]
+    assert "--ps-async" in json.loads(p.stdout.strip().splitlines()[-1])["self_launch"]
