@@ -105,6 +105,17 @@ def keep(*tensors) -> None:
             _keep.extend(t for t in tensors if isinstance(t, torch.Tensor))
 
 
+# TONY_MAIN_FIRST=1: ``parallel`` issues its first thunk (the block's longest chain, on the current
+# stream) before the branch thunks instead of after them.  Autograd runs backward nodes in reverse creation
+# order, so the longest chain's backward is then issued LAST: at a block input with several consumers
+# (ops/residual.py GradJoin, Inception's reduction blocks) the short branches park / accumulate their dX
+# first and the long chain adds into it as it finishes, instead of the short branches' dgrads queueing
+# behind the long chain's (profiles/r6_lean_crit_path_eager.txt: ~0.25 ms idle at Mixed_6a).  Measured
+# slower: GPU time with the host ahead 13.42-13.45 vs 13.28-13.32 ms eager, plan even
+# (profiles/r6_ab_main_first.log) -- opt-in
+MAIN_FIRST = os.environ.get("TONY_MAIN_FIRST", "0") == "1"
+
+
 def parallel(*thunks):
     """Results of the independent ``thunks``; concurrently on branch streams when branches are on."""
     if not _branches_on[0] or len(thunks) < 2:
@@ -112,15 +123,21 @@ def parallel(*thunks):
     main = current(torch.cuda.current_device())
     side = _branch_streams(main.device, len(thunks) - 1)
     outs = [None] * len(thunks)
+    if MAIN_FIRST:
+        for s in side:  # every branch starts from the current stream's position before the first thunk
+            fork(main, s)
+        outs[0] = thunks[0]()
     for i, (f, s) in enumerate(zip(thunks[1:], side), 1):
-        fork(main, s)
+        if not MAIN_FIRST:
+            fork(main, s)
         torch.cuda.set_stream(s)
         try:
             outs[i] = f()
         finally:
             torch.cuda.set_stream(main)
         _used[id(s)] = s
-    outs[0] = thunks[0]()
+    if not MAIN_FIRST:
+        outs[0] = thunks[0]()
     for s in side:
         fork(s, main)
     keep(*[o for o in outs if isinstance(o, torch.Tensor)])
