@@ -98,7 +98,8 @@ def run(rank, world, port, q, mode):
         dist.barrier()  # every rank starts the parameter server together (the reference took minutes)
         model = _model(dev)
         ps = ParameterServer(model, optimizer="sgd", lr=LR, momentum=MU, weight_decay=WD, mode=mode, ps_ranks=(0,),
-                             dtype=torch.float32, device=dev, wire_dtype=torch.float32, bucket_mb=8)
+                             dtype=torch.float32, device=dev, wire_dtype=torch.float32,
+                             bucket_mb=float(os.environ.get("X3PS_BUCKET_MB", "8")))
         workers = list(ps.worker_ranks)
         assert workers[0] == first and len(workers) == nw, (workers, first, nw)
         if ps.is_worker:
@@ -136,6 +137,7 @@ def run(rank, world, port, q, mode):
             res["worst_params_step0"] = sorted(worst, reverse=True)[:6]
             _say(rank, f"result: {res}")
             res["update_norm"] = float(dr.norm())
+            res["plane"] = getattr(ps, "plane_kind", None)
             res["workers"] = len(workers)
         if ps.plane is not None:
             ps.plane.close()
