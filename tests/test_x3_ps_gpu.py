@@ -34,12 +34,14 @@ def test_x3_inception_through_ps_matches_reference(mode, world, monkeypatch):
 
     if mode == "dedicated" and not distinct(world):
         # three processes on one GPU: the xGMI plane's apply kernels and landings wait on the GPU for their
-        # peers (the host stays out of the loop), and with the x3 model's streams in three processes on one
-        # device a worker's queue was observed to make no progress until its peers' wait budgets expired
-        # (profiles/r6_x3_ps_dedicated_shared_gpu.log).  The rehearsal therefore checks the dedicated PS
-        # semantics on the collective plane (reduce -> apply -> broadcast over gloo); the xGMI plane's
-        # protocol is rehearsed on one GPU by tests/test_ps_plane_gpu.py, and a node with a GPU per rank
-        # runs this test on it.  X3PS_PLANE overrides (xgmi: reproduce the shared-GPU stall).
+        # peers (the host stays out of the loop), and with the x3 step's streams in all three processes a
+        # worker's queue was observed to make no progress until its peers' wait budgets expired
+        # (profiles/r6_x3_ps_dedicated_shared_gpu.log); with one compute stream per process it passed once
+        # and stalled once (profiles/r6_x3_ps_dedicated_xgmi_few_streams.log).  So on a shared GPU the
+        # rehearsal checks the dedicated PS semantics on the collective plane (reduce -> apply -> broadcast,
+        # no kernel waits on a peer); tests/test_ps_plane_gpu.py rehearses the xGMI plane's protocol with a
+        # small net, and a node with a GPU per rank runs this test on the xGMI plane.  X3PS_PLANE=xgmi
+        # reproduces the shared-GPU stall.
         monkeypatch.setenv("TONY_PS_PLANE", os.environ.get("X3PS_PLANE", "rccl"))
 
     monkeypatch.setenv("TONY_PS_SPIN_S", os.environ.get("TONY_PS_SPIN_S", "300"))
