@@ -27,6 +27,13 @@ coordinator.py).  A ps and a worker may share one GPU (two processes; TonY's 0-G
 worker's GPU, tony.amd.ps-share-gpu); one process cannot be both.  At init a canary bucket goes
 through push / apply / land and is checked on every worker (``verified``); a mismatch raises on every
 rank and the ParameterServer falls back to the collective plane.
+
+Shared GPUs: every wait here is a kernel spinning on a flag, so the processes on one GPU must all get
+their queues serviced.  The landing walks its chunks on at most one workgroup per CU (two workers' landings
+of the fp32 Inception buckets once filled every workgroup slot and starved the ps's apply), and the
+one-GPU rehearsal of 1 ps + 2 x3 workers with their branch / weight-gradient streams still stalled a
+worker until the wait budget ran out (profiles/r6_x3_ps_dedicated_shared_gpu.log) -- one GPU per rank,
+or the ps sharing ONE worker's GPU, is the supported placement; the budget turns a stall into an error.
 """
 from __future__ import annotations
 
