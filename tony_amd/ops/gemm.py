@@ -82,8 +82,10 @@ def occ_choices(rows: int):
     return WGRAD_OCC_BIG if WGRAD_OCC_BIG and rows >= WGRAD_BIG_ROWS else WGRAD_OCC
 
 
-# the x3 (fp32) weight gradients' plan (ops/x3.py conv_wgrad)
-X3_WGRAD_OCC = float(os.environ.get("TONY_X3_WGRAD_OCC", "1"))
+# the x3 (fp32) weight gradients' plan (ops/x3.py conv_wgrad); 0.5 (one workgroup per two CUs, fewer slab
+# partials): 31.14 vs 31.36 ms per fp32 step over 3 repetitions with the weight-gradient batch of 4
+# (profiles/r6_ab_fp32_wb4.log)
+X3_WGRAD_OCC = float(os.environ.get("TONY_X3_WGRAD_OCC", "0.5"))
 # 2 on the stem-size layers: 32.32 vs 32.42 ms per fp32 step (profiles/r5_ab_wgrad_occ.log); 0: X3_WGRAD_OCC
 X3_WGRAD_OCC_BIG = float(os.environ.get("TONY_X3_WGRAD_OCC_BIG", "2") or 0)
 

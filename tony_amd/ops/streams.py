@@ -155,8 +155,9 @@ def active() -> bool:
 # GPU at 14 ms the host issue cost matters: 2 measured 13.90 / 13.89 ms/step vs 14.1-15.1 at 1
 # (profiles/r2s3_host_levers_ab.log).  Round 6 (lean conv kernels, GPU at 13.3-13.4 ms, eager host 11.4-15 ms):
 # 3 measured 13.265 ms/step mean over 4 repetitions vs 13.755 at 2 (whose host went bound in one of them), GPU
-# time with the host ahead 13.36 vs 13.40 (profiles/r6_ab_wgrad_batch_eager.log)
-BATCH = int(os.environ.get("TONY_WGRAD_BATCH", "3"))
+# time with the host ahead 13.36 vs 13.40 (profiles/r6_ab_wgrad_batch_eager.log); 4 measured the same on bf16
+# (13.38) and 0.3 % faster on the fp32 step, 0.7 % with TONY_X3_WGRAD_OCC=0.5 (profiles/r6_ab_fp32_wb4.log)
+BATCH = int(os.environ.get("TONY_WGRAD_BATCH", "4"))
 _pending: List[tuple] = []  # (fn, the stream that queued it)
 # ...except for big operands: a batch forks from the current stream when it is flushed, so a pending
 # op waits for whatever the compute stream was given in between (the next layer's BN backward and
