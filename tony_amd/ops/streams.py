@@ -155,9 +155,18 @@ def active() -> bool:
 # GPU at 14 ms the host issue cost matters: 2 measured 13.90 / 13.89 ms/step vs 14.1-15.1 at 1
 # (profiles/r2s3_host_levers_ab.log).  Round 6 (lean conv kernels, GPU at 13.3-13.4 ms, eager host 11.4-15 ms):
 # 3 measured 13.265 ms/step mean over 4 repetitions vs 13.755 at 2 (whose host went bound in one of them), GPU
-# time with the host ahead 13.36 vs 13.40 (profiles/r6_ab_wgrad_batch_eager.log); 4 measured the same on bf16
-# (13.38) and 0.3 % faster on the fp32 step, 0.7 % with TONY_X3_WGRAD_OCC=0.5 (profiles/r6_ab_fp32_wb4.log)
-BATCH = int(os.environ.get("TONY_WGRAD_BATCH", "4"))
+# time with the host ahead 13.36 vs 13.40 (profiles/r6_ab_wgrad_batch_eager.log).  The fp32 (x3) step, whose
+# weight gradients are three products deep, takes 4: 0.3 % faster, 0.7 % with TONY_X3_WGRAD_OCC=0.5
+# (profiles/r6_ab_fp32_wb4.log) -- parallel/trainer.py picks it per model (set_batch) unless the env says.
+BATCH = int(os.environ.get("TONY_WGRAD_BATCH", "3"))
+BATCH_FROM_ENV = "TONY_WGRAD_BATCH" in os.environ
+
+
+def set_batch(n: int) -> None:
+    """Weight-gradient ops per side-stream fork from here on (TONY_WGRAD_BATCH, when set, wins)."""
+    global BATCH
+    if not BATCH_FROM_ENV:
+        BATCH = max(1, int(n))
 _pending: List[tuple] = []  # (fn, the stream that queued it)
 # ...except for big operands: a batch forks from the current stream when it is flushed, so a pending
 # op waits for whatever the compute stream was given in between (the next layer's BN backward and

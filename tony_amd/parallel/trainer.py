@@ -56,6 +56,8 @@ class Trainer:
                  branch_streams: bool = True, overlap_comm: bool = True):
         self.model = model
         self.ps = ps
+        # eager weight-gradient forks: 4 ops per fork for the fp32 (x3) model, 3 for bf16 (ops/streams.py BATCH)
+        streams.set_batch(4 if getattr(model, "x3", False) else 3)
         self.loss_fn = loss_fn
         self.use_graph = use_graph
         self.warmup_eager = warmup_eager
